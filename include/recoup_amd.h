@@ -1,0 +1,190 @@
+/*
+ * recoup_amd.h -- C ABI of the MI355X coverage-profile engine (librecoup_amd.so).
+ *
+ * Drop-in boundary for recoup's hot path
+ *   calcCoverage / coverageRef / coverageRnaRef  ->  profileMatrix
+ * The reference is pure R with no FFI; these entry points are what
+ * a thin `.Call` shim replacing the R functions below would bind (INTEGRATION.md shows
+ * that shim and the R-side wrappers):
+ *
+ *   rcp_readset_create   replaces splitBySeqname()            R/util.R:1-13
+ *                        (+ the strand filter of calcCoverage R/coverage.R:141-144)
+ *   rcp_calc_coverage    replaces calcCoverage()              R/coverage.R:126-174
+ *                        and its per-region coverageFromRanges R/coverage.R:176-226
+ *   rcp_plan_create /    replace the coverage -> profile pass:
+ *   rcp_plan_execute /     coverageFromRanges                 R/coverage.R:176-226
+ *   rcp_profile            binCoverageMatrix                  R/profile.R:153-212
+ *                          baseCoverageMatrix                 R/profile.R:100-151
+ *                          splitVector                        R/util.R:15-85
+ *                        fused into one device pass; the caller (profileMatrix,
+ *                        R/profile.R:1-98) describes the column parts it needs.
+ *
+ * Conventions
+ *  - Coordinates are 1-based closed [start, end], as in GRanges.
+ *  - Strand codes: 0 '+', 1 '-', 2 '*'.
+ *  - Matrices are R column-major doubles (element (r, c) at out[c * n_rows + r]).
+ *  - Every function returns RCP_OK (0) or a negative RCP_E* code; the message is
+ *    available from rcp_last_error() (thread-local).  Nothing longjmps.
+ *  - A region the reference maps to NULL (no overlapping reads, chromosome absent,
+ *    subscript out of bounds: R/coverage.R:189-225) is NOT an error: row_valid = 0 and
+ *    the row is zero-filled, as profile.R:116-122 / :191-197 do.
+ *  - The library owns the device buffers it allocates (RAII inside handles); inputs are
+ *    never modified.  Not fork-safe: call it outside mclapply (R/util.R:364-382).
+ */
+#ifndef RECOUP_AMD_H
+#define RECOUP_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define RCP_API __attribute__((visibility("default")))
+#else
+#define RCP_API
+#endif
+
+#define RCP_OK 0
+#define RCP_EINVAL (-1)       /* bad argument / shape */
+#define RCP_EHIP (-2)         /* HIP runtime failure */
+#define RCP_ENOMEM (-3)       /* device allocation failed */
+#define RCP_EUNSUPPORTED (-4) /* valid R input outside what this build implements */
+#define RCP_ESEMANTIC (-5)    /* the reference itself would raise an R error here */
+#define RCP_ENODEVICE (-6)    /* no GPU visible */
+
+enum { RCP_STRAND_PLUS = 0, RCP_STRAND_MINUS = 1, RCP_STRAND_ANY = 2 };
+enum { RCP_STAT_MEAN = 0, RCP_STAT_MEDIAN = 1 };                    /* binParams$sumStat */
+enum { RCP_INTERP_AUTO = 0, RCP_INTERP_SPLINE = 1,                  /* binParams$interpolation */
+       RCP_INTERP_LINEAR = 2, RCP_INTERP_NEIGHBORHOOD = 3 };
+enum { RCP_RNG_REJECTION = 0, RCP_RNG_ROUNDING = 1 };               /* RNGkind(sample.kind=) */
+
+RCP_API const char* rcp_version(void);
+RCP_API const char* rcp_last_error(void);
+RCP_API int rcp_device_count(int* n);
+
+/* ------------------------------------------------------------------ reads */
+typedef struct rcp_readset rcp_readset;
+
+typedef struct {
+    int64_t n;              /* number of reads (< 2^32) */
+    const int32_t* chrom;   /* [n] chromosome code 0..n_chrom-1 (seqnames)            */
+    const int32_t* start;   /* [n] 1-based start                                       */
+    const int32_t* end;     /* [n] 1-based end (inclusive)                             */
+    const int8_t* strand;   /* [n] strand code                                         */
+    int32_t n_chrom;        /* seqlevels                                               */
+    const int64_t* seqlen;  /* [n_chrom] host pointer; -1 = NA seqlength               */
+    int32_t device;         /* HIP device ordinal                                      */
+    int32_t on_device;      /* 1: chrom/start/end/strand are device pointers           */
+    int32_t strand_filter;  /* -1 none, else keep only reads of that strand (calcCoverage strand=) */
+} rcp_reads_desc;
+
+/* Upload (or adopt device arrays), sort by (chrom, strand, start) on the GPU, and build
+ * the per-(chrom, strand) stream offsets plus the prefix-max-of-end search index. */
+RCP_API int rcp_readset_create(const rcp_reads_desc* desc, void* hip_stream, rcp_readset** out);
+RCP_API int rcp_readset_destroy(rcp_readset* rs);
+/* n_reads kept, and stream offsets (host array of n_chrom*3+1, may be NULL). */
+RCP_API int rcp_readset_info(const rcp_readset* rs, int64_t* n_reads, int64_t* stream_off);
+
+/* ------------------------------------------------------------------ rows */
+/* A coverage row is c(cov(g0), cov(g1), ...) over the mask elements ("groups") listed for
+ * that row, each cov(g) being coverageFromRanges() of that mask element (ranges in list
+ * order, reversed when the element's first range is on '-').  A ChIP-seq row has one group
+ * (one GRanges element); a coverageRnaRef row has three: upstream flank, the gene's exon
+ * list (a GRangesList element, reads counted once per exon they overlap), downstream flank
+ * (R/coverage.R:84-121).  The row is NULL when any of its groups is NULL. */
+typedef struct {
+    int32_t n_rows;
+    const int64_t* seg_off;     /* [n_rows+1] segments of each row, groups contiguous      */
+    const int32_t* seg_chrom;   /* [n_seg]                                                 */
+    const int32_t* seg_start;   /* [n_seg]                                                 */
+    const int32_t* seg_end;     /* [n_seg]                                                 */
+    const int8_t* seg_strand;   /* [n_seg]                                                 */
+    const int8_t* seg_group;    /* [n_seg] group index inside the row (0..3); NULL = all 0  */
+    const uint8_t* group_is_list; /* [4] 1 = the group is a GRangesList element; NULL = none */
+    int32_t ignore_strand;      /* findOverlaps(ignore.strand=) (strandedParams$ignoreStrand) */
+} rcp_rows_desc;
+
+/* ------------------------------------------------------------------ bins */
+/* The profile row is cbind over parts (R/profile.R:13-81); part p takes the slice of the
+ * row named by where[p] (profile.R / binCoverageMatrix `where`, with flank = (f1, f2)):
+ *   RCP_WHERE_WHOLE       1:nr             (equal-length branch, profile.R:83-96)
+ *   RCP_WHERE_CENTER      (f1+1):(nr-f2)   (profile.R:166-173)
+ *   RCP_WHERE_UPSTREAM    1:f1             (profile.R:175-181)
+ *   RCP_WHERE_DOWNSTREAM  (nr-f2+1):nr     (profile.R:182-188)
+ * and summarises it with n_bins[p] bins through splitVector (R/util.R:15-85), or per base
+ * when n_bins[p] == 0 (baseCoverageMatrix; the part then has per_base_width[p] columns). */
+enum { RCP_WHERE_WHOLE = 0, RCP_WHERE_CENTER = 1, RCP_WHERE_UPSTREAM = 2, RCP_WHERE_DOWNSTREAM = 3 };
+
+typedef struct {
+    int32_t n_parts;            /* 1..8 */
+    const int32_t* where;       /* [n_parts] RCP_WHERE_* */
+    int32_t flank[2];           /* (f1, f2) */
+    const int32_t* n_bins;      /* [n_parts] 0 = per base */
+    const int32_t* per_base_width; /* [n_parts] columns of a per-base part (else ignored) */
+    int32_t stat;               /* RCP_STAT_* */
+    int32_t interp;             /* RCP_INTERP_* */
+    int32_t rng_kind;           /* RCP_RNG_* */
+    double scale;               /* linear normalization factor (recoup.R:559-577); 1 = none */
+} rcp_bins_desc;
+
+typedef struct rcp_plan rcp_plan;
+
+typedef struct {
+    int64_t n_cols;             /* total matrix columns */
+    int64_t n_segments;
+    int64_t n_interp_rows;      /* (row, part) pairs with fewer positions than bins */
+    int64_t lds_bytes;          /* dynamic LDS of the pileup kernel */
+    int64_t grid;               /* workgroups of the pileup kernel */
+    int32_t tile_rows;
+    int32_t chunk_positions;
+} rcp_plan_info;
+
+/* Host work: orientation of segments, R-RNG bin layouts (set.seed(42); sample(1:n, dif)),
+ * interpolation plans, chunking; uploads the tables to the readset's device.  bins may be
+ * NULL for a calcCoverage-only plan.  The readset must outlive the plan. */
+RCP_API int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
+                    rcp_plan** out);
+RCP_API int rcp_plan_destroy(rcp_plan* plan);
+RCP_API int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info);
+
+/* Device work only (stream-ordered, no host sync, capturable in a hipGraph):
+ *   locate kernel (per segment/stream read ranges + NULL semantics),
+ *   pileup-bin kernel (LDS difference array -> scans -> bins -> column-major out),
+ *   interpolation kernel for rows with fewer positions than bins.
+ * d_out: device [n_rows * n_cols] doubles.  d_valid (device, n_rows) and d_binsum
+ * (device int64 numerators, same shape as d_out; median rows hold 2x the median) may be
+ * NULL.  A device-side status word reports numerator overflow; rcp_plan_status() reads it. */
+RCP_API int rcp_plan_execute(rcp_plan* plan, double* d_out, uint8_t* d_valid, int64_t* d_binsum,
+                     void* hip_stream);
+/* The same pass split into its launches (for per-kernel timing with events between them):
+ * stages is a mask of RCP_STAGE_*; stages must be enqueued in order on one stream. */
+enum { RCP_STAGE_LOCATE = 1, RCP_STAGE_PILEUP = 2, RCP_STAGE_INTERP = 4, RCP_STAGE_ALL = 7 };
+RCP_API int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d_valid, int64_t* d_binsum,
+                                    void* hip_stream, int stages);
+/* Synchronises the stream and returns RCP_OK or the error the last execute raised. */
+RCP_API int rcp_plan_status(rcp_plan* plan, void* hip_stream);
+/* Only the locate kernel: row validity (device pointer), e.g. for profileMatrix's
+ * equal-length test on sample 1 (R/profile.R:6-10). */
+RCP_API int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_stream);
+/* Nominal (valid-row) coverage length of every row, host array [n_rows]. */
+RCP_API int rcp_plan_row_lengths(const rcp_plan* plan, int64_t* out_len);
+
+/* One-shot host-pointer entry point (what the R .Call shim binds): create plan, execute,
+ * copy out (host, R column-major n_rows x n_cols), copy row_valid (host, may be NULL),
+ * destroy. */
+RCP_API int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
+                double* out, uint8_t* row_valid);
+
+/* calcCoverage: per-row integer depth vectors (CSR).  out_off is the host prefix sum of
+ * rcp_plan_row_lengths(); d_cov (device int32 [out_off[n_rows]]) receives each valid row's
+ * depth at its offset; d_valid (device) the NULL mask.  Rows are in the row's own
+ * orientation (reversed for '-'), i.e. exactly the values of the reference's Rle. */
+RCP_API int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t* d_cov, uint8_t* d_valid,
+                      void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RECOUP_AMD_H */

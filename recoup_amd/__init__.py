@@ -1,0 +1,8 @@
+"""recoup_amd -- MI355X-native engine for recoup's coverage -> profile hot path.
+
+Mirrors the reference's R API for that path (hjanime/recoup R/coverage.R, R/profile.R):
+``calcCoverage``, ``coverageRef``, ``coverageRnaRef``, ``profileMatrix`` and the internal
+``binCoverageMatrix`` / ``baseCoverageMatrix``, computed by hand-written gfx950 HIP kernels
+behind the C ABI in ``include/recoup_amd.h``.
+"""
+__version__ = "0.1.0"

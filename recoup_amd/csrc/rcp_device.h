@@ -1,0 +1,94 @@
+// rcp_device.h -- device-side plan layout shared by rcp_kernels.hip and rcp_host.cpp.
+//
+// All tables are built on the host (rcp_host.cpp) and uploaded once per plan; the
+// kernels only read them.  Names follow the reference's domain: reads, streams
+// (a (chromosome, strand) run of start-sorted reads), rows (one mask element, or the
+// c(left, exons, right) of coverageRnaRef), segments (the ranges of a row, in output
+// order), parts (the profile.R slices: upstream / center / downstream) and bins.
+#pragma once
+#include <stdint.h>
+
+#define RCP_MAX_PARTS 8
+#define RCP_BLOCK 256
+
+// One oriented segment of a row: genomic run [lo, hi] written to row positions
+// [off, off + hi - lo] forward (rev = 0) or reversed (rev = 1).
+struct RcpSeg {
+    int32_t lo, hi;      // genomic run (1-based, inclusive)
+    int32_t off;         // first row position (0-based)
+    int32_t gfirst;      // first segment of this segment's group (in the row's table)
+    int16_t gcount;      // number of segments in the group
+    uint8_t rev;         // 1 = reversed in the row
+    uint8_t streams;     // bit s set = query stream s ('+', '-', '*')
+    uint8_t multi;       // 1 = group is a GRangesList element (count reads once per range hit)
+    uint8_t group;       // group index inside the row (0..3)
+    uint8_t query_ok;    // 0 = zero-width query (hits nothing)
+    uint8_t pad;
+};
+
+struct RcpPart {
+    // slice [lo, hi) of the row (0-based): lo = (lo_end ? nr : 0) + lo_off, same for hi
+    int32_t lo_off, hi_off;
+    int32_t lo_end, hi_end;
+    int32_t n_bins;      // bins (per-base parts: the column count)
+    int32_t per_base;    // 1 = per base (bins of one position, no layout)
+    int32_t col_off;     // first output column
+    int32_t chunk_bins;  // bins per workgroup chunk
+    int32_t n_chunks;    // ceil(n_bins / chunk_bins)
+    int32_t lay_base;    // offset of this part's dif -> layout index table (n_bins entries)
+};
+
+struct RcpPlanDev {
+    // reads
+    const int2* se;            // sorted (start, end) pairs
+    const int32_t* pmax;       // prefix max of end inside each stream
+    const int64_t* stream_off; // [n_chrom*3 + 1]
+    const int64_t* seqlen;     // [n_chrom] (-1 = NA)
+    int32_t n_chrom;
+    // rows
+    int32_t n_rows;
+    const int32_t* row_chrom;   // [n_rows]
+    const int32_t* row_seg;     // [n_rows + 1] into segs
+    const int32_t* row_len;     // [n_rows] nominal coverage length nr
+    const uint8_t* row_static;  // [n_rows] 1 = statically NULL (negative index, bad chrom)
+    const RcpSeg* segs;
+    // locate outputs
+    uint32_t* seg_lo;           // [n_seg * 3]
+    uint32_t* seg_hi;           // [n_seg * 3]
+    uint8_t* valid;             // [n_rows]
+    // bins
+    int32_t n_parts;
+    RcpPart part[RCP_MAX_PARTS];
+    int32_t n_chunks_total;     // sum over parts (workgroups per row tile)
+    const int32_t* lay_index;   // per part: [n_bins] dif -> offset into lay_cnt (-1 = none)
+    const int32_t* lay_cnt;     // prefix counts of enlarged bins (n_bins + 1 per layout)
+    int32_t stat;               // 0 mean, 1 median
+    double scale;
+    int64_t n_cols;
+    // interpolation rows
+    int32_t n_interp;
+    const int32_t* interp_row;  // [n_interp]
+    const int32_t* interp_part; // [n_interp]
+    const int32_t* interp_mode; // [n_interp] 1 spline, 2 linear (no-op), 3 neighborhood
+    const int32_t* interp_pos;  // [n_interp] offset into nb_pos (neighborhood) or -1
+    const int32_t* nb_pos;      // orig.pos tables (1-based, sorted)
+    double* interp_scratch;     // per interp row: 5 * max_interp_len doubles
+    int32_t interp_stride;
+    // geometry
+    int32_t chunk_cap;          // max positions per chunk (diff array capacity)
+    int32_t stage_cap;          // max bins per chunk
+    // coverage (CSR) mode
+    const int64_t* csr_off;     // non-null: write per-row depth into csr (calcCoverage)
+    int32_t* csr_out;
+    // status
+    uint32_t* status;           // bit 0: numerator overflow, bit 1: per-base width mismatch
+};
+
+__host__ __device__ inline void rcp_part_slice(const RcpPart& p, int32_t nr, int32_t* lo, int32_t* len) {
+    *lo = (p.lo_end ? nr : 0) + p.lo_off;
+    *len = (p.hi_end ? nr : 0) + p.hi_off - *lo;
+}
+
+#define RCP_STATUS_OVERFLOW 1u
+#define RCP_STATUS_WIDTH 2u
+#define RCP_STATUS_INTERP 4u

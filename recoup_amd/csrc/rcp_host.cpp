@@ -1,0 +1,692 @@
+// rcp_host.cpp -- host side of librecoup_amd.so: the C ABI of include/recoup_amd.h.
+//
+// Owns device memory (RAII), builds per-plan tables from the reference's semantics and
+// launches the gfx950 kernels in rcp_kernels.hip.  Host work is table construction only
+// (segment orientation, R-RNG bin layouts, chunking); every per-read / per-base operation
+// runs on the GPU.  There is no CPU fallback: without a device every entry point fails with
+// RCP_ENODEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/recoup_amd.h"
+#include "rcp_device.h"
+#include "rcp_rng.h"
+
+extern "C" {
+hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
+                          int32_t* vout, int64_t n, int end_bit, hipStream_t stream);
+hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
+                           hipStream_t stream);
+hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream);
+hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_t* binsum, int csr, hipStream_t stream);
+hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStream_t stream);
+size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int tile_rows, int csr);
+hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
+                              const int8_t* strand, int32_t n_chrom, int32_t strand_filter, uint64_t* keys,
+                              int32_t* vals, hipStream_t stream);
+hipError_t rcp_launch_streams(int64_t n, const uint64_t* keys, const int32_t* vals, int64_t* off, int64_t n_off,
+                              int2* se, uint64_t* scan_in, hipStream_t stream);
+hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* pmax, hipStream_t stream);
+}
+
+namespace {
+
+constexpr int kTileRows = 16;
+constexpr int kChunkMax = 16384;     // positions per workgroup chunk (LDS difference array)
+constexpr int kStageMaxBins = 1024;  // bins per chunk (LDS stage = bins x 16 rows x 4 B)
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(e_ == hipErrorOutOfMemory ? RCP_ENOMEM : RCP_EHIP, "%s: %s (%s:%d)", #expr, \
+                        hipGetErrorString(e_), __FILE__, __LINE__);                          \
+    } while (0)
+
+// Device buffer with RAII.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t alloc(size_t n) {
+        reset();
+        bytes = n;
+        if (n == 0) return hipSuccess;
+        return hipMalloc(&p, n);
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+// Switch to a device for the scope of an API call, restoring the caller's device.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        err = hipGetDevice(&prev);
+        if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int check_device(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(RCP_ENODEVICE, "no HIP device visible");
+    if (dev < 0 || dev >= n) return fail(RCP_EINVAL, "device %d out of range (%d devices)", dev, n);
+    return RCP_OK;
+}
+
+}  // namespace
+
+// =====================================================================================
+// readset
+// =====================================================================================
+struct rcp_readset {
+    int device = 0;
+    int64_t n = 0;  // reads kept (strand filter applied)
+    int32_t n_chrom = 0;
+    std::vector<int64_t> seqlen;
+    std::vector<int64_t> h_stream_off;  // n_chrom*3 + 1
+    DevBuf se, pmax, stream_off, d_seqlen;
+};
+
+extern "C" const char* rcp_version(void) { return "recoup_amd 0.1.0 (gfx950)"; }
+extern "C" const char* rcp_last_error(void) { return g_err.c_str(); }
+
+extern "C" int rcp_device_count(int* n) {
+    if (!n) return fail(RCP_EINVAL, "n is NULL");
+    *n = 0;
+    if (hipGetDeviceCount(n) != hipSuccess) *n = 0;
+    return RCP_OK;
+}
+
+extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp_readset** out) {
+    if (!d || !out) return fail(RCP_EINVAL, "NULL argument");
+    *out = nullptr;
+    int rc = check_device(d->device);
+    if (rc) return rc;
+    if (d->n < 0 || d->n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "read count %lld outside [0, 2^31)", (long long)d->n);
+    if (d->n_chrom <= 0 || d->n_chrom > (1 << 20)) return fail(RCP_EINVAL, "n_chrom = %d", d->n_chrom);
+    if (d->n > 0 && (!d->chrom || !d->start || !d->end || !d->strand)) return fail(RCP_EINVAL, "NULL read array");
+    if (d->strand_filter < -1 || d->strand_filter > 2) return fail(RCP_EINVAL, "strand_filter = %d", d->strand_filter);
+    DeviceGuard g(d->device);
+    HIP_TRY(g.err);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    auto rs = std::make_unique<rcp_readset>();
+    rs->device = d->device;
+    rs->n_chrom = d->n_chrom;
+    rs->seqlen.assign(d->n_chrom, -1);
+    if (d->seqlen)
+        for (int c = 0; c < d->n_chrom; ++c) rs->seqlen[c] = d->seqlen[c] < 0 ? -1 : d->seqlen[c];
+    const int64_t n = d->n;
+    const int64_t n_streams = (int64_t)d->n_chrom * 3;  // + 1 sentinel stream (dropped reads)
+
+    // inputs on device
+    DevBuf in_chrom, in_start, in_end, in_strand;
+    const int32_t *pc = d->chrom, *ps = d->start, *pe = d->end;
+    const int8_t* pst = d->strand;
+    if (!d->on_device && n > 0) {
+        HIP_TRY(in_chrom.alloc(4 * n));
+        HIP_TRY(in_start.alloc(4 * n));
+        HIP_TRY(in_end.alloc(4 * n));
+        HIP_TRY(in_strand.alloc(n));
+        HIP_TRY(hipMemcpyAsync(in_chrom.p, d->chrom, 4 * n, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(in_start.p, d->start, 4 * n, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(in_end.p, d->end, 4 * n, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(in_strand.p, d->strand, n, hipMemcpyHostToDevice, s));
+        pc = in_chrom.as<int32_t>();
+        ps = in_start.as<int32_t>();
+        pe = in_end.as<int32_t>();
+        pst = in_strand.as<int8_t>();
+    }
+    DevBuf keys, keys2, vals, vals2, scan_in, scan_out, temp;
+    HIP_TRY(keys.alloc(8 * std::max<int64_t>(n, 1)));
+    HIP_TRY(keys2.alloc(8 * std::max<int64_t>(n, 1)));
+    HIP_TRY(vals.alloc(4 * std::max<int64_t>(n, 1)));
+    HIP_TRY(vals2.alloc(4 * std::max<int64_t>(n, 1)));
+    HIP_TRY(rcp_launch_readset(n, pc, ps, pe, pst, d->n_chrom, d->strand_filter, keys.as<uint64_t>(),
+                               vals.as<int32_t>(), s));
+    int end_bit = 32;
+    while ((int64_t(1) << (end_bit - 32)) <= n_streams) ++end_bit;
+    size_t tb = 0;
+    if (n > 0) {
+        HIP_TRY(rcp_sort_pairs(nullptr, &tb, keys.as<uint64_t>(), keys2.as<uint64_t>(), vals.as<int32_t>(),
+                               vals2.as<int32_t>(), n, end_bit, s));
+        HIP_TRY(temp.alloc(tb));
+        HIP_TRY(rcp_sort_pairs(temp.p, &tb, keys.as<uint64_t>(), keys2.as<uint64_t>(), vals.as<int32_t>(),
+                               vals2.as<int32_t>(), n, end_bit, s));
+    }
+    in_chrom.reset();
+    in_start.reset();
+    in_end.reset();
+    in_strand.reset();
+    keys.reset();
+    vals.reset();
+    HIP_TRY(rs->stream_off.alloc(8 * (n_streams + 2)));
+    HIP_TRY(rs->se.alloc(8 * std::max<int64_t>(n, 1)));
+    HIP_TRY(scan_in.alloc(8 * std::max<int64_t>(n, 1)));
+    HIP_TRY(rcp_launch_streams(n, keys2.as<uint64_t>(), vals2.as<int32_t>(), rs->stream_off.as<int64_t>(),
+                               n_streams + 2, rs->se.as<int2>(), scan_in.as<uint64_t>(), s));
+    keys2.reset();
+    vals2.reset();
+    HIP_TRY(scan_out.alloc(8 * std::max<int64_t>(n, 1)));
+    if (n > 0) {
+        size_t tb2 = 0;
+        HIP_TRY(rcp_segmax_scan(nullptr, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
+        if (tb2 > temp.bytes) HIP_TRY(temp.alloc(tb2));
+        HIP_TRY(rcp_segmax_scan(temp.p, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
+    }
+    HIP_TRY(rs->pmax.alloc(4 * std::max<int64_t>(n, 1)));
+    HIP_TRY(rcp_launch_unpack_pmax(n, scan_out.as<uint64_t>(), rs->pmax.as<int32_t>(), s));
+    rs->h_stream_off.resize(n_streams + 2);
+    HIP_TRY(hipMemcpyAsync(rs->h_stream_off.data(), rs->stream_off.p, 8 * (n_streams + 2), hipMemcpyDeviceToHost, s));
+    HIP_TRY(rs->d_seqlen.alloc(8 * d->n_chrom));
+    HIP_TRY(hipMemcpyAsync(rs->d_seqlen.p, rs->seqlen.data(), 8 * d->n_chrom, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    rs->n = rs->h_stream_off[n_streams];
+    rs->h_stream_off.resize(n_streams + 1);
+    *out = rs.release();
+    return RCP_OK;
+}
+
+extern "C" int rcp_readset_destroy(rcp_readset* rs) {
+    if (!rs) return RCP_OK;
+    DeviceGuard g(rs->device);
+    delete rs;
+    return RCP_OK;
+}
+
+extern "C" int rcp_readset_info(const rcp_readset* rs, int64_t* n_reads, int64_t* stream_off) {
+    if (!rs) return fail(RCP_EINVAL, "NULL readset");
+    if (n_reads) *n_reads = rs->n;
+    if (stream_off) std::memcpy(stream_off, rs->h_stream_off.data(), 8 * rs->h_stream_off.size());
+    return RCP_OK;
+}
+
+// =====================================================================================
+// plan
+// =====================================================================================
+struct rcp_plan {
+    const rcp_readset* rs = nullptr;
+    RcpPlanDev dev{};
+    int32_t n_rows = 0;
+    int64_t n_cols = 0;
+    int64_t n_seg = 0;
+    std::vector<int64_t> row_len;
+    size_t lds = 0;
+    int64_t grid = 0;
+    DevBuf tables;     // read-only tables
+    DevBuf work;       // seg_lo / seg_hi / valid / status
+    DevBuf scratch;    // interpolation scratch
+    int32_t max_row_len = 0;
+};
+
+namespace {
+
+struct Builder {
+    // host copies of the device tables
+    std::vector<int32_t> row_chrom, row_seg, row_len;
+    std::vector<uint8_t> row_static;
+    std::vector<RcpSeg> segs;
+    std::vector<int32_t> lay_index, lay_cnt;
+    std::vector<int32_t> interp_row, interp_part, interp_mode, interp_pos, nb_pos;
+};
+
+uint8_t stream_mask(int ignore_strand, int8_t q) {
+    // findOverlaps strand compatibility: '*' matches everything (Appendix A, Q2)
+    if (ignore_strand || q == RCP_STRAND_ANY) return 0x7;
+    return (uint8_t)((1u << q) | (1u << RCP_STRAND_ANY));
+}
+
+int build_rows(const rcp_readset* rs, const rcp_rows_desc* rows, Builder* B) {
+    const int R = rows->n_rows;
+    B->row_chrom.assign(R, -1);
+    B->row_seg.assign(R + 1, 0);
+    B->row_len.assign(R, 0);
+    B->row_static.assign(R, 0);
+    for (int r = 0; r < R; ++r) {
+        const int64_t j0 = rows->seg_off[r], j1 = rows->seg_off[r + 1];
+        if (j1 < j0) return fail(RCP_EINVAL, "seg_off not monotone at row %d", r);
+        B->row_seg[r] = (int32_t)B->segs.size();
+        if (j1 == j0) {
+            B->row_static[r] = 1;
+            continue;
+        }
+        const int32_t chrom = rows->seg_chrom[j0];
+        B->row_chrom[r] = chrom;
+        if (chrom < 0 || chrom >= rs->n_chrom) B->row_static[r] = 1;
+        int32_t off = 0;
+        // groups appear as contiguous runs of seg_group
+        int64_t g0 = j0;
+        int prev_group = -1;
+        while (g0 < j1) {
+            const int grp = rows->seg_group ? rows->seg_group[g0] : 0;
+            if (grp < 0 || grp > 3) return fail(RCP_EINVAL, "seg_group %d outside 0..3 (row %d)", grp, r);
+            if (grp <= prev_group) return fail(RCP_EINVAL, "groups of row %d not contiguous/increasing", r);
+            prev_group = grp;
+            int64_t g1 = g0;
+            while (g1 < j1 && (rows->seg_group ? rows->seg_group[g1] : 0) == grp) ++g1;
+            const bool multi = rows->group_is_list && rows->group_is_list[grp];
+            const bool rev_group = rows->seg_strand[g0] == RCP_STRAND_MINUS;  // strand(x)[1] == "-"
+            const int32_t gfirst = (int32_t)B->segs.size();
+            const int32_t gcount = (int32_t)(g1 - g0);
+            if (gcount > 32767) return fail(RCP_EUNSUPPORTED, "more than 32767 ranges in one mask element");
+            for (int64_t q = 0; q < gcount; ++q) {
+                const int64_t j = rev_group ? (g1 - 1 - q) : (g0 + q);
+                if (rows->seg_chrom[j] != chrom) {
+                    if (multi) return fail(RCP_EUNSUPPORTED, "row %d: mask element spans several chromosomes", r);
+                    return fail(RCP_EUNSUPPORTED, "row %d: groups on different chromosomes", r);
+                }
+                const int32_t s = rows->seg_start[j], e = rows->seg_end[j];
+                RcpSeg sg{};
+                sg.gfirst = gfirst;
+                sg.gcount = (int16_t)gcount;
+                sg.multi = multi ? 1 : 0;
+                sg.group = (uint8_t)grp;
+                sg.streams = stream_mask(rows->ignore_strand, rows->seg_strand[j]);
+                if (e >= s) {
+                    // i2k piece s:e; R drops index 0 and fails on negative indices
+                    if (s < 0) B->row_static[r] = 1;
+                    sg.lo = std::max<int32_t>(s, 1);
+                    sg.hi = e;
+                    sg.query_ok = 1;
+                    sg.rev = rev_group ? 1 : 0;
+                    if (sg.hi < sg.lo) continue;  // only index 0: nothing left
+                } else {
+                    // zero-width range: findOverlaps finds nothing (documented); s:(s-1) still
+                    // yields two positions, which only matters for rows that are NULL anyway
+                    if (multi) return fail(RCP_EUNSUPPORTED, "row %d: zero-width range inside a range list", r);
+                    if (e < 0) B->row_static[r] = 1;
+                    sg.lo = std::max<int32_t>(e, 1);
+                    sg.hi = s;
+                    sg.query_ok = 0;
+                    sg.rev = rev_group ? 0 : 1;
+                    if (sg.hi < sg.lo) continue;
+                }
+                sg.off = off;
+                off += sg.hi - sg.lo + 1;
+                B->segs.push_back(sg);
+            }
+            // fix gcount for skipped empty pieces
+            const int32_t kept = (int32_t)B->segs.size() - gfirst;
+            for (int32_t q = gfirst; q < gfirst + kept; ++q) B->segs[q].gcount = (int16_t)kept;
+            g0 = g1;
+        }
+        B->row_len[r] = off;
+    }
+    B->row_seg[R] = (int32_t)B->segs.size();
+    return RCP_OK;
+}
+
+template <class T>
+size_t put(std::vector<char>& blob, const std::vector<T>& v) {
+    size_t off = (blob.size() + 255) & ~size_t(255);
+    blob.resize(off + sizeof(T) * std::max<size_t>(v.size(), 1));
+    if (!v.empty()) std::memcpy(blob.data() + off, v.data(), sizeof(T) * v.size());
+    return off;
+}
+
+}  // namespace
+
+extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
+                               rcp_plan** out) {
+    if (!rs || !rows || !out) return fail(RCP_EINVAL, "NULL argument");
+    *out = nullptr;
+    const rcp_bins_desc coverage_only{};  // bins == NULL: a calcCoverage-only plan
+    const bool cov_only = bins == nullptr;
+    if (cov_only) bins = &coverage_only;
+    if (rows->n_rows < 0) return fail(RCP_EINVAL, "n_rows < 0");
+    if (rows->n_rows > 0 && (!rows->seg_off || !rows->seg_chrom || !rows->seg_start || !rows->seg_end || !rows->seg_strand))
+        return fail(RCP_EINVAL, "NULL row array");
+    if (!cov_only && (bins->n_parts < 1 || bins->n_parts > RCP_MAX_PARTS))
+        return fail(RCP_EINVAL, "n_parts = %d", bins->n_parts);
+    if (bins->stat != RCP_STAT_MEAN && bins->stat != RCP_STAT_MEDIAN) return fail(RCP_EINVAL, "stat = %d", bins->stat);
+    if (bins->interp < 0 || bins->interp > 3) return fail(RCP_EINVAL, "interp = %d", bins->interp);
+    const bool rounding = bins->rng_kind == RCP_RNG_ROUNDING;
+    DeviceGuard g(rs->device);
+    HIP_TRY(g.err);
+
+    auto plan = std::make_unique<rcp_plan>();
+    plan->rs = rs;
+    Builder B;
+    int rc = build_rows(rs, rows, &B);
+    if (rc) return rc;
+    const int R = rows->n_rows;
+    plan->n_rows = R;
+    plan->n_seg = (int64_t)B.segs.size();
+    plan->row_len.assign(B.row_len.begin(), B.row_len.end());
+    for (int r = 0; r < R; ++r) plan->max_row_len = std::max(plan->max_row_len, B.row_len[r]);
+
+    RcpPlanDev& P = plan->dev;
+    P.n_parts = bins->n_parts;
+    P.stat = bins->stat;
+    P.scale = bins->scale;
+    int64_t col = 0;
+    int32_t chunk_cap = 1024, stage_cap = 1;
+    int32_t max_interp_len = 0, max_interp_bins = 0;
+    std::map<std::pair<int, int>, int32_t> layout_cache;  // (n, dif) -> offset in lay_cnt
+    std::map<std::pair<int, int>, int32_t> nb_cache;      // (n, L) -> offset in nb_pos
+    for (int p = 0; p < bins->n_parts; ++p) {
+        RcpPart& pt = P.part[p];
+        const int32_t f1 = bins->flank[0], f2 = bins->flank[1];
+        if (f1 < 0 || f2 < 0) return fail(RCP_EINVAL, "negative flank");
+        switch (bins->where ? bins->where[p] : RCP_WHERE_WHOLE) {
+            case RCP_WHERE_WHOLE: pt.lo_off = 0; pt.lo_end = 0; pt.hi_off = 0; pt.hi_end = 1; break;
+            case RCP_WHERE_CENTER: pt.lo_off = f1; pt.lo_end = 0; pt.hi_off = -f2; pt.hi_end = 1; break;
+            case RCP_WHERE_UPSTREAM: pt.lo_off = 0; pt.lo_end = 0; pt.hi_off = f1; pt.hi_end = 0; break;
+            case RCP_WHERE_DOWNSTREAM: pt.lo_off = -f2; pt.lo_end = 1; pt.hi_off = 0; pt.hi_end = 1; break;
+            default: return fail(RCP_EINVAL, "where[%d] = %d", p, bins->where[p]);
+        }
+        const int nb = bins->n_bins[p];
+        if (nb < 0) return fail(RCP_EINVAL, "n_bins[%d] < 0", p);
+        pt.per_base = nb == 0;
+        pt.n_bins = pt.per_base ? (bins->per_base_width ? bins->per_base_width[p] : 0) : nb;
+        if (pt.n_bins <= 0) return fail(RCP_EINVAL, "part %d has no columns", p);
+        pt.col_off = (int32_t)col;
+        col += pt.n_bins;
+        pt.lay_base = (int32_t)B.lay_index.size();
+        int32_t max_bin = 1;
+        if (!pt.per_base) {
+            B.lay_index.resize(B.lay_index.size() + pt.n_bins, -1);
+            for (int r = 0; r < R; ++r) {
+                int32_t head, L;
+                rcp_part_slice(pt, B.row_len[r], &head, &L);
+                if (B.row_static[r] || B.row_seg[r] == B.row_seg[r + 1]) continue;  // always NULL
+                if (L < 0 || head < 0 || head + L > B.row_len[r])
+                    return fail(RCP_EUNSUPPORTED, "row %d: part %d slice out of its %d-long coverage", r, p,
+                                B.row_len[r]);
+                if (L < pt.n_bins) {
+                    int mode = bins->interp;
+                    if (mode == RCP_INTERP_AUTO)
+                        mode = ((double)(pt.n_bins - L) / pt.n_bins < 0.2) ? RCP_INTERP_NEIGHBORHOOD : RCP_INTERP_SPLINE;
+                    int32_t pos_off = -1;
+                    if (mode == RCP_INTERP_NEIGHBORHOOD) {
+                        auto key = std::make_pair(pt.n_bins, L);
+                        auto it = nb_cache.find(key);
+                        if (it == nb_cache.end()) {
+                            std::vector<int32_t> pos;
+                            if (!rcp::neighborhood_positions(pt.n_bins, L, rounding, &pos))
+                                return fail(RCP_ESEMANTIC,
+                                            "splitVector neighborhood interpolation of %d values into %d bins: R raises an error",
+                                            L, pt.n_bins);
+                            pos_off = (int32_t)B.nb_pos.size();
+                            B.nb_pos.insert(B.nb_pos.end(), pos.begin(), pos.end());
+                            nb_cache[key] = pos_off;
+                        } else {
+                            pos_off = it->second;
+                        }
+                    } else if (mode == RCP_INTERP_SPLINE && L < 1) {
+                        return fail(RCP_ESEMANTIC, "spline() of zero points: R raises an error");
+                    } else if (mode == RCP_INTERP_LINEAR && L < 1) {
+                        return fail(RCP_EUNSUPPORTED, "empty slice with the 'linear' interpolation");
+                    }
+                    B.interp_row.push_back(r);
+                    B.interp_part.push_back(p);
+                    B.interp_mode.push_back(mode);
+                    B.interp_pos.push_back(pos_off);
+                    max_interp_len = std::max(max_interp_len, L);
+                    max_interp_bins = std::max(max_interp_bins, pt.n_bins);
+                    continue;
+                }
+                const int32_t bs = L / pt.n_bins;
+                const int32_t dif = L - bs * pt.n_bins;
+                max_bin = std::max(max_bin, bs + (dif ? 1 : 0));
+                if (dif) {
+                    int32_t& slot = B.lay_index[pt.lay_base + dif];
+                    if (slot < 0) {
+                        auto key = std::make_pair(pt.n_bins, dif);
+                        auto it = layout_cache.find(key);
+                        if (it == layout_cache.end()) {
+                            const std::vector<int32_t> cnt = rcp::bin_layout_counts(pt.n_bins, dif, rounding);
+                            const int32_t o = (int32_t)B.lay_cnt.size();
+                            B.lay_cnt.insert(B.lay_cnt.end(), cnt.begin(), cnt.end());
+                            layout_cache[key] = o;
+                            slot = o;
+                        } else {
+                            slot = it->second;
+                        }
+                    }
+                }
+            }
+        }
+        if (max_bin > kChunkMax)
+            return fail(RCP_EUNSUPPORTED, "part %d: a bin of %d positions exceeds the %d-position chunk", p, max_bin,
+                        kChunkMax);
+        pt.chunk_bins = std::min<int32_t>(pt.n_bins, std::min<int32_t>(kStageMaxBins, kChunkMax / max_bin));
+        pt.n_chunks = (pt.n_bins + pt.chunk_bins - 1) / pt.chunk_bins;
+        chunk_cap = std::max(chunk_cap, pt.chunk_bins * max_bin);
+        stage_cap = std::max(stage_cap, pt.chunk_bins);
+    }
+    if (cov_only) chunk_cap = std::min(kChunkMax, std::max(chunk_cap, plan->max_row_len));
+    if (max_interp_len > kChunkMax)
+        return fail(RCP_EUNSUPPORTED, "interpolated slice of %d positions exceeds %d", max_interp_len, kChunkMax);
+    chunk_cap = std::max(chunk_cap, max_interp_len);
+    P.n_cols = col;
+    plan->n_cols = col;
+    P.chunk_cap = chunk_cap;
+    P.stage_cap = stage_cap;
+    P.n_chunks_total = 0;
+    for (int p = 0; p < P.n_parts; ++p) P.n_chunks_total += P.part[p].n_chunks;
+
+    // ---- upload tables (one arena)
+    std::vector<char> blob;
+    const size_t o_row_chrom = put(blob, B.row_chrom);
+    const size_t o_row_seg = put(blob, B.row_seg);
+    const size_t o_row_len = put(blob, B.row_len);
+    const size_t o_row_static = put(blob, B.row_static);
+    const size_t o_segs = put(blob, B.segs);
+    const size_t o_lay_index = put(blob, B.lay_index);
+    const size_t o_lay_cnt = put(blob, B.lay_cnt);
+    const size_t o_irow = put(blob, B.interp_row);
+    const size_t o_ipart = put(blob, B.interp_part);
+    const size_t o_imode = put(blob, B.interp_mode);
+    const size_t o_ipos = put(blob, B.interp_pos);
+    const size_t o_nb = put(blob, B.nb_pos);
+    HIP_TRY(plan->tables.alloc(blob.size()));
+    HIP_TRY(hipMemcpy(plan->tables.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    char* base = plan->tables.as<char>();
+    const int64_t S = std::max<int64_t>(plan->n_seg, 1);
+    const size_t w_lo = 0, w_hi = 12 * S, w_valid = 24 * S, w_status = (24 * S + R + 255) & ~size_t(255);
+    HIP_TRY(plan->work.alloc(w_status + 256));
+    char* wb = plan->work.as<char>();
+    const int32_t n_interp = (int32_t)B.interp_row.size();
+    P.interp_stride = 2 * (max_interp_bins + 1) + 3 * (max_interp_len + 1) + 8;
+    if (n_interp) HIP_TRY(plan->scratch.alloc(8 * (size_t)n_interp * P.interp_stride));
+
+    P.se = rs->se.as<int2>();
+    P.pmax = rs->pmax.as<int32_t>();
+    P.stream_off = rs->stream_off.as<int64_t>();
+    P.seqlen = rs->d_seqlen.as<int64_t>();
+    P.n_chrom = rs->n_chrom;
+    P.n_rows = R;
+    P.row_chrom = reinterpret_cast<const int32_t*>(base + o_row_chrom);
+    P.row_seg = reinterpret_cast<const int32_t*>(base + o_row_seg);
+    P.row_len = reinterpret_cast<const int32_t*>(base + o_row_len);
+    P.row_static = reinterpret_cast<const uint8_t*>(base + o_row_static);
+    P.segs = reinterpret_cast<const RcpSeg*>(base + o_segs);
+    P.seg_lo = reinterpret_cast<uint32_t*>(wb + w_lo);
+    P.seg_hi = reinterpret_cast<uint32_t*>(wb + w_hi);
+    P.valid = reinterpret_cast<uint8_t*>(wb + w_valid);
+    P.status = reinterpret_cast<uint32_t*>(wb + w_status);
+    P.lay_index = reinterpret_cast<const int32_t*>(base + o_lay_index);
+    P.lay_cnt = reinterpret_cast<const int32_t*>(base + o_lay_cnt);
+    P.n_interp = n_interp;
+    P.interp_row = reinterpret_cast<const int32_t*>(base + o_irow);
+    P.interp_part = reinterpret_cast<const int32_t*>(base + o_ipart);
+    P.interp_mode = reinterpret_cast<const int32_t*>(base + o_imode);
+    P.interp_pos = reinterpret_cast<const int32_t*>(base + o_ipos);
+    P.nb_pos = reinterpret_cast<const int32_t*>(base + o_nb);
+    P.interp_scratch = plan->scratch.as<double>();
+    P.csr_off = nullptr;
+    P.csr_out = nullptr;
+    plan->lds = rcp_pileup_lds_bytes(&P, kTileRows, 0);
+    plan->grid = (int64_t)((R + kTileRows - 1) / kTileRows) * P.n_chunks_total;
+    if (plan->lds > 160 * 1024) return fail(RCP_EUNSUPPORTED, "plan needs %zu B of LDS", plan->lds);
+    HIP_TRY(hipMemset(plan->work.p, 0, plan->work.bytes));
+    *out = plan.release();
+    return RCP_OK;
+}
+
+extern "C" int rcp_plan_destroy(rcp_plan* plan) {
+    if (!plan) return RCP_OK;
+    DeviceGuard g(plan->rs->device);
+    delete plan;
+    return RCP_OK;
+}
+
+extern "C" int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info) {
+    if (!plan || !info) return fail(RCP_EINVAL, "NULL argument");
+    info->n_cols = plan->n_cols;
+    info->n_segments = plan->n_seg;
+    info->n_interp_rows = plan->dev.n_interp;
+    info->lds_bytes = (int64_t)plan->lds;
+    info->grid = plan->grid;
+    info->tile_rows = kTileRows;
+    info->chunk_positions = plan->dev.chunk_cap;
+    return RCP_OK;
+}
+
+extern "C" int rcp_plan_row_lengths(const rcp_plan* plan, int64_t* out_len) {
+    if (!plan || !out_len) return fail(RCP_EINVAL, "NULL argument");
+    std::memcpy(out_len, plan->row_len.data(), 8 * plan->row_len.size());
+    return RCP_OK;
+}
+
+extern "C" int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_stream) {
+    if (!plan) return fail(RCP_EINVAL, "NULL plan");
+    DeviceGuard g(plan->rs->device);
+    HIP_TRY(g.err);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    HIP_TRY(rcp_launch_locate(&plan->dev, s));
+    if (d_valid && plan->n_rows)
+        HIP_TRY(hipMemcpyAsync(d_valid, plan->dev.valid, plan->n_rows, hipMemcpyDeviceToDevice, s));
+    return RCP_OK;
+}
+
+extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d_valid, int64_t* d_binsum,
+                                       void* hip_stream, int stages) {
+    if (!plan) return fail(RCP_EINVAL, "NULL plan");
+    if (plan->dev.n_parts == 0) return fail(RCP_EINVAL, "coverage-only plan (created with bins == NULL)");
+    if (!d_out && plan->n_rows && plan->n_cols) return fail(RCP_EINVAL, "NULL output");
+    DeviceGuard g(plan->rs->device);
+    HIP_TRY(g.err);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (stages & RCP_STAGE_LOCATE) {
+        HIP_TRY(hipMemsetAsync(plan->dev.status, 0, 4, s));
+        HIP_TRY(rcp_launch_locate(&plan->dev, s));
+    }
+    if (stages & RCP_STAGE_PILEUP) HIP_TRY(rcp_launch_pileup(&plan->dev, d_out, d_binsum, 0, s));
+    if (stages & RCP_STAGE_INTERP) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
+    if ((stages & RCP_STAGE_LOCATE) && d_valid && plan->n_rows)
+        HIP_TRY(hipMemcpyAsync(d_valid, plan->dev.valid, plan->n_rows, hipMemcpyDeviceToDevice, s));
+    return RCP_OK;
+}
+
+extern "C" int rcp_plan_execute(rcp_plan* plan, double* d_out, uint8_t* d_valid, int64_t* d_binsum,
+                                void* hip_stream) {
+    return rcp_plan_execute_stages(plan, d_out, d_valid, d_binsum, hip_stream, RCP_STAGE_ALL);
+}
+
+extern "C" int rcp_plan_status(rcp_plan* plan, void* hip_stream) {
+    if (!plan) return fail(RCP_EINVAL, "NULL plan");
+    DeviceGuard g(plan->rs->device);
+    HIP_TRY(g.err);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    uint32_t st = 0;
+    HIP_TRY(hipMemcpyAsync(&st, plan->dev.status, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (st & RCP_STATUS_WIDTH)
+        return fail(RCP_EUNSUPPORTED, "a per-base part met a row whose slice width differs from the column count");
+    if (st & RCP_STATUS_INTERP) return fail(RCP_EUNSUPPORTED, "internal plan/layout mismatch (status %u)", st);
+    if (st & RCP_STATUS_OVERFLOW) return fail(RCP_EUNSUPPORTED, "bin numerator exceeded 2^32");
+    return RCP_OK;
+}
+
+extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins, double* out,
+                           uint8_t* row_valid) {
+    rcp_plan* plan = nullptr;
+    int rc = rcp_plan_create(rs, rows, bins, &plan);
+    if (rc) return rc;
+    std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
+    DeviceGuard g(rs->device);
+    HIP_TRY(g.err);
+    const size_t cells = (size_t)plan->n_rows * (size_t)plan->n_cols;
+    DevBuf d_out, d_valid;
+    HIP_TRY(d_out.alloc(8 * std::max<size_t>(cells, 1)));
+    HIP_TRY(d_valid.alloc(std::max<int32_t>(plan->n_rows, 1)));
+    rc = rcp_plan_execute(plan, d_out.as<double>(), d_valid.as<uint8_t>(), nullptr, nullptr);
+    if (rc) return rc;
+    rc = rcp_plan_status(plan, nullptr);
+    if (rc) return rc;
+    if (out && cells) HIP_TRY(hipMemcpy(out, d_out.p, 8 * cells, hipMemcpyDeviceToHost));
+    if (row_valid && plan->n_rows) HIP_TRY(hipMemcpy(row_valid, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost));
+    return RCP_OK;
+}
+
+extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t* d_cov, uint8_t* d_valid,
+                                 void* hip_stream) {
+    if (!plan || !out_off) return fail(RCP_EINVAL, "NULL argument");
+    DeviceGuard g(plan->rs->device);
+    HIP_TRY(g.err);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    for (int r = 0; r < plan->n_rows; ++r)
+        if (out_off[r + 1] - out_off[r] != plan->row_len[r])
+            return fail(RCP_EINVAL, "out_off does not match the row lengths at row %d", r);
+    // one per-base part over the whole row, chunked by the plan's chunk capacity
+    RcpPlanDev P = plan->dev;
+    P.n_parts = 1;
+    RcpPart& pt = P.part[0];
+    pt = RcpPart{};
+    pt.hi_end = 1;
+    pt.per_base = 1;
+    pt.n_bins = std::max<int32_t>(plan->max_row_len, 1);
+    pt.chunk_bins = std::max<int32_t>(std::min(P.chunk_cap, pt.n_bins), 1);
+    pt.n_chunks = (pt.n_bins + pt.chunk_bins - 1) / pt.chunk_bins;
+    P.n_chunks_total = pt.n_chunks;
+    DevBuf d_off;
+    HIP_TRY(d_off.alloc(8 * (plan->n_rows + 1)));
+    HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * (plan->n_rows + 1), hipMemcpyHostToDevice, s));
+    P.csr_off = d_off.as<int64_t>();
+    P.csr_out = d_cov;
+    HIP_TRY(hipMemsetAsync(plan->dev.status, 0, 4, s));
+    HIP_TRY(rcp_launch_locate(&P, s));
+    HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
+    if (d_valid && plan->n_rows)
+        HIP_TRY(hipMemcpyAsync(d_valid, plan->dev.valid, plan->n_rows, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));  // d_off is released on return
+    return RCP_OK;
+}

@@ -1,0 +1,231 @@
+"""Device-resident read sets and profile plans (thin RAII wrappers over the C ABI).
+
+``ReadSet``  -- splitBySeqname (R/util.R:1-13) + strand filter (R/coverage.R:141-144) as a
+               GPU index: reads sorted by (chromosome, strand, start) with a prefix-max-of-end
+               array, held in HBM for the lifetime of the object.
+``RowTable`` -- the mask side: one row per region (GRanges element) or per coverageRnaRef
+               gene (upstream flank, exon list, downstream flank).
+``Plan``     -- one coverage -> profile pass (R/coverage.R:176-226 fused with
+               R/profile.R:100-212 and R/util.R:15-85) ready to execute on a HIP stream.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, cptr, ptr
+
+STRAND = {"+": 0, "-": 1, "*": 2}
+STAT = {"mean": 0, "median": 1}
+INTERP = {"auto": 0, "spline": 1, "linear": 2, "neighborhood": 3}
+RNG = {"Rejection": 0, "Rounding": 1}
+
+
+def _stream(device, stream):
+    if stream is None:
+        return _lib.stream_handle(device)
+    if isinstance(stream, torch.cuda.Stream):
+        return ctypes.c_void_p(stream.cuda_stream)
+    return ctypes.c_void_p(stream)
+
+
+class ReadSet:
+    """Reads of one sample, resident on one GPU.
+
+    ``chrom``/``start``/``end``/``strand`` may be numpy arrays (uploaded) or torch CUDA
+    tensors already on ``device`` (adopted, no host round trip).  ``seqlengths`` has one
+    entry per chromosome code, -1 for NA.
+    """
+
+    def __init__(self, chrom, start, end, strand, seqlengths, device=0, strand_filter=None, stream=None):
+        lib = _lib.lib()
+        if _lib.device_count() == 0:
+            raise _lib.RcpError(-6, "no GPU visible: recoup_amd runs only on the GPU")
+        self.device = int(device)
+        self.seqlengths = np.ascontiguousarray(seqlengths, dtype=np.int64)
+        on_dev = isinstance(start, torch.Tensor)
+        if on_dev:
+            keep = [t.contiguous() for t in (chrom, start, end, strand)]
+            for t, dt in zip(keep, (torch.int32, torch.int32, torch.int32, torch.int8)):
+                if t.dtype != dt or t.device.type != "cuda":
+                    raise TypeError("device reads must be int32/int32/int32/int8 CUDA tensors")
+        else:
+            keep = [np.ascontiguousarray(chrom, dtype=np.int32), np.ascontiguousarray(start, dtype=np.int32),
+                    np.ascontiguousarray(end, dtype=np.int32), np.ascontiguousarray(strand, dtype=np.int8)]
+        n = int(keep[1].shape[0])
+        sf = -1 if strand_filter is None else STRAND.get(strand_filter, strand_filter)
+        d = _lib.ReadsDesc(n, ptr(keep[0]), ptr(keep[1]), ptr(keep[2]), ptr(keep[3]), len(self.seqlengths),
+                           cptr(self.seqlengths, _lib._i64p), self.device, int(on_dev), int(sf))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.rcp_readset_create(ctypes.byref(d), _stream(self.device, stream), ctypes.byref(h)))
+        self.h = h
+        nk = ctypes.c_int64()
+        self.stream_off = np.zeros(3 * len(self.seqlengths) + 1, dtype=np.int64)
+        check(lib.rcp_readset_info(self.h, ctypes.byref(nk), cptr(self.stream_off, _lib._i64p)))
+        self.n = nk.value
+
+    @property
+    def chrom_has_reads(self):
+        so = self.stream_off
+        return np.array([so[3 * c + 3] > so[3 * c] for c in range(len(self.seqlengths))])
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib().rcp_readset_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class RowTable:
+    """Rows of segments.  ``seg_off`` partitions the flat segment arrays by row; inside a
+    row, ``seg_group`` numbers the mask elements whose coverages are concatenated."""
+
+    def __init__(self, seg_off, chrom, start, end, strand, seg_group=None, group_is_list=None,
+                 ignore_strand=True, names=None):
+        self.seg_off = np.ascontiguousarray(seg_off, dtype=np.int64)
+        self.chrom = np.ascontiguousarray(chrom, dtype=np.int32)
+        self.start = np.ascontiguousarray(start, dtype=np.int32)
+        self.end = np.ascontiguousarray(end, dtype=np.int32)
+        self.strand = np.ascontiguousarray(strand, dtype=np.int8)
+        self.seg_group = None if seg_group is None else np.ascontiguousarray(seg_group, dtype=np.int8)
+        self.group_is_list = None if group_is_list is None else np.ascontiguousarray(group_is_list, dtype=np.uint8)
+        self.ignore_strand = bool(ignore_strand)
+        self.n_rows = len(self.seg_off) - 1
+        self.names = names
+
+    @classmethod
+    def from_ranges(cls, chrom, start, end, strand, **kw):
+        return cls(np.arange(len(start) + 1), chrom, start, end, strand, **kw)
+
+    def desc(self):
+        return _lib.RowsDesc(self.n_rows, cptr(self.seg_off, _lib._i64p), cptr(self.chrom, _lib._i32p),
+                             cptr(self.start, _lib._i32p), cptr(self.end, _lib._i32p),
+                             cptr(self.strand, _lib._i8p), cptr(self.seg_group, _lib._i8p),
+                             cptr(self.group_is_list, _lib._u8p), int(self.ignore_strand))
+
+
+WHERE = {"whole": 0, "center": 1, "upstream": 2, "downstream": 3}
+
+
+class Bins:
+    """Column parts of the profile row (R/profile.R slices) and the splitVector options.
+
+    ``parts`` is a list of ``(where, n_bins)`` or ``(where, 0, per_base_width)``; ``where`` is
+    one of whole / center / upstream / downstream (binCoverageMatrix's ``where``)."""
+
+    def __init__(self, parts, flank=(0, 0), stat="mean", interp="auto", rng_kind="Rejection", scale=1.0):
+        self.parts = [tuple(p) for p in parts]
+        self.where = np.array([WHERE[p[0]] if isinstance(p[0], str) else int(p[0]) for p in self.parts],
+                              dtype=np.int32)
+        self.n_bins = np.array([p[1] for p in self.parts], dtype=np.int32)
+        self.width = np.array([p[2] if len(p) > 2 else 0 for p in self.parts], dtype=np.int32)
+        self.flank = (int(flank[0]), int(flank[1]))
+        self.stat = STAT[stat] if isinstance(stat, str) else int(stat)
+        self.interp = INTERP[interp] if isinstance(interp, str) else int(interp)
+        self.rng_kind = RNG[rng_kind] if isinstance(rng_kind, str) else int(rng_kind)
+        self.scale = float(scale)
+
+    @property
+    def n_cols(self):
+        return int(sum(w if b == 0 else b for b, w in zip(self.n_bins, self.width)))
+
+    def desc(self):
+        fl = (ctypes.c_int32 * 2)(*self.flank)
+        return _lib.BinsDesc(len(self.parts), cptr(self.where, _lib._i32p), fl, cptr(self.n_bins, _lib._i32p),
+                             cptr(self.width, _lib._i32p), self.stat, self.interp, self.rng_kind, self.scale)
+
+
+class Plan:
+    """One fused coverage -> profile pass of ``rows`` over ``readset`` with ``bins``."""
+
+    def __init__(self, readset, rows, bins):
+        self.readset = readset  # keeps the device reads alive
+        self.rows = rows
+        self.bins = bins
+        rd = rows.desc()
+        bd = ctypes.byref(bins.desc()) if bins is not None else None
+        h = ctypes.c_void_p()
+        with torch.cuda.device(readset.device):
+            check(_lib.lib().rcp_plan_create(readset.h, ctypes.byref(rd), bd, ctypes.byref(h)))
+        self.h = h
+        info = _lib.PlanInfo()
+        check(_lib.lib().rcp_plan_info_get(self.h, ctypes.byref(info)))
+        self.info = {k: getattr(info, k) for k, _ in _lib.PlanInfo._fields_}
+        self.n_rows = rows.n_rows
+        self.n_cols = int(info.n_cols)
+        self.device = readset.device
+
+    def row_lengths(self):
+        out = np.zeros(self.n_rows, dtype=np.int64)
+        check(_lib.lib().rcp_plan_row_lengths(self.h, cptr(out, _lib._i64p)))
+        return out
+
+    def empty_output(self):
+        return torch.empty((self.n_cols, self.n_rows), dtype=torch.float64, device=f"cuda:{self.device}")
+
+    def execute(self, out=None, valid=None, binsum=None, stream=None):
+        """Enqueue the pass.  ``out`` is a CUDA float64 tensor holding the R column-major
+        matrix (shape (n_cols, n_rows) in torch's row-major terms).  No host sync."""
+        if out is None:
+            out = self.empty_output()
+        check(_lib.lib().rcp_plan_execute(self.h, ptr(out), ptr(valid), ptr(binsum), _stream(self.device, stream)))
+        return out
+
+    def execute_stages(self, stages, out, valid=None, binsum=None, stream=None):
+        """Enqueue only some launches (1 locate, 2 pileup, 4 interpolation) -- for timing."""
+        check(_lib.lib().rcp_plan_execute_stages(self.h, ptr(out), ptr(valid), ptr(binsum),
+                                                 _stream(self.device, stream), int(stages)))
+        return out
+
+    def status(self, stream=None):
+        check(_lib.lib().rcp_plan_status(self.h, _stream(self.device, stream)))
+
+    def validity(self, stream=None):
+        v = torch.empty(max(self.n_rows, 1), dtype=torch.uint8, device=f"cuda:{self.device}")
+        check(_lib.lib().rcp_plan_validity(self.h, ptr(v), _stream(self.device, stream)))
+        return v[:self.n_rows].cpu().numpy().astype(bool)
+
+    def coverage(self, stream=None):
+        """calcCoverage: list of int32 numpy vectors (None for NULL rows)."""
+        ln = self.row_lengths()
+        off = np.zeros(self.n_rows + 1, dtype=np.int64)
+        off[1:] = np.cumsum(ln)
+        cov = torch.empty(max(int(off[-1]), 1), dtype=torch.int32, device=f"cuda:{self.device}")
+        v = torch.empty(max(self.n_rows, 1), dtype=torch.uint8, device=f"cuda:{self.device}")
+        check(_lib.lib().rcp_calc_coverage(self.h, cptr(off, _lib._i64p), ptr(cov), ptr(v),
+                                           _stream(self.device, stream)))
+        self.status(stream)
+        hc = cov.cpu().numpy()
+        hv = v[:self.n_rows].cpu().numpy().astype(bool)
+        return [hc[off[r]:off[r + 1]].copy() if hv[r] else None for r in range(self.n_rows)]
+
+    def run(self, stream=None, binsum=False):
+        """Execute, check status, and return (R x n_cols numpy matrix (F order), valid)."""
+        out = self.empty_output()
+        valid = torch.empty(max(self.n_rows, 1), dtype=torch.uint8, device=f"cuda:{self.device}")
+        bs = torch.empty_like(out, dtype=torch.int64) if binsum else None
+        self.execute(out, valid, bs, stream)
+        self.status(stream)
+        mat = out.cpu().numpy().T  # (n_rows, n_cols) view of the column-major buffer: F order
+        v = valid[:self.n_rows].cpu().numpy().astype(bool)
+        if binsum:
+            return mat, v, bs.cpu().numpy().T
+        return mat, v
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib().rcp_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

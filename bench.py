@@ -1,0 +1,232 @@
+"""Benchmark of the recoup coverage -> profile hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c5]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+A step is one pass of the hot path -- calcCoverage + profileMatrix fused: locate kernel,
+LDS pileup-bin kernel, interpolation kernel -- over one synthetic C4 sample
+(200k ChIP peak summits +-1 kb, 1000 bins, 200M reads) with the reads, region tables and
+output matrix already resident in HBM.  Each rank holds its own C4 partition (regions and
+reads are independent objects: weak scaling, no collective on the data path).
+
+Prints ONE JSON line (rank 0): value = region-bins/s over all ranks, plus
+  roofline      the pileup kernel's algorithmic bytes / its HIP-event-timed duration
+  cpu_baseline  the CPU oracle (test infrastructure, `oracle/`) on a bounded sample, timed here
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=["c4", "c2", "c5"])
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--reads", type=int, default=None, help="override read count (smaller runs)")
+    ap.add_argument("--regions", type=int, default=None, help="override region count")
+    ap.add_argument("--cpu-regions", type=int, default=200000, help="CPU baseline sample (regions)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_c4.json"),
+                    help="PMC traffic summary (from tools/pmc_traffic.py) to attach to the roofline")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = f"cuda:{local}"
+    torch.cuda.set_device(local)
+
+    import synthetic
+    from recoup_amd.engine import Bins, Plan, ReadSet, RowTable
+
+    t0 = time.time()
+    kw = {}
+    if args.reads:
+        kw["n_reads"] = args.reads
+    if args.regions:
+        kw["n_regions"] = args.regions
+    data = getattr(synthetic, args.config)(device=dev, seed=args.seed + 7919 * rank, **kw)
+    reads = data["reads"]
+    reg = data["regions"]
+    R = len(reg["start"])
+    n_reads = int(reads[1].numel())
+    n_ovl = synthetic.n_overlaps(reads, reg, data["width"], device=dev)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] data {args.config}: {n_reads} reads, {R} regions in {time.time() - t0:.1f}s")
+
+    t1 = time.time()
+    rs = ReadSet(*reads, data["seqlen"], device=local)
+    rows = RowTable.from_ranges(reg["chrom"], reg["start"], reg["end"], reg["strand"])
+    if data["n_bins"] > 0:
+        bins = Bins([("whole", data["n_bins"])])
+    else:
+        bins = Bins([("whole", 0, sum(data["flank"]))])
+    tp = time.time()
+    plan = Plan(rs, rows, bins)
+    plan_s = time.time() - tp
+    B = plan.n_cols
+    out = plan.empty_output()
+    valid = torch.empty(R, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] readset + plan in {time.time() - t1:.1f}s (plan {plan_s * 1e3:.1f} ms), info {plan.info}")
+
+    # ---- warmup + correctness gate
+    for _ in range(args.warmup):
+        plan.execute(out, valid)
+    plan.status()
+
+    # ---- timed region: exactly K steps between barrier + synchronize
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    for _ in range(args.steps):
+        plan.execute(out, valid)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - ts
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    plan.status()
+
+    # ---- per-kernel durations with HIP events on the launch stream
+    stream = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    kt = np.zeros(3)
+    for _ in range(args.steps):
+        ev[0].record(stream)
+        plan.execute_stages(1, out, valid)
+        ev[1].record(stream)
+        plan.execute_stages(2, out)
+        ev[2].record(stream)
+        plan.execute_stages(4, out)
+        ev[3].record(stream)
+        torch.cuda.synchronize()
+        kt += [ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3])]
+    kt /= args.steps  # ms per launch
+    plan.status()
+
+    units = R * B  # region-bins per step per rank (1 sample)
+    value = world * units * args.steps / elapsed
+    ovl = int(n_ovl.sum())
+    bytes_pileup = 8 * ovl + 16 * R + 8 * R * B  # reads (start,end) + region meta + f64 out
+    achieved = bytes_pileup / (kt[1] * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tr = json.load(open(args.traffic))
+            if tr.get("config") == args.config and tr.get("regions") == R and tr.get("reads") == n_reads:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    # ---- CPU baseline (rank 0, N = 1): the oracle on a bounded sample of the same workload
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu, parity = cpu_baseline(args, data, reads, reg, out, valid, B)
+
+    if rank == 0:
+        res = {
+            "metric": "region-bins/sec (profileMatrix)",
+            "value": value,
+            "unit": "region-bins/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic",
+            "config": {
+                "workload": {"c4": "C4: 200k ChIP peak summits +-1 kb, 1000 bins (2 bp), 200M reads (180 bp)",
+                             "c2": "C2: 10k TSS +-2 kb, 200 bins, 10M reads (180 bp)",
+                             "c5": "C5: 25k regions x 4000 bp per base, 500M reads (50 bp)"}[args.config],
+                "regions_per_gpu": R, "bins": B, "reads_per_gpu": n_reads, "samples": 1,
+                "parallelism": f"region-sharded x{world} (one partition per GPU, no data-path collective)",
+            },
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "kernel": "rcp_pileup_kernel", "algorithmic_bytes_per_launch": bytes_pileup,
+                         "kernel_ms": kt[1]},
+            "cpu_baseline": cpu,
+            "kernel_ms": {"locate": kt[0], "pileup": kt[1], "interp": kt[2]},
+            "n_overlaps": ovl,
+            "plan_ms": plan_s * 1e3,
+            "parity_sample": parity,
+        }
+        print(json.dumps(res), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+def cpu_baseline(args, data, reads, reg, out, valid, B):
+    """The oracle (C restatement of the reference's per-region dataflow, multithreaded over
+    regions like cmclapply with rc = NULL) on the first --cpu-regions regions."""
+    from oracle import oracle as o
+    R = len(reg["start"])
+    m = min(args.cpu_regions, R)
+    ch = reg["chrom"][:m]
+    keep_chroms = np.unique(ch)
+    chrom, start, end, strand = reads
+    sel = torch.isin(chrom, torch.as_tensor(keep_chroms, device=chrom.device, dtype=chrom.dtype))
+    # hand the oracle its reads in (chrom, start) order so its own index skips the sort
+    c, s, e, st = chrom[sel], start[sel], end[sel], strand[sel]
+    key = (c.to(torch.int64) << 42) + (s.to(torch.int64) << 10) + (e - s).to(torch.int64).clamp(0, 1023)
+    order = torch.argsort(key)
+    c, s, e, st = (x[order].cpu().numpy() for x in (c, s, e, st))
+    ix = o.Index(c, s, e, st, data["seqlen"])
+    mask = o.Mask.from_ranges(ch, reg["start"][:m], reg["end"][:m], reg["strand"][:m])
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))
+    n_bins = data["n_bins"]
+    t = time.perf_counter()
+    if n_bins > 0:
+        ref, rvalid = o.profile_part(ix, mask, n_bins, nthreads=threads)
+    else:
+        ref, rvalid = o.profile_part(ix, mask, 0, ncol=B, nthreads=threads)
+    dt = time.perf_counter() - t
+    gpu = out.cpu().numpy().T[:m]
+    gv = valid.cpu().numpy()[:m].astype(bool)
+    parity = bool(np.array_equal(gv, rvalid.astype(bool)) and np.allclose(gpu, ref, rtol=1e-12, atol=0))
+    cpu = {"value": m * B / dt, "unit": "region-bins/s", "cores": threads, "kind": "port",
+           "sample": f"first {m} of {R} regions (all their reads), {n_bins or 'per-base'} bins; oracle/ C "
+                     f"restatement, {threads} threads over regions; {dt:.2f} s"}
+    return cpu, parity
+
+
+if __name__ == "__main__":
+    main()

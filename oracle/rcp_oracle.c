@@ -405,7 +405,9 @@ orc_index* orc_index_build(const orc_reads_in* r, int strand_filter) {
     }
     for (int c = 0; c < r->n_chrom; c++) {
         chrom_reads* cr = &ix->c[c];
-        qsort(buf[c], (size_t)cnt[c], sizeof(rd), cmp_rd);
+        int sorted = 1; /* skip the sort for input already in (start, end) order */
+        for (int64_t i = 1; i < cnt[c] && sorted; i++) sorted = cmp_rd(&buf[c][i - 1], &buf[c][i]) <= 0;
+        if (!sorted) qsort(buf[c], (size_t)cnt[c], sizeof(rd), cmp_rd);
         cr->n = cnt[c];
         cr->start = (int32_t*)malloc(sizeof(int32_t) * (size_t)(cnt[c] ? cnt[c] : 1));
         cr->end = (int32_t*)malloc(sizeof(int32_t) * (size_t)(cnt[c] ? cnt[c] : 1));

@@ -75,12 +75,26 @@ struct RcpPlanDev {
     double* interp_scratch;     // per interp row: 5 * max_interp_len doubles
     int32_t interp_stride;
     // geometry
-    int32_t chunk_cap;          // max positions per chunk (diff array capacity)
+    int32_t chunk_cap;          // max positions per chunk (one wave's difference array)
+    int32_t wave_words;         // LDS words per wave difference array (multiple of 256)
     int32_t stage_cap;          // max bins per chunk
+    int32_t interp_cap;         // max positions of an interpolated slice
     // coverage (CSR) mode
     const int64_t* csr_off;     // non-null: write per-row depth into csr (calcCoverage)
     int32_t* csr_out;
-    // status
+    // skewed depth: rows with more than heavy_threshold candidate reads are piled up
+    // first by many workgroups (heavy slices) into a global difference array
+    uint32_t* ncand;            // [n_rows] candidate reads (locate output)
+    int32_t heavy_threshold;    // 0 = heavy path off
+    int32_t heavy_cap;          // slots
+    int32_t heavy_stride;       // ints per slot (>= max row length + 1 of eligible rows)
+    int32_t heavy_max_len;      // rows longer than this never take the heavy path
+    int32_t heavy_slice;        // candidate reads per heavy work item
+    int32_t* heavy_slot;        // [n_rows] slot or -1 (locate output)
+    int32_t* heavy_rows;        // [heavy_cap]
+    uint32_t* heavy_slice_off;  // [heavy_cap + 1]
+    int32_t* heavy_gdiff;       // [heavy_cap * heavy_stride], zero between executions
+    // status (status[0]) and heavy slot counter (status[1])
     uint32_t* status;           // bit 0: numerator overflow, bit 1: per-base width mismatch
 };
 

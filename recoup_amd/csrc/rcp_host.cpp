@@ -27,9 +27,13 @@ hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, u
 hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
                            hipStream_t stream);
 hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream);
+hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_t stream);
+hipError_t rcp_launch_heavy_clear(const RcpPlanDev* P, hipStream_t stream);
 hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_t* binsum, int csr, hipStream_t stream);
 hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStream_t stream);
-size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int tile_rows, int csr);
+size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr);
+size_t rcp_interp_lds_bytes(const RcpPlanDev* P);
+int rcp_tile_rows(void);
 hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
                               const int8_t* strand, int32_t n_chrom, int32_t strand_filter, uint64_t* keys,
                               int32_t* vals, hipStream_t stream);
@@ -40,9 +44,18 @@ hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* 
 
 namespace {
 
-constexpr int kTileRows = 16;
-constexpr int kChunkMax = 16384;     // positions per workgroup chunk (LDS difference array)
-constexpr int kStageMaxBins = 1024;  // bins per chunk (LDS stage = bins x 16 rows x 4 B)
+constexpr int kChunkMax = 16384;       // positions per chunk (one wave's LDS difference array)
+constexpr int kStageMaxBins = 1024;    // bins per chunk (LDS stage = bins x 8 rows x 4 B)
+constexpr size_t kLdsBudget = 80 * 1024;  // keep two pileup workgroups per CU when possible
+constexpr int kHeavyThreshold = 8192;  // candidate reads above which a row is split across workgroups
+constexpr int kHeavySlice = 16384;     // candidate reads per heavy work item
+constexpr int kHeavyMaxLen = 16383;    // longer rows never take the heavy path
+constexpr int kHeavyGrid = 1024;
+
+int env_int(const char* name, int def) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : def;
+}
 
 thread_local std::string g_err;
 
@@ -398,6 +411,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     int64_t col = 0;
     int32_t chunk_cap = 1024, stage_cap = 1;
     int32_t max_interp_len = 0, max_interp_bins = 0;
+    std::vector<int32_t> part_max_bin(RCP_MAX_PARTS, 1);
     std::map<std::pair<int, int>, int32_t> layout_cache;  // (n, dif) -> offset in lay_cnt
     std::map<std::pair<int, int>, int32_t> nb_cache;      // (n, L) -> offset in nb_pos
     for (int p = 0; p < bins->n_parts; ++p) {
@@ -486,21 +500,69 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
         if (max_bin > kChunkMax)
             return fail(RCP_EUNSUPPORTED, "part %d: a bin of %d positions exceeds the %d-position chunk", p, max_bin,
                         kChunkMax);
-        pt.chunk_bins = std::min<int32_t>(pt.n_bins, std::min<int32_t>(kStageMaxBins, kChunkMax / max_bin));
-        pt.n_chunks = (pt.n_bins + pt.chunk_bins - 1) / pt.chunk_bins;
-        chunk_cap = std::max(chunk_cap, pt.chunk_bins * max_bin);
-        stage_cap = std::max(stage_cap, pt.chunk_bins);
+        part_max_bin[p] = max_bin;
     }
-    if (cov_only) chunk_cap = std::min(kChunkMax, std::max(chunk_cap, plan->max_row_len));
     if (max_interp_len > kChunkMax)
         return fail(RCP_EUNSUPPORTED, "interpolated slice of %d positions exceeds %d", max_interp_len, kChunkMax);
-    chunk_cap = std::max(chunk_cap, max_interp_len);
+
+    // ---- geometry: the largest per-wave chunk (positions) whose LDS (4 wave difference
+    // arrays + the [bin][row] stage) keeps two workgroups per CU; else the smallest feasible.
+    {
+        int32_t need = 1024;
+        for (int p = 0; p < P.n_parts; ++p) need = std::max(need, P.part[p].n_bins * part_max_bin[p]);
+        if (cov_only) need = std::max(need, plan->max_row_len);
+        need = std::min(need, kChunkMax);
+        const int32_t cands[] = {need, 8192, 4096, 2048, 1024, 512};
+        int32_t best = -1;
+        size_t best_lds = 0;
+        for (int32_t ch : cands) {
+            if (ch > need) continue;
+            int32_t stage = 1;
+            bool ok = true;
+            for (int p = 0; p < P.n_parts; ++p) {
+                if (part_max_bin[p] > ch) ok = false;
+                stage = std::max<int32_t>(stage, std::min<int32_t>(P.part[p].n_bins,
+                                                                   std::min<int32_t>(kStageMaxBins, ch / part_max_bin[p])));
+            }
+            if (!ok) break;  // smaller chunks cannot hold the largest bin either
+            RcpPlanDev t{};
+            t.wave_words = ((ch + 1) + 255) & ~255;
+            t.stage_cap = cov_only ? 0 : stage;
+            const size_t lds = rcp_pileup_lds_bytes(&t, cov_only ? 1 : 0);
+            best = ch;
+            best_lds = lds;
+            if (lds <= kLdsBudget) break;
+        }
+        if (best < 0) return fail(RCP_EUNSUPPORTED, "no chunk geometry fits the bins");
+        (void)best_lds;
+        chunk_cap = best;
+        for (int p = 0; p < P.n_parts; ++p) {
+            RcpPart& pt = P.part[p];
+            pt.chunk_bins = std::min<int32_t>(pt.n_bins, std::min<int32_t>(kStageMaxBins, chunk_cap / part_max_bin[p]));
+            pt.n_chunks = (pt.n_bins + pt.chunk_bins - 1) / pt.chunk_bins;
+            stage_cap = std::max(stage_cap, pt.chunk_bins);
+        }
+    }
     P.n_cols = col;
     plan->n_cols = col;
-    P.chunk_cap = chunk_cap;
+    P.wave_words = ((chunk_cap + 1) + 255) & ~255;
+    P.chunk_cap = P.wave_words - 1;
     P.stage_cap = stage_cap;
+    P.interp_cap = std::max(max_interp_len, 1);
     P.n_chunks_total = 0;
     for (int p = 0; p < P.n_parts; ++p) P.n_chunks_total += P.part[p].n_chunks;
+
+    // ---- skewed rows: heavy slots sized for the eligible (short enough) rows
+    const int32_t heavy_thr = env_int("RCP_HEAVY_THRESHOLD", kHeavyThreshold);
+    int32_t eligible_len = 0;
+    for (int r = 0; r < R; ++r)
+        if (B.row_len[r] <= kHeavyMaxLen) eligible_len = std::max(eligible_len, B.row_len[r]);
+    P.heavy_threshold = heavy_thr;
+    P.heavy_max_len = eligible_len;
+    P.heavy_stride = ((eligible_len + 1) + 63) & ~63;
+    P.heavy_slice = kHeavySlice;
+    P.heavy_cap = (int32_t)std::min<int64_t>(std::max(R, 1), std::min<int64_t>(4096, (256ll << 20) / (4ll * P.heavy_stride)));
+    if (heavy_thr <= 0 || R == 0) P.heavy_threshold = 0;
 
     // ---- upload tables (one arena)
     std::vector<char> blob;
@@ -519,10 +581,26 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     HIP_TRY(plan->tables.alloc(blob.size()));
     HIP_TRY(hipMemcpy(plan->tables.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
     char* base = plan->tables.as<char>();
+    // ---- work arena: locate outputs, heavy-row state, status words
     const int64_t S = std::max<int64_t>(plan->n_seg, 1);
-    const size_t w_lo = 0, w_hi = 12 * S, w_valid = 24 * S, w_status = (24 * S + R + 255) & ~size_t(255);
+    const int64_t Rw = std::max(R, 1);
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t w_lo = 0;
+    const size_t w_hi = al(w_lo + 12 * S);
+    const size_t w_valid = al(w_hi + 12 * S);
+    const size_t w_ncand = al(w_valid + Rw);
+    const size_t w_hslot = al(w_ncand + 4 * Rw);
+    const size_t w_hrows = al(w_hslot + 4 * Rw);
+    const size_t w_hoff = al(w_hrows + 4 * (size_t)P.heavy_cap);
+    const size_t w_gdiff = al(w_hoff + 4 * ((size_t)P.heavy_cap + 1));
+    const size_t w_status = al(w_gdiff + (P.heavy_threshold > 0 ? 4 * (size_t)P.heavy_cap * P.heavy_stride : 0));
     HIP_TRY(plan->work.alloc(w_status + 256));
     char* wb = plan->work.as<char>();
+    P.ncand = reinterpret_cast<uint32_t*>(wb + w_ncand);
+    P.heavy_slot = reinterpret_cast<int32_t*>(wb + w_hslot);
+    P.heavy_rows = reinterpret_cast<int32_t*>(wb + w_hrows);
+    P.heavy_slice_off = reinterpret_cast<uint32_t*>(wb + w_hoff);
+    P.heavy_gdiff = reinterpret_cast<int32_t*>(wb + w_gdiff);
     const int32_t n_interp = (int32_t)B.interp_row.size();
     P.interp_stride = 2 * (max_interp_bins + 1) + 3 * (max_interp_len + 1) + 8;
     if (n_interp) HIP_TRY(plan->scratch.alloc(8 * (size_t)n_interp * P.interp_stride));
@@ -553,8 +631,8 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.interp_scratch = plan->scratch.as<double>();
     P.csr_off = nullptr;
     P.csr_out = nullptr;
-    plan->lds = rcp_pileup_lds_bytes(&P, kTileRows, 0);
-    plan->grid = (int64_t)((R + kTileRows - 1) / kTileRows) * P.n_chunks_total;
+    plan->lds = rcp_pileup_lds_bytes(&P, cov_only ? 1 : 0);
+    plan->grid = (int64_t)((R + rcp_tile_rows() - 1) / rcp_tile_rows()) * P.n_chunks_total;
     if (plan->lds > 160 * 1024) return fail(RCP_EUNSUPPORTED, "plan needs %zu B of LDS", plan->lds);
     HIP_TRY(hipMemset(plan->work.p, 0, plan->work.bytes));
     *out = plan.release();
@@ -575,7 +653,7 @@ extern "C" int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info) {
     info->n_interp_rows = plan->dev.n_interp;
     info->lds_bytes = (int64_t)plan->lds;
     info->grid = plan->grid;
-    info->tile_rows = kTileRows;
+    info->tile_rows = rcp_tile_rows();
     info->chunk_positions = plan->dev.chunk_cap;
     return RCP_OK;
 }
@@ -591,6 +669,7 @@ extern "C" int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_str
     DeviceGuard g(plan->rs->device);
     HIP_TRY(g.err);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    HIP_TRY(hipMemsetAsync(plan->dev.status, 0, 8, s));
     HIP_TRY(rcp_launch_locate(&plan->dev, s));
     if (d_valid && plan->n_rows)
         HIP_TRY(hipMemcpyAsync(d_valid, plan->dev.valid, plan->n_rows, hipMemcpyDeviceToDevice, s));
@@ -606,11 +685,15 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
     HIP_TRY(g.err);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     if (stages & RCP_STAGE_LOCATE) {
-        HIP_TRY(hipMemsetAsync(plan->dev.status, 0, 4, s));
+        HIP_TRY(hipMemsetAsync(plan->dev.status, 0, 8, s));
         HIP_TRY(rcp_launch_locate(&plan->dev, s));
+        HIP_TRY(rcp_launch_heavy(&plan->dev, kHeavyGrid, s));
     }
     if (stages & RCP_STAGE_PILEUP) HIP_TRY(rcp_launch_pileup(&plan->dev, d_out, d_binsum, 0, s));
-    if (stages & RCP_STAGE_INTERP) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
+    if (stages & RCP_STAGE_INTERP) {
+        HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
+        HIP_TRY(rcp_launch_heavy_clear(&plan->dev, s));
+    }
     if ((stages & RCP_STAGE_LOCATE) && d_valid && plan->n_rows)
         HIP_TRY(hipMemcpyAsync(d_valid, plan->dev.valid, plan->n_rows, hipMemcpyDeviceToDevice, s));
     return RCP_OK;
@@ -682,9 +765,11 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
     HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * (plan->n_rows + 1), hipMemcpyHostToDevice, s));
     P.csr_off = d_off.as<int64_t>();
     P.csr_out = d_cov;
-    HIP_TRY(hipMemsetAsync(plan->dev.status, 0, 4, s));
+    HIP_TRY(hipMemsetAsync(plan->dev.status, 0, 8, s));
     HIP_TRY(rcp_launch_locate(&P, s));
+    HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
+    HIP_TRY(rcp_launch_heavy_clear(&P, s));
     if (d_valid && plan->n_rows)
         HIP_TRY(hipMemcpyAsync(d_valid, plan->dev.valid, plan->n_rows, hipMemcpyDeviceToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));  // d_off is released on return

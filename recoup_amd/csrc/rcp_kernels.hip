@@ -3,6 +3,8 @@
 // What they compute (reference semantics):
 //   rcp_locate_kernel   findOverlaps() per region / range / strand stream, plus the
 //                       NULL rules of coverageFromRanges (R/coverage.R:189-225)
+//   rcp_heavy_*         rows with skewed depth (hot peaks): their reads are split into
+//                       slices piled up by many workgroups into a global difference array
 //   rcp_pileup_kernel   coverage(reads)[i2k] (+ rev for '-')  ->  splitVector bins ->
 //                       mean / median (R/util.R:74-84) for a tile of rows, written as the
 //                       R column-major profile matrix (R/profile.R:153-212, :100-151)
@@ -11,13 +13,14 @@
 //   readset kernels     splitBySeqname as a (chromosome, strand) stream index with a
 //                       prefix-max-of-end array for exact overlap search
 //
-// Design: integer interval counting, HBM-bound, no MFMA.  Each workgroup owns
-// T consecutive rows x one column chunk.  Reads of a row are streamed coalesced as 8-byte
-// (start, end) pairs from HBM into +w/-w LDS atomics on a difference array; a two-level
-// block scan turns it into depth and cumulative depth (uint32, modular: any bin sum that
-// fits 32 bits comes out exact), so each bin is two LDS reads; numerators are staged in
-// LDS as [bin][row] so the epilogue writes 16 consecutive rows of a column (128 B) per
-// 16 lanes of the R column-major matrix.
+// Design: integer interval counting, HBM-bound, no MFMA.  A workgroup owns
+// T = 8 consecutive rows x one column chunk; each of its 4 waves owns whole rows, so a
+// row needs no block barrier: the wave streams the row's reads as coalesced 8-byte
+// (start, end) pairs (4 loads in flight per lane), adds +w / -w into its own LDS
+// difference array, turns it into depth / cumulative depth with a wave scan (uint32,
+// modular: a bin sum that fits 32 bits comes out exact), and reads every bin with two LDS
+// reads.  Numerators are staged as [bin][row] so the epilogue writes 8 consecutive rows of a
+// column (64 B) per 8 lanes of the R column-major matrix.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -25,8 +28,9 @@
 
 namespace {
 
-constexpr int kBlock = RCP_BLOCK;
+constexpr int kBlock = RCP_BLOCK;  // 256 threads = 4 waves
 constexpr int kWaves = kBlock / 64;
+constexpr int kTile = 8;           // rows per output round (64 B column segments)
 
 __device__ __forceinline__ uint32_t lower_bound_pmax(const int32_t* __restrict__ pmax, uint32_t lo,
                                                      uint32_t hi, int32_t v) {
@@ -48,6 +52,23 @@ __device__ __forceinline__ uint32_t upper_bound_start(const int2* __restrict__ s
     return lo;
 }
 
+__device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x - v;
+}
+
+__device__ __forceinline__ int32_t wave_sum(int32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
 // Block-wide exclusive scan of one uint32 per thread.  `scratch` holds kWaves words.
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* scratch) {
     const int lane = threadIdx.x & 63;
@@ -55,7 +76,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
     uint32_t x = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
+        const uint32_t y = __shfl_up(x, d, 64);
         if (lane >= d) x += y;
     }
     if (lane == 63) scratch[wave] = x;
@@ -67,14 +88,43 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
     return off + x - v;
 }
 
+
 // ---------------------------------------------------------------------------------
-// Pile the candidate reads of row r over row positions [P0, P0 + npos) into the LDS
-// difference array `diff` (npos + 1 used words, zeroed by the caller).  Returns the number
-// of candidate reads seen (identical in every thread) for the overflow bound.
+// Add read `rd` of segment sg to the difference array of row positions [P0, P0 + npos)
+// restricted to the genomic piece [gps, gpe] of the segment.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ void pileup_rows_segments(const RcpPlanDev& P, int r, int32_t P0,
-                                                     int32_t npos, int32_t* diff) {
-    const int tid = threadIdx.x;
+__device__ __forceinline__ void add_read(const RcpPlanDev& P, const RcpSeg& sg, int2 rd, int32_t gps, int32_t gpe,
+                                         int32_t P0, int32_t* diff) {
+    if (rd.y < gps || rd.x > gpe) return;
+    int32_t w = 1;
+    if (sg.multi) {
+        // subjectHits repeats a read once per range of the list it overlaps
+        // (R/coverage.R:190-192): weight = number of overlapped ranges.
+        w = 0;
+        for (int g = sg.gfirst; g < sg.gfirst + sg.gcount; ++g) {
+            const RcpSeg o = P.segs[g];
+            w += (o.query_ok && o.lo <= rd.y && o.hi >= rd.x) ? 1 : 0;
+        }
+    }
+    const int32_t x0 = max(rd.x, gps);
+    const int32_t x1 = min(rd.y, gpe);
+    int32_t o0, o1;
+    if (!sg.rev) {
+        o0 = sg.off + (x0 - sg.lo);
+        o1 = sg.off + (x1 - sg.lo);
+    } else {
+        o0 = sg.off + (sg.hi - x1);
+        o1 = sg.off + (sg.hi - x0);
+    }
+    atomicAdd(&diff[o0 - P0], w);
+    atomicAdd(&diff[o1 - P0 + 1], -w);
+}
+
+// Pile the candidate reads of row r over row positions [P0, P0 + npos) into `diff`
+// (npos + 1 words, zeroed by the caller).  Threads `t` of `nt` (a wave or a block) split
+// the reads; each keeps 4 coalesced loads in flight.
+__device__ __forceinline__ void pileup_row(const RcpPlanDev& P, int r, int32_t P0, int32_t npos, int32_t* diff,
+                                           int t, int nt) {
     const int32_t P1 = P0 + npos;
     const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
     for (int j = j0; j < j1; ++j) {
@@ -100,44 +150,26 @@ __device__ __forceinline__ void pileup_rows_segments(const RcpPlanDev& P, int r,
             if (!full) {
                 lo = lower_bound_pmax(P.pmax, lo, hi, gps);
                 hi = upper_bound_start(P.se, lo, hi, gpe);
+                if (lo >= hi) continue;
             }
-            for (uint32_t idx = lo + tid; idx < hi; idx += kBlock) {
-                const int2 rd = P.se[idx];
-                if (rd.y < gps) continue;
-                int32_t w = 1;
-                if (sg.multi) {
-                    // subjectHits repeats a read once per range of the list it overlaps
-                    // (R/coverage.R:190-192): weight = number of overlapped ranges.
-                    w = 0;
-                    for (int g = sg.gfirst; g < sg.gfirst + sg.gcount; ++g) {
-                        const RcpSeg o = P.segs[g];
-                        w += (o.query_ok && o.lo <= rd.y && o.hi >= rd.x) ? 1 : 0;
-                    }
-                }
-                const int32_t x0 = max(rd.x, gps);
-                const int32_t x1 = min(rd.y, gpe);
-                int32_t o0, o1;
-                if (!sg.rev) {
-                    o0 = sg.off + (x0 - sg.lo);
-                    o1 = sg.off + (x1 - sg.lo);
-                } else {
-                    o0 = sg.off + (sg.hi - x1);
-                    o1 = sg.off + (sg.hi - x0);
-                }
-                atomicAdd(&diff[o0 - P0], w);
-                atomicAdd(&diff[o1 - P0 + 1], -w);
+            for (uint32_t base = lo + t; base < hi; base += 4 * nt) {
+                int2 rd[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) rd[u] = P.se[min(base + u * nt, hi - 1)];  // clamped: no branch
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (base + u * nt < hi) add_read(P, sg, rd[u], gps, gpe, P0, diff);
             }
         }
     }
 }
 
-// Turn diff[0 .. 256*per) into depth (CUM = false) or cumulative depth (CUM = true).
-// `per` is a multiple of 4.  scratch: 2*kWaves words.
+// Wave scan of diff[0 .. 64*per): depth (CUM = false) or cumulative depth (CUM = true).
 template <bool CUM>
-__device__ __forceinline__ void scan_chunk(int32_t* diff, int per, uint32_t* scratch) {
-    const int tid = threadIdx.x;
-    uint32_t* base = reinterpret_cast<uint32_t*>(diff) + tid * per;
-    uint32_t A = 0, B = 0;  // sum of diff, sum of local depth prefix
+__device__ __forceinline__ void scan_wave(int32_t* diff, int per) {
+    const int lane = threadIdx.x & 63;
+    uint32_t* base = reinterpret_cast<uint32_t*>(diff) + lane * per;
+    uint32_t A = 0, B = 0;  // sum of diff, sum of the local depth prefix
     for (int q = 0; q < per; q += 4) {
         const uint4 v = *reinterpret_cast<const uint4*>(base + q);
         A += v.x; B += A;
@@ -145,12 +177,12 @@ __device__ __forceinline__ void scan_chunk(int32_t* diff, int per, uint32_t* scr
         A += v.z; B += A;
         A += v.w; B += A;
     }
-    const uint32_t D = block_exclusive_scan(A, scratch);  // depth entering this thread
+    const uint32_t D = wave_exclusive_scan(A);  // depth entering this lane
     uint32_t C = 0;
-    if (CUM) C = block_exclusive_scan((uint32_t)per * D + B, scratch + kWaves);
+    if (CUM) C = wave_exclusive_scan((uint32_t)per * D + B);
     uint32_t l = D, c = C;
     for (int q = 0; q < per; q += 4) {
-        uint4 v = *reinterpret_cast<const uint4*>(base + q);
+        const uint4 v = *reinterpret_cast<const uint4*>(base + q);
         uint4 o;
         l += v.x; c += l; o.x = CUM ? c : l;
         l += v.y; c += l; o.y = CUM ? c : l;
@@ -160,14 +192,26 @@ __device__ __forceinline__ void scan_chunk(int32_t* diff, int per, uint32_t* scr
     }
 }
 
-__device__ __forceinline__ int32_t bin_edge(int32_t bs, int32_t lay, const int32_t* __restrict__ cnt,
-                                            int32_t k) {
+// Block scan (interpolation kernel): diff[0 .. 256*per) -> depth.
+__device__ __forceinline__ void scan_block_depth(int32_t* diff, int per, uint32_t* scratch) {
+    const int tid = threadIdx.x;
+    uint32_t* base = reinterpret_cast<uint32_t*>(diff) + tid * per;
+    uint32_t A = 0;
+    for (int q = 0; q < per; ++q) A += base[q];
+    uint32_t l = block_exclusive_scan(A, scratch);
+    for (int q = 0; q < per; ++q) {
+        l += base[q];
+        base[q] = l;
+    }
+}
+
+__device__ __forceinline__ int32_t bin_edge(int32_t bs, int32_t lay, const int32_t* __restrict__ cnt, int32_t k) {
     return bs * k + (lay >= 0 ? cnt[lay + k] : 0);
 }
 
 // k-th smallest (1-based) of depth[a .. b) by bisection on the value (depth is >= 0).
-__device__ __forceinline__ uint32_t kth_smallest(const int32_t* d, int32_t a, int32_t b, int32_t k,
-                                                 int32_t vmin, int32_t vmax) {
+__device__ __forceinline__ uint32_t kth_smallest(const int32_t* d, int32_t a, int32_t b, int32_t k, int32_t vmin,
+                                                 int32_t vmax) {
     int32_t lo = vmin, hi = vmax;
     while (lo < hi) {
         const int32_t mid = lo + ((hi - lo) >> 1);
@@ -176,6 +220,25 @@ __device__ __forceinline__ uint32_t kth_smallest(const int32_t* d, int32_t a, in
         if (c >= k) hi = mid; else lo = mid + 1;
     }
     return (uint32_t)lo;
+}
+
+// Candidate read `q` (0-based over the row's (segment, stream) ranges in order) -> the
+// segment and read index.  Returns false past the end.
+__device__ __forceinline__ bool nth_candidate(const RcpPlanDev& P, int r, uint32_t q, int* seg, uint32_t* idx) {
+    const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
+    for (int j = j0; j < j1; ++j) {
+        for (int s = 0; s < 3; ++s) {
+            const uint32_t lo = P.seg_lo[j * 3 + s], hi = P.seg_hi[j * 3 + s];
+            const uint32_t c = hi > lo ? hi - lo : 0;
+            if (q < c) {
+                *seg = j;
+                *idx = lo + q;
+                return true;
+            }
+            q -= c;
+        }
+    }
+    return false;
 }
 
 }  // namespace
@@ -205,8 +268,7 @@ __global__ void rcp_fill_i64_kernel(int64_t* p, int64_t n, int64_t v) {
     if (i < n) p[i] = v;
 }
 
-__global__ void rcp_stream_bounds_kernel(int64_t n, const uint64_t* __restrict__ keys,
-                                         int64_t* __restrict__ off) {
+__global__ void rcp_stream_bounds_kernel(int64_t n, const uint64_t* __restrict__ keys, int64_t* __restrict__ off) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t sid = (int64_t)(keys[i] >> 32);
@@ -225,14 +287,13 @@ __global__ void rcp_pack_kernel(int64_t n, const uint64_t* __restrict__ keys, co
     scan_in[i] = (k & 0xFFFFFFFF00000000ull) | (uint64_t)((uint32_t)end ^ 0x80000000u);
 }
 
-__global__ void rcp_unpack_pmax_kernel(int64_t n, const uint64_t* __restrict__ scan_out,
-                                       int32_t* __restrict__ pmax) {
+__global__ void rcp_unpack_pmax_kernel(int64_t n, const uint64_t* __restrict__ scan_out, int32_t* __restrict__ pmax) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) pmax[i] = (int32_t)((uint32_t)scan_out[i] ^ 0x80000000u);
 }
 
 struct SegMaxOp {
-    // segmented max: keys in the high word, biased ends in the low word
+    // segmented max: stream id in the high word, biased ends in the low word
     __host__ __device__ __forceinline__ uint64_t operator()(const uint64_t& a, const uint64_t& b) const {
         if ((a >> 32) != (b >> 32)) return b;
         return ((uint32_t)a > (uint32_t)b) ? ((b & 0xFFFFFFFF00000000ull) | (uint32_t)a) : b;
@@ -240,19 +301,17 @@ struct SegMaxOp {
 };
 
 extern "C" hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, uint64_t* kout,
-                                     const int32_t* vin, int32_t* vout, int64_t n, int end_bit,
-                                     hipStream_t stream) {
-    return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, kin, kout, vin, vout, (int)n, 0, end_bit,
-                                              stream);
+                                     const int32_t* vin, int32_t* vout, int64_t n, int end_bit, hipStream_t stream) {
+    return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, kin, kout, vin, vout, (int)n, 0, end_bit, stream);
 }
 
-extern "C" hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
-                                      int64_t n, hipStream_t stream) {
+extern "C" hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
+                                      hipStream_t stream) {
     return hipcub::DeviceScan::InclusiveScan(temp, *temp_bytes, in, out, SegMaxOp(), (int)n, stream);
 }
 
 // =================================================================================
-// locate: per (row, segment, stream) read ranges and the NULL rules
+// locate: per (row, segment, stream) read ranges, the NULL rules, heavy-row slots
 // =================================================================================
 __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -264,6 +323,7 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
     bool present[4] = {false, false, false, false};
     int32_t maxend[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
     int32_t maxpos[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
+    uint32_t ncand = 0;
     for (int j = j0; j < j1; ++j) {
         const RcpSeg sg = P.segs[j];
         const int g = sg.group & 3;
@@ -279,6 +339,7 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
                 if (lo < hi) {
                     hit[g] = true;
                     maxend[g] = max(maxend[g], P.pmax[hi - 1]);
+                    ncand += hi - lo;
                 }
             }
             P.seg_lo[j * 3 + s] = lo;
@@ -296,19 +357,157 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
         }
     }
     P.valid[r] = valid ? 1 : 0;
+    P.ncand[r] = ncand;
+    int32_t slot = -1;
+    if (valid && P.heavy_threshold > 0 && ncand > (uint32_t)P.heavy_threshold && P.row_len[r] <= P.heavy_max_len) {
+        const uint32_t s = atomicAdd(&P.status[1], 1u);
+        if (s < (uint32_t)P.heavy_cap) {
+            slot = (int32_t)s;
+            P.heavy_rows[s] = r;
+        }
+    }
+    P.heavy_slot[r] = slot;
+}
+
+// =================================================================================
+// heavy rows: slice offsets (1 block), slice pileup (many blocks), cleanup
+// =================================================================================
+__global__ void __launch_bounds__(kBlock) rcp_heavy_plan_kernel(RcpPlanDev P) {
+    __shared__ uint32_t scratch[kWaves];
+    __shared__ uint32_t carry;
+    const uint32_t n = min(P.status[1], (uint32_t)P.heavy_cap);
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b = 0; b < n; b += kBlock) {
+        const uint32_t s = b + threadIdx.x;
+        uint32_t c = 0;
+        if (s < n) {
+            const uint32_t nc = P.ncand[P.heavy_rows[s]];
+            c = (nc + P.heavy_slice - 1) / P.heavy_slice;
+        }
+        const uint32_t ex = block_exclusive_scan(c, scratch);
+        const uint32_t base = carry;
+        if (s < n) P.heavy_slice_off[s] = base + ex;
+        __syncthreads();
+        if (threadIdx.x == kBlock - 1) carry = base + ex + c;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) P.heavy_slice_off[n] = carry;
+}
+
+__global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int32_t* diff = reinterpret_cast<int32_t*>(smem);
+    const uint32_t n = min(P.status[1], (uint32_t)P.heavy_cap);
+    if (n == 0) return;
+    const uint32_t total = P.heavy_slice_off[n];
+    for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
+        // slot holding slice w
+        uint32_t lo = 0, hi = n;
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (P.heavy_slice_off[m] <= w) lo = m; else hi = m;
+        }
+        const int slot = (int)lo;
+        const int r = P.heavy_rows[slot];
+        const int32_t nr = P.row_len[r];
+        const uint32_t q0 = (w - P.heavy_slice_off[slot]) * (uint32_t)P.heavy_slice;
+        const uint32_t q1 = min(q0 + (uint32_t)P.heavy_slice, P.ncand[r]);
+        for (int q = threadIdx.x; q <= nr; q += kBlock) diff[q] = 0;
+        __syncthreads();
+        for (uint32_t q = q0 + threadIdx.x; q < q1; q += kBlock) {
+            int j;
+            uint32_t idx;
+            if (!nth_candidate(P, r, q, &j, &idx)) break;
+            const RcpSeg sg = P.segs[j];
+            add_read(P, sg, P.se[idx], sg.lo, sg.hi, 0, diff);
+        }
+        __syncthreads();
+        int32_t* g = P.heavy_gdiff + (size_t)slot * P.heavy_stride;
+        for (int q = threadIdx.x; q <= nr; q += kBlock) {
+            const int32_t v = diff[q];
+            if (v) atomicAdd(&g[q], v);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void rcp_heavy_clear_kernel(RcpPlanDev P) {
+    const uint32_t n = min(P.status[1], (uint32_t)P.heavy_cap);
+    for (uint32_t s = blockIdx.x; s < n; s += gridDim.x) {
+        int32_t* g = P.heavy_gdiff + (size_t)s * P.heavy_stride;
+        const int32_t nr = P.row_len[P.heavy_rows[s]];
+        for (int q = threadIdx.x; q <= nr; q += blockDim.x) g[q] = 0;
+    }
 }
 
 // =================================================================================
 // pileup -> bins -> column-major profile (or CSR coverage)
 // =================================================================================
-template <int T, bool MEDIAN, bool CSR>
+// A workgroup owns kRounds x kTile rows x one column chunk.  Per round, each of the 4 waves
+// piles up 2 rows (one at a time) into its own LDS difference array and stages the bin
+// numerators; the block then writes the round's kTile rows column by column.
+//
+// Latency: all per-row metadata (segment, read ranges per strand stream, refined for the
+// chunk) is resolved once per workgroup by one thread per row (parallel binary searches),
+// and each wave issues the loads of its NEXT row's first 256 candidate reads before
+// working on the current row's LDS, so a row's HBM round trip overlaps the previous row.
+constexpr int kRounds = 4;
+constexpr int kRows = kTile * kRounds;  // rows per workgroup
+
+struct RowMeta {  // [kRows] each, in LDS
+    int32_t flag, bs, lay, P0, npos, kend, heavy;
+    int32_t fast;                 // 1 = single range, reads resolved below
+    int32_t off, slo, shi, rev;   // the range: row offset, genomic run, reversed
+    int32_t gps, gpe;             // genomic piece covered by this chunk
+    uint32_t lo[3], hi[3];        // candidate reads per strand stream (refined to the piece)
+};
+constexpr int kMetaWords = sizeof(RowMeta) / 4;
+
+__device__ __forceinline__ uint32_t fast_candidates(const RowMeta& m) {
+    return (m.hi[0] - m.lo[0]) + (m.hi[1] - m.lo[1]) + (m.hi[2] - m.lo[2]);
+}
+
+// index of candidate q of a fast row (q < fast_candidates)
+__device__ __forceinline__ uint32_t fast_index(const RowMeta& m, uint32_t q) {
+    const uint32_t c0 = m.hi[0] - m.lo[0];
+    const uint32_t c1 = m.hi[1] - m.lo[1];
+    return q < c0 ? m.lo[0] + q : (q < c0 + c1 ? m.lo[1] + (q - c0) : m.lo[2] + (q - c0 - c1));
+}
+
+__device__ __forceinline__ void add_read_fast(const RowMeta& m, int2 rd, int32_t* diff) {
+    if (rd.y < m.gps || rd.x > m.gpe) return;
+    const int32_t x0 = max(rd.x, m.gps);
+    const int32_t x1 = min(rd.y, m.gpe);
+    int32_t o0, o1;
+    if (!m.rev) {
+        o0 = m.off + (x0 - m.slo);
+        o1 = m.off + (x1 - m.slo);
+    } else {
+        o0 = m.off + (m.shi - x1);
+        o1 = m.off + (m.shi - x0);
+    }
+    atomicAdd(&diff[o0 - m.P0], 1);
+    atomicAdd(&diff[o1 - m.P0 + 1], -1);
+}
+
+__device__ __forceinline__ void lds_order() {
+    // a wave's LDS operations complete in issue order; keep the compiler from moving them
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <bool MEDIAN, bool CSR>
 __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
                                                             int64_t* __restrict__ binsum) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int T = kTile;
     const int tid = threadIdx.x;
-    // ---- decode (row tile, part, chunk)
-    const int tile = blockIdx.x / P.n_chunks_total;
-    int c = blockIdx.x - tile * P.n_chunks_total;
+    const int wave = tid >> 6;
+    const int lane = tid & 63;
+    // ---- decode (row block, part, chunk)
+    const int blk = blockIdx.x / P.n_chunks_total;
+    int c = blockIdx.x - blk * P.n_chunks_total;
     int p = 0;
     while (p < P.n_parts - 1 && c >= P.part[p].n_chunks) {
         c -= P.part[p].n_chunks;
@@ -316,140 +515,241 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
     }
     const RcpPart part = P.part[p];
     const int32_t k0 = c * part.chunk_bins;
+    const int row0 = blk * kRows;
 
-    int32_t* diff = reinterpret_cast<int32_t*>(smem);
-    const int diff_words = (P.chunk_cap + 8 + 1023) & ~1023;
-    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + diff_words;
-    int32_t* m_bs = reinterpret_cast<int32_t*>(stage + (CSR ? 0 : P.stage_cap * T));
-    int32_t* m_lay = m_bs + T;
-    int32_t* m_P0 = m_lay + T;
-    int32_t* m_npos = m_P0 + T;
-    int32_t* m_kend = m_npos + T;
-    int32_t* m_flag = m_kend + T;
-    uint32_t* scratch = reinterpret_cast<uint32_t*>(m_flag + T);
+    // per wave: 4 zero words (cum[-1] == 0) then the difference / depth / cumulative array
+    int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * (P.wave_words + 4) + 4;
+    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kWaves * (P.wave_words + 4);
+    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : P.stage_cap * T));
 
-    if (tid < T) {
-        const int r = tile * T + tid;
-        int32_t flag = 2, bs = 0, lay = -1, P0 = 0, npos = 0, kend = k0;
+    // ---- per-row metadata, one thread per row (searches of all rows in flight together)
+    if (tid < kRows) {
+        const int r = row0 + tid;
+        RowMeta m;
+        m.flag = 2; m.bs = 0; m.lay = -1; m.P0 = 0; m.npos = 0; m.kend = k0; m.heavy = -1; m.fast = 0;
+        m.off = m.slo = m.shi = m.rev = m.gps = m.gpe = 0;
+        for (int s = 0; s < 3; ++s) m.lo[s] = m.hi[s] = 0;
         if (r < P.n_rows) {
             int32_t head, L;
             rcp_part_slice(part, P.row_len[r], &head, &L);
             const int32_t n = CSR ? L : part.n_bins;
-            kend = min(k0 + part.chunk_bins, n);
+            m.kend = min(k0 + part.chunk_bins, n);
             if (!P.valid[r]) {
-                flag = CSR ? 2 : 1;  // NULL row -> zeros (profile.R:191-197)
+                m.flag = CSR ? 2 : 1;  // NULL row -> zeros (profile.R:191-197)
             } else if (k0 >= n) {
-                flag = 2;
+                m.flag = 2;
             } else if (!part.per_base && L < n) {
-                flag = 2;  // interpolation rows: rcp_interp_kernel
+                m.flag = 2;  // interpolation rows: rcp_interp_kernel
             } else if (part.per_base && !CSR && L != n) {
                 atomicOr(P.status, RCP_STATUS_WIDTH);
-                flag = 1;
+                m.flag = 1;
             } else {
                 if (part.per_base) {
-                    bs = 1;
+                    m.bs = 1;
                 } else {
-                    bs = L / n;
-                    const int32_t dif = L - bs * n;
+                    m.bs = L / n;
+                    const int32_t dif = L - m.bs * n;
                     if (dif) {
-                        lay = P.lay_index[part.lay_base + dif];
-                        if (lay < 0) {
+                        m.lay = P.lay_index[part.lay_base + dif];
+                        if (m.lay < 0) {
                             atomicOr(P.status, RCP_STATUS_INTERP);
-                            lay = -1;
+                            m.lay = -1;
                         }
                     }
                 }
-                const int32_t e0 = bin_edge(bs, lay, P.lay_cnt, k0);
-                const int32_t e1 = bin_edge(bs, lay, P.lay_cnt, kend);
-                P0 = head + e0;
-                npos = e1 - e0;
-                flag = 0;
-                if (npos > P.chunk_cap) {
+                const int32_t e0 = bin_edge(m.bs, m.lay, P.lay_cnt, k0);
+                const int32_t e1 = bin_edge(m.bs, m.lay, P.lay_cnt, m.kend);
+                m.P0 = head + e0;
+                m.npos = e1 - e0;
+                m.flag = 0;
+                if (m.npos > P.chunk_cap) {
                     atomicOr(P.status, RCP_STATUS_INTERP);
-                    flag = 1;
+                    m.flag = 1;
+                }
+                m.heavy = P.heavy_slot[r];
+                const int j0 = P.row_seg[r];
+                if (m.heavy < 0 && P.row_seg[r + 1] == j0 + 1) {
+                    const RcpSeg sg = P.segs[j0];
+                    if (!sg.multi && sg.query_ok) {
+                        const int32_t len = sg.hi - sg.lo + 1;
+                        const int32_t a = max(m.P0, sg.off);
+                        const int32_t b = min(m.P0 + m.npos, sg.off + len);
+                        m.fast = 1;
+                        m.off = sg.off; m.slo = sg.lo; m.shi = sg.hi; m.rev = sg.rev;
+                        if (a < b) {
+                            if (!sg.rev) {
+                                m.gps = sg.lo + (a - sg.off);
+                                m.gpe = sg.lo + (b - 1 - sg.off);
+                            } else {
+                                m.gpe = sg.hi - (a - sg.off);
+                                m.gps = sg.hi - (b - 1 - sg.off);
+                            }
+                            const bool full = (a == sg.off) && (b == sg.off + len);
+                            for (int s = 0; s < 3; ++s) {
+                                uint32_t lo = P.seg_lo[j0 * 3 + s], hi = P.seg_hi[j0 * 3 + s];
+                                if (lo < hi && !full) {
+                                    lo = lower_bound_pmax(P.pmax, lo, hi, m.gps);
+                                    hi = upper_bound_start(P.se, lo, hi, m.gpe);
+                                }
+                                m.lo[s] = lo;
+                                m.hi[s] = lo < hi ? hi : lo;
+                            }
+                        }
+                    }
                 }
             }
         }
-        m_bs[tid] = bs;
-        m_lay[tid] = lay;
-        m_P0[tid] = P0;
-        m_npos[tid] = npos;
-        m_kend[tid] = kend;
-        m_flag[tid] = flag;
+        meta[tid] = m;
     }
     __syncthreads();
 
-    for (int i = 0; i < T; ++i) {
-        if (m_flag[i] != 0) continue;  // uniform: read from LDS
-        const int r = tile * T + i;
-        const int32_t P0 = m_P0[i];
-        const int32_t npos = m_npos[i];
-        const int per = (((npos + 1 + kBlock - 1) / kBlock) + 3) & ~3;
-        for (int q = tid; q < per * kBlock; q += kBlock) diff[q] = 0;
-        __syncthreads();
-        pileup_rows_segments(P, r, P0, npos, diff);
-        __syncthreads();
-        scan_chunk<!(MEDIAN || CSR)>(diff, per, scratch);
-        __syncthreads();
-        const int32_t bs = m_bs[i], lay = m_lay[i], kend = m_kend[i];
-        const int32_t e0 = bin_edge(bs, lay, P.lay_cnt, k0);
-        for (int32_t k = k0 + tid; k < kend; k += kBlock) {
-            if (CSR) {
-                P.csr_out[P.csr_off[r] + k] = diff[k - k0];
-                continue;
-            }
-            const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
-            const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
-            uint32_t num;
-            if (MEDIAN) {
-                const int32_t m = b - a;
-                int32_t vmin = INT32_MAX, vmax = INT32_MIN;
-                for (int32_t q = a; q < b; ++q) {
-                    vmin = min(vmin, diff[q]);
-                    vmax = max(vmax, diff[q]);
+    // ---- rows of this wave: round rd, sub s -> row rd*T + s*kWaves + wave
+    auto row_of = [&](int step) { return (step >> 1) * T + (step & 1) * kWaves + wave; };
+    int2 pre[4];
+    auto prefetch = [&](int i) {
+        const RowMeta& m = meta[i];
+        const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t q = lane + 64 * u;
+            pre[u] = n ? P.se[fast_index(m, q < n ? q : n - 1)] : make_int2(1, 0);
+        }
+    };
+    prefetch(row_of(0));
+    for (int step = 0; step < 2 * kRounds; ++step) {
+        const int i = row_of(step);
+        int2 cur[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = pre[u];
+        if (step + 1 < 2 * kRounds) prefetch(row_of(step + 1));  // next row's loads in flight now
+        const RowMeta& m = meta[i];
+        if (m.flag == 0) {  // wave-uniform (LDS broadcast)
+            const int r = row0 + i;
+            const int32_t npos = m.npos;
+            const int per = ((npos + 1 + 63) / 64 + 3) & ~3;
+            int4* d4 = reinterpret_cast<int4*>(diff);
+            for (int q = lane - 1; q < per * 16; q += 64) d4[q] = make_int4(0, 0, 0, 0);
+            lds_order();
+            if (m.heavy >= 0) {
+                // skewed row: its difference array was piled up by rcp_heavy_pileup_kernel
+                const int32_t* g = P.heavy_gdiff + (size_t)m.heavy * P.heavy_stride;
+                int32_t carry = 0;
+                for (int q = lane; q < m.P0; q += 64) carry += g[q];
+                carry = wave_sum(carry);
+                for (int q = lane; q <= npos; q += 64) diff[q] = g[m.P0 + q] + (q == 0 ? carry : 0);
+            } else if (m.fast) {
+                const uint32_t n = fast_candidates(m);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (lane + 64u * u < n) add_read_fast(m, cur[u], diff);
+                for (uint32_t q0 = 256; q0 < n; q0 += 256) {
+                    int2 rd[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t q = q0 + lane + 64 * u;
+                        rd[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (q0 + lane + 64u * u < n) add_read_fast(m, rd[u], diff);
                 }
-                const int32_t h = (m + 1) >> 1;
-                const uint32_t x1 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h, vmin, vmax);
-                uint32_t x2 = x1;
-                if (!(m & 1)) x2 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h + 1, vmin, vmax);
-                num = x1 + x2;  // 2 x median
             } else {
-                const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
-                num = cum[b - 1] - (a > 0 ? cum[a - 1] : 0u);
+                pileup_row(P, r, m.P0, npos, diff, lane, 64);
             }
-            stage[(k - k0) * T + i] = num;
+            lds_order();
+            scan_wave<!(MEDIAN || CSR)>(diff, per);
+            lds_order();
+            const int32_t bs = m.bs, lay = m.lay, kend = m.kend;
+            const int ii = i & (T - 1);
+            if (CSR) {
+                for (int32_t k = k0 + lane; k < kend; k += 64) P.csr_out[P.csr_off[r] + k] = diff[k - k0];
+            } else if (MEDIAN) {
+                const int32_t e0 = bin_edge(bs, lay, P.lay_cnt, k0);
+                for (int32_t k = k0 + lane; k < kend; k += 64) {
+                    const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
+                    const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
+                    const int32_t mm = b - a;
+                    int32_t vmin = INT32_MAX, vmax = INT32_MIN;
+                    for (int32_t q = a; q < b; ++q) {
+                        vmin = min(vmin, diff[q]);
+                        vmax = max(vmax, diff[q]);
+                    }
+                    const int32_t h = (mm + 1) >> 1;
+                    const uint32_t x1 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h, vmin, vmax);
+                    uint32_t x2 = x1;
+                    if (!(mm & 1)) x2 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h + 1, vmin, vmax);
+                    stage[(k - k0) * T + ii] = x1 + x2;  // 2 x median
+                }
+            } else if (lay < 0) {
+                // uniform bins: bin k spans cum positions [a, a + bs), cum[-1] == 0
+                const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
+                int32_t a = lane * bs;
+                uint32_t* st = stage + lane * T + ii;
+                for (int32_t k = k0 + lane; k < kend; k += 64, a += 64 * bs, st += 64 * T) *st = cum[a + bs - 1] - cum[a - 1];
+            } else {
+                // splitVector layout: enlarged bins from set.seed(42); sample(1:n, dif)
+                const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
+                const int32_t* cnt = P.lay_cnt + lay;
+                const int32_t e0 = bs * k0 + cnt[k0];
+                for (int32_t k = k0 + lane; k < kend; k += 64) {
+                    const int32_t a = bs * k + cnt[k] - e0;
+                    const int32_t b = bs * (k + 1) + cnt[k + 1] - e0;
+                    stage[(k - k0) * T + ii] = cum[b - 1] - cum[a - 1];
+                }
+            }
+            lds_order();
+        }
+        if (CSR || !(step & 1)) continue;
+        __syncthreads();
+        // ---- round epilogue: stage[bin][row] -> out[col * n_rows + row].  Thread t always
+        // serves row t % 8 (256 is a multiple of 8), so 8 consecutive lanes write 8
+        // consecutive rows (64 B) of one column.
+        {
+            const int rbase = (step >> 1) * T;
+            const int ii = tid & (T - 1);
+            const int r = row0 + rbase + ii;
+            const RowMeta& mr = meta[rbase + ii];
+            const int32_t flag = mr.flag, kend = mr.kend, bs = mr.bs, lay = mr.lay;
+            if (r < P.n_rows && flag != 2) {
+                const size_t R = (size_t)P.n_rows;
+                const int kstep = kBlock / T;
+                int32_t k = k0 + (tid >> 3);
+                size_t o = (size_t)(part.col_off + k) * R + (size_t)r;
+                const size_t ostep = (size_t)kstep * R;
+                const uint32_t* st = stage + (tid >> 3) * T + ii;
+                if (flag == 1) {
+                    for (; k < kend; k += kstep, o += ostep) {
+                        out[o] = 0.0;
+                        if (binsum) binsum[o] = 0;
+                    }
+                } else if (MEDIAN || lay < 0) {
+                    // one divisor for the whole row; a power of two divides exactly by its reciprocal
+                    const int32_t den = MEDIAN ? 2 : bs;
+                    const double dd = (double)den;
+                    const double rd = 1.0 / dd;
+                    const bool pow2 = (den & (den - 1)) == 0;
+                    const double sc = P.scale;
+                    for (; k < kend; k += kstep, o += ostep, st += kstep * T) {
+                        const uint32_t num = *st;
+                        const double x = (double)num * sc;
+                        out[o] = pow2 ? x * rd : x / dd;
+                        if (binsum) binsum[o] = (int64_t)num;
+                    }
+                } else {
+                    const int32_t* cnt = P.lay_cnt + lay;
+                    for (; k < kend; k += kstep, o += ostep, st += kstep * T) {
+                        const uint32_t num = *st;
+                        const double den = (double)(bs + cnt[k + 1] - cnt[k]);
+                        out[o] = ((double)num * P.scale) / den;
+                        if (binsum) binsum[o] = (int64_t)num;
+                    }
+                }
+            }
         }
         __syncthreads();
-    }
-    if (CSR) return;
-
-    // ---- epilogue: stage[bin][row] -> out[(col) * n_rows + row], 16 rows contiguous
-    const int nk = part.chunk_bins;
-    for (int idx = tid; idx < nk * T; idx += kBlock) {
-        const int kk = idx / T;
-        const int i = idx - kk * T;
-        const int r = tile * T + i;
-        const int32_t flag = m_flag[i];
-        const int32_t k = k0 + kk;
-        if (r >= P.n_rows || flag == 2 || k >= m_kend[i]) continue;
-        const size_t o = (size_t)(part.col_off + k) * (size_t)P.n_rows + (size_t)r;
-        if (flag == 1) {
-            out[o] = 0.0;
-            if (binsum) binsum[o] = 0;
-            continue;
-        }
-        const uint32_t num = stage[kk * T + i];
-        double den;
-        if (MEDIAN) {
-            den = 2.0;
-        } else {
-            const int32_t lay = m_lay[i];
-            den = (double)(m_bs[i] + (lay >= 0 ? P.lay_cnt[lay + k + 1] - P.lay_cnt[lay + k] : 0));
-        }
-        out[o] = ((double)num * P.scale) / den;
-        if (binsum) binsum[o] = (int64_t)num;
     }
 }
+
 
 // =================================================================================
 // interpolation rows (length(x) < n): spline "fmm", neighborhood, "inear" no-op
@@ -458,8 +758,8 @@ namespace {
 
 #pragma clang fp contract(off)
 __device__ void fmm_spline_dev(int n, const double* y, double* b, double* c, double* d) {
-    // stats::spline method "fmm" coefficients on x = 1..n (R splines.c fmm_spline),
-    // with 1-based indexing kept for readability.
+    // stats::spline method "fmm" coefficients on knots x = 1..n (R splines.c fmm_spline),
+    // 1-based indexing kept as in the original; knot spacings are all 1.
     const double* Y = y - 1;
     double *B = b - 1, *Cc = c - 1, *D = d - 1;
     if (n < 2) {
@@ -488,8 +788,8 @@ __device__ void fmm_spline_dev(int n, const double* y, double* b, double* c, dou
     if (n > 3) {
         Cc[1] = Cc[3] / 2.0 - Cc[2] / 2.0;          // x[4]-x[2], x[3]-x[1]
         Cc[n] = Cc[nm1] / 2.0 - Cc[n - 2] / 2.0;    // x[n]-x[n-2], x[n-1]-x[n-3]
-        Cc[1] = Cc[1] * D[1] * D[1] / 3.0;           // x[4]-x[1]
-        Cc[n] = -Cc[n] * D[nm1] * D[nm1] / 3.0;      // x[n]-x[n-3]
+        Cc[1] = Cc[1] * D[1] * D[1] / 3.0;          // x[4]-x[1]
+        Cc[n] = -Cc[n] * D[nm1] * D[nm1] / 3.0;     // x[n]-x[n-3]
     }
     for (int i = 2; i <= n; i++) {
         const double t = D[i - 1] / B[i - 1];
@@ -539,7 +839,7 @@ __device__ double spline_eval_dev(int n, const double* y, const double* b, const
 __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* diff = reinterpret_cast<int32_t*>(smem);
-    const int diff_words = (P.chunk_cap + 8 + 1023) & ~1023;
+    const int diff_words = (P.interp_cap + 8 + 1023) & ~1023;
     uint32_t* scratch = reinterpret_cast<uint32_t*>(smem) + diff_words;
     const int e = blockIdx.x;
     const int r = P.interp_row[e];
@@ -552,16 +852,28 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
     }
     int32_t head, L;
     rcp_part_slice(part, P.row_len[r], &head, &L);
-    if (L > P.chunk_cap) {
+    if (L > P.interp_cap) {
         if (threadIdx.x == 0) atomicOr(P.status, RCP_STATUS_INTERP);
         return;
     }
-    const int per = (((L + 1 + kBlock - 1) / kBlock) + 3) & ~3;
+    const int per = (L + 1 + kBlock - 1) / kBlock;
     for (int q = threadIdx.x; q < per * kBlock; q += kBlock) diff[q] = 0;
     __syncthreads();
-    pileup_rows_segments(P, r, head, L, diff);
+    const int32_t slot = P.heavy_slot[r];
+    if (slot >= 0) {
+        const int32_t* g = P.heavy_gdiff + (size_t)slot * P.heavy_stride;
+        if (threadIdx.x == 0) {
+            int32_t carry = 0;
+            for (int q = 0; q < head; ++q) carry += g[q];
+            diff[0] = carry;
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q <= L; q += kBlock) diff[q] += g[head + q];
+    } else {
+        pileup_row(P, r, head, L, diff, threadIdx.x, kBlock);
+    }
     __syncthreads();
-    scan_chunk<false>(diff, per, scratch);
+    scan_block_depth(diff, per, scratch);
     __syncthreads();
     if (threadIdx.x != 0) return;
     double* x = P.interp_scratch + (size_t)e * P.interp_stride;
@@ -611,6 +923,14 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
 // =================================================================================
 // host-callable launchers
 // =================================================================================
+namespace {
+template <class K>
+hipError_t allow_big_lds(K kernel) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024);
+}
+}  // namespace
+
 extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream) {
     if (P->n_rows == 0) return hipSuccess;
     const int grid = (P->n_rows + kBlock - 1) / kBlock;
@@ -618,55 +938,75 @@ extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream)
     return hipGetLastError();
 }
 
-template <int T, bool MEDIAN, bool CSR>
-static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* binsum, size_t lds, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rcp_pileup_kernel<T, MEDIAN, CSR>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+extern "C" hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_t stream) {
+    if (P->n_rows == 0 || P->heavy_threshold <= 0) return hipSuccess;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = allow_big_lds(rcp_heavy_pileup_kernel);
         if (e != hipSuccess) return e;
-        attr_set = true;
+        attr = true;
     }
-    const int tiles = (P->n_rows + T - 1) / T;
-    const int64_t grid = (int64_t)tiles * P->n_chunks_total;
-    hipLaunchKernelGGL((rcp_pileup_kernel<T, MEDIAN, CSR>), dim3((unsigned)grid), dim3(kBlock), lds, s, *P, out,
-                       binsum);
+    hipLaunchKernelGGL(rcp_heavy_plan_kernel, dim3(1), dim3(kBlock), 0, stream, *P);
+    const size_t lds = 4 * ((size_t)P->heavy_max_len + 1 + 64);
+    hipLaunchKernelGGL(rcp_heavy_pileup_kernel, dim3(grid), dim3(kBlock), lds, stream, *P);
     return hipGetLastError();
 }
 
-extern "C" size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int tile_rows, int csr) {
-    const size_t diff_words = (size_t)((P->chunk_cap + 8 + 1023) & ~1023);
-    const size_t stage_words = csr ? 0 : (size_t)P->stage_cap * tile_rows;
-    return 4 * (diff_words + stage_words + 6 * (size_t)tile_rows + 2 * kWaves + 8);
+extern "C" hipError_t rcp_launch_heavy_clear(const RcpPlanDev* P, hipStream_t stream) {
+    if (P->n_rows == 0 || P->heavy_threshold <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rcp_heavy_clear_kernel, dim3(256), dim3(kBlock), 0, stream, *P);
+    return hipGetLastError();
+}
+
+extern "C" size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr) {
+    const size_t stage_words = csr ? 0 : (size_t)P->stage_cap * kTile;
+    return 4 * ((size_t)kWaves * (P->wave_words + 4) + stage_words + (size_t)kRows * kMetaWords + 8);
+}
+
+extern "C" int rcp_tile_rows(void) { return kRows; }
+
+template <bool MEDIAN, bool CSR>
+static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* binsum, size_t lds, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = allow_big_lds(rcp_pileup_kernel<MEDIAN, CSR>);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int tiles = (P->n_rows + kRows - 1) / kRows;
+    const int64_t grid = (int64_t)tiles * P->n_chunks_total;
+    hipLaunchKernelGGL((rcp_pileup_kernel<MEDIAN, CSR>), dim3((unsigned)grid), dim3(kBlock), lds, s, *P, out, binsum);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_t* binsum, int csr,
                                         hipStream_t stream) {
     if (P->n_rows == 0) return hipSuccess;
-    constexpr int T = 16;
-    const size_t lds = rcp_pileup_lds_bytes(P, T, csr);
-    if (csr) return launch_pileup_t<T, false, true>(P, out, binsum, lds, stream);
-    if (P->stat == 1) return launch_pileup_t<T, true, false>(P, out, binsum, lds, stream);
-    return launch_pileup_t<T, false, false>(P, out, binsum, lds, stream);
+    const size_t lds = rcp_pileup_lds_bytes(P, csr);
+    if (csr) return launch_pileup_t<false, true>(P, out, binsum, lds, stream);
+    if (P->stat == 1) return launch_pileup_t<true, false>(P, out, binsum, lds, stream);
+    return launch_pileup_t<false, false>(P, out, binsum, lds, stream);
+}
+
+extern "C" size_t rcp_interp_lds_bytes(const RcpPlanDev* P) {
+    return 4 * ((size_t)((P->interp_cap + 8 + 1023) & ~1023) + 2 * kWaves + 8);
 }
 
 extern "C" hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStream_t stream) {
     if (P->n_interp == 0) return hipSuccess;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rcp_interp_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipError_t e = allow_big_lds(rcp_interp_kernel);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    const size_t lds = 4 * ((size_t)((P->chunk_cap + 8 + 1023) & ~1023) + 2 * kWaves + 8);
-    hipLaunchKernelGGL(rcp_interp_kernel, dim3(P->n_interp), dim3(kBlock), lds, stream, *P, out);
+    hipLaunchKernelGGL(rcp_interp_kernel, dim3(P->n_interp), dim3(kBlock), rcp_interp_lds_bytes(P), stream, *P, out);
     return hipGetLastError();
 }
 
 extern "C" hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
-                                         const int8_t* strand, int32_t n_chrom, int32_t strand_filter,
-                                         uint64_t* keys, int32_t* vals, hipStream_t stream) {
+                                         const int8_t* strand, int32_t n_chrom, int32_t strand_filter, uint64_t* keys,
+                                         int32_t* vals, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const int64_t grid = (n + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(rcp_make_keys_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, chrom, start, end,

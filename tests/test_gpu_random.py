@@ -1,0 +1,263 @@
+"""Randomised GPU-vs-oracle parity over the reference's edge cases.
+
+Each case builds seeded reads and rows, runs the HIP path through the C ABI and compares
+with the CPU oracle: row validity (the reference's NULL rows) and integer numerators
+bit-exact, means within 1e-12 relative, interpolated / median values within 1e-9
+(north_star's bar for means is 1e-6)."""
+import os
+
+import numpy as np
+import pytest
+
+from tests import oracle_rows
+
+pytestmark = pytest.mark.gpu
+
+CHROM_LEN = np.array([400_000, 250_000, 90_000], dtype=np.int64)
+
+
+def make_reads(rng, n, widths=(20, 400), chroms=3, star_frac=0.0):
+    chrom = rng.integers(0, chroms, n).astype(np.int32)
+    start = np.empty(n, dtype=np.int64)
+    for c in range(chroms):
+        m = chrom == c
+        # clustered + uniform starts (hot spots exercise deep pileups)
+        k = int(m.sum())
+        centers = rng.integers(1000, CHROM_LEN[c] - 1000, 20)
+        hot = rng.random(k) < 0.4
+        s = rng.integers(1, CHROM_LEN[c] - widths[1], k)
+        s[hot] = centers[rng.integers(0, 20, hot.sum())] + rng.integers(-600, 600, hot.sum())
+        start[m] = np.clip(s, 1, CHROM_LEN[c] - widths[1])
+    width = rng.integers(widths[0], widths[1] + 1, n)
+    end = start + width - 1
+    strand = rng.integers(0, 2, n).astype(np.int8)
+    if star_frac:
+        strand[rng.random(n) < star_frac] = 2
+    return chrom, start.astype(np.int32), end.astype(np.int32), strand
+
+
+def single_rows(rng, R, width, chroms=3, strands=(0, 1, 2), edge=False):
+    from recoup_amd.engine import RowTable
+    chrom = rng.integers(0, chroms, R).astype(np.int32)
+    s = np.array([rng.integers(1, CHROM_LEN[c] - width) for c in chrom], dtype=np.int64)
+    if edge:
+        s[:3] = [-50, 0, 1]                       # negative index -> NULL; 0 -> dropped index
+        s[3] = CHROM_LEN[chrom[3]] - width // 2     # runs past the chromosome -> NULL
+    e = s + width - 1
+    st = rng.choice(np.array(strands, dtype=np.int8), R)
+    return RowTable.from_ranges(chrom, s, e, st)
+
+
+def run_case(reads, seqlen, rows, bins, strand_filter=None, binsum=False):
+    from recoup_amd.engine import Plan, ReadSet
+    rs = ReadSet(*reads, seqlen, device=0, strand_filter=strand_filter)
+    plan = Plan(rs, rows, bins)
+    res = plan.run(binsum=binsum)
+    ix = oracle_rows.index_for(reads, seqlen, strand_filter)
+    cov = oracle_rows.row_coverage(ix, rows)
+    exp, ev = oracle_rows.profile(cov, bins)
+    return res, (exp, ev, cov)
+
+
+def check(res, expected, rtol=1e-12, atol=0.0):
+    mat, valid = res[0], res[1]
+    exp, ev = expected[0], expected[1]
+    np.testing.assert_array_equal(valid, ev)
+    assert mat.shape == exp.shape
+    np.testing.assert_allclose(mat, exp, rtol=rtol, atol=atol)
+
+
+@pytest.mark.parametrize("n_bins", [1, 7, 64, 150, 1000])
+def test_single_range_bins(gpu, n_bins):
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(100 + n_bins)
+    reads = make_reads(rng, 60_000, star_frac=0.1)
+    rows = single_rows(rng, 300, 2000)
+    res, exp = run_case(reads, CHROM_LEN, rows, Bins([("whole", n_bins)]), binsum=True)
+    check(res, exp)
+    # bin numerators are integer sums: exact
+    cov = exp[2]
+    from oracle import oracle as o
+    for r in range(0, 300, 37):
+        if cov[r] is None:
+            continue
+        ref = o.split_vector(cov[r].astype(float), n_bins, stat="mean")
+        sizes = _layout_sizes(2000, n_bins)
+        np.testing.assert_array_equal(res[2][r], np.rint(ref * sizes).astype(np.int64))
+
+
+def _layout_sizes(L, n):
+    from oracle import oracle as o
+    bs, dif = divmod(L, n)
+    sizes = np.full(n, bs)
+    if dif:
+        o.set_seed(42)
+        sizes[o.sample_int(n, dif) - 1] += 1
+    return sizes
+
+
+def test_per_base_and_edges(gpu):
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(7)
+    reads = make_reads(rng, 80_000)
+    rows = single_rows(rng, 200, 3000, edge=True)
+    # row 1 starts at 0 -> one position shorter: not valid as a per-base row of 3000; use bins
+    res, exp = run_case(reads, CHROM_LEN, rows, Bins([("whole", 100)]))
+    check(res, exp)
+    assert not res[1][0] and not res[1][3]  # negative index, past the chromosome
+
+
+def test_na_seqlengths(gpu):
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(11)
+    reads = make_reads(rng, 40_000)
+    rows = single_rows(rng, 300, 1500)
+    seqlen = np.array([-1, -1, -1], dtype=np.int64)  # Rle spans only to the hits' max end
+    res, exp = run_case(reads, seqlen, rows, Bins([("whole", 30)]))
+    check(res, exp)
+
+
+@pytest.mark.parametrize("strand_filter", [None, "+", "-"])
+def test_stranded(gpu, strand_filter):
+    from recoup_amd.engine import Bins, RowTable
+    rng = np.random.default_rng(21)
+    reads = make_reads(rng, 50_000, star_frac=0.2)
+    r0 = single_rows(rng, 250, 1200)
+    rows = RowTable(r0.seg_off, r0.chrom, r0.start, r0.end, r0.strand, ignore_strand=False)
+    res, exp = run_case(reads, CHROM_LEN, rows, Bins([("whole", 40)]), strand_filter=strand_filter)
+    check(res, exp)
+
+
+def test_rna_multi_exon(gpu):
+    """coverageRnaRef rows: flank | exon list (reads counted once per exon hit) | flank."""
+    from recoup_amd.engine import Bins, RowTable
+    rng = np.random.default_rng(5)
+    reads = make_reads(rng, 120_000, widths=(50, 600))
+    seg_off, ch, st, en, sd, gr = [0], [], [], [], [], []
+    for g in range(120):
+        c = int(rng.integers(0, 3))
+        pos = int(rng.integers(5000, CHROM_LEN[c] - 60000))
+        strand = int(rng.integers(0, 2))
+        ne = int(rng.integers(1, 9))
+        ex_s, ex_e, p = [], [], pos
+        for _ in range(ne):
+            w = int(rng.integers(30, 600))
+            ex_s.append(p)
+            ex_e.append(p + w - 1)
+            p += w + int(rng.integers(-100, 3000))  # some overlapping exons
+        gs, ge = min(ex_s), max(ex_e)
+        f1, f2 = 2000, 2000
+        ls, le = (gs - f1, gs - 1) if strand == 0 else (ge + 1, ge + f1)
+        rs_, re_ = (ge + 1, ge + f2) if strand == 0 else (gs - f2, gs - 1)
+        for s, e, grp in [(ls, le, 0)] + [(a, b, 1) for a, b in zip(ex_s, ex_e)] + [(rs_, re_, 2)]:
+            ch.append(c); st.append(s); en.append(e); sd.append(strand); gr.append(grp)
+        seg_off.append(len(st))
+    rows = RowTable(np.array(seg_off), np.array(ch), np.array(st), np.array(en), np.array(sd),
+                    seg_group=np.array(gr), group_is_list=np.array([0, 1, 0, 0]))
+    for stat in ("mean", "median"):
+        bins = Bins([("upstream", 50), ("center", 100), ("downstream", 50)], flank=(2000, 2000), stat=stat)
+        res, exp = run_case(reads, CHROM_LEN, rows, bins)
+        check(res, exp, rtol=1e-9, atol=1e-12)
+
+
+def test_genebody_unequal_interp(gpu):
+    """Unequal rows: binned flanks, center bins with RNG layouts, spline / neighborhood rows."""
+    from recoup_amd.engine import Bins, RowTable
+    rng = np.random.default_rng(9)
+    reads = make_reads(rng, 100_000)
+    R = 220
+    chrom = rng.integers(0, 3, R).astype(np.int32)
+    width = np.concatenate([rng.integers(20, 140, 40), rng.integers(140, 40_000, R - 40)])
+    s = np.array([rng.integers(3000, CHROM_LEN[c] - 45000) for c in chrom])
+    strand = rng.integers(0, 2, R).astype(np.int8)
+    f1, f2 = 1000, 1500
+    gs = np.where(strand == 0, s - f1, s - f2)
+    ge = np.where(strand == 0, s + width - 1 + f2, s + width - 1 + f1)
+    rows = RowTable.from_ranges(chrom, gs, ge, strand)
+    for interp in ("auto", "spline", "neighborhood", "linear"):
+        bins = Bins([("upstream", 20), ("center", 150), ("downstream", 30)], flank=(f1, f2), interp=interp)
+        if interp == "neighborhood":
+            # R errors for tiny slices; keep the rows where R's neighborhood is defined
+            keep = width >= 60
+            rows_k = RowTable.from_ranges(chrom[keep], gs[keep], ge[keep], strand[keep])
+            res, exp = run_case(reads, CHROM_LEN, rows_k, bins)
+        else:
+            res, exp = run_case(reads, CHROM_LEN, rows, bins)
+        check(res, exp, rtol=1e-9, atol=1e-12)
+    # per-base flanks (flankBinSize = 0) with a binned center
+    bins = Bins([("upstream", 0, f1), ("center", 100), ("downstream", 0, f2)], flank=(f1, f2))
+    res, exp = run_case(reads, CHROM_LEN, rows, bins)
+    check(res, exp, rtol=1e-9, atol=1e-12)
+
+
+def test_long_rows_chunked(gpu):
+    """Rows longer than one chunk: per-base (chunked columns) and coarse bins."""
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(13)
+    reads = make_reads(rng, 150_000)
+    rows = single_rows(rng, 40, 20_000)
+    res, exp = run_case(reads, CHROM_LEN, rows, Bins([("whole", 0, 20_000)]))
+    check(res, exp)
+    res, exp = run_case(reads, CHROM_LEN, rows, Bins([("whole", 333)]))
+    check(res, exp)
+
+
+def test_heavy_rows_match(gpu):
+    """Skewed rows through the heavy split path give the same matrix as the oracle."""
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(17)
+    reads = make_reads(rng, 200_000, widths=(100, 200))
+    rows = single_rows(rng, 100, 2000)
+    os.environ["RCP_HEAVY_THRESHOLD"] = "16"
+    try:
+        res, exp = run_case(reads, CHROM_LEN, rows, Bins([("whole", 100)]))
+        res_m, exp_m = run_case(reads, CHROM_LEN, rows, Bins([("whole", 100)], stat="median"))
+    finally:
+        del os.environ["RCP_HEAVY_THRESHOLD"]
+    check(res, exp)
+    check(res_m, exp_m, rtol=1e-9, atol=1e-12)
+
+
+def test_calc_coverage_csr(gpu):
+    from recoup_amd.engine import Plan, ReadSet
+    rng = np.random.default_rng(3)
+    reads = make_reads(rng, 70_000)
+    rows = single_rows(rng, 150, 5000, edge=True)
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    got = Plan(rs, rows, None).coverage()
+    ix = oracle_rows.index_for(reads, CHROM_LEN)
+    exp = oracle_rows.row_coverage(ix, rows)
+    for g, e in zip(got, exp):
+        if e is None:
+            assert g is None
+        else:
+            np.testing.assert_array_equal(g, e)
+
+
+def test_rounding_sample_kind(gpu):
+    """RNGkind(sample.kind = "Rounding") (pre-3.6 R) bin layouts."""
+    from recoup_amd.engine import Bins
+    from oracle import oracle as o
+    rng = np.random.default_rng(23)
+    reads = make_reads(rng, 30_000)
+    rows = single_rows(rng, 100, 2000)
+    from recoup_amd.engine import Plan, ReadSet
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    mat, valid = Plan(rs, rows, Bins([("whole", 150)], rng_kind="Rounding")).run()
+    ix = oracle_rows.index_for(reads, CHROM_LEN)
+    cov = oracle_rows.row_coverage(ix, rows)
+    exp = o._bin_matrix(cov, 150, "mean", "auto", None, None, 1.0, "Rounding")
+    np.testing.assert_allclose(mat, exp, rtol=1e-12, atol=0)
+
+
+def test_empty_inputs(gpu):
+    from recoup_amd.engine import Bins, Plan, ReadSet, RowTable
+    rs = ReadSet(np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.int8),
+                 CHROM_LEN, device=0)
+    rows = single_rows(np.random.default_rng(1), 20, 1000)
+    mat, valid = Plan(rs, rows, Bins([("whole", 10)])).run()
+    assert not valid.any() and not mat.any()
+    empty = RowTable(np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.int32),
+                     np.zeros(0, np.int8))
+    mat, valid = Plan(rs, empty, Bins([("whole", 10)])).run()
+    assert mat.shape == (0, 10)

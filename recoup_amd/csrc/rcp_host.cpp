@@ -44,13 +44,25 @@ hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* 
 
 namespace {
 
-constexpr int kChunkMax = 16384;       // positions per chunk (one wave's LDS difference array)
+constexpr int kChunkMax = 16384;       // positions of an interpolated slice (block LDS array)
+constexpr int kWaveMax = 4096;         // positions per wave sub-chunk (padded LDS array <= 17 KB)
 constexpr int kStageMaxBins = 1024;    // bins per chunk (LDS stage = bins x 8 rows x 4 B)
 constexpr size_t kLdsBudget = 80 * 1024;  // keep two pileup workgroups per CU when possible
 constexpr int kHeavyThreshold = 8192;  // candidate reads above which a row is split across workgroups
 constexpr int kHeavySlice = 16384;     // candidate reads per heavy work item
 constexpr int kHeavyMaxLen = 16383;    // longer rows never take the heavy path
 constexpr int kHeavyGrid = 1024;
+
+// A wave's difference array: 64 lanes x per positions (per a power of two >= 4), each lane's
+// chunk padded by 4 words (rcp_kernels.hip scan_wave).  Returns the LDS words and the
+// position capacity for a chunk of `positions`.
+void wave_geometry(int32_t positions, int32_t* words, int32_t* capacity) {
+    int32_t need = (positions + 1 + 63) / 64;
+    int32_t per = 4;
+    while (per < need) per <<= 1;
+    *words = 64 * (per + 4);
+    *capacity = 64 * per - 1;
+}
 
 int env_int(const char* name, int def) {
     const char* v = getenv(name);
@@ -478,7 +490,10 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
                 }
                 const int32_t bs = L / pt.n_bins;
                 const int32_t dif = L - bs * pt.n_bins;
-                max_bin = std::max(max_bin, bs + (dif ? 1 : 0));
+                // median bins wider than a wave chunk go to the slow-row kernel (mode 4) and do
+                // not size the chunks of the others
+                if (bins->stat != RCP_STAT_MEDIAN || bs + (dif ? 1 : 0) < kWaveMax)
+                    max_bin = std::max(max_bin, bs + (dif ? 1 : 0));
                 if (dif) {
                     int32_t& slot = B.lay_index[pt.lay_base + dif];
                     if (slot < 0) {
@@ -497,58 +512,72 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
                 }
             }
         }
-        if (max_bin > kChunkMax)
-            return fail(RCP_EUNSUPPORTED, "part %d: a bin of %d positions exceeds the %d-position chunk", p, max_bin,
-                        kChunkMax);
         part_max_bin[p] = max_bin;
     }
     if (max_interp_len > kChunkMax)
         return fail(RCP_EUNSUPPORTED, "interpolated slice of %d positions exceeds %d", max_interp_len, kChunkMax);
 
-    // ---- geometry: the largest per-wave chunk (positions) whose LDS (4 wave difference
-    // arrays + the [bin][row] stage) keeps two workgroups per CU; else the smallest feasible.
+    // ---- geometry.  A workgroup handles <= kStageMaxBins bins of a part for 32 rows; a wave
+    // piles a row's positions for those bins in sub-chunks of at most `chunk_cap` positions
+    // (bins straddling sub-chunks accumulate).  Pick the largest wave chunk (<= kWaveMax) whose
+    // LDS (4 wave arrays + [bin][row] stage + row metadata) keeps two workgroups per CU.
     {
-        int32_t need = 1024;
-        for (int p = 0; p < P.n_parts; ++p) need = std::max(need, P.part[p].n_bins * part_max_bin[p]);
-        if (cov_only) need = std::max(need, plan->max_row_len);
-        need = std::min(need, kChunkMax);
-        const int32_t cands[] = {need, 8192, 4096, 2048, 1024, 512};
-        int32_t best = -1;
-        size_t best_lds = 0;
-        for (int32_t ch : cands) {
-            if (ch > need) continue;
-            int32_t stage = 1;
-            bool ok = true;
-            for (int p = 0; p < P.n_parts; ++p) {
-                if (part_max_bin[p] > ch) ok = false;
-                stage = std::max<int32_t>(stage, std::min<int32_t>(P.part[p].n_bins,
-                                                                   std::min<int32_t>(kStageMaxBins, ch / part_max_bin[p])));
-            }
-            if (!ok) break;  // smaller chunks cannot hold the largest bin either
-            RcpPlanDev t{};
-            t.wave_words = ((ch + 1) + 255) & ~255;
-            t.stage_cap = cov_only ? 0 : stage;
-            const size_t lds = rcp_pileup_lds_bytes(&t, cov_only ? 1 : 0);
-            best = ch;
-            best_lds = lds;
-            if (lds <= kLdsBudget) break;
-        }
-        if (best < 0) return fail(RCP_EUNSUPPORTED, "no chunk geometry fits the bins");
-        (void)best_lds;
-        chunk_cap = best;
+        const bool median = bins->stat == RCP_STAT_MEDIAN;
+        int32_t need = 64;
         for (int p = 0; p < P.n_parts; ++p) {
             RcpPart& pt = P.part[p];
-            pt.chunk_bins = std::min<int32_t>(pt.n_bins, std::min<int32_t>(kStageMaxBins, chunk_cap / part_max_bin[p]));
-            pt.n_chunks = (pt.n_bins + pt.chunk_bins - 1) / pt.chunk_bins;
-            stage_cap = std::max(stage_cap, pt.chunk_bins);
+            int32_t cb = std::min<int32_t>(pt.n_bins, kStageMaxBins);
+            if (median) cb = std::min<int32_t>(cb, std::max<int32_t>(1, kWaveMax / part_max_bin[p]));
+            pt.chunk_bins = cb;
+            pt.n_chunks = (pt.n_bins + cb - 1) / cb;
+            stage_cap = std::max(stage_cap, cb);
+            need = std::max<int64_t>(need, std::min<int64_t>((int64_t)cb * part_max_bin[p], kWaveMax));
         }
+        if (cov_only) need = std::max(need, std::min(plan->max_row_len, kWaveMax));
+        int32_t min_cap = 64;
+        if (median)
+            for (int p = 0; p < P.n_parts; ++p) min_cap = std::max(min_cap, P.part[p].chunk_bins * part_max_bin[p]);
+        const int32_t cands[] = {need, 2048, 1024};
+        chunk_cap = -1;
+        for (int32_t ch : cands) {
+            if (ch > need || ch < min_cap) continue;
+            RcpPlanDev t{};
+            int32_t cap_unused = 0;
+            wave_geometry(ch, &t.wave_words, &cap_unused);
+            t.stage_cap = cov_only ? 0 : stage_cap;
+            chunk_cap = ch;
+            if (rcp_pileup_lds_bytes(&t, cov_only ? 1 : 0) <= kLdsBudget) break;
+        }
+        if (chunk_cap < 0) chunk_cap = need;
     }
     P.n_cols = col;
     plan->n_cols = col;
-    P.wave_words = ((chunk_cap + 1) + 255) & ~255;
-    P.chunk_cap = P.wave_words - 1;
+    wave_geometry(chunk_cap, &P.wave_words, &P.chunk_cap);
     P.stage_cap = stage_cap;
     P.interp_cap = std::max(max_interp_len, 1);
+    if (bins->stat == RCP_STAT_MEDIAN) {
+        // rows whose median bins exceed the wave chunk: block-level windows (mode 4)
+        for (int p = 0; p < P.n_parts; ++p) {
+            const RcpPart& pt = P.part[p];
+            if (pt.per_base) continue;
+            for (int r = 0; r < R; ++r) {
+                if (B.row_static[r] || B.row_seg[r] == B.row_seg[r + 1]) continue;
+                int32_t head, L;
+                rcp_part_slice(pt, B.row_len[r], &head, &L);
+                if (L < pt.n_bins) continue;
+                const int32_t bs = L / pt.n_bins, dif = L - bs * pt.n_bins;
+                const int32_t w = bs + (dif ? 1 : 0);
+                if (w <= P.chunk_cap) continue;
+                if (w > kChunkMax)
+                    return fail(RCP_EUNSUPPORTED, "row %d: a median bin of %d positions exceeds %d", r, w, kChunkMax);
+                B.interp_row.push_back(r);
+                B.interp_part.push_back(p);
+                B.interp_mode.push_back(4);
+                B.interp_pos.push_back(dif ? B.lay_index[pt.lay_base + dif] : -1);
+                P.interp_cap = std::max(P.interp_cap, w);
+            }
+        }
+    }
     P.n_chunks_total = 0;
     for (int p = 0; p < P.n_parts; ++p) P.n_chunks_total += P.part[p].n_chunks;
 

@@ -93,8 +93,12 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
 // Add read `rd` of segment sg to the difference array of row positions [P0, P0 + npos)
 // restricted to the genomic piece [gps, gpe] of the segment.
 // ---------------------------------------------------------------------------------
+// LDS word of row position p in a wave array whose lanes own 2^sh positions each, padded
+// by 4 words per lane (bank-conflict-free b128 scans); sh = 30 leaves p unchanged.
+__device__ __forceinline__ int32_t lp(int32_t p, int sh) { return p + ((p >> sh) << 2); }
+
 __device__ __forceinline__ void add_read(const RcpPlanDev& P, const RcpSeg& sg, int2 rd, int32_t gps, int32_t gpe,
-                                         int32_t P0, int32_t* diff) {
+                                         int32_t P0, int32_t* diff, int sh) {
     if (rd.y < gps || rd.x > gpe) return;
     int32_t w = 1;
     if (sg.multi) {
@@ -116,15 +120,15 @@ __device__ __forceinline__ void add_read(const RcpPlanDev& P, const RcpSeg& sg, 
         o0 = sg.off + (sg.hi - x1);
         o1 = sg.off + (sg.hi - x0);
     }
-    atomicAdd(&diff[o0 - P0], w);
-    atomicAdd(&diff[o1 - P0 + 1], -w);
+    atomicAdd(&diff[lp(o0 - P0, sh)], w);
+    atomicAdd(&diff[lp(o1 - P0 + 1, sh)], -w);
 }
 
 // Pile the candidate reads of row r over row positions [P0, P0 + npos) into `diff`
 // (npos + 1 words, zeroed by the caller).  Threads `t` of `nt` (a wave or a block) split
 // the reads; each keeps 4 coalesced loads in flight.
 __device__ __forceinline__ void pileup_row(const RcpPlanDev& P, int r, int32_t P0, int32_t npos, int32_t* diff,
-                                           int t, int nt) {
+                                           int t, int nt, int sh) {
     const int32_t P1 = P0 + npos;
     const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
     for (int j = j0; j < j1; ++j) {
@@ -158,17 +162,18 @@ __device__ __forceinline__ void pileup_row(const RcpPlanDev& P, int r, int32_t P
                 for (int u = 0; u < 4; ++u) rd[u] = P.se[min(base + u * nt, hi - 1)];  // clamped: no branch
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (base + u * nt < hi) add_read(P, sg, rd[u], gps, gpe, P0, diff);
+                    if (base + u * nt < hi) add_read(P, sg, rd[u], gps, gpe, P0, diff, sh);
             }
         }
     }
 }
 
-// Wave scan of diff[0 .. 64*per): depth (CUM = false) or cumulative depth (CUM = true).
+// Wave scan of the 64*per positions of a padded wave array (lane l owns positions
+// [l*per, (l+1)*per) at words l*(per+4) ..): depth (CUM = false) or cumulative depth.
 template <bool CUM>
 __device__ __forceinline__ void scan_wave(int32_t* diff, int per) {
     const int lane = threadIdx.x & 63;
-    uint32_t* base = reinterpret_cast<uint32_t*>(diff) + lane * per;
+    uint32_t* base = reinterpret_cast<uint32_t*>(diff) + lane * (per + 4);
     uint32_t A = 0, B = 0;  // sum of diff, sum of the local depth prefix
     for (int q = 0; q < per; q += 4) {
         const uint4 v = *reinterpret_cast<const uint4*>(base + q);
@@ -211,12 +216,12 @@ __device__ __forceinline__ int32_t bin_edge(int32_t bs, int32_t lay, const int32
 
 // k-th smallest (1-based) of depth[a .. b) by bisection on the value (depth is >= 0).
 __device__ __forceinline__ uint32_t kth_smallest(const int32_t* d, int32_t a, int32_t b, int32_t k, int32_t vmin,
-                                                 int32_t vmax) {
+                                                 int32_t vmax, int sh) {
     int32_t lo = vmin, hi = vmax;
     while (lo < hi) {
         const int32_t mid = lo + ((hi - lo) >> 1);
         int32_t c = 0;
-        for (int32_t q = a; q < b; ++q) c += d[q] <= mid;
+        for (int32_t q = a; q < b; ++q) c += d[lp(q, sh)] <= mid;
         if (c >= k) hi = mid; else lo = mid + 1;
     }
     return (uint32_t)lo;
@@ -420,7 +425,7 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) 
             uint32_t idx;
             if (!nth_candidate(P, r, q, &j, &idx)) break;
             const RcpSeg sg = P.segs[j];
-            add_read(P, sg, P.se[idx], sg.lo, sg.hi, 0, diff);
+            add_read(P, sg, P.se[idx], sg.lo, sg.hi, 0, diff, 30);
         }
         __syncthreads();
         int32_t* g = P.heavy_gdiff + (size_t)slot * P.heavy_stride;
@@ -475,7 +480,7 @@ __device__ __forceinline__ uint32_t fast_index(const RowMeta& m, uint32_t q) {
     return q < c0 ? m.lo[0] + q : (q < c0 + c1 ? m.lo[1] + (q - c0) : m.lo[2] + (q - c0 - c1));
 }
 
-__device__ __forceinline__ void add_read_fast(const RowMeta& m, int2 rd, int32_t* diff) {
+__device__ __forceinline__ void add_read_fast(const RowMeta& m, int2 rd, int32_t* diff, int sh) {
     if (rd.y < m.gps || rd.x > m.gpe) return;
     const int32_t x0 = max(rd.x, m.gps);
     const int32_t x1 = min(rd.y, m.gpe);
@@ -487,8 +492,8 @@ __device__ __forceinline__ void add_read_fast(const RowMeta& m, int2 rd, int32_t
         o0 = m.off + (m.shi - x1);
         o1 = m.off + (m.shi - x0);
     }
-    atomicAdd(&diff[o0 - m.P0], 1);
-    atomicAdd(&diff[o1 - m.P0 + 1], -1);
+    atomicAdd(&diff[lp(o0 - m.P0, sh)], 1);
+    atomicAdd(&diff[lp(o1 - m.P0 + 1, sh)], -1);
 }
 
 __device__ __forceinline__ void lds_order() {
@@ -517,10 +522,12 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
     const int32_t k0 = c * part.chunk_bins;
     const int row0 = blk * kRows;
 
-    // per wave: 4 zero words (cum[-1] == 0) then the difference / depth / cumulative array
-    int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * (P.wave_words + 4) + 4;
-    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kWaves * (P.wave_words + 4);
-    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : P.stage_cap * T));
+    // per wave: 8 zero words (so cum[lp(-1)] == 0) then the padded difference / depth /
+    // cumulative array; the stage is [bin][T + 1] (odd row stride: conflict-free writes)
+    constexpr int TS = T + 1;
+    int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * (P.wave_words + 8) + 8;
+    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kWaves * (P.wave_words + 8);
+    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : P.stage_cap * TS));
 
     // ---- per-row metadata, one thread per row (searches of all rows in flight together)
     if (tid < kRows) {
@@ -562,13 +569,11 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
                 m.P0 = head + e0;
                 m.npos = e1 - e0;
                 m.flag = 0;
-                if (m.npos > P.chunk_cap) {
-                    atomicOr(P.status, RCP_STATUS_INTERP);
-                    m.flag = 1;
-                }
+                // median bins wider than a wave chunk: rcp_interp_kernel (mode 4)
+                if (MEDIAN && m.bs + (m.lay >= 0 ? 1 : 0) > P.chunk_cap) m.flag = 2;
                 m.heavy = P.heavy_slot[r];
                 const int j0 = P.row_seg[r];
-                if (m.heavy < 0 && P.row_seg[r + 1] == j0 + 1) {
+                if (m.heavy < 0 && m.npos <= P.chunk_cap && P.row_seg[r + 1] == j0 + 1) {
                     const RcpSeg sg = P.segs[j0];
                     if (!sg.multi && sg.query_ok) {
                         const int32_t len = sg.hi - sg.lo + 1;
@@ -626,78 +631,104 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
         if (m.flag == 0) {  // wave-uniform (LDS broadcast)
             const int r = row0 + i;
             const int32_t npos = m.npos;
-            const int per = ((npos + 1 + 63) / 64 + 3) & ~3;
-            int4* d4 = reinterpret_cast<int4*>(diff);
-            for (int q = lane - 1; q < per * 16; q += 64) d4[q] = make_int4(0, 0, 0, 0);
-            lds_order();
-            if (m.heavy >= 0) {
-                // skewed row: its difference array was piled up by rcp_heavy_pileup_kernel
-                const int32_t* g = P.heavy_gdiff + (size_t)m.heavy * P.heavy_stride;
-                int32_t carry = 0;
-                for (int q = lane; q < m.P0; q += 64) carry += g[q];
-                carry = wave_sum(carry);
-                for (int q = lane; q <= npos; q += 64) diff[q] = g[m.P0 + q] + (q == 0 ? carry : 0);
-            } else if (m.fast) {
-                const uint32_t n = fast_candidates(m);
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (lane + 64u * u < n) add_read_fast(m, cur[u], diff);
-                for (uint32_t q0 = 256; q0 < n; q0 += 256) {
-                    int2 rd[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint32_t q = q0 + lane + 64 * u;
-                        rd[u] = P.se[fast_index(m, q < n ? q : n - 1)];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (q0 + lane + 64u * u < n) add_read_fast(m, rd[u], diff);
-                }
-            } else {
-                pileup_row(P, r, m.P0, npos, diff, lane, 64);
-            }
-            lds_order();
-            scan_wave<!(MEDIAN || CSR)>(diff, per);
-            lds_order();
             const int32_t bs = m.bs, lay = m.lay, kend = m.kend;
             const int ii = i & (T - 1);
-            if (CSR) {
-                for (int32_t k = k0 + lane; k < kend; k += 64) P.csr_out[P.csr_off[r] + k] = diff[k - k0];
-            } else if (MEDIAN) {
-                const int32_t e0 = bin_edge(bs, lay, P.lay_cnt, k0);
-                for (int32_t k = k0 + lane; k < kend; k += 64) {
-                    const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
-                    const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
-                    const int32_t mm = b - a;
-                    int32_t vmin = INT32_MAX, vmax = INT32_MIN;
-                    for (int32_t q = a; q < b; ++q) {
-                        vmin = min(vmin, diff[q]);
-                        vmax = max(vmax, diff[q]);
+            const int32_t e0 = bin_edge(bs, lay, P.lay_cnt, k0);
+            // positions [P0, P0 + npos) in sub-chunks of at most chunk_cap positions; a bin
+            // that straddles sub-chunks accumulates its partial sums in the stage
+            for (int32_t s0 = 0; s0 < npos; s0 += P.chunk_cap) {
+                const int32_t sn = min(P.chunk_cap, npos - s0);
+                const bool whole = sn == npos;
+                if (MEDIAN && !whole) {  // the host keeps median bins inside one chunk
+                    if (lane == 0) atomicOr(P.status, RCP_STATUS_INTERP);
+                    break;
+                }
+                // per-lane positions: a power of two >= 4 (lane chunks padded by 4 words)
+                const int need = (sn + 1 + 63) >> 6;
+                const int sh = need <= 4 ? 2 : 32 - __clz(need - 1);
+                const int per = 1 << sh;
+                int4* d4 = reinterpret_cast<int4*>(diff);
+                for (int q = lane - 2; q < (per + 4) * 16; q += 64) d4[q] = make_int4(0, 0, 0, 0);
+                lds_order();
+                if (m.heavy >= 0) {
+                    // skewed row: its difference array was piled up by rcp_heavy_pileup_kernel
+                    const int32_t* g = P.heavy_gdiff + (size_t)m.heavy * P.heavy_stride;
+                    const int32_t base = m.P0 + s0;
+                    int32_t carry = 0;
+                    for (int q = lane; q < base; q += 64) carry += g[q];
+                    carry = wave_sum(carry);
+                    for (int q = lane; q <= sn; q += 64) diff[lp(q, sh)] = g[base + q] + (q == 0 ? carry : 0);
+                } else if (m.fast && whole) {
+                    const uint32_t n = fast_candidates(m);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (lane + 64u * u < n) add_read_fast(m, cur[u], diff, sh);
+                    for (uint32_t q0 = 256; q0 < n; q0 += 256) {
+                        int2 rd[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint32_t q = q0 + lane + 64 * u;
+                            rd[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (q0 + lane + 64u * u < n) add_read_fast(m, rd[u], diff, sh);
                     }
-                    const int32_t h = (mm + 1) >> 1;
-                    const uint32_t x1 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h, vmin, vmax);
-                    uint32_t x2 = x1;
-                    if (!(mm & 1)) x2 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h + 1, vmin, vmax);
-                    stage[(k - k0) * T + ii] = x1 + x2;  // 2 x median
+                } else {
+                    pileup_row(P, r, m.P0 + s0, sn, diff, lane, 64, sh);
                 }
-            } else if (lay < 0) {
-                // uniform bins: bin k spans cum positions [a, a + bs), cum[-1] == 0
-                const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
-                int32_t a = lane * bs;
-                uint32_t* st = stage + lane * T + ii;
-                for (int32_t k = k0 + lane; k < kend; k += 64, a += 64 * bs, st += 64 * T) *st = cum[a + bs - 1] - cum[a - 1];
-            } else {
-                // splitVector layout: enlarged bins from set.seed(42); sample(1:n, dif)
-                const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
-                const int32_t* cnt = P.lay_cnt + lay;
-                const int32_t e0 = bs * k0 + cnt[k0];
-                for (int32_t k = k0 + lane; k < kend; k += 64) {
-                    const int32_t a = bs * k + cnt[k] - e0;
-                    const int32_t b = bs * (k + 1) + cnt[k + 1] - e0;
-                    stage[(k - k0) * T + ii] = cum[b - 1] - cum[a - 1];
+                lds_order();
+                scan_wave<!(MEDIAN || CSR)>(diff, per);
+                lds_order();
+                if (CSR) {
+                    for (int32_t k = k0 + s0 + lane; k < k0 + s0 + sn; k += 64)
+                        P.csr_out[P.csr_off[r] + k] = diff[lp(k - k0 - s0, sh)];
+                } else if (MEDIAN) {
+                    for (int32_t k = k0 + lane; k < kend; k += 64) {
+                        const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
+                        const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
+                        const int32_t mm = b - a;
+                        int32_t vmin = INT32_MAX, vmax = INT32_MIN;
+                        for (int32_t q = a; q < b; ++q) {
+                            const int32_t v = diff[lp(q, sh)];
+                            vmin = min(vmin, v);
+                            vmax = max(vmax, v);
+                        }
+                        const int32_t h = (mm + 1) >> 1;
+                        const uint32_t x1 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h, vmin, vmax, sh);
+                        uint32_t x2 = x1;
+                        if (!(mm & 1))
+                            x2 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h + 1, vmin, vmax, sh);
+                        stage[(k - k0) * TS + ii] = x1 + x2;  // 2 x median
+                    }
+                } else if (whole && lay < 0) {
+                    // uniform bins: bin k spans cum positions [a, a + bs), cum[lp(-1)] == 0
+                    const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
+                    int32_t a = lane * bs;
+                    uint32_t* st = stage + lane * TS + ii;
+                    for (int32_t k = k0 + lane; k < kend; k += 64, a += 64 * bs, st += 64 * TS)
+                        *st = cum[lp(a + bs - 1, sh)] - cum[lp(a - 1, sh)];
+                } else if (whole) {
+                    // splitVector layout: enlarged bins from set.seed(42); sample(1:n, dif)
+                    const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
+                    for (int32_t k = k0 + lane; k < kend; k += 64) {
+                        const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
+                        const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
+                        stage[(k - k0) * TS + ii] = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
+                    }
+                } else {
+                    // sub-chunk [s0, s0 + sn): add each overlapping bin's partial sum
+                    const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
+                    for (int32_t k = k0 + lane; k < kend; k += 64) {
+                        const int32_t a = max(bin_edge(bs, lay, P.lay_cnt, k) - e0, s0) - s0;
+                        const int32_t b = min(bin_edge(bs, lay, P.lay_cnt, k + 1) - e0, s0 + sn) - s0;
+                        uint32_t* st = stage + (k - k0) * TS + ii;
+                        const uint32_t part_sum = a < b ? cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)] : 0u;
+                        *st = (s0 == 0 ? 0u : *st) + part_sum;
+                    }
                 }
+                lds_order();
             }
-            lds_order();
         }
         if (CSR || !(step & 1)) continue;
         __syncthreads();
@@ -716,7 +747,7 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
                 int32_t k = k0 + (tid >> 3);
                 size_t o = (size_t)(part.col_off + k) * R + (size_t)r;
                 const size_t ostep = (size_t)kstep * R;
-                const uint32_t* st = stage + (tid >> 3) * T + ii;
+                const uint32_t* st = stage + (tid >> 3) * TS + ii;
                 if (flag == 1) {
                     for (; k < kend; k += kstep, o += ostep) {
                         out[o] = 0.0;
@@ -729,7 +760,7 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
                     const double rd = 1.0 / dd;
                     const bool pow2 = (den & (den - 1)) == 0;
                     const double sc = P.scale;
-                    for (; k < kend; k += kstep, o += ostep, st += kstep * T) {
+                    for (; k < kend; k += kstep, o += ostep, st += kstep * TS) {
                         const uint32_t num = *st;
                         const double x = (double)num * sc;
                         out[o] = pow2 ? x * rd : x / dd;
@@ -737,7 +768,7 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
                     }
                 } else {
                     const int32_t* cnt = P.lay_cnt + lay;
-                    for (; k < kend; k += kstep, o += ostep, st += kstep * T) {
+                    for (; k < kend; k += kstep, o += ostep, st += kstep * TS) {
                         const uint32_t num = *st;
                         const double den = (double)(bs + cnt[k + 1] - cnt[k]);
                         out[o] = ((double)num * P.scale) / den;
@@ -836,11 +867,40 @@ __device__ double spline_eval_dev(int n, const double* y, const double* b, const
 
 }  // namespace
 
+// Block-level window: depth of row r over row positions [w0, w0 + wn) into diff[0 .. wn)
+// (reads piled by all 256 threads, or copied from a heavy row's global difference array).
+__device__ void block_window_depth(const RcpPlanDev& P, int r, int32_t w0, int32_t wn, int32_t* diff,
+                                   uint32_t* scratch) {
+    const int per = (wn + 1 + kBlock - 1) / kBlock;
+    for (int q = threadIdx.x; q < per * kBlock; q += kBlock) diff[q] = 0;
+    __syncthreads();
+    const int32_t slot = P.heavy_slot[r];
+    if (slot >= 0) {
+        const int32_t* g = P.heavy_gdiff + (size_t)slot * P.heavy_stride;
+        if (threadIdx.x == 0) {
+            int32_t carry = 0;
+            for (int q = 0; q < w0; ++q) carry += g[q];
+            diff[0] = carry;
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q <= wn; q += kBlock) diff[q] += g[w0 + q];
+    } else {
+        pileup_row(P, r, w0, wn, diff, threadIdx.x, kBlock, 30);
+    }
+    __syncthreads();
+    scan_block_depth(diff, per, scratch);
+    __syncthreads();
+}
+
+// Rows the pileup kernel leaves out: interpolation (length(x) < n bins, modes 1-3) and
+// median bins wider than a wave chunk (mode 4, bins taken in groups that fit the window).
 __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* diff = reinterpret_cast<int32_t*>(smem);
     const int diff_words = (P.interp_cap + 8 + 1023) & ~1023;
     uint32_t* scratch = reinterpret_cast<uint32_t*>(smem) + diff_words;
+    // (no static __shared__: the dynamic region may take all 160 KB)
+    int32_t& group_end = reinterpret_cast<int32_t*>(scratch)[2 * kWaves];
     const int e = blockIdx.x;
     const int r = P.interp_row[e];
     const RcpPart part = P.part[P.interp_part[e]];
@@ -852,33 +912,53 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
     }
     int32_t head, L;
     rcp_part_slice(part, P.row_len[r], &head, &L);
+    const int mode = P.interp_mode[e];
+    if (mode == 4) {  // median over bins wider than a wave chunk
+        const int32_t bs = L / n;
+        const int32_t lay = P.interp_pos[e];  // layout of dif = L - bs * n, or -1
+        for (int32_t k = 0; k < n;) {
+            if (threadIdx.x == 0) {
+                int32_t ke = k + 1;
+                const int32_t ek = bin_edge(bs, lay, P.lay_cnt, k);
+                while (ke < n && bin_edge(bs, lay, P.lay_cnt, ke + 1) - ek <= P.interp_cap) ++ke;
+                group_end = ke;
+            }
+            __syncthreads();
+            const int32_t ke = group_end;
+            const int32_t e0 = bin_edge(bs, lay, P.lay_cnt, k);
+            const int32_t wn = bin_edge(bs, lay, P.lay_cnt, ke) - e0;
+            if (wn > P.interp_cap) {
+                if (threadIdx.x == 0) atomicOr(P.status, RCP_STATUS_INTERP);
+                return;
+            }
+            block_window_depth(P, r, head + e0, wn, diff, scratch);
+            for (int32_t kk = k + threadIdx.x; kk < ke; kk += kBlock) {
+                const int32_t a = bin_edge(bs, lay, P.lay_cnt, kk) - e0;
+                const int32_t b = bin_edge(bs, lay, P.lay_cnt, kk + 1) - e0;
+                int32_t vmin = INT32_MAX, vmax = INT32_MIN;
+                for (int32_t q = a; q < b; ++q) {
+                    vmin = min(vmin, diff[q]);
+                    vmax = max(vmax, diff[q]);
+                }
+                const int32_t mm = b - a, h = (mm + 1) >> 1;
+                const uint32_t x1 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h, vmin, vmax, 30);
+                uint32_t x2 = x1;
+                if (!(mm & 1)) x2 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h + 1, vmin, vmax, 30);
+                out[(size_t)(part.col_off + kk) * R + r] = ((double)(x1 + x2) * P.scale) / 2.0;
+            }
+            __syncthreads();
+            k = ke;
+        }
+        return;
+    }
     if (L > P.interp_cap) {
         if (threadIdx.x == 0) atomicOr(P.status, RCP_STATUS_INTERP);
         return;
     }
-    const int per = (L + 1 + kBlock - 1) / kBlock;
-    for (int q = threadIdx.x; q < per * kBlock; q += kBlock) diff[q] = 0;
-    __syncthreads();
-    const int32_t slot = P.heavy_slot[r];
-    if (slot >= 0) {
-        const int32_t* g = P.heavy_gdiff + (size_t)slot * P.heavy_stride;
-        if (threadIdx.x == 0) {
-            int32_t carry = 0;
-            for (int q = 0; q < head; ++q) carry += g[q];
-            diff[0] = carry;
-        }
-        __syncthreads();
-        for (int q = threadIdx.x; q <= L; q += kBlock) diff[q] += g[head + q];
-    } else {
-        pileup_row(P, r, head, L, diff, threadIdx.x, kBlock);
-    }
-    __syncthreads();
-    scan_block_depth(diff, per, scratch);
-    __syncthreads();
+    block_window_depth(P, r, head, L, diff, scratch);
     if (threadIdx.x != 0) return;
     double* x = P.interp_scratch + (size_t)e * P.interp_stride;
     double* y = x + L + 1;
-    const int mode = P.interp_mode[e];
     for (int i = 0; i < L; ++i) x[i] = (double)diff[i] * P.scale;
     if (mode == 1) {  // spline(x, n = n)$y, then x[x < 0] <- 0
         double* b = y + n + 1;
@@ -959,8 +1039,8 @@ extern "C" hipError_t rcp_launch_heavy_clear(const RcpPlanDev* P, hipStream_t st
 }
 
 extern "C" size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr) {
-    const size_t stage_words = csr ? 0 : (size_t)P->stage_cap * kTile;
-    return 4 * ((size_t)kWaves * (P->wave_words + 4) + stage_words + (size_t)kRows * kMetaWords + 8);
+    const size_t stage_words = csr ? 0 : (size_t)P->stage_cap * (kTile + 1);
+    return 4 * ((size_t)kWaves * (P->wave_words + 8) + stage_words + (size_t)kRows * kMetaWords + 8);
 }
 
 extern "C" int rcp_tile_rows(void) { return kRows; }

@@ -1,0 +1,23 @@
+"""Minimal C4 run for rocprofv3 counter passes (one plan, a few executes)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import synthetic  # noqa: E402
+from recoup_amd.engine import Bins, Plan, ReadSet, RowTable  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c4"
+d = getattr(synthetic, cfg)(device="cuda:0")
+reg = d["regions"]
+rs = ReadSet(*d["reads"], d["seqlen"], device=0)
+rows = RowTable.from_ranges(reg["chrom"], reg["start"], reg["end"], reg["strand"])
+bins = Bins([("whole", d["n_bins"])]) if d["n_bins"] else Bins([("whole", 0, sum(d["flank"]))])
+plan = Plan(rs, rows, bins)
+out = plan.empty_output()
+for _ in range(int(os.environ.get("ITERS", "3"))):
+    plan.execute(out)
+plan.status()
+torch.cuda.synchronize()
+print("ok", plan.info)

@@ -13,7 +13,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librecoup_amd.so")
+# RCP_LIB_PATH: an alternative build of the same library (ablation studies, tools/ablate.sh)
+LIB_PATH = os.environ.get("RCP_LIB_PATH", os.path.join(HERE, "librecoup_amd.so"))
 
 RCP_OK = 0
 ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "EUNSUPPORTED", -5: "ESEMANTIC", -6: "ENODEVICE"}

@@ -26,6 +26,20 @@ struct RcpSeg {
     uint8_t pad;
 };
 
+// Per-row record the locate kernel leaves for the pileup kernel (one 64-byte load per row
+// instead of a chain of dependent loads).  lo/hi are the row's candidate reads per strand
+// stream when the row is a single range (flags & RCP_REC_FAST).
+struct RcpRowRec {
+    int32_t flags;       // RCP_REC_*
+    int32_t row_len;     // nominal coverage length nr
+    int32_t heavy;       // heavy slot or -1
+    int32_t off, slo, shi, rev;  // the single range: row offset, genomic run, reversed
+    uint32_t lo[3], hi[3];
+    int32_t pad[3];
+};
+#define RCP_REC_VALID 1
+#define RCP_REC_FAST 2
+
 struct RcpPart {
     // slice [lo, hi) of the row (0-based): lo = (lo_end ? nr : 0) + lo_off, same for hi
     int32_t lo_off, hi_off;
@@ -85,6 +99,7 @@ struct RcpPlanDev {
     // skewed depth: rows with more than heavy_threshold candidate reads are piled up
     // first by many workgroups (heavy slices) into a global difference array
     uint32_t* ncand;            // [n_rows] candidate reads (locate output)
+    RcpRowRec* rec;             // [n_rows] (locate output)
     int32_t heavy_threshold;    // 0 = heavy path off
     int32_t heavy_cap;          // slots
     int32_t heavy_stride;       // ints per slot (>= max row length + 1 of eligible rows)

@@ -46,7 +46,7 @@ namespace {
 
 constexpr int kChunkMax = 16384;       // positions of an interpolated slice (block LDS array)
 constexpr int kWaveMax = 4096;         // positions per wave sub-chunk (padded LDS array <= 17 KB)
-constexpr int kStageMaxBins = 1024;    // bins per chunk (LDS stage = bins x 8 rows x 4 B)
+constexpr int kStageMaxBins = 512;     // bins per chunk (LDS stage = bins x 17 words)
 constexpr size_t kLdsBudget = 80 * 1024;  // keep two pileup workgroups per CU when possible
 constexpr int kHeavyThreshold = 8192;  // candidate reads above which a row is split across workgroups
 constexpr int kHeavySlice = 16384;     // candidate reads per heavy work item
@@ -526,7 +526,9 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
         int32_t need = 64;
         for (int p = 0; p < P.n_parts; ++p) {
             RcpPart& pt = P.part[p];
-            int32_t cb = std::min<int32_t>(pt.n_bins, kStageMaxBins);
+            // equal chunks of at most kStageMaxBins bins
+            const int32_t nch = (pt.n_bins + kStageMaxBins - 1) / kStageMaxBins;
+            int32_t cb = (pt.n_bins + nch - 1) / nch;
             if (median) cb = std::min<int32_t>(cb, std::max<int32_t>(1, kWaveMax / part_max_bin[p]));
             pt.chunk_bins = cb;
             pt.n_chunks = (pt.n_bins + cb - 1) / cb;
@@ -622,7 +624,8 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     const size_t w_hrows = al(w_hslot + 4 * Rw);
     const size_t w_hoff = al(w_hrows + 4 * (size_t)P.heavy_cap);
     const size_t w_gdiff = al(w_hoff + 4 * ((size_t)P.heavy_cap + 1));
-    const size_t w_status = al(w_gdiff + (P.heavy_threshold > 0 ? 4 * (size_t)P.heavy_cap * P.heavy_stride : 0));
+    const size_t w_rec = al(w_gdiff + (P.heavy_threshold > 0 ? 4 * (size_t)P.heavy_cap * P.heavy_stride : 0));
+    const size_t w_status = al(w_rec + sizeof(RcpRowRec) * Rw);
     HIP_TRY(plan->work.alloc(w_status + 256));
     char* wb = plan->work.as<char>();
     P.ncand = reinterpret_cast<uint32_t*>(wb + w_ncand);
@@ -630,6 +633,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.heavy_rows = reinterpret_cast<int32_t*>(wb + w_hrows);
     P.heavy_slice_off = reinterpret_cast<uint32_t*>(wb + w_hoff);
     P.heavy_gdiff = reinterpret_cast<int32_t*>(wb + w_gdiff);
+    P.rec = reinterpret_cast<RcpRowRec*>(wb + w_rec);
     const int32_t n_interp = (int32_t)B.interp_row.size();
     P.interp_stride = 2 * (max_interp_bins + 1) + 3 * (max_interp_len + 1) + 8;
     if (n_interp) HIP_TRY(plan->scratch.alloc(8 * (size_t)n_interp * P.interp_stride));

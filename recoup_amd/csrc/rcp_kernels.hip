@@ -14,13 +14,14 @@
 //                       prefix-max-of-end array for exact overlap search
 //
 // Design: integer interval counting, HBM-bound, no MFMA.  A workgroup owns
-// T = 8 consecutive rows x one column chunk; each of its 4 waves owns whole rows, so a
+// 32 consecutive rows x one column chunk; each of its 4 waves owns whole rows, so a
 // row needs no block barrier: the wave streams the row's reads as coalesced 8-byte
 // (start, end) pairs (4 loads in flight per lane), adds +w / -w into its own LDS
 // difference array, turns it into depth / cumulative depth with a wave scan (uint32,
 // modular: a bin sum that fits 32 bits comes out exact), and reads every bin with two LDS
-// reads.  Numerators are staged as [bin][row] so the epilogue writes 8 consecutive rows of a
-// column (64 B) per 8 lanes of the R column-major matrix.
+// reads.  Numerators are staged as [bin][row] so the epilogue writes 16 consecutive rows of
+// a column (128 B) per 16 lanes of the R column-major matrix (64-B segments write at ~60 %
+// of the 128-B rate: tools/write_bench.hip).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -30,7 +31,7 @@ namespace {
 
 constexpr int kBlock = RCP_BLOCK;  // 256 threads = 4 waves
 constexpr int kWaves = kBlock / 64;
-constexpr int kTile = 8;           // rows per output round (64 B column segments)
+constexpr int kTile = 16;          // rows per output round (128 B column segments)
 
 __device__ __forceinline__ uint32_t lower_bound_pmax(const int32_t* __restrict__ pmax, uint32_t lo,
                                                      uint32_t hi, int32_t v) {
@@ -52,33 +53,31 @@ __device__ __forceinline__ uint32_t upper_bound_start(const int2* __restrict__ s
     return lo;
 }
 
-__device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    return x - v;
+// Wave64 inclusive prefix sum with DPP (row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast:15 / row_bcast:31 across rows): six VALU ops, no LDS round trip.  (__shfl_up
+// lowers to ds_bpermute + an lgkmcnt wait per step.)
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return (uint32_t)x;
 }
 
+__device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v) { return wave_inclusive_scan(v) - v; }
+
 __device__ __forceinline__ int32_t wave_sum(int32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
+    return __builtin_amdgcn_readlane((int)wave_inclusive_scan((uint32_t)v), 63);
 }
 
 // Block-wide exclusive scan of one uint32 per thread.  `scratch` holds kWaves words.
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* scratch) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
+    const uint32_t x = wave_inclusive_scan(v);
     if (lane == 63) scratch[wave] = x;
     __syncthreads();
     uint32_t off = 0;
@@ -372,6 +371,29 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
         }
     }
     P.heavy_slot[r] = slot;
+    // one record per row for the pileup kernel's metadata stage
+    RcpRowRec rec;
+    rec.flags = valid ? RCP_REC_VALID : 0;
+    rec.row_len = P.row_len[r];
+    rec.heavy = slot;
+    rec.off = rec.slo = rec.shi = rec.rev = 0;
+    for (int s = 0; s < 3; ++s) rec.lo[s] = rec.hi[s] = 0;
+    rec.pad[0] = rec.pad[1] = rec.pad[2] = 0;
+    if (j1 == j0 + 1) {
+        const RcpSeg sg = P.segs[j0];
+        if (!sg.multi && sg.query_ok) {
+            rec.flags |= RCP_REC_FAST;
+            rec.off = sg.off; rec.slo = sg.lo; rec.shi = sg.hi; rec.rev = sg.rev;
+            for (int s = 0; s < 3; ++s) {
+                rec.lo[s] = P.seg_lo[j0 * 3 + s];
+                rec.hi[s] = P.seg_hi[j0 * 3 + s];
+            }
+        }
+    }
+    const uint4* src = reinterpret_cast<const uint4*>(&rec);
+    uint4* dst = reinterpret_cast<uint4*>(P.rec + r);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q] = src[q];
 }
 
 // =================================================================================
@@ -457,7 +479,8 @@ __global__ void rcp_heavy_clear_kernel(RcpPlanDev P) {
 // chunk) is resolved once per workgroup by one thread per row (parallel binary searches),
 // and each wave issues the loads of its NEXT row's first 256 candidate reads before
 // working on the current row's LDS, so a row's HBM round trip overlaps the previous row.
-constexpr int kRounds = 4;
+constexpr int kRounds = 2;
+constexpr int kRowsPerWave = kTile / kWaves;  // rows a wave piles per round
 constexpr int kRows = kTile * kRounds;  // rows per workgroup
 
 struct RowMeta {  // [kRows] each, in LDS
@@ -468,6 +491,16 @@ struct RowMeta {  // [kRows] each, in LDS
     uint32_t lo[3], hi[3];        // candidate reads per strand stream (refined to the piece)
 };
 constexpr int kMetaWords = sizeof(RowMeta) / 4;
+
+// Row metadata in SGPRs: every field is wave-uniform (read from LDS, made scalar)
+__device__ __forceinline__ RowMeta uniform_meta(const RowMeta& src) {
+    RowMeta m;
+    const int32_t* s = reinterpret_cast<const int32_t*>(&src);
+    int32_t* d = reinterpret_cast<int32_t*>(&m);
+#pragma unroll
+    for (int q = 0; q < kMetaWords; ++q) d[q] = __builtin_amdgcn_readfirstlane(s[q]);
+    return m;
+}
 
 __device__ __forceinline__ uint32_t fast_candidates(const RowMeta& m) {
     return (m.hi[0] - m.lo[0]) + (m.hi[1] - m.lo[1]) + (m.hi[2] - m.lo[2]);
@@ -481,6 +514,10 @@ __device__ __forceinline__ uint32_t fast_index(const RowMeta& m, uint32_t q) {
 }
 
 __device__ __forceinline__ void add_read_fast(const RowMeta& m, int2 rd, int32_t* diff, int sh) {
+#ifdef RCP_ABL_ATOMICS  // ablation build (tools/ablate.sh): loads kept, no LDS atomics
+    asm volatile("" ::"v"(rd.x), "v"(rd.y));
+    return;
+#endif
     if (rd.y < m.gps || rd.x > m.gpe) return;
     const int32_t x0 = max(rd.x, m.gps);
     const int32_t x1 = min(rd.y, m.gpe);
@@ -511,8 +548,14 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
     const int wave = tid >> 6;
     const int lane = tid & 63;
     // ---- decode (row block, part, chunk)
-    const int blk = blockIdx.x / P.n_chunks_total;
-    int c = blockIdx.x - blk * P.n_chunks_total;
+    // blocks of one row block (all its column chunks) are b, b + 8, b + 16, ...: one XCD
+    // under round-robin dispatch, so a chunk's re-read of the rows' reads hits that L2
+    // (placement only changes speed, never results)
+    const int grp = blockIdx.x / (8 * P.n_chunks_total);
+    const int wg = blockIdx.x - grp * 8 * P.n_chunks_total;
+    int c = wg >> 3;
+    const int blk = grp * 8 + (wg & 7);
+    if (blk * kRows >= P.n_rows) return;
     int p = 0;
     while (p < P.n_parts - 1 && c >= P.part[p].n_chunks) {
         c -= P.part[p].n_chunks;
@@ -530,6 +573,7 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
     RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : P.stage_cap * TS));
 
     // ---- per-row metadata, one thread per row (searches of all rows in flight together)
+    // ---- per-row metadata, one thread per row, from the locate kernel's 64-byte records
     if (tid < kRows) {
         const int r = row0 + tid;
         RowMeta m;
@@ -537,11 +581,18 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
         m.off = m.slo = m.shi = m.rev = m.gps = m.gpe = 0;
         for (int s = 0; s < 3; ++s) m.lo[s] = m.hi[s] = 0;
         if (r < P.n_rows) {
+            RcpRowRec rec;
+            {
+                const uint4* src = reinterpret_cast<const uint4*>(P.rec + r);
+                uint4* dst = reinterpret_cast<uint4*>(&rec);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) dst[q] = src[q];
+            }
             int32_t head, L;
-            rcp_part_slice(part, P.row_len[r], &head, &L);
+            rcp_part_slice(part, rec.row_len, &head, &L);
             const int32_t n = CSR ? L : part.n_bins;
             m.kend = min(k0 + part.chunk_bins, n);
-            if (!P.valid[r]) {
+            if (!(rec.flags & RCP_REC_VALID)) {
                 m.flag = CSR ? 2 : 1;  // NULL row -> zeros (profile.R:191-197)
             } else if (k0 >= n) {
                 m.flag = 2;
@@ -571,34 +622,36 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
                 m.flag = 0;
                 // median bins wider than a wave chunk: rcp_interp_kernel (mode 4)
                 if (MEDIAN && m.bs + (m.lay >= 0 ? 1 : 0) > P.chunk_cap) m.flag = 2;
-                m.heavy = P.heavy_slot[r];
-                const int j0 = P.row_seg[r];
-                if (m.heavy < 0 && m.npos <= P.chunk_cap && P.row_seg[r + 1] == j0 + 1) {
-                    const RcpSeg sg = P.segs[j0];
-                    if (!sg.multi && sg.query_ok) {
-                        const int32_t len = sg.hi - sg.lo + 1;
-                        const int32_t a = max(m.P0, sg.off);
-                        const int32_t b = min(m.P0 + m.npos, sg.off + len);
-                        m.fast = 1;
-                        m.off = sg.off; m.slo = sg.lo; m.shi = sg.hi; m.rev = sg.rev;
-                        if (a < b) {
-                            if (!sg.rev) {
-                                m.gps = sg.lo + (a - sg.off);
-                                m.gpe = sg.lo + (b - 1 - sg.off);
-                            } else {
-                                m.gpe = sg.hi - (a - sg.off);
-                                m.gps = sg.hi - (b - 1 - sg.off);
+                m.heavy = rec.heavy;
+                if (m.heavy < 0 && m.npos <= P.chunk_cap && (rec.flags & RCP_REC_FAST)) {
+                    const int32_t len = rec.shi - rec.slo + 1;
+                    const int32_t a = max(m.P0, rec.off);
+                    const int32_t b = min(m.P0 + m.npos, rec.off + len);
+                    m.fast = 1;
+                    m.off = rec.off; m.slo = rec.slo; m.shi = rec.shi; m.rev = rec.rev;
+                    if (a < b) {
+                        if (!rec.rev) {
+                            m.gps = rec.slo + (a - rec.off);
+                            m.gpe = rec.slo + (b - 1 - rec.off);
+                        } else {
+                            m.gpe = rec.shi - (a - rec.off);
+                            m.gps = rec.shi - (b - 1 - rec.off);
+                        }
+                        const bool full = (a == rec.off) && (b == rec.off + len);
+                        uint32_t all = 0;
+                        for (int s = 0; s < 3; ++s) all += rec.hi[s] - rec.lo[s];
+                        // a chunk of a modest row streams all the row's reads (the piece
+                        // check drops the others; they are L2 hits for the sibling chunks);
+                        // only big rows pay the dependent binary searches
+                        const bool refine = !full && all > 4096;
+                        for (int s = 0; s < 3; ++s) {
+                            uint32_t lo = rec.lo[s], hi = rec.hi[s];
+                            if (lo < hi && refine) {
+                                lo = lower_bound_pmax(P.pmax, lo, hi, m.gps);
+                                hi = upper_bound_start(P.se, lo, hi, m.gpe);
                             }
-                            const bool full = (a == sg.off) && (b == sg.off + len);
-                            for (int s = 0; s < 3; ++s) {
-                                uint32_t lo = P.seg_lo[j0 * 3 + s], hi = P.seg_hi[j0 * 3 + s];
-                                if (lo < hi && !full) {
-                                    lo = lower_bound_pmax(P.pmax, lo, hi, m.gps);
-                                    hi = upper_bound_start(P.se, lo, hi, m.gpe);
-                                }
-                                m.lo[s] = lo;
-                                m.hi[s] = lo < hi ? hi : lo;
-                            }
+                            m.lo[s] = lo;
+                            m.hi[s] = lo < hi ? hi : lo;
                         }
                     }
                 }
@@ -609,26 +662,27 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
     __syncthreads();
 
     // ---- rows of this wave: round rd, sub s -> row rd*T + s*kWaves + wave
-    auto row_of = [&](int step) { return (step >> 1) * T + (step & 1) * kWaves + wave; };
+    auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kWaves + wave; };
     int2 pre[4];
     auto prefetch = [&](int i) {
-        const RowMeta& m = meta[i];
+        const RowMeta m = uniform_meta(meta[i]);
         const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
+            // unconditional (clamped) loads: no branch, no early vmcnt wait
             const uint32_t q = lane + 64 * u;
-            pre[u] = n ? P.se[fast_index(m, q < n ? q : n - 1)] : make_int2(1, 0);
+            pre[u] = P.se[n ? fast_index(m, q < n ? q : n - 1) : 0u];
         }
     };
     prefetch(row_of(0));
-    for (int step = 0; step < 2 * kRounds; ++step) {
+    for (int step = 0; step < kRowsPerWave * kRounds; ++step) {
         const int i = row_of(step);
         int2 cur[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) cur[u] = pre[u];
-        if (step + 1 < 2 * kRounds) prefetch(row_of(step + 1));  // next row's loads in flight now
-        const RowMeta& m = meta[i];
-        if (m.flag == 0) {  // wave-uniform (LDS broadcast)
+        if (step + 1 < kRowsPerWave * kRounds) prefetch(row_of(step + 1));  // next row's loads in flight now
+        const RowMeta m = uniform_meta(meta[i]);
+        if (m.flag == 0) {  // wave-uniform: scalar branch
             const int r = row0 + i;
             const int32_t npos = m.npos;
             const int32_t bs = m.bs, lay = m.lay, kend = m.kend;
@@ -678,7 +732,9 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
                     pileup_row(P, r, m.P0 + s0, sn, diff, lane, 64, sh);
                 }
                 lds_order();
+#ifndef RCP_ABL_SCAN
                 scan_wave<!(MEDIAN || CSR)>(diff, per);
+#endif
                 lds_order();
                 if (CSR) {
                     for (int32_t k = k0 + s0 + lane; k < k0 + s0 + sn; k += 64)
@@ -706,8 +762,10 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
                     const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
                     int32_t a = lane * bs;
                     uint32_t* st = stage + lane * TS + ii;
+#ifndef RCP_ABL_BINS
                     for (int32_t k = k0 + lane; k < kend; k += 64, a += 64 * bs, st += 64 * TS)
                         *st = cum[lp(a + bs - 1, sh)] - cum[lp(a - 1, sh)];
+#endif
                 } else if (whole) {
                     // splitVector layout: enlarged bins from set.seed(42); sample(1:n, dif)
                     const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
@@ -730,13 +788,16 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
                 lds_order();
             }
         }
-        if (CSR || !(step & 1)) continue;
+        if (CSR || (step % kRowsPerWave) != kRowsPerWave - 1) continue;
+#ifdef RCP_ABL_EPI
+        continue;
+#endif
         __syncthreads();
         // ---- round epilogue: stage[bin][row] -> out[col * n_rows + row].  Thread t always
-        // serves row t % 8 (256 is a multiple of 8), so 8 consecutive lanes write 8
-        // consecutive rows (64 B) of one column.
+        // serves row t % 16 (256 is a multiple of 16), so 16 consecutive lanes write 16
+        // consecutive rows (128 B) of one column.
         {
-            const int rbase = (step >> 1) * T;
+            const int rbase = (step / kRowsPerWave) * T;
             const int ii = tid & (T - 1);
             const int r = row0 + rbase + ii;
             const RowMeta& mr = meta[rbase + ii];
@@ -744,10 +805,10 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
             if (r < P.n_rows && flag != 2) {
                 const size_t R = (size_t)P.n_rows;
                 const int kstep = kBlock / T;
-                int32_t k = k0 + (tid >> 3);
+                int32_t k = k0 + tid / T;
                 size_t o = (size_t)(part.col_off + k) * R + (size_t)r;
                 const size_t ostep = (size_t)kstep * R;
-                const uint32_t* st = stage + (tid >> 3) * TS + ii;
+                const uint32_t* st = stage + (tid / T) * TS + ii;
                 if (flag == 1) {
                     for (; k < kend; k += kstep, o += ostep) {
                         out[o] = 0.0;
@@ -1054,7 +1115,7 @@ static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* bin
         attr_set = true;
     }
     const int tiles = (P->n_rows + kRows - 1) / kRows;
-    const int64_t grid = (int64_t)tiles * P->n_chunks_total;
+    const int64_t grid = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
     hipLaunchKernelGGL((rcp_pileup_kernel<MEDIAN, CSR>), dim3((unsigned)grid), dim3(kBlock), lds, s, *P, out, binsum);
     return hipGetLastError();
 }

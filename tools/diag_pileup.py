@@ -49,6 +49,10 @@ def run(name, check_heavy=False, **kw):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "quick":
+        run("c4 default")
+        run("c4 uniform reads only", enriched=0.0)
+        sys.exit(0)
     run("c4 default", check_heavy=True)
     run("c4 uniform reads only", enriched=0.0)
     run("c4 no reads", n_reads=1000)

@@ -6,3 +6,9 @@ Mirrors the reference's R API for that path (hjanime/recoup R/coverage.R, R/prof
 behind the C ABI in ``include/recoup_amd.h``.
 """
 __version__ = "0.1.0"
+
+from .granges import (GRanges, GRangesList, flank, getFlankingRanges, getRegionalRanges,  # noqa: F401
+                      promoters, resize)
+from .api import (CoverageList, DeviceCoverage, RMatrix, baseCoverageMatrix, binCoverageMatrix,  # noqa: F401
+                  calcCoverage, calcLinearFactors, coverageRef, coverageRnaRef, normalizeLinear, profileMatrix)
+from ._lib import RcpError, SemanticError, UnsupportedError  # noqa: F401

@@ -1,0 +1,376 @@
+"""The reference's R API for the coverage -> profile path, over the HIP engine.
+
+Same names, argument meaning and result shapes as hjanime/recoup:
+
+  calcCoverage(input, mask, strand, ignore_strand)        R/coverage.R:126-174
+  coverageRef(input, genomeRanges, region, flank, ...)    R/coverage.R:1-77
+  coverageRnaRef(input, genomeRanges, helperRanges, ...)  R/coverage.R:79-124
+  profileMatrix(input, flank, binParams)                  R/profile.R:1-98
+  binCoverageMatrix(cvrg, binSize, stat, interpolation, flank, where)   R/profile.R:153-212
+  baseCoverageMatrix(cvrg, flank, where)                                R/profile.R:100-151
+  calcLinearFactors(input) / normalizeLinear(input)       R/util.R:349-362, R/recoup.R:559-577
+
+``input`` is a list of samples, each a dict with at least ``id``, ``name`` and ``ranges`` (a
+``GRanges`` of reads) -- the reference's ``input`` list.  coverageRef / coverageRnaRef leave a
+``DeviceCoverage`` in ``sample["coverage"]``: the reads stay indexed in HBM and the coverage
+vectors are only materialised when asked for (``.to_list()``), because profileMatrix fuses
+coverage and binning in one pass over the reads (no per-base vector ever reaches HBM).
+Every call runs on the GPU through librecoup_amd.so; there is no CPU path.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import Bins, Plan, ReadSet, RowTable
+from .granges import GRanges, GRangesList, getFlankingRanges, getRegionalRanges
+
+
+def _device(device):
+    if device is not None:
+        return int(device)
+    return torch.cuda.current_device() if torch.cuda.is_available() else 0
+
+
+def _first(x, default):
+    if x is None:
+        return default
+    if isinstance(x, (list, tuple)):
+        return x[0]
+    return x
+
+
+class CoverageList(list):
+    """An R named list of coverage vectors (int32 numpy arrays or None for R's NULL)."""
+
+    def __init__(self, items, names=None):
+        super().__init__(items)
+        self.names = None if names is None else list(names)
+
+    def lengths(self):
+        """R's lengths(): 0 for NULL elements."""
+        return np.array([0 if x is None else len(x) for x in self], dtype=np.int64)
+
+
+class RMatrix(np.ndarray):
+    """A numpy matrix that carries R's rownames (region names)."""
+
+    def __new__(cls, a, rownames=None):
+        obj = np.asarray(a).view(cls)
+        obj.rownames = None if rownames is None else list(rownames)
+        return obj
+
+    def __array_finalize__(self, obj):
+        self.rownames = getattr(obj, "rownames", None)
+
+
+# ------------------------------------------------------------------------------ reads
+def _readset(reads, device, strand):
+    """splitBySeqname + strand filter as a device index, cached on the GRanges object."""
+    if isinstance(reads, ReadSet):
+        if strand is not None:
+            raise _lib.UnsupportedError(-4, "strand filtering needs the GRanges, not a prebuilt ReadSet")
+        return reads, None
+    if isinstance(reads, dict):  # a splitBySeqname() list: chromosome -> GRanges
+        parts = [g for g in reads.values() if g is not None and len(g)]
+        levels = list(dict.fromkeys(l for g in parts for l in g.seqlevels))
+        reads = GRanges(np.concatenate([g.seqnames.astype(str) for g in parts]) if parts else np.array([], str),
+                        np.concatenate([g.start for g in parts]) if parts else [],
+                        np.concatenate([g.end for g in parts]) if parts else [],
+                        np.concatenate([g.strand for g in parts]) if parts else [], seqlevels=levels,
+                        seqlengths=_merge_seqlengths(parts, levels))
+    if not isinstance(reads, GRanges):
+        raise TypeError("input must be a GRanges of reads (or a per-chromosome dict of them)")
+    cache = reads.__dict__.setdefault("_rcp_readsets", {})
+    key = (device, strand)
+    if key not in cache:
+        if len(reads.seqlevels) == 0:
+            reads = GRanges(np.array(["."]), [1], [0])[np.zeros(0, dtype=np.int64)]
+        cache[key] = ReadSet(reads.seqcodes, reads.start.astype(np.int32), reads.end.astype(np.int32), reads.strand,
+                             reads.seqlengths, device=device, strand_filter=strand)
+    return cache[key], reads.seqlevels
+
+
+def _merge_seqlengths(parts, levels):
+    sl = {}
+    for g in parts:
+        for l, v in zip(g.seqlevels, g.seqlengths):
+            if v >= 0:
+                sl[l] = int(v)
+    return sl
+
+
+def _rows_from_mask(mask, levels, ignore_strand):
+    """RowTable for a GRanges (one range per row) or GRangesList (one element per row)."""
+    if isinstance(mask, GRangesList):
+        flat = mask.flat
+        chrom = flat.codes_in(levels) if levels is not None else flat.seqcodes
+        n = len(flat)
+        return RowTable(mask.offsets, chrom, _i32(flat.start), _i32(flat.end), flat.strand,
+                        seg_group=np.zeros(n, np.int8), group_is_list=np.array([1, 0, 0, 0], np.uint8),
+                        ignore_strand=ignore_strand, names=mask.names)
+    if isinstance(mask, GRanges):
+        chrom = mask.codes_in(levels) if levels is not None else mask.seqcodes
+        return RowTable.from_ranges(chrom, _i32(mask.start), _i32(mask.end), mask.strand,
+                                    ignore_strand=ignore_strand, names=mask.names)
+    raise TypeError("The mask argument must be a GRanges or GRangesList object")
+
+
+def _i32(a):
+    a = np.asarray(a)
+    if a.size and (a.min() < -(2 ** 31) or a.max() >= 2 ** 31):
+        raise _lib.UnsupportedError(-4, "coordinates beyond int32")
+    return a.astype(np.int32)
+
+
+class DeviceCoverage:
+    """The coverage list of one sample over one mask, kept as (device reads, row table).
+
+    ``len`` / ``names`` / ``lengths()`` / ``to_list()`` answer like the R list of Rle the
+    reference stores in ``input[[s]]$coverage``; profileMatrix bins it on the GPU directly.
+    ``scale`` is the normalisation factor applied to the coverage (normalize = "linear")."""
+
+    def __init__(self, readset, rows, names=None, scale=1.0):
+        self.readset = readset
+        self.rows = rows
+        self.names = None if names is None else list(names)
+        self.scale = float(scale)
+        self._len = None
+        self._valid = None
+
+    def __len__(self):
+        return self.rows.n_rows
+
+    def _plan(self):
+        return Plan(self.readset, self.rows, None)
+
+    def valid(self):
+        if self._valid is None:
+            p = self._plan()
+            self._valid = p.validity()
+            self._len = p.row_lengths()
+        return self._valid
+
+    def lengths(self):
+        """R's lengths(cov): the row's length, 0 where the coverage is NULL."""
+        v = self.valid()
+        return np.where(v, self._len, 0)
+
+    def to_list(self):
+        """Materialise the per-region coverage vectors (calcCoverage's return value)."""
+        cov = self._plan().coverage()
+        if self.scale != 1.0:
+            cov = [None if x is None else x.astype(np.float64) * self.scale for x in cov]
+        return CoverageList(cov, self.names)
+
+    def scaled(self, factor):
+        return DeviceCoverage(self.readset, self.rows, self.names, self.scale * float(factor))
+
+
+# ------------------------------------------------------------------------------ coverage
+def calcCoverage(input, mask, strand=None, ignore_strand=True, device=None, rc=None):
+    """R/coverage.R:126-174: one coverage vector per mask element (None = R's NULL)."""
+    dev = _device(device)
+    rs, levels = _readset(input, dev, strand)
+    rows = _rows_from_mask(mask, levels, ignore_strand)
+    return DeviceCoverage(rs, rows, mask.names).to_list()
+
+
+def _strand_params(sp):
+    sp = sp or {}
+    return sp.get("strand"), bool(sp.get("ignoreStrand", True))
+
+
+def _needs(input, key):
+    """The reference recomputes only when some sample lacks the slot (coverage.R:4-6)."""
+    return any(s.get(key) is None for s in input)
+
+
+def coverageRef(input, genomeRanges, region="tss", flank=(2000, 2000), strandedParams=None, bamParams=None,
+                rc=None, device=None):
+    """R/coverage.R:1-77 (coverageBaseRef / coverageAreaRef share calcCoverage)."""
+    if not _needs(input, "coverage"):
+        return input
+    region = _first(region, "tss")
+    main = getRegionalRanges(genomeRanges, region, flank)
+    strand, ign = _strand_params(strandedParams)
+    dev = _device(device)
+    for s in input:
+        rs, levels = _readset(s["ranges"], dev, strand)
+        s["coverage"] = DeviceCoverage(rs, _rows_from_mask(main, levels, ign), genomeRanges.names)
+    return input
+
+
+def _rna_rows(genomeRanges, helperRanges, flank, levels, ignore_strand):
+    """Rows c(left flank, exons..., right flank) per gene (coverage.R:84-120), groups 0 / 1 / 2."""
+    f1, f2 = int(flank[0]), int(flank[1])
+    left = getFlankingRanges(helperRanges, 1 if f1 == 0 else f1, "upstream")
+    right = getFlankingRanges(helperRanges, 1 if f1 == 0 else f2, "downstream")  # the reference tests flank[1]
+    G = len(genomeRanges)
+    if len(helperRanges) != G:
+        raise _lib.SemanticError(-5, "helperRanges and genomeRanges differ in length")
+    ex = genomeRanges.flat
+    n_ex = np.diff(genomeRanges.offsets)
+    seg_off = np.zeros(G + 1, dtype=np.int64)
+    seg_off[1:] = np.cumsum(n_ex + 2)
+    n = int(seg_off[-1])
+    first = seg_off[:-1]
+    last = seg_off[1:] - 1
+    is_ex = np.ones(n, dtype=bool)
+    is_ex[first] = False
+    is_ex[last] = False
+    chrom = np.empty(n, np.int32)
+    start = np.empty(n, np.int64)
+    end = np.empty(n, np.int64)
+    strand = np.empty(n, np.int8)
+    group = np.ones(n, np.int8)
+    chrom[first], start[first], end[first], strand[first], group[first] = \
+        left.codes_in(levels), left.start, left.end, left.strand, 0
+    chrom[last], start[last], end[last], strand[last], group[last] = \
+        right.codes_in(levels), right.start, right.end, right.strand, 2
+    chrom[is_ex], start[is_ex], end[is_ex], strand[is_ex] = ex.codes_in(levels), ex.start, ex.end, ex.strand
+    return RowTable(seg_off, chrom, _i32(start), _i32(end), strand, seg_group=group,
+                    group_is_list=np.array([0, 1, 0, 0], np.uint8), ignore_strand=ignore_strand,
+                    names=genomeRanges.names)
+
+
+def coverageRnaRef(input, genomeRanges, helperRanges, flank=(2000, 2000), strandedParams=None, bamParams=None,
+                   rc=None, device=None):
+    """R/coverage.R:79-124: exon-concatenated gene coverage with gene flanks, NULL if any part is NULL."""
+    if not _needs(input, "coverage"):
+        return input
+    strand, ign = _strand_params(strandedParams)
+    dev = _device(device)
+    for s in input:
+        rs, levels = _readset(s["ranges"], dev, strand)
+        s["coverage"] = DeviceCoverage(rs, _rna_rows(genomeRanges, helperRanges, flank, levels, ign),
+                                       genomeRanges.names)
+    return input
+
+
+# ------------------------------------------------------------------------------ profile
+def _as_device_coverage(cvrg):
+    if isinstance(cvrg, DeviceCoverage):
+        return cvrg
+    raise _lib.UnsupportedError(-4, "profiles are computed from a DeviceCoverage (coverageRef / coverageRnaRef); "
+                                    "materialised coverage lists are not re-uploaded")
+
+
+def _run(cv, bins):
+    plan = Plan(cv.readset, cv.rows, bins)
+    mat, _ = plan.run()
+    return RMatrix(mat, cv.names)
+
+
+def binCoverageMatrix(cvrg, binSize=1000, stat="mean", interpolation="auto", flank=None, where="center", rc=None):
+    """R/profile.R:153-212: splitVector of each (sliced) coverage vector into binSize bins."""
+    cv = _as_device_coverage(cvrg)
+    stat = str(_first(stat, "mean")).lower()
+    interpolation = _first(interpolation, "auto")
+    where = _first(where, "center")
+    if flank is None:
+        bins = Bins([("whole", int(binSize))], stat=stat, interp=interpolation, scale=cv.scale)
+    else:
+        bins = Bins([(where, int(binSize))], flank=flank, stat=stat, interp=interpolation, scale=cv.scale)
+    return _run(cv, bins)
+
+
+def _base_size(cv):
+    ln = cv.lengths()
+    nz = ln[ln > 0]
+    # baseCoverageMatrix sizes NULL rows from element 1, else the first non-NULL element
+    return int(ln[0]) if len(ln) and ln[0] > 0 else (int(nz[0]) if len(nz) else 0)
+
+
+def baseCoverageMatrix(cvrg, flank=None, where="upstream", rc=None):
+    """R/profile.R:100-151: per-base coverage rows (NULL -> zeros)."""
+    cv = _as_device_coverage(cvrg)
+    where = _first(where, "upstream")
+    if flank is None:
+        bins = Bins([("whole", 0, _base_size(cv))], scale=cv.scale)
+    else:
+        size = int(flank[0]) if where == "upstream" else int(flank[1])
+        bins = Bins([(where, 0, size)], flank=flank, scale=cv.scale)
+    return _run(cv, bins)
+
+
+def _profile_bins(binParams, flank, equal, size):
+    """The column parts profileMatrix assembles (profile.R:13-96), fused into one plan."""
+    fbs = int(binParams.get("flankBinSize", 0))
+    rbs = int(binParams.get("regionBinSize", 0))
+    stat = str(_first(binParams.get("sumStat"), "mean")).lower()
+    interp = _first(binParams.get("interpolation"), "auto")
+    if equal:
+        if rbs != 0:  # the equal-length branch leaves interpolation at its default (profile.R:87-89)
+            return Bins([("whole", rbs)], stat=stat, interp="auto")
+        return Bins([("whole", 0, size)])
+    f1, f2 = int(flank[0]), int(flank[1])
+    parts = []
+    if fbs != 0:
+        r = np.asarray([f1, f2], dtype=float) / (f1 + f2)
+        if f1:
+            parts.append(("upstream", int(np.round(2 * fbs * r[0]))))
+        parts.append(("center", rbs))
+        if f2:
+            parts.append(("downstream", int(np.round(2 * fbs * r[1]))))
+    else:
+        if f1:
+            parts.append(("upstream", 0, f1))
+        parts.append(("center", rbs))
+        if f2:
+            parts.append(("downstream", 0, f2))
+    return Bins(parts, flank=(f1, f2), stat=stat, interp=interp)
+
+
+def profileMatrix(input, flank, binParams, rc=None, keep_on_device=False):
+    """R/profile.R:1-98: per-sample R x B double matrix in ``sample["profile"]``.
+
+    The equal-length test uses the first sample's non-NULL lengths only (profile.R:6-10).
+    With ``keep_on_device`` the column-major float64 matrix also stays in HBM as
+    ``sample["profile_device"]`` (shape (B, R) in torch terms)."""
+    if not _needs(input, "profile"):
+        return input
+    cvs = [_as_device_coverage(s["coverage"]) for s in input]
+    ln = cvs[0].lengths()
+    ln = ln[ln != 0]
+    equal = bool(np.all(ln == ln[0])) if len(ln) else True
+    for s, cv in zip(input, cvs):
+        bins = _profile_bins(binParams, flank, equal, _base_size(cv) if equal else 0)
+        bins.scale = cv.scale
+        plan = Plan(cv.readset, cv.rows, bins)
+        out = plan.empty_output()
+        valid = torch.empty(max(plan.n_rows, 1), dtype=torch.uint8, device=out.device)
+        plan.execute(out, valid)
+        plan.status()
+        s["profile"] = RMatrix(out.cpu().numpy().T, cv.names)
+        if keep_on_device:
+            s["profile_device"] = out
+    return input
+
+
+# ------------------------------------------------------------------------------ normalisation
+def calcLinearFactors(input, preprocessParams=None):
+    """R/util.R:349-362: min(libsize) / libsize ("linear", "downsample") or sampleTo / libsize
+    ("sampleto") per sample, libsize = number of reads."""
+    if any(s.get("ranges") is None for s in input):
+        raise _lib.SemanticError(-5, "Please provide input reads before calculation normalization factors")
+    pp = preprocessParams or {"normalize": "linear"}
+    lib = np.array([len(s["ranges"]) for s in input], dtype=np.float64)
+    if pp.get("normalize") in ("linear", "downsample"):
+        return lib.min() / lib
+    if pp.get("normalize") == "sampleto":
+        return float(pp["sampleTo"]) / lib
+    raise _lib.SemanticError(-5, f"no linear factors for normalize = {pp.get('normalize')!r}")
+
+
+def normalizeLinear(input):
+    """R/recoup.R:559-577 (normalize = "linear"): scale each sample's coverage."""
+    f = calcLinearFactors(input)
+    for s, k in zip(input, f):
+        if k == 1:
+            continue
+        cv = s.get("coverage")
+        if isinstance(cv, DeviceCoverage):
+            s["coverage"] = cv.scaled(k)
+        elif cv is not None:
+            s["coverage"] = CoverageList([None if x is None else x * k for x in cv], cv.names)
+    return input

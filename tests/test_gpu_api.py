@@ -1,0 +1,154 @@
+"""The R-mirroring API on the GPU, written like the reference's own tests
+(inst/unitTests/test_recoup.R: TSS per-base, genebody binned; man pages of calcCoverage,
+coverageRnaRef and profileMatrix) over the reference's fixture data/recoup_test_data.rda.
+Expected values: tests/golden/c1_expected.npz (oracle-made, pinned in tests/test_oracle.py)
+and, for coverage lists, the oracle itself."""
+import os
+
+import numpy as np
+import pytest
+
+import recoup_amd as ra
+from oracle import oracle as o
+from tests.golden import c1_cases
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "c1_expected.npz")
+FLANK = (2000, 2000)
+
+
+@pytest.fixture(scope="module")
+def c1(gpu):
+    d = c1_cases.load_inputs()
+    G = c1_cases.genome(d)
+    E = c1_cases.exons(d)
+    genome = ra.GRanges(G["chrom"], G["start"], G["end"], G["strand"], names=G["names"])
+    exons = ra.GRangesList(ra.GRanges(E["chrom"], E["start"], E["end"], E["strand"]), E["seg_off"], E["names"])
+    return dict(d=d, G=G, E=E, genome=genome, exons=exons, gold=dict(np.load(GOLD)))
+
+
+def _input(c1):
+    """test.input: two samples with their reads (recoup_test_data.rda)."""
+    out = []
+    for s in c1_cases.samples(c1["d"]):
+        sl = {lv: int(v) for lv, v in zip(s["seqlevels"], s["seqlengths"]) if v >= 0}
+        reads = ra.GRanges(np.full(len(s["start"]), "chr12"), s["start"], s["end"], s["strand"],
+                           seqlevels=s["seqlevels"], seqlengths=sl)
+        out.append({"id": s["id"], "name": s["name"], "ranges": reads})
+    return out
+
+
+def test_tss_chipseq_per_base(c1):
+    """test_recoup.R:4-13 -- region "tss", flank 2000/2000, binParams all zero."""
+    inp = ra.coverageRef(_input(c1), c1["genome"], "tss", FLANK)
+    inp = ra.profileMatrix(inp, FLANK, {"flankBinSize": 0, "regionBinSize": 0})
+    for k, s in enumerate(inp):
+        assert s["profile"].shape == (100, 4000)
+        np.testing.assert_array_equal(np.asarray(s["profile"]), c1["gold"][f"tss_base_s{k}"].astype(np.float64))
+        assert s["profile"].rownames == list(c1["G"]["names"])
+        # the forced heatmap pass (recoup.R:659-671): binCoverageMatrix(..., binSize = 200)
+        heat = ra.binCoverageMatrix(s["coverage"], binSize=200, stat="mean")
+        np.testing.assert_allclose(heat, c1["gold"][f"tss_heat_s{k}"], rtol=1e-12, atol=0)
+
+
+def test_tss_profile_150_bins(c1):
+    """man/profileMatrix.Rd: regionBinSize 150 over 4000 bp -> the set.seed(42) bin layout."""
+    inp = ra.coverageRef(_input(c1), c1["genome"], "tss", FLANK)
+    inp = ra.profileMatrix(inp, FLANK, {"flankBinSize": 50, "regionBinSize": 150, "sumStat": "mean"})
+    for k, s in enumerate(inp):
+        np.testing.assert_allclose(s["profile"], c1["gold"][f"tss150_s{k}"], rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("stat", ["mean", "median"])
+def test_genebody_binned(c1, stat):
+    """test_recoup.R:15-26 -- region "genebody", flankBinSize 50, regionBinSize 150."""
+    inp = ra.coverageRef(_input(c1), c1["genome"], "genebody", FLANK)
+    inp = ra.profileMatrix(inp, FLANK, {"flankBinSize": 50, "regionBinSize": 150, "sumStat": stat,
+                                        "interpolation": "auto"})
+    for k, s in enumerate(inp):
+        assert s["profile"].shape == (100, 250)
+        np.testing.assert_allclose(s["profile"], c1["gold"][f"gb_{stat}_s{k}"], rtol=1e-9, atol=1e-12)
+
+
+def test_rna_coverage_profile(c1):
+    """man/coverageRnaRef.Rd: exon GRangesList + gene helper ranges."""
+    inp = ra.coverageRnaRef(_input(c1), c1["exons"], c1["genome"], FLANK)
+    inp = ra.profileMatrix(inp, FLANK, {"flankBinSize": 50, "regionBinSize": 150})
+    for k, s in enumerate(inp):
+        np.testing.assert_array_equal(s["coverage"].valid(), c1["gold"][f"rna_valid_s{k}"].astype(bool))
+        np.testing.assert_allclose(s["profile"], c1["gold"][f"rna_s{k}"], rtol=1e-9, atol=1e-12)
+        assert s["profile"].rownames == list(c1["E"]["names"])
+
+
+def _oracle_index(sample):
+    return o.Index(np.zeros(len(sample["start"]), np.int32), sample["start"], sample["end"], sample["strand"],
+                   sample["seqlengths"])
+
+
+def test_calc_coverage_lists(c1):
+    """man/calcCoverage.Rd: calcCoverage(reads, genes) and over the exon GRangesList."""
+    inp = _input(c1)
+    S = c1_cases.samples(c1["d"])
+    G, E = c1["G"], c1["E"]
+    ix = _oracle_index(S[0])
+    cases = [
+        (c1["genome"], o.Mask.from_ranges(np.zeros(100, np.int32), G["start"], G["end"], G["strand"]), True),
+        (c1["exons"], o.Mask(E["seg_off"], np.zeros(len(E["start"]), np.int32), E["start"], E["end"],
+                             E["strand"]), True),
+        (c1["genome"], o.Mask.from_ranges(np.zeros(100, np.int32), G["start"], G["end"], G["strand"]), False),
+    ]
+    for mask, omask, ign in cases:
+        got = ra.calcCoverage(inp[0]["ranges"], mask, ignore_strand=ign)
+        exp = o.coverage(ix, omask, ign)
+        assert len(got) == len(exp)
+        for g, e in zip(got, exp):
+            assert (g is None) == (e is None)
+            if e is not None:
+                np.testing.assert_array_equal(g, e)
+
+
+def test_calc_coverage_strand(c1):
+    inp = _input(c1)
+    S = c1_cases.samples(c1["d"])
+    G = c1["G"]
+    ix = o.Index(np.zeros(len(S[1]["start"]), np.int32), S[1]["start"], S[1]["end"], S[1]["strand"],
+                 S[1]["seqlengths"], strand_filter="-")
+    win = ra.getRegionalRanges(c1["genome"], "tss", FLANK)
+    got = ra.calcCoverage(inp[1]["ranges"], win, strand="-")
+    exp = o.coverage(ix, o.Mask.from_ranges(np.zeros(100, np.int32), win.start, win.end, win.strand))
+    for g, e in zip(got, exp):
+        assert (g is None) == (e is None)
+        if e is not None:
+            np.testing.assert_array_equal(g, e)
+
+
+def test_device_coverage_lengths_and_list(c1):
+    inp = ra.coverageRef(_input(c1), c1["genome"], "genebody", FLANK)
+    cv = inp[0]["coverage"]
+    lst = cv.to_list()
+    np.testing.assert_array_equal(cv.lengths(), lst.lengths())
+    assert lst.names == list(c1["G"]["names"])
+
+
+def test_normalize_linear(c1):
+    inp = ra.coverageRef(_input(c1), c1["genome"], "tss", FLANK)
+    f = ra.calcLinearFactors(inp)
+    inp = ra.normalizeLinear(inp)
+    inp = ra.profileMatrix(inp, FLANK, {"flankBinSize": 0, "regionBinSize": 200})
+    for k, s in enumerate(inp):
+        np.testing.assert_allclose(s["profile"], c1["gold"][f"tss_heat_s{k}"] * f[k], rtol=1e-12, atol=0)
+
+
+def test_profile_needs_device_coverage(c1):
+    inp = ra.coverageRef(_input(c1), c1["genome"], "tss", FLANK)
+    inp[0]["coverage"] = inp[0]["coverage"].to_list()
+    with pytest.raises(ra.UnsupportedError):
+        ra.profileMatrix(inp, FLANK, {"regionBinSize": 200})
+
+
+def test_missing_chromosome_rows_are_null(c1):
+    inp = _input(c1)
+    g = ra.GRanges(["chr12", "chrUn", "chr12"], [1_000_000, 5, 121_257_000], width=[2000, 2000, 2000])
+    cov = ra.calcCoverage(inp[0]["ranges"], g)
+    assert cov[1] is None  # not in the reads' seqlevels -> "chrUn not found!" -> NULL
+    assert cov[2] is None  # crosses the chromosome end -> subscript error -> NULL

@@ -1,0 +1,113 @@
+"""Host logic of the package (no GPU): GRanges construction, the region-window verbs of
+R/ranges.R:67-100, the profileMatrix column-part selection (R/profile.R:1-98) and the
+coverageRnaRef row table (R/coverage.R:79-124), checked against the oracle's independent
+restatement and the reference's documented semantics."""
+import numpy as np
+import pytest
+
+import recoup_amd as ra
+from recoup_amd import api
+from oracle import oracle as o
+from tests.golden import c1_cases
+
+
+@pytest.fixture(scope="module")
+def c1():
+    d = c1_cases.load_inputs()
+    return d, c1_cases.genome(d), c1_cases.exons(d)
+
+
+def _genome(G):
+    return ra.GRanges(G["chrom"], G["start"], G["end"], G["strand"], names=G["names"])
+
+
+def test_granges_basics():
+    g = ra.GRanges(["chr2", "chr1", "chr2"], [10, 20, 30], width=[5, 1, 10], strand=["+", "-", "*"],
+                   seqlengths={"chr1": 100})
+    assert g.seqlevels == ["chr2", "chr1"]
+    np.testing.assert_array_equal(g.end, [14, 20, 39])
+    np.testing.assert_array_equal(g.strand, [0, 1, 2])
+    np.testing.assert_array_equal(g.seqlengths, [-1, 100])
+    np.testing.assert_array_equal(g.codes_in(["chr1", "chr3"]), [-1, 0, -1])
+    assert len(g.keep_strand("-")) == 1
+    sub = g[np.array([True, False, True])]
+    np.testing.assert_array_equal(sub.start, [10, 30])
+    with pytest.raises(ValueError):
+        ra.GRanges(["chr1"], [1], [2], strand=["x"])
+
+
+@pytest.mark.parametrize("region", ["tss", "tes", "genebody", "custom"])
+@pytest.mark.parametrize("flank", [(2000, 2000), (500, 1500), (0, 1000)])
+def test_regional_ranges_match_oracle(c1, region, flank):
+    _, G, _ = c1
+    got = ra.getRegionalRanges(_genome(G), region, flank)
+    s, e = o.regional_ranges(G["start"], G["end"], G["strand"], region, flank)
+    np.testing.assert_array_equal(got.start, s)
+    np.testing.assert_array_equal(got.end, e)
+
+
+def test_point_regions_use_promoters():
+    """custom regions of width 1 (peak summits, config C4) -> promoters (ranges.R:81-83)."""
+    g = ra.GRanges(["c"] * 2, [100, 200], [100, 200], ["+", "-"])
+    r = ra.getRegionalRanges(g, "custom", (1000, 1000))
+    np.testing.assert_array_equal(r.start, [-900, -799])
+    np.testing.assert_array_equal(r.end, [1099, 1200])
+    assert set(r.width) == {2000}
+
+
+def test_flanking_ranges(c1):
+    _, G, _ = c1
+    g = _genome(G)
+    up = ra.getFlankingRanges(g, 2000, "upstream")
+    s, e = o.promoters(G["start"], G["end"], G["strand"], 2000, 0)
+    np.testing.assert_array_equal((up.start, up.end), (s, e))
+    dn = ra.getFlankingRanges(g, 700, "downstream")
+    s, e = o.flank_end(G["start"], G["end"], G["strand"], 700)
+    np.testing.assert_array_equal((dn.start, dn.end), (s, e))
+
+
+def test_profile_bins_equal_lengths():
+    b = api._profile_bins({"regionBinSize": 200, "interpolation": "spline", "sumStat": ["median", "mean"]},
+                          (2000, 2000), True, 4000)
+    assert b.parts == [("whole", 200)] and b.stat == 1 and b.interp == 0  # interpolation left at "auto"
+    b = api._profile_bins({"regionBinSize": 0}, (2000, 2000), True, 4000)
+    assert b.parts == [("whole", 0, 4000)] and b.n_cols == 4000
+
+
+def test_profile_bins_unequal_lengths():
+    b = api._profile_bins({"regionBinSize": 150, "flankBinSize": 50}, (2000, 2000), False, 0)
+    assert b.parts == [("upstream", 50), ("center", 150), ("downstream", 50)]
+    b = api._profile_bins({"regionBinSize": 100, "flankBinSize": 25}, (500, 1500), False, 0)
+    # round(2 * 25 * 0.25) = round(12.5) = 12 (R rounds half to even), round(37.5) = 38
+    assert b.parts == [("upstream", 12), ("center", 100), ("downstream", 38)]
+    b = api._profile_bins({"regionBinSize": 100, "flankBinSize": 0}, (300, 0), False, 0)
+    assert b.parts == [("upstream", 0, 300), ("center", 100)] and b.n_cols == 400
+
+
+def test_rna_row_table(c1):
+    d, G, E = c1
+    gl = ra.GRangesList(ra.GRanges(E["chrom"], E["start"], E["end"], E["strand"]), E["seg_off"], E["names"])
+    levels = ["chr12"]
+    rows = api._rna_rows(gl, _genome(G), (2000, 2000), levels, True)
+    assert rows.n_rows == len(G["start"])
+    n_ex = np.diff(E["seg_off"])
+    np.testing.assert_array_equal(np.diff(rows.seg_off), n_ex + 2)
+    ls, le = o.promoters(G["start"], G["end"], G["strand"], 2000, 0)
+    rs, re_ = o.flank_end(G["start"], G["end"], G["strand"], 2000)
+    first, last = rows.seg_off[:-1], rows.seg_off[1:] - 1
+    np.testing.assert_array_equal(rows.start[first], ls)
+    np.testing.assert_array_equal(rows.end[last], re_)
+    assert set(rows.seg_group[first]) == {0} and set(rows.seg_group[last]) == {2}
+    # flank[1] == 0 -> 1 bp flanks on both sides (the reference tests flank[1] for the right one too)
+    rows0 = api._rna_rows(gl, _genome(G), (0, 2000), levels, True)
+    w = rows0.end - rows0.start + 1
+    assert set(w[rows0.seg_off[:-1]]) == {1} and set(w[rows0.seg_off[1:] - 1]) == {1}
+
+
+def test_linear_factors():
+    s = [{"ranges": ra.GRanges(["c"] * n, np.arange(1, n + 1), width=10)} for n in (100, 50, 200)]
+    np.testing.assert_allclose(ra.calcLinearFactors(s), [0.5, 1.0, 0.25])
+    np.testing.assert_allclose(ra.calcLinearFactors(s, {"normalize": "sampleto", "sampleTo": 25}),
+                               [0.25, 0.5, 0.125])
+    with pytest.raises(ra.SemanticError):
+        ra.calcLinearFactors([{"ranges": None}])

@@ -21,3 +21,8 @@ for _ in range(int(os.environ.get("ITERS", "3"))):
 plan.status()
 torch.cuda.synchronize()
 print("ok", plan.info)
+meta = os.environ.get("PROF_META")
+if meta:
+    import json
+    with open(meta, "w") as f:
+        json.dump({"config": cfg, "regions": len(reg["start"]), "reads": int(d["reads"][1].numel())}, f)

@@ -59,6 +59,13 @@ struct RcpPlanDev {
     const int64_t* stream_off; // [n_chrom*3 + 1]
     const int64_t* seqlen;     // [n_chrom] (-1 = NA)
     int32_t n_chrom;
+    // bucket directory of each stream (buckets of 2^dir_shift bp): for a position v in
+    // bucket b, lower_bound(pmax >= v) lies in [dir_l[b], dir_l[b+1]] and
+    // upper_bound(start > v) in [dir_u[b], dir_u[b+1]] (entries at dir_off[stream] ..)
+    const int32_t* dir_l;
+    const int32_t* dir_u;
+    const int64_t* dir_off;    // [n_chrom*3 + 1]
+    int32_t dir_shift;
     // rows
     int32_t n_rows;
     const int32_t* row_chrom;   // [n_rows]

@@ -40,13 +40,21 @@ hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* st
 hipError_t rcp_launch_streams(int64_t n, const uint64_t* keys, const int32_t* vals, int64_t* off, int64_t n_off,
                               int2* se, uint64_t* scan_in, hipStream_t stream);
 hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* pmax, hipStream_t stream);
+hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t* off, const int32_t* pmax, int32_t* out,
+                                    hipStream_t stream);
+hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const int64_t* dir_off, const int64_t* off,
+                          const int32_t* pmax, const int2* se, int shift, int32_t* dir_l, int32_t* dir_u,
+                          hipStream_t stream);
 }
 
 namespace {
 
 constexpr int kChunkMax = 16384;       // positions of an interpolated slice (block LDS array)
 constexpr int kWaveMax = 4096;         // positions per wave sub-chunk (padded LDS array <= 17 KB)
-constexpr int kStageMaxBins = 512;     // bins per chunk (LDS stage = bins x 17 words)
+#ifndef RCP_STAGE_MAX_BINS
+#define RCP_STAGE_MAX_BINS 512
+#endif
+constexpr int kStageMaxBins = RCP_STAGE_MAX_BINS;  // bins per chunk (LDS stage = bins x 17 words)
 constexpr size_t kLdsBudget = 80 * 1024;  // keep two pileup workgroups per CU when possible
 constexpr int kHeavyThreshold = 8192;  // candidate reads above which a row is split across workgroups
 constexpr int kHeavySlice = 16384;     // candidate reads per heavy work item
@@ -147,6 +155,8 @@ struct rcp_readset {
     std::vector<int64_t> seqlen;
     std::vector<int64_t> h_stream_off;  // n_chrom*3 + 1
     DevBuf se, pmax, stream_off, d_seqlen;
+    DevBuf dir_l, dir_u, dir_off;  // bucket directory (rcp_device.h)
+    int32_t dir_shift = 12;
 };
 
 extern "C" const char* rcp_version(void) { return "recoup_amd 0.1.0 (gfx950)"; }
@@ -241,9 +251,44 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     HIP_TRY(hipMemcpyAsync(rs->h_stream_off.data(), rs->stream_off.p, 8 * (n_streams + 2), hipMemcpyDeviceToHost, s));
     HIP_TRY(rs->d_seqlen.alloc(8 * d->n_chrom));
     HIP_TRY(hipMemcpyAsync(rs->d_seqlen.p, rs->seqlen.data(), 8 * d->n_chrom, hipMemcpyHostToDevice, s));
+    // ---- bucket directory: ~32 reads of a stream per bucket on average
+    DevBuf maxend;
+    HIP_TRY(maxend.alloc(4 * std::max<int64_t>(n_streams, 1)));
+    HIP_TRY(rcp_launch_stream_maxend(n_streams, rs->stream_off.as<int64_t>(), rs->pmax.as<int32_t>(),
+                                     maxend.as<int32_t>(), s));
+    std::vector<int32_t> h_maxend(std::max<int64_t>(n_streams, 1));
+    HIP_TRY(hipMemcpyAsync(h_maxend.data(), maxend.p, 4 * n_streams, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     rs->n = rs->h_stream_off[n_streams];
     rs->h_stream_off.resize(n_streams + 1);
+    {
+        std::vector<int64_t> span(d->n_chrom, 0);
+        double genome = 0;
+        for (int c = 0; c < d->n_chrom; ++c) {
+            int64_t m = std::max<int64_t>(rs->seqlen[c], 0);
+            for (int st = 0; st < 3; ++st) m = std::max<int64_t>(m, h_maxend[c * 3 + st]);
+            span[c] = m;
+            genome += (double)m;
+        }
+        const double want = rs->n > 0 ? 32.0 * 3.0 * genome / (double)rs->n : 1e9;
+        int shift = 6;
+        while (shift < 24 && (double)(int64_t(1) << (shift + 1)) <= want) ++shift;
+        rs->dir_shift = shift;
+        std::vector<int64_t> doff(n_streams + 1, 0);
+        for (int c = 0; c < d->n_chrom; ++c) {
+            const int64_t nb = (span[c] >> shift) + 1;  // buckets 0 .. nb-1, entries 0 .. nb
+            for (int st = 0; st < 3; ++st) doff[c * 3 + st + 1] = doff[c * 3 + st] + nb + 1;
+        }
+        const int64_t ne = doff[n_streams];
+        HIP_TRY(rs->dir_off.alloc(8 * (n_streams + 1)));
+        HIP_TRY(rs->dir_l.alloc(4 * std::max<int64_t>(ne, 1)));
+        HIP_TRY(rs->dir_u.alloc(4 * std::max<int64_t>(ne, 1)));
+        HIP_TRY(hipMemcpyAsync(rs->dir_off.p, doff.data(), 8 * (n_streams + 1), hipMemcpyHostToDevice, s));
+        HIP_TRY(rcp_launch_dir(ne, n_streams, rs->dir_off.as<int64_t>(), rs->stream_off.as<int64_t>(),
+                               rs->pmax.as<int32_t>(), rs->se.as<int2>(), shift, rs->dir_l.as<int32_t>(),
+                               rs->dir_u.as<int32_t>(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
     *out = rs.release();
     return RCP_OK;
 }
@@ -642,6 +687,10 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.pmax = rs->pmax.as<int32_t>();
     P.stream_off = rs->stream_off.as<int64_t>();
     P.seqlen = rs->d_seqlen.as<int64_t>();
+    P.dir_l = rs->dir_l.as<int32_t>();
+    P.dir_u = rs->dir_u.as<int32_t>();
+    P.dir_off = rs->dir_off.as<int64_t>();
+    P.dir_shift = rs->dir_shift;
     P.n_chrom = rs->n_chrom;
     P.n_rows = R;
     P.row_chrom = reinterpret_cast<const int32_t*>(base + o_row_chrom);

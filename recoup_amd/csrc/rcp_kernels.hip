@@ -314,6 +314,35 @@ extern "C" hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint
     return hipcub::DeviceScan::InclusiveScan(temp, *temp_bytes, in, out, SegMaxOp(), (int)n, stream);
 }
 
+// Last prefix-max of every stream = its largest read end (-1 for an empty stream).
+__global__ void rcp_stream_maxend_kernel(int64_t n_streams, const int64_t* __restrict__ off,
+                                         const int32_t* __restrict__ pmax, int32_t* __restrict__ out) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_streams) return;
+    out[s] = off[s + 1] > off[s] ? pmax[off[s + 1] - 1] : -1;
+}
+
+// Directory entry e (stream found by bisection on dir_off): bucket b = e - dir_off[s];
+// dir_l = lower_bound(pmax >= b << shift), dir_u = upper_bound(start > (b << shift) - 1).
+__global__ void rcp_dir_kernel(int64_t n_entries, int64_t n_streams, const int64_t* __restrict__ dir_off,
+                               const int64_t* __restrict__ off, const int32_t* __restrict__ pmax,
+                               const int2* __restrict__ se, int shift, int32_t* __restrict__ dir_l,
+                               int32_t* __restrict__ dir_u) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_entries) return;
+    int64_t a = 0, b = n_streams;  // last stream with dir_off[s] <= e
+    while (b - a > 1) {
+        const int64_t m = (a + b) >> 1;
+        if (dir_off[m] <= e) a = m; else b = m;
+    }
+    const int64_t bucket = e - dir_off[a];
+    const int64_t v = bucket << shift;
+    const int32_t vc = (int32_t)min(v, (int64_t)INT32_MAX);
+    const uint32_t so = (uint32_t)off[a], eo = (uint32_t)off[a + 1];
+    dir_l[e] = (int32_t)lower_bound_pmax(pmax, so, eo, vc);
+    dir_u[e] = (int32_t)upper_bound_start(se, so, eo, (int32_t)min(v - 1, (int64_t)INT32_MAX));
+}
+
 // =================================================================================
 // locate: per (row, segment, stream) read ranges, the NULL rules, heavy-row slots
 // =================================================================================
@@ -336,10 +365,14 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
         for (int s = 0; s < 3; ++s) {
             uint32_t lo = 0, hi = 0;
             if (ok && sg.query_ok && ((sg.streams >> s) & 1)) {
-                const uint32_t so = (uint32_t)P.stream_off[chrom * 3 + s];
-                const uint32_t eo = (uint32_t)P.stream_off[chrom * 3 + s + 1];
-                lo = lower_bound_pmax(P.pmax, so, eo, sg.lo);
-                hi = upper_bound_start(P.se, lo, eo, sg.hi);
+                // bucket directory: both searches start inside one bucket's reads
+                const int64_t d0 = P.dir_off[chrom * 3 + s];
+                const int32_t nb = (int32_t)(P.dir_off[chrom * 3 + s + 1] - d0) - 1;
+                const int32_t bl = min(max(sg.lo, 0) >> P.dir_shift, nb - 1);
+                const int32_t bh = min(max(sg.hi, 0) >> P.dir_shift, nb - 1);
+                lo = lower_bound_pmax(P.pmax, (uint32_t)P.dir_l[d0 + bl], (uint32_t)P.dir_l[d0 + bl + 1], sg.lo);
+                hi = upper_bound_start(P.se, max(lo, (uint32_t)P.dir_u[d0 + bh]),
+                                       max(lo, (uint32_t)P.dir_u[d0 + bh + 1]), sg.hi);
                 if (lo < hi) {
                     hit[g] = true;
                     maxend[g] = max(maxend[g], P.pmax[hi - 1]);
@@ -479,8 +512,21 @@ __global__ void rcp_heavy_clear_kernel(RcpPlanDev P) {
 // chunk) is resolved once per workgroup by one thread per row (parallel binary searches),
 // and each wave issues the loads of its NEXT row's first 256 candidate reads before
 // working on the current row's LDS, so a row's HBM round trip overlaps the previous row.
-constexpr int kRounds = 2;
-constexpr int kRowsPerWave = kTile / kWaves;  // rows a wave piles per round
+#ifndef RCP_PILE_WAVES
+#define RCP_PILE_WAVES 8
+#endif
+#ifndef RCP_PILE_ROUNDS
+#define RCP_PILE_ROUNDS 4
+#endif
+constexpr int kPWaves = RCP_PILE_WAVES;  // waves per pileup workgroup (they share one stage)
+constexpr int kPBlock = 64 * kPWaves;
+constexpr int kRounds = RCP_PILE_ROUNDS;
+static_assert(kTile % kPWaves == 0, "a round's rows are split evenly over the waves");
+constexpr int kRowsPerWave = kTile / kPWaves;  // rows a wave piles per round
+#ifndef RCP_PF_AHEAD
+#define RCP_PF_AHEAD 2
+#endif
+constexpr int kAhead = RCP_PF_AHEAD;  // rows whose first reads are prefetched
 constexpr int kRows = kTile * kRounds;  // rows per workgroup
 
 struct RowMeta {  // [kRows] each, in LDS
@@ -540,7 +586,7 @@ __device__ __forceinline__ void lds_order() {
 }
 
 template <bool MEDIAN, bool CSR>
-__global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
+__global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
                                                             int64_t* __restrict__ binsum) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int T = kTile;
@@ -569,7 +615,7 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
     // cumulative array; the stage is [bin][T + 1] (odd row stride: conflict-free writes)
     constexpr int TS = T + 1;
     int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * (P.wave_words + 8) + 8;
-    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kWaves * (P.wave_words + 8);
+    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * (P.wave_words + 8);
     RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : P.stage_cap * TS));
 
     // ---- per-row metadata, one thread per row (searches of all rows in flight together)
@@ -661,26 +707,35 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
     }
     __syncthreads();
 
-    // ---- rows of this wave: round rd, sub s -> row rd*T + s*kWaves + wave
-    auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kWaves + wave; };
-    int2 pre[4];
-    auto prefetch = [&](int i) {
+    // ---- rows of this wave: round rd, sub s -> row rd*T + s*kPWaves + wave
+    auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
+    // software pipeline: the first 256 candidate reads of the next kAhead rows are in flight
+    // while a row is piled up (registers are free: LDS, not VGPRs, limits occupancy)
+    constexpr int kSteps = kRowsPerWave * kRounds;
+    auto prefetch = [&](int i, int2* dst) {
         const RowMeta m = uniform_meta(meta[i]);
         const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             // unconditional (clamped) loads: no branch, no early vmcnt wait
             const uint32_t q = lane + 64 * u;
-            pre[u] = P.se[n ? fast_index(m, q < n ? q : n - 1) : 0u];
+            dst[u] = P.se[n ? fast_index(m, q < n ? q : n - 1) : 0u];
         }
     };
-    prefetch(row_of(0));
-    for (int step = 0; step < kRowsPerWave * kRounds; ++step) {
+    int2 pre[kAhead][4];
+#pragma unroll
+    for (int a = 0; a < kAhead; ++a)
+        if (a < kSteps) prefetch(row_of(a), pre[a]);
+    for (int step = 0; step < kSteps; ++step) {
         const int i = row_of(step);
         int2 cur[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) cur[u] = pre[u];
-        if (step + 1 < kRowsPerWave * kRounds) prefetch(row_of(step + 1));  // next row's loads in flight now
+        for (int u = 0; u < 4; ++u) cur[u] = pre[0][u];
+#pragma unroll
+        for (int a = 0; a + 1 < kAhead; ++a)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) pre[a][u] = pre[a + 1][u];
+        if (step + kAhead < kSteps) prefetch(row_of(step + kAhead), pre[kAhead - 1]);
         const RowMeta m = uniform_meta(meta[i]);
         if (m.flag == 0) {  // wave-uniform: scalar branch
             const int r = row0 + i;
@@ -714,19 +769,21 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
                     for (int q = lane; q <= sn; q += 64) diff[lp(q, sh)] = g[base + q] + (q == 0 ? carry : 0);
                 } else if (m.fast && whole) {
                     const uint32_t n = fast_candidates(m);
+                    // batch q0 + 256 is loaded while batch q0 is added
+                    for (uint32_t q0 = 0; q0 < n; q0 += 256) {
+                        int2 nx[4];
+                        if (q0 + 256 < n) {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (lane + 64u * u < n) add_read_fast(m, cur[u], diff, sh);
-                    for (uint32_t q0 = 256; q0 < n; q0 += 256) {
-                        int2 rd[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const uint32_t q = q0 + lane + 64 * u;
-                            rd[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+                            for (int u = 0; u < 4; ++u) {
+                                const uint32_t q = q0 + 256 + lane + 64 * u;
+                                nx[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+                            }
                         }
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            if (q0 + lane + 64u * u < n) add_read_fast(m, rd[u], diff, sh);
+                            if (q0 + lane + 64u * u < n) add_read_fast(m, cur[u], diff, sh);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) cur[u] = nx[u];
                     }
                 } else {
                     pileup_row(P, r, m.P0 + s0, sn, diff, lane, 64, sh);
@@ -804,7 +861,7 @@ __global__ void __launch_bounds__(kBlock) rcp_pileup_kernel(RcpPlanDev P, double
             const int32_t flag = mr.flag, kend = mr.kend, bs = mr.bs, lay = mr.lay;
             if (r < P.n_rows && flag != 2) {
                 const size_t R = (size_t)P.n_rows;
-                const int kstep = kBlock / T;
+                const int kstep = kPBlock / T;
                 int32_t k = k0 + tid / T;
                 size_t o = (size_t)(part.col_off + k) * R + (size_t)r;
                 const size_t ostep = (size_t)kstep * R;
@@ -1101,7 +1158,7 @@ extern "C" hipError_t rcp_launch_heavy_clear(const RcpPlanDev* P, hipStream_t st
 
 extern "C" size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr) {
     const size_t stage_words = csr ? 0 : (size_t)P->stage_cap * (kTile + 1);
-    return 4 * ((size_t)kWaves * (P->wave_words + 8) + stage_words + (size_t)kRows * kMetaWords + 8);
+    return 4 * ((size_t)kPWaves * (P->wave_words + 8) + stage_words + (size_t)kRows * kMetaWords + 8);
 }
 
 extern "C" int rcp_tile_rows(void) { return kRows; }
@@ -1116,7 +1173,7 @@ static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* bin
     }
     const int tiles = (P->n_rows + kRows - 1) / kRows;
     const int64_t grid = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
-    hipLaunchKernelGGL((rcp_pileup_kernel<MEDIAN, CSR>), dim3((unsigned)grid), dim3(kBlock), lds, s, *P, out, binsum);
+    hipLaunchKernelGGL((rcp_pileup_kernel<MEDIAN, CSR>), dim3((unsigned)grid), dim3(kPBlock), lds, s, *P, out, binsum);
     return hipGetLastError();
 }
 
@@ -1163,6 +1220,23 @@ extern "C" hipError_t rcp_launch_streams(int64_t n, const uint64_t* keys, const 
     const int64_t grid = (n + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(rcp_stream_bounds_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, keys, off);
     hipLaunchKernelGGL(rcp_pack_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, keys, vals, se, scan_in);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t* off, const int32_t* pmax,
+                                               int32_t* out, hipStream_t stream) {
+    if (n_streams == 0) return hipSuccess;
+    hipLaunchKernelGGL(rcp_stream_maxend_kernel, dim3((unsigned)((n_streams + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       stream, n_streams, off, pmax, out);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const int64_t* dir_off, const int64_t* off,
+                                     const int32_t* pmax, const int2* se, int shift, int32_t* dir_l, int32_t* dir_u,
+                                     hipStream_t stream) {
+    if (n_entries == 0) return hipSuccess;
+    hipLaunchKernelGGL(rcp_dir_kernel, dim3((unsigned)((n_entries + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                       n_entries, n_streams, dir_off, off, pmax, se, shift, dir_l, dir_u);
     return hipGetLastError();
 }
 

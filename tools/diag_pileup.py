@@ -49,6 +49,12 @@ def run(name, check_heavy=False, **kw):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "volume":
+        run("c4 default (skewed, 92M ovl)")
+        run("c4 no reads", n_reads=1000)
+        run("c4 uniform 200M reads", enriched=0.0)
+        run("c4 uniform 600M reads", enriched=0.0, n_reads=600_000_000)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "quick":
         run("c4 default")
         run("c4 uniform reads only", enriched=0.0)

@@ -39,6 +39,8 @@ struct RcpRowRec {
 };
 #define RCP_REC_VALID 1
 #define RCP_REC_FAST 2
+#define RCP_REC_CRANGE 4  // crange holds this row's per-chunk read ranges
+#define RCP_MAX_CRANGE_CHUNKS 8
 
 struct RcpPart {
     // slice [lo, hi) of the row (0-based): lo = (lo_end ? nr : 0) + lo_off, same for hi
@@ -107,6 +109,9 @@ struct RcpPlanDev {
     // first by many workgroups (heavy slices) into a global difference array
     uint32_t* ncand;            // [n_rows] candidate reads (locate output)
     RcpRowRec* rec;             // [n_rows] (locate output)
+    // candidate reads of each (row, column chunk) of a single-range row, per strand stream:
+    // [crange[((r * n_chunks_total + c) * 3 + s)].x, .y)  (locate output; null = not kept)
+    uint2* crange;
     int32_t heavy_threshold;    // 0 = heavy path off
     int32_t heavy_cap;          // slots
     int32_t heavy_stride;       // ints per slot (>= max row length + 1 of eligible rows)

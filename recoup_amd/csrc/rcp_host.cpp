@@ -56,8 +56,11 @@ constexpr int kWaveMax = 4096;         // positions per wave sub-chunk (padded L
 #endif
 constexpr int kStageMaxBins = RCP_STAGE_MAX_BINS;  // bins per chunk (LDS stage = bins x 17 words)
 constexpr size_t kLdsBudget = 80 * 1024;  // keep two pileup workgroups per CU when possible
-constexpr int kHeavyThreshold = 8192;  // candidate reads above which a row is split across workgroups
-constexpr int kHeavySlice = 16384;     // candidate reads per heavy work item
+constexpr int kHeavyThreshold = 4096;  // candidate reads above which a row is split across workgroups
+#ifndef RCP_HEAVY_SLICE
+#define RCP_HEAVY_SLICE 4096
+#endif
+constexpr int kHeavySlice = RCP_HEAVY_SLICE;  // candidate reads per heavy work item
 constexpr int kHeavyMaxLen = 16383;    // longer rows never take the heavy path
 constexpr int kHeavyGrid = 1024;
 
@@ -670,7 +673,9 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     const size_t w_hoff = al(w_hrows + 4 * (size_t)P.heavy_cap);
     const size_t w_gdiff = al(w_hoff + 4 * ((size_t)P.heavy_cap + 1));
     const size_t w_rec = al(w_gdiff + (P.heavy_threshold > 0 ? 4 * (size_t)P.heavy_cap * P.heavy_stride : 0));
-    const size_t w_status = al(w_rec + sizeof(RcpRowRec) * Rw);
+    const bool keep_crange = P.n_chunks_total > 1 && P.n_chunks_total <= RCP_MAX_CRANGE_CHUNKS;
+    const size_t w_crange = al(w_rec + sizeof(RcpRowRec) * Rw);
+    const size_t w_status = al(w_crange + (keep_crange ? sizeof(uint2) * 3 * (size_t)P.n_chunks_total * Rw : 0));
     HIP_TRY(plan->work.alloc(w_status + 256));
     char* wb = plan->work.as<char>();
     P.ncand = reinterpret_cast<uint32_t*>(wb + w_ncand);
@@ -679,6 +684,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.heavy_slice_off = reinterpret_cast<uint32_t*>(wb + w_hoff);
     P.heavy_gdiff = reinterpret_cast<int32_t*>(wb + w_gdiff);
     P.rec = reinterpret_cast<RcpRowRec*>(wb + w_rec);
+    P.crange = keep_crange ? reinterpret_cast<uint2*>(wb + w_crange) : nullptr;
     const int32_t n_interp = (int32_t)B.interp_row.size();
     P.interp_stride = 2 * (max_interp_bins + 1) + 3 * (max_interp_len + 1) + 8;
     if (n_interp) HIP_TRY(plan->scratch.alloc(8 * (size_t)n_interp * P.interp_stride));
@@ -842,6 +848,7 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
     pt.chunk_bins = std::max<int32_t>(std::min(P.chunk_cap, pt.n_bins), 1);
     pt.n_chunks = (pt.n_bins + pt.chunk_bins - 1) / pt.chunk_bins;
     P.n_chunks_total = pt.n_chunks;
+    P.crange = nullptr;  // sized for the plan's chunks, not these
     DevBuf d_off;
     HIP_TRY(d_off.alloc(8 * (plan->n_rows + 1)));
     HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * (plan->n_rows + 1), hipMemcpyHostToDevice, s));

@@ -226,25 +226,6 @@ __device__ __forceinline__ uint32_t kth_smallest(const int32_t* d, int32_t a, in
     return (uint32_t)lo;
 }
 
-// Candidate read `q` (0-based over the row's (segment, stream) ranges in order) -> the
-// segment and read index.  Returns false past the end.
-__device__ __forceinline__ bool nth_candidate(const RcpPlanDev& P, int r, uint32_t q, int* seg, uint32_t* idx) {
-    const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
-    for (int j = j0; j < j1; ++j) {
-        for (int s = 0; s < 3; ++s) {
-            const uint32_t lo = P.seg_lo[j * 3 + s], hi = P.seg_hi[j * 3 + s];
-            const uint32_t c = hi > lo ? hi - lo : 0;
-            if (q < c) {
-                *seg = j;
-                *idx = lo + q;
-                return true;
-            }
-            q -= c;
-        }
-    }
-    return false;
-}
-
 }  // namespace
 
 // =================================================================================
@@ -346,35 +327,79 @@ __global__ void rcp_dir_kernel(int64_t n_entries, int64_t n_streams, const int64
 // =================================================================================
 // locate: per (row, segment, stream) read ranges, the NULL rules, heavy-row slots
 // =================================================================================
+// Row positions [*p0, *p0 + *np) that column chunk (part, first bin k0) piles up for a
+// valid row of nominal length nr, mirroring the pileup kernel's metadata stage; false when
+// that stage would not pile the chunk (interpolated, wide median, width mismatch, empty).
+__device__ __forceinline__ bool chunk_window(const RcpPlanDev& P, const RcpPart& part, int32_t k0, int32_t nr,
+                                             int32_t* p0, int32_t* np) {
+    int32_t head, L;
+    rcp_part_slice(part, nr, &head, &L);
+    const int32_t n = part.n_bins;
+    if (k0 >= n) return false;
+    if (part.per_base ? L != n : L < n) return false;
+    const int32_t kend = min(k0 + part.chunk_bins, n);
+    int32_t bs = 1, lay = -1;
+    if (!part.per_base) {
+        bs = L / n;
+        const int32_t dif = L - bs * n;
+        if (dif) lay = max(P.lay_index[part.lay_base + dif], -1);
+    }
+    if (P.stat == 1 && bs + (lay >= 0 ? 1 : 0) > P.chunk_cap) return false;
+    const int32_t e0 = bs * k0 + (lay >= 0 ? P.lay_cnt[lay + k0] : 0);
+    const int32_t e1 = bs * kend + (lay >= 0 ? P.lay_cnt[lay + kend] : 0);
+    *p0 = head + e0;
+    *np = e1 - e0;
+    return true;
+}
+
+// DPP quad permutations (lanes 4k .. 4k+3): xor 1, xor 2, broadcast lane 1 / lane 2
+template <int CTRL>
+__device__ __forceinline__ int qperm(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false); }
+
+// Four lanes per row: lane q < 3 searches read stream q (+, -, *) for every segment of the
+// row, lane 3 idles; the quad then combines hits / max ends / candidate counts.  Searches of
+// one row run in parallel instead of one after another.
 __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P.n_rows) return;
-    const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
-    const int32_t chrom = P.row_chrom[r];
-    const bool ok = !P.row_static[r] && chrom >= 0 && chrom < P.n_chrom && j1 > j0;
-    bool hit[4] = {false, false, false, false};
-    bool present[4] = {false, false, false, false};
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = t >> 2;
+    const int s = t & 3;
+    const bool in_row = r < P.n_rows;
+    int j0 = 0, j1 = 0;
+    int32_t chrom = -1;
+    bool ok = false;
+    if (in_row) {
+        j0 = P.row_seg[r];
+        j1 = P.row_seg[r + 1];
+        chrom = P.row_chrom[r];
+        ok = !P.row_static[r] && chrom >= 0 && chrom < P.n_chrom && j1 > j0;
+    }
+    uint32_t hit = 0, present = 0;  // bit g: group g
     int32_t maxend[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
     int32_t maxpos[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
-    uint32_t ncand = 0;
+    uint32_t ncand = 0, lo = 0, hi = 0;
+    int64_t d0 = 0;
+    int32_t nb = 1;
+    if (ok && s < 3) {
+        d0 = P.dir_off[chrom * 3 + s];
+        nb = (int32_t)(P.dir_off[chrom * 3 + s + 1] - d0) - 1;
+    }
     for (int j = j0; j < j1; ++j) {
         const RcpSeg sg = P.segs[j];
         const int g = sg.group & 3;
-        present[g] = true;
+        present |= 1u << g;
         maxpos[g] = max(maxpos[g], sg.hi);
-        for (int s = 0; s < 3; ++s) {
-            uint32_t lo = 0, hi = 0;
+        lo = 0;
+        hi = 0;
+        if (s < 3) {
             if (ok && sg.query_ok && ((sg.streams >> s) & 1)) {
                 // bucket directory: both searches start inside one bucket's reads
-                const int64_t d0 = P.dir_off[chrom * 3 + s];
-                const int32_t nb = (int32_t)(P.dir_off[chrom * 3 + s + 1] - d0) - 1;
                 const int32_t bl = min(max(sg.lo, 0) >> P.dir_shift, nb - 1);
                 const int32_t bh = min(max(sg.hi, 0) >> P.dir_shift, nb - 1);
                 lo = lower_bound_pmax(P.pmax, (uint32_t)P.dir_l[d0 + bl], (uint32_t)P.dir_l[d0 + bl + 1], sg.lo);
                 hi = upper_bound_start(P.se, max(lo, (uint32_t)P.dir_u[d0 + bh]),
                                        max(lo, (uint32_t)P.dir_u[d0 + bh + 1]), sg.hi);
                 if (lo < hi) {
-                    hit[g] = true;
+                    hit |= 1u << g;
                     maxend[g] = max(maxend[g], P.pmax[hi - 1]);
                     ncand += hi - lo;
                 }
@@ -383,44 +408,103 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
             P.seg_hi[j * 3 + s] = hi;
         }
     }
+    // ---- combine the quad (all lanes active: DPP reads neighbours)
+    hit |= (uint32_t)qperm<0xB1>((int)hit);
+    hit |= (uint32_t)qperm<0x4E>((int)hit);
+    ncand += (uint32_t)qperm<0xB1>((int)ncand);
+    ncand += (uint32_t)qperm<0x4E>((int)ncand);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        maxend[g] = max(maxend[g], qperm<0xB1>(maxend[g]));
+        maxend[g] = max(maxend[g], qperm<0x4E>(maxend[g]));
+    }
+    // the single range of a fast row: lo / hi of streams 1 and 2 from lanes 1 and 2
+    const uint32_t lo1 = (uint32_t)qperm<0x55>((int)lo), hi1 = (uint32_t)qperm<0x55>((int)hi);
+    const uint32_t lo2 = (uint32_t)qperm<0xAA>((int)lo), hi2 = (uint32_t)qperm<0xAA>((int)hi);
     bool valid = ok;
     if (ok) {
         const int64_t sl = P.seqlen[chrom];
         for (int g = 0; g < 4; ++g) {
-            if (!present[g]) continue;
+            if (!((present >> g) & 1)) continue;
             // no hits -> NULL (coverage.R:224-225); Rle[i2k] beyond the Rle -> error -> NULL
             // (coverage.R:217-222): the Rle spans seqlength, or the hits' max end when NA.
-            valid = valid && hit[g] && (sl >= 0 ? (int64_t)maxpos[g] <= sl : maxpos[g] <= maxend[g]);
+            valid = valid && ((hit >> g) & 1) && (sl >= 0 ? (int64_t)maxpos[g] <= sl : maxpos[g] <= maxend[g]);
         }
     }
-    P.valid[r] = valid ? 1 : 0;
-    P.ncand[r] = ncand;
     int32_t slot = -1;
-    if (valid && P.heavy_threshold > 0 && ncand > (uint32_t)P.heavy_threshold && P.row_len[r] <= P.heavy_max_len) {
-        const uint32_t s = atomicAdd(&P.status[1], 1u);
-        if (s < (uint32_t)P.heavy_cap) {
-            slot = (int32_t)s;
-            P.heavy_rows[s] = r;
+    if (in_row && s == 0) {
+        P.valid[r] = valid ? 1 : 0;
+        P.ncand[r] = ncand;
+        if (valid && P.heavy_threshold > 0 && ncand > (uint32_t)P.heavy_threshold &&
+            P.row_len[r] <= P.heavy_max_len) {
+            const uint32_t q = atomicAdd(&P.status[1], 1u);
+            if (q < (uint32_t)P.heavy_cap) {
+                slot = (int32_t)q;
+                P.heavy_rows[q] = r;
+            }
+        }
+        P.heavy_slot[r] = slot;
+    }
+    slot = qperm<0x00>(slot);
+    // per-chunk candidate ranges of a single-range row: each column chunk streams only the
+    // reads that reach its piece of the row (lane s < 3: stream s)
+    RcpSeg sg0{};
+    bool fast = false;
+    if (in_row && j1 == j0 + 1) {
+        sg0 = P.segs[j0];
+        fast = !sg0.multi && sg0.query_ok;
+    }
+    const bool cr = P.crange != nullptr && fast && valid && slot < 0;
+    if (cr && s < 3) {
+        const int32_t nr = P.row_len[r];
+        const int32_t len = sg0.hi - sg0.lo + 1;
+        int p = 0, cp = 0;
+        for (int c = 0; c < P.n_chunks_total; ++c, ++cp) {
+            while (p < P.n_parts - 1 && cp >= P.part[p].n_chunks) {
+                cp -= P.part[p].n_chunks;
+                ++p;
+            }
+            uint32_t clo = lo, chi = hi;
+            int32_t p0, np;
+            if (lo < hi && chunk_window(P, P.part[p], cp * P.part[p].chunk_bins, nr, &p0, &np)) {
+                const int32_t a = max(p0, sg0.off), b = min(p0 + np, sg0.off + len);
+                if (a >= b) {
+                    chi = clo;
+                } else if (!(a == sg0.off && b == sg0.off + len)) {
+                    int32_t gps, gpe;
+                    if (!sg0.rev) {
+                        gps = sg0.lo + (a - sg0.off);
+                        gpe = sg0.lo + (b - 1 - sg0.off);
+                    } else {
+                        gpe = sg0.hi - (a - sg0.off);
+                        gps = sg0.hi - (b - 1 - sg0.off);
+                    }
+                    // a piece that starts (ends) with the row's range keeps its lo (hi)
+                    if (gps > sg0.lo) clo = lower_bound_pmax(P.pmax, lo, hi, gps);
+                    if (gpe < sg0.hi) chi = upper_bound_start(P.se, clo, hi, gpe);
+                    chi = max(clo, chi);
+                }
+            }
+            P.crange[((size_t)r * P.n_chunks_total + c) * 3 + s] = make_uint2(clo, chi);
         }
     }
-    P.heavy_slot[r] = slot;
+    if (!in_row || s != 0) return;
     // one record per row for the pileup kernel's metadata stage
     RcpRowRec rec;
     rec.flags = valid ? RCP_REC_VALID : 0;
     rec.row_len = P.row_len[r];
     rec.heavy = slot;
     rec.off = rec.slo = rec.shi = rec.rev = 0;
-    for (int s = 0; s < 3; ++s) rec.lo[s] = rec.hi[s] = 0;
+    for (int q = 0; q < 3; ++q) rec.lo[q] = rec.hi[q] = 0;
     rec.pad[0] = rec.pad[1] = rec.pad[2] = 0;
-    if (j1 == j0 + 1) {
-        const RcpSeg sg = P.segs[j0];
-        if (!sg.multi && sg.query_ok) {
-            rec.flags |= RCP_REC_FAST;
+    if (fast) {
+        const RcpSeg& sg = sg0;
+        {
+            rec.flags |= RCP_REC_FAST | (cr ? RCP_REC_CRANGE : 0);
             rec.off = sg.off; rec.slo = sg.lo; rec.shi = sg.hi; rec.rev = sg.rev;
-            for (int s = 0; s < 3; ++s) {
-                rec.lo[s] = P.seg_lo[j0 * 3 + s];
-                rec.hi[s] = P.seg_hi[j0 * 3 + s];
-            }
+            rec.lo[0] = lo; rec.hi[0] = hi;
+            rec.lo[1] = lo1; rec.hi[1] = hi1;
+            rec.lo[2] = lo2; rec.hi[2] = hi2;
         }
     }
     const uint4* src = reinterpret_cast<const uint4*>(&rec);
@@ -475,12 +559,29 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) 
         const uint32_t q1 = min(q0 + (uint32_t)P.heavy_slice, P.ncand[r]);
         for (int q = threadIdx.x; q <= nr; q += kBlock) diff[q] = 0;
         __syncthreads();
-        for (uint32_t q = q0 + threadIdx.x; q < q1; q += kBlock) {
-            int j;
-            uint32_t idx;
-            if (!nth_candidate(P, r, q, &j, &idx)) break;
+        // walk the row's (segment, stream) read ranges in candidate order; the slice's part
+        // of each range is streamed with 4 loads in flight per thread
+        const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
+        uint32_t base = 0;
+        for (int j = j0; j < j1 && base < q1; ++j) {
             const RcpSeg sg = P.segs[j];
-            add_read(P, sg, P.se[idx], sg.lo, sg.hi, 0, diff, 30);
+            for (int s = 0; s < 3 && base < q1; ++s) {
+                const uint32_t lo = P.seg_lo[j * 3 + s], hi = P.seg_hi[j * 3 + s];
+                const uint32_t c = hi > lo ? hi - lo : 0;
+                const uint32_t a = max(q0, base), b = min(q1, base + c);
+                if (a < b) {
+                    const uint32_t i0 = lo + (a - base), i1 = lo + (b - base);
+                    for (uint32_t i = i0 + threadIdx.x; i < i1; i += 4 * kBlock) {
+                        int2 rd[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) rd[u] = P.se[min(i + u * kBlock, i1 - 1)];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (i + u * kBlock < i1) add_read(P, sg, rd[u], sg.lo, sg.hi, 0, diff, 30);
+                    }
+                }
+                base += c;
+            }
         }
         __syncthreads();
         int32_t* g = P.heavy_gdiff + (size_t)slot * P.heavy_stride;
@@ -585,6 +686,68 @@ __device__ __forceinline__ void lds_order() {
     asm volatile("" ::: "memory");
 }
 
+// Words per stage row: >= cap and = 4 (mod 8), so a row's bins are consecutive (b128
+// writes stay aligned) and 16 rows x 4 consecutive columns fall in 64 distinct banks.
+__host__ __device__ __forceinline__ int stage_stride(int cap) { return ((cap + 3) >> 3 << 3) + 4; }
+
+// Fused pass for uniform bins of 2^lbs positions with 2^lbs <= PER (every bin inside one
+// lane's positions): read the lane's PER differences once, zero them for the next row, turn
+// them into depth with one wave scan and write the lane's bin sums straight to the stage row.
+// Replaces zeroing + two scan passes + the bin reads of the general path.
+template <int PER>
+__device__ __forceinline__ void scan_bins_fast(int32_t* diff, int lbs, uint32_t* srow, int32_t nbins) {
+    const int lane = threadIdx.x & 63;
+    uint4* base = reinterpret_cast<uint4*>(diff + lane * (PER + 4));
+    uint32_t v[PER];
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+        const uint4 x = base[q];
+        v[4 * q] = x.x;
+        v[4 * q + 1] = x.y;
+        v[4 * q + 2] = x.z;
+        v[4 * q + 3] = x.w;
+    }
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) base[q] = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t A = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) A += v[j];
+    uint32_t d = wave_exclusive_scan(A);  // depth entering this lane
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        d += v[j];
+        v[j] = d;
+    }
+    // bin sums by pairwise levels (uniform branches; register indices stay static)
+#pragma unroll
+    for (int L = 1; (1 << L) <= PER; ++L) {
+        if (L <= lbs) {
+#pragma unroll
+            for (int i = 0; i < (PER >> L); ++i) v[i] = v[2 * i] + v[2 * i + 1];
+        }
+    }
+    const int nb = PER >> lbs;
+    const int b0 = lane * nb;
+    if (nb >= 4) {
+#pragma unroll
+        for (int m = 0; m < PER; m += 4) {
+            if (m < nb) {
+                if (b0 + m + 3 < nbins) {
+                    *reinterpret_cast<uint4*>(srow + b0 + m) = make_uint4(v[m], v[m + 1], v[m + 2], v[m + 3]);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (b0 + m + u < nbins) srow[b0 + m + u] = v[m + u];
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if (m < nb && b0 + m < nbins) srow[b0 + m] = v[m];
+    }
+}
+
 template <bool MEDIAN, bool CSR>
 __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
                                                             int64_t* __restrict__ binsum) {
@@ -600,6 +763,7 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
     const int grp = blockIdx.x / (8 * P.n_chunks_total);
     const int wg = blockIdx.x - grp * 8 * P.n_chunks_total;
     int c = wg >> 3;
+    const int cidx = c;  // column chunk over all parts
     const int blk = grp * 8 + (wg & 7);
     if (blk * kRows >= P.n_rows) return;
     int p = 0;
@@ -612,11 +776,11 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
     const int row0 = blk * kRows;
 
     // per wave: 8 zero words (so cum[lp(-1)] == 0) then the padded difference / depth /
-    // cumulative array; the stage is [bin][T + 1] (odd row stride: conflict-free writes)
-    constexpr int TS = T + 1;
+    // cumulative array; the stage is [row][RS] (stage_stride)
+    const int RS = stage_stride(P.stage_cap);
     int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * (P.wave_words + 8) + 8;
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * (P.wave_words + 8);
-    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : P.stage_cap * TS));
+    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : T * RS));
 
     // ---- per-row metadata, one thread per row (searches of all rows in flight together)
     // ---- per-row metadata, one thread per row, from the locate kernel's 64-byte records
@@ -690,6 +854,15 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                         // check drops the others; they are L2 hits for the sibling chunks);
                         // only big rows pay the dependent binary searches
                         const bool refine = !full && all > 4096;
+                        if (rec.flags & RCP_REC_CRANGE) {
+                            // exact ranges for this chunk from the locate kernel
+                            const uint2* cr = P.crange + ((size_t)r * P.n_chunks_total + cidx) * 3;
+                            for (int s = 0; s < 3; ++s) {
+                                const uint2 v = cr[s];
+                                m.lo[s] = v.x;
+                                m.hi[s] = v.y;
+                            }
+                        } else
                         for (int s = 0; s < 3; ++s) {
                             uint32_t lo = rec.lo[s], hi = rec.hi[s];
                             if (lo < hi && refine) {
@@ -714,7 +887,11 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
     constexpr int kSteps = kRowsPerWave * kRounds;
     auto prefetch = [&](int i, int2* dst) {
         const RowMeta m = uniform_meta(meta[i]);
+#ifdef RCP_ABL_LOADS
+        const uint32_t n = 0;
+#else
         const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
+#endif
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             // unconditional (clamped) loads: no branch, no early vmcnt wait
@@ -726,6 +903,8 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
 #pragma unroll
     for (int a = 0; a < kAhead; ++a)
         if (a < kSteps) prefetch(row_of(a), pre[a]);
+    bool clean = false;  // this wave's difference array is all zero (layout clean_sh)
+    int clean_sh = -1;
     for (int step = 0; step < kSteps; ++step) {
         const int i = row_of(step);
         int2 cur[4];
@@ -756,8 +935,15 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                 const int need = (sn + 1 + 63) >> 6;
                 const int sh = need <= 4 ? 2 : 32 - __clz(need - 1);
                 const int per = 1 << sh;
-                int4* d4 = reinterpret_cast<int4*>(diff);
-                for (int q = lane - 2; q < (per + 4) * 16; q += 64) d4[q] = make_int4(0, 0, 0, 0);
+                // the fused pass leaves the array zeroed for the next row of the same geometry
+                const bool fast_bins = !MEDIAN && !CSR && whole && lay < 0 && (bs & (bs - 1)) == 0 && bs <= per &&
+                                       per <= 16;
+                if (!(clean && clean_sh == sh)) {
+                    int4* d4 = reinterpret_cast<int4*>(diff);
+                    for (int q = lane - 2; q < (per + 4) * 16; q += 64) d4[q] = make_int4(0, 0, 0, 0);
+                }
+                clean = fast_bins;
+                clean_sh = sh;
                 lds_order();
                 if (m.heavy >= 0) {
                     // skewed row: its difference array was piled up by rcp_heavy_pileup_kernel
@@ -768,7 +954,11 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                     carry = wave_sum(carry);
                     for (int q = lane; q <= sn; q += 64) diff[lp(q, sh)] = g[base + q] + (q == 0 ? carry : 0);
                 } else if (m.fast && whole) {
+#ifdef RCP_ABL_LOADS
+                    const uint32_t n = 0;
+#else
                     const uint32_t n = fast_candidates(m);
+#endif
                     // batch q0 + 256 is loaded while batch q0 is added
                     for (uint32_t q0 = 0; q0 < n; q0 += 256) {
                         int2 nx[4];
@@ -789,6 +979,19 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                     pileup_row(P, r, m.P0 + s0, sn, diff, lane, 64, sh);
                 }
                 lds_order();
+                if (!MEDIAN && !CSR && fast_bins) {
+                    uint32_t* srow = stage + ii * RS;
+                    const int lbs = 31 - __clz(bs);
+#ifdef RCP_ABL_SCAN
+                    if (lane == 0) srow[0] = (uint32_t)lbs;
+                    continue;
+#endif
+                    if (sh == 2) scan_bins_fast<4>(diff, lbs, srow, kend - k0);
+                    else if (sh == 3) scan_bins_fast<8>(diff, lbs, srow, kend - k0);
+                    else scan_bins_fast<16>(diff, lbs, srow, kend - k0);
+                    lds_order();
+                    continue;
+                }
 #ifndef RCP_ABL_SCAN
                 scan_wave<!(MEDIAN || CSR)>(diff, per);
 #endif
@@ -812,15 +1015,15 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                         uint32_t x2 = x1;
                         if (!(mm & 1))
                             x2 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h + 1, vmin, vmax, sh);
-                        stage[(k - k0) * TS + ii] = x1 + x2;  // 2 x median
+                        stage[ii * RS + (k - k0)] = x1 + x2;  // 2 x median
                     }
                 } else if (whole && lay < 0) {
                     // uniform bins: bin k spans cum positions [a, a + bs), cum[lp(-1)] == 0
                     const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
                     int32_t a = lane * bs;
-                    uint32_t* st = stage + lane * TS + ii;
+                    uint32_t* st = stage + ii * RS + lane;
 #ifndef RCP_ABL_BINS
-                    for (int32_t k = k0 + lane; k < kend; k += 64, a += 64 * bs, st += 64 * TS)
+                    for (int32_t k = k0 + lane; k < kend; k += 64, a += 64 * bs, st += 64)
                         *st = cum[lp(a + bs - 1, sh)] - cum[lp(a - 1, sh)];
 #endif
                 } else if (whole) {
@@ -829,7 +1032,7 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                     for (int32_t k = k0 + lane; k < kend; k += 64) {
                         const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
                         const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
-                        stage[(k - k0) * TS + ii] = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
+                        stage[ii * RS + (k - k0)] = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
                     }
                 } else {
                     // sub-chunk [s0, s0 + sn): add each overlapping bin's partial sum
@@ -837,7 +1040,7 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                     for (int32_t k = k0 + lane; k < kend; k += 64) {
                         const int32_t a = max(bin_edge(bs, lay, P.lay_cnt, k) - e0, s0) - s0;
                         const int32_t b = min(bin_edge(bs, lay, P.lay_cnt, k + 1) - e0, s0 + sn) - s0;
-                        uint32_t* st = stage + (k - k0) * TS + ii;
+                        uint32_t* st = stage + ii * RS + (k - k0);
                         const uint32_t part_sum = a < b ? cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)] : 0u;
                         *st = (s0 == 0 ? 0u : *st) + part_sum;
                     }
@@ -865,7 +1068,7 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                 int32_t k = k0 + tid / T;
                 size_t o = (size_t)(part.col_off + k) * R + (size_t)r;
                 const size_t ostep = (size_t)kstep * R;
-                const uint32_t* st = stage + (tid / T) * TS + ii;
+                const uint32_t* st = stage + ii * RS + tid / T;
                 if (flag == 1) {
                     for (; k < kend; k += kstep, o += ostep) {
                         out[o] = 0.0;
@@ -878,15 +1081,19 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                     const double rd = 1.0 / dd;
                     const bool pow2 = (den & (den - 1)) == 0;
                     const double sc = P.scale;
-                    for (; k < kend; k += kstep, o += ostep, st += kstep * TS) {
+                    for (; k < kend; k += kstep, o += ostep, st += kstep) {
                         const uint32_t num = *st;
                         const double x = (double)num * sc;
+#ifdef RCP_ABL_STORES  // ablation: barriers and stage reads kept, no global stores
+                        asm volatile("" ::"v"(x));
+                        continue;
+#endif
                         out[o] = pow2 ? x * rd : x / dd;
                         if (binsum) binsum[o] = (int64_t)num;
                     }
                 } else {
                     const int32_t* cnt = P.lay_cnt + lay;
-                    for (; k < kend; k += kstep, o += ostep, st += kstep * TS) {
+                    for (; k < kend; k += kstep, o += ostep, st += kstep) {
                         const uint32_t num = *st;
                         const double den = (double)(bs + cnt[k + 1] - cnt[k]);
                         out[o] = ((double)num * P.scale) / den;
@@ -1131,8 +1338,8 @@ hipError_t allow_big_lds(K kernel) {
 
 extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream) {
     if (P->n_rows == 0) return hipSuccess;
-    const int grid = (P->n_rows + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(rcp_locate_kernel, dim3(grid), dim3(kBlock), 0, stream, *P);
+    const int64_t grid = (4 * (int64_t)P->n_rows + kBlock - 1) / kBlock;  // four lanes per row
+    hipLaunchKernelGGL(rcp_locate_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
     return hipGetLastError();
 }
 
@@ -1157,7 +1364,7 @@ extern "C" hipError_t rcp_launch_heavy_clear(const RcpPlanDev* P, hipStream_t st
 }
 
 extern "C" size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr) {
-    const size_t stage_words = csr ? 0 : (size_t)P->stage_cap * (kTile + 1);
+    const size_t stage_words = csr ? 0 : (size_t)kTile * stage_stride(P->stage_cap);
     return 4 * ((size_t)kPWaves * (P->wave_words + 8) + stage_words + (size_t)kRows * kMetaWords + 8);
 }
 

@@ -35,7 +35,7 @@ size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr);
 size_t rcp_interp_lds_bytes(const RcpPlanDev* P);
 int rcp_tile_rows(void);
 hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
-                              const int8_t* strand, int32_t n_chrom, int32_t strand_filter, uint64_t* keys,
+                              const int8_t* strand, int32_t n_chrom, int32_t strand_filter, int merge, uint64_t* keys,
                               int32_t* vals, hipStream_t stream);
 hipError_t rcp_launch_streams(int64_t n, const uint64_t* keys, const int32_t* vals, int64_t* off, int64_t n_off,
                               int2* se, uint64_t* scan_in, hipStream_t stream);
@@ -151,15 +151,25 @@ int check_device(int dev) {
 // =====================================================================================
 // readset
 // =====================================================================================
+// One sorted layout of the reads: streams (chromosome x strand) of start-sorted (start, end)
+// pairs with their prefix max of end and bucket directory (rcp_device.h).  A readset keeps two:
+// `stranded` (stream c*3 + strand, for findOverlaps with strand compatibility) and `merged`
+// (all strands in stream c*3, streams c*3+1, c*3+2 empty: ignore.strand = TRUE, the default),
+// so the default path searches and streams one range per segment instead of three.
+struct ReadLayout {
+    std::vector<int64_t> h_stream_off;  // n_chrom*3 + 1
+    DevBuf se, pmax, stream_off;
+    DevBuf dir_l, dir_u, dir_off;
+    int32_t dir_shift = 12;
+};
+
 struct rcp_readset {
     int device = 0;
     int64_t n = 0;  // reads kept (strand filter applied)
     int32_t n_chrom = 0;
     std::vector<int64_t> seqlen;
-    std::vector<int64_t> h_stream_off;  // n_chrom*3 + 1
-    DevBuf se, pmax, stream_off, d_seqlen;
-    DevBuf dir_l, dir_u, dir_off;  // bucket directory (rcp_device.h)
-    int32_t dir_shift = 12;
+    DevBuf d_seqlen;
+    ReadLayout stranded, merged;
 };
 
 extern "C" const char* rcp_version(void) { return "recoup_amd 0.1.0 (gfx950)"; }
@@ -171,6 +181,99 @@ extern "C" int rcp_device_count(int* n) {
     if (hipGetDeviceCount(n) != hipSuccess) *n = 0;
     return RCP_OK;
 }
+
+namespace {
+
+// Sort the reads into layout L (merge = strands share stream c*3) and build its search index.
+int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, const int32_t* ps, const int32_t* pe,
+                 const int8_t* pst, int merge, ReadLayout* L, hipStream_t s) {
+    const int64_t n = d->n;
+    const int64_t n_streams = (int64_t)d->n_chrom * 3;  // + 1 sentinel stream (dropped reads)
+    DevBuf keys, keys2, vals, vals2, scan_in, scan_out, temp;
+    HIP_TRY(keys.alloc(8 * std::max<int64_t>(n, 1)));
+    HIP_TRY(keys2.alloc(8 * std::max<int64_t>(n, 1)));
+    HIP_TRY(vals.alloc(4 * std::max<int64_t>(n, 1)));
+    HIP_TRY(vals2.alloc(4 * std::max<int64_t>(n, 1)));
+    HIP_TRY(rcp_launch_readset(n, pc, ps, pe, pst, d->n_chrom, d->strand_filter, merge, keys.as<uint64_t>(),
+                               vals.as<int32_t>(), s));
+    int end_bit = 32;
+    while ((int64_t(1) << (end_bit - 32)) <= n_streams) ++end_bit;
+    size_t tb = 0;
+    if (n > 0) {
+        HIP_TRY(rcp_sort_pairs(nullptr, &tb, keys.as<uint64_t>(), keys2.as<uint64_t>(), vals.as<int32_t>(),
+                               vals2.as<int32_t>(), n, end_bit, s));
+        HIP_TRY(temp.alloc(tb));
+        HIP_TRY(rcp_sort_pairs(temp.p, &tb, keys.as<uint64_t>(), keys2.as<uint64_t>(), vals.as<int32_t>(),
+                               vals2.as<int32_t>(), n, end_bit, s));
+    }
+    keys.reset();
+    vals.reset();
+    HIP_TRY(L->stream_off.alloc(8 * (n_streams + 2)));
+    HIP_TRY(L->se.alloc(8 * std::max<int64_t>(n, 1)));
+    HIP_TRY(scan_in.alloc(8 * std::max<int64_t>(n, 1)));
+    HIP_TRY(rcp_launch_streams(n, keys2.as<uint64_t>(), vals2.as<int32_t>(), L->stream_off.as<int64_t>(),
+                               n_streams + 2, L->se.as<int2>(), scan_in.as<uint64_t>(), s));
+    keys2.reset();
+    vals2.reset();
+    HIP_TRY(scan_out.alloc(8 * std::max<int64_t>(n, 1)));
+    if (n > 0) {
+        size_t tb2 = 0;
+        HIP_TRY(rcp_segmax_scan(nullptr, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
+        if (tb2 > temp.bytes) HIP_TRY(temp.alloc(tb2));
+        HIP_TRY(rcp_segmax_scan(temp.p, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
+    }
+    HIP_TRY(L->pmax.alloc(4 * std::max<int64_t>(n, 1)));
+    HIP_TRY(rcp_launch_unpack_pmax(n, scan_out.as<uint64_t>(), L->pmax.as<int32_t>(), s));
+    scan_in.reset();
+    scan_out.reset();
+    temp.reset();
+    L->h_stream_off.resize(n_streams + 2);
+    HIP_TRY(hipMemcpyAsync(L->h_stream_off.data(), L->stream_off.p, 8 * (n_streams + 2), hipMemcpyDeviceToHost, s));
+    // ---- bucket directory: ~32 reads of a stream per bucket on average
+    DevBuf maxend;
+    HIP_TRY(maxend.alloc(4 * std::max<int64_t>(n_streams, 1)));
+    HIP_TRY(rcp_launch_stream_maxend(n_streams, L->stream_off.as<int64_t>(), L->pmax.as<int32_t>(),
+                                     maxend.as<int32_t>(), s));
+    std::vector<int32_t> h_maxend(std::max<int64_t>(n_streams, 1));
+    HIP_TRY(hipMemcpyAsync(h_maxend.data(), maxend.p, 4 * n_streams, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int64_t kept = L->h_stream_off[n_streams];
+    L->h_stream_off.resize(n_streams + 1);
+    std::vector<int64_t> span(d->n_chrom, 0);
+    double genome = 0;
+    for (int c = 0; c < d->n_chrom; ++c) {
+        int64_t m = std::max<int64_t>(rs->seqlen[c], 0);
+        for (int st = 0; st < 3; ++st) m = std::max<int64_t>(m, h_maxend[c * 3 + st]);
+        span[c] = m;
+        genome += (double)m;
+    }
+    const int used = merge ? 1 : 3;  // streams per chromosome that hold reads
+    const double want = kept > 0 ? 32.0 * used * genome / (double)kept : 1e9;
+    int shift = 6;
+    while (shift < 24 && (double)(int64_t(1) << (shift + 1)) <= want) ++shift;
+    L->dir_shift = shift;
+    std::vector<int64_t> doff(n_streams + 1, 0);
+    for (int c = 0; c < d->n_chrom; ++c) {
+        for (int st = 0; st < 3; ++st) {
+            // buckets 0 .. nb-1, entries 0 .. nb (an empty stream gets one bucket)
+            const int64_t nb = (merge && st > 0) ? 1 : (span[c] >> shift) + 1;
+            doff[c * 3 + st + 1] = doff[c * 3 + st] + nb + 1;
+        }
+    }
+    const int64_t ne = doff[n_streams];
+    HIP_TRY(L->dir_off.alloc(8 * (n_streams + 1)));
+    HIP_TRY(L->dir_l.alloc(4 * std::max<int64_t>(ne, 1)));
+    HIP_TRY(L->dir_u.alloc(4 * std::max<int64_t>(ne, 1)));
+    HIP_TRY(hipMemcpyAsync(L->dir_off.p, doff.data(), 8 * (n_streams + 1), hipMemcpyHostToDevice, s));
+    HIP_TRY(rcp_launch_dir(ne, n_streams, L->dir_off.as<int64_t>(), L->stream_off.as<int64_t>(),
+                           L->pmax.as<int32_t>(), L->se.as<int2>(), shift, L->dir_l.as<int32_t>(),
+                           L->dir_u.as<int32_t>(), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    rs->n = kept;
+    return RCP_OK;
+}
+
+}  // namespace
 
 extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp_readset** out) {
     if (!d || !out) return fail(RCP_EINVAL, "NULL argument");
@@ -191,7 +294,6 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     if (d->seqlen)
         for (int c = 0; c < d->n_chrom; ++c) rs->seqlen[c] = d->seqlen[c] < 0 ? -1 : d->seqlen[c];
     const int64_t n = d->n;
-    const int64_t n_streams = (int64_t)d->n_chrom * 3;  // + 1 sentinel stream (dropped reads)
 
     // inputs on device
     DevBuf in_chrom, in_start, in_end, in_strand;
@@ -211,87 +313,13 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
         pe = in_end.as<int32_t>();
         pst = in_strand.as<int8_t>();
     }
-    DevBuf keys, keys2, vals, vals2, scan_in, scan_out, temp;
-    HIP_TRY(keys.alloc(8 * std::max<int64_t>(n, 1)));
-    HIP_TRY(keys2.alloc(8 * std::max<int64_t>(n, 1)));
-    HIP_TRY(vals.alloc(4 * std::max<int64_t>(n, 1)));
-    HIP_TRY(vals2.alloc(4 * std::max<int64_t>(n, 1)));
-    HIP_TRY(rcp_launch_readset(n, pc, ps, pe, pst, d->n_chrom, d->strand_filter, keys.as<uint64_t>(),
-                               vals.as<int32_t>(), s));
-    int end_bit = 32;
-    while ((int64_t(1) << (end_bit - 32)) <= n_streams) ++end_bit;
-    size_t tb = 0;
-    if (n > 0) {
-        HIP_TRY(rcp_sort_pairs(nullptr, &tb, keys.as<uint64_t>(), keys2.as<uint64_t>(), vals.as<int32_t>(),
-                               vals2.as<int32_t>(), n, end_bit, s));
-        HIP_TRY(temp.alloc(tb));
-        HIP_TRY(rcp_sort_pairs(temp.p, &tb, keys.as<uint64_t>(), keys2.as<uint64_t>(), vals.as<int32_t>(),
-                               vals2.as<int32_t>(), n, end_bit, s));
-    }
-    in_chrom.reset();
-    in_start.reset();
-    in_end.reset();
-    in_strand.reset();
-    keys.reset();
-    vals.reset();
-    HIP_TRY(rs->stream_off.alloc(8 * (n_streams + 2)));
-    HIP_TRY(rs->se.alloc(8 * std::max<int64_t>(n, 1)));
-    HIP_TRY(scan_in.alloc(8 * std::max<int64_t>(n, 1)));
-    HIP_TRY(rcp_launch_streams(n, keys2.as<uint64_t>(), vals2.as<int32_t>(), rs->stream_off.as<int64_t>(),
-                               n_streams + 2, rs->se.as<int2>(), scan_in.as<uint64_t>(), s));
-    keys2.reset();
-    vals2.reset();
-    HIP_TRY(scan_out.alloc(8 * std::max<int64_t>(n, 1)));
-    if (n > 0) {
-        size_t tb2 = 0;
-        HIP_TRY(rcp_segmax_scan(nullptr, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
-        if (tb2 > temp.bytes) HIP_TRY(temp.alloc(tb2));
-        HIP_TRY(rcp_segmax_scan(temp.p, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
-    }
-    HIP_TRY(rs->pmax.alloc(4 * std::max<int64_t>(n, 1)));
-    HIP_TRY(rcp_launch_unpack_pmax(n, scan_out.as<uint64_t>(), rs->pmax.as<int32_t>(), s));
-    rs->h_stream_off.resize(n_streams + 2);
-    HIP_TRY(hipMemcpyAsync(rs->h_stream_off.data(), rs->stream_off.p, 8 * (n_streams + 2), hipMemcpyDeviceToHost, s));
+    rc = build_layout(rs.get(), d, pc, ps, pe, pst, 0, &rs->stranded, s);
+    if (rc) return rc;
+    rc = build_layout(rs.get(), d, pc, ps, pe, pst, 1, &rs->merged, s);
+    if (rc) return rc;
     HIP_TRY(rs->d_seqlen.alloc(8 * d->n_chrom));
     HIP_TRY(hipMemcpyAsync(rs->d_seqlen.p, rs->seqlen.data(), 8 * d->n_chrom, hipMemcpyHostToDevice, s));
-    // ---- bucket directory: ~32 reads of a stream per bucket on average
-    DevBuf maxend;
-    HIP_TRY(maxend.alloc(4 * std::max<int64_t>(n_streams, 1)));
-    HIP_TRY(rcp_launch_stream_maxend(n_streams, rs->stream_off.as<int64_t>(), rs->pmax.as<int32_t>(),
-                                     maxend.as<int32_t>(), s));
-    std::vector<int32_t> h_maxend(std::max<int64_t>(n_streams, 1));
-    HIP_TRY(hipMemcpyAsync(h_maxend.data(), maxend.p, 4 * n_streams, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    rs->n = rs->h_stream_off[n_streams];
-    rs->h_stream_off.resize(n_streams + 1);
-    {
-        std::vector<int64_t> span(d->n_chrom, 0);
-        double genome = 0;
-        for (int c = 0; c < d->n_chrom; ++c) {
-            int64_t m = std::max<int64_t>(rs->seqlen[c], 0);
-            for (int st = 0; st < 3; ++st) m = std::max<int64_t>(m, h_maxend[c * 3 + st]);
-            span[c] = m;
-            genome += (double)m;
-        }
-        const double want = rs->n > 0 ? 32.0 * 3.0 * genome / (double)rs->n : 1e9;
-        int shift = 6;
-        while (shift < 24 && (double)(int64_t(1) << (shift + 1)) <= want) ++shift;
-        rs->dir_shift = shift;
-        std::vector<int64_t> doff(n_streams + 1, 0);
-        for (int c = 0; c < d->n_chrom; ++c) {
-            const int64_t nb = (span[c] >> shift) + 1;  // buckets 0 .. nb-1, entries 0 .. nb
-            for (int st = 0; st < 3; ++st) doff[c * 3 + st + 1] = doff[c * 3 + st] + nb + 1;
-        }
-        const int64_t ne = doff[n_streams];
-        HIP_TRY(rs->dir_off.alloc(8 * (n_streams + 1)));
-        HIP_TRY(rs->dir_l.alloc(4 * std::max<int64_t>(ne, 1)));
-        HIP_TRY(rs->dir_u.alloc(4 * std::max<int64_t>(ne, 1)));
-        HIP_TRY(hipMemcpyAsync(rs->dir_off.p, doff.data(), 8 * (n_streams + 1), hipMemcpyHostToDevice, s));
-        HIP_TRY(rcp_launch_dir(ne, n_streams, rs->dir_off.as<int64_t>(), rs->stream_off.as<int64_t>(),
-                               rs->pmax.as<int32_t>(), rs->se.as<int2>(), shift, rs->dir_l.as<int32_t>(),
-                               rs->dir_u.as<int32_t>(), s));
-        HIP_TRY(hipStreamSynchronize(s));
-    }
     *out = rs.release();
     return RCP_OK;
 }
@@ -306,7 +334,7 @@ extern "C" int rcp_readset_destroy(rcp_readset* rs) {
 extern "C" int rcp_readset_info(const rcp_readset* rs, int64_t* n_reads, int64_t* stream_off) {
     if (!rs) return fail(RCP_EINVAL, "NULL readset");
     if (n_reads) *n_reads = rs->n;
-    if (stream_off) std::memcpy(stream_off, rs->h_stream_off.data(), 8 * rs->h_stream_off.size());
+    if (stream_off) std::memcpy(stream_off, rs->stranded.h_stream_off.data(), 8 * rs->stranded.h_stream_off.size());
     return RCP_OK;
 }
 
@@ -341,7 +369,8 @@ struct Builder {
 
 uint8_t stream_mask(int ignore_strand, int8_t q) {
     // findOverlaps strand compatibility: '*' matches everything (Appendix A, Q2)
-    if (ignore_strand || q == RCP_STRAND_ANY) return 0x7;
+    if (ignore_strand) return 0x1;  // the merged layout: every strand in stream 0
+    if (q == RCP_STRAND_ANY) return 0x7;
     return (uint8_t)((1u << q) | (1u << RCP_STRAND_ANY));
 }
 
@@ -689,14 +718,15 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.interp_stride = 2 * (max_interp_bins + 1) + 3 * (max_interp_len + 1) + 8;
     if (n_interp) HIP_TRY(plan->scratch.alloc(8 * (size_t)n_interp * P.interp_stride));
 
-    P.se = rs->se.as<int2>();
-    P.pmax = rs->pmax.as<int32_t>();
-    P.stream_off = rs->stream_off.as<int64_t>();
+    const ReadLayout& RL = rows->ignore_strand ? rs->merged : rs->stranded;
+    P.se = RL.se.as<int2>();
+    P.pmax = RL.pmax.as<int32_t>();
+    P.stream_off = RL.stream_off.as<int64_t>();
     P.seqlen = rs->d_seqlen.as<int64_t>();
-    P.dir_l = rs->dir_l.as<int32_t>();
-    P.dir_u = rs->dir_u.as<int32_t>();
-    P.dir_off = rs->dir_off.as<int64_t>();
-    P.dir_shift = rs->dir_shift;
+    P.dir_l = RL.dir_l.as<int32_t>();
+    P.dir_u = RL.dir_u.as<int32_t>();
+    P.dir_off = RL.dir_off.as<int64_t>();
+    P.dir_shift = RL.dir_shift;
     P.n_chrom = rs->n_chrom;
     P.n_rows = R;
     P.row_chrom = reinterpret_cast<const int32_t*>(base + o_row_chrom);

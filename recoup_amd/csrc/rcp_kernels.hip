@@ -234,7 +234,7 @@ __device__ __forceinline__ uint32_t kth_smallest(const int32_t* d, int32_t a, in
 __global__ void rcp_make_keys_kernel(int64_t n, const int32_t* __restrict__ chrom,
                                      const int32_t* __restrict__ start, const int32_t* __restrict__ end,
                                      const int8_t* __restrict__ strand, int32_t n_chrom, int32_t strand_filter,
-                                     uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+                                     int merge, uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int32_t st = strand[i];
@@ -243,7 +243,7 @@ __global__ void rcp_make_keys_kernel(int64_t n, const int32_t* __restrict__ chro
     if ((strand_filter >= 0 && st != strand_filter) || c < 0 || c >= n_chrom || st < 0 || st > 2)
         sid = (uint32_t)n_chrom * 3u;  // sentinel stream: dropped reads sort last
     else
-        sid = (uint32_t)c * 3u + (uint32_t)st;
+        sid = (uint32_t)c * 3u + (merge ? 0u : (uint32_t)st);
     keys[i] = ((uint64_t)sid << 32) | (uint64_t)((uint32_t)start[i] ^ 0x80000000u);
     vals[i] = end[i];
 }
@@ -1410,12 +1410,12 @@ extern "C" hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStr
 }
 
 extern "C" hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
-                                         const int8_t* strand, int32_t n_chrom, int32_t strand_filter, uint64_t* keys,
-                                         int32_t* vals, hipStream_t stream) {
+                                         const int8_t* strand, int32_t n_chrom, int32_t strand_filter, int merge,
+                                         uint64_t* keys, int32_t* vals, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const int64_t grid = (n + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(rcp_make_keys_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, chrom, start, end,
-                       strand, n_chrom, strand_filter, keys, vals);
+                       strand, n_chrom, strand_filter, merge, keys, vals);
     return hipGetLastError();
 }
 

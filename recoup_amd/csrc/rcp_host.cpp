@@ -55,7 +55,10 @@ constexpr int kWaveMax = 4096;         // positions per wave sub-chunk (padded L
 #define RCP_STAGE_MAX_BINS 512
 #endif
 constexpr int kStageMaxBins = RCP_STAGE_MAX_BINS;  // bins per chunk (LDS stage = bins x 17 words)
-constexpr size_t kLdsBudget = 80 * 1024;  // keep two pileup workgroups per CU when possible
+#ifndef RCP_LDS_BUDGET
+#define RCP_LDS_BUDGET (80 * 1024)
+#endif
+constexpr size_t kLdsBudget = RCP_LDS_BUDGET;  // pileup LDS per workgroup (80 KB: two per CU)
 constexpr int kHeavyThreshold = 4096;  // candidate reads above which a row is split across workgroups
 #ifndef RCP_HEAVY_SLICE
 #define RCP_HEAVY_SLICE 4096

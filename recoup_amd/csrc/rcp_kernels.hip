@@ -628,6 +628,10 @@ constexpr int kRowsPerWave = kTile / kPWaves;  // rows a wave piles per round
 #define RCP_PF_AHEAD 2
 #endif
 constexpr int kAhead = RCP_PF_AHEAD;  // rows whose first reads are prefetched
+#ifndef RCP_STAGE_BUFS
+#define RCP_STAGE_BUFS 1
+#endif
+constexpr int kStageBufs = RCP_STAGE_BUFS;  // 2: double-buffered stage (epilogue overlaps the next round)
 constexpr int kRows = kTile * kRounds;  // rows per workgroup
 
 struct RowMeta {  // [kRows] each, in LDS
@@ -780,7 +784,7 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
     const int RS = stage_stride(P.stage_cap);
     int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * (P.wave_words + 8) + 8;
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * (P.wave_words + 8);
-    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : T * RS));
+    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : kStageBufs * T * RS));
 
     // ---- per-row metadata, one thread per row (searches of all rows in flight together)
     // ---- per-row metadata, one thread per row, from the locate kernel's 64-byte records
@@ -903,6 +907,54 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
 #pragma unroll
     for (int a = 0; a < kAhead; ++a)
         if (a < kSteps) prefetch(row_of(a), pre[a]);
+    // ---- round epilogue: stage row -> out[col * n_rows + row].  Thread t always serves row
+    // t % 16, so 16 consecutive lanes write 16 consecutive rows (128 B) of one column.
+    auto flush = [&](int rd) {
+        const int rbase = rd * T;
+        const int ii = tid & (T - 1);
+        const int r = row0 + rbase + ii;
+        const RowMeta& mr = meta[rbase + ii];
+        const int32_t flag = mr.flag, kend = mr.kend, bs = mr.bs, lay = mr.lay;
+        if (r >= P.n_rows || flag == 2) return;
+        const size_t R = (size_t)P.n_rows;
+        const int kstep = kPBlock / T;
+        int32_t k = k0 + tid / T;
+        size_t o = (size_t)(part.col_off + k) * R + (size_t)r;
+        const size_t ostep = (size_t)kstep * R;
+        const uint32_t* st = stage + (rd % kStageBufs) * T * RS + ii * RS + tid / T;
+        if (flag == 1) {
+            for (; k < kend; k += kstep, o += ostep) {
+                __builtin_nontemporal_store(0.0, out + o);
+                if (binsum) binsum[o] = 0;
+            }
+        } else if (MEDIAN || lay < 0) {
+            // one divisor for the whole row; a power of two divides exactly by its reciprocal
+            const int32_t den = MEDIAN ? 2 : bs;
+            const double dd = (double)den;
+            const double rdd = 1.0 / dd;
+            const bool pow2 = (den & (den - 1)) == 0;
+            const double sc = P.scale;
+            for (; k < kend; k += kstep, o += ostep, st += kstep) {
+                const uint32_t num = *st;
+                const double x = (double)num * sc;
+#ifdef RCP_ABL_STORES  // ablation: barriers and stage reads kept, no global stores
+                asm volatile("" ::"v"(x));
+                continue;
+#endif
+                // write-once output: non-temporal stores keep the reads' lines in L2 / MALL
+                __builtin_nontemporal_store(pow2 ? x * rdd : x / dd, out + o);
+                if (binsum) binsum[o] = (int64_t)num;
+            }
+        } else {
+            const int32_t* cnt = P.lay_cnt + lay;
+            for (; k < kend; k += kstep, o += ostep, st += kstep) {
+                const uint32_t num = *st;
+                const double den = (double)(bs + cnt[k + 1] - cnt[k]);
+                __builtin_nontemporal_store(((double)num * P.scale) / den, out + o);
+                if (binsum) binsum[o] = (int64_t)num;
+            }
+        }
+    };
     bool clean = false;  // this wave's difference array is all zero (layout clean_sh)
     int clean_sh = -1;
     for (int step = 0; step < kSteps; ++step) {
@@ -916,6 +968,7 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
             for (int u = 0; u < 4; ++u) pre[a][u] = pre[a + 1][u];
         if (step + kAhead < kSteps) prefetch(row_of(step + kAhead), pre[kAhead - 1]);
         const RowMeta m = uniform_meta(meta[i]);
+        uint32_t* sbuf = stage + ((step / kRowsPerWave) % kStageBufs) * T * RS;  // this round's stage
         if (m.flag == 0) {  // wave-uniform: scalar branch
             const int r = row0 + i;
             const int32_t npos = m.npos;
@@ -980,7 +1033,7 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                 }
                 lds_order();
                 if (!MEDIAN && !CSR && fast_bins) {
-                    uint32_t* srow = stage + ii * RS;
+                    uint32_t* srow = sbuf + ii * RS;
                     const int lbs = 31 - __clz(bs);
 #ifdef RCP_ABL_SCAN
                     if (lane == 0) srow[0] = (uint32_t)lbs;
@@ -1015,13 +1068,13 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                         uint32_t x2 = x1;
                         if (!(mm & 1))
                             x2 = (vmin == vmax) ? (uint32_t)vmin : kth_smallest(diff, a, b, h + 1, vmin, vmax, sh);
-                        stage[ii * RS + (k - k0)] = x1 + x2;  // 2 x median
+                        sbuf[ii * RS + (k - k0)] = x1 + x2;  // 2 x median
                     }
                 } else if (whole && lay < 0) {
                     // uniform bins: bin k spans cum positions [a, a + bs), cum[lp(-1)] == 0
                     const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
                     int32_t a = lane * bs;
-                    uint32_t* st = stage + ii * RS + lane;
+                    uint32_t* st = sbuf + ii * RS + lane;
 #ifndef RCP_ABL_BINS
                     for (int32_t k = k0 + lane; k < kend; k += 64, a += 64 * bs, st += 64)
                         *st = cum[lp(a + bs - 1, sh)] - cum[lp(a - 1, sh)];
@@ -1032,7 +1085,7 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                     for (int32_t k = k0 + lane; k < kend; k += 64) {
                         const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
                         const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
-                        stage[ii * RS + (k - k0)] = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
+                        sbuf[ii * RS + (k - k0)] = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
                     }
                 } else {
                     // sub-chunk [s0, s0 + sn): add each overlapping bin's partial sum
@@ -1040,7 +1093,7 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
                     for (int32_t k = k0 + lane; k < kend; k += 64) {
                         const int32_t a = max(bin_edge(bs, lay, P.lay_cnt, k) - e0, s0) - s0;
                         const int32_t b = min(bin_edge(bs, lay, P.lay_cnt, k + 1) - e0, s0 + sn) - s0;
-                        uint32_t* st = stage + ii * RS + (k - k0);
+                        uint32_t* st = sbuf + ii * RS + (k - k0);
                         const uint32_t part_sum = a < b ? cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)] : 0u;
                         *st = (s0 == 0 ? 0u : *st) + part_sum;
                     }
@@ -1052,58 +1105,19 @@ __global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, doubl
 #ifdef RCP_ABL_EPI
         continue;
 #endif
-        __syncthreads();
-        // ---- round epilogue: stage[bin][row] -> out[col * n_rows + row].  Thread t always
-        // serves row t % 16 (256 is a multiple of 16), so 16 consecutive lanes write 16
-        // consecutive rows (128 B) of one column.
-        {
-            const int rbase = (step / kRowsPerWave) * T;
-            const int ii = tid & (T - 1);
-            const int r = row0 + rbase + ii;
-            const RowMeta& mr = meta[rbase + ii];
-            const int32_t flag = mr.flag, kend = mr.kend, bs = mr.bs, lay = mr.lay;
-            if (r < P.n_rows && flag != 2) {
-                const size_t R = (size_t)P.n_rows;
-                const int kstep = kPBlock / T;
-                int32_t k = k0 + tid / T;
-                size_t o = (size_t)(part.col_off + k) * R + (size_t)r;
-                const size_t ostep = (size_t)kstep * R;
-                const uint32_t* st = stage + ii * RS + tid / T;
-                if (flag == 1) {
-                    for (; k < kend; k += kstep, o += ostep) {
-                        out[o] = 0.0;
-                        if (binsum) binsum[o] = 0;
-                    }
-                } else if (MEDIAN || lay < 0) {
-                    // one divisor for the whole row; a power of two divides exactly by its reciprocal
-                    const int32_t den = MEDIAN ? 2 : bs;
-                    const double dd = (double)den;
-                    const double rd = 1.0 / dd;
-                    const bool pow2 = (den & (den - 1)) == 0;
-                    const double sc = P.scale;
-                    for (; k < kend; k += kstep, o += ostep, st += kstep) {
-                        const uint32_t num = *st;
-                        const double x = (double)num * sc;
-#ifdef RCP_ABL_STORES  // ablation: barriers and stage reads kept, no global stores
-                        asm volatile("" ::"v"(x));
-                        continue;
-#endif
-                        out[o] = pow2 ? x * rd : x / dd;
-                        if (binsum) binsum[o] = (int64_t)num;
-                    }
-                } else {
-                    const int32_t* cnt = P.lay_cnt + lay;
-                    for (; k < kend; k += kstep, o += ostep, st += kstep) {
-                        const uint32_t num = *st;
-                        const double den = (double)(bs + cnt[k + 1] - cnt[k]);
-                        out[o] = ((double)num * P.scale) / den;
-                        if (binsum) binsum[o] = (int64_t)num;
-                    }
-                }
-            }
+        const int rd = step / kRowsPerWave;
+        if (kStageBufs == 2) {
+            // double-buffered stage: round rd - 1 is written while other waves still pile
+            // round rd; one barrier per round; the last round is written after the loop
+            if (rd > 0) flush(rd - 1);
+            __syncthreads();
+        } else {
+            __syncthreads();
+            flush(rd);
+            __syncthreads();
         }
-        __syncthreads();
     }
+    if (!CSR && kStageBufs == 2) flush(kRounds - 1);
 }
 
 
@@ -1364,7 +1378,7 @@ extern "C" hipError_t rcp_launch_heavy_clear(const RcpPlanDev* P, hipStream_t st
 }
 
 extern "C" size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr) {
-    const size_t stage_words = csr ? 0 : (size_t)kTile * stage_stride(P->stage_cap);
+    const size_t stage_words = csr ? 0 : (size_t)kStageBufs * kTile * stage_stride(P->stage_cap);
     return 4 * ((size_t)kPWaves * (P->wave_words + 8) + stage_words + (size_t)kRows * kMetaWords + 8);
 }
 

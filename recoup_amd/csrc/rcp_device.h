@@ -68,6 +68,7 @@ struct RcpPlanDev {
     const int32_t* dir_u;
     const int64_t* dir_off;    // [n_chrom*3 + 1]
     int32_t dir_shift;
+    int32_t merged;            // 1: the strand-merged layout (all reads in stream chrom*3)
     // rows
     int32_t n_rows;
     const int32_t* row_chrom;   // [n_rows]

@@ -730,6 +730,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.dir_u = RL.dir_u.as<int32_t>();
     P.dir_off = RL.dir_off.as<int64_t>();
     P.dir_shift = RL.dir_shift;
+    P.merged = rows->ignore_strand ? 1 : 0;
     P.n_chrom = rs->n_chrom;
     P.n_rows = R;
     P.row_chrom = reinterpret_cast<const int32_t*>(base + o_row_chrom);

@@ -352,17 +352,38 @@ __device__ __forceinline__ bool chunk_window(const RcpPlanDev& P, const RcpPart&
     return true;
 }
 
-// DPP quad permutations (lanes 4k .. 4k+3): xor 1, xor 2, broadcast lane 1 / lane 2
+// DPP quad permutations (lanes 4k .. 4k+3): 0xB1 xor 1, 0x4E xor 2, 0x00 / 0x55 / 0xAA
+// broadcast lane 0 / 1 / 2
 template <int CTRL>
 __device__ __forceinline__ int qperm(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false); }
 
-// Four lanes per row: lane q < 3 searches read stream q (+, -, *) for every segment of the
-// row, lane 3 idles; the quad then combines hits / max ends / candidate counts.  Searches of
-// one row run in parallel instead of one after another.
+// lower_bound(pmax >= v) / upper_bound(start > v) of stream `st`, each search confined to the
+// reads of v's directory bucket (rcp_device.h)
+__device__ __forceinline__ uint32_t dir_lower(const RcpPlanDev& P, int st, int32_t v) {
+    const int64_t d0 = P.dir_off[st];
+    const int32_t nb = (int32_t)(P.dir_off[st + 1] - d0) - 1;
+    const int32_t b = min(max(v, 0) >> P.dir_shift, nb - 1);
+    return lower_bound_pmax(P.pmax, (uint32_t)P.dir_l[d0 + b], (uint32_t)P.dir_l[d0 + b + 1], v);
+}
+__device__ __forceinline__ uint32_t dir_upper(const RcpPlanDev& P, int st, int32_t v) {
+    const int64_t d0 = P.dir_off[st];
+    const int32_t nb = (int32_t)(P.dir_off[st + 1] - d0) - 1;
+    const int32_t b = min(max(v, 0) >> P.dir_shift, nb - 1);
+    return upper_bound_start(P.se, (uint32_t)P.dir_u[d0 + b], (uint32_t)P.dir_u[d0 + b + 1], v);
+}
+
+// Four lanes per row.  The row's (segment, stream) searches are dealt round-robin to the
+// quad's lanes (one stream per segment in the merged layout, three in the stranded one), so
+// multi-range rows search in parallel; the quad then combines hits / max ends / candidate
+// counts with DPP.  For a single-range row the lanes also split the per-chunk range searches.
+// Every search is bounded by the bucket directory and independent of the others: the
+// dependent chain per lane is one bucket search, not a sequence of them.
 __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
+    __shared__ uint32_t xres[kBlock / 4][2 * RCP_MAX_CRANGE_CHUNKS];  // per quad: chunk bounds
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = t >> 2;
-    const int s = t & 3;
+    const int q = t & 3;
+    uint32_t* xr = xres[threadIdx.x >> 2];
     const bool in_row = r < P.n_rows;
     int j0 = 0, j1 = 0;
     int32_t chrom = -1;
@@ -373,57 +394,58 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
         chrom = P.row_chrom[r];
         ok = !P.row_static[r] && chrom >= 0 && chrom < P.n_chrom && j1 > j0;
     }
+    const int ns = P.merged ? 1 : 3;  // streams searched per segment
+    const int npairs = (j1 - j0) * ns;
     uint32_t hit = 0, present = 0;  // bit g: group g
     int32_t maxend[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
     int32_t maxpos[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
     uint32_t ncand = 0, lo = 0, hi = 0;
-    int64_t d0 = 0;
-    int32_t nb = 1;
-    if (ok && s < 3) {
-        d0 = P.dir_off[chrom * 3 + s];
-        nb = (int32_t)(P.dir_off[chrom * 3 + s + 1] - d0) - 1;
-    }
-    for (int j = j0; j < j1; ++j) {
+    const int64_t sl = ok ? P.seqlen[chrom] : -1;
+    for (int pi = q; pi < npairs; pi += 4) {
+        const int j = j0 + pi / ns;
+        const int s = pi % ns;
         const RcpSeg sg = P.segs[j];
         const int g = sg.group & 3;
         present |= 1u << g;
         maxpos[g] = max(maxpos[g], sg.hi);
         lo = 0;
         hi = 0;
-        if (s < 3) {
-            if (ok && sg.query_ok && ((sg.streams >> s) & 1)) {
-                // bucket directory: both searches start inside one bucket's reads
-                const int32_t bl = min(max(sg.lo, 0) >> P.dir_shift, nb - 1);
-                const int32_t bh = min(max(sg.hi, 0) >> P.dir_shift, nb - 1);
-                lo = lower_bound_pmax(P.pmax, (uint32_t)P.dir_l[d0 + bl], (uint32_t)P.dir_l[d0 + bl + 1], sg.lo);
-                hi = upper_bound_start(P.se, max(lo, (uint32_t)P.dir_u[d0 + bh]),
-                                       max(lo, (uint32_t)P.dir_u[d0 + bh + 1]), sg.hi);
-                if (lo < hi) {
-                    hit |= 1u << g;
-                    maxend[g] = max(maxend[g], P.pmax[hi - 1]);
-                    ncand += hi - lo;
-                }
+        if (ok && sg.query_ok && ((sg.streams >> s) & 1)) {
+            lo = dir_lower(P, chrom * 3 + s, sg.lo);
+            hi = max(lo, dir_upper(P, chrom * 3 + s, sg.hi));
+            if (lo < hi) {
+                hit |= 1u << g;
+                if (sl < 0) maxend[g] = max(maxend[g], P.pmax[hi - 1]);  // only NA seqlengths need it
+                ncand += hi - lo;
             }
-            P.seg_lo[j * 3 + s] = lo;
-            P.seg_hi[j * 3 + s] = hi;
+        }
+        P.seg_lo[j * 3 + s] = lo;
+        P.seg_hi[j * 3 + s] = hi;
+        if (ns == 1) {  // merged layout: streams 1, 2 hold no reads
+            P.seg_lo[j * 3 + 1] = P.seg_hi[j * 3 + 1] = 0;
+            P.seg_lo[j * 3 + 2] = P.seg_hi[j * 3 + 2] = 0;
         }
     }
     // ---- combine the quad (all lanes active: DPP reads neighbours)
     hit |= (uint32_t)qperm<0xB1>((int)hit);
     hit |= (uint32_t)qperm<0x4E>((int)hit);
+    present |= (uint32_t)qperm<0xB1>((int)present);
+    present |= (uint32_t)qperm<0x4E>((int)present);
     ncand += (uint32_t)qperm<0xB1>((int)ncand);
     ncand += (uint32_t)qperm<0x4E>((int)ncand);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
         maxend[g] = max(maxend[g], qperm<0xB1>(maxend[g]));
         maxend[g] = max(maxend[g], qperm<0x4E>(maxend[g]));
+        maxpos[g] = max(maxpos[g], qperm<0xB1>(maxpos[g]));
+        maxpos[g] = max(maxpos[g], qperm<0x4E>(maxpos[g]));
     }
-    // the single range of a fast row: lo / hi of streams 1 and 2 from lanes 1 and 2
+    // the single range of a fast row: (lo, hi) of pairs 0, 1, 2 sit in lanes 0, 1, 2
+    const uint32_t lo0 = (uint32_t)qperm<0x00>((int)lo), hi0 = (uint32_t)qperm<0x00>((int)hi);
     const uint32_t lo1 = (uint32_t)qperm<0x55>((int)lo), hi1 = (uint32_t)qperm<0x55>((int)hi);
     const uint32_t lo2 = (uint32_t)qperm<0xAA>((int)lo), hi2 = (uint32_t)qperm<0xAA>((int)hi);
     bool valid = ok;
     if (ok) {
-        const int64_t sl = P.seqlen[chrom];
         for (int g = 0; g < 4; ++g) {
             if (!((present >> g) & 1)) continue;
             // no hits -> NULL (coverage.R:224-225); Rle[i2k] beyond the Rle -> error -> NULL
@@ -432,22 +454,22 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
         }
     }
     int32_t slot = -1;
-    if (in_row && s == 0) {
+    if (in_row && q == 0) {
         P.valid[r] = valid ? 1 : 0;
         P.ncand[r] = ncand;
         if (valid && P.heavy_threshold > 0 && ncand > (uint32_t)P.heavy_threshold &&
             P.row_len[r] <= P.heavy_max_len) {
-            const uint32_t q = atomicAdd(&P.status[1], 1u);
-            if (q < (uint32_t)P.heavy_cap) {
-                slot = (int32_t)q;
-                P.heavy_rows[q] = r;
+            const uint32_t u = atomicAdd(&P.status[1], 1u);
+            if (u < (uint32_t)P.heavy_cap) {
+                slot = (int32_t)u;
+                P.heavy_rows[u] = r;
             }
         }
         P.heavy_slot[r] = slot;
     }
     slot = qperm<0x00>(slot);
-    // per-chunk candidate ranges of a single-range row: each column chunk streams only the
-    // reads that reach its piece of the row (lane s < 3: stream s)
+    // ---- per-chunk candidate ranges of a single-range row: each column chunk streams only
+    // the reads that reach its piece of the row
     RcpSeg sg0{};
     bool fast = false;
     if (in_row && j1 == j0 + 1) {
@@ -455,54 +477,93 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
         fast = !sg0.multi && sg0.query_ok;
     }
     const bool cr = P.crange != nullptr && fast && valid && slot < 0;
-    if (cr && s < 3) {
-        const int32_t nr = P.row_len[r];
-        const int32_t len = sg0.hi - sg0.lo + 1;
-        int p = 0, cp = 0;
-        for (int c = 0; c < P.n_chunks_total; ++c, ++cp) {
-            while (p < P.n_parts - 1 && cp >= P.part[p].n_chunks) {
-                cp -= P.part[p].n_chunks;
-                ++p;
-            }
-            uint32_t clo = lo, chi = hi;
-            int32_t p0, np;
-            if (lo < hi && chunk_window(P, P.part[p], cp * P.part[p].chunk_bins, nr, &p0, &np)) {
-                const int32_t a = max(p0, sg0.off), b = min(p0 + np, sg0.off + len);
-                if (a >= b) {
+    const int nc = P.n_chunks_total;
+    const int32_t nr = in_row ? P.row_len[r] : 0;
+    const int32_t len = sg0.hi - sg0.lo + 1;
+    // genomic piece of chunk c (false: the chunk streams the whole range / nothing special)
+    auto piece = [&](int c, int32_t* gps, int32_t* gpe, bool* empty) -> bool {
+        int p = 0, cp = c;
+        while (p < P.n_parts - 1 && cp >= P.part[p].n_chunks) {
+            cp -= P.part[p].n_chunks;
+            ++p;
+        }
+        int32_t p0, np;
+        *empty = false;
+        if (!chunk_window(P, P.part[p], cp * P.part[p].chunk_bins, nr, &p0, &np)) return false;
+        const int32_t a = max(p0, sg0.off), b = min(p0 + np, sg0.off + len);
+        if (a >= b) {
+            *empty = true;
+            return false;
+        }
+        if (!sg0.rev) {
+            *gps = sg0.lo + (a - sg0.off);
+            *gpe = sg0.lo + (b - 1 - sg0.off);
+        } else {
+            *gpe = sg0.hi - (a - sg0.off);
+            *gps = sg0.hi - (b - 1 - sg0.off);
+        }
+        return true;
+    };
+    if (cr && ns == 1) {
+        // merged layout: the 2 * nc bound searches are dealt to the four lanes
+        for (int task = q; task < 2 * nc; task += 4) {
+            const int c = task >> 1;
+            int32_t gps = 0, gpe = 0;
+            bool empty;
+            uint32_t v = 0;
+            if (piece(c, &gps, &gpe, &empty))
+                v = (task & 1) ? (gpe < sg0.hi ? dir_upper(P, chrom * 3, gpe) : hi0)
+                               : (gps > sg0.lo ? dir_lower(P, chrom * 3, gps) : lo0);
+            xr[task] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (q == 0) {
+            for (int c = 0; c < nc; ++c) {
+                int32_t gps, gpe;
+                bool empty;
+                uint32_t clo = lo0, chi = hi0;
+                if (piece(c, &gps, &gpe, &empty)) {
+                    clo = xr[2 * c];
+                    chi = max(clo, xr[2 * c + 1]);
+                } else if (empty) {
                     chi = clo;
-                } else if (!(a == sg0.off && b == sg0.off + len)) {
-                    int32_t gps, gpe;
-                    if (!sg0.rev) {
-                        gps = sg0.lo + (a - sg0.off);
-                        gpe = sg0.lo + (b - 1 - sg0.off);
-                    } else {
-                        gpe = sg0.hi - (a - sg0.off);
-                        gps = sg0.hi - (b - 1 - sg0.off);
-                    }
-                    // a piece that starts (ends) with the row's range keeps its lo (hi)
-                    if (gps > sg0.lo) clo = lower_bound_pmax(P.pmax, lo, hi, gps);
-                    if (gpe < sg0.hi) chi = upper_bound_start(P.se, clo, hi, gpe);
-                    chi = max(clo, chi);
                 }
+                P.crange[((size_t)r * nc + c) * 3] = make_uint2(clo, chi);
+                P.crange[((size_t)r * nc + c) * 3 + 1] = make_uint2(0u, 0u);
+                P.crange[((size_t)r * nc + c) * 3 + 2] = make_uint2(0u, 0u);
             }
-            P.crange[((size_t)r * P.n_chunks_total + c) * 3 + s] = make_uint2(clo, chi);
+        }
+    } else if (cr && q < 3) {
+        // stranded layout: lane q refines its own stream's range chunk by chunk
+        for (int c = 0; c < nc; ++c) {
+            int32_t gps, gpe;
+            bool empty;
+            uint32_t clo = lo, chi = hi;
+            if (lo < hi && piece(c, &gps, &gpe, &empty)) {
+                if (gps > sg0.lo) clo = lower_bound_pmax(P.pmax, lo, hi, gps);
+                if (gpe < sg0.hi) chi = upper_bound_start(P.se, clo, hi, gpe);
+                chi = max(clo, chi);
+            } else if (lo < hi && empty) {
+                chi = clo;
+            }
+            P.crange[((size_t)r * nc + c) * 3 + q] = make_uint2(clo, chi);
         }
     }
-    if (!in_row || s != 0) return;
+    if (!in_row || q != 0) return;
     // one record per row for the pileup kernel's metadata stage
     RcpRowRec rec;
     rec.flags = valid ? RCP_REC_VALID : 0;
-    rec.row_len = P.row_len[r];
+    rec.row_len = nr;
     rec.heavy = slot;
     rec.off = rec.slo = rec.shi = rec.rev = 0;
-    for (int q = 0; q < 3; ++q) rec.lo[q] = rec.hi[q] = 0;
+    for (int u = 0; u < 3; ++u) rec.lo[u] = rec.hi[u] = 0;
     rec.pad[0] = rec.pad[1] = rec.pad[2] = 0;
     if (fast) {
-        const RcpSeg& sg = sg0;
-        {
-            rec.flags |= RCP_REC_FAST | (cr ? RCP_REC_CRANGE : 0);
-            rec.off = sg.off; rec.slo = sg.lo; rec.shi = sg.hi; rec.rev = sg.rev;
-            rec.lo[0] = lo; rec.hi[0] = hi;
+        rec.flags |= RCP_REC_FAST | (cr ? RCP_REC_CRANGE : 0);
+        rec.off = sg0.off; rec.slo = sg0.lo; rec.shi = sg0.hi; rec.rev = sg0.rev;
+        rec.lo[0] = lo0; rec.hi[0] = hi0;
+        if (ns == 3) {
             rec.lo[1] = lo1; rec.hi[1] = hi1;
             rec.lo[2] = lo2; rec.hi[2] = hi2;
         }
@@ -510,7 +571,7 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
     const uint4* src = reinterpret_cast<const uint4*>(&rec);
     uint4* dst = reinterpret_cast<uint4*>(P.rec + r);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dst[q] = src[q];
+    for (int u = 0; u < 4; ++u) dst[u] = src[u];
 }
 
 // =================================================================================

@@ -10,6 +10,7 @@
  *   rcp_readset_create   replaces splitBySeqname()            R/util.R:1-13
  *                        (+ the strand filter of calcCoverage R/coverage.R:141-144)
  *   rcp_calc_coverage    replaces calcCoverage()              R/coverage.R:126-174
+ *   rcp_rle_encode       the Rle values / lengths of each coverage (R/coverage.R:171-173)
  *                        and its per-region coverageFromRanges R/coverage.R:176-226
  *   rcp_plan_create /    replace the coverage -> profile pass:
  *   rcp_plan_execute /     coverageFromRanges                 R/coverage.R:176-226
@@ -183,6 +184,16 @@ RCP_API int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, const 
  * orientation (reversed for '-'), i.e. exactly the values of the reference's Rle. */
 RCP_API int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t* d_cov, uint8_t* d_valid,
                       void* hip_stream);
+
+/* Run-length encoding of a CSR coverage (the output of rcp_calc_coverage): the values and
+ * lengths of each row's Rle, as S4Vectors::Rle(values, lengths) holds them
+ * (R/coverage.R:171-173 returns a list of Rle; the R shim rebuilds them without expanding).
+ * out_off: host [n_rows + 1] offsets of d_cov (device int32).  d_values / d_lengths: device
+ * int32 arrays of at least out_off[n_rows] entries.  run_off: host [n_rows + 1] (runs of row r
+ * are run_off[r] .. run_off[r+1]); n_runs: total runs.  Blocks until done. */
+RCP_API int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int32_t* d_cov, int device,
+                           int32_t* d_values, int32_t* d_lengths, int64_t* run_off, int64_t* n_runs,
+                           void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,7 @@ __version__ = "0.1.0"
 
 from .granges import (GRanges, GRangesList, flank, getFlankingRanges, getRegionalRanges,  # noqa: F401
                       promoters, resize)
-from .api import (CoverageList, DeviceCoverage, RMatrix, baseCoverageMatrix, binCoverageMatrix,  # noqa: F401
-                  calcCoverage, calcLinearFactors, coverageRef, coverageRnaRef, normalizeLinear, profileMatrix)
+from .api import (CoverageList, DeviceCoverage, RMatrix, Rle, baseCoverageMatrix, binCoverageMatrix,  # noqa: F401
+                  calcCoverage, calcLinearFactors, coverageRef, coverageRnaRef, normalizeLinear, profileMatrix,
+                  recoupProfiles)
 from ._lib import RcpError, SemanticError, UnsupportedError  # noqa: F401

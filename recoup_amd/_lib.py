@@ -83,6 +83,7 @@ SIGNATURES = [
     ("rcp_plan_row_lengths", ctypes.c_int, [_vp, _i64p]),
     ("rcp_profile", ctypes.c_int, [_vp, ctypes.POINTER(RowsDesc), ctypes.POINTER(BinsDesc), _dp, _u8p]),
     ("rcp_calc_coverage", ctypes.c_int, [_vp, _i64p, _vp, _vp, _vp]),
+    ("rcp_rle_encode", ctypes.c_int, [ctypes.c_int32, _i64p, _vp, ctypes.c_int, _vp, _vp, _i64p, _i64p, _vp]),
 ]
 
 _LIB = None

@@ -51,6 +51,25 @@ class CoverageList(list):
         return np.array([0 if x is None else len(x) for x in self], dtype=np.int64)
 
 
+class Rle:
+    """A run-length encoded integer vector (S4Vectors::Rle): ``values`` repeated ``lengths`` times."""
+
+    __slots__ = ("values", "lengths")
+
+    def __init__(self, values, lengths):
+        self.values = np.asarray(values)
+        self.lengths = np.asarray(lengths)
+
+    def __len__(self):
+        return int(self.lengths.sum())
+
+    def decode(self):
+        return np.repeat(self.values, self.lengths)
+
+    def __repr__(self):
+        return f"Rle({len(self)} positions in {len(self.values)} runs)"
+
+
 class RMatrix(np.ndarray):
     """A numpy matrix that carries R's rownames (region names)."""
 
@@ -155,10 +174,13 @@ class DeviceCoverage:
         v = self.valid()
         return np.where(v, self._len, 0)
 
-    def to_list(self):
-        """Materialise the per-region coverage vectors (calcCoverage's return value)."""
-        cov = self._plan().coverage()
-        if self.scale != 1.0:
+    def to_list(self, rle=False):
+        """Materialise the per-region coverage vectors (calcCoverage's return value); with
+        ``rle`` as ``Rle`` objects run-length encoded on the GPU."""
+        cov = self._plan().coverage(rle=rle)
+        if rle:
+            cov = [None if x is None else Rle(x[0] * self.scale if self.scale != 1.0 else x[0], x[1]) for x in cov]
+        elif self.scale != 1.0:
             cov = [None if x is None else x.astype(np.float64) * self.scale for x in cov]
         return CoverageList(cov, self.names)
 
@@ -167,12 +189,13 @@ class DeviceCoverage:
 
 
 # ------------------------------------------------------------------------------ coverage
-def calcCoverage(input, mask, strand=None, ignore_strand=True, device=None, rc=None):
-    """R/coverage.R:126-174: one coverage vector per mask element (None = R's NULL)."""
+def calcCoverage(input, mask, strand=None, ignore_strand=True, device=None, rc=None, rle=False):
+    """R/coverage.R:126-174: one coverage vector per mask element (None = R's NULL); with
+    ``rle`` the elements are ``Rle`` objects, the form the reference returns."""
     dev = _device(device)
     rs, levels = _readset(input, dev, strand)
     rows = _rows_from_mask(mask, levels, ignore_strand)
-    return DeviceCoverage(rs, rows, mask.names).to_list()
+    return DeviceCoverage(rs, rows, mask.names).to_list(rle=rle)
 
 
 def _strand_params(sp):
@@ -344,6 +367,63 @@ def profileMatrix(input, flank, binParams, rc=None, keep_on_device=False):
         s["profile"] = RMatrix(out.cpu().numpy().T, cv.names)
         if keep_on_device:
             s["profile_device"] = out
+    return input
+
+
+def recoupProfiles(input, genomeRanges, region, flank, binParams, keep_on_device=False):
+    """The profile steps of recoup() over coverages already in ``input``: the forced
+    regionBinSize (R/recoup.R:579-596), profileMatrix (:597) and the forced heatmap binning
+    pass (:659-714), computed in ONE device pass per sample when both agree on the statistic
+    and interpolation (the plan's column parts are the profile's followed by the heatmap's).
+    Leaves ``sample["profile"]`` and, when the reference computes it, ``sample["heatmap"]``.
+
+    As in the reference, the heatmap pass of a non-base region (genebody / wide custom) fails:
+    R/recoup.R:703 reads the undefined ``forcedBinSize[1]`` -> SemanticError."""
+    bp = dict(binParams)
+    f1, f2 = int(flank[0]), int(flank[1])
+    custom_is_base = region == "custom" and bool(np.all(genomeRanges.width == 1))
+    must_bin = region == "genebody" or (region == "custom" and not bool(np.all(genomeRanges.width == genomeRanges.width[0])))
+    if must_bin and int(bp.get("regionBinSize", 0)) == 0:
+        bp["regionBinSize"] = 1000  # R/recoup.R:590-596
+    forced = bool(bp.get("forceHeatmapBinning", True)) and (int(bp.get("regionBinSize", 0)) == 0 or
+                                                              int(bp.get("flankBinSize", 0)) == 0)
+    base_region = region in ("tss", "tes") or custom_is_base
+    if forced and not base_region:
+        raise _lib.SemanticError(-5, "recoup.R:703: object 'forcedBinSize' not found (the reference's forced "
+                                     "heatmap binning of a non-base region)")
+    fbs = bp.get("forcedBinSize", (50, 200))
+    cvs = [_as_device_coverage(s["coverage"]) for s in input]
+    ln = cvs[0].lengths()
+    ln = ln[ln != 0]
+    equal = bool(np.all(ln == ln[0])) if len(ln) else True
+    stat = str(_first(bp.get("sumStat"), "mean")).lower()
+    for s, cv in zip(input, cvs):
+        prof = _profile_bins(bp, flank, equal, _base_size(cv) if equal else 0)
+        parts = list(prof.parts)
+        heat = None
+        if forced:
+            # binCoverageMatrix(coverage, binSize = forcedBinSize[2], stat) with its default
+            # interpolation "auto" (R/recoup.R:664-668)
+            heat = Bins([("whole", int(fbs[1]))], stat=stat, interp="auto")
+        fuse = heat is not None and prof.interp == heat.interp and prof.stat == heat.stat
+        bins = Bins(parts + (heat.parts if fuse else []), flank=(f1, f2), stat=prof.stat, interp=prof.interp,
+                    scale=cv.scale)
+        plan = Plan(cv.readset, cv.rows, bins)
+        out = plan.empty_output()
+        valid = torch.empty(max(plan.n_rows, 1), dtype=torch.uint8, device=out.device)
+        plan.execute(out, valid)
+        plan.status()
+        full = out.cpu().numpy().T
+        npc = prof.n_cols
+        s["profile"] = RMatrix(full[:, :npc], cv.names)
+        if keep_on_device:
+            s["profile_device"] = out
+        if heat is not None:
+            if fuse:
+                s["heatmap"] = RMatrix(full[:, npc:], cv.names)
+            else:
+                heat.scale = cv.scale
+                s["heatmap"] = _run(cv, heat)
     return input
 
 

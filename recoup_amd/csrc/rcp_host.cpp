@@ -40,6 +40,10 @@ hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* st
 hipError_t rcp_launch_streams(int64_t n, const uint64_t* keys, const int32_t* vals, int64_t* off, int64_t n_off,
                               int2* se, uint64_t* scan_in, hipStream_t stream);
 hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* pmax, hipStream_t stream);
+hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, int64_t n, const int32_t* d_cov, uint8_t* rowstart,
+                              uint32_t* flags, uint32_t* run, void* temp, size_t* temp_bytes, int32_t* d_values,
+                              int64_t* run_start, int32_t* d_lengths, int64_t* d_run_off, uint32_t* n_runs_host,
+                              hipStream_t stream);
 hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t* off, const int32_t* pmax, int32_t* out,
                                     hipStream_t stream);
 hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const int64_t* dir_off, const int64_t* off,
@@ -896,5 +900,42 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
     if (d_valid && plan->n_rows)
         HIP_TRY(hipMemcpyAsync(d_valid, plan->dev.valid, plan->n_rows, hipMemcpyDeviceToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));  // d_off is released on return
+    return RCP_OK;
+}
+
+extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int32_t* d_cov, int device,
+                              int32_t* d_values, int32_t* d_lengths, int64_t* run_off, int64_t* n_runs,
+                              void* hip_stream) {
+    if (n_rows < 0 || !out_off || !run_off || !n_runs) return fail(RCP_EINVAL, "NULL argument");
+    const int64_t n = out_off[n_rows];
+    if (n < 0 || n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "%lld positions", (long long)n);
+    if (n > 0 && (!d_cov || !d_values || !d_lengths)) return fail(RCP_EINVAL, "NULL device array");
+    for (int32_t r = 0; r < n_rows; ++r)
+        if (out_off[r + 1] < out_off[r]) return fail(RCP_EINVAL, "out_off decreases at row %d", r);
+    int rc = check_device(device);
+    if (rc) return rc;
+    DeviceGuard g(device);
+    HIP_TRY(g.err);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    const int64_t nn = std::max<int64_t>(n, 1);
+    DevBuf d_off, rowstart, flags, run, run_start, d_run_off, temp;
+    HIP_TRY(d_off.alloc(8 * ((size_t)n_rows + 1)));
+    HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * ((size_t)n_rows + 1), hipMemcpyHostToDevice, s));
+    HIP_TRY(rowstart.alloc(nn));
+    HIP_TRY(flags.alloc(4 * nn));
+    HIP_TRY(run.alloc(4 * nn));
+    HIP_TRY(run_start.alloc(8 * nn));
+    HIP_TRY(d_run_off.alloc(8 * ((size_t)n_rows + 1)));
+    size_t tb = 0;
+    uint32_t nr = 0;
+    HIP_TRY(rcp_rle_encode_dev(n_rows, d_off.as<int64_t>(), n, d_cov, nullptr, flags.as<uint32_t>(), run.as<uint32_t>(),
+                               nullptr, &tb, nullptr, nullptr, nullptr, nullptr, &nr, s));
+    HIP_TRY(temp.alloc(std::max<size_t>(tb, 1)));
+    HIP_TRY(rcp_rle_encode_dev(n_rows, d_off.as<int64_t>(), n, d_cov, rowstart.as<uint8_t>(), flags.as<uint32_t>(),
+                               run.as<uint32_t>(), temp.p, &tb, d_values, run_start.as<int64_t>(), d_lengths,
+                               d_run_off.as<int64_t>(), &nr, s));
+    HIP_TRY(hipMemcpyAsync(run_off, d_run_off.p, 8 * ((size_t)n_rows + 1), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n_runs = nr;
     return RCP_OK;
 }

@@ -1522,6 +1522,69 @@ extern "C" hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const
     return hipGetLastError();
 }
 
+// =================================================================================
+// run-length encoding of CSR coverage (the Rle objects of calcCoverage, S4Vectors)
+// =================================================================================
+// run starts: a row's first position, or a value change inside a row
+__global__ void rcp_rle_flags_kernel(int64_t n, const int32_t* __restrict__ cov, const uint8_t* __restrict__ rowstart,
+                                     uint32_t* __restrict__ flags) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    flags[i] = (rowstart[i] || cov[i] != cov[i - 1 >= 0 ? i - 1 : 0]) ? 1u : 0u;
+}
+
+__global__ void rcp_rle_rowstart_kernel(int32_t n_rows, const int64_t* __restrict__ off, uint8_t* __restrict__ rowstart) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n_rows && off[r + 1] > off[r]) rowstart[off[r]] = 1;
+}
+
+__global__ void rcp_rle_scatter_kernel(int64_t n, const int32_t* __restrict__ cov, const uint32_t* __restrict__ flags,
+                                       const uint32_t* __restrict__ run, int32_t* __restrict__ values,
+                                       int64_t* __restrict__ run_start) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flags[i]) return;
+    values[run[i]] = cov[i];
+    run_start[run[i]] = i;
+}
+
+__global__ void rcp_rle_finish_kernel(int32_t n_rows, int64_t n, uint32_t n_runs, const int64_t* __restrict__ off,
+                                      const uint32_t* __restrict__ run, const int64_t* __restrict__ run_start,
+                                      int32_t* __restrict__ lengths, int64_t* __restrict__ run_off) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n_runs) lengths[t] = (int32_t)((t + 1 < n_runs ? run_start[t + 1] : n) - run_start[t]);
+    if (t <= n_rows) run_off[t] = off[t] < n ? (int64_t)run[off[t]] : (int64_t)n_runs;
+}
+
+extern "C" hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, int64_t n, const int32_t* d_cov,
+                                         uint8_t* rowstart, uint32_t* flags, uint32_t* run, void* temp, size_t* temp_bytes,
+                                         int32_t* d_values, int64_t* run_start, int32_t* d_lengths, int64_t* d_run_off,
+                                         uint32_t* n_runs_host, hipStream_t stream) {
+    if (!temp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, flags, run, (int)std::max<int64_t>(n, 1),
+                                                       stream);
+    hipError_t e;
+    const unsigned gn = (unsigned)((n + kBlock - 1) / kBlock);
+    if ((e = hipMemsetAsync(rowstart, 0, (size_t)std::max<int64_t>(n, 1), stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(rcp_rle_rowstart_kernel, dim3((n_rows + kBlock - 1) / kBlock + 1), dim3(kBlock), 0, stream,
+                       n_rows, d_off, rowstart);
+    uint32_t nr = 0;
+    if (n > 0) {
+        hipLaunchKernelGGL(rcp_rle_flags_kernel, dim3(gn), dim3(kBlock), 0, stream, n, d_cov, rowstart, flags);
+        if ((e = hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, flags, run, (int)n, stream)) != hipSuccess) return e;
+        uint32_t last[2];
+        if ((e = hipMemcpyAsync(&last[0], run + n - 1, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(&last[1], flags + n - 1, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
+        nr = last[0] + last[1];
+        hipLaunchKernelGGL(rcp_rle_scatter_kernel, dim3(gn), dim3(kBlock), 0, stream, n, d_cov, flags, run, d_values,
+                           run_start);
+    }
+    const int64_t work = std::max<int64_t>((int64_t)nr, (int64_t)n_rows + 1);
+    hipLaunchKernelGGL(rcp_rle_finish_kernel, dim3((unsigned)((work + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                       n_rows, n, nr, d_off, run, run_start, d_lengths, d_run_off);
+    *n_runs_host = nr;
+    return hipGetLastError();
+}
+
 extern "C" hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* pmax, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const int64_t grid = (n + kBlock - 1) / kBlock;

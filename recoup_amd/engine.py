@@ -192,8 +192,9 @@ class Plan:
         check(_lib.lib().rcp_plan_validity(self.h, ptr(v), _stream(self.device, stream)))
         return v[:self.n_rows].cpu().numpy().astype(bool)
 
-    def coverage(self, stream=None):
-        """calcCoverage: list of int32 numpy vectors (None for NULL rows)."""
+    def coverage(self, stream=None, rle=False):
+        """calcCoverage: list of int32 numpy vectors (None for NULL rows); with ``rle`` each
+        vector comes as its Rle ``(values, lengths)`` pair, encoded on the GPU."""
         ln = self.row_lengths()
         off = np.zeros(self.n_rows + 1, dtype=np.int64)
         off[1:] = np.cumsum(ln)
@@ -202,8 +203,19 @@ class Plan:
         check(_lib.lib().rcp_calc_coverage(self.h, cptr(off, _lib._i64p), ptr(cov), ptr(v),
                                            _stream(self.device, stream)))
         self.status(stream)
-        hc = cov.cpu().numpy()
         hv = v[:self.n_rows].cpu().numpy().astype(bool)
+        if rle:
+            vals = torch.empty_like(cov)
+            lens = torch.empty_like(cov)
+            run_off = np.zeros(self.n_rows + 1, dtype=np.int64)
+            nruns = ctypes.c_int64()
+            check(_lib.lib().rcp_rle_encode(self.n_rows, cptr(off, _lib._i64p), ptr(cov), self.device, ptr(vals),
+                                            ptr(lens), cptr(run_off, _lib._i64p), ctypes.byref(nruns),
+                                            _stream(self.device, stream)))
+            hv_, hl_ = vals[:nruns.value].cpu().numpy(), lens[:nruns.value].cpu().numpy()
+            return [(hv_[run_off[r]:run_off[r + 1]].copy(), hl_[run_off[r]:run_off[r + 1]].copy()) if hv[r] else None
+                    for r in range(self.n_rows)]
+        hc = cov.cpu().numpy()
         return [hc[off[r]:off[r + 1]].copy() if hv[r] else None for r in range(self.n_rows)]
 
     def run(self, stream=None, binsum=False):

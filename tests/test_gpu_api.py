@@ -152,3 +152,59 @@ def test_missing_chromosome_rows_are_null(c1):
     cov = ra.calcCoverage(inp[0]["ranges"], g)
     assert cov[1] is None  # not in the reads' seqlevels -> "chrUn not found!" -> NULL
     assert cov[2] is None  # crosses the chromosome end -> subscript error -> NULL
+
+
+def _runs_ok(rle, dense):
+    np.testing.assert_array_equal(rle.decode(), dense)
+    assert len(rle.values) == len(rle.lengths)
+    assert (rle.lengths > 0).all()
+    assert (np.diff(rle.values) != 0).all()  # runs are maximal, as Rle() builds them
+
+
+def test_calc_coverage_rle(c1):
+    """calcCoverage returns Rle objects in the reference (R/coverage.R:171-173)."""
+    inp = _input(c1)
+    for mask in (c1["genome"], c1["exons"], ra.getRegionalRanges(c1["genome"], "tss", FLANK)):
+        dense = ra.calcCoverage(inp[1]["ranges"], mask)
+        rle = ra.calcCoverage(inp[1]["ranges"], mask, rle=True)
+        assert len(rle) == len(dense)
+        for d, e in zip(dense, rle):
+            assert (d is None) == (e is None)
+            if d is not None:
+                _runs_ok(e, d)
+
+
+def test_rle_edge_rows(c1):
+    """Empty (index-0-only) and NULL rows between ordinary ones keep their run offsets."""
+    inp = _input(c1)
+    g = ra.GRanges(["chr12"] * 5, [0, 1_000_000, -5, 1_000_100, 121_257_000],
+                   [0, 1_003_000, 10, 1_000_100, 121_258_000])
+    dense = ra.calcCoverage(inp[0]["ranges"], g)
+    rle = ra.calcCoverage(inp[0]["ranges"], g, rle=True)
+    for d, e in zip(dense, rle):
+        assert (d is None) == (e is None)
+        if d is not None:
+            _runs_ok(e, d)
+
+
+def test_recoup_profiles_fused_heatmap(c1):
+    """recoup() TSS per-base profile + its forced 200-bin heatmap pass (R/recoup.R:659-671),
+    computed from one device pass."""
+    inp = ra.coverageRef(_input(c1), c1["genome"], "tss", FLANK)
+    inp = ra.recoupProfiles(inp, c1["genome"], "tss", FLANK, {"flankBinSize": 0, "regionBinSize": 0})
+    for k, s in enumerate(inp):
+        np.testing.assert_array_equal(np.asarray(s["profile"]), c1["gold"][f"tss_base_s{k}"].astype(np.float64))
+        np.testing.assert_allclose(s["heatmap"], c1["gold"][f"tss_heat_s{k}"], rtol=1e-12, atol=0)
+
+
+def test_recoup_profiles_genebody(c1):
+    inp = ra.coverageRef(_input(c1), c1["genome"], "genebody", FLANK)
+    inp = ra.recoupProfiles(inp, c1["genome"], "genebody", FLANK,
+                            {"flankBinSize": 50, "regionBinSize": 150, "sumStat": "median"})
+    for k, s in enumerate(inp):
+        np.testing.assert_allclose(s["profile"], c1["gold"][f"gb_median_s{k}"], rtol=1e-9, atol=1e-12)
+        assert "heatmap" not in s
+    # the reference's forced heatmap pass of a genebody profile errors (recoup.R:703)
+    inp = ra.coverageRef(_input(c1), c1["genome"], "genebody", FLANK)
+    with pytest.raises(ra.SemanticError):
+        ra.recoupProfiles(inp, c1["genome"], "genebody", FLANK, {"flankBinSize": 0, "regionBinSize": 150})

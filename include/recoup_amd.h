@@ -11,6 +11,7 @@
  *                        (+ the strand filter of calcCoverage R/coverage.R:141-144)
  *   rcp_calc_coverage    replaces calcCoverage()              R/coverage.R:126-174
  *   rcp_rle_encode       the Rle values / lengths of each coverage (R/coverage.R:171-173)
+ *   rcp_bam_read         readBam() -> the read arrays      R/ranges.R:111-146 (next row)
  *                        and its per-region coverageFromRanges R/coverage.R:176-226
  *   rcp_plan_create /    replace the coverage -> profile pass:
  *   rcp_plan_execute /     coverageFromRanges                 R/coverage.R:176-226
@@ -184,6 +185,24 @@ RCP_API int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, const 
  * orientation (reversed for '-'), i.e. exactly the values of the reference's Rle. */
 RCP_API int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t* d_cov, uint8_t* d_valid,
                       void* hip_stream);
+
+/* ------------------------------------------------------------------ BAM ingest */
+/* readBam (R/ranges.R:111-146) on the host: BGZF blocks inflated by n_threads threads, mapped
+ * alignments (readGAlignments) turned into 1-based ranges on their reference and strand:
+ *   RCP_SPLICE_KEEP    the reference span (as(GAlignments, "GRanges"))
+ *   RCP_SPLICE_SPLIT   one range per block between N-skips (unlist(grglist(.)))
+ *   RCP_SPLICE_REMOVE  spans, minus those wider than quantile(width, remove_q) (type 7)
+ * all clipped to [1, seqlength] (trim()).  The arrays feed rcp_readset_create (chrom = BAM
+ * reference index, seqlen = the header's lengths). */
+enum { RCP_SPLICE_KEEP = 0, RCP_SPLICE_REMOVE = 1, RCP_SPLICE_SPLIT = 2 };
+typedef struct rcp_bam rcp_bam;
+RCP_API int rcp_bam_read(const char* path, int splice_action, double remove_q, int n_threads, rcp_bam** out);
+RCP_API int rcp_bam_info(const rcp_bam* bam, int64_t* n_reads, int32_t* n_ref, int64_t* n_alignments);
+RCP_API const char* rcp_bam_ref_name(const rcp_bam* bam, int32_t i);
+/* Copy out: ref_len [n_ref]; chrom / start / end / strand [n_reads] (any may be NULL). */
+RCP_API int rcp_bam_copy(const rcp_bam* bam, int64_t* ref_len, int32_t* chrom, int32_t* start, int32_t* end,
+                         int8_t* strand);
+RCP_API int rcp_bam_free(rcp_bam* bam);
 
 /* Run-length encoding of a CSR coverage (the output of rcp_calc_coverage): the values and
  * lengths of each row's Rle, as S4Vectors::Rle(values, lengths) holds them

@@ -84,6 +84,12 @@ SIGNATURES = [
     ("rcp_profile", ctypes.c_int, [_vp, ctypes.POINTER(RowsDesc), ctypes.POINTER(BinsDesc), _dp, _u8p]),
     ("rcp_calc_coverage", ctypes.c_int, [_vp, _i64p, _vp, _vp, _vp]),
     ("rcp_rle_encode", ctypes.c_int, [ctypes.c_int32, _i64p, _vp, ctypes.c_int, _vp, _vp, _i64p, _i64p, _vp]),
+    ("rcp_bam_read", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                    ctypes.POINTER(_vp)]),
+    ("rcp_bam_info", ctypes.c_int, [_vp, _i64p, _i32p, _i64p]),
+    ("rcp_bam_ref_name", ctypes.c_char_p, [_vp, ctypes.c_int32]),
+    ("rcp_bam_copy", ctypes.c_int, [_vp, _i64p, _i32p, _i32p, _i32p, _i8p]),
+    ("rcp_bam_free", ctypes.c_int, [_vp]),
 ]
 
 _LIB = None

@@ -454,3 +454,34 @@ def normalizeLinear(input):
         elif cv is not None:
             s["coverage"] = CoverageList([None if x is None else x * k for x in cv], cv.names)
     return input
+
+
+# ------------------------------------------------------------------------------ ingest
+SPLICE = {"keep": 0, "remove": 1, "split": 2}
+
+
+def readBam(bam, spliceAction="keep", spliceRemoveQ=0.75, threads=8):
+    """readBam (R/ranges.R:120-146): the mapped alignments of a BAM file as a GRanges of
+    reads (BGZF inflated on ``threads`` host threads by librecoup_amd.so)."""
+    import ctypes
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    _lib.check(L.rcp_bam_read(str(bam).encode(), SPLICE[_first(spliceAction, "keep")], float(spliceRemoveQ),
+                              int(threads), ctypes.byref(h)))
+    try:
+        n = ctypes.c_int64()
+        nref = ctypes.c_int32()
+        nal = ctypes.c_int64()
+        _lib.check(L.rcp_bam_info(h, ctypes.byref(n), ctypes.byref(nref), ctypes.byref(nal)))
+        names = [L.rcp_bam_ref_name(h, i).decode() for i in range(nref.value)]
+        ref_len = np.zeros(max(nref.value, 1), np.int64)
+        chrom = np.zeros(n.value, np.int32)
+        start = np.zeros(n.value, np.int32)
+        end = np.zeros(n.value, np.int32)
+        strand = np.zeros(n.value, np.int8)
+        _lib.check(L.rcp_bam_copy(h, _lib.cptr(ref_len, _lib._i64p), _lib.cptr(chrom, _lib._i32p),
+                                  _lib.cptr(start, _lib._i32p), _lib.cptr(end, _lib._i32p),
+                                  _lib.cptr(strand, _lib._i8p)))
+    finally:
+        L.rcp_bam_free(h)
+    return GRanges(chrom, start, end, strand, seqlevels=names, seqlengths=ref_len[:len(names)])

@@ -13,7 +13,7 @@ ARCH = os.environ.get("RCP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
             "-fvisibility=hidden"]
-SOURCES = ["rcp_kernels.hip", "rcp_host.cpp"]
+SOURCES = ["rcp_kernels.hip", "rcp_host.cpp", "rcp_bam.cpp"]
 DEPS = ["rcp_device.h", "rcp_rng.h", os.path.join("..", "..", "include", "recoup_amd.h")]
 
 
@@ -39,7 +39,8 @@ def build(force=False, verbose=True):
                 print(" ".join(cmd), flush=True)
             subprocess.check_call(cmd)
     if force or _newer(OUT, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fvisibility=hidden", "-o", OUT] + objs
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fvisibility=hidden", "-o", OUT] + objs + ["-lz",
+                                                                                                   "-pthread"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)

@@ -179,6 +179,8 @@ struct rcp_readset {
     ReadLayout stranded, merged;
 };
 
+int rcp_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
+
 extern "C" const char* rcp_version(void) { return "recoup_amd 0.1.0 (gfx950)"; }
 extern "C" const char* rcp_last_error(void) { return g_err.c_str(); }
 

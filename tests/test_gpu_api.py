@@ -208,3 +208,21 @@ def test_recoup_profiles_genebody(c1):
     inp = ra.coverageRef(_input(c1), c1["genome"], "genebody", FLANK)
     with pytest.raises(ra.SemanticError):
         ra.recoupProfiles(inp, c1["genome"], "genebody", FLANK, {"flankBinSize": 0, "regionBinSize": 150})
+
+
+def test_bam_ingest_to_profile(c1):
+    """readBam (R/ranges.R:120-124) -> coverageRef -> profileMatrix on the reference's BAM
+    fixtures, against the oracle on the same reads."""
+    bams = [os.path.join(os.path.dirname(__file__), "golden", "bam", f)
+            for f in ("WT_H4K20me1_50kr.bam", "Set8KO_H4K20me1_50kr.bam")]
+    inp = [{"id": f"s{k}", "name": os.path.basename(b), "ranges": ra.readBam(b)} for k, b in enumerate(bams)]
+    inp = ra.coverageRef(inp, c1["genome"], "tss", FLANK)
+    inp = ra.profileMatrix(inp, FLANK, {"flankBinSize": 0, "regionBinSize": 100})
+    win = ra.getRegionalRanges(c1["genome"], "tss", FLANK)
+    for s in inp:
+        g = s["ranges"]
+        ix = o.Index(g.seqcodes, g.start, g.end, g.strand, g.seqlengths)
+        mask = o.Mask.from_ranges(win.codes_in(g.seqlevels), win.start, win.end, win.strand)
+        ref, rv = o.profile_part(ix, mask, 100)
+        np.testing.assert_allclose(s["profile"], ref, rtol=1e-12, atol=0)
+        assert s["profile"].sum() > 0

@@ -12,6 +12,7 @@
  *   rcp_calc_coverage    replaces calcCoverage()              R/coverage.R:126-174
  *   rcp_rle_encode       the Rle values / lengths of each coverage (R/coverage.R:171-173)
  *   rcp_bam_read         readBam() -> the read arrays      R/ranges.R:111-146 (next row)
+ *   rcp_rng_*            set.seed + sort(sample(n, k)) of downsample / sampleto  R/ranges.R:32-62
  *                        and its per-region coverageFromRanges R/coverage.R:176-226
  *   rcp_plan_create /    replace the coverage -> profile pass:
  *   rcp_plan_execute /     coverageFromRanges                 R/coverage.R:176-226
@@ -203,6 +204,18 @@ RCP_API const char* rcp_bam_ref_name(const rcp_bam* bam, int32_t i);
 RCP_API int rcp_bam_copy(const rcp_bam* bam, int64_t* ref_len, int32_t* chrom, int32_t* start, int32_t* end,
                          int8_t* strand);
 RCP_API int rcp_bam_free(rcp_bam* bam);
+
+/* ------------------------------------------------------------------ R RNG */
+/* The preprocessing steps normalize = "downsample" / "sampleto" (R/ranges.R:32-62):
+ * set.seed(seed) once, then per sample sort(sample(libsize, size)) -- written to `out` as
+ * 1-based read indices, in the RNG state order R uses (sample.int's hash variant when
+ * n > 1e7 and k <= n/2).  k > n is the R error "cannot take a sample larger than the
+ * population" (RCP_ESEMANTIC).  kind: RCP_RNG_*. */
+typedef struct rcp_rng rcp_rng;
+RCP_API int rcp_rng_create(uint32_t seed, int kind, rcp_rng** out);
+RCP_API int rcp_rng_unif(rcp_rng* rng, int64_t k, double* out);
+RCP_API int rcp_rng_sample_sorted(rcp_rng* rng, int64_t n, int64_t k, int64_t* out);
+RCP_API int rcp_rng_free(rcp_rng* rng);
 
 /* Run-length encoding of a CSR coverage (the output of rcp_calc_coverage): the values and
  * lengths of each row's Rle, as S4Vectors::Rle(values, lengths) holds them

@@ -11,5 +11,5 @@ from .granges import (GRanges, GRangesList, flank, getFlankingRanges, getRegiona
                       promoters, resize)
 from .api import (CoverageList, DeviceCoverage, RMatrix, Rle, baseCoverageMatrix, binCoverageMatrix,  # noqa: F401
                   calcCoverage, calcLinearFactors, coverageRef, coverageRnaRef, normalizeLinear, profileMatrix,
-                  readBam, recoupProfiles)
+                  RRng, preprocessRanges, readBam, recoupProfiles)
 from ._lib import RcpError, SemanticError, UnsupportedError  # noqa: F401

@@ -90,6 +90,10 @@ SIGNATURES = [
     ("rcp_bam_ref_name", ctypes.c_char_p, [_vp, ctypes.c_int32]),
     ("rcp_bam_copy", ctypes.c_int, [_vp, _i64p, _i32p, _i32p, _i32p, _i8p]),
     ("rcp_bam_free", ctypes.c_int, [_vp]),
+    ("rcp_rng_create", ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(_vp)]),
+    ("rcp_rng_unif", ctypes.c_int, [_vp, ctypes.c_int64, _dp]),
+    ("rcp_rng_sample_sorted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _i64p]),
+    ("rcp_rng_free", ctypes.c_int, [_vp]),
 ]
 
 _LIB = None

@@ -485,3 +485,56 @@ def readBam(bam, spliceAction="keep", spliceRemoveQ=0.75, threads=8):
     finally:
         L.rcp_bam_free(h)
     return GRanges(chrom, start, end, strand, seqlevels=names, seqlengths=ref_len[:len(names)])
+
+
+class RRng:
+    """R's RNG after ``set.seed(seed)`` (Mersenne-Twister, ``sample.kind`` Rejection or Rounding)."""
+
+    def __init__(self, seed, kind="Rejection"):
+        import ctypes
+        self._h = ctypes.c_void_p()
+        _lib.check(_lib.lib().rcp_rng_create(int(seed) & 0xFFFFFFFF, {"Rejection": 0, "Rounding": 1}[kind],
+                                             ctypes.byref(self._h)))
+
+    def runif(self, k):
+        out = np.zeros(max(int(k), 1))
+        _lib.check(_lib.lib().rcp_rng_unif(self._h, int(k), _lib.cptr(out, _lib._dp)))
+        return out[:k]
+
+    def sample_sorted(self, n, k):
+        """``sort(sample(n, k))`` (1-based)."""
+        out = np.zeros(max(int(k), 1), dtype=np.int64)
+        _lib.check(_lib.lib().rcp_rng_sample_sorted(self._h, int(n), int(k), _lib.cptr(out, _lib._i64p)))
+        return out[:k]
+
+    def __del__(self):
+        try:
+            _lib.lib().rcp_rng_free(self._h)
+        except Exception:
+            pass
+
+
+def preprocessRanges(input, preprocessParams=None, bamParams=None, rc=None):
+    """R/ranges.R:1-62: read each sample's BAM (``file``, when ``ranges`` is missing) and apply
+    normalize = "downsample" (every sample down to the smallest library) or "sampleto"
+    (every sample to ``sampleTo`` reads): ``set.seed(seed)`` once, then per sample
+    ``ranges[sort(sample(libsize, size))]``.  "none" / "linear" only read."""
+    pp = {"normalize": "none", "sampleTo": 1e6, "spliceAction": "split", "spliceRemoveQ": 0.75, "seed": 42}
+    pp.update(preprocessParams or {})
+    if not _needs(input, "ranges"):
+        return input
+    for s in input:
+        if s.get("ranges") is None:
+            fmt = str(s.get("format", "bam")).lower()
+            if fmt != "bam":
+                raise _lib.UnsupportedError(-4, f"reading {fmt} input is outside this build (BAM only)")
+            s["ranges"] = readBam(s["file"], _first(pp["spliceAction"], "split"), pp["spliceRemoveQ"])
+    norm = _first(pp["normalize"], "none")
+    if norm in ("downsample", "sampleto"):
+        libs = [len(s["ranges"]) for s in input]
+        size = min(libs) if norm == "downsample" else int(pp["sampleTo"])
+        rng = RRng(int(pp["seed"]))
+        for s, n in zip(input, libs):
+            idx = rng.sample_sorted(n, size) - 1
+            s["ranges"] = s["ranges"][idx]
+    return input

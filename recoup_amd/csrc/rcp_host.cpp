@@ -941,3 +941,39 @@ extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int3
     *n_runs = nr;
     return RCP_OK;
 }
+
+// =====================================================================================
+// R RNG for the preprocessing steps (downsample / sampleto, R/ranges.R:32-62)
+// =====================================================================================
+struct rcp_rng {
+    rcp::RRng rng;
+    bool rounding;
+    rcp_rng(uint32_t seed, bool r) : rng(seed), rounding(r) {}
+};
+
+extern "C" int rcp_rng_create(uint32_t seed, int kind, rcp_rng** out) {
+    if (!out) return fail(RCP_EINVAL, "NULL argument");
+    if (kind != RCP_RNG_REJECTION && kind != RCP_RNG_ROUNDING) return fail(RCP_EINVAL, "rng kind %d", kind);
+    *out = new rcp_rng(seed, kind == RCP_RNG_ROUNDING);
+    return RCP_OK;
+}
+
+extern "C" int rcp_rng_unif(rcp_rng* g, int64_t k, double* out) {
+    if (!g || (k > 0 && !out)) return fail(RCP_EINVAL, "NULL argument");
+    for (int64_t i = 0; i < k; ++i) out[i] = g->rng.unif_rand();
+    return RCP_OK;
+}
+
+extern "C" int rcp_rng_sample_sorted(rcp_rng* g, int64_t n, int64_t k, int64_t* out) {
+    if (!g || (k > 0 && !out)) return fail(RCP_EINVAL, "NULL argument");
+    std::vector<int64_t> v;
+    if (!g->rng.sample_sorted(n, k, g->rounding, &v))
+        return fail(RCP_ESEMANTIC, "cannot take a sample larger than the population when 'replace = FALSE'");
+    std::copy(v.begin(), v.end(), out);
+    return RCP_OK;
+}
+
+extern "C" int rcp_rng_free(rcp_rng* g) {
+    delete g;
+    return RCP_OK;
+}

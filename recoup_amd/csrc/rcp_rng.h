@@ -68,6 +68,42 @@ class RRng {
         return out;
     }
 
+    // sort(sample(n, k)) of the preprocessing steps (R/ranges.R:32-62), 1-based.  R's
+    // sample.int switches to .Internal(sample2()) -- rejection of repeated unif_index draws --
+    // when n > 1e7 and k <= n / 2; otherwise it is the partial Fisher-Yates of sample_int.
+    // Returns false when k > n (R: "cannot take a sample larger than the population").
+    bool sample_sorted(int64_t n, int64_t k, bool rounding, std::vector<int64_t>* out) {
+        out->clear();
+        if (k < 0 || k > n) return false;
+        if (n > 10000000 && 2 * k <= n) {
+            std::vector<uint64_t> seen((size_t)(n / 64 + 1), 0);
+            for (int64_t got = 0; got < k;) {
+                const int64_t v = (int64_t)unif_index((double)n, rounding);
+                uint64_t& w = seen[(size_t)(v >> 6)];
+                const uint64_t bit = uint64_t(1) << (v & 63);
+                if (!(w & bit)) {
+                    w |= bit;
+                    ++got;
+                }
+            }
+            out->reserve((size_t)k);
+            for (size_t i = 0; i < seen.size(); ++i)
+                for (uint64_t w = seen[i]; w; w &= w - 1) out->push_back((int64_t)(i * 64 + __builtin_ctzll(w)) + 1);
+            return true;
+        }
+        std::vector<int64_t> pool((size_t)n);
+        for (int64_t i = 0; i < n; ++i) pool[(size_t)i] = i;
+        int64_t m = n;
+        out->resize((size_t)k);
+        for (int64_t i = 0; i < k; ++i) {
+            const int64_t j = (int64_t)unif_index((double)m, rounding);
+            (*out)[(size_t)i] = pool[(size_t)j] + 1;
+            pool[(size_t)j] = pool[(size_t)--m];
+        }
+        std::sort(out->begin(), out->end());
+        return true;
+    }
+
   private:
     static constexpr int kN = 624;
     static constexpr int kM = 397;

@@ -2,6 +2,8 @@
 R/ranges.R:67-100, the profileMatrix column-part selection (R/profile.R:1-98) and the
 coverageRnaRef row table (R/coverage.R:79-124), checked against the oracle's independent
 restatement and the reference's documented semantics."""
+import os
+
 import numpy as np
 import pytest
 
@@ -111,3 +113,64 @@ def test_linear_factors():
                                [0.25, 0.5, 0.125])
     with pytest.raises(ra.SemanticError):
         ra.calcLinearFactors([{"ranges": None}])
+
+
+# ----------------------------------------------------------------------------- R RNG (product)
+def test_product_rng_known_answers():
+    """The library's own R RNG (rcp_rng_*) against R's published set.seed(42) outputs."""
+    np.testing.assert_array_equal(ra.RRng(42).runif(3), [0.9148060434963554, 0.9370754132978618, 0.2861395347863436])
+    assert list(ra.RRng(42).sample_sorted(10, 3)) == [1, 5, 10]
+    assert list(ra.RRng(42, "Rounding").sample_sorted(10, 3)) == [3, 9, 10]
+    with pytest.raises(ra.SemanticError):
+        ra.RRng(1).sample_sorted(5, 6)
+
+
+def test_product_rng_matches_oracle_sequence():
+    """Successive sort(sample(n, k)) calls continue one RNG stream, as lapply() does after a
+    single set.seed (R/ranges.R:40-44)."""
+    g = ra.RRng(7)
+    o.set_seed(7)
+    for n, k in [(50000, 1000), (1234, 1234), (99, 3)]:
+        np.testing.assert_array_equal(g.sample_sorted(n, k), np.sort(o.sample_int(n, k)))
+
+
+def _r_unif_index(u_stream, dn):
+    """R_unif_index (Rejection): rbits(ceil(log2 n)) until below n, 16 bits per unif_rand."""
+    bits = int(np.ceil(np.log2(dn)))
+    while True:
+        v = 0
+        for _ in range(0, bits + 1, 16):
+            v = 65536 * v + int(np.floor(next(u_stream) * 65536))
+        v &= (1 << bits) - 1
+        if v < dn:
+            return v
+
+
+def test_product_rng_hash_variant():
+    """n > 1e7, k <= n/2: sample.int's .Internal(sample2()) draws indices until k distinct."""
+    n, k = 20_000_001, 50
+    o.set_seed(11)
+    u = iter(o.runif(5000))
+    seen = []
+    while len(seen) < k:
+        v = _r_unif_index(u, n) + 1
+        if v not in seen:
+            seen.append(v)
+    np.testing.assert_array_equal(ra.RRng(11).sample_sorted(n, k), np.sort(seen))
+
+
+def test_preprocess_sampleto_on_bam_fixtures():
+    bams = [os.path.join(os.path.dirname(__file__), "golden", "bam", f)
+            for f in ("WT_H4K20me1_50kr.bam", "Set8KO_H4K20me1_50kr.bam")]
+    inp = [{"id": "a", "file": bams[0]}, {"id": "b", "file": bams[1]}]
+    inp = ra.preprocessRanges(inp, {"normalize": "sampleto", "sampleTo": 10000, "spliceAction": "keep"})
+    o.set_seed(42)
+    for s, b in zip(inp, bams):
+        full = ra.readBam(b)
+        idx = np.sort(o.sample_int(len(full), 10000)) - 1
+        assert len(s["ranges"]) == 10000
+        np.testing.assert_array_equal(s["ranges"].start, full.start[idx])
+        np.testing.assert_array_equal(s["ranges"].strand, full.strand[idx])
+    ds = ra.preprocessRanges([{"id": "a", "file": bams[0]}, {"id": "b", "file": bams[1]}],
+                             {"normalize": "downsample"})
+    assert [len(s["ranges"]) for s in ds] == [50000, 50000]

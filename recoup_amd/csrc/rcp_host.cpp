@@ -54,7 +54,7 @@ hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const int64_t* d
 namespace {
 
 constexpr int kChunkMax = 16384;       // positions of an interpolated slice (block LDS array)
-constexpr int kWaveMax = 4096;         // positions per wave sub-chunk (padded LDS array <= 17 KB)
+constexpr int kWaveMax = 2048;         // positions per wave sub-chunk (padded LDS array <= 9 KB; 8 waves)
 #ifndef RCP_STAGE_MAX_BINS
 #define RCP_STAGE_MAX_BINS 512
 #endif

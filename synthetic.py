@@ -124,3 +124,120 @@ def n_overlaps(reads, regions, width, device="cuda:0"):
     hi = rc * (1 << 32) + torch.as_tensor(regions["end"], device=device, dtype=torch.int64)
     cnt = torch.searchsorted(ks, hi, right=True) - torch.searchsorted(ks, lo, right=False)
     return cnt.cpu().numpy()
+
+
+def c3(device="cuda:0", seed=20261015, n_genes=25_000, n_pairs=50_000_000, width=100, exonic=0.70,
+       flank=2000, region_bins=500, flank_bins=50, short_frac=0.05, genome=None):
+    """coverageRnaRef spliced (C3): genes of 1 + Poisson(8) exons (lognormal widths, median 150 bp;
+    lognormal introns, median 2 kb; ~5 % of genes with < 500 exonic bp -> interpolated centres),
+    2 x n_pairs mate alignments of `width` bp (mates read independently, R/ranges.R:117-120),
+    `exonic` of them drawn along transcripts -- those crossing an exon junction are split into
+    two blocks (spliceAction "split") -- the rest uniform.  Rows: c(upstream flank, exon list,
+    downstream flank) per gene, flank bins 50 / centre 500 bins."""
+    lens_np = MM10 if genome is None else np.asarray(genome, dtype=np.int64)
+    rng = np.random.default_rng(seed)
+    n_ex = 1 + rng.poisson(8, n_genes)
+    short = rng.random(n_genes) < short_frac
+    n_ex[short] = rng.integers(1, 3, short.sum())
+    tot = int(n_ex.sum())
+    ew = np.maximum(np.round(rng.lognormal(np.log(150), 0.6, tot)), 20).astype(np.int64)
+    gi = np.repeat(np.arange(n_genes), n_ex)
+    ew[short[gi]] = np.minimum(ew[short[gi]], 200)
+    iw = np.maximum(np.round(rng.lognormal(np.log(2000), 1.0, tot)), 50).astype(np.int64)
+    first = np.zeros(n_genes + 1, np.int64)
+    first[1:] = np.cumsum(n_ex)
+    iw[first[1:] - 1] = 0  # no intron after a gene's last exon
+    span = np.add.reduceat(ew + iw, first[:-1])
+    chrom = rng.choice(len(lens_np), n_genes, p=lens_np / lens_np.sum()).astype(np.int32)
+    gstart = (flank + 10 + rng.random(n_genes) * (lens_np[chrom] - span - 2 * flank - 20)).astype(np.int64)
+    order = np.lexsort((gstart, chrom))
+    chrom, gstart, n_ex2, span = chrom[order], gstart[order], n_ex[order], span[order]
+    # exon coordinates in sorted gene order
+    ex_s, ex_e, ex_gene = [], [], []
+    for new, old in enumerate(order):
+        w = ew[first[old]:first[old + 1]]
+        gaps = iw[first[old]:first[old + 1]]
+        st = gstart[new] + np.concatenate([[0], np.cumsum(w + gaps)[:-1]])
+        ex_s.append(st)
+        ex_e.append(st + w - 1)
+        ex_gene.append(np.full(len(w), new))
+    ex_s, ex_e, ex_gene = np.concatenate(ex_s), np.concatenate(ex_e), np.concatenate(ex_gene)
+    seg_off = np.zeros(n_genes + 1, np.int64)
+    seg_off[1:] = np.cumsum(n_ex2)
+    gstrand = rng.integers(0, 2, n_genes).astype(np.int8)
+    gend = ex_e[seg_off[1:] - 1]
+    # ---- reads on the GPU
+    g = _gen(device, seed)
+    n = 2 * n_pairs
+    n_ex_reads = int(n * exonic)
+    dev = device
+    exlen_g = torch.as_tensor(np.add.reduceat(ex_e - ex_s + 1, seg_off[:-1]), device=dev)
+    cum = torch.as_tensor(np.concatenate([[0], np.cumsum(ex_e - ex_s + 1)]), device=dev)  # flat transcript coords
+    t_s = torch.as_tensor(ex_s, device=dev)
+    t_e = torch.as_tensor(ex_e, device=dev)
+    gsel = torch.randint(0, n_genes, (n_ex_reads,), generator=g, device=dev)
+    base = cum[torch.as_tensor(seg_off[:-1], device=dev)][gsel]
+    room = (exlen_g[gsel] - width).clamp_(min=0)
+    t = base + (torch.rand(n_ex_reads, generator=g, device=dev, dtype=torch.float64) * (room + 1)).to(torch.int64)
+    k = (torch.searchsorted(cum, t, right=True) - 1).clamp_(max=len(ex_s) - 1)
+    gs = t_s[k] + (t - cum[k])
+    left = t_e[k] - gs + 1  # bases to the end of exon k
+    last = torch.as_tensor(seg_off[1:] - 1, device=dev)[gsel]
+    split = (left < width) & (k < last)
+    b1e = torch.where(split, t_e[k], gs + width - 1)
+    kn = (k + 1).clamp_(max=len(ex_s) - 1)
+    b2s = t_s[kn][split]
+    b2e = b2s + (width - left[split]) - 1
+    gch = torch.as_tensor(chrom, device=dev)[torch.as_tensor(ex_gene, device=dev)[k]]
+    uc, us = _uniform_positions(n - n_ex_reads, torch.as_tensor(lens_np, device=dev), g, dev, margin=width)
+    c_all = torch.cat([gch, gch[split], uc.to(gch.dtype)])
+    s_all = torch.cat([gs, b2s, us])
+    e_all = torch.cat([b1e, b2e, us + width - 1])
+    st = torch.randint(0, 2, (c_all.numel(),), generator=g, device=dev, dtype=torch.int8)
+    reads = (c_all.to(torch.int32), s_all.clamp(min=1).to(torch.int32), e_all.to(torch.int32), st)
+    genes = dict(chrom=chrom, start=gstart.astype(np.int64), end=gend.astype(np.int64), strand=gstrand)
+    exons = dict(seg_off=seg_off, chrom=chrom[ex_gene], start=ex_s, end=ex_e, strand=gstrand[ex_gene])
+    return dict(name="c3", reads=reads, seqlen=lens_np.copy(), genes=genes, exons=exons, flank=(flank, flank),
+                region_bins=region_bins, flank_bins=flank_bins, n_split=int(split.sum()), width=width)
+
+
+def rna_rows(d, ignore_strand=True):
+    """coverageRnaRef rows of a c3 data set: [upstream flank | exons (list) | downstream flank]."""
+    from recoup_amd.engine import RowTable
+    G, E = d["genes"], d["exons"]
+    f1, f2 = d["flank"]
+    n = len(G["start"])
+    minus = G["strand"] == 1
+    # promoters(up = f1, down = 0) and flank(width = f2, start = FALSE) of the gene
+    ls = np.where(minus, G["end"] + 1, G["start"] - f1)
+    le = np.where(minus, G["end"] + f1, G["start"] - 1)
+    rs = np.where(minus, G["start"] - f2, G["end"] + 1)
+    re_ = np.where(minus, G["start"] - 1, G["end"] + f2)
+    cnt = np.diff(E["seg_off"]) + 2
+    seg_off = np.zeros(n + 1, np.int64)
+    seg_off[1:] = np.cumsum(cnt)
+    m = int(seg_off[-1])
+    first, lastp = seg_off[:-1], seg_off[1:] - 1
+    inner = np.ones(m, bool)
+    inner[first] = False
+    inner[lastp] = False
+    ch = np.empty(m, np.int32); s = np.empty(m, np.int64); e = np.empty(m, np.int64)
+    st = np.empty(m, np.int8); grp = np.ones(m, np.int8)
+    ch[first], s[first], e[first], st[first], grp[first] = G["chrom"], ls, le, G["strand"], 0
+    ch[lastp], s[lastp], e[lastp], st[lastp], grp[lastp] = G["chrom"], rs, re_, G["strand"], 2
+    ch[inner], s[inner], e[inner], st[inner] = E["chrom"], E["start"], E["end"], E["strand"]
+    return RowTable(seg_off, ch, s.astype(np.int32), e.astype(np.int32), st, seg_group=grp,
+                    group_is_list=np.array([0, 1, 0, 0], np.uint8), ignore_strand=ignore_strand)
+
+
+def n_overlaps_segments(reads, seg_chrom, seg_start, seg_end, device="cuda:0"):
+    """Reads overlapping each segment, any widths: #(start <= e) - #(end < s) on one chromosome."""
+    chrom, start, end, _ = reads
+    ks, _ = torch.sort(chrom.to(torch.int64) * (1 << 32) + start.to(torch.int64))
+    ke, _ = torch.sort(chrom.to(torch.int64) * (1 << 32) + end.to(torch.int64))
+    c = torch.as_tensor(seg_chrom, device=device, dtype=torch.int64) * (1 << 32)
+    s = c + torch.as_tensor(seg_start, device=device, dtype=torch.int64)
+    e = c + torch.as_tensor(seg_end, device=device, dtype=torch.int64)
+    a = torch.searchsorted(ks, e, right=True) - torch.searchsorted(ks, c, right=False)
+    b = torch.searchsorted(ke, s, right=False) - torch.searchsorted(ke, c, right=False)
+    return (a - b).cpu().numpy()

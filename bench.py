@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c4", choices=["c4", "c2", "c5"])
+    ap.add_argument("--config", default="c4", choices=["c4", "c2", "c3", "c5"])
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--reads", type=int, default=None, help="override read count (smaller runs)")
     ap.add_argument("--regions", type=int, default=None, help="override region count")
@@ -49,6 +49,45 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+WORKLOADS = {
+    "c4": "C4: 200k ChIP peak summits +-1 kb, 1000 bins (2 bp), 200M reads (180 bp)",
+    "c2": "C2: 10k TSS +-2 kb, 200 bins, 10M reads (180 bp)",
+    "c3": "C3: coverageRnaRef, 25k genes (exon lists + 2 kb flanks), 50 + 500 + 50 bins, 50M read pairs "
+          "(100 bp mates, junction reads split)",
+    "c5": "C5: 25k regions x 4000 bp per base, 500M reads (50 bp)",
+}
+
+
+def workload(args, dev, rank):
+    """(data, RowTable, Bins, total read-segment overlaps) of the chosen BASELINE config."""
+    import synthetic
+    from recoup_amd.engine import Bins, RowTable
+    seed = args.seed + 7919 * rank
+    if args.config == "c3":
+        kw = {}
+        if args.reads:
+            kw["n_pairs"] = args.reads // 2
+        if args.regions:
+            kw["n_genes"] = args.regions
+        d = synthetic.c3(device=dev, seed=seed, **kw)
+        rows = synthetic.rna_rows(d)
+        bins = Bins([("upstream", d["flank_bins"]), ("center", d["region_bins"]), ("downstream", d["flank_bins"])],
+                    flank=d["flank"])
+        ovl = synthetic.n_overlaps_segments(d["reads"], rows.chrom, rows.start, rows.end, device=dev).sum()
+        return d, rows, bins, ovl
+    kw = {}
+    if args.reads:
+        kw["n_reads"] = args.reads
+    if args.regions:
+        kw["n_regions"] = args.regions
+    d = getattr(synthetic, args.config)(device=dev, seed=seed, **kw)
+    reg = d["regions"]
+    rows = RowTable.from_ranges(reg["chrom"], reg["start"], reg["end"], reg["strand"])
+    bins = Bins([("whole", d["n_bins"])]) if d["n_bins"] > 0 else Bins([("whole", 0, sum(d["flank"]))])
+    ovl = synthetic.n_overlaps(d["reads"], reg, d["width"], device=dev).sum()
+    return d, rows, bins, ovl
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -62,31 +101,18 @@ def main():
     dev = f"cuda:{local}"
     torch.cuda.set_device(local)
 
-    import synthetic
-    from recoup_amd.engine import Bins, Plan, ReadSet, RowTable
+    from recoup_amd.engine import Plan, ReadSet
 
     t0 = time.time()
-    kw = {}
-    if args.reads:
-        kw["n_reads"] = args.reads
-    if args.regions:
-        kw["n_regions"] = args.regions
-    data = getattr(synthetic, args.config)(device=dev, seed=args.seed + 7919 * rank, **kw)
+    data, rows, bins, ovl_rows = workload(args, dev, rank)
     reads = data["reads"]
-    reg = data["regions"]
-    R = len(reg["start"])
+    R = rows.n_rows
     n_reads = int(reads[1].numel())
-    n_ovl = synthetic.n_overlaps(reads, reg, data["width"], device=dev)
     torch.cuda.synchronize()
-    log(f"[rank {rank}] data {args.config}: {n_reads} reads, {R} regions in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] data {args.config}: {n_reads} reads, {R} rows in {time.time() - t0:.1f}s")
 
     t1 = time.time()
     rs = ReadSet(*reads, data["seqlen"], device=local)
-    rows = RowTable.from_ranges(reg["chrom"], reg["start"], reg["end"], reg["strand"])
-    if data["n_bins"] > 0:
-        bins = Bins([("whole", data["n_bins"])])
-    else:
-        bins = Bins([("whole", 0, sum(data["flank"]))])
     tp = time.time()
     plan = Plan(rs, rows, bins)
     plan_s = time.time() - tp
@@ -137,8 +163,11 @@ def main():
 
     units = R * B  # region-bins per step per rank (1 sample)
     value = world * units * args.steps / elapsed
-    ovl = int(n_ovl.sum())
-    bytes_pileup = 8 * ovl + 16 * R + 8 * R * B  # reads (start,end) + region meta + f64 out
+    ovl = int(ovl_rows)
+    # 8 B per overlapping (read, segment) + 16 B per region + 8 B per further segment
+    # of a multi-range row + the f64 output written once
+    n_seg = len(rows.start)
+    bytes_pileup = 8 * ovl + 16 * R + 8 * (n_seg - R) + 8 * R * B
     achieved = bytes_pileup / (kt[1] * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic):
@@ -153,7 +182,7 @@ def main():
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, parity = cpu_baseline(args, data, reads, reg, out, valid, B)
+        cpu, parity = cpu_baseline(args, data, rows, bins, out, valid, B)
 
     if rank == 0:
         res = {
@@ -170,9 +199,7 @@ def main():
             "dtype": "int32",
             "data": "synthetic",
             "config": {
-                "workload": {"c4": "C4: 200k ChIP peak summits +-1 kb, 1000 bins (2 bp), 200M reads (180 bp)",
-                             "c2": "C2: 10k TSS +-2 kb, 200 bins, 10M reads (180 bp)",
-                             "c5": "C5: 25k regions x 4000 bp per base, 500M reads (50 bp)"}[args.config],
+                "workload": WORKLOADS[args.config],
                 "regions_per_gpu": R, "bins": B, "reads_per_gpu": n_reads, "samples": 1,
                 "parallelism": f"region-sharded x{world} (one partition per GPU, no data-path collective)",
             },
@@ -191,48 +218,67 @@ def main():
         tdist.destroy_process_group()
 
 
-def cpu_baseline(args, data, reads, reg, out, valid, B):
+def cpu_baseline(args, data, rows, bins, out, valid, B):
     """The oracle (C restatement of the reference's per-region dataflow, multithreaded over
-    regions like cmclapply with rc = NULL) on the first --cpu-regions regions."""
+    regions like cmclapply with rc = NULL) on the first --cpu-regions rows, repeated for about
+    --cpu-seconds; multi-range rows (C3) go through the oracle's per-group coverage + splitVector."""
     from oracle import oracle as o
-    R = len(reg["start"])
+    R = rows.n_rows
     m = min(args.cpu_regions, R)
-    ch = reg["chrom"][:m]
-    keep_chroms = np.unique(ch)
-    chrom, start, end, strand = reads
-    sel = torch.isin(chrom, torch.as_tensor(keep_chroms, device=chrom.device, dtype=chrom.dtype))
+    chrom, start, end, strand = data["reads"]
+    keep = np.unique(rows.chrom[:rows.seg_off[m]])
+    sel = torch.isin(chrom, torch.as_tensor(keep, device=chrom.device, dtype=chrom.dtype))
     # hand the oracle its reads in (chrom, start) order so its own index skips the sort
     c, s, e, st = chrom[sel], start[sel], end[sel], strand[sel]
     key = (c.to(torch.int64) << 42) + (s.to(torch.int64) << 10) + (e - s).to(torch.int64).clamp(0, 1023)
     order = torch.argsort(key)
     c, s, e, st = (x[order].cpu().numpy() for x in (c, s, e, st))
     ix = o.Index(c, s, e, st, data["seqlen"])
-    mask = o.Mask.from_ranges(ch, reg["start"][:m], reg["end"][:m], reg["strand"][:m])
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
     threads = max(1, min(16, cores))
-    n_bins = data["n_bins"]
+    single = bool(np.all(np.diff(rows.seg_off[:m + 1]) == 1)) and len(bins.parts) == 1
+    if single:
+        mask = o.Mask.from_ranges(rows.chrom[:m], rows.start[:m], rows.end[:m], rows.strand[:m])
+        nb = int(bins.n_bins[0])
+
+        def run():
+            if nb > 0:
+                return o.profile_part(ix, mask, nb, nthreads=threads)
+            return o.profile_part(ix, mask, 0, ncol=B, nthreads=threads)
+    else:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_rows
+        from recoup_amd.engine import RowTable
+        sub = RowTable(rows.seg_off[:m + 1], rows.chrom[:rows.seg_off[m]], rows.start[:rows.seg_off[m]],
+                       rows.end[:rows.seg_off[m]], rows.strand[:rows.seg_off[m]],
+                       seg_group=None if rows.seg_group is None else rows.seg_group[:rows.seg_off[m]],
+                       group_is_list=rows.group_is_list, ignore_strand=rows.ignore_strand)
+        threads = 1
+
+        def run():
+            return oracle_rows.profile(oracle_rows.row_coverage(ix, sub), bins)
     # repeat the sample until about args.cpu_seconds of wall time (a single pass over C4 takes
     # well under a second on a many-core host) and report the mean pass
     reps = 0
     t = time.perf_counter()
     while True:
-        if n_bins > 0:
-            ref, rvalid = o.profile_part(ix, mask, n_bins, nthreads=threads)
-        else:
-            ref, rvalid = o.profile_part(ix, mask, 0, ncol=B, nthreads=threads)
+        ref, rvalid = run()
         reps += 1
         if time.perf_counter() - t >= args.cpu_seconds:
             break
     dt = (time.perf_counter() - t) / reps
     gpu = out.cpu().numpy().T[:m]
     gv = valid.cpu().numpy()[:m].astype(bool)
-    parity = bool(np.array_equal(gv, rvalid.astype(bool)) and np.allclose(gpu, ref, rtol=1e-12, atol=0))
+    # NaN where the reference's neighborhood fill averages four NAs (mean(na.rm = TRUE) of nothing)
+    parity = bool(np.array_equal(gv, np.asarray(rvalid).astype(bool)) and
+                  np.allclose(gpu, ref, rtol=1e-9, atol=1e-12, equal_nan=True))
     cpu = {"value": m * B / dt, "unit": "region-bins/s", "cores": threads, "kind": "port",
-           "sample": f"first {m} of {R} regions (all their reads), {n_bins or 'per-base'} bins; oracle/ C "
-                     f"restatement, {threads} threads over regions; mean of {reps} passes, {dt:.3f} s/pass"}
+           "sample": f"first {m} of {R} rows (all their reads), {B} columns; oracle/ C restatement"
+                     f"{', %d threads over regions' % threads if single else ' (per-group coverage, Python splitVector)'}; "
+                     f"mean of {reps} passes, {dt:.3f} s/pass"}
     return cpu, parity
 
 

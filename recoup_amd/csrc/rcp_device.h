@@ -24,6 +24,9 @@ struct RcpSeg {
     uint8_t group;       // group index inside the row (0..3)
     uint8_t query_ok;    // 0 = zero-width query (hits nothing)
     uint8_t pad;
+    // multi groups: a read [x, y] of this range overlaps no other range of its group when
+    // nb_lo < x and y < nb_hi (nb_lo = INT32_MAX when the group's ranges intersect this one)
+    int32_t nb_lo, nb_hi;
 };
 
 // Per-row record the locate kernel leaves for the pileup kernel (one 64-byte load per row
@@ -98,6 +101,7 @@ struct RcpPlanDev {
     const int32_t* nb_pos;      // orig.pos tables (1-based, sorted)
     double* interp_scratch;     // per interp row: 5 * max_interp_len doubles
     int32_t interp_stride;
+    int32_t interp_lds;         // byte offset of the row's doubles in LDS, -1 = global scratch (launcher)
     // geometry
     int32_t chunk_cap;          // max positions per chunk (one wave's difference array)
     int32_t wave_words;         // LDS words per wave difference array (multiple of 256)

@@ -54,7 +54,7 @@ hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const int64_t* d
 namespace {
 
 constexpr int kChunkMax = 16384;       // positions of an interpolated slice (block LDS array)
-constexpr int kWaveMax = 2048;         // positions per wave sub-chunk (padded LDS array <= 9 KB; 8 waves)
+constexpr int kWaveMax = 2047;         // positions per wave sub-chunk (64 x 32 slots incl. the end sentinel)
 #ifndef RCP_STAGE_MAX_BINS
 #define RCP_STAGE_MAX_BINS 512
 #endif
@@ -455,6 +455,20 @@ int build_rows(const rcp_readset* rs, const rcp_rows_desc* rows, Builder* B) {
             // fix gcount for skipped empty pieces
             const int32_t kept = (int32_t)B->segs.size() - gfirst;
             for (int32_t q = gfirst; q < gfirst + kept; ++q) B->segs[q].gcount = (int16_t)kept;
+            // nearest other ranges of the group (the pileup's one-range weight shortcut)
+            for (int32_t q = gfirst; q < gfirst + kept; ++q) {
+                RcpSeg& a = B->segs[q];
+                a.nb_lo = INT32_MIN;
+                a.nb_hi = INT32_MAX;
+                if (!multi) continue;
+                for (int32_t t = gfirst; t < gfirst + kept; ++t) {
+                    if (t == q || !B->segs[t].query_ok) continue;
+                    const RcpSeg& b = B->segs[t];
+                    if (b.hi < a.lo) a.nb_lo = std::max(a.nb_lo, b.hi);
+                    else if (b.lo > a.hi) a.nb_hi = std::min(a.nb_hi, b.lo);
+                    else a.nb_lo = INT32_MAX;  // intersecting ranges: always count
+                }
+            }
             g0 = g1;
         }
         B->row_len[r] = off;
@@ -625,7 +639,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
         int32_t min_cap = 64;
         if (median)
             for (int p = 0; p < P.n_parts; ++p) min_cap = std::max(min_cap, P.part[p].chunk_bins * part_max_bin[p]);
-        const int32_t cands[] = {need, 2048, 1024};
+        const int32_t cands[] = {need, 2047, 1023, 511};  // 64 * 2^k - 1: the +1 sentinel fits
         chunk_cap = -1;
         for (int32_t ch : cands) {
             if (ch > need || ch < min_cap) continue;

@@ -100,7 +100,7 @@ __device__ __forceinline__ void add_read(const RcpPlanDev& P, const RcpSeg& sg, 
                                          int32_t P0, int32_t* diff, int sh) {
     if (rd.y < gps || rd.x > gpe) return;
     int32_t w = 1;
-    if (sg.multi) {
+    if (sg.multi && !(rd.x > sg.nb_lo && rd.y < sg.nb_hi)) {
         // subjectHits repeats a read once per range of the list it overlaps
         // (R/coverage.R:190-192): weight = number of overlapped ranges.
         w = 0;
@@ -150,18 +150,29 @@ __device__ __forceinline__ void pileup_row(const RcpPlanDev& P, int r, int32_t P
             uint32_t lo = P.seg_lo[j * 3 + s];
             uint32_t hi = P.seg_hi[j * 3 + s];
             if (lo >= hi) continue;
-            if (!full) {
+            // narrowing a partly covered segment costs two dependent binary searches; below a
+            // few batches of reads it is cheaper to stream them all (the piece test drops the rest)
+            if (!full && hi - lo > 1024) {
                 lo = lower_bound_pmax(P.pmax, lo, hi, gps);
                 hi = upper_bound_start(P.se, lo, hi, gpe);
                 if (lo >= hi) continue;
             }
-            for (uint32_t base = lo + t; base < hi; base += 4 * nt) {
-                int2 rd[4];
+            // batch base + 4 nt is loaded while batch base is added
+            int2 rd[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) rd[u] = P.se[min(base + u * nt, hi - 1)];  // clamped: no branch
+            for (int u = 0; u < 4; ++u) rd[u] = P.se[min(lo + t + u * nt, hi - 1)];  // clamped: no branch
+            for (uint32_t base = lo + t; base < hi; base += 4 * nt) {
+                int2 nx[4];
+                const uint32_t nb = base + 4 * nt;
+                if (nb - t < hi) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) nx[u] = P.se[min(nb + u * nt, hi - 1)];
+                }
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     if (base + u * nt < hi) add_read(P, sg, rd[u], gps, gpe, P0, diff, sh);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) rd[u] = nx[u];
             }
         }
     }
@@ -457,8 +468,11 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
     if (in_row && q == 0) {
         P.valid[r] = valid ? 1 : 0;
         P.ncand[r] = ncand;
+        // skewed rows only: many candidates AND a deep pileup (> 2 reads per position), so a
+        // long row with proportionally many reads stays on the workgroup path
+        const int32_t rl = P.row_len[r];
         if (valid && P.heavy_threshold > 0 && ncand > (uint32_t)P.heavy_threshold &&
-            P.row_len[r] <= P.heavy_max_len) {
+            ncand > 2u * (uint32_t)max(rl, 0) && rl <= P.heavy_max_len) {
             const uint32_t u = atomicAdd(&P.status[1], 1u);
             if (u < (uint32_t)P.heavy_cap) {
                 slot = (int32_t)u;
@@ -686,7 +700,7 @@ constexpr int kRounds = RCP_PILE_ROUNDS;
 static_assert(kTile % kPWaves == 0, "a round's rows are split evenly over the waves");
 constexpr int kRowsPerWave = kTile / kPWaves;  // rows a wave piles per round
 #ifndef RCP_PF_AHEAD
-#define RCP_PF_AHEAD 2
+#define RCP_PF_AHEAD 1
 #endif
 constexpr int kAhead = RCP_PF_AHEAD;  // rows whose first reads are prefetched
 #ifndef RCP_STAGE_BUFS
@@ -814,7 +828,7 @@ __device__ __forceinline__ void scan_bins_fast(int32_t* diff, int lbs, uint32_t*
 }
 
 template <bool MEDIAN, bool CSR>
-__global__ void __launch_bounds__(kPBlock) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
+__global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4))) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
                                                             int64_t* __restrict__ binsum) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int T = kTile;
@@ -1356,10 +1370,13 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
         return;
     }
     block_window_depth(P, r, head, L, diff, scratch);
-    if (threadIdx.x != 0) return;
-    double* x = P.interp_scratch + (size_t)e * P.interp_stride;
+    // the sequential spline / fill works on LDS copies (global scratch only for huge rows)
+    double* x = P.interp_lds >= 0 ? reinterpret_cast<double*>(smem + P.interp_lds)
+                                  : P.interp_scratch + (size_t)e * P.interp_stride;
     double* y = x + L + 1;
-    for (int i = 0; i < L; ++i) x[i] = (double)diff[i] * P.scale;
+    for (int i = threadIdx.x; i < L; i += kBlock) x[i] = (double)diff[i] * P.scale;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     if (mode == 1) {  // spline(x, n = n)$y, then x[x < 0] <- 0
         double* b = y + n + 1;
         double* c = b + L + 1;
@@ -1468,8 +1485,17 @@ extern "C" hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_
     return launch_pileup_t<false, false>(P, out, binsum, lds, stream);
 }
 
-extern "C" size_t rcp_interp_lds_bytes(const RcpPlanDev* P) {
+// [depth window | block-scan scratch | (when it fits) the row's spline / fill doubles]
+static size_t interp_int_bytes(const RcpPlanDev* P) {
     return 4 * ((size_t)((P->interp_cap + 8 + 1023) & ~1023) + 2 * kWaves + 8);
+}
+
+static bool interp_in_lds(const RcpPlanDev* P) {
+    return interp_int_bytes(P) + 8 * (size_t)P->interp_stride + 16 <= 160 * 1024;
+}
+
+extern "C" size_t rcp_interp_lds_bytes(const RcpPlanDev* P) {
+    return interp_int_bytes(P) + (interp_in_lds(P) ? 8 * (size_t)P->interp_stride + 16 : 0);
 }
 
 extern "C" hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStream_t stream) {
@@ -1480,7 +1506,9 @@ extern "C" hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStr
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL(rcp_interp_kernel, dim3(P->n_interp), dim3(kBlock), rcp_interp_lds_bytes(P), stream, *P, out);
+    RcpPlanDev Q = *P;
+    Q.interp_lds = interp_in_lds(P) ? (int32_t)((interp_int_bytes(P) + 15) / 16 * 16) : -1;
+    hipLaunchKernelGGL(rcp_interp_kernel, dim3(P->n_interp), dim3(kBlock), rcp_interp_lds_bytes(P), stream, Q, out);
     return hipGetLastError();
 }
 

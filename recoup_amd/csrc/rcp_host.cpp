@@ -738,7 +738,9 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.rec = reinterpret_cast<RcpRowRec*>(wb + w_rec);
     P.crange = keep_crange ? reinterpret_cast<uint2*>(wb + w_crange) : nullptr;
     const int32_t n_interp = (int32_t)B.interp_row.size();
-    P.interp_stride = 2 * (max_interp_bins + 1) + 3 * (max_interp_len + 1) + 8;
+    // x (L+1) | y (n+1) | b, c, d (3 (L+1)) | interval index per output point (n ints); the
+    // neighborhood fill's n pre-fill values reuse b..
+    P.interp_stride = 2 * (max_interp_bins + 1) + 4 * (max_interp_len + 1) + 8;
     if (n_interp) HIP_TRY(plan->scratch.alloc(8 * (size_t)n_interp * P.interp_stride));
 
     const ReadLayout& RL = rows->ignore_strand ? rs->merged : rs->stranded;

@@ -1202,55 +1202,77 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
 namespace {
 
 #pragma clang fp contract(off)
-__device__ void fmm_spline_dev(int n, const double* y, double* b, double* c, double* d) {
-    // stats::spline method "fmm" coefficients on knots x = 1..n (R splines.c fmm_spline),
-    // 1-based indexing kept as in the original; knot spacings are all 1.
-    const double* Y = y - 1;
-    double *B = b - 1, *Cc = c - 1, *D = d - 1;
-    if (n < 2) {
-        for (int i = 1; i <= n; ++i) B[i] = Cc[i] = D[i] = 0.0;
-        return;
-    }
+// stats::spline method "fmm" (R splines.c fmm_spline) on knots x = 1..n: every knot spacing
+// d[i] is 1.0, so the operations below are the original ones with the multiplications and
+// divisions by d[i] = 1.0 (exact) dropped.  Data-parallel loops run over the block's
+// threads; the two recurrences (forward elimination, back substitution) run on thread 0
+// with register carries.  Same operations in the same order per element as R: bit-equal.
+// Call from all threads of the block; y, b, c, d in LDS (or global), 0-based.
+__device__ void fmm_spline_block(int n, const double* y, double* b, double* c, double* d) {
+    const int t = threadIdx.x;
     if (n < 3) {
-        const double t = (Y[2] - Y[1]);
-        B[1] = t / 1.0;
-        B[2] = B[1];
-        Cc[1] = Cc[2] = D[1] = D[2] = 0.0;
+        if (t == 0) {
+            if (n == 2) {
+                b[0] = b[1] = y[1] - y[0];
+            } else if (n == 1) {
+                b[0] = 0.0;
+            }
+            for (int i = 0; i < n; ++i) c[i] = d[i] = 0.0;
+        }
+        __syncthreads();
         return;
     }
-    const int nm1 = n - 1;
-    D[1] = 1.0;
-    Cc[2] = (Y[2] - Y[1]) / D[1];
-    for (int i = 2; i < n; i++) {
-        D[i] = 1.0;
-        B[i] = 2.0 * (D[i - 1] + D[i]);
-        Cc[i + 1] = (Y[i + 1] - Y[i]) / D[i];
-        Cc[i] = Cc[i + 1] - Cc[i];
+    // 1-based i = 2 .. n-1 (0-based i - 1): c[i] = (y[i+1] - y[i]) - (y[i] - y[i-1]), b[i] = 4
+    for (int i = 1 + t; i < n - 1; i += blockDim.x) {
+        c[i] = (y[i + 1] - y[i]) - (y[i] - y[i - 1]);
+        b[i] = 2.0 * (1.0 + 1.0);
+        d[i] = 1.0;
     }
-    B[1] = -D[1];
-    B[n] = -D[nm1];
-    Cc[1] = Cc[n] = 0.0;
-    if (n > 3) {
-        Cc[1] = Cc[3] / 2.0 - Cc[2] / 2.0;          // x[4]-x[2], x[3]-x[1]
-        Cc[n] = Cc[nm1] / 2.0 - Cc[n - 2] / 2.0;    // x[n]-x[n-2], x[n-1]-x[n-3]
-        Cc[1] = Cc[1] * D[1] * D[1] / 3.0;          // x[4]-x[1]
-        Cc[n] = -Cc[n] * D[nm1] * D[nm1] / 3.0;     // x[n]-x[n-3]
+    __syncthreads();
+    if (t == 0) {
+        b[0] = -1.0;
+        b[n - 1] = -1.0;
+        d[0] = 1.0;
+        double c1 = 0.0, cn = 0.0;
+        if (n > 3) {
+            c1 = c[2] / 2.0 - c[1] / 2.0;
+            cn = c[n - 2] / 2.0 - c[n - 3] / 2.0;
+            c1 = c1 / 3.0;  // * d[1] * d[1] (= 1) / 3
+            cn = -cn / 3.0;
+        }
+        c[0] = c1;
+        c[n - 1] = cn;
+        // forward elimination: t = d[i-1] / b[i-1]; b[i] -= t d[i-1]; c[i] -= t c[i-1]
+        double bp = b[0], cp = c1;
+        for (int i = 1; i < n; ++i) {
+            const double tt = 1.0 / bp;
+            const double bi = b[i] - tt;
+            const double ci = c[i] - tt * cp;
+            b[i] = bi;
+            c[i] = ci;
+            bp = bi;
+            cp = ci;
+        }
+        // back substitution
+        double cnext = cp / bp;
+        c[n - 1] = cnext;
+        for (int i = n - 2; i >= 0; --i) {
+            cnext = (c[i] - cnext) / b[i];
+            c[i] = cnext;
+        }
+        b[n - 1] = (y[n - 1] - y[n - 2]) + (c[n - 2] + 2.0 * c[n - 1]);
     }
-    for (int i = 2; i <= n; i++) {
-        const double t = D[i - 1] / B[i - 1];
-        B[i] = B[i] - t * D[i - 1];
-        Cc[i] = Cc[i] - t * Cc[i - 1];
+    __syncthreads();
+    // coefficients: b[i] = (y[i+1] - y[i]) - (c[i+1] + 2 c[i]); d[i] = c[i+1] - c[i]; c[i] *= 3
+    for (int i = t; i < n - 1; i += blockDim.x) {
+        const double ci = c[i], cn1 = c[i + 1];
+        b[i] = (y[i + 1] - y[i]) - (cn1 + 2.0 * ci);
+        d[i] = cn1 - ci;
     }
-    Cc[n] = Cc[n] / B[n];
-    for (int i = nm1; i >= 1; i--) Cc[i] = (Cc[i] - D[i] * Cc[i + 1]) / B[i];
-    B[n] = (Y[n] - Y[n - 1]) / D[n - 1] + D[n - 1] * (Cc[n - 1] + 2.0 * Cc[n]);
-    for (int i = 1; i <= nm1; i++) {
-        B[i] = (Y[i + 1] - Y[i]) / D[i] - D[i] * (Cc[i + 1] + 2.0 * Cc[i]);
-        D[i] = (Cc[i + 1] - Cc[i]) / D[i];
-        Cc[i] = 3.0 * Cc[i];
-    }
-    Cc[n] = 3.0 * Cc[n];
-    D[n] = D[nm1];
+    __syncthreads();
+    for (int i = t; i < n; i += blockDim.x) c[i] = 3.0 * c[i];
+    if (t == 0) d[n - 1] = d[n - 2];
+    __syncthreads();
 }
 
 __device__ double seq_point(int L, int n, int i) {
@@ -1261,19 +1283,28 @@ __device__ double seq_point(int L, int n, int i) {
     return (i < n / 2) ? 1.0 + (double)i * by : (double)L - (double)(n - 1 - i) * by;
 }
 
-__device__ double spline_eval_dev(int n, const double* y, const double* b, const double* c, const double* d,
-                                  double u, int& i) {
-    // spline_eval (R splines.c): keep the previous interval while x[i] <= u <= x[i+1],
-    // else bisect; knots are x = 1..n.
-    const int n_1 = n - 1;
-    if (u < (double)(i + 1) || (i < n_1 && (double)(i + 2) < u)) {
-        i = 0;
-        int j = n;
-        do {
-            const int k = (i + j) / 2;
-            if (u < (double)(k + 1)) j = k; else i = k;
-        } while (j > i + 1);
+// spline_eval's interval for each output point, in R's order: the previous interval is kept
+// while x[i] <= u <= x[i+1], else bisection (knots x = 1..n) -- integer-only, on thread 0.
+__device__ void spline_intervals(int L, int n, int32_t* iv) {
+    int i = 0;
+    const int n_1 = L - 1;
+    for (int k = 0; k < n; ++k) {
+        const double u = seq_point(L, n, k);
+        if (u < (double)(i + 1) || (i < n_1 && (double)(i + 2) < u)) {
+            i = 0;
+            int j = L;
+            do {
+                const int m = (i + j) / 2;
+                if (u < (double)(m + 1)) j = m; else i = m;
+            } while (j > i + 1);
+        }
+        iv[k] = i;
     }
+}
+
+// spline_eval's cubic on interval i (no FMA contraction: R's rounding)
+__device__ double spline_eval_at(const double* y, const double* b, const double* c, const double* d, int i,
+                                 double u) {
     const double dx = u - (double)(i + 1);
     return y[i] + dx * (b[i] + dx * (c[i] + dx * d[i]));
 }
@@ -1370,51 +1401,62 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
         return;
     }
     block_window_depth(P, r, head, L, diff, scratch);
-    // the sequential spline / fill works on LDS copies (global scratch only for huge rows)
+    // the spline / fill works on LDS copies (global scratch only for huge rows)
     double* x = P.interp_lds >= 0 ? reinterpret_cast<double*>(smem + P.interp_lds)
                                   : P.interp_scratch + (size_t)e * P.interp_stride;
     double* y = x + L + 1;
+    double* b = y + n + 1;
     for (int i = threadIdx.x; i < L; i += kBlock) x[i] = (double)diff[i] * P.scale;
     __syncthreads();
-    if (threadIdx.x != 0) return;
     if (mode == 1) {  // spline(x, n = n)$y, then x[x < 0] <- 0
-        double* b = y + n + 1;
         double* c = b + L + 1;
         double* d = c + L + 1;
-        fmm_spline_dev(L, x, b, c, d);
-        int iv = 0;
-        for (int i = 0; i < n; ++i) {
-            const double v = (L == 1) ? x[0] : spline_eval_dev(L, x, b, c, d, seq_point(L, n, i), iv);
-            y[i] = v < 0 ? 0.0 : v;
+        int32_t* iv = reinterpret_cast<int32_t*>(d + L + 1);
+        fmm_spline_block(L, x, b, c, d);
+        if (threadIdx.x == 0) spline_intervals(L, n, iv);
+        __syncthreads();
+        for (int k = threadIdx.x; k < n; k += kBlock) {
+            double v;
+            if (L == 1) {
+                v = x[0];
+            } else {
+                v = spline_eval_at(x, b, c, d, iv[k], seq_point(L, n, k));
+            }
+            y[k] = v < 0 ? 0.0 : v;
         }
-    } else if (mode == 3) {  // neighborhood fill (util.R:53-69)
+    } else if (mode == 3) {  // neighborhood fill (util.R:53-69), from the pre-fill vector
         const int32_t* pos = P.nb_pos + P.interp_pos[e];
-        double* pre = y + n + 1;
-        for (int i = 0; i < n; ++i) pre[i] = __builtin_nan("");
-        pre[0] = x[0];
-        pre[1] = x[1];
-        pre[n - 2] = x[L - 2];
-        pre[n - 1] = x[L - 1];
-        for (int i = 0; i < L - 4; ++i) pre[pos[i] - 1] = x[2 + i];
-        for (int z = 0; z < n; ++z) {
+        double* pre = b;
+        for (int i = threadIdx.x; i < n; i += kBlock) pre[i] = __builtin_nan("");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            pre[0] = x[0];
+            pre[1] = x[1];
+            pre[n - 2] = x[L - 2];
+            pre[n - 1] = x[L - 1];
+        }
+        for (int i = threadIdx.x; i < L - 4; i += kBlock) pre[pos[i] - 1] = x[2 + i];
+        __syncthreads();
+        for (int z = threadIdx.x; z < n; z += kBlock) {
             if (!isnan(pre[z])) {
                 y[z] = pre[z];
                 continue;
             }
-            double s = 0.0;
+            double sm = 0.0;
             int m = 0;
             const int nb[4] = {z - 2, z - 1, z + 1, z + 2};
             for (int q = 0; q < 4; ++q)
                 if (nb[q] >= 0 && nb[q] < n && !isnan(pre[nb[q]])) {
-                    s += pre[nb[q]];
+                    sm += pre[nb[q]];
                     ++m;
                 }
-            y[z] = m ? s / m : __builtin_nan("");
+            y[z] = m ? sm / m : __builtin_nan("");
         }
     } else {  // "linear": the switch arm is spelled "inear" -> x unchanged; rbind recycles
-        for (int i = 0; i < n; ++i) y[i] = x[i % L];
+        for (int i = threadIdx.x; i < n; i += kBlock) y[i] = x[i % L];
     }
-    for (int k = 0; k < n; ++k) out[(size_t)(part.col_off + k) * R + r] = y[k];
+    __syncthreads();
+    for (int k = threadIdx.x; k < n; k += kBlock) out[(size_t)(part.col_off + k) * R + r] = y[k];
 }
 
 // =================================================================================

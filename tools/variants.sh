@@ -17,8 +17,11 @@ if [ "$mode" = build ]; then
             -c "$ROOT/recoup_amd/csrc/rcp_kernels.hip" -o "$OUT/$name/k.o" &&
         /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wno-unused-result $defs \
             -c "$ROOT/recoup_amd/csrc/rcp_host.cpp" -o "$OUT/$name/h.o" &&
-        /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/$name/librecoup_amd.so" "$OUT/$name/k.o" "$OUT/$name/h.o" &&
-        rm -f "$OUT/$name/k.o" "$OUT/$name/h.o"
+        /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wno-unused-result \
+            -c "$ROOT/recoup_amd/csrc/rcp_bam.cpp" -o "$OUT/$name/b.o" &&
+        /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/$name/librecoup_amd.so" "$OUT/$name/k.o" "$OUT/$name/h.o" \
+            "$OUT/$name/b.o" -lz -pthread &&
+        rm -f "$OUT/$name/k.o" "$OUT/$name/h.o" "$OUT/$name/b.o"
         ) &
     done
     wait

@@ -94,10 +94,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # rehearsal of the N > 1 path on fewer GPUs: RCP_DIST_BACKEND=gloo RCP_SHARE_GPU=1 puts
+    # several ranks on one device and the barrier / max-reduction on the host
+    backend = os.environ.get("RCP_DIST_BACKEND", "nccl")
+    if os.environ.get("RCP_SHARE_GPU") == "1":
+        local = local % torch.cuda.device_count()
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            tdist.init_process_group(backend)
     dev = f"cuda:{local}"
     torch.cuda.set_device(local)
 
@@ -139,7 +147,7 @@ def main():
         tdist.barrier()
     elapsed = time.perf_counter() - ts
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     plan.status()

@@ -627,8 +627,19 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
         for (int p = 0; p < P.n_parts; ++p) {
             RcpPart& pt = P.part[p];
             // equal chunks of at most kStageMaxBins bins
-            const int32_t nch = (pt.n_bins + kStageMaxBins - 1) / kStageMaxBins;
+            int32_t nch = (pt.n_bins + kStageMaxBins - 1) / kStageMaxBins;
             int32_t cb = (pt.n_bins + nch - 1) / nch;
+            // wide binned chunks would be piled in several wave sub-chunks, each streaming the
+            // chunk's reads again: split them into more (up to 8) column chunks instead -- more
+            // workgroups for small row counts, and per-chunk read ranges from locate
+            if (!median && !pt.per_base && part_max_bin[p] > 0 && (int64_t)cb * part_max_bin[p] > 1023) {
+                const int32_t cb2 = std::max<int32_t>(1, 1023 / part_max_bin[p]);
+                const int32_t nch2 = (pt.n_bins + cb2 - 1) / cb2;
+                if (nch2 <= RCP_MAX_CRANGE_CHUNKS) {
+                    nch = nch2;
+                    cb = (pt.n_bins + nch - 1) / nch;
+                }
+            }
             if (median) cb = std::min<int32_t>(cb, std::max<int32_t>(1, kWaveMax / part_max_bin[p]));
             pt.chunk_bins = cb;
             pt.n_chunks = (pt.n_bins + cb - 1) / cb;

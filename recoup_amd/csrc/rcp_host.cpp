@@ -69,7 +69,10 @@ constexpr int kHeavyThreshold = 4096;  // candidate reads above which a row is s
 #endif
 constexpr int kHeavySlice = RCP_HEAVY_SLICE;  // candidate reads per heavy work item
 constexpr int kHeavyMaxLen = 16383;    // longer rows never take the heavy path
-constexpr int kHeavyGrid = 1024;
+#ifndef RCP_HEAVY_GRID
+#define RCP_HEAVY_GRID 4096
+#endif
+constexpr int kHeavyGrid = RCP_HEAVY_GRID;
 
 // A wave's difference array: 64 lanes x per positions (per a power of two >= 4), each lane's
 // chunk padded by 4 words (rcp_kernels.hip scan_wave).  Returns the LDS words and the

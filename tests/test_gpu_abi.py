@@ -1,0 +1,98 @@
+"""The C ABI as an R .Call shim uses it: the one-shot host-pointer entry point
+rcp_profile, the coverage + Rle entry points, and the error contract (negative codes, a
+message from rcp_last_error, no partial output) on a real device."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from recoup_amd import _lib
+from recoup_amd.engine import Bins, Plan, RowTable
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "c1_expected.npz")
+
+
+@pytest.fixture(scope="module")
+def c1(gpu):
+    d, S, G, E = helpers.c1()
+    return dict(S=S, G=G, rs=[helpers.readset(s) for s in S], gold=dict(np.load(GOLD)))
+
+
+def _profile(rs, rows, bins):
+    """What the shim does: R allocates the R x B double matrix and the logical vector."""
+    rd, bd = rows.desc(), bins.desc()
+    out = np.full((rows.n_rows, bins.n_cols), np.nan, order="F")  # R column-major
+    valid = np.zeros(rows.n_rows, np.uint8)
+    rc = _lib.lib().rcp_profile(rs.h, ctypes.byref(rd), ctypes.byref(bd), out.ctypes.data_as(_lib._dp),
+                                valid.ctypes.data_as(_lib._u8p))
+    return rc, out, valid
+
+
+def test_rcp_profile_host_buffers(c1):
+    rows = helpers.tss_rows(c1["G"])
+    for k, rs in enumerate(c1["rs"]):
+        rc, out, valid = _profile(rs, rows, Bins([("whole", 200)]))
+        assert rc == 0
+        np.testing.assert_allclose(out, c1["gold"][f"tss_heat_s{k}"], rtol=1e-12, atol=0)
+        np.testing.assert_array_equal(valid, c1["gold"][f"tss_valid_s{k}"])
+        rc, out, _ = _profile(rs, rows, Bins([("whole", 0, 4000)]))
+        assert rc == 0
+        np.testing.assert_array_equal(out, c1["gold"][f"tss_base_s{k}"].astype(np.float64))
+
+
+def test_rcp_profile_errors_leave_output_untouched(c1):
+    rows = helpers.tss_rows(c1["G"])
+    # per-base part whose width differs from the rows' length: the library refuses
+    rc, out, _ = _profile(c1["rs"][0], rows, Bins([("whole", 0, 3999)]))
+    assert rc == -4 and b"width" in _lib.lib().rcp_last_error()
+    assert np.isnan(out).all()
+    # nine parts: more than RCP_MAX_PARTS
+    rc, out, _ = _profile(c1["rs"][0], rows, Bins([("whole", 10)] * 9))
+    assert rc == -1 and np.isnan(out).all()
+
+
+def test_invalid_row_tables(c1):
+    rs = c1["rs"][0]
+    bad_groups = RowTable(np.array([0, 2]), np.zeros(2, np.int32), np.array([10, 50]), np.array([20, 60]),
+                          np.zeros(2, np.int8), seg_group=np.array([1, 0], np.int8))
+    with pytest.raises(_lib.RcpError):
+        Plan(rs, bad_groups, Bins([("whole", 2)]))
+    two_chroms = RowTable(np.array([0, 2]), np.array([0, 1], np.int32), np.array([10, 50]), np.array([20, 60]),
+                          np.zeros(2, np.int8), seg_group=np.zeros(2, np.int8),
+                          group_is_list=np.array([1, 0, 0, 0], np.uint8))
+    with pytest.raises(_lib.UnsupportedError):
+        Plan(rs, two_chroms, Bins([("whole", 2)]))
+
+
+def test_execute_contract(c1):
+    rs = c1["rs"][0]
+    rows = helpers.tss_rows(c1["G"])
+    cov_only = Plan(rs, rows, None)
+    with pytest.raises(_lib.RcpError):  # a calcCoverage plan has no columns to execute
+        cov_only.execute(torch.empty((1, rows.n_rows), dtype=torch.float64, device="cuda:0"))
+    p = Plan(rs, rows, Bins([("whole", 200)]))
+    assert _lib.lib().rcp_plan_execute(p.h, None, None, None, None) == -1  # NULL output
+    np.testing.assert_array_equal(p.validity(), c1["gold"]["tss_valid_s0"].astype(bool))
+    np.testing.assert_array_equal(p.row_lengths(), np.full(rows.n_rows, 4000))
+
+
+def test_readset_info_and_strand_filter(c1):
+    from recoup_amd.engine import ReadSet
+    s = c1["S"][0]
+    chrom = np.zeros(len(s["start"]), np.int32)
+    full = ReadSet(chrom, s["start"], s["end"], s["strand"], s["seqlengths"])
+    minus = ReadSet(chrom, s["start"], s["end"], s["strand"], s["seqlengths"], strand_filter="-")
+    assert full.n == len(s["start"])
+    assert minus.n == int((s["strand"] == 1).sum())
+    assert full.stream_off[-1] == full.n and full.stream_off[0] == 0
+    # reads of an unknown chromosome code or strand code are dropped, not an error
+    bad = chrom.copy()
+    bad[:10] = 7
+    st = s["strand"].copy()
+    st[10:20] = 5
+    r = ReadSet(bad, s["start"], s["end"], st, s["seqlengths"])
+    assert r.n == len(s["start"]) - 20

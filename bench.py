@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--cpu-regions", type=int, default=200000, help="CPU baseline sample (regions)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline: repeat the sample this long")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the one-off host-to-host timing")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_c4.json"),
                     help="PMC traffic summary (from tools/pmc_traffic.py) to attach to the roofline")
     return ap.parse_args()
@@ -186,6 +187,17 @@ def main():
         except Exception:
             traffic = None
 
+    # ---- end to end once (not `value`): what a host caller (the R shim's rcp_profile) pays --
+    # host read arrays -> H2D + device sort (readset), plan, one pass, D2H of the matrix
+    e2e = None
+    if not args.no_e2e:
+        e2e = end_to_end(data, rows, bins, local, R * B)
+        if dist:
+            t = torch.tensor([e2e["ms"]], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            e2e["ms"] = float(t.item())
+            e2e["region_bins_per_s"] = world * R * B / (e2e["ms"] * 1e-3)
+
     # ---- CPU baseline (rank 0, N = 1): the oracle on a bounded sample of the same workload
     cpu = None
     parity = None
@@ -216,6 +228,7 @@ def main():
                          "kernel": "rcp_pileup_kernel", "algorithmic_bytes_per_launch": bytes_pileup,
                          "kernel_ms": kt[1]},
             "cpu_baseline": cpu,
+            "e2e": e2e,
             "kernel_ms": {"locate": kt[0], "pileup": kt[1], "interp": kt[2]},
             "n_overlaps": ovl,
             "plan_ms": plan_s * 1e3,
@@ -224,6 +237,34 @@ def main():
         print(json.dumps(res), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def end_to_end(data, rows, bins, local, units):
+    """One host-to-host pass, timed in phases: pageable host read arrays (as R holds them) ->
+    ReadSet (H2D + device radix sort + stream index) -> Plan -> execute -> D2H of the R
+    column-major matrix into pageable host memory.  Reported beside `value`, never as it."""
+    from recoup_amd.engine import Plan, ReadSet
+    host = [x.cpu().numpy() for x in data["reads"]]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rs = ReadSet(*host, data["seqlen"], device=local)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    plan = Plan(rs, rows, bins)
+    t2 = time.perf_counter()
+    out = plan.empty_output()
+    plan.execute(out)
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    mat = out.cpu()
+    t4 = time.perf_counter()
+    plan.status()
+    del plan, rs, out, mat
+    ms = (t4 - t0) * 1e3
+    return {"ms": ms, "region_bins_per_s": units / (ms * 1e-3),
+            "phases_ms": {"readset_h2d_sort": (t1 - t0) * 1e3, "plan": (t2 - t1) * 1e3,
+                          "execute": (t3 - t2) * 1e3, "d2h_matrix": (t4 - t3) * 1e3},
+            "note": "one pass from pageable host arrays to a host matrix; includes PCIe both ways"}
 
 
 def cpu_baseline(args, data, rows, bins, out, valid, B):

@@ -383,6 +383,26 @@ __device__ __forceinline__ uint32_t dir_upper(const RcpPlanDev& P, int st, int32
     return upper_bound_start(P.se, (uint32_t)P.dir_u[d0 + b], (uint32_t)P.dir_u[d0 + b + 1], v);
 }
 
+// dir_lower (upper = false) or dir_upper (upper = true) as ONE instruction stream: first
+// index of the bucket with key >= thr, key = pmax or start.  Lanes of a quad that look for
+// different bounds then search in lockstep, their loads in flight together (two separate
+// functions would run one after the other under the exec mask).
+__device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32_t v, bool upper) {
+    const int64_t d0 = P.dir_off[st];
+    const int32_t nb = (int32_t)(P.dir_off[st + 1] - d0) - 1;
+    const int32_t b = min(max(v, 0) >> P.dir_shift, nb - 1);
+    const int32_t* dir = upper ? P.dir_u : P.dir_l;
+    uint32_t lo = (uint32_t)dir[d0 + b], hi = (uint32_t)dir[d0 + b + 1];
+    const int32_t* key = upper ? reinterpret_cast<const int32_t*>(P.se) : P.pmax;
+    const int ksh = upper ? 1 : 0;                      // start of read m is word 2m of se
+    const int64_t thr = (int64_t)v + (upper ? 1 : 0);  // start > v  <=>  start >= v + 1
+    while (lo < hi) {
+        const uint32_t m = lo + ((hi - lo) >> 1);
+        if ((int64_t)key[(size_t)m << ksh] < thr) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
 // Four lanes per row.  The row's (segment, stream) searches are dealt round-robin to the
 // quad's lanes (one stream per segment in the merged layout, three in the stranded one), so
 // multi-range rows search in parallel; the quad then combines hits / max ends / candidate
@@ -412,7 +432,108 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
     int32_t maxpos[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
     uint32_t ncand = 0, lo = 0, hi = 0;
     const int64_t sl = ok ? P.seqlen[chrom] : -1;
-    for (int pi = q; pi < npairs; pi += 4) {
+    // ---- single-range rows: the per-chunk candidate ranges (each column chunk streams only
+    // the reads that reach its piece of the row) need bound searches at the interior chunk
+    // edges; they do not depend on the row's own bounds, so they run in the same round
+    RcpSeg sg0{};
+    bool fast = false;
+    if (in_row && j1 == j0 + 1) {
+        sg0 = P.segs[j0];
+        fast = !sg0.multi && sg0.query_ok;
+    }
+    const int nc = P.n_chunks_total;
+    const int32_t nr = in_row ? P.row_len[r] : 0;
+    const int32_t len = sg0.hi - sg0.lo + 1;
+    // genomic piece of chunk c (false: the chunk streams the whole range / nothing special)
+    auto piece = [&](int c, int32_t* gps, int32_t* gpe, bool* empty) -> bool {
+        int p = 0, cp = c;
+        while (p < P.n_parts - 1 && cp >= P.part[p].n_chunks) {
+            cp -= P.part[p].n_chunks;
+            ++p;
+        }
+        int32_t p0, np;
+        *empty = false;
+        if (!chunk_window(P, P.part[p], cp * P.part[p].chunk_bins, nr, &p0, &np)) return false;
+        const int32_t a = max(p0, sg0.off), b = min(p0 + np, sg0.off + len);
+        if (a >= b) {
+            *empty = true;
+            return false;
+        }
+        if (!sg0.rev) {
+            *gps = sg0.lo + (a - sg0.off);
+            *gpe = sg0.lo + (b - 1 - sg0.off);
+        } else {
+            *gpe = sg0.hi - (a - sg0.off);
+            *gps = sg0.hi - (b - 1 - sg0.off);
+        }
+        return true;
+    };
+    // one search pair (a single-range row in the merged layout): searches [lower, upper,
+    // interior chunk edges ...] are dealt to the quad's lanes and run in lockstep
+    const bool split1 = ns == 1 && npairs == 1;
+    const bool spec_cr = split1 && P.crange != nullptr && fast && ok;
+    if (split1) {
+        const RcpSeg sg = P.segs[j0];
+        const int g = sg.group & 3;
+        present = 1u << g;
+        maxpos[g] = sg.hi;
+        const bool qok = ok && sg.query_ok && (sg.streams & 1);
+        // the searches, numbered k = 0 (lower), 1 (upper), 2.. (interior chunk edges): lane q
+        // takes k = q, q + 4, ... (at most 4 each: <= 2 + 2 * (RCP_MAX_CRANGE_CHUNKS - 1))
+        int32_t sx[4] = {0, 0, 0, 0};
+        int sdst[4] = {0, 0, 0, 0};  // -2 lower, -1 upper, >= 0 xr index (its parity = upper)
+        int cnt = 0, k = 0;
+        for (int task = -2; task < (spec_cr ? 2 * nc : 0); ++task) {
+            int32_t x = 0;
+            bool need = false;
+            if (task < 0) {
+                x = task == -1 ? sg.hi : sg.lo;
+                need = qok;
+            } else {
+                int32_t gps = 0, gpe = 0;
+                bool empty;
+                if (piece(task >> 1, &gps, &gpe, &empty)) {
+                    need = (task & 1) ? gpe < sg0.hi : gps > sg0.lo;  // a row end: the row's own bound
+                    x = (task & 1) ? gpe : gps;
+                }
+            }
+            if (!need) continue;
+            if ((k & 3) == q) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (cnt == u) {
+                        sx[u] = x;
+                        sdst[u] = task;
+                    }
+                ++cnt;
+            }
+            ++k;
+        }
+        uint32_t v = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (u < cnt) {  // one dir_bound per round: the lanes' loads are in flight together
+                const bool up = sdst[u] == -1 || (sdst[u] >= 0 && (sdst[u] & 1));
+                const uint32_t w = dir_bound(P, chrom * 3, sx[u], up);
+                if (sdst[u] < 0) v = w; else xr[sdst[u]] = w;
+            }
+        }
+        lo = (uint32_t)qperm<0x00>((int)v);
+        hi = max(lo, (uint32_t)qperm<0x55>((int)v));
+        if (lo < hi) {
+            hit = 1u << g;
+            if (sl < 0 && q == 0) maxend[g] = P.pmax[hi - 1];
+            if (q == 0) ncand = hi - lo;
+        }
+        if (q == 0) {
+            P.seg_lo[j0 * 3] = lo;
+            P.seg_hi[j0 * 3] = hi;
+            P.seg_lo[j0 * 3 + 1] = P.seg_hi[j0 * 3 + 1] = 0;
+            P.seg_lo[j0 * 3 + 2] = P.seg_hi[j0 * 3 + 2] = 0;
+        }
+        if (q != 0) lo = hi = 0;  // the quad combine below reads (lo, hi) from lane 0
+    }
+    for (int pi = split1 ? npairs : q; pi < npairs; pi += 4) {
         const int j = j0 + pi / ns;
         const int s = pi % ns;
         const RcpSeg sg = P.segs[j];
@@ -482,54 +603,9 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
         P.heavy_slot[r] = slot;
     }
     slot = qperm<0x00>(slot);
-    // ---- per-chunk candidate ranges of a single-range row: each column chunk streams only
-    // the reads that reach its piece of the row
-    RcpSeg sg0{};
-    bool fast = false;
-    if (in_row && j1 == j0 + 1) {
-        sg0 = P.segs[j0];
-        fast = !sg0.multi && sg0.query_ok;
-    }
     const bool cr = P.crange != nullptr && fast && valid && slot < 0;
-    const int nc = P.n_chunks_total;
-    const int32_t nr = in_row ? P.row_len[r] : 0;
-    const int32_t len = sg0.hi - sg0.lo + 1;
-    // genomic piece of chunk c (false: the chunk streams the whole range / nothing special)
-    auto piece = [&](int c, int32_t* gps, int32_t* gpe, bool* empty) -> bool {
-        int p = 0, cp = c;
-        while (p < P.n_parts - 1 && cp >= P.part[p].n_chunks) {
-            cp -= P.part[p].n_chunks;
-            ++p;
-        }
-        int32_t p0, np;
-        *empty = false;
-        if (!chunk_window(P, P.part[p], cp * P.part[p].chunk_bins, nr, &p0, &np)) return false;
-        const int32_t a = max(p0, sg0.off), b = min(p0 + np, sg0.off + len);
-        if (a >= b) {
-            *empty = true;
-            return false;
-        }
-        if (!sg0.rev) {
-            *gps = sg0.lo + (a - sg0.off);
-            *gpe = sg0.lo + (b - 1 - sg0.off);
-        } else {
-            *gpe = sg0.hi - (a - sg0.off);
-            *gps = sg0.hi - (b - 1 - sg0.off);
-        }
-        return true;
-    };
     if (cr && ns == 1) {
-        // merged layout: the 2 * nc bound searches are dealt to the four lanes
-        for (int task = q; task < 2 * nc; task += 4) {
-            const int c = task >> 1;
-            int32_t gps = 0, gpe = 0;
-            bool empty;
-            uint32_t v = 0;
-            if (piece(c, &gps, &gpe, &empty))
-                v = (task & 1) ? (gpe < sg0.hi ? dir_upper(P, chrom * 3, gpe) : hi0)
-                               : (gps > sg0.lo ? dir_lower(P, chrom * 3, gps) : lo0);
-            xr[task] = v;
-        }
+        // merged layout: the interior edges were searched with the row's bounds (xr)
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (q == 0) {
@@ -538,8 +614,8 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
                 bool empty;
                 uint32_t clo = lo0, chi = hi0;
                 if (piece(c, &gps, &gpe, &empty)) {
-                    clo = xr[2 * c];
-                    chi = max(clo, xr[2 * c + 1]);
+                    clo = gps > sg0.lo ? xr[2 * c] : lo0;
+                    chi = max(clo, gpe < sg0.hi ? xr[2 * c + 1] : hi0);
                 } else if (empty) {
                     chi = clo;
                 }
@@ -614,6 +690,11 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_plan_kernel(RcpPlanDev P) {
     if (threadIdx.x == 0) P.heavy_slice_off[n] = carry;
 }
 
+#ifndef RCP_HEAVY_LOADS
+#define RCP_HEAVY_LOADS 16
+#endif
+constexpr int kHeavyLoads = RCP_HEAVY_LOADS;  // = RCP_HEAVY_SLICE / kBlock: one round trip per slice
+
 __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* diff = reinterpret_cast<int32_t*>(smem);
@@ -635,7 +716,8 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) 
         for (int q = threadIdx.x; q <= nr; q += kBlock) diff[q] = 0;
         __syncthreads();
         // walk the row's (segment, stream) read ranges in candidate order; the slice's part
-        // of each range is streamed with 4 loads in flight per thread
+        // of each range is streamed with kHeavyLoads loads in flight per thread (a whole
+        // slice of one range is one round trip)
         const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
         uint32_t base = 0;
         for (int j = j0; j < j1 && base < q1; ++j) {
@@ -646,12 +728,12 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) 
                 const uint32_t a = max(q0, base), b = min(q1, base + c);
                 if (a < b) {
                     const uint32_t i0 = lo + (a - base), i1 = lo + (b - base);
-                    for (uint32_t i = i0 + threadIdx.x; i < i1; i += 4 * kBlock) {
-                        int2 rd[4];
+                    for (uint32_t i = i0 + threadIdx.x; i < i1; i += kHeavyLoads * kBlock) {
+                        int2 rd[kHeavyLoads];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) rd[u] = P.se[min(i + u * kBlock, i1 - 1)];
+                        for (int u = 0; u < kHeavyLoads; ++u) rd[u] = P.se[min(i + u * kBlock, i1 - 1)];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u)
+                        for (int u = 0; u < kHeavyLoads; ++u)
                             if (i + u * kBlock < i1) add_read(P, sg, rd[u], sg.lo, sg.hi, 0, diff, 30);
                     }
                 }
@@ -734,9 +816,36 @@ __device__ __forceinline__ uint32_t fast_candidates(const RowMeta& m) {
 
 // index of candidate q of a fast row (q < fast_candidates)
 __device__ __forceinline__ uint32_t fast_index(const RowMeta& m, uint32_t q) {
+    // one stream (the merged layout, or a strand-specific row): a scalar test, no selects
+    if (m.hi[1] == m.lo[1] && m.hi[2] == m.lo[2]) return m.lo[0] + q;
     const uint32_t c0 = m.hi[0] - m.lo[0];
     const uint32_t c1 = m.hi[1] - m.lo[1];
     return q < c0 ? m.lo[0] + q : (q < c0 + c1 ? m.lo[1] + (q - c0) : m.lo[2] + (q - c0 - c1));
+}
+
+// Same as add_read_fast with the orientation known at compile time: the chunk positions of
+// the read's first covered base and of the base after its last are one add each.
+template <bool REV>
+__device__ __forceinline__ void add_read_fast_t(const RowMeta& m, int2 rd, int32_t* diff, int sh) {
+#ifdef RCP_ABL_ATOMICS  // ablation build (tools/ablate.sh): loads kept, no LDS atomics
+    asm volatile("" ::"v"(rd.x), "v"(rd.y));
+    return;
+#endif
+    if (rd.y < m.gps || rd.x > m.gpe) return;
+    const int32_t x0 = max(rd.x, m.gps);
+    const int32_t x1 = min(rd.y, m.gpe);
+    int32_t a, b;
+    if (!REV) {
+        const int32_t k = m.off - m.slo - m.P0;  // wave-uniform
+        a = x0 + k;
+        b = x1 + k + 1;
+    } else {
+        const int32_t k = m.off + m.shi - m.P0;
+        a = k - x1;
+        b = k - x0 + 1;
+    }
+    atomicAdd(&diff[lp(a, sh)], 1);
+    atomicAdd(&diff[lp(b, sh)], -1);
 }
 
 __device__ __forceinline__ void add_read_fast(const RowMeta& m, int2 rd, int32_t* diff, int sh) {
@@ -825,6 +934,15 @@ __device__ __forceinline__ void scan_bins_fast(int32_t* diff, int lbs, uint32_t*
         for (int m = 0; m < 4; ++m)
             if (m < nb && b0 + m < nbins) srow[b0 + m] = v[m];
     }
+}
+
+// write-once output: non-temporal stores keep the reads' lines in L2 / MALL
+__device__ __forceinline__ void out_store(double x, double* p) {
+#ifdef RCP_STORE_PLAIN
+    *p = x;
+#else
+    __builtin_nontemporal_store(x, p);
+#endif
 }
 
 template <bool MEDIAN, bool CSR>
@@ -982,8 +1100,9 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
     for (int a = 0; a < kAhead; ++a)
         if (a < kSteps) prefetch(row_of(a), pre[a]);
-    // ---- round epilogue: stage row -> out[col * n_rows + row].  Thread t always serves row
-    // t % 16, so 16 consecutive lanes write 16 consecutive rows (128 B) of one column.
+    // ---- round epilogue: stage row -> out[col * n_rows + row].  Thread t serves row t % 16
+    // and column quads t / 16, t / 16 + 32, ...: one 16-B stage read feeds four stores, and
+    // the 16 lanes of a quad column write 16 consecutive rows (128 B) of one column.
     auto flush = [&](int rd) {
         const int rbase = rd * T;
         const int ii = tid & (T - 1);
@@ -992,41 +1111,75 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
         const int32_t flag = mr.flag, kend = mr.kend, bs = mr.bs, lay = mr.lay;
         if (r >= P.n_rows || flag == 2) return;
         const size_t R = (size_t)P.n_rows;
-        const int kstep = kPBlock / T;
-        int32_t k = k0 + tid / T;
-        size_t o = (size_t)(part.col_off + k) * R + (size_t)r;
-        const size_t ostep = (size_t)kstep * R;
-        const uint32_t* st = stage + (rd % kStageBufs) * T * RS + ii * RS + tid / T;
-        if (flag == 1) {
-            for (; k < kend; k += kstep, o += ostep) {
-                __builtin_nontemporal_store(0.0, out + o);
-                if (binsum) binsum[o] = 0;
+        constexpr int kQuads = kPBlock / T;  // column quads per pass
+        constexpr int kStep = 4 * kQuads;    // columns per pass
+        const int32_t kq = k0 + 4 * (tid / T);
+        const size_t o0 = (size_t)(part.col_off + kq) * R + (size_t)r;
+        const size_t ostep = (size_t)kStep * R;
+        const uint32_t* st0 = stage + (rd % kStageBufs) * T * RS + ii * RS + 4 * (tid / T);
+        // value of bin k from its stage count: zero row / one divisor / splitVector layout
+        const double sc = P.scale;
+        const int32_t den = MEDIAN ? 2 : bs;
+        const double dd = (double)den;
+        const bool pow2 = (MEDIAN || lay < 0) && (den & (den - 1)) == 0;
+        const double rdd = 1.0 / dd;
+        auto put4 = [&](int32_t k, double* o, const double (&x)[4]) {
+            if (k + 3 < kend) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) out_store(x[u], o + u * R);
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (k + u < kend) out_store(x[u], o + u * R);
             }
-        } else if (MEDIAN || lay < 0) {
-            // one divisor for the whole row; a power of two divides exactly by its reciprocal
-            const int32_t den = MEDIAN ? 2 : bs;
-            const double dd = (double)den;
-            const double rdd = 1.0 / dd;
-            const bool pow2 = (den & (den - 1)) == 0;
-            const double sc = P.scale;
-            for (; k < kend; k += kstep, o += ostep, st += kstep) {
-                const uint32_t num = *st;
-                const double x = (double)num * sc;
+        };
+        double* o = out + o0;
+        if (flag == 1) {
+            const double z[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int32_t k = kq; k < kend; k += kStep, o += ostep) put4(k, o, z);
+        } else if (pow2) {
+            // a power of two divides exactly by its reciprocal
+            const uint32_t* st = st0;
+            for (int32_t k = kq; k < kend; k += kStep, o += ostep, st += kStep) {
+                const uint4 q = *reinterpret_cast<const uint4*>(st);
+                const double x[4] = {((double)q.x * sc) * rdd, ((double)q.y * sc) * rdd,
+                                     ((double)q.z * sc) * rdd, ((double)q.w * sc) * rdd};
 #ifdef RCP_ABL_STORES  // ablation: barriers and stage reads kept, no global stores
-                asm volatile("" ::"v"(x));
+                asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
                 continue;
 #endif
-                // write-once output: non-temporal stores keep the reads' lines in L2 / MALL
-                __builtin_nontemporal_store(pow2 ? x * rdd : x / dd, out + o);
-                if (binsum) binsum[o] = (int64_t)num;
+                put4(k, o, x);
+            }
+        } else if (MEDIAN || lay < 0) {
+            const uint32_t* st = st0;
+            for (int32_t k = kq; k < kend; k += kStep, o += ostep, st += kStep) {
+                const uint4 q = *reinterpret_cast<const uint4*>(st);
+                const double x[4] = {((double)q.x * sc) / dd, ((double)q.y * sc) / dd,
+                                     ((double)q.z * sc) / dd, ((double)q.w * sc) / dd};
+                put4(k, o, x);
             }
         } else {
             const int32_t* cnt = P.lay_cnt + lay;
-            for (; k < kend; k += kstep, o += ostep, st += kstep) {
-                const uint32_t num = *st;
-                const double den = (double)(bs + cnt[k + 1] - cnt[k]);
-                __builtin_nontemporal_store(((double)num * P.scale) / den, out + o);
-                if (binsum) binsum[o] = (int64_t)num;
+            const uint32_t* st = st0;
+            for (int32_t k = kq; k < kend; k += kStep, o += ostep, st += kStep) {
+                const uint4 q = *reinterpret_cast<const uint4*>(st);
+                const uint32_t num[4] = {q.x, q.y, q.z, q.w};
+                double x[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    x[u] = k + u < kend ? ((double)num[u] * sc) / (double)(bs + cnt[k + u + 1] - cnt[k + u]) : 0.0;
+                put4(k, o, x);
+            }
+        }
+        if (binsum) {  // optional int64 bin sums, same layout
+            int64_t* bo = binsum + o0;
+            const uint32_t* st = st0;
+            for (int32_t k = kq; k < kend; k += kStep, bo += ostep, st += kStep) {
+                const uint4 q = flag == 1 ? make_uint4(0u, 0u, 0u, 0u) : *reinterpret_cast<const uint4*>(st);
+                const uint32_t num[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (k + u < kend) bo[u * R] = (int64_t)num[u];
             }
         }
     };
@@ -1097,9 +1250,15 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
                                 nx[u] = P.se[fast_index(m, q < n ? q : n - 1)];
                             }
                         }
+                        if (m.rev) {  // wave-uniform orientation
 #pragma unroll
-                        for (int u = 0; u < 4; ++u)
-                            if (q0 + lane + 64u * u < n) add_read_fast(m, cur[u], diff, sh);
+                            for (int u = 0; u < 4; ++u)
+                                if (q0 + lane + 64u * u < n) add_read_fast_t<true>(m, cur[u], diff, sh);
+                        } else {
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                if (q0 + lane + 64u * u < n) add_read_fast_t<false>(m, cur[u], diff, sh);
+                        }
 #pragma unroll
                         for (int u = 0; u < 4; ++u) cur[u] = nx[u];
                     }

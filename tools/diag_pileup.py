@@ -33,6 +33,16 @@ def run(name, check_heavy=False, **kw):
         torch.cuda.synchronize()
         ts.append([ev[i].elapsed_time(ev[i + 1]) for i in range(3)])
     ts = np.median(np.array(ts), axis=0)
+    # pileup alone, back to back: 3 blocks of 20 launches, best block (less clock noise)
+    blk = []
+    for _ in range(3):
+        ev[0].record()
+        for _ in range(20):
+            plan.execute_stages(2, out)
+        ev[1].record()
+        torch.cuda.synchronize()
+        blk.append(ev[0].elapsed_time(ev[1]) / 20)
+    ts[1] = min(blk)
     n_ovl = synthetic.n_overlaps(d["reads"], reg, d["width"]).astype(np.int64)
     byt = 8 * n_ovl.sum() + 16 * len(n_ovl) + 8 * len(n_ovl) * plan.n_cols
     print(f"{name:34s} locate+heavy {ts[0]:7.3f} ms  pileup {ts[1]:7.3f} ms ({byt / ts[1] / 1e6:7.1f} GB/s)  "

@@ -695,6 +695,21 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_plan_kernel(RcpPlanDev P) {
 #endif
 constexpr int kHeavyLoads = RCP_HEAVY_LOADS;  // = RCP_HEAVY_SLICE / kBlock: one round trip per slice
 
+// diff[key] += w * (length of the run of equal keys starting at this lane), once per run of
+// consecutive lanes holding the same key; inactive lanes split runs and add nothing.  The
+// reads of a wave are consecutive in start order, so the reads of a hot row pile onto a
+// few positions per wave: one LDS atomic per run instead of one per read.
+__device__ __forceinline__ void run_add(int32_t* diff, int32_t key, bool act, int32_t w) {
+    const int lane = threadIdx.x & 63;
+    const int32_t k = act ? key : -1;                                   // -1: never a position
+    const int32_t prev = __builtin_amdgcn_update_dpp(-2, k, 0x138, 0xf, 0xf, false);  // wave_shr:1
+    const bool head = lane == 0 || k != prev;
+    const uint64_t heads = __ballot(head);
+    const uint64_t above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+    const int nxt = above ? __builtin_ctzll(above) : 64;
+    if (head && act) atomicAdd(&diff[k], w * (nxt - lane));
+}
+
 __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* diff = reinterpret_cast<int32_t*>(smem);
@@ -728,13 +743,30 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) 
                 const uint32_t a = max(q0, base), b = min(q1, base + c);
                 if (a < b) {
                     const uint32_t i0 = lo + (a - base), i1 = lo + (b - base);
-                    for (uint32_t i = i0 + threadIdx.x; i < i1; i += kHeavyLoads * kBlock) {
+                    // wave-uniform trip count: run_add needs every lane of the wave
+                    const uint32_t lane = threadIdx.x & 63;
+                    for (uint32_t wb = i0 + (threadIdx.x & ~63u); wb < i1; wb += kHeavyLoads * kBlock) {
+                        const uint32_t i = wb + lane;
                         int2 rd[kHeavyLoads];
 #pragma unroll
                         for (int u = 0; u < kHeavyLoads; ++u) rd[u] = P.se[min(i + u * kBlock, i1 - 1)];
+                        if (sg.multi) {
 #pragma unroll
-                        for (int u = 0; u < kHeavyLoads; ++u)
-                            if (i + u * kBlock < i1) add_read(P, sg, rd[u], sg.lo, sg.hi, 0, diff, 30);
+                            for (int u = 0; u < kHeavyLoads; ++u)
+                                if (i + u * kBlock < i1) add_read(P, sg, rd[u], sg.lo, sg.hi, 0, diff, 30);
+                        } else {
+#pragma unroll
+                            for (int u = 0; u < kHeavyLoads; ++u) {
+                                // add_read with weight 1, the two atomics merged per run
+                                const int2 x = rd[u];
+                                const bool act = i + u * kBlock < i1 && !(x.y < sg.lo || x.x > sg.hi);
+                                const int32_t x0 = max(x.x, sg.lo), x1 = min(x.y, sg.hi);
+                                const int32_t o0 = sg.rev ? sg.off + (sg.hi - x1) : sg.off + (x0 - sg.lo);
+                                const int32_t o1 = sg.rev ? sg.off + (sg.hi - x0) : sg.off + (x1 - sg.lo);
+                                run_add(diff, o0, act, 1);
+                                run_add(diff, o1 + 1, act, -1);
+                            }
+                        }
                     }
                 }
                 base += c;

@@ -218,6 +218,35 @@ def test_heavy_rows_match(gpu):
     check(res_m, exp_m, rtol=1e-9, atol=1e-12)
 
 
+def test_heavy_duplicate_stacks_match(gpu):
+    """Hot rows made of PCR-duplicate stacks (thousands of reads on one start, equal widths):
+    the heavy path merges a wave's equal positions into one LDS add per run, both strands,
+    per-base and binned, plus stranded (ignore.strand = FALSE) multi-stream rows."""
+    from recoup_amd.engine import Bins, RowTable
+    rng = np.random.default_rng(29)
+    n = 120_000
+    chrom = np.zeros(n, np.int32)
+    stacks = rng.integers(5000, 5400, 40)                        # 40 duplicate stacks near one spot
+    start = np.where(rng.random(n) < 0.8, stacks[rng.integers(0, 40, n)], rng.integers(1, 900_000, n))
+    width = np.where(rng.random(n) < 0.9, 150, rng.integers(30, 300, n))
+    reads = (chrom, start.astype(np.int64), (start + width - 1).astype(np.int64),
+             rng.integers(0, 3, n).astype(np.int8))
+    seqlen = np.array([1_000_000], np.int64)
+    s0 = np.array([4000, 4100, 4500, 5100, 3000, 5300, 100_000], np.int64)
+    rows = RowTable.from_ranges(np.zeros(7, np.int32), s0, s0 + 1999, np.array([0, 1, 2, 1, 0, 1, 2], np.int8))
+    os.environ["RCP_HEAVY_THRESHOLD"] = "16"
+    try:
+        for bins in (Bins([("whole", 100)]), Bins([("whole", 0, 2000)])):
+            res, exp = run_case(reads, seqlen, rows, bins)
+            check(res, exp)
+        stranded = RowTable.from_ranges(np.zeros(7, np.int32), s0, s0 + 1999,
+                                        np.array([0, 1, 2, 1, 0, 1, 2], np.int8), ignore_strand=False)
+        res, exp = run_case(reads, seqlen, stranded, Bins([("whole", 250)]))
+        check(res, exp)
+    finally:
+        del os.environ["RCP_HEAVY_THRESHOLD"]
+
+
 def test_calc_coverage_csr(gpu):
     from recoup_amd.engine import Plan, ReadSet
     rng = np.random.default_rng(3)

@@ -63,7 +63,10 @@ constexpr int kStageMaxBins = RCP_STAGE_MAX_BINS;  // bins per chunk (LDS stage 
 #define RCP_LDS_BUDGET (80 * 1024)
 #endif
 constexpr size_t kLdsBudget = RCP_LDS_BUDGET;  // pileup LDS per workgroup (80 KB: two per CU)
-constexpr int kHeavyThreshold = 4096;  // candidate reads above which a row is split across workgroups
+constexpr int kHeavyThreshold = 8192;  // candidate reads per column chunk above which a row is split across workgroups
+#ifndef RCP_DIR_READS
+#define RCP_DIR_READS 8  // mean reads per directory bucket (the locate kernel's search depth)
+#endif
 #ifndef RCP_HEAVY_SLICE
 #define RCP_HEAVY_SLICE 4096
 #endif
@@ -260,7 +263,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
         genome += (double)m;
     }
     const int used = merge ? 1 : 3;  // streams per chromosome that hold reads
-    const double want = kept > 0 ? 32.0 * used * genome / (double)kept : 1e9;
+    const double want = kept > 0 ? (double)RCP_DIR_READS * used * genome / (double)kept : 1e9;
     int shift = 6;
     while (shift < 24 && (double)(int64_t(1) << (shift + 1)) <= want) ++shift;
     L->dir_shift = shift;

@@ -396,6 +396,9 @@ __device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32
     const int32_t* key = upper ? reinterpret_cast<const int32_t*>(P.se) : P.pmax;
     const int ksh = upper ? 1 : 0;                      // start of read m is word 2m of se
     const int64_t thr = (int64_t)v + (upper ? 1 : 0);  // start > v  <=>  start >= v + 1
+#ifdef RCP_ABL_SEARCH  // ablation: bucket lookup only
+    return upper ? hi : lo;
+#endif
     while (lo < hi) {
         const uint32_t m = lo + ((hi - lo) >> 1);
         if ((int64_t)key[(size_t)m << ksh] < thr) lo = m + 1; else hi = m;
@@ -409,7 +412,10 @@ __device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32
 // counts with DPP.  For a single-range row the lanes also split the per-chunk range searches.
 // Every search is bounded by the bucket directory and independent of the others: the
 // dependent chain per lane is one bucket search, not a sequence of them.
-__global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
+#ifndef RCP_LOC_WPE
+#define RCP_LOC_WPE 1
+#endif
+__global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlanDev P) {
     __shared__ uint32_t xres[kBlock / 4][2 * RCP_MAX_CRANGE_CHUNKS];  // per quad: chunk bounds
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = t >> 2;
@@ -589,10 +595,12 @@ __global__ void __launch_bounds__(kBlock) rcp_locate_kernel(RcpPlanDev P) {
     if (in_row && q == 0) {
         P.valid[r] = valid ? 1 : 0;
         P.ncand[r] = ncand;
-        // skewed rows only: many candidates AND a deep pileup (> 2 reads per position), so a
-        // long row with proportionally many reads stays on the workgroup path
+        // skewed rows only: many candidates per column chunk (each chunk of a row is one
+        // wave's work) AND a deep pileup (> 2 reads per position), so a long row with
+        // proportionally many reads stays on the workgroup path
         const int32_t rl = P.row_len[r];
-        if (valid && P.heavy_threshold > 0 && ncand > (uint32_t)P.heavy_threshold &&
+        if (valid && P.heavy_threshold > 0 &&
+            (uint64_t)ncand > (uint64_t)P.heavy_threshold * (uint64_t)max(P.n_chunks_total, 1) &&
             ncand > 2u * (uint32_t)max(rl, 0) && rl <= P.heavy_max_len) {
             const uint32_t u = atomicAdd(&P.status[1], 1u);
             if (u < (uint32_t)P.heavy_cap) {

@@ -142,6 +142,8 @@ typedef struct {
     int64_t grid;               /* workgroups of the pileup kernel */
     int32_t tile_rows;
     int32_t chunk_positions;
+    int32_t pileup_kernel;   /* 0: general pileup kernel; 1: lean kernel (pile + store waves) */
+    int32_t reserved;
 } rcp_plan_info;
 
 /* Host work: orientation of segments, R-RNG bin layouts (set.seed(42); sample(1:n, dif)),

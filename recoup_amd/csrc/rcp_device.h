@@ -107,6 +107,8 @@ struct RcpPlanDev {
     int32_t wave_words;         // LDS words per wave difference array (multiple of 256)
     int32_t stage_cap;          // max bins per chunk
     int32_t interp_cap;         // max positions of an interpolated slice
+    int32_t lean;               // 1: every row is one plain range with uniform power-of-two bins
+                                //    of one wave chunk -> rcp_pileup_lean_kernel
     // coverage (CSR) mode
     const int64_t* csr_off;     // non-null: write per-row depth into csr (calcCoverage)
     int32_t* csr_out;

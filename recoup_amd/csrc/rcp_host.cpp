@@ -34,6 +34,7 @@ hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStream_t strea
 size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr);
 size_t rcp_interp_lds_bytes(const RcpPlanDev* P);
 int rcp_tile_rows(void);
+int rcp_lean_max_bins(void);
 hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
                               const int8_t* strand, int32_t n_chrom, int32_t strand_filter, int merge, uint64_t* keys,
                               int32_t* vals, hipStream_t stream);
@@ -528,6 +529,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.scale = bins->scale;
     int64_t col = 0;
     int32_t chunk_cap = 1024, stage_cap = 1;
+    bool lean_ok = true;  // so far: uniform power-of-two bins (no R-RNG layouts)
     int32_t max_interp_len = 0, max_interp_bins = 0;
     std::vector<int32_t> part_max_bin(RCP_MAX_PARTS, 1);
     std::map<std::pair<int, int>, int32_t> layout_cache;  // (n, dif) -> offset in lay_cnt
@@ -596,6 +598,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
                 }
                 const int32_t bs = L / pt.n_bins;
                 const int32_t dif = L - bs * pt.n_bins;
+                if (dif || (bs & (bs - 1))) lean_ok = false;
                 // median bins wider than a wave chunk go to the slow-row kernel (mode 4) and do
                 // not size the chunks of the others
                 if (bins->stat != RCP_STAT_MEDIAN || bs + (dif ? 1 : 0) < kWaveMax)
@@ -699,6 +702,25 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     }
     P.n_chunks_total = 0;
     for (int p = 0; p < P.n_parts; ++p) P.n_chunks_total += P.part[p].n_chunks;
+
+    // ---- lean pileup kernel: every row one plain range (no exon list, no zero-width query),
+    // mean of uniform power-of-two bins, each chunk inside one wave's fused pass (<= 1023
+    // positions) and the stage inside the store waves' registers
+    {
+        bool lean = lean_ok && !cov_only && bins->stat == RCP_STAT_MEAN && P.chunk_cap <= 1023 &&
+                    stage_cap <= rcp_lean_max_bins() && env_int("RCP_LEAN", 1) != 0;
+        for (int p = 0; lean && p < P.n_parts; ++p) {
+            const RcpPart& pt = P.part[p];
+            const int64_t w = pt.per_base ? 1 : part_max_bin[p];
+            if ((int64_t)pt.chunk_bins * w > P.chunk_cap) lean = false;
+        }
+        for (int r = 0; lean && r < R; ++r) {
+            const int32_t j0 = B.row_seg[r], j1 = B.row_seg[r + 1];
+            if (j1 - j0 > 1) lean = false;
+            else if (j1 == j0 + 1 && (B.segs[j0].multi || !B.segs[j0].query_ok)) lean = false;
+        }
+        P.lean = lean ? 1 : 0;
+    }
 
     // ---- skewed rows: heavy slots sized for the eligible (short enough) rows
     const int32_t heavy_thr = env_int("RCP_HEAVY_THRESHOLD", kHeavyThreshold);
@@ -816,6 +838,8 @@ extern "C" int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info) {
     info->grid = plan->grid;
     info->tile_rows = rcp_tile_rows();
     info->chunk_positions = plan->dev.chunk_cap;
+    info->pileup_kernel = plan->dev.lean;
+    info->reserved = 0;
     return RCP_OK;
 }
 

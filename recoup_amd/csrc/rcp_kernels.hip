@@ -908,6 +908,20 @@ __device__ __forceinline__ void add_read_fast(const RowMeta& m, int2 rd, int32_t
     atomicAdd(&diff[lp(o1 - m.P0 + 1, sh)], -1);
 }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup-scope release of
+// all address spaces, which on gfx9 waits for vmcnt(0): every global store of the previous
+// epilogue (and every prefetched read) would have to land before the barrier.  The pileup
+// kernel's waves share nothing through global memory, so LDS ordering is enough.
+__device__ __forceinline__ void lds_barrier() {
+#ifdef RCP_FULL_BARRIER
+    __syncthreads();
+#else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#endif
+}
+
 __device__ __forceinline__ void lds_order() {
     // a wave's LDS operations complete in issue order; keep the compiler from moving them
     __builtin_amdgcn_wave_barrier();
@@ -985,6 +999,104 @@ __device__ __forceinline__ void out_store(double x, double* p) {
 #endif
 }
 
+// Row metadata of row r for column chunk (part, k0, cidx), from the locate kernel's 64-byte
+// record (one thread per row; the refine searches of all rows are in flight together).
+// flag: 0 = pile up, 1 = NULL row (zeros), 2 = not this kernel's (interp / outside).
+template <bool MEDIAN, bool CSR>
+__device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart& part, int32_t k0, int cidx, int r) {
+    RowMeta m;
+    m.flag = 2; m.bs = 0; m.lay = -1; m.P0 = 0; m.npos = 0; m.kend = k0; m.heavy = -1; m.fast = 0;
+    m.off = m.slo = m.shi = m.rev = m.gps = m.gpe = 0;
+    for (int s = 0; s < 3; ++s) m.lo[s] = m.hi[s] = 0;
+    if (r < P.n_rows) {
+        RcpRowRec rec;
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(P.rec + r);
+            uint4* dst = reinterpret_cast<uint4*>(&rec);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[q] = src[q];
+        }
+        int32_t head, L;
+        rcp_part_slice(part, rec.row_len, &head, &L);
+        const int32_t n = CSR ? L : part.n_bins;
+        m.kend = min(k0 + part.chunk_bins, n);
+        if (!(rec.flags & RCP_REC_VALID)) {
+            m.flag = CSR ? 2 : 1;  // NULL row -> zeros (profile.R:191-197)
+        } else if (k0 >= n) {
+            m.flag = 2;
+        } else if (!part.per_base && L < n) {
+            m.flag = 2;  // interpolation rows: rcp_interp_kernel
+        } else if (part.per_base && !CSR && L != n) {
+            atomicOr(P.status, RCP_STATUS_WIDTH);
+            m.flag = 1;
+        } else {
+            if (part.per_base) {
+                m.bs = 1;
+            } else {
+                m.bs = L / n;
+                const int32_t dif = L - m.bs * n;
+                if (dif) {
+                    m.lay = P.lay_index[part.lay_base + dif];
+                    if (m.lay < 0) {
+                        atomicOr(P.status, RCP_STATUS_INTERP);
+                        m.lay = -1;
+                    }
+                }
+            }
+            const int32_t e0 = bin_edge(m.bs, m.lay, P.lay_cnt, k0);
+            const int32_t e1 = bin_edge(m.bs, m.lay, P.lay_cnt, m.kend);
+            m.P0 = head + e0;
+            m.npos = e1 - e0;
+            m.flag = 0;
+            // median bins wider than a wave chunk: rcp_interp_kernel (mode 4)
+            if (MEDIAN && m.bs + (m.lay >= 0 ? 1 : 0) > P.chunk_cap) m.flag = 2;
+            m.heavy = rec.heavy;
+            if (m.heavy < 0 && m.npos <= P.chunk_cap && (rec.flags & RCP_REC_FAST)) {
+                const int32_t len = rec.shi - rec.slo + 1;
+                const int32_t a = max(m.P0, rec.off);
+                const int32_t b = min(m.P0 + m.npos, rec.off + len);
+                m.fast = 1;
+                m.off = rec.off; m.slo = rec.slo; m.shi = rec.shi; m.rev = rec.rev;
+                if (a < b) {
+                    if (!rec.rev) {
+                        m.gps = rec.slo + (a - rec.off);
+                        m.gpe = rec.slo + (b - 1 - rec.off);
+                    } else {
+                        m.gpe = rec.shi - (a - rec.off);
+                        m.gps = rec.shi - (b - 1 - rec.off);
+                    }
+                    const bool full = (a == rec.off) && (b == rec.off + len);
+                    uint32_t all = 0;
+                    for (int s = 0; s < 3; ++s) all += rec.hi[s] - rec.lo[s];
+                    // a chunk of a modest row streams all the row's reads (the piece
+                    // check drops the others; they are L2 hits for the sibling chunks);
+                    // only big rows pay the dependent binary searches
+                    const bool refine = !full && all > 4096;
+                    if (rec.flags & RCP_REC_CRANGE) {
+                        // exact ranges for this chunk from the locate kernel
+                        const uint2* cr = P.crange + ((size_t)r * P.n_chunks_total + cidx) * 3;
+                        for (int s = 0; s < 3; ++s) {
+                            const uint2 v = cr[s];
+                            m.lo[s] = v.x;
+                            m.hi[s] = v.y;
+                        }
+                    } else
+                    for (int s = 0; s < 3; ++s) {
+                        uint32_t lo = rec.lo[s], hi = rec.hi[s];
+                        if (lo < hi && refine) {
+                            lo = lower_bound_pmax(P.pmax, lo, hi, m.gps);
+                            hi = upper_bound_start(P.se, lo, hi, m.gpe);
+                        }
+                        m.lo[s] = lo;
+                        m.hi[s] = lo < hi ? hi : lo;
+                    }
+                }
+            }
+        }
+    }
+    return m;
+}
+
 template <bool MEDIAN, bool CSR>
 __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4))) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
                                                             int64_t* __restrict__ binsum) {
@@ -1019,103 +1131,11 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * (P.wave_words + 8);
     RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : kStageBufs * T * RS));
 
-    // ---- per-row metadata, one thread per row (searches of all rows in flight together)
     // ---- per-row metadata, one thread per row, from the locate kernel's 64-byte records
     if (tid < kRows) {
-        const int r = row0 + tid;
-        RowMeta m;
-        m.flag = 2; m.bs = 0; m.lay = -1; m.P0 = 0; m.npos = 0; m.kend = k0; m.heavy = -1; m.fast = 0;
-        m.off = m.slo = m.shi = m.rev = m.gps = m.gpe = 0;
-        for (int s = 0; s < 3; ++s) m.lo[s] = m.hi[s] = 0;
-        if (r < P.n_rows) {
-            RcpRowRec rec;
-            {
-                const uint4* src = reinterpret_cast<const uint4*>(P.rec + r);
-                uint4* dst = reinterpret_cast<uint4*>(&rec);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) dst[q] = src[q];
-            }
-            int32_t head, L;
-            rcp_part_slice(part, rec.row_len, &head, &L);
-            const int32_t n = CSR ? L : part.n_bins;
-            m.kend = min(k0 + part.chunk_bins, n);
-            if (!(rec.flags & RCP_REC_VALID)) {
-                m.flag = CSR ? 2 : 1;  // NULL row -> zeros (profile.R:191-197)
-            } else if (k0 >= n) {
-                m.flag = 2;
-            } else if (!part.per_base && L < n) {
-                m.flag = 2;  // interpolation rows: rcp_interp_kernel
-            } else if (part.per_base && !CSR && L != n) {
-                atomicOr(P.status, RCP_STATUS_WIDTH);
-                m.flag = 1;
-            } else {
-                if (part.per_base) {
-                    m.bs = 1;
-                } else {
-                    m.bs = L / n;
-                    const int32_t dif = L - m.bs * n;
-                    if (dif) {
-                        m.lay = P.lay_index[part.lay_base + dif];
-                        if (m.lay < 0) {
-                            atomicOr(P.status, RCP_STATUS_INTERP);
-                            m.lay = -1;
-                        }
-                    }
-                }
-                const int32_t e0 = bin_edge(m.bs, m.lay, P.lay_cnt, k0);
-                const int32_t e1 = bin_edge(m.bs, m.lay, P.lay_cnt, m.kend);
-                m.P0 = head + e0;
-                m.npos = e1 - e0;
-                m.flag = 0;
-                // median bins wider than a wave chunk: rcp_interp_kernel (mode 4)
-                if (MEDIAN && m.bs + (m.lay >= 0 ? 1 : 0) > P.chunk_cap) m.flag = 2;
-                m.heavy = rec.heavy;
-                if (m.heavy < 0 && m.npos <= P.chunk_cap && (rec.flags & RCP_REC_FAST)) {
-                    const int32_t len = rec.shi - rec.slo + 1;
-                    const int32_t a = max(m.P0, rec.off);
-                    const int32_t b = min(m.P0 + m.npos, rec.off + len);
-                    m.fast = 1;
-                    m.off = rec.off; m.slo = rec.slo; m.shi = rec.shi; m.rev = rec.rev;
-                    if (a < b) {
-                        if (!rec.rev) {
-                            m.gps = rec.slo + (a - rec.off);
-                            m.gpe = rec.slo + (b - 1 - rec.off);
-                        } else {
-                            m.gpe = rec.shi - (a - rec.off);
-                            m.gps = rec.shi - (b - 1 - rec.off);
-                        }
-                        const bool full = (a == rec.off) && (b == rec.off + len);
-                        uint32_t all = 0;
-                        for (int s = 0; s < 3; ++s) all += rec.hi[s] - rec.lo[s];
-                        // a chunk of a modest row streams all the row's reads (the piece
-                        // check drops the others; they are L2 hits for the sibling chunks);
-                        // only big rows pay the dependent binary searches
-                        const bool refine = !full && all > 4096;
-                        if (rec.flags & RCP_REC_CRANGE) {
-                            // exact ranges for this chunk from the locate kernel
-                            const uint2* cr = P.crange + ((size_t)r * P.n_chunks_total + cidx) * 3;
-                            for (int s = 0; s < 3; ++s) {
-                                const uint2 v = cr[s];
-                                m.lo[s] = v.x;
-                                m.hi[s] = v.y;
-                            }
-                        } else
-                        for (int s = 0; s < 3; ++s) {
-                            uint32_t lo = rec.lo[s], hi = rec.hi[s];
-                            if (lo < hi && refine) {
-                                lo = lower_bound_pmax(P.pmax, lo, hi, m.gps);
-                                hi = upper_bound_start(P.se, lo, hi, m.gpe);
-                            }
-                            m.lo[s] = lo;
-                            m.hi[s] = lo < hi ? hi : lo;
-                        }
-                    }
-                }
-            }
-        }
-        meta[tid] = m;
+        meta[tid] = decode_row<MEDIAN, CSR>(P, part, k0, cidx, row0 + tid);
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---- rows of this wave: round rd, sub s -> row rd*T + s*kPWaves + wave
     auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
@@ -1129,17 +1149,21 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
 #else
         const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
 #endif
+        if (n) {  // wave-uniform
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            // unconditional (clamped) loads: no branch, no early vmcnt wait
-            const uint32_t q = lane + 64 * u;
-            dst[u] = P.se[n ? fast_index(m, q < n ? q : n - 1) : 0u];
+            for (int u = 0; u < 4; ++u) {
+                // unconditional (clamped) loads: no divergent branch, no early vmcnt wait
+                const uint32_t q = lane + 64 * u;
+                dst[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+            }
         }
     };
-    int2 pre[kAhead][4];
-#pragma unroll
-    for (int a = 0; a < kAhead; ++a)
-        if (a < kSteps) prefetch(row_of(a), pre[a]);
+    static_assert(kAhead == 1 && kRowsPerWave % 2 == 0, "ping-pong prefetch buffers: one row ahead, even rows per round");
+    // Two read buffers used alternately (no register copies across steps): a copy at the loop
+    // back-edge would need the prefetched reads to have landed right after the epilogue's
+    // stores, and gfx9's single in-order vmcnt would make that wait for the stores too.
+    int2 bufA[4], bufB[4];
+    prefetch(row_of(0), bufA);
     // ---- round epilogue: stage row -> out[col * n_rows + row].  Thread t serves row t % 16
     // and column quads t / 16, t / 16 + 32, ...: one 16-B stage read feeds four stores, and
     // the 16 lanes of a quad column write 16 consecutive rows (128 B) of one column.
@@ -1225,16 +1249,10 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     };
     bool clean = false;  // this wave's difference array is all zero (layout clean_sh)
     int clean_sh = -1;
-    for (int step = 0; step < kSteps; ++step) {
+    // one row of this wave: `cur` holds its first reads; the next row's go to `nxt`
+    auto pile_step = [&](int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
         const int i = row_of(step);
-        int2 cur[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) cur[u] = pre[0][u];
-#pragma unroll
-        for (int a = 0; a + 1 < kAhead; ++a)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) pre[a][u] = pre[a + 1][u];
-        if (step + kAhead < kSteps) prefetch(row_of(step + kAhead), pre[kAhead - 1]);
+        if (step + 1 < kSteps) prefetch(row_of(step + 1), nxt);
         const RowMeta m = uniform_meta(meta[i]);
         uint32_t* sbuf = stage + ((step / kRowsPerWave) % kStageBufs) * T * RS;  // this round's stage
         if (m.flag == 0) {  // wave-uniform: scalar branch
@@ -1375,25 +1393,221 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
                 lds_order();
             }
         }
-        if (CSR || (step % kRowsPerWave) != kRowsPerWave - 1) continue;
+    };
+    for (int rd = 0; rd < kRounds; ++rd) {
+        for (int s2 = 0; s2 < kRowsPerWave; s2 += 2) {
+            pile_step(rd * kRowsPerWave + s2, bufA, bufB);
+            pile_step(rd * kRowsPerWave + s2 + 1, bufB, bufA);
+        }
+        if (CSR) continue;
 #ifdef RCP_ABL_EPI
         continue;
 #endif
-        const int rd = step / kRowsPerWave;
         if (kStageBufs == 2) {
             // double-buffered stage: round rd - 1 is written while other waves still pile
             // round rd; one barrier per round; the last round is written after the loop
             if (rd > 0) flush(rd - 1);
-            __syncthreads();
+            lds_barrier();
         } else {
-            __syncthreads();
+            lds_barrier();
             flush(rd);
-            __syncthreads();
+            lds_barrier();
         }
     }
     if (!CSR && kStageBufs == 2) flush(kRounds - 1);
 }
 
+
+
+// ---------------------------------------------------------------------------------
+// Lean pileup kernel: pile waves + store waves.
+// For plans whose every row is one plain range with uniform power-of-two bins of one
+// wave chunk (C4 peaks, C5 per-base, TSS/TES windows: rcp_plan decides, `P.lean`), the
+// row work is the fused pass only, so the kernel drops the general paths and splits the
+// workgroup by role:
+//   waves 0..7  (pile)  pile rows into their LDS difference arrays and stage bin sums;
+//                       they never store to global memory
+//   waves 8..11 (store) copy a finished round of the stage into registers and write it
+//                       as R column-major fp64; they never load from global memory
+// gfx9 has one in-order vmcnt for loads and stores, so a wave that stores and then waits
+// for a read also waits for its stores to be acknowledged.  With the roles split, the
+// epilogue's writes of round rd drain while the pile waves already stream round rd + 1.
+// Two LDS-only barriers per round: (A) stage full, (B) stage copied out.
+// ---------------------------------------------------------------------------------
+constexpr int kLStoreWaves = 4;
+constexpr int kLBlock = 64 * (kPWaves + kLStoreWaves);
+constexpr int kLQuads = 64 * kLStoreWaves / kTile;  // column quads per store pass
+constexpr int kLMaxPass = 8;                        // stage_cap <= 4 * kLQuads * kLMaxPass
+
+__global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(6)))
+rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int T = kTile;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int lane = tid & 63;
+    // XCD-aware (row block, chunk) decode: as rcp_pileup_kernel
+    const int grp = blockIdx.x / (8 * P.n_chunks_total);
+    const int wg = blockIdx.x - grp * 8 * P.n_chunks_total;
+    int c = wg >> 3;
+    const int cidx = c;
+    const int blk = grp * 8 + (wg & 7);
+    if (blk * kRows >= P.n_rows) return;
+    int p = 0;
+    while (p < P.n_parts - 1 && c >= P.part[p].n_chunks) {
+        c -= P.part[p].n_chunks;
+        ++p;
+    }
+    const RcpPart part = P.part[p];
+    const int32_t k0 = c * part.chunk_bins;
+    const int row0 = blk * kRows;
+
+    const int RS = stage_stride(P.stage_cap);
+    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * (P.wave_words + 8);
+    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + T * RS);
+    if (tid < kRows) meta[tid] = decode_row<false, false>(P, part, k0, cidx, row0 + tid);
+    lds_barrier();
+
+    if (wave < kPWaves) {
+        // ================= pile waves
+        int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * (P.wave_words + 8) + 8;
+        auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
+        constexpr int kSteps = kRowsPerWave * kRounds;
+        auto prefetch = [&](int i, int2* dst) {
+            const RowMeta m = uniform_meta(meta[i]);
+            const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
+            if (n) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t q = lane + 64 * u;
+                    dst[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+                }
+            }
+        };
+        int clean_sh = -1;  // the difference array is all zero for this lane geometry
+        auto pile_step = [&](int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
+            const int i = row_of(step);
+            if (step + 1 < kSteps) prefetch(row_of(step + 1), nxt);
+            const RowMeta m = uniform_meta(meta[i]);
+            if (m.flag != 0) return;
+            if (!m.fast && m.heavy < 0) {  // the plan promised single-range rows
+                if (lane == 0) atomicOr(P.status, RCP_STATUS_INTERP);
+                return;
+            }
+            const int32_t npos = m.npos;
+            const int need = (npos + 1 + 63) >> 6;
+            const int sh = need <= 4 ? 2 : 32 - __clz(need - 1);
+            if (clean_sh != sh) {
+                int4* d4 = reinterpret_cast<int4*>(diff);
+                for (int q = lane - 2; q < ((1 << sh) + 4) * 16; q += 64) d4[q] = make_int4(0, 0, 0, 0);
+            }
+            lds_order();
+            if (m.heavy >= 0) {
+                // skewed row: difference array piled up by rcp_heavy_pileup_kernel
+                const int32_t* g = P.heavy_gdiff + (size_t)m.heavy * P.heavy_stride;
+                int32_t carry = 0;
+                for (int q = lane; q < m.P0; q += 64) carry += g[q];
+                carry = wave_sum(carry);
+                for (int q = lane; q <= npos; q += 64) diff[lp(q, sh)] = g[m.P0 + q] + (q == 0 ? carry : 0);
+            } else {
+                const uint32_t n = fast_candidates(m);
+                for (uint32_t q0 = 0; q0 < n; q0 += 256) {
+                    int2 nx[4];
+                    if (q0 + 256 < n) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint32_t q = q0 + 256 + lane + 64 * u;
+                            nx[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+                        }
+                    }
+                    if (m.rev) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (q0 + lane + 64u * u < n) add_read_fast_t<true>(m, cur[u], diff, sh);
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (q0 + lane + 64u * u < n) add_read_fast_t<false>(m, cur[u], diff, sh);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) cur[u] = nx[u];
+                }
+            }
+            lds_order();
+            uint32_t* srow = stage + (i & (T - 1)) * RS;
+            const int lbs = 31 - __clz(m.bs);
+            if (sh == 2) scan_bins_fast<4>(diff, lbs, srow, m.kend - k0);
+            else if (sh == 3) scan_bins_fast<8>(diff, lbs, srow, m.kend - k0);
+            else scan_bins_fast<16>(diff, lbs, srow, m.kend - k0);
+            clean_sh = sh;
+            lds_order();
+        };
+        int2 bufA[4], bufB[4];
+        prefetch(row_of(0), bufA);
+        for (int rd = 0; rd < kRounds; ++rd) {
+            for (int s2 = 0; s2 < kRowsPerWave; s2 += 2) {
+                pile_step(rd * kRowsPerWave + s2, bufA, bufB);
+                pile_step(rd * kRowsPerWave + s2 + 1, bufB, bufA);
+            }
+            lds_barrier();  // A: the round's stage rows are complete
+            lds_barrier();  // B: the store waves hold them in registers
+        }
+    } else {
+        // ================= store waves: thread (row ii, column quad qd)
+        const int st = tid - 64 * kPWaves;
+        const int ii = st & (T - 1);
+        const int qd = st / T;
+        const size_t R = (size_t)P.n_rows;
+        const double sc = P.scale;
+        const int npass = (P.stage_cap + 4 * kLQuads - 1) / (4 * kLQuads);
+        // nothing of this wave is in flight any more (the row-record loads of the metadata
+        // stage have landed): later waits can only be for its own stores, and there are none
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        for (int rd = 0; rd < kRounds; ++rd) {
+            lds_barrier();  // A
+            const int rb = rd * T + ii;
+            const int r = row0 + rb;
+            const RowMeta& mr = meta[rb];
+            const int32_t flag = mr.flag, kend = mr.kend, bs = mr.bs;
+            const bool live = r < P.n_rows && flag != 2;
+            // the round's stage -> registers (uniform pass count; the reads past a row's kend
+            // stay inside LDS and are never stored)
+            uint4 v[kLMaxPass];
+            const uint32_t* st0 = stage + ii * RS + 4 * qd;
+#pragma unroll
+            for (int j = 0; j < kLMaxPass; ++j)
+                v[j] = j < npass ? *reinterpret_cast<const uint4*>(st0 + 4 * kLQuads * j) : make_uint4(0u, 0u, 0u, 0u);
+            lds_barrier();  // B: the stage is free for the next round
+            // opaque after the barrier: keeps the conversions (2 VGPRs per value) below it
+#pragma unroll
+            for (int j = 0; j < kLMaxPass; ++j)
+                if (j < npass) asm volatile("" : "+v"(v[j].x), "+v"(v[j].y), "+v"(v[j].z), "+v"(v[j].w));
+            if (!live) continue;
+            // power-of-two bin width: dividing by its reciprocal is exact; a NULL row (flag 1)
+            // scales its (unwritten) stage words by 0.0 -> zeros
+            const double rdd = 1.0 / (double)(bs > 0 ? bs : 1);
+            const double scf = flag == 0 ? sc : 0.0;
+            const int32_t nk = kend - (k0 + 4 * qd);  // columns left from this thread's first quad
+            double* o = out + (size_t)(part.col_off + k0 + 4 * qd) * R + (size_t)r;
+#pragma unroll
+            for (int j = 0; j < kLMaxPass; ++j) {
+                constexpr int kStep = 4 * kLQuads;
+                if (j >= npass || kStep * j >= nk) break;
+                double* oj = o + (size_t)(kStep * j) * R;
+                const double x[4] = {((double)v[j].x * scf) * rdd, ((double)v[j].y * scf) * rdd,
+                                     ((double)v[j].z * scf) * rdd, ((double)v[j].w * scf) * rdd};
+                if (kStep * j + 3 < nk) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) out_store(x[u], oj + u * R);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (kStep * j + u < nk) out_store(x[u], oj + u * R);
+                }
+            }
+        }
+    }
+}
 
 // =================================================================================
 // interpolation rows (length(x) < n): spline "fmm", neighborhood, "inear" no-op
@@ -1703,6 +1917,25 @@ extern "C" size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr) {
 
 extern "C" int rcp_tile_rows(void) { return kRows; }
 
+// bins per column chunk the lean kernel's store waves can hold
+extern "C" int rcp_lean_max_bins(void) { return 4 * kLQuads * kLMaxPass; }
+
+static hipError_t launch_pileup_lean(const RcpPlanDev* P, double* out, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = allow_big_lds(rcp_pileup_lean_kernel);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    // [pile waves' difference arrays | one stage | row metadata]
+    const size_t lds = 4 * ((size_t)kPWaves * (P->wave_words + 8) + (size_t)kTile * stage_stride(P->stage_cap) +
+                            (size_t)kRows * kMetaWords + 8);
+    const int tiles = (P->n_rows + kRows - 1) / kRows;
+    const int64_t grid = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
+    hipLaunchKernelGGL(rcp_pileup_lean_kernel, dim3((unsigned)grid), dim3(kLBlock), lds, s, *P, out);
+    return hipGetLastError();
+}
+
 template <bool MEDIAN, bool CSR>
 static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* binsum, size_t lds, hipStream_t s) {
     static bool attr_set = false;
@@ -1721,6 +1954,7 @@ extern "C" hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_
                                         hipStream_t stream) {
     if (P->n_rows == 0) return hipSuccess;
     const size_t lds = rcp_pileup_lds_bytes(P, csr);
+    if (!csr && P->lean && P->stat == 0 && !binsum) return launch_pileup_lean(P, out, stream);
     if (csr) return launch_pileup_t<false, true>(P, out, binsum, lds, stream);
     if (P->stat == 1) return launch_pileup_t<true, false>(P, out, binsum, lds, stream);
     return launch_pileup_t<false, false>(P, out, binsum, lds, stream);

@@ -1,0 +1,111 @@
+"""The lean pileup kernel (pile waves + store waves, rcp_kernels.hip rcp_pileup_lean_kernel).
+
+Plans whose rows are all one plain range with uniform power-of-two bins take the lean kernel
+(plan info "pileup_kernel" == 1).  Each case checks it against the CPU oracle (validity and
+means as in test_gpu_random: integer numerators exact, means within 1e-12 relative) and
+bit-for-bit against the general kernel on the same plan (RCP_LEAN=0)."""
+import os
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_random import CHROM_LEN, check, make_reads, single_rows
+
+pytestmark = pytest.mark.gpu
+
+
+def plans(reads, seqlen, rows, bins, strand_filter=None):
+    """(lean result, general result, lean kernel id, expected) for one configuration."""
+    from recoup_amd.engine import Plan, ReadSet
+    from tests import oracle_rows
+    rs = ReadSet(*reads, seqlen, device=0, strand_filter=strand_filter)
+    lean = Plan(rs, rows, bins)
+    os.environ["RCP_LEAN"] = "0"
+    try:
+        general = Plan(rs, rows, bins)
+    finally:
+        del os.environ["RCP_LEAN"]
+    assert general.info["pileup_kernel"] == 0
+    r_lean, r_gen = lean.run(), general.run()
+    ix = oracle_rows.index_for(reads, seqlen, strand_filter)
+    exp = oracle_rows.profile(oracle_rows.row_coverage(ix, rows), bins)
+    return r_lean, r_gen, lean.info["pileup_kernel"], exp
+
+
+def same(a, b):
+    np.testing.assert_array_equal(a[1], b[1])
+    assert np.array_equal(a[0].view(np.uint64), b[0].view(np.uint64))  # bit-identical doubles
+
+
+@pytest.mark.parametrize("width,n_bins", [(2000, 1000), (2000, 500), (2000, 125), (4000, 250), (1024, 1024)])
+def test_lean_binned(gpu, width, n_bins):
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(300 + n_bins)
+    reads = make_reads(rng, 80_000, star_frac=0.1)
+    rows = single_rows(rng, 700, width, edge=True)  # NULL rows: negative index, past the end
+    rows.start[1], rows.end[1] = 1, width  # (a start at 0 shortens its row: an R-RNG layout)
+    lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, Bins([("whole", n_bins)]))
+    assert kind == 1
+    check(lean, exp)
+    same(lean, gen)
+
+
+def test_lean_per_base_and_flanks(gpu):
+    """Per-base parts (C5) and upstream / center / downstream parts of one row table."""
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(41)
+    reads = make_reads(rng, 90_000, widths=(30, 90))
+    rows = single_rows(rng, 333, 4000)
+    for bins in (Bins([("whole", 0, 4000)]),
+                 Bins([("upstream", 0, 1000), ("center", 500), ("downstream", 0, 1000)], flank=(1000, 1000))):
+        lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, bins)
+        assert kind == 1
+        check(lean, exp)
+        same(lean, gen)
+
+
+@pytest.mark.parametrize("strand_filter", [None, "+"])
+def test_lean_stranded_rows(gpu, strand_filter):
+    """ignore.strand = FALSE: up to three candidate streams per row."""
+    from recoup_amd.engine import Bins, RowTable
+    rng = np.random.default_rng(53)
+    reads = make_reads(rng, 70_000, star_frac=0.25)
+    r0 = single_rows(rng, 260, 2048)
+    rows = RowTable(r0.seg_off, r0.chrom, r0.start, r0.end, r0.strand, ignore_strand=False)
+    lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, Bins([("whole", 256)]), strand_filter)
+    assert kind == 1
+    check(lean, exp)
+    same(lean, gen)
+
+
+def test_lean_heavy_rows(gpu):
+    """Skewed rows handed over by the heavy slice kernel."""
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(67)
+    reads = make_reads(rng, 200_000, widths=(100, 200))
+    rows = single_rows(rng, 150, 2000)
+    os.environ["RCP_HEAVY_THRESHOLD"] = "16"
+    try:
+        lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, Bins([("whole", 1000)]))
+    finally:
+        del os.environ["RCP_HEAVY_THRESHOLD"]
+    assert kind == 1
+    check(lean, exp)
+    same(lean, gen)
+
+
+def test_lean_not_taken(gpu):
+    """R-RNG bin layouts, non-power-of-two bins, medians and exon lists stay on the general kernel."""
+    from recoup_amd.engine import Bins, Plan, ReadSet, RowTable
+    rng = np.random.default_rng(71)
+    reads = make_reads(rng, 20_000)
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    rows = single_rows(rng, 50, 2000)
+    assert Plan(rs, rows, Bins([("whole", 150)])).info["pileup_kernel"] == 0       # dif != 0
+    assert Plan(rs, rows, Bins([("whole", 200)])).info["pileup_kernel"] == 0       # bs = 10
+    assert Plan(rs, rows, Bins([("whole", 1000)], stat="median")).info["pileup_kernel"] == 0
+    assert Plan(rs, rows, Bins([("whole", 1000)])).info["pileup_kernel"] == 1
+    seg_off = np.array([0, 2, 3], np.int64)
+    exons = RowTable(seg_off, np.zeros(3, np.int32), np.array([1000, 3000, 9000]), np.array([1999, 3999, 10999]),
+                     np.zeros(3, np.int8), seg_group=np.zeros(3, np.int8), group_is_list=np.array([1, 0, 0, 0], np.uint8))
+    assert Plan(rs, exons, Bins([("whole", 100)])).info["pileup_kernel"] == 0

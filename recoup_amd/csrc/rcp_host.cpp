@@ -35,6 +35,7 @@ size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr);
 size_t rcp_interp_lds_bytes(const RcpPlanDev* P);
 int rcp_tile_rows(void);
 int rcp_lean_max_bins(void);
+size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
 hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
                               const int8_t* strand, int32_t n_chrom, int32_t strand_filter, int merge, uint64_t* keys,
                               int32_t* vals, hipStream_t stream);
@@ -641,8 +642,9 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
             // wide binned chunks would be piled in several wave sub-chunks, each streaming the
             // chunk's reads again: split them into more (up to 8) column chunks instead -- more
             // workgroups for small row counts, and per-chunk read ranges from locate
-            if (!median && !pt.per_base && part_max_bin[p] > 0 && (int64_t)cb * part_max_bin[p] > 1023) {
-                const int32_t cb2 = std::max<int32_t>(1, 1023 / part_max_bin[p]);
+            const int32_t pos_max = env_int("RCP_CHUNK_POS", 1023);  // (tuning experiments)
+            if (!median && !pt.per_base && part_max_bin[p] > 0 && (int64_t)cb * part_max_bin[p] > pos_max) {
+                const int32_t cb2 = std::max<int32_t>(1, pos_max / part_max_bin[p]);
                 const int32_t nch2 = (pt.n_bins + cb2 - 1) / cb2;
                 if (nch2 <= RCP_MAX_CRANGE_CHUNKS) {
                     nch = nch2;
@@ -814,7 +816,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.interp_scratch = plan->scratch.as<double>();
     P.csr_off = nullptr;
     P.csr_out = nullptr;
-    plan->lds = rcp_pileup_lds_bytes(&P, cov_only ? 1 : 0);
+    plan->lds = P.lean ? rcp_pileup_lean_lds_bytes(&P) : rcp_pileup_lds_bytes(&P, cov_only ? 1 : 0);
     plan->grid = (int64_t)((R + rcp_tile_rows() - 1) / rcp_tile_rows()) * P.n_chunks_total;
     if (plan->lds > 160 * 1024) return fail(RCP_EUNSUPPORTED, "plan needs %zu B of LDS", plan->lds);
     HIP_TRY(hipMemset(plan->work.p, 0, plan->work.bytes));

@@ -1420,7 +1420,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
 
 
 // ---------------------------------------------------------------------------------
-// Lean pileup kernel: pile waves + store waves.
+// Lean pileup kernel: persistent workgroups of pile waves + store waves.
 // For plans whose every row is one plain range with uniform power-of-two bins of one
 // wave chunk (C4 peaks, C5 per-base, TSS/TES windows: rcp_plan decides, `P.lean`), the
 // row work is the fused pass only, so the kernel drops the general paths and splits the
@@ -1428,67 +1428,200 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
 //   waves 0..7  (pile)  pile rows into their LDS difference arrays and stage bin sums;
 //                       they never store to global memory
 //   waves 8..11 (store) copy a finished round of the stage into registers and write it
-//                       as R column-major fp64; they never load from global memory
+//                       as R column-major fp64; they never wait for a global load, except
+//                       store wave 0 fetching the next work item (below)
 // gfx9 has one in-order vmcnt for loads and stores, so a wave that stores and then waits
 // for a read also waits for its stores to be acknowledged.  With the roles split, the
 // epilogue's writes of round rd drain while the pile waves already stream round rd + 1.
 // Two LDS-only barriers per round: (A) stage full, (B) stage copied out.
+//
+// Work items are (row tile of kRows rows, column chunk).  Workgroups are persistent (two
+// per CU) and take items from a per-XCD counter: workgroup b serves XCD b % 8 and only
+// tiles t = xcd (mod 8), so the column chunks of one tile (which stream the same reads)
+// share that XCD's L2.  While the pile waves work on item k, store wave 0 claims item
+// k + 1 and decodes its 64 row records into the second metadata buffer, and the pile waves
+// prefetch its first reads during item k's last row: no workgroup start-up latency.
 // ---------------------------------------------------------------------------------
-constexpr int kLStoreWaves = 4;
+#ifndef RCP_LSTORE_WAVES
+#define RCP_LSTORE_WAVES 4
+#endif
+#ifndef RCP_LWPE
+#define RCP_LWPE 6
+#endif
+constexpr int kLStoreWaves = RCP_LSTORE_WAVES;
 constexpr int kLBlock = 64 * (kPWaves + kLStoreWaves);
 constexpr int kLQuads = 64 * kLStoreWaves / kTile;  // column quads per store pass
 constexpr int kLMaxPass = 8;                        // stage_cap <= 4 * kLQuads * kLMaxPass
+static_assert(kRows == 64 && kRounds >= 2, "store wave 0 decodes one row per lane; the next item's "
+                                            "metadata is published one round before it is read");
 
-__global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(6)))
-rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int T = kTile;
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6;
-    const int lane = tid & 63;
-    // XCD-aware (row block, chunk) decode: as rcp_pileup_kernel
-    const int grp = blockIdx.x / (8 * P.n_chunks_total);
-    const int wg = blockIdx.x - grp * 8 * P.n_chunks_total;
-    int c = wg >> 3;
-    const int cidx = c;
-    const int blk = grp * 8 + (wg & 7);
-    if (blk * kRows >= P.n_rows) return;
-    int p = 0;
+// Row metadata of the lean kernel (64 B): w0 = flag | fast << 2 | rev << 3 | log2(bin) << 4
+// | (heavy slot + 1) << 9; the read -> chunk position offset `k` folds orientation and origin.
+struct LeanMeta {
+    int32_t w0, P0, npos, kend;
+    int32_t k, gps, gpe, pad;
+    uint32_t lo[3], hi[3];
+    uint32_t pad2[2];
+};
+static_assert(sizeof(LeanMeta) == 64, "LeanMeta is four b128 words");
+
+__device__ __forceinline__ LeanMeta lean_pack(const RowMeta& m) {
+    LeanMeta q;
+    const int lbs = m.bs > 0 ? 31 - __clz(m.bs) : 0;
+    q.w0 = m.flag | (m.fast << 2) | (m.rev << 3) | (lbs << 4) | ((m.heavy + 1) << 9);
+    q.P0 = m.P0;
+    q.npos = m.npos;
+    q.kend = m.kend;
+    q.k = m.rev ? m.off + m.shi - m.P0 : m.off - m.slo - m.P0;
+    q.gps = m.gps;
+    q.gpe = m.gpe;
+    q.pad = 0;
+    for (int s = 0; s < 3; ++s) {
+        q.lo[s] = m.lo[s];
+        q.hi[s] = m.hi[s];
+    }
+    q.pad2[0] = q.pad2[1] = 0;
+    return q;
+}
+
+struct LeanRow {  // wave-uniform view (SGPRs)
+    int32_t flag, fast, rev, lbs, heavy, P0, npos, kend, k, gps, gpe;
+    uint32_t lo[3], hi[3];
+};
+
+__device__ __forceinline__ LeanRow lean_row(const LeanMeta& src) {
+    const int32_t* s = reinterpret_cast<const int32_t*>(&src);
+    int32_t v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = q == 7 || q >= 14 ? 0 : __builtin_amdgcn_readfirstlane(s[q]);
+    LeanRow m;
+    m.flag = v[0] & 3;
+    m.fast = (v[0] >> 2) & 1;
+    m.rev = (v[0] >> 3) & 1;
+    m.lbs = (v[0] >> 4) & 31;
+    m.heavy = (v[0] >> 9) - 1;
+    m.P0 = v[1]; m.npos = v[2]; m.kend = v[3]; m.k = v[4]; m.gps = v[5]; m.gpe = v[6];
+    for (int q = 0; q < 3; ++q) {
+        m.lo[q] = (uint32_t)v[8 + q];
+        m.hi[q] = (uint32_t)v[11 + q];
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint32_t lean_candidates(const LeanRow& m) {
+    return (m.hi[0] - m.lo[0]) + (m.hi[1] - m.lo[1]) + (m.hi[2] - m.lo[2]);
+}
+
+__device__ __forceinline__ uint32_t lean_index(const LeanRow& m, uint32_t q) {
+    if (m.hi[1] == m.lo[1] && m.hi[2] == m.lo[2]) return m.lo[0] + q;
+    const uint32_t c0 = m.hi[0] - m.lo[0];
+    const uint32_t c1 = m.hi[1] - m.lo[1];
+    return q < c0 ? m.lo[0] + q : (q < c0 + c1 ? m.lo[1] + (q - c0) : m.lo[2] + (q - c0 - c1));
+}
+
+template <bool REV>
+__device__ __forceinline__ void lean_add(const LeanRow& m, int2 rd, int32_t* diff, int sh) {
+    if (rd.y < m.gps || rd.x > m.gpe) return;
+    const int32_t x0 = max(rd.x, m.gps);
+    const int32_t x1 = min(rd.y, m.gpe);
+    const int32_t a = REV ? m.k - x1 : x0 + m.k;
+    const int32_t b = REV ? m.k - x0 + 1 : x1 + m.k + 1;
+    atomicAdd(&diff[lp(a, sh)], 1);
+    atomicAdd(&diff[lp(b, sh)], -1);
+}
+
+// (tile, chunk) of an item code, its part and first bin
+struct LeanItem {
+    int tile, cidx, p;
+    int32_t k0;
+};
+
+__device__ __forceinline__ LeanItem lean_item(const RcpPlanDev& P, int code) {
+    LeanItem it;
+    it.tile = code / P.n_chunks_total;
+    it.cidx = code - it.tile * P.n_chunks_total;
+    int c = it.cidx, p = 0;
     while (p < P.n_parts - 1 && c >= P.part[p].n_chunks) {
         c -= P.part[p].n_chunks;
         ++p;
     }
-    const RcpPart part = P.part[p];
-    const int32_t k0 = c * part.chunk_bins;
-    const int row0 = blk * kRows;
+    it.p = p;
+    it.k0 = c * P.part[p].chunk_bins;
+    return it;
+}
 
+// MAXPER: positions per lane of the widest chunk (16: <= 1023 positions, 8: <= 511)
+template <int MAXPER>
+__global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(RCP_LWPE)))
+rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int T = kTile;
+    constexpr int kSteps = kRowsPerWave * kRounds;  // rows of one wave per item
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int lane = tid & 63;
     const int RS = stage_stride(P.stage_cap);
-    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * (P.wave_words + 8);
-    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + T * RS);
-    if (tid < kRows) meta[tid] = decode_row<false, false>(P, part, k0, cidx, row0 + tid);
+    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * P.wave_words;
+    LeanMeta* lmeta = reinterpret_cast<LeanMeta*>(stage + T * RS);  // [2][kRows]
+    int32_t* item = reinterpret_cast<int32_t*>(lmeta + 2 * kRows);  // [2]: item code or -1
+    const int xcd = blockIdx.x & 7;
+    const int n_tiles = (P.n_rows + kRows - 1) / kRows;
+    const uint32_t n_items_x = (uint32_t)((n_tiles - xcd + 7) / 8) * (uint32_t)P.n_chunks_total;
+
+    // store wave 0: claim the next item of this XCD, decode its rows into buffer buf
+    auto claim = [&](int buf) {
+        uint32_t j = 0;
+        if (lane == 0) j = atomicAdd(&P.status[8 + xcd], 1u);
+        j = __builtin_amdgcn_readfirstlane(j);
+        int code = -1;
+        if (j < n_items_x) {
+            const int tl = (int)(j / P.n_chunks_total);
+            code = (tl * 8 + xcd) * P.n_chunks_total + (int)(j - (uint32_t)tl * P.n_chunks_total);
+            const LeanItem it = lean_item(P, code);
+            lmeta[buf * kRows + lane] =
+                lean_pack(decode_row<false, false>(P, P.part[it.p], it.k0, it.cidx, it.tile * kRows + lane));
+        }
+        if (lane == 0) item[buf] = code;
+        // nothing of the claim stays in flight: later register writes of this wave never
+        // wait on its loads (only its stores remain outstanding, and nothing waits on them)
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+    };
+    if (wave == kPWaves) claim(0);
     lds_barrier();
 
     if (wave < kPWaves) {
         // ================= pile waves
-        int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * (P.wave_words + 8) + 8;
+        int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * P.wave_words;
         auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
-        constexpr int kSteps = kRowsPerWave * kRounds;
-        auto prefetch = [&](int i, int2* dst) {
-            const RowMeta m = uniform_meta(meta[i]);
-            const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
+        auto prefetch = [&](const LeanMeta& mm, int2* dst) {
+            const LeanRow m = lean_row(mm);
+#ifdef RCP_LABL_NOREAD
+            const uint32_t n = 0;
+#else
+            const uint32_t n = (m.flag == 0 && m.fast) ? lean_candidates(m) : 0;
+#endif
             if (n) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const uint32_t q = lane + 64 * u;
-                    dst[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+                    dst[u] = P.se[lean_index(m, q < n ? q : n - 1)];
                 }
             }
         };
         int clean_sh = -1;  // the difference array is all zero for this lane geometry
-        auto pile_step = [&](int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
+        int buf = 0;
+        int code = item[0];
+        // one row: `cur` holds its first reads; the next row's (possibly the next item's
+        // first row) go to `nxt`
+        auto pile_step = [&](const LeanItem& it, int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
             const int i = row_of(step);
-            if (step + 1 < kSteps) prefetch(row_of(step + 1), nxt);
-            const RowMeta m = uniform_meta(meta[i]);
+            if (step + 1 < kSteps) {
+                prefetch(lmeta[buf * kRows + row_of(step + 1)], nxt);
+            } else {
+                const int nc = item[buf ^ 1];  // published by store wave 0 rounds ago
+                if (nc >= 0) prefetch(lmeta[(buf ^ 1) * kRows + row_of(0)], nxt);
+            }
+            const LeanRow m = lean_row(lmeta[buf * kRows + i]);
             if (m.flag != 0) return;
             if (!m.fast && m.heavy < 0) {  // the plan promised single-range rows
                 if (lane == 0) atomicOr(P.status, RCP_STATUS_INTERP);
@@ -1499,7 +1632,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             const int sh = need <= 4 ? 2 : 32 - __clz(need - 1);
             if (clean_sh != sh) {
                 int4* d4 = reinterpret_cast<int4*>(diff);
-                for (int q = lane - 2; q < ((1 << sh) + 4) * 16; q += 64) d4[q] = make_int4(0, 0, 0, 0);
+                for (int q = lane; q < ((1 << sh) + 4) * 16; q += 64) d4[q] = make_int4(0, 0, 0, 0);
             }
             lds_order();
             if (m.heavy >= 0) {
@@ -1510,24 +1643,28 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 carry = wave_sum(carry);
                 for (int q = lane; q <= npos; q += 64) diff[lp(q, sh)] = g[m.P0 + q] + (q == 0 ? carry : 0);
             } else {
-                const uint32_t n = fast_candidates(m);
+#ifdef RCP_LABL_NOREAD  // ablation: no read loads / LDS adds
+                const uint32_t n = 0;
+#else
+                const uint32_t n = lean_candidates(m);
+#endif
                 for (uint32_t q0 = 0; q0 < n; q0 += 256) {
                     int2 nx[4];
                     if (q0 + 256 < n) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             const uint32_t q = q0 + 256 + lane + 64 * u;
-                            nx[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+                            nx[u] = P.se[lean_index(m, q < n ? q : n - 1)];
                         }
                     }
                     if (m.rev) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            if (q0 + lane + 64u * u < n) add_read_fast_t<true>(m, cur[u], diff, sh);
+                            if (q0 + lane + 64u * u < n) lean_add<true>(m, cur[u], diff, sh);
                     } else {
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            if (q0 + lane + 64u * u < n) add_read_fast_t<false>(m, cur[u], diff, sh);
+                            if (q0 + lane + 64u * u < n) lean_add<false>(m, cur[u], diff, sh);
                     }
 #pragma unroll
                     for (int u = 0; u < 4; ++u) cur[u] = nx[u];
@@ -1535,22 +1672,26 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             }
             lds_order();
             uint32_t* srow = stage + (i & (T - 1)) * RS;
-            const int lbs = 31 - __clz(m.bs);
-            if (sh == 2) scan_bins_fast<4>(diff, lbs, srow, m.kend - k0);
-            else if (sh == 3) scan_bins_fast<8>(diff, lbs, srow, m.kend - k0);
-            else scan_bins_fast<16>(diff, lbs, srow, m.kend - k0);
+            if (sh == 2) scan_bins_fast<4>(diff, m.lbs, srow, m.kend - it.k0);
+            else if (MAXPER == 8 || sh == 3) scan_bins_fast<8>(diff, m.lbs, srow, m.kend - it.k0);
+            else scan_bins_fast<MAXPER>(diff, m.lbs, srow, m.kend - it.k0);
             clean_sh = sh;
             lds_order();
         };
         int2 bufA[4], bufB[4];
-        prefetch(row_of(0), bufA);
-        for (int rd = 0; rd < kRounds; ++rd) {
-            for (int s2 = 0; s2 < kRowsPerWave; s2 += 2) {
-                pile_step(rd * kRowsPerWave + s2, bufA, bufB);
-                pile_step(rd * kRowsPerWave + s2 + 1, bufB, bufA);
+        if (code >= 0) prefetch(lmeta[row_of(0)], bufA);
+        while (code >= 0) {
+            const LeanItem it = lean_item(P, code);
+            for (int rd = 0; rd < kRounds; ++rd) {
+                for (int s2 = 0; s2 < kRowsPerWave; s2 += 2) {
+                    pile_step(it, rd * kRowsPerWave + s2, bufA, bufB);
+                    pile_step(it, rd * kRowsPerWave + s2 + 1, bufB, bufA);
+                }
+                lds_barrier();  // A: the round's stage rows are complete
+                lds_barrier();  // B: the store waves hold them in registers
             }
-            lds_barrier();  // A: the round's stage rows are complete
-            lds_barrier();  // B: the store waves hold them in registers
+            buf ^= 1;
+            code = item[buf];
         }
     } else {
         // ================= store waves: thread (row ii, column quad qd)
@@ -1560,51 +1701,75 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         const size_t R = (size_t)P.n_rows;
         const double sc = P.scale;
         const int npass = (P.stage_cap + 4 * kLQuads - 1) / (4 * kLQuads);
-        // nothing of this wave is in flight any more (the row-record loads of the metadata
-        // stage have landed): later waits can only be for its own stores, and there are none
-        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-        for (int rd = 0; rd < kRounds; ++rd) {
-            lds_barrier();  // A
-            const int rb = rd * T + ii;
-            const int r = row0 + rb;
-            const RowMeta& mr = meta[rb];
-            const int32_t flag = mr.flag, kend = mr.kend, bs = mr.bs;
-            const bool live = r < P.n_rows && flag != 2;
-            // the round's stage -> registers (uniform pass count; the reads past a row's kend
-            // stay inside LDS and are never stored)
-            uint4 v[kLMaxPass];
-            const uint32_t* st0 = stage + ii * RS + 4 * qd;
+        int buf = 0;
+        int code = item[0];
+        while (code >= 0) {
+            const LeanItem it = lean_item(P, code);
+            const int32_t col0 = P.part[it.p].col_off + it.k0 + 4 * qd;
+            for (int rd = 0; rd < kRounds; ++rd) {
+                lds_barrier();  // A
+                const int rb = rd * T + ii;
+                const int r = it.tile * kRows + rb;
+                const LeanMeta& mr = lmeta[buf * kRows + rb];
+                const int32_t w0 = mr.w0, kend = mr.kend;
+                const int32_t flag = w0 & 3;
+                const bool live = r < P.n_rows && flag != 2;
+                // the round's stage -> registers (uniform pass count; the reads past a row's
+                // kend stay inside LDS and are never stored)
+                uint4 v[kLMaxPass];
+                const uint32_t* st0 = stage + ii * RS + 4 * qd;
 #pragma unroll
-            for (int j = 0; j < kLMaxPass; ++j)
-                v[j] = j < npass ? *reinterpret_cast<const uint4*>(st0 + 4 * kLQuads * j) : make_uint4(0u, 0u, 0u, 0u);
-            lds_barrier();  // B: the stage is free for the next round
-            // opaque after the barrier: keeps the conversions (2 VGPRs per value) below it
+                for (int j = 0; j < kLMaxPass; ++j)
+                    v[j] = j < npass ? *reinterpret_cast<const uint4*>(st0 + 4 * kLQuads * j) : make_uint4(0u, 0u, 0u, 0u);
+                lds_barrier();  // B: the stage is free for the next round
+                // opaque after the barrier: keeps the conversions (2 VGPRs per value) below it
 #pragma unroll
-            for (int j = 0; j < kLMaxPass; ++j)
-                if (j < npass) asm volatile("" : "+v"(v[j].x), "+v"(v[j].y), "+v"(v[j].z), "+v"(v[j].w));
-            if (!live) continue;
-            // power-of-two bin width: dividing by its reciprocal is exact; a NULL row (flag 1)
-            // scales its (unwritten) stage words by 0.0 -> zeros
-            const double rdd = 1.0 / (double)(bs > 0 ? bs : 1);
-            const double scf = flag == 0 ? sc : 0.0;
-            const int32_t nk = kend - (k0 + 4 * qd);  // columns left from this thread's first quad
-            double* o = out + (size_t)(part.col_off + k0 + 4 * qd) * R + (size_t)r;
+                for (int j = 0; j < kLMaxPass; ++j)
+                    if (j < npass) asm volatile("" : "+v"(v[j].x), "+v"(v[j].y), "+v"(v[j].z), "+v"(v[j].w));
+                if (live) {
+                    // power-of-two bin width: multiplying by its reciprocal is exact; a NULL row
+                    // (flag 1) scales its (unwritten) stage words by 0.0 -> zeros
+                    const double rdd = 1.0 / (double)(1 << ((w0 >> 4) & 31));
+                    const double scf = flag == 0 ? sc : 0.0;
+                    const int32_t nk = kend - (it.k0 + 4 * qd);  // columns left from this thread's first quad
+                    double* o = out + (size_t)col0 * R + (size_t)r;
 #pragma unroll
-            for (int j = 0; j < kLMaxPass; ++j) {
-                constexpr int kStep = 4 * kLQuads;
-                if (j >= npass || kStep * j >= nk) break;
-                double* oj = o + (size_t)(kStep * j) * R;
-                const double x[4] = {((double)v[j].x * scf) * rdd, ((double)v[j].y * scf) * rdd,
-                                     ((double)v[j].z * scf) * rdd, ((double)v[j].w * scf) * rdd};
-                if (kStep * j + 3 < nk) {
+                    for (int j = 0; j < kLMaxPass; ++j) {
+                        constexpr int kStep = 4 * kLQuads;
+                        if (j >= npass || kStep * j >= nk) break;
+                        double* oj = o + (size_t)(kStep * j) * R;
+                        const double x[4] = {((double)v[j].x * scf) * rdd, ((double)v[j].y * scf) * rdd,
+                                             ((double)v[j].z * scf) * rdd, ((double)v[j].w * scf) * rdd};
+#ifdef RCP_LABL_NOSTORE  // ablation: stage copied and converted, no global stores
+                        asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(oj));
+                        continue;
+#endif
+                        if (kStep * j + 3 < nk) {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) out_store(x[u], oj + u * R);
-                } else {
+                            for (int u = 0; u < 4; ++u) out_store(x[u], oj + u * R);
+                        } else {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (kStep * j + u < nk) out_store(x[u], oj + u * R);
+                            for (int u = 0; u < 4; ++u)
+                                if (kStep * j + u < nk) out_store(x[u], oj + u * R);
+                        }
+                    }
                 }
+                // the next item: claimed and decoded after round 0's stores were issued (its
+                // loads wait for them, with a whole round of pile work to hide that); read
+                // by the pile waves from round 2 on, after this wave has passed barrier A(1)
+                if (rd == 0 && wave == kPWaves) claim(buf ^ 1);
             }
+            buf ^= 1;
+            code = item[buf];
+        }
+    }
+    // the last workgroup out resets the item counters for the next launch
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const uint32_t done = atomicAdd(&P.status[16], 1u);
+        if (done == gridDim.x - 1) {
+            for (int x = 0; x < 8; ++x) atomicExch(&P.status[8 + x], 0u);
+            atomicExch(&P.status[16], 0u);
         }
     }
 }
@@ -1920,20 +2085,42 @@ extern "C" int rcp_tile_rows(void) { return kRows; }
 // bins per column chunk the lean kernel's store waves can hold
 extern "C" int rcp_lean_max_bins(void) { return 4 * kLQuads * kLMaxPass; }
 
-static hipError_t launch_pileup_lean(const RcpPlanDev* P, double* out, hipStream_t s) {
+extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
+
+template <int MAXPER>
+static hipError_t launch_pileup_lean_t(const RcpPlanDev* P, double* out, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = allow_big_lds(rcp_pileup_lean_kernel);
+        hipError_t e = allow_big_lds(rcp_pileup_lean_kernel<MAXPER>);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    // [pile waves' difference arrays | one stage | row metadata]
-    const size_t lds = 4 * ((size_t)kPWaves * (P->wave_words + 8) + (size_t)kTile * stage_stride(P->stage_cap) +
-                            (size_t)kRows * kMetaWords + 8);
+    // [pile waves' difference arrays | one stage | row metadata x 2 | item codes x 2]
+    const size_t lds = rcp_pileup_lean_lds_bytes(P);
+    // persistent: as many workgroups as fit at once (LDS: two per CU), a multiple of 8
+    // (workgroup b serves XCD b % 8), never more than there are work items
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+    }
+    const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
     const int tiles = (P->n_rows + kRows - 1) / kRows;
-    const int64_t grid = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
-    hipLaunchKernelGGL(rcp_pileup_lean_kernel, dim3((unsigned)grid), dim3(kLBlock), lds, s, *P, out);
+    const int64_t items = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
+    const int64_t grid = std::min<int64_t>(((int64_t)per_cu * cus + 7) / 8 * 8, items);
+    hipLaunchKernelGGL(rcp_pileup_lean_kernel<MAXPER>, dim3((unsigned)grid), dim3(kLBlock), lds, s, *P, out);
     return hipGetLastError();
+}
+
+extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P) {
+    return 4 * ((size_t)kPWaves * P->wave_words + (size_t)kTile * stage_stride(P->stage_cap)) +
+           2 * (size_t)kRows * sizeof(LeanMeta) + 16;
+}
+
+static hipError_t launch_pileup_lean(const RcpPlanDev* P, double* out, hipStream_t s) {
+    return P->chunk_cap <= 511 ? launch_pileup_lean_t<8>(P, out, s) : launch_pileup_lean_t<16>(P, out, s);
 }
 
 template <bool MEDIAN, bool CSR>

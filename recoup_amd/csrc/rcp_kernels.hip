@@ -1445,6 +1445,11 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
 #ifndef RCP_LSTORE_WAVES
 #define RCP_LSTORE_WAVES 4
 #endif
+// 1: three batches of reads in flight per row instead of two (measured neutral on C4 / C5 /
+// C3, tools/ab_variants.sh: kept as a build option, off by default)
+#ifndef RCP_LRING3
+#define RCP_LRING3 0
+#endif
 #ifndef RCP_LWPE
 #define RCP_LWPE 6
 #endif
@@ -1648,27 +1653,55 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 #else
                 const uint32_t n = lean_candidates(m);
 #endif
-                for (uint32_t q0 = 0; q0 < n; q0 += 256) {
-                    int2 nx[4];
-                    if (q0 + 256 < n) {
+                // batches of 256 reads, three in flight: `cur` (prefetched with the previous
+                // row), b1, b2; the loop is unrolled over the ring so no buffer is copied
+                auto load_batch = [&](uint32_t q0, int2 (&dst)[4]) {
+                    if (q0 < n) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
-                            const uint32_t q = q0 + 256 + lane + 64 * u;
-                            nx[u] = P.se[lean_index(m, q < n ? q : n - 1)];
+                            const uint32_t q = q0 + lane + 64 * u;
+                            dst[u] = P.se[lean_index(m, q < n ? q : n - 1)];
                         }
                     }
+                };
+                auto add_batch = [&](uint32_t q0, const int2 (&src)[4]) {
                     if (m.rev) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            if (q0 + lane + 64u * u < n) lean_add<true>(m, cur[u], diff, sh);
+                            if (q0 + lane + 64u * u < n) lean_add<true>(m, src[u], diff, sh);
                     } else {
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            if (q0 + lane + 64u * u < n) lean_add<false>(m, cur[u], diff, sh);
+                            if (q0 + lane + 64u * u < n) lean_add<false>(m, src[u], diff, sh);
                     }
+                };
+#if RCP_LRING3
+                if (n <= 256) {
+                    add_batch(0, cur);
+                } else {
+                    int2 b1[4], b2[4];
+                    load_batch(256, b1);
+                    load_batch(512, b2);
+                    for (uint32_t q0 = 0; q0 < n; q0 += 768) {
+                        add_batch(q0, cur);
+                        load_batch(q0 + 768, cur);
+                        if (q0 + 256 >= n) break;
+                        add_batch(q0 + 256, b1);
+                        load_batch(q0 + 1024, b1);
+                        if (q0 + 512 >= n) break;
+                        add_batch(q0 + 512, b2);
+                        load_batch(q0 + 1280, b2);
+                    }
+                }
+#else
+                for (uint32_t q0 = 0; q0 < n; q0 += 256) {
+                    int2 nx[4];
+                    load_batch(q0 + 256, nx);
+                    add_batch(q0, cur);
 #pragma unroll
                     for (int u = 0; u < 4; ++u) cur[u] = nx[u];
                 }
+#endif
             }
             lds_order();
             uint32_t* srow = stage + (i & (T - 1)) * RS;

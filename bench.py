@@ -28,6 +28,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+# plan.info["pileup_kernel"] -> kernel name (as rocprofv3 lists it)
+PILEUP_KERNELS = {0: "rcp_pileup_kernel", 1: "rcp_pileup_lean_kernel"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -225,7 +229,8 @@ def main():
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "kernel": "rcp_pileup_kernel", "algorithmic_bytes_per_launch": bytes_pileup,
+                         "kernel": PILEUP_KERNELS[plan.info["pileup_kernel"]],
+                         "algorithmic_bytes_per_launch": bytes_pileup,
                          "kernel_ms": kt[1]},
             "cpu_baseline": cpu,
             "e2e": e2e,

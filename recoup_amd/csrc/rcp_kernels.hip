@@ -178,6 +178,133 @@ __device__ __forceinline__ void pileup_row(const RcpPlanDev& P, int r, int32_t P
     }
 }
 
+// One wave piles row r (any number of segments x strand streams, e.g. a coverageRnaRef
+// c(flank, exons, flank) row) over row positions [P0, P0 + npos).  pileup_row walks the
+// (segment, stream) pairs one after the other -- one HBM round trip per pair, a dozen per
+// gene.  Here lane t owns pair t (its candidate range, narrowed by its own binary searches
+// in parallel with the other lanes'); a wave scan lays the pairs' candidates end to end, and
+// batches of 256 candidates cross pair boundaries, so a row costs one round trip per 256
+// candidates with the next batch in flight while the current one is added.  The per-pair
+// data each candidate needs is picked by a scalar loop over the (few) pairs a batch spans.
+#ifndef RCP_ROW_WAVE
+#define RCP_ROW_WAVE 1
+#endif
+__device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int32_t P0, int32_t npos, int32_t* diff,
+                                                int sh) {
+    const int lane = threadIdx.x & 63;
+    const int32_t P1 = P0 + npos;
+    const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
+    const int n_all = (j1 - j0) * 3;
+    for (int t0 = 0; t0 < n_all; t0 += 64) {
+        // ---- lane t: pair (segment j, stream s)
+        const int t = t0 + lane;
+        RcpSeg sg = {};
+        int32_t gps = 0, gpe = -1;
+        uint32_t lo = 0, hi = 0;
+        if (t < n_all) {
+            const int j = j0 + t / 3, s = t % 3;
+            sg = P.segs[j];
+            const int32_t len = sg.hi - sg.lo + 1;
+            const int32_t a = max(P0, sg.off);
+            const int32_t b = min(P1, sg.off + len);
+            if (a < b && sg.query_ok && ((sg.streams >> s) & 1)) {
+                if (!sg.rev) {
+                    gps = sg.lo + (a - sg.off);
+                    gpe = sg.lo + (b - 1 - sg.off);
+                } else {
+                    gpe = sg.hi - (a - sg.off);
+                    gps = sg.hi - (b - 1 - sg.off);
+                }
+                lo = P.seg_lo[j * 3 + s];
+                hi = P.seg_hi[j * 3 + s];
+                const bool full = (a == sg.off) && (b == sg.off + len);
+                if (lo < hi && !full && hi - lo > 1024) {
+                    lo = lower_bound_pmax(P.pmax, lo, hi, gps);
+                    hi = upper_bound_start(P.se, lo, hi, gpe);
+                }
+                if (hi < lo) hi = lo;
+            }
+        }
+        const uint32_t cnt = hi - lo;
+        const uint32_t incl = wave_inclusive_scan(cnt);
+        const uint32_t start = incl - cnt;
+        const uint32_t N = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (N == 0) continue;  // wave-uniform
+        const uint32_t delta = lo - start;  // candidate q of this pair is read lo + (q - start)
+        const uint64_t nz = __ballot(cnt > 0);
+        // pairs a batch [q0, q0 + 256) spans: nonempty pairs from the one holding q0
+        int pl = __builtin_ctzll(nz);  // pair holding the next batch's first candidate (loads)
+        auto load_batch = [&](uint32_t q0, int2 (&dst)[4], int (&sel)[4]) {
+            while ((uint32_t)__builtin_amdgcn_readlane((int)incl, pl) <= q0) ++pl;
+            uint32_t qc[4], d[4];
+            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)delta, pl);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                qc[u] = min(q0 + lane + 64u * u, N - 1);
+                sel[u] = pl;
+                d[u] = d0;
+            }
+            const uint32_t qe = min(q0 + 256u, N);
+            uint64_t m = pl < 63 ? nz & (~0ull << (pl + 1)) : 0ull;
+            while (m) {
+                const int p = __builtin_ctzll(m);
+                const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)start, p);
+                if (sp >= qe) break;
+                const uint32_t dp = (uint32_t)__builtin_amdgcn_readlane((int)delta, p);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (qc[u] >= sp) {
+                        sel[u] = p;
+                        d[u] = dp;
+                    }
+                m &= m - 1;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) dst[u] = P.se[qc[u] + d[u]];
+        };
+        int pa = pl;  // pair holding the current batch's first candidate (adds)
+        auto add_batch = [&](uint32_t q0, const int2 (&rd)[4], const int (&sel)[4]) {
+            while ((uint32_t)__builtin_amdgcn_readlane((int)incl, pa) <= q0) ++pa;
+            const uint32_t qe = min(q0 + 256u, N);
+            uint64_t m = nz & (~0ull << pa);
+            while (m) {
+                const int p = __builtin_ctzll(m);
+                if ((uint32_t)__builtin_amdgcn_readlane((int)start, p) >= qe) break;
+                RcpSeg o;
+                o.lo = __builtin_amdgcn_readlane(sg.lo, p);
+                o.hi = __builtin_amdgcn_readlane(sg.hi, p);
+                o.off = __builtin_amdgcn_readlane(sg.off, p);
+                o.gfirst = __builtin_amdgcn_readlane(sg.gfirst, p);
+                o.gcount = (int16_t)__builtin_amdgcn_readlane((int)sg.gcount, p);
+                o.rev = (uint8_t)__builtin_amdgcn_readlane((int)sg.rev, p);
+                o.multi = (uint8_t)__builtin_amdgcn_readlane((int)sg.multi, p);
+                o.nb_lo = __builtin_amdgcn_readlane(sg.nb_lo, p);
+                o.nb_hi = __builtin_amdgcn_readlane(sg.nb_hi, p);
+                const int32_t ps = __builtin_amdgcn_readlane(gps, p);
+                const int32_t pe = __builtin_amdgcn_readlane(gpe, p);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (sel[u] == p && q0 + lane + 64u * u < N) add_read(P, o, rd[u], ps, pe, P0, diff, sh);
+                m &= m - 1;
+            }
+        };
+        int2 cur[4];
+        int scur[4];
+        load_batch(0, cur, scur);
+        for (uint32_t q0 = 0; q0 < N; q0 += 256) {
+            int2 nx[4];
+            int snx[4];
+            if (q0 + 256 < N) load_batch(q0 + 256, nx, snx);
+            add_batch(q0, cur, scur);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                cur[u] = nx[u];
+                scur[u] = snx[u];
+            }
+        }
+    }
+}
+
 // Wave scan of the 64*per positions of a padded wave array (lane l owns positions
 // [l*per, (l+1)*per) at words l*(per+4) ..): depth (CUM = false) or cumulative depth.
 template <bool CUM>
@@ -1321,7 +1448,11 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
                         for (int u = 0; u < 4; ++u) cur[u] = nx[u];
                     }
                 } else {
+#if RCP_ROW_WAVE
+                    pileup_row_wave(P, r, m.P0 + s0, sn, diff, sh);
+#else
                     pileup_row(P, r, m.P0 + s0, sn, diff, lane, 64, sh);
+#endif
                 }
                 lds_order();
                 if (!MEDIAN && !CSR && fast_bins) {
@@ -1840,7 +1971,11 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* c, d
         d[i] = 1.0;
     }
     __syncthreads();
+#ifdef RCP_IABL_NOSPLINE  // ablation: no serial recurrences
+    if (t == 0 && n < 0) {
+#else
     if (t == 0) {
+#endif
         b[0] = -1.0;
         b[n - 1] = -1.0;
         d[0] = 1.0;
@@ -2011,7 +2146,9 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
         if (threadIdx.x == 0) atomicOr(P.status, RCP_STATUS_INTERP);
         return;
     }
+#ifndef RCP_IABL_NOWIN
     block_window_depth(P, r, head, L, diff, scratch);
+#endif
     // the spline / fill works on LDS copies (global scratch only for huge rows)
     double* x = P.interp_lds >= 0 ? reinterpret_cast<double*>(smem + P.interp_lds)
                                   : P.interp_scratch + (size_t)e * P.interp_stride;
@@ -2024,7 +2161,11 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
         double* d = c + L + 1;
         int32_t* iv = reinterpret_cast<int32_t*>(d + L + 1);
         fmm_spline_block(L, x, b, c, d);
+#ifdef RCP_IABL_NOIV
+        for (int k = threadIdx.x; k < n; k += kBlock) iv[k] = min((int)((int64_t)k * (L - 1) / n), L - 1);
+#else
         if (threadIdx.x == 0) spline_intervals(L, n, iv);
+#endif
         __syncthreads();
         for (int k = threadIdx.x; k < n; k += kBlock) {
             double v;

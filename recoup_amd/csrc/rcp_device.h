@@ -99,6 +99,10 @@ struct RcpPlanDev {
     const int32_t* interp_mode; // [n_interp] 1 spline, 2 linear (no-op), 3 neighborhood
     const int32_t* interp_pos;  // [n_interp] offset into nb_pos (neighborhood) or -1
     const int32_t* nb_pos;      // orig.pos tables (1-based, sorted)
+    // fmm spline elimination on unit knot spacing (R splines.c fmm_spline): the pivots do not
+    // depend on the data, so spl_tb[2i] = t_i = 1 / b_{i-1} and spl_tb[2i+1] = b_i (b_0 = -1,
+    // b_i = 4 - t_i) are tabulated once on the host, in R's operation order (exact IEEE ops)
+    const double* spl_tb;       // [2 * (interp_cap + 1)]
     double* interp_scratch;     // per interp row: 5 * max_interp_len doubles
     int32_t interp_stride;
     int32_t interp_lds;         // byte offset of the row's doubles in LDS, -1 = global scratch (launcher)

@@ -750,6 +750,19 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     const size_t o_imode = put(blob, B.interp_mode);
     const size_t o_ipos = put(blob, B.interp_pos);
     const size_t o_nb = put(blob, B.nb_pos);
+    // fmm pivots (see RcpPlanDev::spl_tb): the elimination of R's fmm_spline with d[i] = 1
+    std::vector<double> spl_tb(2 * ((size_t)std::max(max_interp_len, 1) + 1), 0.0);
+    {
+        double bp = -1.0;
+        spl_tb[1] = bp;
+        for (size_t i = 1; 2 * i + 1 < spl_tb.size(); ++i) {
+            const double t = 1.0 / bp;
+            bp = 4.0 - t;
+            spl_tb[2 * i] = t;
+            spl_tb[2 * i + 1] = bp;
+        }
+    }
+    const size_t o_spl = put(blob, spl_tb);
     HIP_TRY(plan->tables.alloc(blob.size()));
     HIP_TRY(hipMemcpy(plan->tables.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
     char* base = plan->tables.as<char>();
@@ -813,6 +826,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.interp_mode = reinterpret_cast<const int32_t*>(base + o_imode);
     P.interp_pos = reinterpret_cast<const int32_t*>(base + o_ipos);
     P.nb_pos = reinterpret_cast<const int32_t*>(base + o_nb);
+    P.spl_tb = reinterpret_cast<const double*>(base + o_spl);
     P.interp_scratch = plan->scratch.as<double>();
     P.csr_off = nullptr;
     P.csr_out = nullptr;

@@ -1946,11 +1946,16 @@ namespace {
 #pragma clang fp contract(off)
 // stats::spline method "fmm" (R splines.c fmm_spline) on knots x = 1..n: every knot spacing
 // d[i] is 1.0, so the operations below are the original ones with the multiplications and
-// divisions by d[i] = 1.0 (exact) dropped.  Data-parallel loops run over the block's
-// threads; the two recurrences (forward elimination, back substitution) run on thread 0
-// with register carries.  Same operations in the same order per element as R: bit-equal.
+// divisions by d[i] = 1.0 (exact) dropped.  With unit spacing the elimination's pivots
+// b_i and multipliers t_i = 1 / b_{i-1} do not depend on y: the host tabulates them once
+// per plan (P.spl_tb, same operations in the same order), so the forward elimination is
+// the dependent chain c_i = c_i - t_i c_{i-1} alone (one multiply, one subtract per step)
+// and the back substitution divides by tabulated pivots; both chains run on thread 0 with
+// the next 8 table / LDS values loaded ahead.  Data-parallel loops run over the block.
+// Same operations in the same order per element as R: bit-equal.
 // Call from all threads of the block; y, b, c, d in LDS (or global), 0-based.
-__device__ void fmm_spline_block(int n, const double* y, double* b, double* c, double* d) {
+__device__ void fmm_spline_block(int n, const double* y, double* b, double* __restrict__ c, double* d,
+                                 const double* __restrict__ tb) {
     const int t = threadIdx.x;
     if (n < 3) {
         if (t == 0) {
@@ -1964,21 +1969,14 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* c, d
         __syncthreads();
         return;
     }
-    // 1-based i = 2 .. n-1 (0-based i - 1): c[i] = (y[i+1] - y[i]) - (y[i] - y[i-1]), b[i] = 4
-    for (int i = 1 + t; i < n - 1; i += blockDim.x) {
-        c[i] = (y[i + 1] - y[i]) - (y[i] - y[i - 1]);
-        b[i] = 2.0 * (1.0 + 1.0);
-        d[i] = 1.0;
-    }
+    // 1-based i = 2 .. n-1 (0-based i - 1): c[i] = (y[i+1] - y[i]) - (y[i] - y[i-1])
+    for (int i = 1 + t; i < n - 1; i += blockDim.x) c[i] = (y[i + 1] - y[i]) - (y[i] - y[i - 1]);
     __syncthreads();
 #ifdef RCP_IABL_NOSPLINE  // ablation: no serial recurrences
     if (t == 0 && n < 0) {
 #else
     if (t == 0) {
 #endif
-        b[0] = -1.0;
-        b[n - 1] = -1.0;
-        d[0] = 1.0;
         double c1 = 0.0, cn = 0.0;
         if (n > 3) {
             c1 = c[2] / 2.0 - c[1] / 2.0;
@@ -1989,21 +1987,45 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* c, d
         c[0] = c1;
         c[n - 1] = cn;
         // forward elimination: t = d[i-1] / b[i-1]; b[i] -= t d[i-1]; c[i] -= t c[i-1]
-        double bp = b[0], cp = c1;
-        for (int i = 1; i < n; ++i) {
-            const double tt = 1.0 / bp;
-            const double bi = b[i] - tt;
-            const double ci = c[i] - tt * cp;
-            b[i] = bi;
-            c[i] = ci;
-            bp = bi;
-            cp = ci;
+        double cp = c1;
+        int i = 1;
+        for (; i + 8 <= n; i += 8) {
+            double cv[8], tv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cv[u] = c[i + u];
+                tv[u] = tb[2 * (i + u)];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cp = cv[u] - tv[u] * cp;
+                c[i + u] = cp;
+            }
         }
-        // back substitution
-        double cnext = cp / bp;
+        for (; i < n; ++i) {
+            cp = c[i] - tb[2 * i] * cp;
+            c[i] = cp;
+        }
+        const double bn = -1.0 - tb[2 * (n - 1)];  // b[n-1] = -1 - t_{n-1}
+        // back substitution: c[i] = (c[i] - c[i+1]) / b[i]
+        double cnext = cp / bn;
         c[n - 1] = cnext;
-        for (int i = n - 2; i >= 0; --i) {
-            cnext = (c[i] - cnext) / b[i];
+        i = n - 2;
+        for (; i >= 7; i -= 8) {
+            double cv[8], bv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cv[u] = c[i - u];
+                bv[u] = tb[2 * (i - u) + 1];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cnext = (cv[u] - cnext) / bv[u];
+                c[i - u] = cnext;
+            }
+        }
+        for (; i >= 0; --i) {
+            cnext = (c[i] - cnext) / tb[2 * i + 1];
             c[i] = cnext;
         }
         b[n - 1] = (y[n - 1] - y[n - 2]) + (c[n - 2] + 2.0 * c[n - 1]);
@@ -2046,6 +2068,28 @@ __device__ void spline_intervals(int L, int n, int32_t* iv) {
         }
         iv[k] = i;
     }
+}
+
+__device__ __forceinline__ int spline_bisect(int L, double u) {
+    int i = 0, j = L;
+    do {
+        const int m = (i + j) / 2;
+        if (u < (double)(m + 1)) j = m; else i = m;
+    } while (j > i + 1);
+    return i;
+}
+
+// The same interval for point k alone, for interpolated rows (L < n: output points closer
+// than one knot apart).  spline_intervals keeps interval i for u in [i+1, i+2] and bisects
+// otherwise; the bisection lands on floor(u) - 1, so the two differ only at a point sitting
+// exactly on a knot m = i + 2 just after a point of interval i (it keeps i, the evaluation
+// runs at dx = 1).  Because consecutive points are less than 1 apart, the interval held at
+// point k - 1 is bisect(u_{k-1}) whenever it matters, and each point is decided alone.
+__device__ __forceinline__ int spline_interval_at(int L, int n, int k) {
+    const double u = seq_point(L, n, k);
+    const int prev = k == 0 ? 0 : spline_bisect(L, seq_point(L, n, k - 1));
+    if (u < (double)(prev + 1) || (prev < L - 1 && (double)(prev + 2) < u)) return spline_bisect(L, u);
+    return prev;
 }
 
 // spline_eval's cubic on interval i (no FMA contraction: R's rounding)
@@ -2160,12 +2204,12 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
         double* c = b + L + 1;
         double* d = c + L + 1;
         int32_t* iv = reinterpret_cast<int32_t*>(d + L + 1);
-        fmm_spline_block(L, x, b, c, d);
-#ifdef RCP_IABL_NOIV
-        for (int k = threadIdx.x; k < n; k += kBlock) iv[k] = min((int)((int64_t)k * (L - 1) / n), L - 1);
-#else
-        if (threadIdx.x == 0) spline_intervals(L, n, iv);
-#endif
+        fmm_spline_block(L, x, b, c, d, P.spl_tb);
+        if (L < n) {  // always, for rows of this kernel; the sequential walk stays as the rule
+            for (int k = threadIdx.x; k < n; k += kBlock) iv[k] = spline_interval_at(L, n, k);
+        } else if (threadIdx.x == 0) {
+            spline_intervals(L, n, iv);
+        }
         __syncthreads();
         for (int k = threadIdx.x; k < n; k += kBlock) {
             double v;

@@ -190,6 +190,29 @@ def test_genebody_unequal_interp(gpu):
     check(res, exp, rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("n_bins", [201, 150, 1000])
+def test_spline_rows_bit_exact(gpu, n_bins):
+    """Interpolated rows (length < bins) equal R's spline() bit for bit: widths whose output
+    points fall exactly on knots (n = 201, L = 101 / 51 / 41 / 21 / 11 / 5: points 1/2, 1/4,
+    ... apart), where spline_eval keeps the previous interval and evaluates at dx = 1, plus
+    widths 2 and 3 (the n < 4 branches) and a spread of others."""
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(31 + n_bins)
+    reads = make_reads(rng, 60_000, widths=(20, 200))
+    widths = [2, 3, 4, 5, 11, 21, 41, 51, 101, 149, 150, 200]
+    widths = [w for w in widths if w < n_bins] + list(rng.integers(2, min(n_bins, 700), 12))
+    from recoup_amd.engine import RowTable
+    R = len(widths) * 6
+    chrom = rng.integers(0, 3, R).astype(np.int32)
+    w = np.repeat(np.array(widths, dtype=np.int64), 6)
+    # starts inside the hot spots' span so most rows carry signal
+    s = np.array([rng.integers(2000, CHROM_LEN[c] - 2000) for c in chrom], dtype=np.int64)
+    rows = RowTable.from_ranges(chrom, s, s + w - 1, rng.integers(0, 2, R).astype(np.int8))
+    res, exp = run_case(reads, CHROM_LEN, rows, Bins([("whole", n_bins)], interp="spline"))
+    np.testing.assert_array_equal(res[1], exp[1])
+    np.testing.assert_array_equal(res[0], exp[0])
+
+
 def test_long_rows_chunked(gpu):
     """Rows longer than one chunk: per-base (chunked columns) and coarse bins."""
     from recoup_amd.engine import Bins

@@ -191,6 +191,9 @@ __device__ __forceinline__ void pileup_row(const RcpPlanDev& P, int r, int32_t P
 #endif
 __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int32_t P0, int32_t npos, int32_t* diff,
                                                 int sh) {
+#ifdef RCP_ABL_RW_SKIP  // ablation: no reads at all for multi-range rows
+    return;
+#endif
     const int lane = threadIdx.x & 63;
     const int32_t P1 = P0 + npos;
     const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
@@ -282,9 +285,13 @@ __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int3
                 o.nb_hi = __builtin_amdgcn_readlane(sg.nb_hi, p);
                 const int32_t ps = __builtin_amdgcn_readlane(gps, p);
                 const int32_t pe = __builtin_amdgcn_readlane(gpe, p);
+#ifdef RCP_ABL_RW_NOADD  // ablation: reads loaded, not added
+                asm volatile("" ::"v"(rd[0].x), "v"(rd[1].x), "v"(rd[2].x), "v"(rd[3].x), "s"(ps), "s"(pe));
+#else
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     if (sel[u] == p && q0 + lane + 64u * u < N) add_read(P, o, rd[u], ps, pe, P0, diff, sh);
+#endif
                 m &= m - 1;
             }
         };
@@ -1505,6 +1512,9 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
                 } else if (whole) {
                     // splitVector layout: enlarged bins from set.seed(42); sample(1:n, dif)
                     const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
+#ifdef RCP_ABL_BINS
+                    if (lane < 64) continue;
+#endif
                     for (int32_t k = k0 + lane; k < kend; k += 64) {
                         const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
                         const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;

@@ -43,7 +43,10 @@ def main():
         ("center only", [("center", cb)]),
         ("downstream only", [("downstream", fb)]),
     ]
+    only = sys.argv[1:]  # case names to run (default: all)
     for name, parts in cases:
+        if only and name.split()[0] not in only:
+            continue
         plan = Plan(rs, rows, Bins(parts, flank=fl))
         out = plan.empty_output()
         t = timed(plan, out)

@@ -1676,6 +1676,22 @@ __device__ __forceinline__ void lean_add(const LeanRow& m, int2 rd, int32_t* dif
     atomicAdd(&diff[lp(b, sh)], -1);
 }
 
+// Dense rows (at least one candidate read per position, e.g. C5's per-base DNase rows): the
+// 64 reads of a wave are consecutive in start order and pile onto a few dozen positions, so
+// plain LDS atomics serialise on equal addresses (C5: 1.7e8 bank-conflict cycles, 10x C4's).
+// Equal positions of neighbouring lanes are merged into one add per run (run_add); all lanes
+// of the wave take part (`act` false for lanes past the row's candidates).
+template <bool REV>
+__device__ __forceinline__ void lean_add_runs(const LeanRow& m, int2 rd, bool act, int32_t* diff, int sh) {
+    act = act && !(rd.y < m.gps || rd.x > m.gpe);
+    const int32_t x0 = max(rd.x, m.gps);
+    const int32_t x1 = min(rd.y, m.gpe);
+    const int32_t a = REV ? m.k - x1 : x0 + m.k;
+    const int32_t b = REV ? m.k - x0 + 1 : x1 + m.k + 1;
+    run_add(diff, lp(a, sh), act, 1);
+    run_add(diff, lp(b, sh), act, -1);
+}
+
 // (tile, chunk) of an item code, its part and first bin
 struct LeanItem {
     int tile, cidx, p;
@@ -1805,8 +1821,20 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                         }
                     }
                 };
+#ifndef RCP_LDENSE
+#define RCP_LDENSE 1
+#endif
+                const bool dense = RCP_LDENSE && n >= (uint32_t)npos;  // wave-uniform
                 auto add_batch = [&](uint32_t q0, const int2 (&src)[4]) {
-                    if (m.rev) {
+                    if (dense) {
+                        if (m.rev) {
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) lean_add_runs<true>(m, src[u], q0 + lane + 64u * u < n, diff, sh);
+                        } else {
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) lean_add_runs<false>(m, src[u], q0 + lane + 64u * u < n, diff, sh);
+                        }
+                    } else if (m.rev) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
                             if (q0 + lane + 64u * u < n) lean_add<true>(m, src[u], diff, sh);

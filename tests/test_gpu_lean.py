@@ -78,6 +78,33 @@ def test_lean_stranded_rows(gpu, strand_filter):
     same(lean, gen)
 
 
+@pytest.mark.parametrize("stranded", [False, True])
+def test_lean_dense_rows(gpu, stranded):
+    """Rows with more reads than positions (C5-like DNase depth, PCR-duplicate stacks): the
+    run-merged LDS adds, on both row orientations, per-base and binned, in both layouts."""
+    from recoup_amd.engine import Bins, RowTable
+    rng = np.random.default_rng(59)
+    n = 240_000
+    chrom = rng.integers(0, 3, n).astype(np.int32)
+    base = np.array([20_000, 30_000, 40_000])[chrom]
+    start = base + rng.integers(0, 12_000, n)
+    dup = rng.random(n) < 0.3  # duplicate stacks: runs of equal starts and ends
+    start[dup] = base[dup] + 4000 + 37 * rng.integers(0, 40, dup.sum())
+    width = np.where(dup, 50, rng.integers(20, 80, n))
+    reads = (chrom, start.astype(np.int32), (start + width - 1).astype(np.int32),
+             rng.integers(0, 3, n).astype(np.int8))
+    R = 240
+    rc = rng.integers(0, 3, R).astype(np.int32)
+    rs_ = np.array([20_000, 30_000, 40_000])[rc] + rng.integers(-500, 10_000, R)
+    strand = rng.integers(0, 3, R).astype(np.int8)
+    rows = RowTable(np.arange(R + 1), rc, rs_, rs_ + 2047, strand, ignore_strand=not stranded)
+    for bins in (Bins([("whole", 0, 2048)]), Bins([("whole", 512)])):
+        lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, bins)
+        assert kind == 1
+        check(lean, exp)
+        same(lean, gen)
+
+
 def test_lean_heavy_rows(gpu):
     """Skewed rows handed over by the heavy slice kernel."""
     from recoup_amd.engine import Bins

@@ -96,6 +96,22 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
 // by 4 words per lane (bank-conflict-free b128 scans); sh = 30 leaves p unchanged.
 __device__ __forceinline__ int32_t lp(int32_t p, int sh) { return p + ((p >> sh) << 2); }
 
+// diff[key] += w * (length of the run of equal keys starting at this lane), once per run of
+// consecutive lanes holding the same key; inactive lanes split runs and add nothing.  The
+// reads of a wave are consecutive in start order, so the reads of a hot row pile onto a
+// few positions per wave: one LDS atomic per run instead of one per read.
+__device__ __forceinline__ void run_add(int32_t* diff, int32_t key, bool act, int32_t w) {
+    const int lane = threadIdx.x & 63;
+    const int32_t k = act ? key : -1;                                   // -1: never a position
+    const int32_t prev = __builtin_amdgcn_update_dpp(-2, k, 0x138, 0xf, 0xf, false);  // wave_shr:1
+    const bool head = lane == 0 || k != prev;
+    const uint64_t heads = __ballot(head);
+    const uint64_t above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+    const int nxt = above ? __builtin_ctzll(above) : 64;
+    if (head && act) atomicAdd(&diff[k], w * (nxt - lane));
+}
+
+
 __device__ __forceinline__ void add_read(const RcpPlanDev& P, const RcpSeg& sg, int2 rd, int32_t gps, int32_t gpe,
                                          int32_t P0, int32_t* diff, int sh) {
     if (rd.y < gps || rd.x > gpe) return;
@@ -836,21 +852,6 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_plan_kernel(RcpPlanDev P) {
 #define RCP_HEAVY_LOADS 16
 #endif
 constexpr int kHeavyLoads = RCP_HEAVY_LOADS;  // = RCP_HEAVY_SLICE / kBlock: one round trip per slice
-
-// diff[key] += w * (length of the run of equal keys starting at this lane), once per run of
-// consecutive lanes holding the same key; inactive lanes split runs and add nothing.  The
-// reads of a wave are consecutive in start order, so the reads of a hot row pile onto a
-// few positions per wave: one LDS atomic per run instead of one per read.
-__device__ __forceinline__ void run_add(int32_t* diff, int32_t key, bool act, int32_t w) {
-    const int lane = threadIdx.x & 63;
-    const int32_t k = act ? key : -1;                                   // -1: never a position
-    const int32_t prev = __builtin_amdgcn_update_dpp(-2, k, 0x138, 0xf, 0xf, false);  // wave_shr:1
-    const bool head = lane == 0 || k != prev;
-    const uint64_t heads = __ballot(head);
-    const uint64_t above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
-    const int nxt = above ? __builtin_ctzll(above) : 64;
-    if (head && act) atomicAdd(&diff[k], w * (nxt - lane));
-}
 
 __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];

@@ -1,4 +1,5 @@
-"""Minimal C4 run for rocprofv3 counter passes (one plan, a few executes)."""
+"""Minimal run of one BASELINE config (c4 default; c2, c3, c5) for rocprofv3 counter passes (one plan, a few
+executes).  C3_PART=center keeps one column part of C3."""
 import os
 import sys
 
@@ -10,10 +11,18 @@ from recoup_amd.engine import Bins, Plan, ReadSet, RowTable  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c4"
 d = getattr(synthetic, cfg)(device="cuda:0")
-reg = d["regions"]
 rs = ReadSet(*d["reads"], d["seqlen"], device=0)
-rows = RowTable.from_ranges(reg["chrom"], reg["start"], reg["end"], reg["strand"])
-bins = Bins([("whole", d["n_bins"])]) if d["n_bins"] else Bins([("whole", 0, sum(d["flank"]))])
+if cfg == "c3":  # coverageRnaRef rows, flank / centre / flank parts (as bench.py)
+    rows = synthetic.rna_rows(d)
+    parts = [("upstream", d["flank_bins"]), ("center", d["region_bins"]), ("downstream", d["flank_bins"])]
+    if os.environ.get("C3_PART"):
+        parts = [p for p in parts if p[0] == os.environ["C3_PART"]]
+    bins = Bins(parts, flank=d["flank"])
+    reg = {"start": rows.seg_off[1:]}
+else:
+    reg = d["regions"]
+    rows = RowTable.from_ranges(reg["chrom"], reg["start"], reg["end"], reg["strand"])
+    bins = Bins([("whole", d["n_bins"])]) if d["n_bins"] else Bins([("whole", 0, sum(d["flank"]))])
 plan = Plan(rs, rows, bins)
 out = plan.empty_output()
 for _ in range(int(os.environ.get("ITERS", "3"))):

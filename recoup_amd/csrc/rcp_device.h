@@ -29,6 +29,22 @@ struct RcpSeg {
     int32_t nb_lo, nb_hi;
 };
 
+// Per-row locate input, built with the plan from the row table and the bound readset's stream
+// directory offsets: one 80-byte load per row instead of a chain of dependent table loads
+// (row_seg -> segs, row_chrom -> dir_off / seqlen).
+struct RcpRowInfo {
+    int32_t j0, j1;    // segments [j0, j1)
+    int32_t chrom;     // chromosome index
+    int32_t row_len;   // nominal coverage length nr
+    int64_t seqlen;    // seqlengths[chrom] (-1 = NA)
+    int64_t d0;        // first directory entry of stream chrom*3 in the plan's layout
+    int32_t nb;        // its bucket count
+    int32_t stat;      // row_static
+    int32_t pad[2];
+    RcpSeg seg0;       // segment j0
+};
+static_assert(sizeof(RcpSeg) == 32 && sizeof(RcpRowInfo) == 80, "RcpRowInfo is five 16-byte words");
+
 // Per-row record the locate kernel leaves for the pileup kernel (one 64-byte load per row
 // instead of a chain of dependent loads).  lo/hi are the row's candidate reads per strand
 // stream when the row is a single range (flags & RCP_REC_FAST).
@@ -79,6 +95,7 @@ struct RcpPlanDev {
     const int32_t* row_len;     // [n_rows] nominal coverage length nr
     const uint8_t* row_static;  // [n_rows] 1 = statically NULL (negative index, bad chrom)
     const RcpSeg* segs;
+    const RcpRowInfo* row_info; // [n_rows]
     // locate outputs
     uint32_t* seg_lo;           // [n_seg * 3]
     uint32_t* seg_hi;           // [n_seg * 3]

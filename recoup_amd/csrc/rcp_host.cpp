@@ -173,6 +173,7 @@ int check_device(int dev) {
 // so the default path searches and streams one range per segment instead of three.
 struct ReadLayout {
     std::vector<int64_t> h_stream_off;  // n_chrom*3 + 1
+    std::vector<int64_t> h_dir_off;     // n_chrom*3 + 1
     DevBuf se, pmax, stream_off;
     DevBuf dir_l, dir_u, dir_off;
     int32_t dir_shift = 12;
@@ -282,6 +283,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     HIP_TRY(L->dir_l.alloc(4 * std::max<int64_t>(ne, 1)));
     HIP_TRY(L->dir_u.alloc(4 * std::max<int64_t>(ne, 1)));
     HIP_TRY(hipMemcpyAsync(L->dir_off.p, doff.data(), 8 * (n_streams + 1), hipMemcpyHostToDevice, s));
+    L->h_dir_off = doff;
     HIP_TRY(rcp_launch_dir(ne, n_streams, L->dir_off.as<int64_t>(), L->stream_off.as<int64_t>(),
                            L->pmax.as<int32_t>(), L->se.as<int2>(), shift, L->dir_l.as<int32_t>(),
                            L->dir_u.as<int32_t>(), s));
@@ -750,6 +752,28 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     const size_t o_imode = put(blob, B.interp_mode);
     const size_t o_ipos = put(blob, B.interp_pos);
     const size_t o_nb = put(blob, B.nb_pos);
+    // locate's per-row input (RcpRowInfo)
+    std::vector<RcpRowInfo> row_info((size_t)std::max(R, 1));
+    {
+        const ReadLayout& RL0 = rows->ignore_strand ? rs->merged : rs->stranded;
+        for (int r = 0; r < R; ++r) {
+            RcpRowInfo& ri = row_info[r];
+            std::memset(&ri, 0, sizeof(ri));
+            ri.j0 = B.row_seg[r];
+            ri.j1 = B.row_seg[r + 1];
+            ri.chrom = B.row_chrom[r];
+            ri.row_len = B.row_len[r];
+            ri.stat = B.row_static[r];
+            const bool cok = ri.chrom >= 0 && ri.chrom < rs->n_chrom;
+            ri.seqlen = cok ? rs->seqlen[ri.chrom] : -1;
+            if (cok) {
+                ri.d0 = RL0.h_dir_off[(size_t)ri.chrom * 3];
+                ri.nb = (int32_t)(RL0.h_dir_off[(size_t)ri.chrom * 3 + 1] - ri.d0) - 1;
+            }
+            if (ri.j1 > ri.j0) ri.seg0 = B.segs[ri.j0];
+        }
+    }
+    const size_t o_rinfo = put(blob, row_info);
     // fmm pivots (see RcpPlanDev::spl_tb): the elimination of R's fmm_spline with d[i] = 1
     std::vector<double> spl_tb(2 * ((size_t)std::max(max_interp_len, 1) + 1), 0.0);
     {
@@ -814,6 +838,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.row_len = reinterpret_cast<const int32_t*>(base + o_row_len);
     P.row_static = reinterpret_cast<const uint8_t*>(base + o_row_static);
     P.segs = reinterpret_cast<const RcpSeg*>(base + o_segs);
+    P.row_info = reinterpret_cast<const RcpRowInfo*>(base + o_rinfo);
     P.seg_lo = reinterpret_cast<uint32_t*>(wb + w_lo);
     P.seg_hi = reinterpret_cast<uint32_t*>(wb + w_hi);
     P.valid = reinterpret_cast<uint8_t*>(wb + w_valid);

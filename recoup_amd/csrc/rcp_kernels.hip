@@ -524,9 +524,7 @@ __device__ __forceinline__ int qperm(int x) { return __builtin_amdgcn_update_dpp
 // that look for different bounds then search in lockstep, their loads in flight together
 // (two separate functions would run one after the other under the exec mask).  (An 8-ary
 // variant -- 7 probes in flight per step -- measured slower on C4: 0.099 vs 0.082 ms.)
-__device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32_t v, bool upper) {
-    const int64_t d0 = P.dir_off[st];
-    const int32_t nb = (int32_t)(P.dir_off[st + 1] - d0) - 1;
+__device__ __forceinline__ uint32_t dir_bound_at(const RcpPlanDev& P, int64_t d0, int32_t nb, int32_t v, bool upper) {
     const int32_t b = min(max(v, 0) >> P.dir_shift, nb - 1);
     const int32_t* dir = upper ? P.dir_u : P.dir_l;
     uint32_t lo = (uint32_t)dir[d0 + b], hi = (uint32_t)dir[d0 + b + 1];
@@ -541,6 +539,11 @@ __device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32
         if ((int64_t)key[(size_t)m << ksh] < thr) lo = m + 1; else hi = m;
     }
     return lo;
+}
+
+__device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32_t v, bool upper) {
+    const int64_t d0 = P.dir_off[st];
+    return dir_bound_at(P, d0, (int32_t)(P.dir_off[st + 1] - d0) - 1, v, upper);
 }
 
 // Four lanes per row.  The row's (segment, stream) searches are dealt round-robin to the
@@ -559,33 +562,40 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
     const int q = t & 3;
     uint32_t* xr = xres[threadIdx.x >> 2];
     const bool in_row = r < P.n_rows;
-    int j0 = 0, j1 = 0;
-    int32_t chrom = -1;
-    bool ok = false;
-    if (in_row) {
-        j0 = P.row_seg[r];
-        j1 = P.row_seg[r + 1];
-        chrom = P.row_chrom[r];
-        ok = !P.row_static[r] && chrom >= 0 && chrom < P.n_chrom && j1 > j0;
+    // the row's locate input: one 80-byte record (RcpRowInfo, built with the plan)
+    RcpRowInfo ri;
+    {
+        uint4* d = reinterpret_cast<uint4*>(&ri);
+        if (in_row) {
+            const uint4* src = reinterpret_cast<const uint4*>(P.row_info + r);
+#pragma unroll
+            for (int u = 0; u < (int)(sizeof(RcpRowInfo) / 16); ++u) d[u] = src[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < (int)(sizeof(RcpRowInfo) / 16); ++u) d[u] = make_uint4(0u, 0u, 0u, 0u);
+        }
     }
+    const int j0 = ri.j0, j1 = ri.j1;
+    const int32_t chrom = in_row ? ri.chrom : -1;
+    const bool ok = in_row && !ri.stat && chrom >= 0 && chrom < P.n_chrom && j1 > j0;
     const int ns = P.merged ? 1 : 3;  // streams searched per segment
     const int npairs = (j1 - j0) * ns;
     uint32_t hit = 0, present = 0;  // bit g: group g
     int32_t maxend[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
     int32_t maxpos[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
     uint32_t ncand = 0, lo = 0, hi = 0;
-    const int64_t sl = ok ? P.seqlen[chrom] : -1;
+    const int64_t sl = ok ? ri.seqlen : -1;
     // ---- single-range rows: the per-chunk candidate ranges (each column chunk streams only
     // the reads that reach its piece of the row) need bound searches at the interior chunk
     // edges; they do not depend on the row's own bounds, so they run in the same round
     RcpSeg sg0{};
     bool fast = false;
     if (in_row && j1 == j0 + 1) {
-        sg0 = P.segs[j0];
+        sg0 = ri.seg0;
         fast = !sg0.multi && sg0.query_ok;
     }
     const int nc = P.n_chunks_total;
-    const int32_t nr = in_row ? P.row_len[r] : 0;
+    const int32_t nr = in_row ? ri.row_len : 0;
     const int32_t len = sg0.hi - sg0.lo + 1;
     // genomic piece of chunk c (false: the chunk streams the whole range / nothing special)
     auto piece = [&](int c, int32_t* gps, int32_t* gpe, bool* empty) -> bool {
@@ -616,7 +626,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
     const bool split1 = ns == 1 && npairs == 1;
     const bool spec_cr = split1 && P.crange != nullptr && fast && ok;
     if (split1) {
-        const RcpSeg sg = P.segs[j0];
+        const RcpSeg sg = ri.seg0;
         const int g = sg.group & 3;
         present = 1u << g;
         maxpos[g] = sg.hi;
@@ -657,7 +667,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         for (int u = 0; u < 4; ++u) {
             if (u < cnt) {  // one dir_bound per round: the lanes' loads are in flight together
                 const bool up = sdst[u] == -1 || (sdst[u] >= 0 && (sdst[u] & 1));
-                const uint32_t w = dir_bound(P, chrom * 3, sx[u], up);
+                const uint32_t w = dir_bound_at(P, ri.d0, ri.nb, sx[u], up);
                 if (sdst[u] < 0) v = w; else xr[sdst[u]] = w;
             }
         }
@@ -735,7 +745,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         // skewed rows only: many candidates per column chunk (each chunk of a row is one
         // wave's work) AND a deep pileup (> 2 reads per position), so a long row with
         // proportionally many reads stays on the workgroup path
-        const int32_t rl = P.row_len[r];
+        const int32_t rl = nr;
         if (valid && P.heavy_threshold > 0 &&
             (uint64_t)ncand > (uint64_t)P.heavy_threshold * (uint64_t)max(P.n_chunks_total, 1) &&
             ncand > 2u * (uint32_t)max(rl, 0) && rl <= P.heavy_max_len) {

@@ -1246,7 +1246,9 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     int c = wg >> 3;
     const int cidx = c;  // column chunk over all parts
     const int blk = grp * 8 + (wg & 7);
-    if (blk * kRows >= P.n_rows) return;
+    const int rounds = P.rounds;        // rounds of T rows (<= kRounds)
+    const int rows_wg = T * rounds;     // rows of this workgroup
+    if (blk * rows_wg >= P.n_rows) return;
     int p = 0;
     while (p < P.n_parts - 1 && c >= P.part[p].n_chunks) {
         c -= P.part[p].n_chunks;
@@ -1254,7 +1256,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     }
     const RcpPart part = P.part[p];
     const int32_t k0 = c * part.chunk_bins;
-    const int row0 = blk * kRows;
+    const int row0 = blk * rows_wg;
 
     // per wave: 8 zero words (so cum[lp(-1)] == 0) then the padded difference / depth /
     // cumulative array; the stage is [row][RS] (stage_stride)
@@ -1264,7 +1266,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : kStageBufs * T * RS));
 
     // ---- per-row metadata, one thread per row, from the locate kernel's 64-byte records
-    if (tid < kRows) {
+    if (tid < rows_wg) {
         meta[tid] = decode_row<MEDIAN, CSR>(P, part, k0, cidx, row0 + tid);
     }
     lds_barrier();
@@ -1273,7 +1275,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
     // software pipeline: the first 256 candidate reads of the next kAhead rows are in flight
     // while a row is piled up (registers are free: LDS, not VGPRs, limits occupancy)
-    constexpr int kSteps = kRowsPerWave * kRounds;
+    const int n_steps = kRowsPerWave * rounds;
     auto prefetch = [&](int i, int2* dst) {
         const RowMeta m = uniform_meta(meta[i]);
 #ifdef RCP_ABL_LOADS
@@ -1384,7 +1386,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     // one row of this wave: `cur` holds its first reads; the next row's go to `nxt`
     auto pile_step = [&](int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
         const int i = row_of(step);
-        if (step + 1 < kSteps) prefetch(row_of(step + 1), nxt);
+        if (step + 1 < n_steps) prefetch(row_of(step + 1), nxt);
         const RowMeta m = uniform_meta(meta[i]);
         uint32_t* sbuf = stage + ((step / kRowsPerWave) % kStageBufs) * T * RS;  // this round's stage
         if (m.flag == 0) {  // wave-uniform: scalar branch
@@ -1533,7 +1535,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
             }
         }
     };
-    for (int rd = 0; rd < kRounds; ++rd) {
+    for (int rd = 0; rd < rounds; ++rd) {
         for (int s2 = 0; s2 < kRowsPerWave; s2 += 2) {
             pile_step(rd * kRowsPerWave + s2, bufA, bufB);
             pile_step(rd * kRowsPerWave + s2 + 1, bufB, bufA);
@@ -1553,7 +1555,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
             lds_barrier();
         }
     }
-    if (!CSR && kStageBufs == 2) flush(kRounds - 1);
+    if (!CSR && kStageBufs == 2) flush(rounds - 1);
 }
 
 
@@ -2336,6 +2338,12 @@ extern "C" size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr) {
 
 extern "C" int rcp_tile_rows(void) { return kRows; }
 
+// rows per round of the general pileup kernel and its maximum rounds per workgroup
+extern "C" void rcp_tile_geometry(int* tile, int* rounds_max) {
+    *tile = kTile;
+    *rounds_max = kRounds;
+}
+
 // bins per column chunk the lean kernel's store waves can hold
 extern "C" int rcp_lean_max_bins(void) { return 4 * kLQuads * kLMaxPass; }
 
@@ -2385,7 +2393,8 @@ static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* bin
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    const int tiles = (P->n_rows + kRows - 1) / kRows;
+    const int rows_wg = kTile * P->rounds;
+    const int tiles = (P->n_rows + rows_wg - 1) / rows_wg;
     const int64_t grid = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
     hipLaunchKernelGGL((rcp_pileup_kernel<MEDIAN, CSR>), dim3((unsigned)grid), dim3(kPBlock), lds, s, *P, out, binsum);
     return hipGetLastError();

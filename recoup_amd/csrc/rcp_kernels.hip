@@ -541,6 +541,54 @@ __device__ __forceinline__ uint32_t dir_bound_at(const RcpPlanDev& P, int64_t d0
     return lo;
 }
 
+#ifndef RCP_LOC_LOCKSTEP
+#define RCP_LOC_LOCKSTEP 1
+#endif
+// Up to 4 searches of one lane (search u: v[u], upper when dst[u] == -1 or dst[u] is odd, as
+// the locate task numbering has it) bisecting in lockstep: each step issues the probes of all
+// unfinished searches before using any, so they cost one chain of round trips together.
+__device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0, int32_t nb, const int32_t (&v)[4],
+                                                const int (&dst)[4], int cnt, uint32_t (&res)[4]) {
+    uint32_t lo[4], hi[4];
+    int64_t thr[4];
+    bool up[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        up[u] = dst[u] == -1 || (dst[u] >= 0 && (dst[u] & 1));
+        lo[u] = hi[u] = 0;
+        thr[u] = (int64_t)v[u] + (up[u] ? 1 : 0);
+        if (u < cnt) {
+            const int32_t b = min(max(v[u], 0) >> P.dir_shift, nb - 1);
+            const int32_t* dir = up[u] ? P.dir_u : P.dir_l;
+            lo[u] = (uint32_t)dir[d0 + b];
+            hi[u] = (uint32_t)dir[d0 + b + 1];
+        }
+    }
+    const int32_t* se = reinterpret_cast<const int32_t*>(P.se);
+    while (true) {
+        uint32_t m[4];
+        int32_t kv[4];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (lo[u] < hi[u]) {
+                m[u] = lo[u] + ((hi[u] - lo[u]) >> 1);
+                kv[u] = up[u] ? se[(size_t)m[u] << 1] : P.pmax[m[u]];
+                any = true;
+            }
+        }
+        if (!any) break;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (lo[u] < hi[u]) {
+                if ((int64_t)kv[u] < thr[u]) lo[u] = m[u] + 1; else hi[u] = m[u];
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) res[u] = lo[u];
+}
+
 __device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32_t v, bool upper) {
     const int64_t d0 = P.dir_off[st];
     return dir_bound_at(P, d0, (int32_t)(P.dir_off[st + 1] - d0) - 1, v, upper);
@@ -663,6 +711,19 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
             ++k;
         }
         uint32_t v = 0;
+#if RCP_LOC_LOCKSTEP
+        {
+            // the lane's (up to 4) searches bisect in lockstep: one round of dependent loads
+            // serves all of them (C2: 8 searches per row -> 2 per lane, C5: 16 -> 4)
+            uint32_t w[4];
+            dir_bound_multi(P, ri.d0, ri.nb, sx, sdst, cnt, w);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (u < cnt) {
+                    if (sdst[u] < 0) v = w[u]; else xr[sdst[u]] = w[u];
+                }
+        }
+#else
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (u < cnt) {  // one dir_bound per round: the lanes' loads are in flight together
@@ -671,6 +732,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
                 if (sdst[u] < 0) v = w; else xr[sdst[u]] = w;
             }
         }
+#endif
         lo = (uint32_t)qperm<0x00>((int)v);
         hi = max(lo, (uint32_t)qperm<0x55>((int)v));
         if (lo < hi) {

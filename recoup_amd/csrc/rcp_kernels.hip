@@ -557,7 +557,11 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0,
         up[u] = dst[u] == -1 || (dst[u] >= 0 && (dst[u] & 1));
         lo[u] = hi[u] = 0;
         thr[u] = (int64_t)v[u] + (up[u] ? 1 : 0);
+#ifdef RCP_ABL_NODIR  // ablation (locate timing): no directory / search loads
+        if (false) {
+#else
         if (u < cnt) {
+#endif
             const int32_t b = min(max(v[u], 0) >> P.dir_shift, nb - 1);
             const int32_t* dir = up[u] ? P.dir_u : P.dir_l;
             lo[u] = (uint32_t)dir[d0 + b];
@@ -743,8 +747,6 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         if (q == 0) {
             P.seg_lo[j0 * 3] = lo;
             P.seg_hi[j0 * 3] = hi;
-            P.seg_lo[j0 * 3 + 1] = P.seg_hi[j0 * 3 + 1] = 0;
-            P.seg_lo[j0 * 3 + 2] = P.seg_hi[j0 * 3 + 2] = 0;
         }
         if (q != 0) lo = hi = 0;  // the quad combine below reads (lo, hi) from lane 0
     }
@@ -768,10 +770,8 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         }
         P.seg_lo[j * 3 + s] = lo;
         P.seg_hi[j * 3 + s] = hi;
-        if (ns == 1) {  // merged layout: streams 1, 2 hold no reads
-            P.seg_lo[j * 3 + 1] = P.seg_hi[j * 3 + 1] = 0;
-            P.seg_lo[j * 3 + 2] = P.seg_hi[j * 3 + 2] = 0;
-        }
+        // (merged layout: the entries of streams 1, 2 -- and their crange words -- stay as the
+        // plan zeroed them; no read lives there)
     }
     // ---- combine the quad (all lanes active: DPP reads neighbours)
     hit |= (uint32_t)qperm<0xB1>((int)hit);
@@ -837,8 +837,6 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
                     chi = clo;
                 }
                 P.crange[((size_t)r * nc + c) * 3] = make_uint2(clo, chi);
-                P.crange[((size_t)r * nc + c) * 3 + 1] = make_uint2(0u, 0u);
-                P.crange[((size_t)r * nc + c) * 3 + 2] = make_uint2(0u, 0u);
             }
         }
     } else if (cr && q < 3) {
@@ -877,6 +875,9 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
     }
     const uint4* src = reinterpret_cast<const uint4*>(&rec);
     uint4* dst = reinterpret_cast<uint4*>(P.rec + r);
+#ifdef RCP_ABL_NOREC  // ablation (locate timing): no record writes (rows read as NULL)
+    if (r >= 0) return;
+#endif
 #pragma unroll
     for (int u = 0; u < 4; ++u) dst[u] = src[u];
 }

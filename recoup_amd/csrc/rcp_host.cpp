@@ -36,6 +36,7 @@ size_t rcp_interp_lds_bytes(const RcpPlanDev* P);
 int rcp_tile_rows(void);
 void rcp_tile_geometry(int* tile, int* rounds_max);
 int rcp_lean_max_bins(void);
+int rcp_lean_gen_max_bins(void);
 size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
 hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
                               const int8_t* strand, int32_t n_chrom, int32_t strand_filter, int merge, uint64_t* keys,
@@ -712,20 +713,27 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     // ---- lean pileup kernel: every row one plain range (no exon list, no zero-width query),
     // mean of uniform power-of-two bins, each chunk inside one wave's fused pass (<= 1023
     // positions) and the stage inside the store waves' registers
+    // With RCP_LEAN=2 (opt-in), other plans take its general-bins mode (lean == 2): any uniform
+    // width, R-RNG layouts and multi-range rows, as long as every chunk is one wave's pass (no
+    // sub-chunks) and holds <= rcp_lean_gen_max_bins() bins.  Measured slower than the general
+    // kernel on C2 (0.082 vs 0.063 ms) and C3 (0.96 vs 0.88 ms), so off by default.  RCP_LEAN=0
+    // keeps every plan on the general kernel.
     {
-        bool lean = lean_ok && !cov_only && bins->stat == RCP_STAT_MEAN && P.chunk_cap <= 1023 &&
-                    stage_cap <= rcp_lean_max_bins() && env_int("RCP_LEAN", 1) != 0;
-        for (int p = 0; lean && p < P.n_parts; ++p) {
+        const int lean_env = env_int("RCP_LEAN", 1);
+        bool base = !cov_only && bins->stat == RCP_STAT_MEAN && P.chunk_cap <= 1023 && lean_env != 0;
+        for (int p = 0; base && p < P.n_parts; ++p) {
             const RcpPart& pt = P.part[p];
             const int64_t w = pt.per_base ? 1 : part_max_bin[p];
-            if ((int64_t)pt.chunk_bins * w > P.chunk_cap) lean = false;
+            if ((int64_t)pt.chunk_bins * w > P.chunk_cap) base = false;
         }
+        bool lean = base && lean_ok && stage_cap <= rcp_lean_max_bins();
         for (int r = 0; lean && r < R; ++r) {
             const int32_t j0 = B.row_seg[r], j1 = B.row_seg[r + 1];
             if (j1 - j0 > 1) lean = false;
             else if (j1 == j0 + 1 && (B.segs[j0].multi || !B.segs[j0].query_ok)) lean = false;
         }
-        P.lean = lean ? 1 : 0;
+        const bool gen = !lean && base && lean_env >= 2 && stage_cap <= rcp_lean_gen_max_bins();
+        P.lean = lean ? 1 : (gen ? 2 : 0);
     }
 
     // ---- skewed rows: heavy slots sized for the eligible (short enough) rows

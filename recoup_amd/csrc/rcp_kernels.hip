@@ -1668,9 +1668,9 @@ static_assert(kRows == 64 && kRounds >= 2, "store wave 0 decodes one row per lan
 // | (heavy slot + 1) << 9; the read -> chunk position offset `k` folds orientation and origin.
 struct LeanMeta {
     int32_t w0, P0, npos, kend;
-    int32_t k, gps, gpe, pad;
+    int32_t k, gps, gpe, bs;   // bs: bin width (general-bins mode)
     uint32_t lo[3], hi[3];
-    uint32_t pad2[2];
+    int32_t lay, pad2;         // lay: R-RNG layout (-1: none)
 };
 static_assert(sizeof(LeanMeta) == 64, "LeanMeta is four b128 words");
 
@@ -1684,17 +1684,18 @@ __device__ __forceinline__ LeanMeta lean_pack(const RowMeta& m) {
     q.k = m.rev ? m.off + m.shi - m.P0 : m.off - m.slo - m.P0;
     q.gps = m.gps;
     q.gpe = m.gpe;
-    q.pad = 0;
+    q.bs = m.bs;
     for (int s = 0; s < 3; ++s) {
         q.lo[s] = m.lo[s];
         q.hi[s] = m.hi[s];
     }
-    q.pad2[0] = q.pad2[1] = 0;
+    q.lay = m.lay;
+    q.pad2 = 0;
     return q;
 }
 
 struct LeanRow {  // wave-uniform view (SGPRs)
-    int32_t flag, fast, rev, lbs, heavy, P0, npos, kend, k, gps, gpe;
+    int32_t flag, fast, rev, lbs, heavy, P0, npos, kend, k, gps, gpe, bs, lay;
     uint32_t lo[3], hi[3];
 };
 
@@ -1702,7 +1703,7 @@ __device__ __forceinline__ LeanRow lean_row(const LeanMeta& src) {
     const int32_t* s = reinterpret_cast<const int32_t*>(&src);
     int32_t v[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = q == 7 || q >= 14 ? 0 : __builtin_amdgcn_readfirstlane(s[q]);
+    for (int q = 0; q < 16; ++q) v[q] = q == 15 ? 0 : __builtin_amdgcn_readfirstlane(s[q]);
     LeanRow m;
     m.flag = v[0] & 3;
     m.fast = (v[0] >> 2) & 1;
@@ -1710,6 +1711,7 @@ __device__ __forceinline__ LeanRow lean_row(const LeanMeta& src) {
     m.lbs = (v[0] >> 4) & 31;
     m.heavy = (v[0] >> 9) - 1;
     m.P0 = v[1]; m.npos = v[2]; m.kend = v[3]; m.k = v[4]; m.gps = v[5]; m.gpe = v[6];
+    m.bs = v[7]; m.lay = v[14];
     for (int q = 0; q < 3; ++q) {
         m.lo[q] = (uint32_t)v[8 + q];
         m.hi[q] = (uint32_t)v[11 + q];
@@ -1775,9 +1777,17 @@ __device__ __forceinline__ LeanItem lean_item(const RcpPlanDev& P, int code) {
     return it;
 }
 
-// MAXPER: positions per lane of the widest chunk (16: <= 1023 positions, 8: <= 511)
-template <int MAXPER>
-__global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(RCP_LWPE)))
+// MAXPER: positions per lane of the widest chunk (16: <= 1023 positions, 8: <= 511).
+// GEN (plan lean == 2): general bins -- any uniform width or R-RNG layouts (splitVector's
+// enlarged bins), multi-range rows (exon lists).  Pile waves then stage bin numerators from a
+// cumulative scan (bin-edge differences, as the general kernel) plus a per-row bitmask of the
+// enlarged bins, and store waves divide by the bin width.
+constexpr int kLMaxPassGen = 4;  // general-bins mode: <= 4 * kLQuads * 4 = 256 bins per chunk
+#ifndef RCP_LWPE_GEN
+#define RCP_LWPE_GEN RCP_LWPE
+#endif
+template <int MAXPER, bool GEN>
+__global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(GEN ? RCP_LWPE_GEN : RCP_LWPE)))
 rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int T = kTile;
@@ -1787,7 +1797,8 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     const int lane = tid & 63;
     const int RS = stage_stride(P.stage_cap);
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * P.wave_words;
-    LeanMeta* lmeta = reinterpret_cast<LeanMeta*>(stage + T * RS);  // [2][kRows]
+    uint32_t* emask = stage + T * RS;  // GEN: [row][16] enlarged-bin bits of the round
+    LeanMeta* lmeta = reinterpret_cast<LeanMeta*>(emask + (GEN ? T * 16 : 0));  // [2][kRows]
     int32_t* item = reinterpret_cast<int32_t*>(lmeta + 2 * kRows);  // [2]: item code or -1
     const int xcd = blockIdx.x & 7;
     const int n_tiles = (P.n_rows + kRows - 1) / kRows;
@@ -1848,7 +1859,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             }
             const LeanRow m = lean_row(lmeta[buf * kRows + i]);
             if (m.flag != 0) return;
-            if (!m.fast && m.heavy < 0) {  // the plan promised single-range rows
+            if (!GEN && !m.fast && m.heavy < 0) {  // the plan promised single-range rows
                 if (lane == 0) atomicOr(P.status, RCP_STATUS_INTERP);
                 return;
             }
@@ -1867,6 +1878,9 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 for (int q = lane; q < m.P0; q += 64) carry += g[q];
                 carry = wave_sum(carry);
                 for (int q = lane; q <= npos; q += 64) diff[lp(q, sh)] = g[m.P0 + q] + (q == 0 ? carry : 0);
+            } else if (GEN && !m.fast) {
+                // several ranges (exon list): the wave streams the row's (segment, stream) pairs
+                pileup_row_wave(P, it.tile * kRows + i, m.P0, npos, diff, sh);
             } else {
 #ifdef RCP_LABL_NOREAD  // ablation: no read loads / LDS adds
                 const uint32_t n = 0;
@@ -1937,10 +1951,34 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             }
             lds_order();
             uint32_t* srow = stage + (i & (T - 1)) * RS;
-            if (sh == 2) scan_bins_fast<4>(diff, m.lbs, srow, m.kend - it.k0);
-            else if (MAXPER == 8 || sh == 3) scan_bins_fast<8>(diff, m.lbs, srow, m.kend - it.k0);
-            else scan_bins_fast<MAXPER>(diff, m.lbs, srow, m.kend - it.k0);
-            clean_sh = sh;
+            const int per = 1 << sh;
+            if (!GEN || (m.lay < 0 && m.bs > 0 && (m.bs & (m.bs - 1)) == 0 && m.bs <= per)) {
+                if (sh == 2) scan_bins_fast<4>(diff, m.lbs, srow, m.kend - it.k0);
+                else if (MAXPER == 8 || sh == 3) scan_bins_fast<8>(diff, m.lbs, srow, m.kend - it.k0);
+                else scan_bins_fast<MAXPER>(diff, m.lbs, srow, m.kend - it.k0);
+                clean_sh = sh;
+                if (GEN && lane < 16) emask[(i & (T - 1)) * 16 + lane] = 0u;
+            } else {
+                // cumulative depth, then bin k = cum[end - 1] - cum[start - 1] (uint32: a bin sum
+                // that fits 32 bits comes out exact); enlarged bins (width bs + 1) flagged in emask
+                scan_wave<true>(diff, per);
+                lds_order();
+                const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
+                const int32_t e0 = bin_edge(m.bs, m.lay, P.lay_cnt, it.k0);
+                for (int32_t k0l = 0; k0l < 4 * kLQuads * kLMaxPassGen; k0l += 64) {
+                    const int32_t k = it.k0 + k0l + lane;
+                    bool enl = false;
+                    if (k < m.kend) {
+                        const int32_t a = bin_edge(m.bs, m.lay, P.lay_cnt, k) - e0;
+                        const int32_t b = bin_edge(m.bs, m.lay, P.lay_cnt, k + 1) - e0;
+                        srow[k - it.k0] = cum[lp(b - 1, sh)] - (a > 0 ? cum[lp(a - 1, sh)] : 0u);
+                        enl = b - a > m.bs;
+                    }
+                    const uint64_t bits = __ballot(enl);
+                    if (lane < 2) emask[(i & (T - 1)) * 16 + (k0l >> 5) + lane] = (uint32_t)(bits >> (32 * lane));
+                }
+                clean_sh = -1;  // the array now holds cumulative depth
+            }
             lds_order();
         };
         int2 bufA[4], bufB[4];
@@ -1966,6 +2004,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         const size_t R = (size_t)P.n_rows;
         const double sc = P.scale;
         const int npass = (P.stage_cap + 4 * kLQuads - 1) / (4 * kLQuads);
+        constexpr int kPass = GEN ? kLMaxPassGen : kLMaxPass;
         int buf = 0;
         int code = item[0];
         while (code >= 0) {
@@ -1981,15 +2020,22 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 const bool live = r < P.n_rows && flag != 2;
                 // the round's stage -> registers (uniform pass count; the reads past a row's
                 // kend stay inside LDS and are never stored)
-                uint4 v[kLMaxPass];
+                uint4 v[kPass];
                 const uint32_t* st0 = stage + ii * RS + 4 * qd;
 #pragma unroll
-                for (int j = 0; j < kLMaxPass; ++j)
+                for (int j = 0; j < kPass; ++j)
                     v[j] = j < npass ? *reinterpret_cast<const uint4*>(st0 + 4 * kLQuads * j) : make_uint4(0u, 0u, 0u, 0u);
+                // GEN: 4 enlarged-bin bits per pass (bins 4 qd + 64 j .. + 3), packed
+                uint32_t enl = 0;
+                if (GEN) {
+#pragma unroll
+                    for (int j = 0; j < kPass; ++j)
+                        if (j < npass) enl |= ((emask[ii * 16 + 2 * j + (qd >> 3)] >> ((4 * qd) & 31)) & 15u) << (4 * j);
+                }
                 lds_barrier();  // B: the stage is free for the next round
                 // opaque after the barrier: keeps the conversions (2 VGPRs per value) below it
 #pragma unroll
-                for (int j = 0; j < kLMaxPass; ++j)
+                for (int j = 0; j < kPass; ++j)
                     if (j < npass) asm volatile("" : "+v"(v[j].x), "+v"(v[j].y), "+v"(v[j].z), "+v"(v[j].w));
                 if (live) {
                     // power-of-two bin width: multiplying by its reciprocal is exact; a NULL row
@@ -1998,13 +2044,26 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                     const double scf = flag == 0 ? sc : 0.0;
                     const int32_t nk = kend - (it.k0 + 4 * qd);  // columns left from this thread's first quad
                     double* o = out + (size_t)col0 * R + (size_t)r;
+                    const int32_t bsr = GEN ? mr.bs : 1;
 #pragma unroll
-                    for (int j = 0; j < kLMaxPass; ++j) {
+                    for (int j = 0; j < kPass; ++j) {
                         constexpr int kStep = 4 * kLQuads;
                         if (j >= npass || kStep * j >= nk) break;
                         double* oj = o + (size_t)(kStep * j) * R;
-                        const double x[4] = {((double)v[j].x * scf) * rdd, ((double)v[j].y * scf) * rdd,
-                                             ((double)v[j].z * scf) * rdd, ((double)v[j].w * scf) * rdd};
+                        double x[4];
+                        if (GEN) {
+                            // mean of a bin = numerator * scale / width (profile.R via splitVector;
+                            // the general kernel's flush); a NULL row writes zeros
+                            const uint32_t q4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                x[u] = flag == 0 ? ((double)q4[u] * sc) / (double)(bsr + ((enl >> (4 * j + u)) & 1)) : 0.0;
+                        } else {
+                            x[0] = ((double)v[j].x * scf) * rdd;
+                            x[1] = ((double)v[j].y * scf) * rdd;
+                            x[2] = ((double)v[j].z * scf) * rdd;
+                            x[3] = ((double)v[j].w * scf) * rdd;
+                        }
 #ifdef RCP_LABL_NOSTORE  // ablation: stage copied and converted, no global stores
                         asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(oj));
                         continue;
@@ -2409,14 +2468,15 @@ extern "C" void rcp_tile_geometry(int* tile, int* rounds_max) {
 
 // bins per column chunk the lean kernel's store waves can hold
 extern "C" int rcp_lean_max_bins(void) { return 4 * kLQuads * kLMaxPass; }
+extern "C" int rcp_lean_gen_max_bins(void) { return 4 * kLQuads * kLMaxPassGen; }
 
 extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
 
-template <int MAXPER>
+template <int MAXPER, bool GEN>
 static hipError_t launch_pileup_lean_t(const RcpPlanDev* P, double* out, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = allow_big_lds(rcp_pileup_lean_kernel<MAXPER>);
+        hipError_t e = allow_big_lds(rcp_pileup_lean_kernel<MAXPER, GEN>);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
@@ -2435,17 +2495,22 @@ static hipError_t launch_pileup_lean_t(const RcpPlanDev* P, double* out, hipStre
     const int tiles = (P->n_rows + kRows - 1) / kRows;
     const int64_t items = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
     const int64_t grid = std::min<int64_t>(((int64_t)per_cu * cus + 7) / 8 * 8, items);
-    hipLaunchKernelGGL(rcp_pileup_lean_kernel<MAXPER>, dim3((unsigned)grid), dim3(kLBlock), lds, s, *P, out);
+    hipLaunchKernelGGL((rcp_pileup_lean_kernel<MAXPER, GEN>), dim3((unsigned)grid), dim3(kLBlock), lds, s, *P, out);
     return hipGetLastError();
 }
 
 extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P) {
-    return 4 * ((size_t)kPWaves * P->wave_words + (size_t)kTile * stage_stride(P->stage_cap)) +
+    // [pile waves' difference arrays | stage | (general bins) enlarged-bin bits | row metadata
+    //  x 2 | item codes x 2]
+    return 4 * ((size_t)kPWaves * P->wave_words + (size_t)kTile * stage_stride(P->stage_cap) +
+                (P->lean == 2 ? (size_t)kTile * 16 : 0)) +
            2 * (size_t)kRows * sizeof(LeanMeta) + 16;
 }
 
 static hipError_t launch_pileup_lean(const RcpPlanDev* P, double* out, hipStream_t s) {
-    return P->chunk_cap <= 511 ? launch_pileup_lean_t<8>(P, out, s) : launch_pileup_lean_t<16>(P, out, s);
+    if (P->lean == 2)
+        return P->chunk_cap <= 511 ? launch_pileup_lean_t<8, true>(P, out, s) : launch_pileup_lean_t<16, true>(P, out, s);
+    return P->chunk_cap <= 511 ? launch_pileup_lean_t<8, false>(P, out, s) : launch_pileup_lean_t<16, false>(P, out, s);
 }
 
 template <bool MEDIAN, bool CSR>

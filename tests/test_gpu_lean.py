@@ -1,7 +1,8 @@
 """The lean pileup kernel (pile waves + store waves, rcp_kernels.hip rcp_pileup_lean_kernel).
 
 Plans whose rows are all one plain range with uniform power-of-two bins take the lean kernel
-(plan info "pileup_kernel" == 1).  Each case checks it against the CPU oracle (validity and
+(plan info "pileup_kernel" == 1); other mean plans whose chunks fit one wave pass take its
+general-bins mode (2: any bin width, R-RNG layouts, exon lists) when opted in (RCP_LEAN=2).  Each case checks it against the CPU oracle (validity and
 means as in test_gpu_random: integer numerators exact, means within 1e-12 relative) and
 bit-for-bit against the general kernel on the same plan (RCP_LEAN=0)."""
 import os
@@ -14,12 +15,18 @@ from tests.test_gpu_random import CHROM_LEN, check, make_reads, single_rows
 pytestmark = pytest.mark.gpu
 
 
-def plans(reads, seqlen, rows, bins, strand_filter=None):
-    """(lean result, general result, lean kernel id, expected) for one configuration."""
+def plans(reads, seqlen, rows, bins, strand_filter=None, lean_mode=None):
+    """(lean result, general result, lean kernel id, expected) for one configuration;
+    lean_mode "2" opts in to the general-bins mode."""
     from recoup_amd.engine import Plan, ReadSet
     from tests import oracle_rows
     rs = ReadSet(*reads, seqlen, device=0, strand_filter=strand_filter)
-    lean = Plan(rs, rows, bins)
+    if lean_mode:
+        os.environ["RCP_LEAN"] = lean_mode
+    try:
+        lean = Plan(rs, rows, bins)
+    finally:
+        os.environ.pop("RCP_LEAN", None)
     os.environ["RCP_LEAN"] = "0"
     try:
         general = Plan(rs, rows, bins)
@@ -121,18 +128,74 @@ def test_lean_heavy_rows(gpu):
     same(lean, gen)
 
 
-def test_lean_not_taken(gpu):
-    """R-RNG bin layouts, non-power-of-two bins, medians and exon lists stay on the general kernel."""
+def test_lean_kernel_choice(gpu):
+    """Power-of-two uniform bins of single-range rows take the lean kernel (1); R-RNG layouts,
+    other widths and exon lists stay on the general kernel (0) unless the general-bins mode is
+    opted in (RCP_LEAN=2); medians always stay on the general kernel."""
     from recoup_amd.engine import Bins, Plan, ReadSet, RowTable
     rng = np.random.default_rng(71)
     reads = make_reads(rng, 20_000)
     rs = ReadSet(*reads, CHROM_LEN, device=0)
     rows = single_rows(rng, 50, 2000)
-    assert Plan(rs, rows, Bins([("whole", 150)])).info["pileup_kernel"] == 0       # dif != 0
-    assert Plan(rs, rows, Bins([("whole", 200)])).info["pileup_kernel"] == 0       # bs = 10
-    assert Plan(rs, rows, Bins([("whole", 1000)], stat="median")).info["pileup_kernel"] == 0
-    assert Plan(rs, rows, Bins([("whole", 1000)])).info["pileup_kernel"] == 1
     seg_off = np.array([0, 2, 3], np.int64)
     exons = RowTable(seg_off, np.zeros(3, np.int32), np.array([1000, 3000, 9000]), np.array([1999, 3999, 10999]),
                      np.zeros(3, np.int8), seg_group=np.zeros(3, np.int8), group_is_list=np.array([1, 0, 0, 0], np.uint8))
-    assert Plan(rs, exons, Bins([("whole", 100)])).info["pileup_kernel"] == 0
+    for mode, other in ((None, 0), ("2", 2)):
+        if mode:
+            os.environ["RCP_LEAN"] = mode
+        try:
+            assert Plan(rs, rows, Bins([("whole", 150)])).info["pileup_kernel"] == other   # dif != 0
+            assert Plan(rs, rows, Bins([("whole", 200)])).info["pileup_kernel"] == other   # bs = 10
+            assert Plan(rs, exons, Bins([("whole", 100)])).info["pileup_kernel"] == other
+            assert Plan(rs, rows, Bins([("whole", 1000)], stat="median")).info["pileup_kernel"] == 0
+            assert Plan(rs, rows, Bins([("whole", 1000)])).info["pileup_kernel"] == 1
+        finally:
+            os.environ.pop("RCP_LEAN", None)
+
+
+@pytest.mark.parametrize("width,n_bins", [(2000, 150), (4000, 200), (1500, 256), (3000, 64), (2000, 1000)])
+def test_lean_general_bins(gpu, width, n_bins):
+    """General-bins mode on single-range rows: R-RNG layouts (2000/150), 20-bp bins (C2),
+    24-bp-ish layouts, 47-bp bins with layouts; bit-equal to the general kernel."""
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(500 + n_bins)
+    reads = make_reads(rng, 80_000, star_frac=0.1)
+    rows = single_rows(rng, 400, width, edge=True)
+    rows.start[1], rows.end[1] = 1, width  # (a start at 0 would shorten the row)
+    lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, Bins([("whole", n_bins)]), lean_mode="2")
+    assert kind == (1 if (n_bins, width) == (1000, 2000) else 2)
+    check(lean, exp)
+    same(lean, gen)
+
+
+@pytest.mark.parametrize("stranded", [False, True])
+def test_lean_general_exon_lists(gpu, stranded):
+    """coverageRnaRef rows (flank | exon list | flank) in the general-bins mode: flank bins,
+    R-RNG centre layouts, exon-list weights; interpolated short genes stay on the interp kernel."""
+    from recoup_amd.engine import Bins, RowTable
+    rng = np.random.default_rng(77)
+    reads = make_reads(rng, 120_000, widths=(50, 400))
+    seg_off, ch, st, en, sd, gr = [0], [], [], [], [], []
+    for g in range(150):
+        c = int(rng.integers(0, 3))
+        pos = int(rng.integers(5000, CHROM_LEN[c] - 60000))
+        strand = int(rng.integers(0, 2))
+        ex_s, ex_e, p = [], [], pos
+        for _ in range(int(rng.integers(1, 9))):
+            w = int(rng.integers(30, 500))
+            ex_s.append(p)
+            ex_e.append(p + w - 1)
+            p += w + int(rng.integers(-100, 2000))  # some overlapping exons
+        gs, ge = min(ex_s), max(ex_e)
+        ls, le = (gs - 1000, gs - 1) if strand == 0 else (ge + 1, ge + 1000)
+        rs_, re_ = (ge + 1, ge + 1000) if strand == 0 else (gs - 1000, gs - 1)
+        for s_, e_, grp in [(ls, le, 0)] + [(a, b, 1) for a, b in zip(ex_s, ex_e)] + [(rs_, re_, 2)]:
+            ch.append(c); st.append(s_); en.append(e_); sd.append(strand); gr.append(grp)
+        seg_off.append(len(st))
+    rows = RowTable(np.array(seg_off), np.array(ch), np.array(st), np.array(en), np.array(sd),
+                    seg_group=np.array(gr), group_is_list=np.array([0, 1, 0, 0]), ignore_strand=not stranded)
+    bins = Bins([("upstream", 40), ("center", 100), ("downstream", 40)], flank=(1000, 1000))
+    lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, bins, lean_mode="2")
+    assert kind == 2
+    check(lean, exp, rtol=1e-9, atol=1e-12)
+    same(lean, gen)

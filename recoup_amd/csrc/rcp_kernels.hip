@@ -541,9 +541,6 @@ __device__ __forceinline__ uint32_t dir_bound_at(const RcpPlanDev& P, int64_t d0
     return lo;
 }
 
-#ifndef RCP_LOC_LOCKSTEP
-#define RCP_LOC_LOCKSTEP 1
-#endif
 // Up to 4 searches of one lane (search u: v[u], upper when dst[u] == -1 or dst[u] is odd, as
 // the locate task numbering has it) bisecting in lockstep: each step issues the probes of all
 // unfinished searches before using any, so they cost one chain of round trips together.
@@ -609,6 +606,9 @@ __device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32
 #endif
 __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlanDev P) {
     __shared__ uint32_t xres[kBlock / 4][2 * RCP_MAX_CRANGE_CHUNKS];  // per quad: chunk bounds
+#ifdef RCP_ABL_LOC_EMPTY  // ablation (locate timing): launch and dispatch only
+    if (P.n_rows >= 0) return;
+#endif
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = t >> 2;
     const int q = t & 3;
@@ -627,6 +627,10 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
             for (int u = 0; u < (int)(sizeof(RcpRowInfo) / 16); ++u) d[u] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
+#ifdef RCP_ABL_LOC_RIONLY  // ablation (locate timing): the record load and one store only
+    if (in_row && (t & 3) == 0) P.ncand[r] = (uint32_t)(ri.j0 + ri.j1 + ri.chrom + ri.row_len + ri.nb + ri.seg0.lo);
+    return;
+#endif
     const int j0 = ri.j0, j1 = ri.j1;
     const int32_t chrom = in_row ? ri.chrom : -1;
     const bool ok = in_row && !ri.stat && chrom >= 0 && chrom < P.n_chrom && j1 > j0;
@@ -683,12 +687,26 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         present = 1u << g;
         maxpos[g] = sg.hi;
         const bool qok = ok && sg.query_ok && (sg.streams & 1);
-        // the searches, numbered k = 0 (lower), 1 (upper), 2.. (interior chunk edges): lane q
-        // takes k = q, q + 4, ... (at most 4 each: <= 2 + 2 * (RCP_MAX_CRANGE_CHUNKS - 1))
+        // the searches, tasks -2 (lower), -1 (upper), 0 .. 2 nc - 1 (chunk edges): lane q takes
+        // tasks -2 + q, -2 + q + 4, ... (up to 5 of 2 + 2 * RCP_MAX_CRANGE_CHUNKS = 18; edges at
+        // the row's ends are skipped) and evaluates only its own chunk windows
         int32_t sx[4] = {0, 0, 0, 0};
         int sdst[4] = {0, 0, 0, 0};  // -2 lower, -1 upper, >= 0 xr index (its parity = upper)
-        int cnt = 0, k = 0;
-        for (int task = -2; task < (spec_cr ? 2 * nc : 0); ++task) {
+        int cnt = 0;
+        uint32_t v = 0;
+        // up to 4 searches bisect in lockstep (one chain of dependent loads for all of them:
+        // C2 has 8 searches per row -> 2 per lane, C5 16 -> 4); a 5th starts a second round
+        auto run = [&]() {
+            uint32_t w[4];
+            dir_bound_multi(P, ri.d0, ri.nb, sx, sdst, cnt, w);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (u < cnt) {
+                    if (sdst[u] < 0) v = w[u]; else xr[sdst[u]] = w[u];
+                }
+            cnt = 0;
+        };
+        for (int task = -2 + q; task < (spec_cr ? 2 * nc : 0); task += 4) {
             int32_t x = 0;
             bool need = false;
             if (task < 0) {
@@ -697,46 +715,25 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
             } else {
                 int32_t gps = 0, gpe = 0;
                 bool empty;
+#ifdef RCP_ABL_NOPIECE  // ablation (locate timing): no chunk-window arithmetic
+                if (task < -100 && piece(task >> 1, &gps, &gpe, &empty)) {
+#else
                 if (piece(task >> 1, &gps, &gpe, &empty)) {
+#endif
                     need = (task & 1) ? gpe < sg0.hi : gps > sg0.lo;  // a row end: the row's own bound
                     x = (task & 1) ? gpe : gps;
                 }
             }
             if (!need) continue;
-            if ((k & 3) == q) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (cnt == u) {
-                        sx[u] = x;
-                        sdst[u] = task;
-                    }
-                ++cnt;
-            }
-            ++k;
-        }
-        uint32_t v = 0;
-#if RCP_LOC_LOCKSTEP
-        {
-            // the lane's (up to 4) searches bisect in lockstep: one round of dependent loads
-            // serves all of them (C2: 8 searches per row -> 2 per lane, C5: 16 -> 4)
-            uint32_t w[4];
-            dir_bound_multi(P, ri.d0, ri.nb, sx, sdst, cnt, w);
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (u < cnt) {
-                    if (sdst[u] < 0) v = w[u]; else xr[sdst[u]] = w[u];
+                if (cnt == u) {
+                    sx[u] = x;
+                    sdst[u] = task;
                 }
+            if (++cnt == 4) run();
         }
-#else
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (u < cnt) {  // one dir_bound per round: the lanes' loads are in flight together
-                const bool up = sdst[u] == -1 || (sdst[u] >= 0 && (sdst[u] & 1));
-                const uint32_t w = dir_bound_at(P, ri.d0, ri.nb, sx[u], up);
-                if (sdst[u] < 0) v = w; else xr[sdst[u]] = w;
-            }
-        }
-#endif
+        if (cnt) run();
         lo = (uint32_t)qperm<0x00>((int)v);
         hi = max(lo, (uint32_t)qperm<0x55>((int)v));
         if (lo < hi) {

@@ -213,6 +213,18 @@ def test_spline_rows_bit_exact(gpu, n_bins):
     np.testing.assert_array_equal(res[0], exp[0])
 
 
+def test_chunk_edges_all_inside(gpu):
+    """A centre part of 8 column chunks whose every edge lies inside the row (flanks on both
+    sides): 2 + 16 locate searches per row, more than one lockstep round per lane."""
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(17)
+    reads = make_reads(rng, 120_000, widths=(50, 300))
+    rows = single_rows(rng, 120, 9000)
+    for n_bins in (4000, 2900):  # 2 bp bins (lean kernel), R-RNG layout (general kernel)
+        res, exp = run_case(reads, CHROM_LEN, rows, Bins([("center", n_bins)], flank=(500, 500)))
+        check(res, exp)
+
+
 def test_long_rows_chunked(gpu):
     """Rows longer than one chunk: per-base (chunked columns) and coarse bins."""
     from recoup_amd.engine import Bins

@@ -128,6 +128,8 @@ struct RcpPlanDev {
     int32_t wave_words;         // LDS words per wave difference array (multiple of 256)
     int32_t stage_cap;          // max bins per chunk
     int32_t interp_cap;         // max positions of an interpolated slice
+    int32_t loc_lpr;            // locate lanes per row: 4, or 1 for single-range rows in the merged
+                                //    layout with <= 8 searches per row
     int32_t rounds;             // general pileup kernel: rounds of kTile rows per workgroup (1..4;
                                 //    fewer for small row tables, so more workgroups fill the chip)
     int32_t lean;               // 1: every row is one plain range with uniform power-of-two bins

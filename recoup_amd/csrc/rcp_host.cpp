@@ -874,7 +874,9 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
         rcp_tile_geometry(&tile, &rmax);
         int cus = 256;
         int dev = 0;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
         P.rounds = std::min(rmax, 2);
         while (P.rounds > 1 &&
                (int64_t)((R + tile * P.rounds - 1) / (tile * P.rounds)) * P.n_chunks_total < 2 * (int64_t)cus)
@@ -883,6 +885,14 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
         plan->tile_rows = P.lean ? rcp_tile_rows() : tile * P.rounds;
     }
     plan->grid = (int64_t)((R + plan->tile_rows - 1) / plan->tile_rows) * P.n_chunks_total;
+    // locate: one lane per row when every row is one range in the merged layout and its
+    // searches (bounds + interior chunk edges) fit one lockstep round of 8
+    {
+        bool one = rows->ignore_strand && 2 + 2 * P.n_chunks_total <= 8;
+        for (int r = 0; one && r < R; ++r)
+            if (B.row_seg[r + 1] - B.row_seg[r] > 1) one = false;
+        P.loc_lpr = (one && env_int("RCP_LOC_LPR", 4) == 1) ? 1 : 4;
+    }
     if (plan->lds > 160 * 1024) return fail(RCP_EUNSUPPORTED, "plan needs %zu B of LDS", plan->lds);
     HIP_TRY(hipMemset(plan->work.p, 0, plan->work.bytes));
     *out = plan.release();

@@ -541,16 +541,17 @@ __device__ __forceinline__ uint32_t dir_bound_at(const RcpPlanDev& P, int64_t d0
     return lo;
 }
 
-// Up to 4 searches of one lane (search u: v[u], upper when dst[u] == -1 or dst[u] is odd, as
+// Up to K searches of one lane (search u: v[u], upper when dst[u] == -1 or dst[u] is odd, as
 // the locate task numbering has it) bisecting in lockstep: each step issues the probes of all
 // unfinished searches before using any, so they cost one chain of round trips together.
-__device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0, int32_t nb, const int32_t (&v)[4],
-                                                const int (&dst)[4], int cnt, uint32_t (&res)[4]) {
-    uint32_t lo[4], hi[4];
-    int64_t thr[4];
-    bool up[4];
+template <int K>
+__device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0, int32_t nb, const int32_t (&v)[K],
+                                                const int (&dst)[K], int cnt, uint32_t (&res)[K]) {
+    uint32_t lo[K], hi[K];
+    int64_t thr[K];
+    bool up[K];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < K; ++u) {
         up[u] = dst[u] == -1 || (dst[u] >= 0 && (dst[u] & 1));
         lo[u] = hi[u] = 0;
         thr[u] = (int64_t)v[u] + (up[u] ? 1 : 0);
@@ -567,11 +568,11 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0,
     }
     const int32_t* se = reinterpret_cast<const int32_t*>(P.se);
     while (true) {
-        uint32_t m[4];
-        int32_t kv[4];
+        uint32_t m[K];
+        int32_t kv[K];
         bool any = false;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < K; ++u) {
             if (lo[u] < hi[u]) {
                 m[u] = lo[u] + ((hi[u] - lo[u]) >> 1);
                 kv[u] = up[u] ? se[(size_t)m[u] << 1] : P.pmax[m[u]];
@@ -580,14 +581,14 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0,
         }
         if (!any) break;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < K; ++u) {
             if (lo[u] < hi[u]) {
                 if ((int64_t)kv[u] < thr[u]) lo[u] = m[u] + 1; else hi[u] = m[u];
             }
         }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) res[u] = lo[u];
+    for (int u = 0; u < K; ++u) res[u] = lo[u];
 }
 
 __device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32_t v, bool upper) {
@@ -595,24 +596,29 @@ __device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32
     return dir_bound_at(P, d0, (int32_t)(P.dir_off[st + 1] - d0) - 1, v, upper);
 }
 
-// Four lanes per row.  The row's (segment, stream) searches are dealt round-robin to the
+// LPR = 4 lanes per row: the row's (segment, stream) searches are dealt round-robin to the
 // quad's lanes (one stream per segment in the merged layout, three in the stranded one), so
 // multi-range rows search in parallel; the quad then combines hits / max ends / candidate
 // counts with DPP.  For a single-range row the lanes also split the per-chunk range searches.
+// LPR = 1 (plans of single-range rows in the merged layout with <= 8 searches per row: C4,
+// C2): one lane per row runs all its searches in one lockstep round -- the same dependent
+// chain with a quarter of the waves and none of the quad's duplicated integer work.
 // Every search is bounded by the bucket directory and independent of the others: the
 // dependent chain per lane is one bucket search, not a sequence of them.
 #ifndef RCP_LOC_WPE
 #define RCP_LOC_WPE 1
 #endif
+template <int LPR>
 __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlanDev P) {
-    __shared__ uint32_t xres[kBlock / 4][2 * RCP_MAX_CRANGE_CHUNKS];  // per quad: chunk bounds
+    constexpr int KS = LPR == 1 ? 8 : 4;  // searches of one lockstep round
+    __shared__ uint32_t xres[kBlock / LPR][2 * RCP_MAX_CRANGE_CHUNKS];  // per row: chunk bounds
 #ifdef RCP_ABL_LOC_EMPTY  // ablation (locate timing): launch and dispatch only
     if (P.n_rows >= 0) return;
 #endif
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int r = t >> 2;
-    const int q = t & 3;
-    uint32_t* xr = xres[threadIdx.x >> 2];
+    const int r = t / LPR;
+    const int q = t % LPR;
+    uint32_t* xr = xres[threadIdx.x / LPR];
     const bool in_row = r < P.n_rows;
     // the row's locate input: one 80-byte record (RcpRowInfo, built with the plan)
     RcpRowInfo ri;
@@ -690,23 +696,25 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         // the searches, tasks -2 (lower), -1 (upper), 0 .. 2 nc - 1 (chunk edges): lane q takes
         // tasks -2 + q, -2 + q + 4, ... (up to 5 of 2 + 2 * RCP_MAX_CRANGE_CHUNKS = 18; edges at
         // the row's ends are skipped) and evaluates only its own chunk windows
-        int32_t sx[4] = {0, 0, 0, 0};
-        int sdst[4] = {0, 0, 0, 0};  // -2 lower, -1 upper, >= 0 xr index (its parity = upper)
+        int32_t sx[KS] = {};
+        int sdst[KS] = {};  // -2 lower, -1 upper, >= 0 xr index (its parity = upper)
         int cnt = 0;
-        uint32_t v = 0;
+        uint32_t v = 0, v_up = 0;  // LPR 1: the lane's own lower and upper bound
         // up to 4 searches bisect in lockstep (one chain of dependent loads for all of them:
         // C2 has 8 searches per row -> 2 per lane, C5 16 -> 4); a 5th starts a second round
         auto run = [&]() {
-            uint32_t w[4];
-            dir_bound_multi(P, ri.d0, ri.nb, sx, sdst, cnt, w);
+            uint32_t w[KS];
+            dir_bound_multi<KS>(P, ri.d0, ri.nb, sx, sdst, cnt, w);
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < KS; ++u)
                 if (u < cnt) {
-                    if (sdst[u] < 0) v = w[u]; else xr[sdst[u]] = w[u];
+                    if (sdst[u] == -2) v = w[u];
+                    else if (sdst[u] == -1) { if (LPR == 1) v_up = w[u]; else v = w[u]; }
+                    else xr[sdst[u]] = w[u];
                 }
             cnt = 0;
         };
-        for (int task = -2 + q; task < (spec_cr ? 2 * nc : 0); task += 4) {
+        for (int task = -2 + q; task < (spec_cr ? 2 * nc : 0); task += LPR) {
             int32_t x = 0;
             bool need = false;
             if (task < 0) {
@@ -726,16 +734,21 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
             }
             if (!need) continue;
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < KS; ++u)
                 if (cnt == u) {
                     sx[u] = x;
                     sdst[u] = task;
                 }
-            if (++cnt == 4) run();
+            if (++cnt == KS) run();
         }
         if (cnt) run();
-        lo = (uint32_t)qperm<0x00>((int)v);
-        hi = max(lo, (uint32_t)qperm<0x55>((int)v));
+        if (LPR == 1) {
+            lo = v;
+            hi = max(lo, v_up);
+        } else {
+            lo = (uint32_t)qperm<0x00>((int)v);
+            hi = max(lo, (uint32_t)qperm<0x55>((int)v));
+        }
         if (lo < hi) {
             hit = 1u << g;
             if (sl < 0 && q == 0) maxend[g] = P.pmax[hi - 1];
@@ -747,7 +760,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         }
         if (q != 0) lo = hi = 0;  // the quad combine below reads (lo, hi) from lane 0
     }
-    for (int pi = split1 ? npairs : q; pi < npairs; pi += 4) {
+    for (int pi = split1 ? npairs : q; pi < npairs; pi += LPR) {
         const int j = j0 + pi / ns;
         const int s = pi % ns;
         const RcpSeg sg = P.segs[j];
@@ -771,23 +784,26 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         // plan zeroed them; no read lives there)
     }
     // ---- combine the quad (all lanes active: DPP reads neighbours)
-    hit |= (uint32_t)qperm<0xB1>((int)hit);
-    hit |= (uint32_t)qperm<0x4E>((int)hit);
-    present |= (uint32_t)qperm<0xB1>((int)present);
-    present |= (uint32_t)qperm<0x4E>((int)present);
-    ncand += (uint32_t)qperm<0xB1>((int)ncand);
-    ncand += (uint32_t)qperm<0x4E>((int)ncand);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        maxend[g] = max(maxend[g], qperm<0xB1>(maxend[g]));
-        maxend[g] = max(maxend[g], qperm<0x4E>(maxend[g]));
-        maxpos[g] = max(maxpos[g], qperm<0xB1>(maxpos[g]));
-        maxpos[g] = max(maxpos[g], qperm<0x4E>(maxpos[g]));
+    if (LPR == 4) {
+        hit |= (uint32_t)qperm<0xB1>((int)hit);
+        hit |= (uint32_t)qperm<0x4E>((int)hit);
+        present |= (uint32_t)qperm<0xB1>((int)present);
+        present |= (uint32_t)qperm<0x4E>((int)present);
+        ncand += (uint32_t)qperm<0xB1>((int)ncand);
+        ncand += (uint32_t)qperm<0x4E>((int)ncand);
+    #pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            maxend[g] = max(maxend[g], qperm<0xB1>(maxend[g]));
+            maxend[g] = max(maxend[g], qperm<0x4E>(maxend[g]));
+            maxpos[g] = max(maxpos[g], qperm<0xB1>(maxpos[g]));
+            maxpos[g] = max(maxpos[g], qperm<0x4E>(maxpos[g]));
+        }
     }
-    // the single range of a fast row: (lo, hi) of pairs 0, 1, 2 sit in lanes 0, 1, 2
-    const uint32_t lo0 = (uint32_t)qperm<0x00>((int)lo), hi0 = (uint32_t)qperm<0x00>((int)hi);
-    const uint32_t lo1 = (uint32_t)qperm<0x55>((int)lo), hi1 = (uint32_t)qperm<0x55>((int)hi);
-    const uint32_t lo2 = (uint32_t)qperm<0xAA>((int)lo), hi2 = (uint32_t)qperm<0xAA>((int)hi);
+    // the single range of a fast row: (lo, hi) of pairs 0, 1, 2 sit in lanes 0, 1, 2 (LPR 1:
+    // the merged layout's one pair, in the lane itself)
+    const uint32_t lo0 = LPR == 1 ? lo : (uint32_t)qperm<0x00>((int)lo), hi0 = LPR == 1 ? hi : (uint32_t)qperm<0x00>((int)hi);
+    const uint32_t lo1 = LPR == 1 ? 0u : (uint32_t)qperm<0x55>((int)lo), hi1 = LPR == 1 ? 0u : (uint32_t)qperm<0x55>((int)hi);
+    const uint32_t lo2 = LPR == 1 ? 0u : (uint32_t)qperm<0xAA>((int)lo), hi2 = LPR == 1 ? 0u : (uint32_t)qperm<0xAA>((int)hi);
     bool valid = ok;
     if (ok) {
         for (int g = 0; g < 4; ++g) {
@@ -816,7 +832,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         }
         P.heavy_slot[r] = slot;
     }
-    slot = qperm<0x00>(slot);
+    if (LPR == 4) slot = qperm<0x00>(slot);
     const bool cr = P.crange != nullptr && fast && valid && slot < 0;
     if (cr && ns == 1) {
         // merged layout: the interior edges were searched with the row's bounds (xr)
@@ -2425,8 +2441,13 @@ hipError_t allow_big_lds(K kernel) {
 
 extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream) {
     if (P->n_rows == 0) return hipSuccess;
-    const int64_t grid = (4 * (int64_t)P->n_rows + kBlock - 1) / kBlock;  // four lanes per row
-    hipLaunchKernelGGL(rcp_locate_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
+    if (P->loc_lpr == 1) {
+        const int64_t grid = ((int64_t)P->n_rows + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(rcp_locate_kernel<1>, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
+    } else {
+        const int64_t grid = (4 * (int64_t)P->n_rows + kBlock - 1) / kBlock;  // four lanes per row
+        hipLaunchKernelGGL(rcp_locate_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
+    }
     return hipGetLastError();
 }
 

@@ -100,6 +100,8 @@ struct RcpPlanDev {
     uint32_t* seg_lo;           // [n_seg * 3]
     uint32_t* seg_hi;           // [n_seg * 3]
     uint8_t* valid;             // [n_rows]
+    uint8_t* valid_out;         // [n_rows] or NULL: the caller's validity vector, written by
+                                //    locate next to `valid` (no separate device copy per call)
     // bins
     int32_t n_parts;
     RcpPart part[RCP_MAX_PARTS];
@@ -151,9 +153,11 @@ struct RcpPlanDev {
     int32_t heavy_slice;        // candidate reads per heavy work item
     int32_t* heavy_slot;        // [n_rows] slot or -1 (locate output)
     int32_t* heavy_rows;        // [heavy_cap]
-    uint32_t* heavy_slice_off;  // [heavy_cap + 1]
-    int32_t* heavy_gdiff;       // [heavy_cap * heavy_stride], zero between executions
-    // status (status[0]) and heavy slot counter (status[1])
+    uint32_t* heavy_nslice;     // [heavy_cap] slices of each slot (locate output)
+    int32_t* heavy_gdiff;       // [heavy_cap * heavy_stride]; the slots the last execution used
+                                //    are cleared by the next one's reset kernel
+    // status (status[0]), heavy slot counter (status[1]), reset ticket (status[3]), lean work
+    // counters (status[8 .. 16])
     uint32_t* status;           // bit 0: numerator overflow, bit 1: per-base width mismatch
 };
 

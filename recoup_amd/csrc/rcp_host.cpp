@@ -28,7 +28,7 @@ hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, u
                            hipStream_t stream);
 hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream);
 hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_t stream);
-hipError_t rcp_launch_heavy_clear(const RcpPlanDev* P, hipStream_t stream);
+hipError_t rcp_launch_exec_reset(const RcpPlanDev* P, hipStream_t stream);
 hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_t* binsum, int csr, hipStream_t stream);
 hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStream_t stream);
 size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr);
@@ -821,7 +821,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.ncand = reinterpret_cast<uint32_t*>(wb + w_ncand);
     P.heavy_slot = reinterpret_cast<int32_t*>(wb + w_hslot);
     P.heavy_rows = reinterpret_cast<int32_t*>(wb + w_hrows);
-    P.heavy_slice_off = reinterpret_cast<uint32_t*>(wb + w_hoff);
+    P.heavy_nslice = reinterpret_cast<uint32_t*>(wb + w_hoff);
     P.heavy_gdiff = reinterpret_cast<int32_t*>(wb + w_gdiff);
     P.rec = reinterpret_cast<RcpRowRec*>(wb + w_rec);
     P.crange = keep_crange ? reinterpret_cast<uint2*>(wb + w_crange) : nullptr;
@@ -931,10 +931,10 @@ extern "C" int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_str
     DeviceGuard g(plan->rs->device);
     HIP_TRY(g.err);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    HIP_TRY(hipMemsetAsync(plan->dev.status, 0, 8, s));
-    HIP_TRY(rcp_launch_locate(&plan->dev, s));
-    if (d_valid && plan->n_rows)
-        HIP_TRY(hipMemcpyAsync(d_valid, plan->dev.valid, plan->n_rows, hipMemcpyDeviceToDevice, s));
+    RcpPlanDev Q = plan->dev;
+    Q.valid_out = d_valid;
+    HIP_TRY(rcp_launch_exec_reset(&Q, s));
+    HIP_TRY(rcp_launch_locate(&Q, s));
     return RCP_OK;
 }
 
@@ -947,17 +947,16 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
     HIP_TRY(g.err);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     if (stages & RCP_STAGE_LOCATE) {
-        HIP_TRY(hipMemsetAsync(plan->dev.status, 0, 8, s));
-        HIP_TRY(rcp_launch_locate(&plan->dev, s));
-        HIP_TRY(rcp_launch_heavy(&plan->dev, kHeavyGrid, s));
+        // reset (the previous execution's heavy slots, status words), locate (also writes the
+        // caller's validity vector), heavy slices
+        RcpPlanDev Q = plan->dev;
+        Q.valid_out = d_valid;
+        HIP_TRY(rcp_launch_exec_reset(&Q, s));
+        HIP_TRY(rcp_launch_locate(&Q, s));
+        HIP_TRY(rcp_launch_heavy(&Q, kHeavyGrid, s));
     }
     if (stages & RCP_STAGE_PILEUP) HIP_TRY(rcp_launch_pileup(&plan->dev, d_out, d_binsum, 0, s));
-    if (stages & RCP_STAGE_INTERP) {
-        HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
-        HIP_TRY(rcp_launch_heavy_clear(&plan->dev, s));
-    }
-    if ((stages & RCP_STAGE_LOCATE) && d_valid && plan->n_rows)
-        HIP_TRY(hipMemcpyAsync(d_valid, plan->dev.valid, plan->n_rows, hipMemcpyDeviceToDevice, s));
+    if (stages & RCP_STAGE_INTERP) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
     return RCP_OK;
 }
 
@@ -1028,13 +1027,11 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
     HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * (plan->n_rows + 1), hipMemcpyHostToDevice, s));
     P.csr_off = d_off.as<int64_t>();
     P.csr_out = d_cov;
-    HIP_TRY(hipMemsetAsync(plan->dev.status, 0, 8, s));
+    P.valid_out = d_valid;
+    HIP_TRY(rcp_launch_exec_reset(&P, s));
     HIP_TRY(rcp_launch_locate(&P, s));
     HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
-    HIP_TRY(rcp_launch_heavy_clear(&P, s));
-    if (d_valid && plan->n_rows)
-        HIP_TRY(hipMemcpyAsync(d_valid, plan->dev.valid, plan->n_rows, hipMemcpyDeviceToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));  // d_off is released on return
     return RCP_OK;
 }

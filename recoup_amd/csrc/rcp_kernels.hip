@@ -816,6 +816,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
     int32_t slot = -1;
     if (in_row && q == 0) {
         P.valid[r] = valid ? 1 : 0;
+        if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
         P.ncand[r] = ncand;
         // skewed rows only: many candidates per column chunk (each chunk of a row is one
         // wave's work) AND a deep pileup (> 2 reads per position), so a long row with
@@ -828,6 +829,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
             if (u < (uint32_t)P.heavy_cap) {
                 slot = (int32_t)u;
                 P.heavy_rows[u] = r;
+                P.heavy_nslice[u] = (ncand + (uint32_t)P.heavy_slice - 1) / (uint32_t)P.heavy_slice;
             }
         }
         P.heavy_slot[r] = slot;
@@ -896,29 +898,30 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
 }
 
 // =================================================================================
-// heavy rows: slice offsets (1 block), slice pileup (many blocks), cleanup
+// heavy rows: execution reset (clears the previous execution's slots), slice pileup
 // =================================================================================
-__global__ void __launch_bounds__(kBlock) rcp_heavy_plan_kernel(RcpPlanDev P) {
-    __shared__ uint32_t scratch[kWaves];
-    __shared__ uint32_t carry;
-    const uint32_t n = min(P.status[1], (uint32_t)P.heavy_cap);
-    if (threadIdx.x == 0) carry = 0;
+// First kernel of every execution (it replaces a status memset before locate and a clear
+// kernel after the pileup): zeroes the difference arrays of the slots the previous execution
+// claimed -- the pileup kernels read them across column chunks, so no reader can clear them
+// -- and, once every block has read the slot count, the status words (last block's ticket).
+__global__ void __launch_bounds__(kBlock) rcp_exec_reset_kernel(RcpPlanDev P) {
+    __shared__ uint32_t sn;
+    if (threadIdx.x == 0) sn = P.heavy_threshold > 0 ? min(P.status[1], (uint32_t)P.heavy_cap) : 0u;
     __syncthreads();
-    for (uint32_t b = 0; b < n; b += kBlock) {
-        const uint32_t s = b + threadIdx.x;
-        uint32_t c = 0;
-        if (s < n) {
-            const uint32_t nc = P.ncand[P.heavy_rows[s]];
-            c = (nc + P.heavy_slice - 1) / P.heavy_slice;
-        }
-        const uint32_t ex = block_exclusive_scan(c, scratch);
-        const uint32_t base = carry;
-        if (s < n) P.heavy_slice_off[s] = base + ex;
-        __syncthreads();
-        if (threadIdx.x == kBlock - 1) carry = base + ex + c;
-        __syncthreads();
+    const uint32_t n = sn;
+    for (uint32_t s = blockIdx.x; s < n; s += gridDim.x) {
+        int32_t* g = P.heavy_gdiff + (size_t)s * P.heavy_stride;
+        const int32_t nr = P.row_len[P.heavy_rows[s]];
+        for (int q = threadIdx.x; q <= nr; q += blockDim.x) g[q] = 0;
     }
-    if (threadIdx.x == 0) P.heavy_slice_off[n] = carry;
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&P.status[3], 1u) == gridDim.x - 1) {
+            atomicExch(&P.status[0], 0u);
+            atomicExch(&P.status[1], 0u);
+            atomicExch(&P.status[3], 0u);
+        }
+    }
 }
 
 #ifndef RCP_HEAVY_LOADS
@@ -927,22 +930,40 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_plan_kernel(RcpPlanDev P) {
 constexpr int kHeavyLoads = RCP_HEAVY_LOADS;  // = RCP_HEAVY_SLICE / kBlock: one round trip per slice
 
 __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) {
+    // dynamic LDS only (a static array on top of the 160 KB dynamic limit fails the launch
+    // attribute): 16 words of scan scratch, the row's difference array, the slice offsets
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    int32_t* diff = reinterpret_cast<int32_t*>(smem);
+    uint32_t* scratch = reinterpret_cast<uint32_t*>(smem);
+    int32_t* diff = reinterpret_cast<int32_t*>(smem) + 16;
+    uint32_t* offs = reinterpret_cast<uint32_t*>(diff) + (P.heavy_max_len + 1 + 64);  // [heavy_cap + 1]
     const uint32_t n = min(P.status[1], (uint32_t)P.heavy_cap);
     if (n == 0) return;
-    const uint32_t total = P.heavy_slice_off[n];
+    // slice offsets of the slots: every block scans the per-slot slice counts locate stored
+    // when it claimed them (no separate one-block planning kernel between the two)
+    uint32_t total = 0;
+    for (uint32_t b = 0; b < n; b += kBlock) {
+        const uint32_t s = b + threadIdx.x;
+        const uint32_t c = s < n ? P.heavy_nslice[s] : 0u;
+        const uint32_t ex = block_exclusive_scan(c, scratch);
+        if (s < n) offs[s] = total + ex;
+        uint32_t round = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) round += scratch[w];
+        total += round;
+        __syncthreads();  // scratch is rewritten by the next round
+    }
+    __syncthreads();
     for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
         // slot holding slice w
         uint32_t lo = 0, hi = n;
         while (hi - lo > 1) {
             const uint32_t m = (lo + hi) >> 1;
-            if (P.heavy_slice_off[m] <= w) lo = m; else hi = m;
+            if (offs[m] <= w) lo = m; else hi = m;
         }
         const int slot = (int)lo;
         const int r = P.heavy_rows[slot];
         const int32_t nr = P.row_len[r];
-        const uint32_t q0 = (w - P.heavy_slice_off[slot]) * (uint32_t)P.heavy_slice;
+        const uint32_t q0 = (w - offs[slot]) * (uint32_t)P.heavy_slice;
         const uint32_t q1 = min(q0 + (uint32_t)P.heavy_slice, P.ncand[r]);
         for (int q = threadIdx.x; q <= nr; q += kBlock) diff[q] = 0;
         __syncthreads();
@@ -995,15 +1016,6 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) 
             if (v) atomicAdd(&g[q], v);
         }
         __syncthreads();
-    }
-}
-
-__global__ void rcp_heavy_clear_kernel(RcpPlanDev P) {
-    const uint32_t n = min(P.status[1], (uint32_t)P.heavy_cap);
-    for (uint32_t s = blockIdx.x; s < n; s += gridDim.x) {
-        int32_t* g = P.heavy_gdiff + (size_t)s * P.heavy_stride;
-        const int32_t nr = P.row_len[P.heavy_rows[s]];
-        for (int q = threadIdx.x; q <= nr; q += blockDim.x) g[q] = 0;
     }
 }
 
@@ -2459,15 +2471,16 @@ extern "C" hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(rcp_heavy_plan_kernel, dim3(1), dim3(kBlock), 0, stream, *P);
-    const size_t lds = 4 * ((size_t)P->heavy_max_len + 1 + 64);
+    // difference array of one row + the slots' slice offsets
+    const size_t lds = 4 * (16 + (size_t)P->heavy_max_len + 1 + 64) + 4 * ((size_t)P->heavy_cap + 1);
     hipLaunchKernelGGL(rcp_heavy_pileup_kernel, dim3(grid), dim3(kBlock), lds, stream, *P);
     return hipGetLastError();
 }
 
-extern "C" hipError_t rcp_launch_heavy_clear(const RcpPlanDev* P, hipStream_t stream) {
-    if (P->n_rows == 0 || P->heavy_threshold <= 0) return hipSuccess;
-    hipLaunchKernelGGL(rcp_heavy_clear_kernel, dim3(256), dim3(kBlock), 0, stream, *P);
+// before every locate: see rcp_exec_reset_kernel
+extern "C" hipError_t rcp_launch_exec_reset(const RcpPlanDev* P, hipStream_t stream) {
+    const unsigned grid = (P->n_rows > 0 && P->heavy_threshold > 0) ? 256u : 1u;
+    hipLaunchKernelGGL(rcp_exec_reset_kernel, dim3(grid), dim3(kBlock), 0, stream, *P);
     return hipGetLastError();
 }
 

@@ -282,6 +282,35 @@ def test_heavy_duplicate_stacks_match(gpu):
         del os.environ["RCP_HEAVY_THRESHOLD"]
 
 
+def test_heavy_repeated_executions(gpu):
+    """Each execution starts with the reset kernel, which clears the heavy slots the previous
+    call left (there is no clear after the pileup): one plan run repeatedly, with validity-only
+    and coverage calls in between, gives the oracle's matrix every time."""
+    from recoup_amd.engine import Bins, Plan, ReadSet
+    rng = np.random.default_rng(31)
+    reads = make_reads(rng, 200_000, widths=(100, 200))
+    rows = single_rows(rng, 100, 2000)
+    os.environ["RCP_HEAVY_THRESHOLD"] = "16"
+    try:
+        rs = ReadSet(*reads, CHROM_LEN, device=0)
+        plan = Plan(rs, rows, Bins([("whole", 100)]))
+        ix = oracle_rows.index_for(reads, CHROM_LEN)
+        cov = oracle_rows.row_coverage(ix, rows)
+        exp = oracle_rows.profile(cov, Bins([("whole", 100)]))
+        for k in range(3):
+            check(plan.run(), exp)
+            if k == 0:
+                np.testing.assert_array_equal(plan.validity(), exp[1])
+            if k == 1:
+                got = plan.coverage()
+                for g, e in zip(got, cov):
+                    assert (g is None) == (e is None)
+                    if e is not None:
+                        np.testing.assert_array_equal(g, e)
+    finally:
+        del os.environ["RCP_HEAVY_THRESHOLD"]
+
+
 def test_calc_coverage_csr(gpu):
     from recoup_amd.engine import Plan, ReadSet
     rng = np.random.default_rng(3)

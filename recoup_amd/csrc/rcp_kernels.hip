@@ -840,19 +840,18 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         // merged layout: the interior edges were searched with the row's bounds (xr)
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (q == 0) {
-            for (int c = 0; c < nc; ++c) {
-                int32_t gps, gpe;
-                bool empty;
-                uint32_t clo = lo0, chi = hi0;
-                if (piece(c, &gps, &gpe, &empty)) {
-                    clo = gps > sg0.lo ? xr[2 * c] : lo0;
-                    chi = max(clo, gpe < sg0.hi ? xr[2 * c + 1] : hi0);
-                } else if (empty) {
-                    chi = clo;
-                }
-                P.crange[((size_t)r * nc + c) * 3] = make_uint2(clo, chi);
+        // the quad's lanes take every LPR-th chunk (lo0 / hi0 are broadcast, xr is shared)
+        for (int c = q; c < nc; c += LPR) {
+            int32_t gps, gpe;
+            bool empty;
+            uint32_t clo = lo0, chi = hi0;
+            if (piece(c, &gps, &gpe, &empty)) {
+                clo = gps > sg0.lo ? xr[2 * c] : lo0;
+                chi = max(clo, gpe < sg0.hi ? xr[2 * c + 1] : hi0);
+            } else if (empty) {
+                chi = clo;
             }
+            P.crange[((size_t)r * nc + c) * 3] = make_uint2(clo, chi);
         }
     } else if (cr && q < 3) {
         // stranded layout: lane q refines its own stream's range chunk by chunk
@@ -1827,17 +1826,26 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     int32_t* item = reinterpret_cast<int32_t*>(lmeta + 2 * kRows);  // [2]: item code or -1
     const int xcd = blockIdx.x & 7;
     const int n_tiles = (P.n_rows + kRows - 1) / kRows;
-    const uint32_t n_items_x = (uint32_t)((n_tiles - xcd + 7) / 8) * (uint32_t)P.n_chunks_total;
+    auto n_items_of = [&](int x) { return (uint32_t)((n_tiles - x + 7) / 8) * (uint32_t)P.n_chunks_total; };
 
-    // store wave 0: claim the next item of this XCD, decode its rows into buffer buf
+    // store wave 0: claim the next item of this XCD, decode its rows into buffer buf; once
+    // this XCD's items are gone, take the other XCDs' remaining ones (tail balance)
     auto claim = [&](int buf) {
         uint32_t j = 0;
+        int xs = xcd;
         if (lane == 0) j = atomicAdd(&P.status[8 + xcd], 1u);
         j = __builtin_amdgcn_readfirstlane(j);
+#ifndef RCP_LEAN_NO_STEAL
+        for (int k = 1; k < 8 && j >= n_items_of(xs); ++k) {
+            xs = (xcd + k) & 7;
+            if (lane == 0) j = atomicAdd(&P.status[8 + xs], 1u);
+            j = __builtin_amdgcn_readfirstlane(j);
+        }
+#endif
         int code = -1;
-        if (j < n_items_x) {
+        if (j < n_items_of(xs)) {
             const int tl = (int)(j / P.n_chunks_total);
-            code = (tl * 8 + xcd) * P.n_chunks_total + (int)(j - (uint32_t)tl * P.n_chunks_total);
+            code = (tl * 8 + xs) * P.n_chunks_total + (int)(j - (uint32_t)tl * P.n_chunks_total);
             const LeanItem it = lean_item(P, code);
             lmeta[buf * kRows + lane] =
                 lean_pack(decode_row<false, false>(P, P.part[it.p], it.k0, it.cidx, it.tile * kRows + lane));

@@ -1810,12 +1810,15 @@ constexpr int kLMaxPassGen = 4;  // general-bins mode: <= 4 * kLQuads * 4 = 256 
 #ifndef RCP_LWPE_GEN
 #define RCP_LWPE_GEN RCP_LWPE
 #endif
+#ifndef RCP_LEAN_DYN
+#define RCP_LEAN_DYN 1
+#endif
 template <int MAXPER, bool GEN>
 __global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(GEN ? RCP_LWPE_GEN : RCP_LWPE)))
 rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int T = kTile;
-    constexpr int kSteps = kRowsPerWave * kRounds;  // rows of one wave per item
+    [[maybe_unused]] constexpr int kSteps = kRowsPerWave * kRounds;  // rows of one wave per item
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int lane = tid & 63;
@@ -1856,12 +1859,13 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     };
     if (wave == kPWaves) claim(0);
+    if (tid == 0) item[2] = 0;  // the pile waves' row counter (RCP_LEAN_DYN)
     lds_barrier();
 
     if (wave < kPWaves) {
         // ================= pile waves
         int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * P.wave_words;
-        auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
+        [[maybe_unused]] auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
         auto prefetch = [&](const LeanMeta& mm, int2* dst) {
             const LeanRow m = lean_row(mm);
 #ifdef RCP_LABL_NOREAD
@@ -1882,14 +1886,8 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         int code = item[0];
         // one row: `cur` holds its first reads; the next row's (possibly the next item's
         // first row) go to `nxt`
-        auto pile_step = [&](const LeanItem& it, int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
-            const int i = row_of(step);
-            if (step + 1 < kSteps) {
-                prefetch(lmeta[buf * kRows + row_of(step + 1)], nxt);
-            } else {
-                const int nc = item[buf ^ 1];  // published by store wave 0 rounds ago
-                if (nc >= 0) prefetch(lmeta[(buf ^ 1) * kRows + row_of(0)], nxt);
-            }
+        // pile row i of the item (tile row), its first reads in `cur`; bin sums -> stage
+        auto pile_row = [&](const LeanItem& it, int i, int2 (&cur)[4]) __attribute__((always_inline)) {
             const LeanRow m = lean_row(lmeta[buf * kRows + i]);
             if (m.flag != 0) return;
             if (!GEN && !m.fast && m.heavy < 0) {  // the plan promised single-range rows
@@ -2015,6 +2013,66 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             lds_order();
         };
         int2 bufA[4], bufB[4];
+#if RCP_LEAN_DYN
+        // Rows are dealt dynamically: a wave takes the workgroup's next row number g from an
+        // LDS counter (rows 64 q .. 64 q + 63 = the q-th item of this workgroup, 16 per round)
+        // when it starts its current row, and prefetches g's first reads.  A round ends when
+        // its 16 rows are taken and piled, so a wave that drew a long row takes fewer of them
+        // (a static 2 rows per wave waited at barrier A for the round's slowest pair).  A wave
+        // holds at most one row ahead: the next round's, or the next item's round 0, whose
+        // metadata store wave 0 published rounds ago.
+        static_assert(kPWaves <= kTile, "pending rows of one round fit the next round");
+        uint32_t* ctr = reinterpret_cast<uint32_t*>(item + 2);
+        auto take = [&]() -> uint32_t {
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(ctr, 1u);
+            return __builtin_amdgcn_readfirstlane(v);
+        };
+        auto fetch = [&](uint32_t rel, int2 (&dst)[4]) {  // rel: row number relative to this item
+            if (rel < (uint32_t)kRows) {
+                prefetch(lmeta[buf * kRows + rel], dst);
+            } else {
+                const int nc = item[buf ^ 1];
+                if (nc >= 0) prefetch(lmeta[(buf ^ 1) * kRows + (rel - kRows)], dst);
+            }
+        };
+        uint32_t base = 0;       // first row number of the current item
+        uint32_t g = take();     // this wave's pending row
+        bool in_a = true;        // its first reads sit in bufA (else bufB)
+        if (code >= 0) fetch(g, bufA);
+        while (code >= 0) {
+            const LeanItem it = lean_item(P, code);
+            for (int rd = 0; rd < kRounds; ++rd) {
+                const uint32_t lim = base + (uint32_t)(T * (rd + 1));
+                while (g < lim) {
+                    const uint32_t gn = take();
+                    if (in_a) {
+                        fetch(gn - base, bufB);
+                        pile_row(it, (int)(g - base), bufA);
+                    } else {
+                        fetch(gn - base, bufA);
+                        pile_row(it, (int)(g - base), bufB);
+                    }
+                    in_a = !in_a;
+                    g = gn;
+                }
+                lds_barrier();  // A: the round's stage rows are complete
+                lds_barrier();  // B: the store waves hold them in registers
+            }
+            base += kRows;
+            buf ^= 1;
+            code = item[buf];
+        }
+#else
+        auto pile_step = [&](const LeanItem& it, int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
+            if (step + 1 < kSteps) {
+                prefetch(lmeta[buf * kRows + row_of(step + 1)], nxt);
+            } else {
+                const int nc = item[buf ^ 1];  // published by store wave 0 rounds ago
+                if (nc >= 0) prefetch(lmeta[(buf ^ 1) * kRows + row_of(0)], nxt);
+            }
+            pile_row(it, row_of(step), cur);
+        };
         if (code >= 0) prefetch(lmeta[row_of(0)], bufA);
         while (code >= 0) {
             const LeanItem it = lean_item(P, code);
@@ -2029,6 +2087,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             buf ^= 1;
             code = item[buf];
         }
+#endif
     } else {
         // ================= store waves: thread (row ii, column quad qd)
         const int st = tid - 64 * kPWaves;

@@ -1032,6 +1032,9 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) 
 #ifndef RCP_PILE_WAVES
 #define RCP_PILE_WAVES 8
 #endif
+#ifndef RCP_GEN_DYN  // dynamic row dealing in the general kernel: measured slower (C3 pileup 0.95
+#define RCP_GEN_DYN 0   // vs 0.88 ms, C2 0.072 vs 0.063: 16 VGPRs spilled at the 128 cap vs 5), off
+#endif
 #ifndef RCP_PILE_ROUNDS
 #define RCP_PILE_ROUNDS 4
 #endif
@@ -1356,13 +1359,15 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     if (tid < rows_wg) {
         meta[tid] = decode_row<MEDIAN, CSR>(P, part, k0, cidx, row0 + tid);
     }
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(meta + kRows);  // row counter (RCP_GEN_DYN), in the tail words
+    if (tid == 0) *ctr = 0u;
     lds_barrier();
 
-    // ---- rows of this wave: round rd, sub s -> row rd*T + s*kPWaves + wave
-    auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
+    // ---- rows of this wave (static dealing): round rd, sub s -> row rd*T + s*kPWaves + wave
+    [[maybe_unused]] auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
     // software pipeline: the first 256 candidate reads of the next kAhead rows are in flight
     // while a row is piled up (registers are free: LDS, not VGPRs, limits occupancy)
-    const int n_steps = kRowsPerWave * rounds;
+    [[maybe_unused]] const int n_steps = kRowsPerWave * rounds;
     auto prefetch = [&](int i, int2* dst) {
         const RowMeta m = uniform_meta(meta[i]);
 #ifdef RCP_ABL_LOADS
@@ -1384,7 +1389,6 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     // back-edge would need the prefetched reads to have landed right after the epilogue's
     // stores, and gfx9's single in-order vmcnt would make that wait for the stores too.
     int2 bufA[4], bufB[4];
-    prefetch(row_of(0), bufA);
     // ---- round epilogue: stage row -> out[col * n_rows + row].  Thread t serves row t % 16
     // and column quads t / 16, t / 16 + 32, ...: one 16-B stage read feeds four stores, and
     // the 16 lanes of a quad column write 16 consecutive rows (128 B) of one column.
@@ -1471,11 +1475,10 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     bool clean = false;  // this wave's difference array is all zero (layout clean_sh)
     int clean_sh = -1;
     // one row of this wave: `cur` holds its first reads; the next row's go to `nxt`
-    auto pile_step = [&](int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
-        const int i = row_of(step);
-        if (step + 1 < n_steps) prefetch(row_of(step + 1), nxt);
+    // pile row i of the workgroup (round i / T), its first reads in `cur`
+    auto pile_row = [&](int i, int2 (&cur)[4]) __attribute__((always_inline)) {
         const RowMeta m = uniform_meta(meta[i]);
-        uint32_t* sbuf = stage + ((step / kRowsPerWave) % kStageBufs) * T * RS;  // this round's stage
+        uint32_t* sbuf = stage + ((i / T) % kStageBufs) * T * RS;  // this round's stage
         if (m.flag == 0) {  // wave-uniform: scalar branch
             const int r = row0 + i;
             const int32_t npos = m.npos;
@@ -1622,11 +1625,47 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
             }
         }
     };
+#if RCP_GEN_DYN
+    // rows dealt dynamically, as in the lean kernel: a wave takes the next row number from an
+    // LDS counter when it starts its current row and prefetches it; a round ends when its T
+    // rows are taken and piled (a static 2 rows per wave waited for the round's slowest pair)
+    static_assert(kPWaves <= T, "pending rows of one round fit the next round");
+    auto take = [&]() -> uint32_t {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(ctr, 1u);
+        return __builtin_amdgcn_readfirstlane(v);
+    };
+    uint32_t g = take();  // this wave's pending row
+    bool in_a = true;     // its first reads sit in bufA (else bufB)
+    if (g < (uint32_t)rows_wg) prefetch((int)g, bufA);
+#else
+    auto pile_step = [&](int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
+        if (step + 1 < n_steps) prefetch(row_of(step + 1), nxt);
+        pile_row(row_of(step), cur);
+    };
+    prefetch(row_of(0), bufA);
+#endif
     for (int rd = 0; rd < rounds; ++rd) {
+#if RCP_GEN_DYN
+        const uint32_t lim = (uint32_t)(T * (rd + 1));
+        while (g < lim) {
+            const uint32_t gn = take();
+            if (in_a) {
+                if (gn < (uint32_t)rows_wg) prefetch((int)gn, bufB);
+                pile_row((int)g, bufA);
+            } else {
+                if (gn < (uint32_t)rows_wg) prefetch((int)gn, bufA);
+                pile_row((int)g, bufB);
+            }
+            in_a = !in_a;
+            g = gn;
+        }
+#else
         for (int s2 = 0; s2 < kRowsPerWave; s2 += 2) {
             pile_step(rd * kRowsPerWave + s2, bufA, bufB);
             pile_step(rd * kRowsPerWave + s2 + 1, bufB, bufA);
         }
+#endif
         if (CSR) continue;
 #ifdef RCP_ABL_EPI
         continue;

@@ -155,7 +155,9 @@ RCP_API int rcp_plan_destroy(rcp_plan* plan);
 RCP_API int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info);
 
 /* Device work only (stream-ordered, no host sync, capturable in a hipGraph):
- *   locate kernel (per segment/stream read ranges + NULL semantics),
+ *   reset kernel (clears the skewed-row state the previous execution of this plan left),
+ *   locate kernel (per segment/stream read ranges + NULL semantics; writes d_valid),
+ *   skewed-row slice kernel,
  *   pileup-bin kernel (LDS difference array -> scans -> bins -> column-major out),
  *   interpolation kernel for rows with fewer positions than bins.
  * d_out: device [n_rows * n_cols] doubles.  d_valid (device, n_rows) and d_binsum

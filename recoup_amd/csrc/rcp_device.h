@@ -130,6 +130,10 @@ struct RcpPlanDev {
     int32_t wave_words;         // LDS words per wave difference array (multiple of 256)
     int32_t stage_cap;          // max bins per chunk
     int32_t interp_cap;         // max positions of an interpolated slice
+    // chunk windows of rows of nominal length cw_len (-1: none), tabulated by the plan:
+    // chunk c piles row positions [cw[2c], cw[2c] + cw[2c+1]); cw[2c+1] < 0: not piled
+    int32_t cw_len;
+    int32_t cw[2 * RCP_MAX_CRANGE_CHUNKS];
     int32_t loc_lpr;            // locate lanes per row: 4, or 1 for single-range rows in the merged
                                 //    layout with <= 8 searches per row
     int32_t rounds;             // general pileup kernel: rounds of kTile rows per workgroup (1..4;

@@ -825,6 +825,36 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.heavy_gdiff = reinterpret_cast<int32_t*>(wb + w_gdiff);
     P.rec = reinterpret_cast<RcpRowRec*>(wb + w_rec);
     P.crange = keep_crange ? reinterpret_cast<uint2*>(wb + w_crange) : nullptr;
+    // the locate kernel's chunk windows for the rows of the first row's length (all rows of
+    // C2 / C4 / C5), when no part of that length has an R-RNG layout: the same arithmetic as
+    // the kernel's chunk_window, once per plan instead of once per (row, chunk)
+    P.cw_len = -1;
+    if (keep_crange && R > 0 && env_int("RCP_CW_TABLE", 1)) {
+        const int32_t nr = B.row_len[0];
+        bool ok = true;
+        int c = 0;
+        for (int p = 0; ok && p < P.n_parts; ++p) {
+            const RcpPart& pt = P.part[p];
+            for (int cp = 0; cp < pt.n_chunks; ++cp, ++c) {
+                int32_t head, L;
+                rcp_part_slice(pt, nr, &head, &L);
+                const int32_t n = pt.n_bins, k0 = cp * pt.chunk_bins;
+                P.cw[2 * c] = 0;
+                P.cw[2 * c + 1] = -1;
+                if (k0 >= n || (pt.per_base ? L != n : L < n)) continue;
+                const int32_t bs = pt.per_base ? 1 : L / n;
+                if (!pt.per_base && L - bs * n != 0) {
+                    ok = false;  // an R-RNG layout: the kernel computes these rows itself
+                    break;
+                }
+                if (P.stat == 1 && bs > P.chunk_cap) continue;
+                const int32_t kend = std::min(k0 + pt.chunk_bins, n);
+                P.cw[2 * c] = head + bs * k0;
+                P.cw[2 * c + 1] = bs * (kend - k0);
+            }
+        }
+        if (ok) P.cw_len = nr;
+    }
     const int32_t n_interp = (int32_t)B.interp_row.size();
     // x (L+1) | y (n+1) | b, c, d (3 (L+1)) | interval index per output point (n ints); the
     // neighborhood fill's n pre-fill values reuse b..
@@ -1022,6 +1052,7 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
     pt.n_chunks = (pt.n_bins + pt.chunk_bins - 1) / pt.chunk_bins;
     P.n_chunks_total = pt.n_chunks;
     P.crange = nullptr;  // sized for the plan's chunks, not these
+    P.cw_len = -1;
     DevBuf d_off;
     HIP_TRY(d_off.alloc(8 * (plan->n_rows + 1)));
     HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * (plan->n_rows + 1), hipMemcpyHostToDevice, s));

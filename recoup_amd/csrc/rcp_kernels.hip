@@ -661,14 +661,23 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
     const int32_t len = sg0.hi - sg0.lo + 1;
     // genomic piece of chunk c (false: the chunk streams the whole range / nothing special)
     auto piece = [&](int c, int32_t* gps, int32_t* gpe, bool* empty) -> bool {
-        int p = 0, cp = c;
-        while (p < P.n_parts - 1 && cp >= P.part[p].n_chunks) {
-            cp -= P.part[p].n_chunks;
-            ++p;
-        }
         int32_t p0, np;
         *empty = false;
-        if (!chunk_window(P, P.part[p], cp * P.part[p].chunk_bins, nr, &p0, &np)) return false;
+#ifndef RCP_NO_CW_TABLE
+        if (nr == P.cw_len) {  // the plan's common row length: windows tabulated on the host
+            np = P.cw[2 * c + 1];
+            if (np < 0) return false;
+            p0 = P.cw[2 * c];
+        } else
+#endif
+        {
+            int p = 0, cp = c;
+            while (p < P.n_parts - 1 && cp >= P.part[p].n_chunks) {
+                cp -= P.part[p].n_chunks;
+                ++p;
+            }
+            if (!chunk_window(P, P.part[p], cp * P.part[p].chunk_bins, nr, &p0, &np)) return false;
+        }
         const int32_t a = max(p0, sg0.off), b = min(p0 + np, sg0.off + len);
         if (a >= b) {
             *empty = true;

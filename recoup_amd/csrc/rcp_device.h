@@ -82,7 +82,8 @@ struct RcpPlanDev {
     int32_t n_chrom;
     // bucket directory of each stream (buckets of 2^dir_shift bp): for a position v in
     // bucket b, lower_bound(pmax >= v) lies in [dir_l[b], dir_l[b+1]] and
-    // upper_bound(start > v) in [dir_u[b], dir_u[b+1]] (entries at dir_off[stream] ..)
+    // upper_bound(start > v) in [dir_u[b], dir_u[b+1]] (entries at dir_off[stream] ..; the two
+    // arrays are interleaved, entry e at word 2e of each pointer, dir_u = dir_l + 1)
     const int32_t* dir_l;
     const int32_t* dir_u;
     const int64_t* dir_off;    // [n_chrom*3 + 1]

@@ -282,13 +282,12 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     }
     const int64_t ne = doff[n_streams];
     HIP_TRY(L->dir_off.alloc(8 * (n_streams + 1)));
-    HIP_TRY(L->dir_l.alloc(4 * std::max<int64_t>(ne, 1)));
-    HIP_TRY(L->dir_u.alloc(4 * std::max<int64_t>(ne, 1)));
+    HIP_TRY(L->dir_l.alloc(8 * std::max<int64_t>(ne, 1)));  // interleaved (l, u) per entry
     HIP_TRY(hipMemcpyAsync(L->dir_off.p, doff.data(), 8 * (n_streams + 1), hipMemcpyHostToDevice, s));
     L->h_dir_off = doff;
     HIP_TRY(rcp_launch_dir(ne, n_streams, L->dir_off.as<int64_t>(), L->stream_off.as<int64_t>(),
                            L->pmax.as<int32_t>(), L->se.as<int2>(), shift, L->dir_l.as<int32_t>(),
-                           L->dir_u.as<int32_t>(), s));
+                           L->dir_l.as<int32_t>() + 1, s));
     HIP_TRY(hipStreamSynchronize(s));
     rs->n = kept;
     return RCP_OK;
@@ -867,7 +866,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     P.stream_off = RL.stream_off.as<int64_t>();
     P.seqlen = rs->d_seqlen.as<int64_t>();
     P.dir_l = RL.dir_l.as<int32_t>();
-    P.dir_u = RL.dir_u.as<int32_t>();
+    P.dir_u = RL.dir_l.as<int32_t>() + 1;  // interleaved with dir_l (stride 2)
     P.dir_off = RL.dir_off.as<int64_t>();
     P.dir_shift = RL.dir_shift;
     P.merged = rows->ignore_strand ? 1 : 0;

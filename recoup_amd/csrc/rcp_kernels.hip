@@ -481,8 +481,10 @@ __global__ void rcp_dir_kernel(int64_t n_entries, int64_t n_streams, const int64
     const int64_t v = bucket << shift;
     const int32_t vc = (int32_t)min(v, (int64_t)INT32_MAX);
     const uint32_t so = (uint32_t)off[a], eo = (uint32_t)off[a + 1];
-    dir_l[e] = (int32_t)lower_bound_pmax(pmax, so, eo, vc);
-    dir_u[e] = (int32_t)upper_bound_start(se, so, eo, (int32_t)min(v - 1, (int64_t)INT32_MAX));
+    // one 8-byte entry per bucket edge: a region's lower- and upper-bound searches at the
+    // same position (the interior chunk edges) read one directory line
+    dir_l[2 * e] = (int32_t)lower_bound_pmax(pmax, so, eo, vc);
+    dir_u[2 * e] = (int32_t)upper_bound_start(se, so, eo, (int32_t)min(v - 1, (int64_t)INT32_MAX));
 }
 
 // =================================================================================
@@ -526,8 +528,8 @@ __device__ __forceinline__ int qperm(int x) { return __builtin_amdgcn_update_dpp
 // variant -- 7 probes in flight per step -- measured slower on C4: 0.099 vs 0.082 ms.)
 __device__ __forceinline__ uint32_t dir_bound_at(const RcpPlanDev& P, int64_t d0, int32_t nb, int32_t v, bool upper) {
     const int32_t b = min(max(v, 0) >> P.dir_shift, nb - 1);
-    const int32_t* dir = upper ? P.dir_u : P.dir_l;
-    uint32_t lo = (uint32_t)dir[d0 + b], hi = (uint32_t)dir[d0 + b + 1];
+    const int32_t* dir = upper ? P.dir_u : P.dir_l;  // interleaved (l, u) pairs: stride 2
+    uint32_t lo = (uint32_t)dir[2 * (d0 + b)], hi = (uint32_t)dir[2 * (d0 + b + 1)];
     const int32_t* key = upper ? reinterpret_cast<const int32_t*>(P.se) : P.pmax;
     const int ksh = upper ? 1 : 0;                      // start of read m is word 2m of se
     const int64_t thr = (int64_t)v + (upper ? 1 : 0);  // start > v  <=>  start >= v + 1
@@ -561,9 +563,9 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0,
         if (u < cnt) {
 #endif
             const int32_t b = min(max(v[u], 0) >> P.dir_shift, nb - 1);
-            const int32_t* dir = up[u] ? P.dir_u : P.dir_l;
-            lo[u] = (uint32_t)dir[d0 + b];
-            hi[u] = (uint32_t)dir[d0 + b + 1];
+            const int32_t* dir = up[u] ? P.dir_u : P.dir_l;  // interleaved: stride 2
+            lo[u] = (uint32_t)dir[2 * (d0 + b)];
+            hi[u] = (uint32_t)dir[2 * (d0 + b + 1)];
         }
     }
     const int32_t* se = reinterpret_cast<const int32_t*>(P.se);

@@ -920,9 +920,10 @@ __global__ void __launch_bounds__(kBlock) rcp_exec_reset_kernel(RcpPlanDev P) {
     __syncthreads();
     const uint32_t n = sn;
     for (uint32_t s = blockIdx.x; s < n; s += gridDim.x) {
-        int32_t* g = P.heavy_gdiff + (size_t)s * P.heavy_stride;
-        const int32_t nr = P.row_len[P.heavy_rows[s]];
-        for (int q = threadIdx.x; q <= nr; q += blockDim.x) g[q] = 0;
+        // 16-byte stores: a slot is heavy_stride (a multiple of 64) ints, 16-byte aligned
+        int4* g4 = reinterpret_cast<int4*>(P.heavy_gdiff + (size_t)s * P.heavy_stride);
+        const int32_t n4 = (P.row_len[P.heavy_rows[s]] + 1 + 3) >> 2;
+        for (int q = threadIdx.x; q < n4; q += blockDim.x) g4[q] = make_int4(0, 0, 0, 0);
     }
     if (threadIdx.x == 0) {
         __threadfence();

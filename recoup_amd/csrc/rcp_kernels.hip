@@ -2597,7 +2597,10 @@ extern "C" hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_
 
 // before every locate: see rcp_exec_reset_kernel
 extern "C" hipError_t rcp_launch_exec_reset(const RcpPlanDev* P, hipStream_t stream) {
-    const unsigned grid = (P->n_rows > 0 && P->heavy_threshold > 0) ? 256u : 1u;
+#ifndef RCP_RESET_GRID
+#define RCP_RESET_GRID 64  // fewer last-block tickets: C2 0.093 -> 0.089 ms, C4 -0.005 ms (vs 256)
+#endif
+    const unsigned grid = (P->n_rows > 0 && P->heavy_threshold > 0) ? (unsigned)RCP_RESET_GRID : 1u;
     hipLaunchKernelGGL(rcp_exec_reset_kernel, dim3(grid), dim3(kBlock), 0, stream, *P);
     return hipGetLastError();
 }

@@ -151,6 +151,21 @@ typedef struct {
  * NULL for a calcCoverage-only plan.  The readset must outlive the plan. */
 RCP_API int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
                     rcp_plan** out);
+/* Plan options (NULL = defaults).  pileup_kernel: RCP_KERNEL_AUTO picks the lean kernel
+ * (pile + store waves) where every row is one plain range with uniform power-of-two bins,
+ * else the general kernel; RCP_KERNEL_GENERAL forces the general kernel; RCP_KERNEL_LEAN_ANY
+ * also routes other mean plans whose chunks fit one wave pass through the lean kernel's
+ * general-bins mode.  All choices give bit-identical results.  heavy_threshold: candidate
+ * reads per column chunk above which a skewed row is piled by many workgroups first
+ * (-1 = default 4096, 0 = never). */
+enum { RCP_KERNEL_AUTO = 0, RCP_KERNEL_GENERAL = 1, RCP_KERNEL_LEAN_ANY = 2 };
+typedef struct {
+    int32_t pileup_kernel;
+    int32_t heavy_threshold;
+    int32_t reserved[6];        /* zero */
+} rcp_plan_opts;
+RCP_API int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
+                               const rcp_plan_opts* opts, rcp_plan** out);
 RCP_API int rcp_plan_destroy(rcp_plan* plan);
 RCP_API int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info);
 

@@ -65,6 +65,11 @@ class PlanInfo(ctypes.Structure):
                 ("chunk_positions", ctypes.c_int32), ("pileup_kernel", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class PlanOpts(ctypes.Structure):
+    _fields_ = [("pileup_kernel", ctypes.c_int32), ("heavy_threshold", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 6)]
+
+
 # every symbol include/recoup_amd.h declares: (name, restype, argtypes)
 SIGNATURES = [
     ("rcp_version", ctypes.c_char_p, []),
@@ -74,6 +79,8 @@ SIGNATURES = [
     ("rcp_readset_destroy", ctypes.c_int, [_vp]),
     ("rcp_readset_info", ctypes.c_int, [_vp, _i64p, _i64p]),
     ("rcp_plan_create", ctypes.c_int, [_vp, ctypes.POINTER(RowsDesc), ctypes.POINTER(BinsDesc), ctypes.POINTER(_vp)]),
+    ("rcp_plan_create_ex", ctypes.c_int, [_vp, ctypes.POINTER(RowsDesc), ctypes.POINTER(BinsDesc),
+                                          ctypes.POINTER(PlanOpts), ctypes.POINTER(_vp)]),
     ("rcp_plan_destroy", ctypes.c_int, [_vp]),
     ("rcp_plan_info_get", ctypes.c_int, [_vp, ctypes.POINTER(PlanInfo)]),
     ("rcp_plan_execute", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),

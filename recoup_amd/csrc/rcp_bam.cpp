@@ -46,7 +46,26 @@ struct rcp_bam {
     int64_t n_alignments = 0;  // mapped alignments read
 };
 
+namespace {
+int bam_read(const char* path, int splice_action, double remove_q, int n_threads, rcp_bam** out);
+}
+
 extern "C" int rcp_bam_read(const char* path, int splice_action, double remove_q, int n_threads, rcp_bam** out) {
+    // nothing may escape into the caller's process (an R session): every C++ exception
+    // becomes an RCP_E* code
+    try {
+        return bam_read(path, splice_action, remove_q, n_threads, out);
+    } catch (const std::bad_alloc&) {
+        return bam_fail(RCP_ENOMEM, "host memory exhausted while reading the BAM file");
+    } catch (const std::exception& e) {
+        return bam_fail(RCP_ESEMANTIC, e.what());
+    } catch (...) {
+        return bam_fail(RCP_ESEMANTIC, "unexpected error while reading the BAM file");
+    }
+}
+
+namespace {
+int bam_read(const char* path, int splice_action, double remove_q, int n_threads, rcp_bam** out) {
     if (!path || !out) return bam_fail(RCP_EINVAL, "NULL argument");
     *out = nullptr;
     if (splice_action < RCP_SPLICE_KEEP || splice_action > RCP_SPLICE_SPLIT)
@@ -76,19 +95,24 @@ extern "C" int rcp_bam_read(const char* path, int splice_action, double remove_q
         const uint8_t* h = file.data() + p;
         if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return bam_fail(RCP_ESEMANTIC, "not a BGZF file");
         const uint16_t xlen = rd16(h + 10);
+        // the extra field must lie inside the file before any subfield is read
+        if ((size_t)xlen + 12 > file.size() - p) return bam_fail(RCP_ESEMANTIC, "truncated BGZF extra field");
         int64_t bsize = -1;
         for (size_t x = 12; x + 4 <= 12 + (size_t)xlen;) {
             const uint16_t slen = rd16(h + x + 2);
+            if (x + 4 + (size_t)slen > 12 + (size_t)xlen) return bam_fail(RCP_ESEMANTIC, "BGZF subfield beyond XLEN");
             if (h[x] == 66 && h[x + 1] == 67 && slen == 2) bsize = rd16(h + x + 4);
             x += 4 + slen;
         }
         if (bsize < 0) return bam_fail(RCP_ESEMANTIC, "BGZF block without BSIZE");
         const size_t blen = (size_t)bsize + 1;
-        if (p + blen > file.size() || blen < (size_t)xlen + 20) return bam_fail(RCP_ESEMANTIC, "truncated BGZF block");
+        if (blen > file.size() - p || blen < (size_t)xlen + 20) return bam_fail(RCP_ESEMANTIC, "truncated BGZF block");
         Block b;
         b.off = p + 12 + xlen;
         b.clen = blen - xlen - 20;
         b.ulen = (size_t)(uint32_t)rd32(file.data() + p + blen - 4);
+        // ISIZE of a BGZF block is at most 64 KiB (SAM spec 4.1); larger values are corrupt
+        if (b.ulen > 65536) return bam_fail(RCP_ESEMANTIC, "BGZF block ISIZE above 65536");
         b.uoff = total;
         total += b.ulen;
         blocks.push_back(b);
@@ -120,7 +144,13 @@ extern "C" int rcp_bam_read(const char* path, int splice_action, double remove_q
     };
     {
         std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        for (int t = 1; t < nt; ++t) {
+            try {
+                th.emplace_back(work);
+            } catch (const std::exception&) {
+                break;  // fewer threads (the calling one always works)
+            }
+        }
         work();
         for (auto& t : th) t.join();
     }
@@ -225,6 +255,7 @@ extern "C" int rcp_bam_read(const char* path, int splice_action, double remove_q
     *out = guard.release();
     return RCP_OK;
 }
+}  // namespace
 
 extern "C" int rcp_bam_info(const rcp_bam* b, int64_t* n_reads, int32_t* n_ref, int64_t* n_alignments) {
     if (!b) return bam_fail(RCP_EINVAL, "NULL handle");

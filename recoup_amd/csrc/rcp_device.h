@@ -135,8 +135,7 @@ struct RcpPlanDev {
     // chunk c piles row positions [cw[2c], cw[2c] + cw[2c+1]); cw[2c+1] < 0: not piled
     int32_t cw_len;
     int32_t cw[2 * RCP_MAX_CRANGE_CHUNKS];
-    int32_t loc_lpr;            // locate lanes per row: 4, or 1 for single-range rows in the merged
-                                //    layout with <= 8 searches per row
+    int32_t n_cus;              // compute units of the plan's device (persistent grid sizing)
     int32_t rounds;             // general pileup kernel: rounds of kTile rows per workgroup (1..4;
                                 //    fewer for small row tables, so more workgroups fill the chip)
     int32_t lean;               // 1: every row is one plain range with uniform power-of-two bins

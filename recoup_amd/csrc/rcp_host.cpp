@@ -11,8 +11,10 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <memory>
+#include <new>
 #include <string>
 #include <utility>
 #include <vector>
@@ -93,11 +95,6 @@ void wave_geometry(int32_t positions, int32_t* words, int32_t* capacity) {
     *capacity = 64 * per - 1;
 }
 
-int env_int(const char* name, int def) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : def;
-}
-
 thread_local std::string g_err;
 
 int fail(int code, const char* fmt, ...) {
@@ -117,6 +114,22 @@ int fail(int code, const char* fmt, ...) {
             return fail(e_ == hipErrorOutOfMemory ? RCP_ENOMEM : RCP_EHIP, "%s: %s (%s:%d)", #expr, \
                         hipGetErrorString(e_), __FILE__, __LINE__);                          \
     } while (0)
+
+// Nothing may escape into the caller's process (an R session): every C++ exception that a
+// body can raise (std::bad_alloc from table building, std::system_error from threads) becomes
+// an RCP_E* code.
+#define RCP_TRY try {
+#define RCP_CATCH                                                                         \
+    }                                                                                     \
+    catch (const std::bad_alloc&) {                                                       \
+        return fail(RCP_ENOMEM, "host memory exhausted in %s", __func__);                 \
+    }                                                                                     \
+    catch (const std::exception& e_) {                                                    \
+        return fail(RCP_EINVAL, "%s: %s", __func__, e_.what());                          \
+    }                                                                                     \
+    catch (...) {                                                                         \
+        return fail(RCP_EINVAL, "%s: unexpected C++ exception", __func__);               \
+    }
 
 // Device buffer with RAII.
 struct DevBuf {
@@ -197,10 +210,12 @@ extern "C" const char* rcp_version(void) { return "recoup_amd 0.1.0 (gfx950)"; }
 extern "C" const char* rcp_last_error(void) { return g_err.c_str(); }
 
 extern "C" int rcp_device_count(int* n) {
+    RCP_TRY
     if (!n) return fail(RCP_EINVAL, "n is NULL");
     *n = 0;
     if (hipGetDeviceCount(n) != hipSuccess) *n = 0;
     return RCP_OK;
+    RCP_CATCH
 }
 
 namespace {
@@ -297,6 +312,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
 }  // namespace
 
 extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp_readset** out) {
+    RCP_TRY
     if (!d || !out) return fail(RCP_EINVAL, "NULL argument");
     *out = nullptr;
     int rc = check_device(d->device);
@@ -343,20 +359,25 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     HIP_TRY(hipStreamSynchronize(s));
     *out = rs.release();
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_readset_destroy(rcp_readset* rs) {
+    RCP_TRY
     if (!rs) return RCP_OK;
     DeviceGuard g(rs->device);
     delete rs;
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_readset_info(const rcp_readset* rs, int64_t* n_reads, int64_t* stream_off) {
+    RCP_TRY
     if (!rs) return fail(RCP_EINVAL, "NULL readset");
     if (n_reads) *n_reads = rs->n;
     if (stream_off) std::memcpy(stream_off, rs->stranded.h_stream_off.data(), 8 * rs->stranded.h_stream_off.size());
     return RCP_OK;
+    RCP_CATCH
 }
 
 // =====================================================================================
@@ -502,7 +523,19 @@ size_t put(std::vector<char>& blob, const std::vector<T>& v) {
 
 extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
                                rcp_plan** out) {
+    RCP_TRY
+    return rcp_plan_create_ex(rs, rows, bins, nullptr, out);
+    RCP_CATCH
+}
+
+extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
+                                  const rcp_plan_opts* opts, rcp_plan** out) {
+    RCP_TRY
     if (!rs || !rows || !out) return fail(RCP_EINVAL, "NULL argument");
+    const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, {0, 0, 0, 0, 0, 0}};
+    if (!opts) opts = &default_opts;
+    if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_LEAN_ANY)
+        return fail(RCP_EINVAL, "pileup_kernel = %d", opts->pileup_kernel);
     *out = nullptr;
     const rcp_bins_desc coverage_only{};  // bins == NULL: a calcCoverage-only plan
     const bool cov_only = bins == nullptr;
@@ -647,7 +680,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
             // wide binned chunks would be piled in several wave sub-chunks, each streaming the
             // chunk's reads again: split them into more (up to 8) column chunks instead -- more
             // workgroups for small row counts, and per-chunk read ranges from locate
-            const int32_t pos_max = env_int("RCP_CHUNK_POS", 1023);  // (tuning experiments)
+            const int32_t pos_max = 1023;
             if (!median && !pt.per_base && part_max_bin[p] > 0 && (int64_t)cb * part_max_bin[p] > pos_max) {
                 const int32_t cb2 = std::max<int32_t>(1, pos_max / part_max_bin[p]);
                 const int32_t nch2 = (pt.n_bins + cb2 - 1) / cb2;
@@ -713,14 +746,14 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     // ---- lean pileup kernel: every row one plain range (no exon list, no zero-width query),
     // mean of uniform power-of-two bins, each chunk inside one wave's fused pass (<= 1023
     // positions) and the stage inside the store waves' registers
-    // With RCP_LEAN=2 (opt-in), other plans take its general-bins mode (lean == 2): any uniform
-    // width, R-RNG layouts and multi-range rows, as long as every chunk is one wave's pass (no
-    // sub-chunks) and holds <= rcp_lean_gen_max_bins() bins.  Measured slower than the general
-    // kernel on C2 (0.082 vs 0.063 ms) and C3 (0.96 vs 0.88 ms), so off by default.  RCP_LEAN=0
-    // keeps every plan on the general kernel.
+    // With opts->pileup_kernel == RCP_KERNEL_LEAN_ANY, other plans take its general-bins mode
+    // (lean == 2): any uniform width, R-RNG layouts and multi-range rows, as long as every chunk
+    // is one wave's pass (no sub-chunks) and holds <= rcp_lean_gen_max_bins() bins.  Measured
+    // slower than the general kernel on C2 (0.082 vs 0.063 ms) and C3 (0.96 vs 0.88 ms), so
+    // AUTO does not choose it.  RCP_KERNEL_GENERAL keeps every plan on the general kernel.
     {
-        const int lean_env = env_int("RCP_LEAN", 1);
-        bool base = !cov_only && bins->stat == RCP_STAT_MEAN && P.chunk_cap <= 1023 && lean_env != 0;
+        const int kind = opts->pileup_kernel;
+        bool base = !cov_only && bins->stat == RCP_STAT_MEAN && P.chunk_cap <= 1023 && kind != RCP_KERNEL_GENERAL;
         for (int p = 0; base && p < P.n_parts; ++p) {
             const RcpPart& pt = P.part[p];
             const int64_t w = pt.per_base ? 1 : part_max_bin[p];
@@ -732,12 +765,12 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
             if (j1 - j0 > 1) lean = false;
             else if (j1 == j0 + 1 && (B.segs[j0].multi || !B.segs[j0].query_ok)) lean = false;
         }
-        const bool gen = !lean && base && lean_env >= 2 && stage_cap <= rcp_lean_gen_max_bins();
+        const bool gen = !lean && base && kind == RCP_KERNEL_LEAN_ANY && stage_cap <= rcp_lean_gen_max_bins();
         P.lean = lean ? 1 : (gen ? 2 : 0);
     }
 
     // ---- skewed rows: heavy slots sized for the eligible (short enough) rows
-    const int32_t heavy_thr = env_int("RCP_HEAVY_THRESHOLD", kHeavyThreshold);
+    const int32_t heavy_thr = opts->heavy_threshold < 0 ? kHeavyThreshold : opts->heavy_threshold;
     int32_t eligible_len = 0;
     for (int r = 0; r < R; ++r)
         if (B.row_len[r] <= kHeavyMaxLen) eligible_len = std::max(eligible_len, B.row_len[r]);
@@ -829,7 +862,7 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
     // C2 / C4 / C5), when no part of that length has an R-RNG layout: the same arithmetic as
     // the kernel's chunk_window, once per plan instead of once per (row, chunk)
     P.cw_len = -1;
-    if (keep_crange && R > 0 && env_int("RCP_CW_TABLE", 1)) {
+    if (keep_crange && R > 0) {
         const int32_t nr = B.row_len[0];
         bool ok = true;
         int c = 0;
@@ -903,40 +936,34 @@ extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows,
         int tile = 16, rmax = 4;
         rcp_tile_geometry(&tile, &rmax);
         int cus = 256;
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, rs->device) != hipSuccess || cus <= 0)
             cus = 256;
+        P.n_cus = cus;
         P.rounds = std::min(rmax, 2);
         while (P.rounds > 1 &&
                (int64_t)((R + tile * P.rounds - 1) / (tile * P.rounds)) * P.n_chunks_total < 2 * (int64_t)cus)
             P.rounds /= 2;
-        P.rounds = std::max(1, std::min(rmax, env_int("RCP_ROUNDS", P.rounds)));
         plan->tile_rows = P.lean ? rcp_tile_rows() : tile * P.rounds;
     }
     plan->grid = (int64_t)((R + plan->tile_rows - 1) / plan->tile_rows) * P.n_chunks_total;
-    // locate: one lane per row when every row is one range in the merged layout and its
-    // searches (bounds + interior chunk edges) fit one lockstep round of 8
-    {
-        bool one = rows->ignore_strand && 2 + 2 * P.n_chunks_total <= 8;
-        for (int r = 0; one && r < R; ++r)
-            if (B.row_seg[r + 1] - B.row_seg[r] > 1) one = false;
-        P.loc_lpr = (one && env_int("RCP_LOC_LPR", 4) == 1) ? 1 : 4;
-    }
     if (plan->lds > 160 * 1024) return fail(RCP_EUNSUPPORTED, "plan needs %zu B of LDS", plan->lds);
     HIP_TRY(hipMemset(plan->work.p, 0, plan->work.bytes));
     *out = plan.release();
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_plan_destroy(rcp_plan* plan) {
+    RCP_TRY
     if (!plan) return RCP_OK;
     DeviceGuard g(plan->rs->device);
     delete plan;
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info) {
+    RCP_TRY
     if (!plan || !info) return fail(RCP_EINVAL, "NULL argument");
     info->n_cols = plan->n_cols;
     info->n_segments = plan->n_seg;
@@ -948,15 +975,19 @@ extern "C" int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info) {
     info->pileup_kernel = plan->dev.lean;
     info->reserved = 0;
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_plan_row_lengths(const rcp_plan* plan, int64_t* out_len) {
+    RCP_TRY
     if (!plan || !out_len) return fail(RCP_EINVAL, "NULL argument");
     std::memcpy(out_len, plan->row_len.data(), 8 * plan->row_len.size());
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_stream) {
+    RCP_TRY
     if (!plan) return fail(RCP_EINVAL, "NULL plan");
     DeviceGuard g(plan->rs->device);
     HIP_TRY(g.err);
@@ -966,10 +997,12 @@ extern "C" int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_str
     HIP_TRY(rcp_launch_exec_reset(&Q, s));
     HIP_TRY(rcp_launch_locate(&Q, s));
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d_valid, int64_t* d_binsum,
                                        void* hip_stream, int stages) {
+    RCP_TRY
     if (!plan) return fail(RCP_EINVAL, "NULL plan");
     if (plan->dev.n_parts == 0) return fail(RCP_EINVAL, "coverage-only plan (created with bins == NULL)");
     if (!d_out && plan->n_rows && plan->n_cols) return fail(RCP_EINVAL, "NULL output");
@@ -988,14 +1021,18 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
     if (stages & RCP_STAGE_PILEUP) HIP_TRY(rcp_launch_pileup(&plan->dev, d_out, d_binsum, 0, s));
     if (stages & RCP_STAGE_INTERP) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_plan_execute(rcp_plan* plan, double* d_out, uint8_t* d_valid, int64_t* d_binsum,
                                 void* hip_stream) {
+    RCP_TRY
     return rcp_plan_execute_stages(plan, d_out, d_valid, d_binsum, hip_stream, RCP_STAGE_ALL);
+    RCP_CATCH
 }
 
 extern "C" int rcp_plan_status(rcp_plan* plan, void* hip_stream) {
+    RCP_TRY
     if (!plan) return fail(RCP_EINVAL, "NULL plan");
     DeviceGuard g(plan->rs->device);
     HIP_TRY(g.err);
@@ -1008,10 +1045,12 @@ extern "C" int rcp_plan_status(rcp_plan* plan, void* hip_stream) {
     if (st & RCP_STATUS_INTERP) return fail(RCP_EUNSUPPORTED, "internal plan/layout mismatch (status %u)", st);
     if (st & RCP_STATUS_OVERFLOW) return fail(RCP_EUNSUPPORTED, "bin numerator exceeded 2^32");
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins, double* out,
                            uint8_t* row_valid) {
+    RCP_TRY
     rcp_plan* plan = nullptr;
     int rc = rcp_plan_create(rs, rows, bins, &plan);
     if (rc) return rc;
@@ -1029,10 +1068,12 @@ extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, con
     if (out && cells) HIP_TRY(hipMemcpy(out, d_out.p, 8 * cells, hipMemcpyDeviceToHost));
     if (row_valid && plan->n_rows) HIP_TRY(hipMemcpy(row_valid, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost));
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t* d_cov, uint8_t* d_valid,
                                  void* hip_stream) {
+    RCP_TRY
     if (!plan || !out_off) return fail(RCP_EINVAL, "NULL argument");
     DeviceGuard g(plan->rs->device);
     HIP_TRY(g.err);
@@ -1065,11 +1106,13 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
     HIP_TRY(hipStreamSynchronize(s));  // d_off is released on return
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int32_t* d_cov, int device,
                               int32_t* d_values, int32_t* d_lengths, int64_t* run_off, int64_t* n_runs,
                               void* hip_stream) {
+    RCP_TRY
     if (n_rows < 0 || !out_off || !run_off || !n_runs) return fail(RCP_EINVAL, "NULL argument");
     const int64_t n = out_off[n_rows];
     if (n < 0 || n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "%lld positions", (long long)n);
@@ -1102,6 +1145,7 @@ extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int3
     HIP_TRY(hipStreamSynchronize(s));
     *n_runs = nr;
     return RCP_OK;
+    RCP_CATCH
 }
 
 // =====================================================================================
@@ -1114,28 +1158,36 @@ struct rcp_rng {
 };
 
 extern "C" int rcp_rng_create(uint32_t seed, int kind, rcp_rng** out) {
+    RCP_TRY
     if (!out) return fail(RCP_EINVAL, "NULL argument");
     if (kind != RCP_RNG_REJECTION && kind != RCP_RNG_ROUNDING) return fail(RCP_EINVAL, "rng kind %d", kind);
     *out = new rcp_rng(seed, kind == RCP_RNG_ROUNDING);
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_rng_unif(rcp_rng* g, int64_t k, double* out) {
+    RCP_TRY
     if (!g || (k > 0 && !out)) return fail(RCP_EINVAL, "NULL argument");
     for (int64_t i = 0; i < k; ++i) out[i] = g->rng.unif_rand();
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_rng_sample_sorted(rcp_rng* g, int64_t n, int64_t k, int64_t* out) {
+    RCP_TRY
     if (!g || (k > 0 && !out)) return fail(RCP_EINVAL, "NULL argument");
     std::vector<int64_t> v;
     if (!g->rng.sample_sorted(n, k, g->rounding, &v))
         return fail(RCP_ESEMANTIC, "cannot take a sample larger than the population when 'replace = FALSE'");
     std::copy(v.begin(), v.end(), out);
     return RCP_OK;
+    RCP_CATCH
 }
 
 extern "C" int rcp_rng_free(rcp_rng* g) {
+    RCP_TRY
     delete g;
     return RCP_OK;
+    RCP_CATCH
 }

@@ -25,6 +25,10 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "rcp_device.h"
 
 namespace {
@@ -202,14 +206,8 @@ __device__ __forceinline__ void pileup_row(const RcpPlanDev& P, int r, int32_t P
 // batches of 256 candidates cross pair boundaries, so a row costs one round trip per 256
 // candidates with the next batch in flight while the current one is added.  The per-pair
 // data each candidate needs is picked by a scalar loop over the (few) pairs a batch spans.
-#ifndef RCP_ROW_WAVE
-#define RCP_ROW_WAVE 1
-#endif
 __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int32_t P0, int32_t npos, int32_t* diff,
                                                 int sh) {
-#ifdef RCP_ABL_RW_SKIP  // ablation: no reads at all for multi-range rows
-    return;
-#endif
     const int lane = threadIdx.x & 63;
     const int32_t P1 = P0 + npos;
     const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
@@ -301,13 +299,9 @@ __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int3
                 o.nb_hi = __builtin_amdgcn_readlane(sg.nb_hi, p);
                 const int32_t ps = __builtin_amdgcn_readlane(gps, p);
                 const int32_t pe = __builtin_amdgcn_readlane(gpe, p);
-#ifdef RCP_ABL_RW_NOADD  // ablation: reads loaded, not added
-                asm volatile("" ::"v"(rd[0].x), "v"(rd[1].x), "v"(rd[2].x), "v"(rd[3].x), "s"(ps), "s"(pe));
-#else
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     if (sel[u] == p && q0 + lane + 64u * u < N) add_read(P, o, rd[u], ps, pe, P0, diff, sh);
-#endif
                 m &= m - 1;
             }
         };
@@ -533,9 +527,6 @@ __device__ __forceinline__ uint32_t dir_bound_at(const RcpPlanDev& P, int64_t d0
     const int32_t* key = upper ? reinterpret_cast<const int32_t*>(P.se) : P.pmax;
     const int ksh = upper ? 1 : 0;                      // start of read m is word 2m of se
     const int64_t thr = (int64_t)v + (upper ? 1 : 0);  // start > v  <=>  start >= v + 1
-#ifdef RCP_ABL_SEARCH  // ablation: bucket lookup only
-    return upper ? hi : lo;
-#endif
     while (lo < hi) {
         const uint32_t m = lo + ((hi - lo) >> 1);
         if ((int64_t)key[(size_t)m << ksh] < thr) lo = m + 1; else hi = m;
@@ -557,11 +548,7 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0,
         up[u] = dst[u] == -1 || (dst[u] >= 0 && (dst[u] & 1));
         lo[u] = hi[u] = 0;
         thr[u] = (int64_t)v[u] + (up[u] ? 1 : 0);
-#ifdef RCP_ABL_NODIR  // ablation (locate timing): no directory / search loads
-        if (false) {
-#else
         if (u < cnt) {
-#endif
             const int32_t b = min(max(v[u], 0) >> P.dir_shift, nb - 1);
             const int32_t* dir = up[u] ? P.dir_u : P.dir_l;  // interleaved: stride 2
             lo[u] = (uint32_t)dir[2 * (d0 + b)];
@@ -602,21 +589,15 @@ __device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32
 // quad's lanes (one stream per segment in the merged layout, three in the stranded one), so
 // multi-range rows search in parallel; the quad then combines hits / max ends / candidate
 // counts with DPP.  For a single-range row the lanes also split the per-chunk range searches.
-// LPR = 1 (plans of single-range rows in the merged layout with <= 8 searches per row: C4,
-// C2): one lane per row runs all its searches in one lockstep round -- the same dependent
-// chain with a quarter of the waves and none of the quad's duplicated integer work.
 // Every search is bounded by the bucket directory and independent of the others: the
 // dependent chain per lane is one bucket search, not a sequence of them.
 #ifndef RCP_LOC_WPE
 #define RCP_LOC_WPE 1
 #endif
-template <int LPR>
 __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlanDev P) {
-    constexpr int KS = LPR == 1 ? 8 : 4;  // searches of one lockstep round
+    constexpr int LPR = 4;                 // lanes per row (a quad)
+    constexpr int KS = 4;                  // searches of one lockstep round
     __shared__ uint32_t xres[kBlock / LPR][2 * RCP_MAX_CRANGE_CHUNKS];  // per row: chunk bounds
-#ifdef RCP_ABL_LOC_EMPTY  // ablation (locate timing): launch and dispatch only
-    if (P.n_rows >= 0) return;
-#endif
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = t / LPR;
     const int q = t % LPR;
@@ -635,10 +616,6 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
             for (int u = 0; u < (int)(sizeof(RcpRowInfo) / 16); ++u) d[u] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
-#ifdef RCP_ABL_LOC_RIONLY  // ablation (locate timing): the record load and one store only
-    if (in_row && (t & 3) == 0) P.ncand[r] = (uint32_t)(ri.j0 + ri.j1 + ri.chrom + ri.row_len + ri.nb + ri.seg0.lo);
-    return;
-#endif
     const int j0 = ri.j0, j1 = ri.j1;
     const int32_t chrom = in_row ? ri.chrom : -1;
     const bool ok = in_row && !ri.stat && chrom >= 0 && chrom < P.n_chrom && j1 > j0;
@@ -665,13 +642,11 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
     auto piece = [&](int c, int32_t* gps, int32_t* gpe, bool* empty) -> bool {
         int32_t p0, np;
         *empty = false;
-#ifndef RCP_NO_CW_TABLE
         if (nr == P.cw_len) {  // the plan's common row length: windows tabulated on the host
             np = P.cw[2 * c + 1];
             if (np < 0) return false;
             p0 = P.cw[2 * c];
         } else
-#endif
         {
             int p = 0, cp = c;
             while (p < P.n_parts - 1 && cp >= P.part[p].n_chunks) {
@@ -710,7 +685,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         int32_t sx[KS] = {};
         int sdst[KS] = {};  // -2 lower, -1 upper, >= 0 xr index (its parity = upper)
         int cnt = 0;
-        uint32_t v = 0, v_up = 0;  // LPR 1: the lane's own lower and upper bound
+        uint32_t v = 0;
         // up to 4 searches bisect in lockstep (one chain of dependent loads for all of them:
         // C2 has 8 searches per row -> 2 per lane, C5 16 -> 4); a 5th starts a second round
         auto run = [&]() {
@@ -720,7 +695,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
             for (int u = 0; u < KS; ++u)
                 if (u < cnt) {
                     if (sdst[u] == -2) v = w[u];
-                    else if (sdst[u] == -1) { if (LPR == 1) v_up = w[u]; else v = w[u]; }
+                    else if (sdst[u] == -1) v = w[u];
                     else xr[sdst[u]] = w[u];
                 }
             cnt = 0;
@@ -734,11 +709,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
             } else {
                 int32_t gps = 0, gpe = 0;
                 bool empty;
-#ifdef RCP_ABL_NOPIECE  // ablation (locate timing): no chunk-window arithmetic
-                if (task < -100 && piece(task >> 1, &gps, &gpe, &empty)) {
-#else
                 if (piece(task >> 1, &gps, &gpe, &empty)) {
-#endif
                     need = (task & 1) ? gpe < sg0.hi : gps > sg0.lo;  // a row end: the row's own bound
                     x = (task & 1) ? gpe : gps;
                 }
@@ -753,13 +724,8 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
             if (++cnt == KS) run();
         }
         if (cnt) run();
-        if (LPR == 1) {
-            lo = v;
-            hi = max(lo, v_up);
-        } else {
-            lo = (uint32_t)qperm<0x00>((int)v);
-            hi = max(lo, (uint32_t)qperm<0x55>((int)v));
-        }
+        lo = (uint32_t)qperm<0x00>((int)v);
+        hi = max(lo, (uint32_t)qperm<0x55>((int)v));
         if (lo < hi) {
             hit = 1u << g;
             if (sl < 0 && q == 0) maxend[g] = P.pmax[hi - 1];
@@ -795,7 +761,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         // plan zeroed them; no read lives there)
     }
     // ---- combine the quad (all lanes active: DPP reads neighbours)
-    if (LPR == 4) {
+    {
         hit |= (uint32_t)qperm<0xB1>((int)hit);
         hit |= (uint32_t)qperm<0x4E>((int)hit);
         present |= (uint32_t)qperm<0xB1>((int)present);
@@ -812,9 +778,9 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
     }
     // the single range of a fast row: (lo, hi) of pairs 0, 1, 2 sit in lanes 0, 1, 2 (LPR 1:
     // the merged layout's one pair, in the lane itself)
-    const uint32_t lo0 = LPR == 1 ? lo : (uint32_t)qperm<0x00>((int)lo), hi0 = LPR == 1 ? hi : (uint32_t)qperm<0x00>((int)hi);
-    const uint32_t lo1 = LPR == 1 ? 0u : (uint32_t)qperm<0x55>((int)lo), hi1 = LPR == 1 ? 0u : (uint32_t)qperm<0x55>((int)hi);
-    const uint32_t lo2 = LPR == 1 ? 0u : (uint32_t)qperm<0xAA>((int)lo), hi2 = LPR == 1 ? 0u : (uint32_t)qperm<0xAA>((int)hi);
+    const uint32_t lo0 = (uint32_t)qperm<0x00>((int)lo), hi0 = (uint32_t)qperm<0x00>((int)hi);
+    const uint32_t lo1 = (uint32_t)qperm<0x55>((int)lo), hi1 = (uint32_t)qperm<0x55>((int)hi);
+    const uint32_t lo2 = (uint32_t)qperm<0xAA>((int)lo), hi2 = (uint32_t)qperm<0xAA>((int)hi);
     bool valid = ok;
     if (ok) {
         for (int g = 0; g < 4; ++g) {
@@ -845,7 +811,7 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
         }
         P.heavy_slot[r] = slot;
     }
-    if (LPR == 4) slot = qperm<0x00>(slot);
+    slot = qperm<0x00>(slot);
     const bool cr = P.crange != nullptr && fast && valid && slot < 0;
     if (cr && ns == 1) {
         // merged layout: the interior edges were searched with the row's bounds (xr)
@@ -900,9 +866,6 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
     }
     const uint4* src = reinterpret_cast<const uint4*>(&rec);
     uint4* dst = reinterpret_cast<uint4*>(P.rec + r);
-#ifdef RCP_ABL_NOREC  // ablation (locate timing): no record writes (rows read as NULL)
-    if (r >= 0) return;
-#endif
 #pragma unroll
     for (int u = 0; u < 4; ++u) dst[u] = src[u];
 }
@@ -1044,9 +1007,6 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) 
 #ifndef RCP_PILE_WAVES
 #define RCP_PILE_WAVES 8
 #endif
-#ifndef RCP_GEN_DYN  // dynamic row dealing in the general kernel: measured slower (C3 pileup 0.95
-#define RCP_GEN_DYN 0   // vs 0.88 ms, C2 0.072 vs 0.063: 16 VGPRs spilled at the 128 cap vs 5), off
-#endif
 #ifndef RCP_PILE_ROUNDS
 #define RCP_PILE_ROUNDS 4
 #endif
@@ -1101,10 +1061,6 @@ __device__ __forceinline__ uint32_t fast_index(const RowMeta& m, uint32_t q) {
 // the read's first covered base and of the base after its last are one add each.
 template <bool REV>
 __device__ __forceinline__ void add_read_fast_t(const RowMeta& m, int2 rd, int32_t* diff, int sh) {
-#ifdef RCP_ABL_ATOMICS  // ablation build (tools/ablate.sh): loads kept, no LDS atomics
-    asm volatile("" ::"v"(rd.x), "v"(rd.y));
-    return;
-#endif
     if (rd.y < m.gps || rd.x > m.gpe) return;
     const int32_t x0 = max(rd.x, m.gps);
     const int32_t x1 = min(rd.y, m.gpe);
@@ -1123,10 +1079,6 @@ __device__ __forceinline__ void add_read_fast_t(const RowMeta& m, int2 rd, int32
 }
 
 __device__ __forceinline__ void add_read_fast(const RowMeta& m, int2 rd, int32_t* diff, int sh) {
-#ifdef RCP_ABL_ATOMICS  // ablation build (tools/ablate.sh): loads kept, no LDS atomics
-    asm volatile("" ::"v"(rd.x), "v"(rd.y));
-    return;
-#endif
     if (rd.y < m.gps || rd.x > m.gpe) return;
     const int32_t x0 = max(rd.x, m.gps);
     const int32_t x1 = min(rd.y, m.gpe);
@@ -1147,13 +1099,9 @@ __device__ __forceinline__ void add_read_fast(const RowMeta& m, int2 rd, int32_t
 // epilogue (and every prefetched read) would have to land before the barrier.  The pileup
 // kernel's waves share nothing through global memory, so LDS ordering is enough.
 __device__ __forceinline__ void lds_barrier() {
-#ifdef RCP_FULL_BARRIER
-    __syncthreads();
-#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#endif
 }
 
 __device__ __forceinline__ void lds_order() {
@@ -1226,11 +1174,7 @@ __device__ __forceinline__ void scan_bins_fast(int32_t* diff, int lbs, uint32_t*
 
 // write-once output: non-temporal stores keep the reads' lines in L2 / MALL
 __device__ __forceinline__ void out_store(double x, double* p) {
-#ifdef RCP_STORE_PLAIN
-    *p = x;
-#else
     __builtin_nontemporal_store(x, p);
-#endif
 }
 
 // Row metadata of row r for column chunk (part, k0, cidx), from the locate kernel's 64-byte
@@ -1382,11 +1326,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     [[maybe_unused]] const int n_steps = kRowsPerWave * rounds;
     auto prefetch = [&](int i, int2* dst) {
         const RowMeta m = uniform_meta(meta[i]);
-#ifdef RCP_ABL_LOADS
-        const uint32_t n = 0;
-#else
         const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
-#endif
         if (n) {  // wave-uniform
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -1445,10 +1385,6 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
                 const uint4 q = *reinterpret_cast<const uint4*>(st);
                 const double x[4] = {((double)q.x * sc) * rdd, ((double)q.y * sc) * rdd,
                                      ((double)q.z * sc) * rdd, ((double)q.w * sc) * rdd};
-#ifdef RCP_ABL_STORES  // ablation: barriers and stage reads kept, no global stores
-                asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
-                continue;
-#endif
                 put4(k, o, x);
             }
         } else if (MEDIAN || lay < 0) {
@@ -1529,11 +1465,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
                     carry = wave_sum(carry);
                     for (int q = lane; q <= sn; q += 64) diff[lp(q, sh)] = g[base + q] + (q == 0 ? carry : 0);
                 } else if (m.fast && whole) {
-#ifdef RCP_ABL_LOADS
-                    const uint32_t n = 0;
-#else
                     const uint32_t n = fast_candidates(m);
-#endif
                     // batch q0 + 256 is loaded while batch q0 is added
                     for (uint32_t q0 = 0; q0 < n; q0 += 256) {
                         int2 nx[4];
@@ -1557,29 +1489,19 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
                         for (int u = 0; u < 4; ++u) cur[u] = nx[u];
                     }
                 } else {
-#if RCP_ROW_WAVE
                     pileup_row_wave(P, r, m.P0 + s0, sn, diff, sh);
-#else
-                    pileup_row(P, r, m.P0 + s0, sn, diff, lane, 64, sh);
-#endif
                 }
                 lds_order();
                 if (!MEDIAN && !CSR && fast_bins) {
                     uint32_t* srow = sbuf + ii * RS;
                     const int lbs = 31 - __clz(bs);
-#ifdef RCP_ABL_SCAN
-                    if (lane == 0) srow[0] = (uint32_t)lbs;
-                    continue;
-#endif
                     if (sh == 2) scan_bins_fast<4>(diff, lbs, srow, kend - k0);
                     else if (sh == 3) scan_bins_fast<8>(diff, lbs, srow, kend - k0);
                     else scan_bins_fast<16>(diff, lbs, srow, kend - k0);
                     lds_order();
                     continue;
                 }
-#ifndef RCP_ABL_SCAN
                 scan_wave<!(MEDIAN || CSR)>(diff, per);
-#endif
                 lds_order();
                 if (CSR) {
                     for (int32_t k = k0 + s0 + lane; k < k0 + s0 + sn; k += 64)
@@ -1607,16 +1529,11 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
                     const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
                     int32_t a = lane * bs;
                     uint32_t* st = sbuf + ii * RS + lane;
-#ifndef RCP_ABL_BINS
                     for (int32_t k = k0 + lane; k < kend; k += 64, a += 64 * bs, st += 64)
                         *st = cum[lp(a + bs - 1, sh)] - cum[lp(a - 1, sh)];
-#endif
                 } else if (whole) {
                     // splitVector layout: enlarged bins from set.seed(42); sample(1:n, dif)
                     const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
-#ifdef RCP_ABL_BINS
-                    if (lane < 64) continue;
-#endif
                     for (int32_t k = k0 + lane; k < kend; k += 64) {
                         const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
                         const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
@@ -1637,51 +1554,17 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
             }
         }
     };
-#if RCP_GEN_DYN
-    // rows dealt dynamically, as in the lean kernel: a wave takes the next row number from an
-    // LDS counter when it starts its current row and prefetches it; a round ends when its T
-    // rows are taken and piled (a static 2 rows per wave waited for the round's slowest pair)
-    static_assert(kPWaves <= T, "pending rows of one round fit the next round");
-    auto take = [&]() -> uint32_t {
-        uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(ctr, 1u);
-        return __builtin_amdgcn_readfirstlane(v);
-    };
-    uint32_t g = take();  // this wave's pending row
-    bool in_a = true;     // its first reads sit in bufA (else bufB)
-    if (g < (uint32_t)rows_wg) prefetch((int)g, bufA);
-#else
     auto pile_step = [&](int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
         if (step + 1 < n_steps) prefetch(row_of(step + 1), nxt);
         pile_row(row_of(step), cur);
     };
     prefetch(row_of(0), bufA);
-#endif
     for (int rd = 0; rd < rounds; ++rd) {
-#if RCP_GEN_DYN
-        const uint32_t lim = (uint32_t)(T * (rd + 1));
-        while (g < lim) {
-            const uint32_t gn = take();
-            if (in_a) {
-                if (gn < (uint32_t)rows_wg) prefetch((int)gn, bufB);
-                pile_row((int)g, bufA);
-            } else {
-                if (gn < (uint32_t)rows_wg) prefetch((int)gn, bufA);
-                pile_row((int)g, bufB);
-            }
-            in_a = !in_a;
-            g = gn;
-        }
-#else
         for (int s2 = 0; s2 < kRowsPerWave; s2 += 2) {
             pile_step(rd * kRowsPerWave + s2, bufA, bufB);
             pile_step(rd * kRowsPerWave + s2 + 1, bufB, bufA);
         }
-#endif
         if (CSR) continue;
-#ifdef RCP_ABL_EPI
-        continue;
-#endif
         if (kStageBufs == 2) {
             // double-buffered stage: round rd - 1 is written while other waves still pile
             // round rd; one barrier per round; the last round is written after the loop
@@ -1726,9 +1609,6 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
 #endif
 // 1: three batches of reads in flight per row instead of two (measured neutral on C4 / C5 /
 // C3, tools/ab_variants.sh: kept as a build option, off by default)
-#ifndef RCP_LRING3
-#define RCP_LRING3 0
-#endif
 #ifndef RCP_LWPE
 #define RCP_LWPE 6
 #endif
@@ -1861,9 +1741,6 @@ constexpr int kLMaxPassGen = 4;  // general-bins mode: <= 4 * kLQuads * 4 = 256 
 #ifndef RCP_LWPE_GEN
 #define RCP_LWPE_GEN RCP_LWPE
 #endif
-#ifndef RCP_LEAN_DYN
-#define RCP_LEAN_DYN 1
-#endif
 template <int MAXPER, bool GEN>
 __global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(GEN ? RCP_LWPE_GEN : RCP_LWPE)))
 rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
@@ -1889,13 +1766,11 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         int xs = xcd;
         if (lane == 0) j = atomicAdd(&P.status[8 + xcd], 1u);
         j = __builtin_amdgcn_readfirstlane(j);
-#ifndef RCP_LEAN_NO_STEAL
         for (int k = 1; k < 8 && j >= n_items_of(xs); ++k) {
             xs = (xcd + k) & 7;
             if (lane == 0) j = atomicAdd(&P.status[8 + xs], 1u);
             j = __builtin_amdgcn_readfirstlane(j);
         }
-#endif
         int code = -1;
         if (j < n_items_of(xs)) {
             const int tl = (int)(j / P.n_chunks_total);
@@ -1919,11 +1794,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         [[maybe_unused]] auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
         auto prefetch = [&](const LeanMeta& mm, int2* dst) {
             const LeanRow m = lean_row(mm);
-#ifdef RCP_LABL_NOREAD
-            const uint32_t n = 0;
-#else
             const uint32_t n = (m.flag == 0 && m.fast) ? lean_candidates(m) : 0;
-#endif
             if (n) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
@@ -1964,11 +1835,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 // several ranges (exon list): the wave streams the row's (segment, stream) pairs
                 pileup_row_wave(P, it.tile * kRows + i, m.P0, npos, diff, sh);
             } else {
-#ifdef RCP_LABL_NOREAD  // ablation: no read loads / LDS adds
-                const uint32_t n = 0;
-#else
                 const uint32_t n = lean_candidates(m);
-#endif
                 // batches of 256 reads, three in flight: `cur` (prefetched with the previous
                 // row), b1, b2; the loop is unrolled over the ring so no buffer is copied
                 auto load_batch = [&](uint32_t q0, int2 (&dst)[4]) {
@@ -2003,25 +1870,6 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                             if (q0 + lane + 64u * u < n) lean_add<false>(m, src[u], diff, sh);
                     }
                 };
-#if RCP_LRING3
-                if (n <= 256) {
-                    add_batch(0, cur);
-                } else {
-                    int2 b1[4], b2[4];
-                    load_batch(256, b1);
-                    load_batch(512, b2);
-                    for (uint32_t q0 = 0; q0 < n; q0 += 768) {
-                        add_batch(q0, cur);
-                        load_batch(q0 + 768, cur);
-                        if (q0 + 256 >= n) break;
-                        add_batch(q0 + 256, b1);
-                        load_batch(q0 + 1024, b1);
-                        if (q0 + 512 >= n) break;
-                        add_batch(q0 + 512, b2);
-                        load_batch(q0 + 1280, b2);
-                    }
-                }
-#else
                 for (uint32_t q0 = 0; q0 < n; q0 += 256) {
                     int2 nx[4];
                     load_batch(q0 + 256, nx);
@@ -2029,7 +1877,6 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) cur[u] = nx[u];
                 }
-#endif
             }
             lds_order();
             uint32_t* srow = stage + (i & (T - 1)) * RS;
@@ -2064,7 +1911,6 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             lds_order();
         };
         int2 bufA[4], bufB[4];
-#if RCP_LEAN_DYN
         // Rows are dealt dynamically: a wave takes the workgroup's next row number g from an
         // LDS counter (rows 64 q .. 64 q + 63 = the q-th item of this workgroup, 16 per round)
         // when it starts its current row, and prefetches g's first reads.  A round ends when
@@ -2114,31 +1960,6 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             buf ^= 1;
             code = item[buf];
         }
-#else
-        auto pile_step = [&](const LeanItem& it, int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
-            if (step + 1 < kSteps) {
-                prefetch(lmeta[buf * kRows + row_of(step + 1)], nxt);
-            } else {
-                const int nc = item[buf ^ 1];  // published by store wave 0 rounds ago
-                if (nc >= 0) prefetch(lmeta[(buf ^ 1) * kRows + row_of(0)], nxt);
-            }
-            pile_row(it, row_of(step), cur);
-        };
-        if (code >= 0) prefetch(lmeta[row_of(0)], bufA);
-        while (code >= 0) {
-            const LeanItem it = lean_item(P, code);
-            for (int rd = 0; rd < kRounds; ++rd) {
-                for (int s2 = 0; s2 < kRowsPerWave; s2 += 2) {
-                    pile_step(it, rd * kRowsPerWave + s2, bufA, bufB);
-                    pile_step(it, rd * kRowsPerWave + s2 + 1, bufB, bufA);
-                }
-                lds_barrier();  // A: the round's stage rows are complete
-                lds_barrier();  // B: the store waves hold them in registers
-            }
-            buf ^= 1;
-            code = item[buf];
-        }
-#endif
     } else {
         // ================= store waves: thread (row ii, column quad qd)
         const int st = tid - 64 * kPWaves;
@@ -2207,10 +2028,6 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                             x[2] = ((double)v[j].z * scf) * rdd;
                             x[3] = ((double)v[j].w * scf) * rdd;
                         }
-#ifdef RCP_LABL_NOSTORE  // ablation: stage copied and converted, no global stores
-                        asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(oj));
-                        continue;
-#endif
                         if (kStep * j + 3 < nk) {
 #pragma unroll
                             for (int u = 0; u < 4; ++u) out_store(x[u], oj + u * R);
@@ -2275,11 +2092,7 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
     // 1-based i = 2 .. n-1 (0-based i - 1): c[i] = (y[i+1] - y[i]) - (y[i] - y[i-1])
     for (int i = 1 + t; i < n - 1; i += blockDim.x) c[i] = (y[i + 1] - y[i]) - (y[i] - y[i - 1]);
     __syncthreads();
-#ifdef RCP_IABL_NOSPLINE  // ablation: no serial recurrences
-    if (t == 0 && n < 0) {
-#else
     if (t == 0) {
-#endif
         double c1 = 0.0, cn = 0.0;
         if (n > 3) {
             c1 = c[2] / 2.0 - c[1] / 2.0;
@@ -2493,9 +2306,7 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
         if (threadIdx.x == 0) atomicOr(P.status, RCP_STATUS_INTERP);
         return;
     }
-#ifndef RCP_IABL_NOWIN
     block_window_depth(P, r, head, L, diff, scratch);
-#endif
     // the spline / fill works on LDS copies (global scratch only for huge rows)
     double* x = P.interp_lds >= 0 ? reinterpret_cast<double*>(smem + P.interp_lds)
                                   : P.interp_scratch + (size_t)e * P.interp_stride;
@@ -2562,32 +2373,39 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
 // host-callable launchers
 // =================================================================================
 namespace {
+// hipFuncSetAttribute acts on the function object of the CURRENT device, so the 160 KB
+// dynamic-LDS opt-in is made once per (kernel, device); host threads driving different GPUs
+// (rcp_profile_multi) may launch concurrently.
+hipError_t allow_big_lds_fn(const void* fn) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count({fn, dev})) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e == hipSuccess) done.insert({fn, dev});
+    return e;
+}
 template <class K>
 hipError_t allow_big_lds(K kernel) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024);
+    return allow_big_lds_fn(reinterpret_cast<const void*>(kernel));
 }
 }  // namespace
 
 extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream) {
     if (P->n_rows == 0) return hipSuccess;
-    if (P->loc_lpr == 1) {
-        const int64_t grid = ((int64_t)P->n_rows + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL(rcp_locate_kernel<1>, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
-    } else {
-        const int64_t grid = (4 * (int64_t)P->n_rows + kBlock - 1) / kBlock;  // four lanes per row
-        hipLaunchKernelGGL(rcp_locate_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
-    }
+    const int64_t grid = (4 * (int64_t)P->n_rows + kBlock - 1) / kBlock;  // four lanes per row
+    hipLaunchKernelGGL(rcp_locate_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
     return hipGetLastError();
 }
 
 extern "C" hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_t stream) {
     if (P->n_rows == 0 || P->heavy_threshold <= 0) return hipSuccess;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = allow_big_lds(rcp_heavy_pileup_kernel);
+    {
+        const hipError_t e = allow_big_lds(rcp_heavy_pileup_kernel);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     // difference array of one row + the slots' slice offsets
     const size_t lds = 4 * (16 + (size_t)P->heavy_max_len + 1 + 64) + 4 * ((size_t)P->heavy_cap + 1);
@@ -2626,23 +2444,15 @@ extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
 
 template <int MAXPER, bool GEN>
 static hipError_t launch_pileup_lean_t(const RcpPlanDev* P, double* out, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = allow_big_lds(rcp_pileup_lean_kernel<MAXPER, GEN>);
+    {
+        const hipError_t e = allow_big_lds(rcp_pileup_lean_kernel<MAXPER, GEN>);
         if (e != hipSuccess) return e;
-        attr_set = true;
     }
     // [pile waves' difference arrays | one stage | row metadata x 2 | item codes x 2]
     const size_t lds = rcp_pileup_lean_lds_bytes(P);
     // persistent: as many workgroups as fit at once (LDS: two per CU), a multiple of 8
     // (workgroup b serves XCD b % 8), never more than there are work items
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e != hipSuccess) return e;
-    }
+    const int cus = std::max(1, P->n_cus);  // of the plan's device (rcp_plan_create)
     const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
     const int tiles = (P->n_rows + kRows - 1) / kRows;
     const int64_t items = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
@@ -2667,11 +2477,9 @@ static hipError_t launch_pileup_lean(const RcpPlanDev* P, double* out, hipStream
 
 template <bool MEDIAN, bool CSR>
 static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* binsum, size_t lds, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = allow_big_lds(rcp_pileup_kernel<MEDIAN, CSR>);
+    {
+        const hipError_t e = allow_big_lds(rcp_pileup_kernel<MEDIAN, CSR>);
         if (e != hipSuccess) return e;
-        attr_set = true;
     }
     const int rows_wg = kTile * P->rounds;
     const int tiles = (P->n_rows + rows_wg - 1) / rows_wg;
@@ -2705,11 +2513,9 @@ extern "C" size_t rcp_interp_lds_bytes(const RcpPlanDev* P) {
 
 extern "C" hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStream_t stream) {
     if (P->n_interp == 0) return hipSuccess;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = allow_big_lds(rcp_interp_kernel);
+    {
+        const hipError_t e = allow_big_lds(rcp_interp_kernel);
         if (e != hipSuccess) return e;
-        attr_set = true;
     }
     RcpPlanDev Q = *P;
     Q.interp_lds = interp_in_lds(P) ? (int32_t)((interp_int_bytes(P) + 15) / 16 * 16) : -1;

@@ -20,6 +20,7 @@ STRAND = {"+": 0, "-": 1, "*": 2}
 STAT = {"mean": 0, "median": 1}
 INTERP = {"auto": 0, "spline": 1, "linear": 2, "neighborhood": 3}
 RNG = {"Rejection": 0, "Rounding": 1}
+KERNEL = {"auto": 0, "general": 1, "lean_any": 2}
 
 
 def _stream(device, stream):
@@ -145,15 +146,19 @@ class Bins:
 class Plan:
     """One fused coverage -> profile pass of ``rows`` over ``readset`` with ``bins``."""
 
-    def __init__(self, readset, rows, bins):
+    def __init__(self, readset, rows, bins, kernel="auto", heavy_threshold=-1):
+        """``kernel``: "auto" | "general" | "lean_any" (rcp_plan_opts.pileup_kernel; every choice
+        gives bit-identical results); ``heavy_threshold``: -1 default, 0 off."""
         self.readset = readset  # keeps the device reads alive
         self.rows = rows
         self.bins = bins
         rd = rows.desc()
         bd = ctypes.byref(bins.desc()) if bins is not None else None
+        opts = _lib.PlanOpts(KERNEL[kernel] if isinstance(kernel, str) else int(kernel), int(heavy_threshold))
         h = ctypes.c_void_p()
         with torch.cuda.device(readset.device):
-            check(_lib.lib().rcp_plan_create(readset.h, ctypes.byref(rd), bd, ctypes.byref(h)))
+            check(_lib.lib().rcp_plan_create_ex(readset.h, ctypes.byref(rd), bd, ctypes.byref(opts),
+                                                ctypes.byref(h)))
         self.h = h
         info = _lib.PlanInfo()
         check(_lib.lib().rcp_plan_info_get(self.h, ctypes.byref(info)))

@@ -2,10 +2,9 @@
 
 Plans whose rows are all one plain range with uniform power-of-two bins take the lean kernel
 (plan info "pileup_kernel" == 1); other mean plans whose chunks fit one wave pass take its
-general-bins mode (2: any bin width, R-RNG layouts, exon lists) when opted in (RCP_LEAN=2).  Each case checks it against the CPU oracle (validity and
+general-bins mode (2: any bin width, R-RNG layouts, exon lists) when opted in (kernel="lean_any").  Each case checks it against the CPU oracle (validity and
 means as in test_gpu_random: integer numerators exact, means within 1e-12 relative) and
-bit-for-bit against the general kernel on the same plan (RCP_LEAN=0)."""
-import os
+bit-for-bit against the general kernel on the same plan (kernel="general")."""
 
 import numpy as np
 import pytest
@@ -15,23 +14,14 @@ from tests.test_gpu_random import CHROM_LEN, check, make_reads, single_rows
 pytestmark = pytest.mark.gpu
 
 
-def plans(reads, seqlen, rows, bins, strand_filter=None, lean_mode=None):
+def plans(reads, seqlen, rows, bins, strand_filter=None, lean_mode=None, heavy_threshold=-1):
     """(lean result, general result, lean kernel id, expected) for one configuration;
-    lean_mode "2" opts in to the general-bins mode."""
+    lean_mode "lean_any" opts in to the general-bins mode."""
     from recoup_amd.engine import Plan, ReadSet
     from tests import oracle_rows
     rs = ReadSet(*reads, seqlen, device=0, strand_filter=strand_filter)
-    if lean_mode:
-        os.environ["RCP_LEAN"] = lean_mode
-    try:
-        lean = Plan(rs, rows, bins)
-    finally:
-        os.environ.pop("RCP_LEAN", None)
-    os.environ["RCP_LEAN"] = "0"
-    try:
-        general = Plan(rs, rows, bins)
-    finally:
-        del os.environ["RCP_LEAN"]
+    lean = Plan(rs, rows, bins, kernel=lean_mode or "auto", heavy_threshold=heavy_threshold)
+    general = Plan(rs, rows, bins, kernel="general", heavy_threshold=heavy_threshold)
     assert general.info["pileup_kernel"] == 0
     r_lean, r_gen = lean.run(), general.run()
     ix = oracle_rows.index_for(reads, seqlen, strand_filter)
@@ -118,11 +108,7 @@ def test_lean_heavy_rows(gpu):
     rng = np.random.default_rng(67)
     reads = make_reads(rng, 200_000, widths=(100, 200))
     rows = single_rows(rng, 150, 2000)
-    os.environ["RCP_HEAVY_THRESHOLD"] = "16"
-    try:
-        lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, Bins([("whole", 1000)]))
-    finally:
-        del os.environ["RCP_HEAVY_THRESHOLD"]
+    lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, Bins([("whole", 1000)]))
     assert kind == 1
     check(lean, exp)
     same(lean, gen)
@@ -131,7 +117,7 @@ def test_lean_heavy_rows(gpu):
 def test_lean_kernel_choice(gpu):
     """Power-of-two uniform bins of single-range rows take the lean kernel (1); R-RNG layouts,
     other widths and exon lists stay on the general kernel (0) unless the general-bins mode is
-    opted in (RCP_LEAN=2); medians always stay on the general kernel."""
+    opted in (kernel="lean_any"); medians always stay on the general kernel."""
     from recoup_amd.engine import Bins, Plan, ReadSet, RowTable
     rng = np.random.default_rng(71)
     reads = make_reads(rng, 20_000)
@@ -140,17 +126,13 @@ def test_lean_kernel_choice(gpu):
     seg_off = np.array([0, 2, 3], np.int64)
     exons = RowTable(seg_off, np.zeros(3, np.int32), np.array([1000, 3000, 9000]), np.array([1999, 3999, 10999]),
                      np.zeros(3, np.int8), seg_group=np.zeros(3, np.int8), group_is_list=np.array([1, 0, 0, 0], np.uint8))
-    for mode, other in ((None, 0), ("2", 2)):
-        if mode:
-            os.environ["RCP_LEAN"] = mode
-        try:
-            assert Plan(rs, rows, Bins([("whole", 150)])).info["pileup_kernel"] == other   # dif != 0
-            assert Plan(rs, rows, Bins([("whole", 200)])).info["pileup_kernel"] == other   # bs = 10
-            assert Plan(rs, exons, Bins([("whole", 100)])).info["pileup_kernel"] == other
-            assert Plan(rs, rows, Bins([("whole", 1000)], stat="median")).info["pileup_kernel"] == 0
-            assert Plan(rs, rows, Bins([("whole", 1000)])).info["pileup_kernel"] == 1
-        finally:
-            os.environ.pop("RCP_LEAN", None)
+    for mode, other in (("auto", 0), ("lean_any", 2)):
+        assert Plan(rs, rows, Bins([("whole", 150)]), kernel=mode).info["pileup_kernel"] == other   # dif != 0
+        assert Plan(rs, rows, Bins([("whole", 200)]), kernel=mode).info["pileup_kernel"] == other   # bs = 10
+        assert Plan(rs, exons, Bins([("whole", 100)]), kernel=mode).info["pileup_kernel"] == other
+        assert Plan(rs, rows, Bins([("whole", 1000)], stat="median"), kernel=mode).info["pileup_kernel"] == 0
+        assert Plan(rs, rows, Bins([("whole", 1000)]), kernel=mode).info["pileup_kernel"] == 1
+        assert Plan(rs, rows, Bins([("whole", 1000)]), kernel="general").info["pileup_kernel"] == 0
 
 
 @pytest.mark.parametrize("width,n_bins", [(2000, 150), (4000, 200), (1500, 256), (3000, 64), (2000, 1000)])
@@ -162,7 +144,7 @@ def test_lean_general_bins(gpu, width, n_bins):
     reads = make_reads(rng, 80_000, star_frac=0.1)
     rows = single_rows(rng, 400, width, edge=True)
     rows.start[1], rows.end[1] = 1, width  # (a start at 0 would shorten the row)
-    lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, Bins([("whole", n_bins)]), lean_mode="2")
+    lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, Bins([("whole", n_bins)]), lean_mode="lean_any")
     assert kind == (1 if (n_bins, width) == (1000, 2000) else 2)
     check(lean, exp)
     same(lean, gen)
@@ -195,7 +177,7 @@ def test_lean_general_exon_lists(gpu, stranded):
     rows = RowTable(np.array(seg_off), np.array(ch), np.array(st), np.array(en), np.array(sd),
                     seg_group=np.array(gr), group_is_list=np.array([0, 1, 0, 0]), ignore_strand=not stranded)
     bins = Bins([("upstream", 40), ("center", 100), ("downstream", 40)], flank=(1000, 1000))
-    lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, bins, lean_mode="2")
+    lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, bins, lean_mode="lean_any")
     assert kind == 2
     check(lean, exp, rtol=1e-9, atol=1e-12)
     same(lean, gen)

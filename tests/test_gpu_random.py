@@ -48,10 +48,10 @@ def single_rows(rng, R, width, chroms=3, strands=(0, 1, 2), edge=False):
     return RowTable.from_ranges(chrom, s, e, st)
 
 
-def run_case(reads, seqlen, rows, bins, strand_filter=None, binsum=False):
+def run_case(reads, seqlen, rows, bins, strand_filter=None, binsum=False, **plan_kw):
     from recoup_amd.engine import Plan, ReadSet
     rs = ReadSet(*reads, seqlen, device=0, strand_filter=strand_filter)
-    plan = Plan(rs, rows, bins)
+    plan = Plan(rs, rows, bins, **plan_kw)
     res = plan.run(binsum=binsum)
     ix = oracle_rows.index_for(reads, seqlen, strand_filter)
     cov = oracle_rows.row_coverage(ix, rows)
@@ -243,12 +243,8 @@ def test_heavy_rows_match(gpu):
     rng = np.random.default_rng(17)
     reads = make_reads(rng, 200_000, widths=(100, 200))
     rows = single_rows(rng, 100, 2000)
-    os.environ["RCP_HEAVY_THRESHOLD"] = "16"
-    try:
-        res, exp = run_case(reads, CHROM_LEN, rows, Bins([("whole", 100)]))
-        res_m, exp_m = run_case(reads, CHROM_LEN, rows, Bins([("whole", 100)], stat="median"))
-    finally:
-        del os.environ["RCP_HEAVY_THRESHOLD"]
+    res, exp = run_case(reads, CHROM_LEN, rows, Bins([("whole", 100)]), heavy_threshold=16)
+    res_m, exp_m = run_case(reads, CHROM_LEN, rows, Bins([("whole", 100)], stat="median"), heavy_threshold=16)
     check(res, exp)
     check(res_m, exp_m, rtol=1e-9, atol=1e-12)
 
@@ -269,17 +265,13 @@ def test_heavy_duplicate_stacks_match(gpu):
     seqlen = np.array([1_000_000], np.int64)
     s0 = np.array([4000, 4100, 4500, 5100, 3000, 5300, 100_000], np.int64)
     rows = RowTable.from_ranges(np.zeros(7, np.int32), s0, s0 + 1999, np.array([0, 1, 2, 1, 0, 1, 2], np.int8))
-    os.environ["RCP_HEAVY_THRESHOLD"] = "16"
-    try:
-        for bins in (Bins([("whole", 100)]), Bins([("whole", 0, 2000)])):
-            res, exp = run_case(reads, seqlen, rows, bins)
-            check(res, exp)
-        stranded = RowTable.from_ranges(np.zeros(7, np.int32), s0, s0 + 1999,
-                                        np.array([0, 1, 2, 1, 0, 1, 2], np.int8), ignore_strand=False)
-        res, exp = run_case(reads, seqlen, stranded, Bins([("whole", 250)]))
+    for bins in (Bins([("whole", 100)]), Bins([("whole", 0, 2000)])):
+        res, exp = run_case(reads, seqlen, rows, bins, heavy_threshold=16)
         check(res, exp)
-    finally:
-        del os.environ["RCP_HEAVY_THRESHOLD"]
+    stranded = RowTable.from_ranges(np.zeros(7, np.int32), s0, s0 + 1999,
+                                    np.array([0, 1, 2, 1, 0, 1, 2], np.int8), ignore_strand=False)
+    res, exp = run_case(reads, seqlen, stranded, Bins([("whole", 250)]), heavy_threshold=16)
+    check(res, exp)
 
 
 def test_heavy_repeated_executions(gpu):
@@ -290,25 +282,21 @@ def test_heavy_repeated_executions(gpu):
     rng = np.random.default_rng(31)
     reads = make_reads(rng, 200_000, widths=(100, 200))
     rows = single_rows(rng, 100, 2000)
-    os.environ["RCP_HEAVY_THRESHOLD"] = "16"
-    try:
-        rs = ReadSet(*reads, CHROM_LEN, device=0)
-        plan = Plan(rs, rows, Bins([("whole", 100)]))
-        ix = oracle_rows.index_for(reads, CHROM_LEN)
-        cov = oracle_rows.row_coverage(ix, rows)
-        exp = oracle_rows.profile(cov, Bins([("whole", 100)]))
-        for k in range(3):
-            check(plan.run(), exp)
-            if k == 0:
-                np.testing.assert_array_equal(plan.validity(), exp[1])
-            if k == 1:
-                got = plan.coverage()
-                for g, e in zip(got, cov):
-                    assert (g is None) == (e is None)
-                    if e is not None:
-                        np.testing.assert_array_equal(g, e)
-    finally:
-        del os.environ["RCP_HEAVY_THRESHOLD"]
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    plan = Plan(rs, rows, Bins([("whole", 100)]), heavy_threshold=16)
+    ix = oracle_rows.index_for(reads, CHROM_LEN)
+    cov = oracle_rows.row_coverage(ix, rows)
+    exp = oracle_rows.profile(cov, Bins([("whole", 100)]))
+    for k in range(3):
+        check(plan.run(), exp)
+        if k == 0:
+            np.testing.assert_array_equal(plan.validity(), exp[1])
+        if k == 1:
+            got = plan.coverage()
+            for g, e in zip(got, cov):
+                assert (g is None) == (e is None)
+                if e is not None:
+                    np.testing.assert_array_equal(g, e)
 
 
 def test_calc_coverage_csr(gpu):

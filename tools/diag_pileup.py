@@ -49,11 +49,9 @@ def run(name, check_heavy=False, **kw):
           f"n_ovl {n_ovl.sum():>10d} max {n_ovl.max():>8d}  lds {plan.info['lds_bytes']}", flush=True)
     if check_heavy:
         ref = out.clone()
-        os.environ["RCP_HEAVY_THRESHOLD"] = "0"
-        p2 = Plan(rs, rows, Bins([("whole", d["n_bins"])]))
+        p2 = Plan(rs, rows, Bins([("whole", d["n_bins"])]), heavy_threshold=0)
         o2 = p2.execute()
         p2.status()
-        del os.environ["RCP_HEAVY_THRESHOLD"]
         print("   heavy path == plain path:", bool(torch.equal(ref, o2)), flush=True)
     del plan, rs, d
 

@@ -1,16 +1,23 @@
 """Benchmark of the recoup coverage -> profile hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-A step is one pass of the hot path -- calcCoverage + profileMatrix fused: locate kernel,
-LDS pileup-bin kernel, interpolation kernel -- over one synthetic C4 sample
-(200k ChIP peak summits +-1 kb, 1000 bins, 200M reads) with the reads, region tables and
-output matrix already resident in HBM.  Each rank holds its own C4 partition (regions and
-reads are independent objects: weak scaling, no collective on the data path).
+A step is one pass of the hot path -- calcCoverage + profileMatrix fused: reset, locate,
+heavy-slice, pileup-bin and interpolation kernels -- over one synthetic workload (default
+C4: 200k ChIP peak summits +-1 kb, 1000 bins, 200M reads) with the reads, region tables and
+output matrix already resident in HBM.  With N ranks the ONE workload is region-sharded
+(BASELINE config 4 "region-sharded across 8xMI355X"): regions sorted by
+(chromosome, start) are cut into N contiguous shards balanced by overlapping reads, each rank
+indexes only the reads its shard touches and computes its rows; no collective on the data
+path (strong scaling: value = all regions x bins / the slowest rank's time).  The optional
+reassembly of the R x B matrix (one RCCL all_gather over xGMI) is timed separately
+(`gather`), never inside `value`.
 
-Prints ONE JSON line (rank 0): value = region-bins/s over all ranks, plus
-  roofline      the pileup kernel's algorithmic bytes / its HIP-event-timed duration
+Prints ONE JSON line (rank 0): value = region-bins/s of the whole job, plus
+  roofline      the pileup kernel's algorithmic bytes / its HIP-event-timed duration (rank 0's
+                shard), PMC traffic of the same kernel when profiles/ holds it, and the
+                whole-step fraction
   cpu_baseline  the CPU oracle (test infrastructure, `oracle/`) on a bounded sample, timed here
 """
 import argparse
@@ -44,9 +51,11 @@ def parse():
     ap.add_argument("--cpu-regions", type=int, default=200000, help="CPU baseline sample (regions)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline: repeat the sample this long")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verify-gather", action="store_true",
+                    help="N > 1: rank 0 also runs the whole workload alone and checks the gathered matrix bit for bit")
     ap.add_argument("--no-e2e", action="store_true", help="skip the one-off host-to-host timing")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_c4.json"),
-                    help="PMC traffic summary (from tools/pmc_traffic.py) to attach to the roofline")
+    ap.add_argument("--traffic", default=None,
+                    help="PMC traffic summary (tools/pmc_traffic.py); default profiles/traffic_<config>.json")
     return ap.parse_args()
 
 
@@ -63,11 +72,12 @@ WORKLOADS = {
 }
 
 
-def workload(args, dev, rank):
-    """(data, RowTable, Bins, total read-segment overlaps) of the chosen BASELINE config."""
+def workload(args, dev):
+    """(data, RowTable, Bins, per-row overlapping read-segment pairs) of the chosen BASELINE
+    config.  Every rank generates the SAME data (one seed, Philox on the device)."""
     import synthetic
     from recoup_amd.engine import Bins, RowTable
-    seed = args.seed + 7919 * rank
+    seed = args.seed
     if args.config == "c3":
         kw = {}
         if args.reads:
@@ -78,8 +88,9 @@ def workload(args, dev, rank):
         rows = synthetic.rna_rows(d)
         bins = Bins([("upstream", d["flank_bins"]), ("center", d["region_bins"]), ("downstream", d["flank_bins"])],
                     flank=d["flank"])
-        ovl = synthetic.n_overlaps_segments(d["reads"], rows.chrom, rows.start, rows.end, device=dev).sum()
-        return d, rows, bins, ovl
+        seg = synthetic.n_overlaps_segments(d["reads"], rows.chrom, rows.start, rows.end, device=dev)
+        ovl = np.add.reduceat(seg, rows.seg_off[:-1]) if len(seg) else np.zeros(rows.n_rows, np.int64)
+        return d, rows, bins, ovl.astype(np.int64)
     kw = {}
     if args.reads:
         kw["n_reads"] = args.reads
@@ -89,8 +100,87 @@ def workload(args, dev, rank):
     reg = d["regions"]
     rows = RowTable.from_ranges(reg["chrom"], reg["start"], reg["end"], reg["strand"])
     bins = Bins([("whole", d["n_bins"])]) if d["n_bins"] > 0 else Bins([("whole", 0, sum(d["flank"]))])
-    ovl = synthetic.n_overlaps(d["reads"], reg, d["width"], device=dev).sum()
+    ovl = synthetic.n_overlaps(d["reads"], reg, d["width"], device=dev).astype(np.int64)
     return d, rows, bins, ovl
+
+
+def shard_of(rows, ovl, world, rank, per_region=64.0):
+    """Rows [lo, hi) of this rank: contiguous in (chromosome, start) order (the synthetic
+    region tables are sorted that way), balanced by overlapping reads + a per-region constant
+    (recoup_amd.shard.balance)."""
+    from recoup_amd.shard import balance
+    cuts = balance(np.asarray(ovl, np.float64) + per_region, world)
+    return int(cuts[rank]), int(cuts[rank + 1]), cuts
+
+
+def subset_rows(rows, lo, hi):
+    from recoup_amd.engine import RowTable
+    j0, j1 = int(rows.seg_off[lo]), int(rows.seg_off[hi])
+    sl = slice(j0, j1)
+    return RowTable(rows.seg_off[lo:hi + 1] - j0, rows.chrom[sl], rows.start[sl], rows.end[sl], rows.strand[sl],
+                    seg_group=None if rows.seg_group is None else rows.seg_group[sl],
+                    group_is_list=rows.group_is_list, ignore_strand=rows.ignore_strand)
+
+
+def reads_for_rows(reads, rows, n_chrom):
+    """The reads a shard can touch, selected on the device: per chromosome, those overlapping
+    [min segment start, max segment end] of the shard's rows.  A row's coverage depends only
+    on the reads it hits (with NA seqlengths its Rle length is their max end,
+    R/coverage.R:201), so the shard's rows are unchanged (recoup_amd.shard.reads_for)."""
+    chrom, start, end, strand = reads
+    dev = start.device
+    lo = torch.full((n_chrom,), 2 ** 31 - 1, dtype=torch.int64, device=dev)
+    hi = torch.full((n_chrom,), -(2 ** 31), dtype=torch.int64, device=dev)
+    c = torch.as_tensor(rows.chrom, dtype=torch.int64, device=dev)
+    if c.numel():
+        lo.scatter_reduce_(0, c, torch.as_tensor(rows.start, dtype=torch.int64, device=dev), "amin")
+        hi.scatter_reduce_(0, c, torch.as_tensor(rows.end, dtype=torch.int64, device=dev), "amax")
+    ci = chrom.to(torch.int64)
+    keep = (end.to(torch.int64) >= lo[ci]) & (start.to(torch.int64) <= hi[ci])
+    return tuple(x[keep].contiguous() for x in (chrom, start, end, strand))
+
+
+def host_cores():
+    """CPU threads this process may use: the affinity mask, capped by a cgroup CPU quota
+    (cpu.max) when one is set.  Returns (threads, basis string)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    n, basis = aff, f"sched_getaffinity {aff}"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+            basis += f", cgroup cpu.max {quota}"
+            n = min(n, quota)
+    except (OSError, ValueError):
+        pass
+    return n, basis
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def load_traffic(path, args, kernel, R, n_reads, world):
+    """PMC traffic per launch of THIS kernel on THIS workload (tools/pmc_traffic.py), else None."""
+    if not path or not os.path.exists(path) or world != 1:
+        return None
+    try:
+        tr = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if (tr.get("config") == args.config and tr.get("regions") == R and tr.get("reads") == n_reads
+            and tr.get("kernel") == kernel):
+        return tr.get("hbm_bytes_per_launch")
+    return None
 
 
 def main():
@@ -100,7 +190,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     # rehearsal of the N > 1 path on fewer GPUs: RCP_DIST_BACKEND=gloo RCP_SHARE_GPU=1 puts
-    # several ranks on one device and the barrier / max-reduction on the host
+    # several ranks on one device and the barrier / max-reduction / gather on the host
     backend = os.environ.get("RCP_DIST_BACKEND", "nccl")
     if os.environ.get("RCP_SHARE_GPU") == "1":
         local = local % torch.cuda.device_count()
@@ -117,12 +207,19 @@ def main():
     from recoup_amd.engine import Plan, ReadSet
 
     t0 = time.time()
-    data, rows, bins, ovl_rows = workload(args, dev, rank)
-    reads = data["reads"]
+    data, rows_all, bins, ovl_all = workload(args, dev)
+    R_total = rows_all.n_rows
+    n_reads_total = int(data["reads"][1].numel())
+    lo, hi, cuts = shard_of(rows_all, ovl_all, world, rank)
+    rows = subset_rows(rows_all, lo, hi) if world > 1 else rows_all
+    reads = reads_for_rows(data["reads"], rows, len(data["seqlen"])) if world > 1 else data["reads"]
+    if world > 1 and not args.verify_gather:
+        data["reads"] = None  # the full read set is not kept on this rank
     R = rows.n_rows
     n_reads = int(reads[1].numel())
     torch.cuda.synchronize()
-    log(f"[rank {rank}] data {args.config}: {n_reads} reads, {R} rows in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] data {args.config}: shard rows [{lo}, {hi}) of {R_total}, {n_reads} of {n_reads_total} "
+        f"reads in {time.time() - t0:.1f}s")
 
     t1 = time.time()
     rs = ReadSet(*reads, data["seqlen"], device=local)
@@ -131,7 +228,7 @@ def main():
     plan_s = time.time() - tp
     B = plan.n_cols
     out = plan.empty_output()
-    valid = torch.empty(R, dtype=torch.uint8, device=dev)
+    valid = torch.empty(max(R, 1), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     log(f"[rank {rank}] readset + plan in {time.time() - t1:.1f}s (plan {plan_s * 1e3:.1f} ms), info {plan.info}")
 
@@ -173,34 +270,46 @@ def main():
         kt += [ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3])]
     kt /= args.steps  # ms per launch
     plan.status()
+    heavy = plan.heavy_rows()
 
-    units = R * B  # region-bins per step per rank (1 sample)
-    value = world * units * args.steps / elapsed
-    ovl = int(ovl_rows)
+    # ---- reassembly of the R x B matrix (not in `value`): one all_gather of each rank's
+    # column-major block, padded to the largest shard, then placement into region order
+    gather = None
+    if dist:
+        gather, full = gather_matrix(tdist, backend, out, R, B, cuts, dev, R_total)
+        if args.verify_gather and rank == 0:
+            rs_all = ReadSet(*data["reads"], data["seqlen"], device=local)
+            ref = Plan(rs_all, rows_all, bins).execute()
+            torch.cuda.synchronize()
+            gather["parity_vs_single_gpu"] = bool(torch.equal(full.to(ref.device).view(torch.int64),
+                                                              ref.view(torch.int64)))
+            del rs_all, ref
+        del full
+
+    units = R_total * B  # region-bins per step of the whole job
+    value = units * args.steps / elapsed
+    ovl = int(np.asarray(ovl_all)[lo:hi].sum())
     # 8 B per overlapping (read, segment) + 16 B per region + 8 B per further segment
-    # of a multi-range row + the f64 output written once
+    # of a multi-range row + the f64 output written once (this rank's shard)
     n_seg = len(rows.start)
     bytes_pileup = 8 * ovl + 16 * R + 8 * (n_seg - R) + 8 * R * B
     achieved = bytes_pileup / (kt[1] * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic):
-        try:
-            tr = json.load(open(args.traffic))
-            if tr.get("config") == args.config and tr.get("regions") == R and tr.get("reads") == n_reads:
-                traffic = tr.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    kernel = PILEUP_KERNELS[plan.info["pileup_kernel"]]
+    traffic = load_traffic(args.traffic or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json"), args,
+                           kernel, R, n_reads, world)
+    step_ms = elapsed / args.steps * 1e3
 
     # ---- end to end once (not `value`): what a host caller (the R shim's rcp_profile) pays --
     # host read arrays -> H2D + device sort (readset), plan, one pass, D2H of the matrix
     e2e = None
     if not args.no_e2e:
-        e2e = end_to_end(data, rows, bins, local, R * B)
+        e2e = end_to_end(reads, data["seqlen"], rows, bins, local, R * B)
         if dist:
             t = torch.tensor([e2e["ms"]], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
             tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
             e2e["ms"] = float(t.item())
-            e2e["region_bins_per_s"] = world * R * B / (e2e["ms"] * 1e-3)
+            e2e["region_bins_per_s"] = units / (e2e["ms"] * 1e-3)
+            e2e["note"] += "; per rank on its shard, max over ranks"
 
     # ---- CPU baseline (rank 0, N = 1): the oracle on a bounded sample of the same workload
     cpu = None
@@ -216,25 +325,30 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": step_ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
             "config": {
                 "workload": WORKLOADS[args.config],
-                "regions_per_gpu": R, "bins": B, "reads_per_gpu": n_reads, "samples": 1,
-                "parallelism": f"region-sharded x{world} (one partition per GPU, no data-path collective)",
+                "regions": R_total, "bins": B, "reads": n_reads_total, "samples": 1,
+                "parallelism": f"region-sharded x{world}: one contiguous region shard per GPU, balanced by "
+                               f"overlapping reads; no data-path collective",
+                "rank0_shard": {"regions": R, "reads": n_reads},
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "kernel": PILEUP_KERNELS[plan.info["pileup_kernel"]],
+                         "kernel": kernel,
                          "algorithmic_bytes_per_launch": bytes_pileup,
-                         "kernel_ms": kt[1]},
+                         "kernel_ms": kt[1],
+                         "step_frac": bytes_pileup / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if world == 1 else None},
             "cpu_baseline": cpu,
             "e2e": e2e,
+            "gather": gather,
             "kernel_ms": {"locate": kt[0], "pileup": kt[1], "interp": kt[2]},
+            "heavy_rows": heavy,
             "n_overlaps": ovl,
             "plan_ms": plan_s * 1e3,
             "parity_sample": parity,
@@ -244,32 +358,59 @@ def main():
         tdist.destroy_process_group()
 
 
-def end_to_end(data, rows, bins, local, units):
-    """One host-to-host pass, timed in phases: pageable host read arrays (as R holds them) ->
-    ReadSet (H2D + device radix sort + stream index) -> Plan -> execute -> D2H of the R
-    column-major matrix into pageable host memory.  Reported beside `value`, never as it."""
-    from recoup_amd.engine import Plan, ReadSet
-    host = [x.cpu().numpy() for x in data["reads"]]
+def gather_matrix(tdist, backend, out, R, B, cuts, dev, R_total, reps=3):
+    """Reassemble the full R x B column-major matrix on every rank: all_gather of each rank's
+    (B, n_r) block padded to the largest shard (RCCL over xGMI on GPU ranks), then one device
+    copy per rank block into region order.  Returns timing (max over ranks) and bytes."""
+    world = len(cuts) - 1
+    nmax = int(np.max(np.diff(cuts)))
+    on_gpu = backend == "nccl"
+    blk = torch.zeros((B, nmax), dtype=torch.float64, device=dev if on_gpu else "cpu")
+    recv = torch.empty((world, B, nmax), dtype=torch.float64, device=blk.device)
+    full = torch.empty((B, R_total), dtype=torch.float64, device=blk.device)
+    times = []
+    for _ in range(reps):
+        tdist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        blk[:, :R].copy_(out[:, :R], non_blocking=True)
+        if on_gpu:
+            tdist.all_gather_into_tensor(recv, blk)
+        else:
+            tdist.all_gather(list(recv.unbind(0)), blk)
+        for r in range(world):
+            full[:, cuts[r]:cuts[r + 1]].copy_(recv[r, :, :cuts[r + 1] - cuts[r]], non_blocking=True)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t)
+    ms = float(np.mean(times[1:] if len(times) > 1 else times)) * 1e3
+    tt = torch.tensor([ms], dtype=torch.float64, device=blk.device)
+    tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+    return {"ms": float(tt.item()), "bytes_per_rank_received": (world - 1) * B * nmax * 8,
+            "backend": "rccl" if on_gpu else backend,
+            "note": "all_gather_into_tensor of padded (B, R/N) blocks + placement; not part of value"}, full
+
+
+def end_to_end(reads, seqlen, rows, bins, local, units):
+    """One host-to-host pass through the C ABI entry points the R shim binds, timed in two
+    phases: rcp_readset_create from host read arrays (as R holds them: H2D + device radix
+    sort + stream index), then rcp_profile (plan + one pass + D2H of the R column-major
+    matrix into caller-owned host memory, already touched as R's allocMatrix result is).
+    Reported beside `value`, never as it."""
+    from recoup_amd.engine import ReadSet, profile_host
+    host = [x.cpu().numpy() for x in reads]
+    out = np.zeros((bins.n_cols, rows.n_rows))  # R's matrix: allocated + touched before the call
+    valid = np.zeros(max(rows.n_rows, 1), np.uint8)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    rs = ReadSet(*host, data["seqlen"], device=local)
-    torch.cuda.synchronize()
+    rs = ReadSet(*host, seqlen, device=local)
     t1 = time.perf_counter()
-    plan = Plan(rs, rows, bins)
+    profile_host(rs, rows, bins, out, valid)
     t2 = time.perf_counter()
-    out = plan.empty_output()
-    plan.execute(out)
-    torch.cuda.synchronize()
-    t3 = time.perf_counter()
-    mat = out.cpu()
-    t4 = time.perf_counter()
-    plan.status()
-    del plan, rs, out, mat
-    ms = (t4 - t0) * 1e3
+    del rs
+    ms = (t2 - t0) * 1e3
     return {"ms": ms, "region_bins_per_s": units / (ms * 1e-3),
-            "phases_ms": {"readset_h2d_sort": (t1 - t0) * 1e3, "plan": (t2 - t1) * 1e3,
-                          "execute": (t3 - t2) * 1e3, "d2h_matrix": (t4 - t3) * 1e3},
-            "note": "one pass from pageable host arrays to a host matrix; includes PCIe both ways"}
+            "phases_ms": {"readset_create": (t1 - t0) * 1e3, "profile_one_shot": (t2 - t1) * 1e3},
+            "note": "C ABI: rcp_readset_create from host arrays + rcp_profile into a host matrix; PCIe both ways"}
 
 
 def cpu_baseline(args, data, rows, bins, out, valid, B):
@@ -288,11 +429,7 @@ def cpu_baseline(args, data, rows, bins, out, valid, B):
     order = torch.argsort(key)
     c, s, e, st = (x[order].cpu().numpy() for x in (c, s, e, st))
     ix = o.Index(c, s, e, st, data["seqlen"])
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
+    threads, basis = host_cores()
     single = bool(np.all(np.diff(rows.seg_off[:m + 1]) == 1)) and len(bins.parts) == 1
     if single:
         mask = o.Mask.from_ranges(rows.chrom[:m], rows.start[:m], rows.end[:m], rows.strand[:m])
@@ -303,17 +440,14 @@ def cpu_baseline(args, data, rows, bins, out, valid, B):
                 return o.profile_part(ix, mask, nb, nthreads=threads)
             return o.profile_part(ix, mask, 0, ncol=B, nthreads=threads)
     else:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_rows
         from recoup_amd.engine import RowTable
         sub = RowTable(rows.seg_off[:m + 1], rows.chrom[:rows.seg_off[m]], rows.start[:rows.seg_off[m]],
                        rows.end[:rows.seg_off[m]], rows.strand[:rows.seg_off[m]],
                        seg_group=None if rows.seg_group is None else rows.seg_group[:rows.seg_off[m]],
                        group_is_list=rows.group_is_list, ignore_strand=rows.ignore_strand)
-        threads = 1
 
         def run():
-            return oracle_rows.profile(oracle_rows.row_coverage(ix, sub), bins)
+            return o.profile_rows(ix, sub, bins, nthreads=threads)
     # repeat the sample until about args.cpu_seconds of wall time (a single pass over C4 takes
     # well under a second on a many-core host) and report the mean pass
     reps = 0
@@ -330,9 +464,9 @@ def cpu_baseline(args, data, rows, bins, out, valid, B):
     parity = bool(np.array_equal(gv, np.asarray(rvalid).astype(bool)) and
                   np.allclose(gpu, ref, rtol=1e-9, atol=1e-12, equal_nan=True))
     cpu = {"value": m * B / dt, "unit": "region-bins/s", "cores": threads, "kind": "port",
-           "sample": f"first {m} of {R} rows (all their reads), {B} columns; oracle/ C restatement"
-                     f"{', %d threads over regions' % threads if single else ' (per-group coverage, Python splitVector)'}; "
-                     f"mean of {reps} passes, {dt:.3f} s/pass"}
+           "sample": f"first {m} of {R} rows (all their reads), {B} columns; oracle/ C restatement, "
+                     f"{threads} threads over regions ({basis}); mean of {reps} passes, {dt:.3f} s/pass",
+           "cpu_model": cpu_model()}
     return cpu, parity
 
 

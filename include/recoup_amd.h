@@ -187,6 +187,9 @@ RCP_API int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d_va
                                     void* hip_stream, int stages);
 /* Synchronises the stream and returns RCP_OK or the error the last execute raised. */
 RCP_API int rcp_plan_status(rcp_plan* plan, void* hip_stream);
+/* Rows the last execution sent through the skewed-row (heavy slice) path; synchronises the
+ * stream.  Diagnostics / tests: the count is cleared by the next execution's first kernel. */
+RCP_API int rcp_plan_heavy_rows(rcp_plan* plan, void* hip_stream, int32_t* n_rows);
 /* Only the locate kernel: row validity (device pointer), e.g. for profileMatrix's
  * equal-length test on sample 1 (R/profile.R:6-10). */
 RCP_API int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_stream);

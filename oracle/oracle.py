@@ -40,6 +40,17 @@ class _MaskIn(ctypes.Structure):
                 ("seg_start", _i32p), ("seg_end", _i32p), ("seg_strand", _i8p)]
 
 
+class _RowsIn(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("seg_off", _i64p), ("seg_chrom", _i32p), ("seg_start", _i32p),
+                ("seg_end", _i32p), ("seg_strand", _i8p), ("seg_group", _i8p), ("group_is_list", _u8p)]
+
+
+class _PartsIn(ctypes.Structure):
+    _fields_ = [("n_parts", ctypes.c_int32), ("where", _i32p), ("n_bins", _i32p), ("per_base_width", _i32p),
+                ("f1", ctypes.c_int32), ("f2", ctypes.c_int32), ("stat", ctypes.c_int32), ("interp", ctypes.c_int32),
+                ("rng_kind", ctypes.c_int32), ("scale", ctypes.c_double)]
+
+
 def build():
     """Compile the oracle with its own Makefile (gcc)."""
     import subprocess
@@ -63,6 +74,8 @@ def lib():
         L.orc_profile.argtypes = [ctypes.c_void_p, ctypes.POINTER(_MaskIn), ctypes.c_int, ctypes.c_double,
                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int64, _u8p]
+        L.orc_profile_rows.argtypes = [ctypes.c_void_p, ctypes.POINTER(_RowsIn), ctypes.POINTER(_PartsIn), ctypes.c_int,
+                                       ctypes.c_int, _dp, _u8p]
         L.orc_set_seed.argtypes = [ctypes.c_uint32]
         L.orc_unif_rand.restype = ctypes.c_double
         L.orc_sample.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p]
@@ -178,6 +191,36 @@ def profile_part(index, mask, n, ncol=None, where="whole", flank=(0, 0), interp=
                            int(nthreads), out.ctypes.data_as(_dp), int(ncol), _p(valid, _u8p))
     if rc:
         raise ValueError(f"profile: R would raise an error here (code {rc})")
+    return out, valid
+
+
+def profile_rows(index, rows, bins, nthreads=1):
+    """Rows of several mask elements (coverageRnaRef's c(left, exons, right), R/coverage.R:79-124)
+    over several column parts (profileMatrix's cbind, R/profile.R:13-81), multithreaded over
+    rows.  ``rows`` / ``bins`` are duck-typed like recoup_amd.engine.RowTable / Bins:
+    rows.seg_off/chrom/start/end/strand/seg_group/group_is_list/ignore_strand, bins.where/
+    n_bins/width/flank/stat/interp/rng_kind/scale.  Returns (R x n_cols F-order matrix, valid)."""
+    keep = [np.ascontiguousarray(rows.seg_off, np.int64), np.ascontiguousarray(rows.chrom, np.int32),
+            np.ascontiguousarray(rows.start, np.int32), np.ascontiguousarray(rows.end, np.int32),
+            np.ascontiguousarray(rows.strand, np.int8),
+            None if rows.seg_group is None else np.ascontiguousarray(rows.seg_group, np.int8),
+            None if rows.group_is_list is None else np.ascontiguousarray(rows.group_is_list, np.uint8)]
+    n = len(keep[0]) - 1
+    ri = _RowsIn(n, _p(keep[0], _i64p), _p(keep[1], _i32p), _p(keep[2], _i32p), _p(keep[3], _i32p),
+                 _p(keep[4], _i8p), None if keep[5] is None else _p(keep[5], _i8p),
+                 None if keep[6] is None else _p(keep[6], _u8p))
+    where = np.ascontiguousarray(bins.where, np.int32)
+    nb = np.ascontiguousarray(bins.n_bins, np.int32)
+    width = np.ascontiguousarray(bins.width, np.int32)
+    pi = _PartsIn(len(nb), _p(where, _i32p), _p(nb, _i32p), _p(width, _i32p), int(bins.flank[0]), int(bins.flank[1]),
+                  int(bins.stat), int(bins.interp), int(bins.rng_kind), float(bins.scale))
+    ncol = int(sum(w if b == 0 else b for b, w in zip(nb, width)))
+    out = np.zeros((n, ncol), dtype=np.float64, order="F")
+    valid = np.zeros(n, dtype=np.uint8)
+    rc = lib().orc_profile_rows(index.h, ctypes.byref(ri), ctypes.byref(pi), int(bool(rows.ignore_strand)),
+                                int(nthreads), out.ctypes.data_as(_dp), _p(valid, _u8p))
+    if rc:
+        raise ValueError(f"profile_rows: R would raise an error here (code {rc})")
     return out, valid
 
 

@@ -683,3 +683,103 @@ int orc_profile(const orc_index* ix, const orc_mask_in* mask, int ignore_strand,
     parallel_for(mask->n, nthreads, prof_task, &c);
     return c.err ? -c.err : 0;
 }
+
+/* ------------------------------------------------------------------------- */
+/* Rows of several mask elements (coverageRnaRef) + several column parts      */
+/* ------------------------------------------------------------------------- */
+/* A row is c(cov(g0), cov(g1), ...) over its groups (R/coverage.R:101-121: left flank,
+ * the gene's exon list, right flank), NULL when any group is NULL; the profile row is
+ * cbind over the parts (R/profile.R:13-81): each part slices the row (where, flank) and
+ * bins it with splitVector (n_bins > 0) or copies it per base (n_bins == 0); a NULL row
+ * gives zeros (rep(0, binSize) binned, rep(0, size) per base). */
+typedef struct {
+    const orc_index* ix;
+    const orc_rows_in* rows;
+    const orc_parts_in* parts;
+    int ignore_strand;
+    double* out;
+    uint8_t* valid;
+    int64_t ncol;
+    volatile int err;
+} rows_ctx;
+
+static void rows_task(void* c_, int32_t r) {
+    rows_ctx* c = (rows_ctx*)c_;
+    const orc_rows_in* R = c->rows;
+    const orc_parts_in* P = c->parts;
+    const int64_t j0 = R->seg_off[r], j1 = R->seg_off[r + 1];
+    int64_t cap = 0;
+    {
+        orc_mask_in all = {1, NULL, R->seg_chrom + j0, R->seg_start + j0, R->seg_end + j0, R->seg_strand + j0};
+        int64_t off[2] = {0, j1 - j0};
+        int neg = 0;
+        all.seg_off = off;
+        cap = nominal_length(&all, 0, &neg);
+    }
+    int32_t* cov = (int32_t*)malloc(sizeof(int32_t) * (size_t)(cap > 0 ? cap : 1));
+    int64_t L = 0;
+    int ok = j1 > j0;
+    for (int64_t g0 = j0; ok && g0 < j1;) {
+        const int grp = R->seg_group ? R->seg_group[g0] : 0;
+        int64_t g1 = g0;
+        while (g1 < j1 && (R->seg_group ? R->seg_group[g1] : 0) == grp) ++g1;
+        /* one mask element: a GRangesList element (all its ranges) or one GRanges range each */
+        const int multi = R->group_is_list && R->group_is_list[grp];
+        for (int64_t a = g0; ok && a < g1; a = multi ? g1 : a + 1) {
+            const int64_t b = multi ? g1 : a + 1;
+            int64_t off[2] = {0, b - a};
+            orc_mask_in m = {1, off, R->seg_chrom + a, R->seg_start + a, R->seg_end + a, R->seg_strand + a};
+            const int64_t k = coverage_one(c->ix, &m, 0, c->ignore_strand, cov + L);
+            if (k < 0) ok = 0; else L += k;
+        }
+        g0 = g1;
+    }
+    c->valid[r] = (uint8_t)ok;
+    int64_t col = 0;
+    for (int p = 0; p < P->n_parts; ++p) {
+        const int n = P->n_bins[p];
+        const int64_t ncol_p = n > 0 ? n : P->per_base_width[p];
+        int64_t need = ncol_p > L ? ncol_p : L;
+        double* x = (double*)malloc(sizeof(double) * (size_t)(need + 1));
+        double* row = (double*)malloc(sizeof(double) * (size_t)(need + 1));
+        int64_t rl = 0;
+        if (!ok) {
+            for (int64_t i = 0; i < ncol_p; i++) x[i] = 0.0;
+            if (n > 0) {
+                if (orc_split_vector(x, n, n, P->interp, P->stat, P->rng_kind, row, &rl)) c->err = 1;
+            } else {
+                memcpy(row, x, sizeof(double) * (size_t)ncol_p);
+                rl = ncol_p;
+            }
+        } else {
+            int64_t a = 0, b = L;
+            const int w = P->where[p];
+            if (w == ORC_WHERE_CENTER) { a = P->f1; b = L - P->f2; }
+            else if (w == ORC_WHERE_UPSTREAM) { a = 0; b = P->f1; }
+            else if (w == ORC_WHERE_DOWNSTREAM) { a = L - P->f2; b = L; }
+            if (a < 0 || b > L || b < a) {
+                c->err = 2;
+            } else {
+                for (int64_t i = a; i < b; i++) x[i - a] = (double)cov[i] * P->scale;
+                if (n > 0) {
+                    if (orc_split_vector(x, b - a, n, P->interp, P->stat, P->rng_kind, row, &rl)) c->err = 1;
+                } else {
+                    memcpy(row, x, sizeof(double) * (size_t)(b - a));
+                    rl = b - a;
+                }
+            }
+        }
+        for (int64_t j = 0; j < ncol_p; j++) c->out[(size_t)(col + j) * R->n + r] = rl > 0 ? row[j % rl] : 0.0;
+        col += ncol_p;
+        free(x);
+        free(row);
+    }
+    free(cov);
+}
+
+int orc_profile_rows(const orc_index* ix, const orc_rows_in* rows, const orc_parts_in* parts, int ignore_strand,
+                     int nthreads, double* out, uint8_t* valid) {
+    rows_ctx c = {ix, rows, parts, ignore_strand, out, valid, 0, 0};
+    parallel_for(rows->n, nthreads, rows_task, &c);
+    return c.err ? -c.err : 0;
+}

@@ -81,6 +81,32 @@ int orc_profile(const orc_index* ix, const orc_mask_in* mask, int ignore_strand,
                 int where, int f1, int f2, int n, int interp, int stat, int rng_kind,
                 int nthreads, double* out, int64_t ncol, uint8_t* valid);
 
+/* Rows of several mask elements ("groups"; coverageRnaRef: left flank, exon list, right
+ * flank, R/coverage.R:79-124) profiled over several column parts (R/profile.R:13-81). */
+typedef struct {
+    int32_t n;
+    const int64_t* seg_off;     /* n+1 */
+    const int32_t* seg_chrom;
+    const int32_t* seg_start;
+    const int32_t* seg_end;
+    const int8_t* seg_strand;
+    const int8_t* seg_group;    /* NULL = one group */
+    const uint8_t* group_is_list; /* [4]; NULL = no lists */
+} orc_rows_in;
+
+typedef struct {
+    int32_t n_parts;
+    const int32_t* where;
+    const int32_t* n_bins;      /* 0 = per base */
+    const int32_t* per_base_width;
+    int32_t f1, f2;
+    int32_t stat, interp, rng_kind;
+    double scale;
+} orc_parts_in;
+
+int orc_profile_rows(const orc_index* ix, const orc_rows_in* rows, const orc_parts_in* parts, int ignore_strand,
+                     int nthreads, double* out, uint8_t* valid);
+
 /* R RNG restatement, exposed for known-answer tests. */
 void orc_set_seed(uint32_t seed);
 double orc_unif_rand(void);

@@ -87,6 +87,7 @@ SIGNATURES = [
     ("rcp_plan_execute_stages", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     ("rcp_plan_status", ctypes.c_int, [_vp, _vp]),
     ("rcp_plan_validity", ctypes.c_int, [_vp, _vp, _vp]),
+    ("rcp_plan_heavy_rows", ctypes.c_int, [_vp, _vp, _i32p]),
     ("rcp_plan_row_lengths", ctypes.c_int, [_vp, _i64p]),
     ("rcp_profile", ctypes.c_int, [_vp, ctypes.POINTER(RowsDesc), ctypes.POINTER(BinsDesc), _dp, _u8p]),
     ("rcp_calc_coverage", ctypes.c_int, [_vp, _i64p, _vp, _vp, _vp]),

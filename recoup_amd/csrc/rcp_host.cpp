@@ -1048,6 +1048,20 @@ extern "C" int rcp_plan_status(rcp_plan* plan, void* hip_stream) {
     RCP_CATCH
 }
 
+extern "C" int rcp_plan_heavy_rows(rcp_plan* plan, void* hip_stream, int32_t* n_rows) {
+    RCP_TRY
+    if (!plan || !n_rows) return fail(RCP_EINVAL, "NULL argument");
+    DeviceGuard g(plan->rs->device);
+    HIP_TRY(g.err);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    uint32_t n = 0;
+    HIP_TRY(hipMemcpyAsync(&n, plan->dev.status + 1, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n_rows = (int32_t)std::min<uint32_t>(n, (uint32_t)std::max(plan->dev.heavy_cap, 0));
+    return RCP_OK;
+    RCP_CATCH
+}
+
 extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins, double* out,
                            uint8_t* row_valid) {
     RCP_TRY

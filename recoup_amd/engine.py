@@ -192,6 +192,12 @@ class Plan:
     def status(self, stream=None):
         check(_lib.lib().rcp_plan_status(self.h, _stream(self.device, stream)))
 
+    def heavy_rows(self, stream=None):
+        """Rows the last execution piled through the skewed-row (heavy slice) path."""
+        n = ctypes.c_int32()
+        check(_lib.lib().rcp_plan_heavy_rows(self.h, _stream(self.device, stream), ctypes.byref(n)))
+        return n.value
+
     def validity(self, stream=None):
         v = torch.empty(max(self.n_rows, 1), dtype=torch.uint8, device=f"cuda:{self.device}")
         check(_lib.lib().rcp_plan_validity(self.h, ptr(v), _stream(self.device, stream)))
@@ -246,3 +252,18 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+def profile_host(readset, rows, bins, out, valid=None):
+    """rcp_profile: the one-shot host entry point the R .Call shim binds -- plan, one pass and
+    the copy of the R column-major matrix into the caller's host array ``out`` (float64,
+    C-contiguous shape (n_cols, n_rows), i.e. R's column-major n_rows x n_cols matrix) and of
+    the NULL mask into ``valid`` (uint8, n_rows)."""
+    if out.dtype != np.float64 or not out.flags.c_contiguous or out.size != bins.n_cols * rows.n_rows:
+        raise ValueError("out must be a C-contiguous float64 array of n_cols x n_rows")
+    rd = rows.desc()
+    bd = bins.desc()
+    with torch.cuda.device(readset.device):
+        check(_lib.lib().rcp_profile(readset.h, ctypes.byref(rd), ctypes.byref(bd), cptr(out, _lib._dp),
+                                     None if valid is None else cptr(valid, _lib._u8p)))
+    return out

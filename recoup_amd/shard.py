@@ -6,7 +6,7 @@ regions sorted by (chromosome, start) are cut into ``world`` contiguous shards b
 an estimate of their work (overlapping reads + a per-region constant), and each rank
 indexes only the reads that can touch its shard.  The only collective is the optional
 reassembly of the R x B matrix after the compute (``gather=``), done once with RCCL (nccl
-backend) on GPU ranks or gloo on CPU ranks.
+backend) on device-resident blocks on GPU ranks, or gloo on CPU ranks.
 """
 import numpy as np
 import torch
@@ -70,11 +70,17 @@ def reads_for(reads, regions):
     return reads[keep]
 
 
-def profile_sharded(reads, regions, compute, group=None, gather="all", per_region=64.0):
-    """Run ``compute(shard_reads, shard_regions) -> (matrix (n, B) float64, valid (n,) bool)``
-    on this rank's shard and, with ``gather="all"``, reassemble the full R x B matrix (region
-    order of ``regions``) on every rank with one all_gather.  ``gather=None`` returns only the
-    local shard: (indices, matrix, valid)."""
+def profile_sharded(reads, regions, compute, group=None, gather="all", per_region=64.0, as_tensor=False):
+    """Run ``compute(shard_reads, shard_regions)`` on this rank's shard and, with
+    ``gather="all"``, reassemble the full R x B matrix (region order of ``regions``) on every
+    rank with one all_gather.
+
+    ``compute`` returns either ``(matrix (n, B) numpy, valid (n,) bool)`` (host compute, e.g.
+    the oracle in CPU tests) or ``(out (B, n) torch tensor, valid (n,) tensor)`` -- the engine's
+    R column-major device buffer (``gpu_compute``).  A device result stays in HBM through the
+    collective (RCCL over xGMI) and the placement; only the final matrix is copied to the host
+    (or returned on the device with ``as_tensor``: shape (B, R), column-major R x B).
+    ``gather=None`` returns only the local shard: (indices, matrix, valid)."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -83,36 +89,40 @@ def profile_sharded(reads, regions, compute, group=None, gather="all", per_regio
     mine = shards[rank]
     sub = regions[mine]
     mat, valid = compute(reads_for(reads, sub), sub)
-    mat = np.asarray(mat, dtype=np.float64)
-    valid = np.asarray(valid, dtype=bool)
-    if gather is None or world == 1:
-        if world == 1:
-            out = np.zeros((len(regions), mat.shape[1]))
-            v = np.zeros(len(regions), dtype=bool)
-            out[mine], v[mine] = mat, valid
-            return out, v
-        return mine, mat, valid
-    B = int(mat.shape[1]) if mat.ndim == 2 else 0
-    nmax = max(len(s) for s in shards)
-    backend = dist.get_backend(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-    # one padded block per rank: B columns of values + 1 column of validity
-    blk = torch.zeros((nmax, B + 1), dtype=torch.float64, device=dev)
-    if len(mine):
-        blk[:len(mine), :B] = torch.from_numpy(mat).to(dev)
-        blk[:len(mine), B] = torch.from_numpy(valid.astype(np.float64)).to(dev)
-    allb = torch.empty((world, nmax, B + 1), dtype=torch.float64, device=dev)
-    if backend == "nccl":
-        dist.all_gather_into_tensor(allb, blk, group=group)
+    if isinstance(mat, torch.Tensor):
+        cm = mat  # (B, n) column-major
+        vt = torch.as_tensor(valid, device=cm.device).to(torch.float64).reshape(1, -1)
     else:
-        dist.all_gather(list(allb.unbind(0)), blk, group=group)
-    allb = allb.cpu().numpy()
-    out = np.zeros((len(regions), B))
-    v = np.zeros(len(regions), dtype=bool)
+        cm = torch.from_numpy(np.ascontiguousarray(np.asarray(mat, dtype=np.float64).T))
+        vt = torch.from_numpy(np.asarray(valid, dtype=np.float64)).reshape(1, -1)
+    B = int(cm.shape[0])
+    if gather is None and world > 1:
+        return mine, cm.T.cpu().numpy() if not as_tensor else cm, vt[0].cpu().numpy() != 0
+    backend = dist.get_backend(group) if world > 1 else None
+    dev = cm.device if (backend in (None, "nccl")) else torch.device("cpu")
+    nmax = max(len(s) for s in shards)
+    # one padded block per rank: B rows of values + 1 row of validity, columns = the shard's regions
+    blk = torch.zeros((B + 1, nmax), dtype=torch.float64, device=dev)
+    n = len(mine)
+    if n:
+        blk[:B, :n].copy_(cm[:, :n])
+        blk[B, :n].copy_(vt[0, :n])
+    if world > 1:
+        allb = torch.empty((world, B + 1, nmax), dtype=torch.float64, device=dev)
+        if backend == "nccl":
+            dist.all_gather_into_tensor(allb, blk, group=group)
+        else:
+            dist.all_gather(list(allb.unbind(0)), blk, group=group)
+    else:
+        allb = blk.unsqueeze(0)
+    full = torch.zeros((B + 1, len(regions)), dtype=torch.float64, device=dev)
     for r, idx in enumerate(shards):
-        out[idx] = allb[r, :len(idx), :B]
-        v[idx] = allb[r, :len(idx), B] != 0
-    return out, v
+        if len(idx):
+            full.index_copy_(1, torch.as_tensor(idx, device=dev), allb[r, :, :len(idx)])
+    valid_all = (full[B] != 0).cpu().numpy()
+    if as_tensor:
+        return full[:B], valid_all
+    return full[:B].T.cpu().numpy(), valid_all
 
 
 def gpu_compute(bins, device=None, ignore_strand=True):
@@ -123,7 +133,12 @@ def gpu_compute(bins, device=None, ignore_strand=True):
     def run(shard_reads, shard_regions):
         dev = torch.cuda.current_device() if device is None else device
         rs, levels = _readset(shard_reads, dev, None)
-        return Plan(rs, _rows_from_mask(shard_regions, levels, ignore_strand), bins).run()
+        plan = Plan(rs, _rows_from_mask(shard_regions, levels, ignore_strand), bins)
+        out = plan.empty_output()  # (B, n): the R column-major matrix, stays in HBM
+        valid = torch.empty(max(plan.n_rows, 1), dtype=torch.uint8, device=out.device)
+        plan.execute(out, valid)
+        plan.status()
+        return out, valid[:plan.n_rows]
     return run
 
 

@@ -1,11 +1,14 @@
 """HBM traffic per launch of the pileup kernel from rocprofv3 --pmc passes (tools/pmc.sh).
 
-    python tools/pmc_traffic.py PMC_DIR [OUT_JSON]
+    python tools/pmc_traffic.py PMC_DIR [OUT_JSON] [CALIB_JSON]
 
 Reads PMC_DIR/fetch/*_counter_collection.csv (FETCH_SIZE) and PMC_DIR/write/... (WRITE_SIZE),
 both in KiB per dispatch, averages over the pileup kernel's dispatches (lean or general) and applies the gfx950
-correction of MI355X_MICROARCH.md (HBM section): FETCH_SIZE reports half the bytes of wide
-coalesced reads, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.
+correction: MI355X_MICROARCH.md (HBM section) documents FETCH_SIZE = 1/2 of the bytes for
+16-B-per-lane coalesced reads; the pileup streams 8-B int2 reads, so the factor measured for
+that shape by tools/fetch_calib.hip (CALIB_JSON from tools/pmc_calib.py, kernel read8_plain)
+is used when given, else x2.  WRITE_SIZE: the calibrated factor of the 8-B non-temporal
+column-segment stores (write8_seg16), else as is.
 PMC_DIR/meta.json (written by tools/prof_c4.py via PROF_META) names the workload so bench.py
 only attaches the number to the same configuration.
 """
@@ -21,7 +24,7 @@ KERNELS = ("rcp_pileup_lean_kernel<", "rcp_pileup_kernel<")  # whichever the pla
 def per_launch(path, counter):
     for kernel in KERNELS:
         vals = []
-        for f in glob.glob(os.path.join(path, "*counter_collection.csv")):
+        for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
                 if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
                     vals.append(float(row["Counter_Value"]) * 1024.0)
@@ -33,13 +36,20 @@ def per_launch(path, counter):
 def main():
     d = sys.argv[1]
     out = sys.argv[2] if len(sys.argv) > 2 else None
+    fk, wk, how = 2.0, 1.0, "FETCH_SIZE x2 (guide's 16-B/lane rule), WRITE_SIZE as is"
+    if len(sys.argv) > 3:
+        cal = json.load(open(sys.argv[3]))
+        fk = cal["fetch_factor"]["read8_plain"]
+        wk = cal["write_factor"].get("write8_seg16", 1.0)
+        how = (f"FETCH_SIZE x{fk:.3f} (calibrated: 8-B/lane int2 streaming reads, tools/fetch_calib.hip), "
+               f"WRITE_SIZE x{wk:.3f} (calibrated: 8-B nt column-segment stores)")
     fetch, nf, kernel = per_launch(os.path.join(d, "fetch"), "FETCH_SIZE")
     write, nw, _ = per_launch(os.path.join(d, "write"), "WRITE_SIZE")
     meta = json.load(open(os.path.join(d, "meta.json")))
     res = dict(meta)
-    res.update({"kernel": kernel, "fetch_size_bytes_raw": fetch, "fetch_bytes": 2 * fetch,
-                "write_bytes": write, "hbm_bytes_per_launch": 2 * fetch + write, "dispatches": [nf, nw],
-                "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE as is"})
+    res.update({"kernel": kernel, "fetch_size_bytes_raw": fetch, "fetch_bytes": fk * fetch,
+                "write_size_bytes_raw": write, "write_bytes": wk * write,
+                "hbm_bytes_per_launch": fk * fetch + wk * write, "dispatches": [nf, nw], "correction": how})
     txt = json.dumps(res, indent=1)
     print(txt)
     if out:

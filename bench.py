@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-regions", type=int, default=200000, help="CPU baseline sample (regions)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline: repeat the sample this long")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--sim-shard", default=None, metavar="K/N",
+                    help="one GPU runs exactly rank K's shard of an N-way split (strong-scaling rehearsal)")
     ap.add_argument("--verify-gather", action="store_true",
                     help="N > 1: rank 0 also runs the whole workload alone and checks the gathered matrix bit for bit")
     ap.add_argument("--no-e2e", action="store_true", help="skip the one-off host-to-host timing")
@@ -210,9 +212,12 @@ def main():
     data, rows_all, bins, ovl_all = workload(args, dev)
     R_total = rows_all.n_rows
     n_reads_total = int(data["reads"][1].numel())
-    lo, hi, cuts = shard_of(rows_all, ovl_all, world, rank)
-    rows = subset_rows(rows_all, lo, hi) if world > 1 else rows_all
-    reads = reads_for_rows(data["reads"], rows, len(data["seqlen"])) if world > 1 else data["reads"]
+    s_rank, s_world = rank, world
+    if args.sim_shard:
+        s_rank, s_world = (int(x) for x in args.sim_shard.split("/"))
+    lo, hi, cuts = shard_of(rows_all, ovl_all, s_world, s_rank)
+    rows = subset_rows(rows_all, lo, hi) if s_world > 1 else rows_all
+    reads = reads_for_rows(data["reads"], rows, len(data["seqlen"])) if s_world > 1 else data["reads"]
     if world > 1 and not args.verify_gather:
         data["reads"] = None  # the full read set is not kept on this rank
     R = rows.n_rows
@@ -287,6 +292,8 @@ def main():
         del full
 
     units = R_total * B  # region-bins per step of the whole job
+    if args.sim_shard:
+        units = R * B  # a rehearsal of one shard: its own region-bins
     value = units * args.steps / elapsed
     ovl = int(np.asarray(ovl_all)[lo:hi].sum())
     # 8 B per overlapping (read, segment) + 16 B per region + 8 B per further segment
@@ -314,7 +321,7 @@ def main():
     # ---- CPU baseline (rank 0, N = 1): the oracle on a bounded sample of the same workload
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not args.sim_shard:
         cpu, parity = cpu_baseline(args, data, rows, bins, out, valid, B)
 
     if rank == 0:
@@ -336,7 +343,7 @@ def main():
                 "regions": R_total, "bins": B, "reads": n_reads_total, "samples": 1,
                 "parallelism": f"region-sharded x{world}: one contiguous region shard per GPU, balanced by "
                                f"overlapping reads; no data-path collective",
-                "rank0_shard": {"regions": R, "reads": n_reads},
+                "rank0_shard": {"regions": R, "reads": n_reads, "sim_shard": args.sim_shard},
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,

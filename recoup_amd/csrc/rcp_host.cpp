@@ -22,6 +22,7 @@
 #include "../../include/recoup_amd.h"
 #include "rcp_device.h"
 #include "rcp_rng.h"
+#include "rcp_stage.h"
 
 extern "C" {
 hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
@@ -341,10 +342,11 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
         HIP_TRY(in_start.alloc(4 * n));
         HIP_TRY(in_end.alloc(4 * n));
         HIP_TRY(in_strand.alloc(n));
-        HIP_TRY(hipMemcpyAsync(in_chrom.p, d->chrom, 4 * n, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(in_start.p, d->start, 4 * n, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(in_end.p, d->end, 4 * n, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(in_strand.p, d->strand, n, hipMemcpyHostToDevice, s));
+        // caller-owned pageable arrays (R vectors): pinned double-buffered staging (rcp_stage.h)
+        HIP_TRY(rcp::stage_h2d(in_chrom.p, d->chrom, 4 * n, d->device, s));
+        HIP_TRY(rcp::stage_h2d(in_start.p, d->start, 4 * n, d->device, s));
+        HIP_TRY(rcp::stage_h2d(in_end.p, d->end, 4 * n, d->device, s));
+        HIP_TRY(rcp::stage_h2d(in_strand.p, d->strand, n, d->device, s));
         pc = in_chrom.as<int32_t>();
         ps = in_start.as<int32_t>();
         pe = in_end.as<int32_t>();
@@ -1079,7 +1081,8 @@ extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, con
     if (rc) return rc;
     rc = rcp_plan_status(plan, nullptr);
     if (rc) return rc;
-    if (out && cells) HIP_TRY(hipMemcpy(out, d_out.p, 8 * cells, hipMemcpyDeviceToHost));
+    // into R's allocMatrix memory (pageable): pinned double-buffered staging (rcp_stage.h)
+    if (out && cells) HIP_TRY(rcp::stage_d2h(out, d_out.p, 8 * cells, rs->device, nullptr));
     if (row_valid && plan->n_rows) HIP_TRY(hipMemcpy(row_valid, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost));
     return RCP_OK;
     RCP_CATCH

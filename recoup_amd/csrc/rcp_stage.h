@@ -1,0 +1,30 @@
+// rcp_stage.h -- host <-> device copies of caller-owned (pageable) host memory through pinned
+// staging buffers (rcp_stage.cpp).
+//
+// The one-shot entry points the R shim binds move the reference's data across PCIe: the reads
+// R holds (rcp_readset_create, ~13 B per read) and the R x B double matrix R allocated
+// (rcp_profile: 1.6 GB on C4).  HIP copies pageable memory through small internal staging
+// buffers at 22-48 GB/s and hipHostRegister of the caller's matrix costs ~70 ms per 1.6 GB
+// (profiles/r02/pcie.log); two 64 MB pinned buffers per device, filled / drained by host
+// threads while the DMA engine moves the other one, run at 51-54 GB/s (pinned: 55-57).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace rcp {
+
+// dst (device) <- src (host); returns once the copy has completed on `stream`.
+hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipStream_t stream);
+
+// dst (host) <- src (device), after everything enqueued on `stream` so far; blocks until done.
+// Rows of `width` bytes: src rows are contiguous (src pitch = width), dst rows `dpitch` apart --
+// e.g. one GPU's block of rows of an R column-major matrix (height = columns).
+hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t width, size_t height, int device,
+                        hipStream_t stream);
+
+inline hipError_t stage_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t stream) {
+    return stage_d2h_2d(dst, bytes, src, bytes, 1, device, stream);
+}
+
+}  // namespace rcp

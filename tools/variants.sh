@@ -13,15 +13,14 @@ if [ "$mode" = build ]; then
         name=${spec%%=*}; defs=${spec#*=}
         mkdir -p "$OUT/$name"
         (
-        /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wno-unused-result $defs \
-            -c "$ROOT/recoup_amd/csrc/rcp_kernels.hip" -o "$OUT/$name/k.o" &&
-        /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wno-unused-result $defs \
-            -c "$ROOT/recoup_amd/csrc/rcp_host.cpp" -o "$OUT/$name/h.o" &&
-        /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wno-unused-result \
-            -c "$ROOT/recoup_amd/csrc/rcp_bam.cpp" -o "$OUT/$name/b.o" &&
-        /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/$name/librecoup_amd.so" "$OUT/$name/k.o" "$OUT/$name/h.o" \
-            "$OUT/$name/b.o" -lz -pthread &&
-        rm -f "$OUT/$name/k.o" "$OUT/$name/h.o" "$OUT/$name/b.o"
+        objs=""
+        for src in rcp_kernels.hip rcp_host.cpp rcp_stage.cpp rcp_bam.cpp; do
+            /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wno-unused-result $defs \
+                -c "$ROOT/recoup_amd/csrc/$src" -o "$OUT/$name/$src.o" || exit 1
+            objs="$objs $OUT/$name/$src.o"
+        done
+        /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/$name/librecoup_amd.so" $objs -lz -pthread &&
+        rm -f $objs
         ) &
     done
     wait

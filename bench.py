@@ -229,7 +229,7 @@ def main():
     t1 = time.time()
     rs = ReadSet(*reads, data["seqlen"], device=local)
     tp = time.time()
-    plan = Plan(rs, rows, bins)
+    plan = Plan(rs, rows, bins, out_ld="padded")  # whole 128-B lines per 16-row column segment
     plan_s = time.time() - tp
     B = plan.n_cols
     out = plan.empty_output()

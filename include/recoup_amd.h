@@ -157,13 +157,18 @@ RCP_API int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows, co
  * also routes other mean plans whose chunks fit one wave pass through the lean kernel's
  * general-bins mode.  All choices give bit-identical results.  heavy_threshold: candidate
  * reads per column chunk above which a skewed row is piled by many workgroups first
- * (-1 = default 4096, 0 = never). */
+ * (-1 = default 4096, 0 = never).  out_ld: see the field. */
 enum { RCP_KERNEL_AUTO = 0, RCP_KERNEL_GENERAL = 1, RCP_KERNEL_LEAN_ANY = 2 };
 typedef struct {
     int32_t pileup_kernel;
     int32_t heavy_threshold;
-    int32_t reserved[6];        /* zero */
+    int64_t out_ld;             /* column stride (leading dimension) of d_out / d_binsum in elements:
+                                 * 0 = n_rows (plain R column-major); >= n_rows otherwise.  A multiple
+                                 * of 16 keeps every 16-row column segment on whole 128-B lines
+                                 * (RCP_OUT_LD_PADDED picks the next multiple of 16) */
+    int32_t reserved[4];        /* zero */
 } rcp_plan_opts;
+#define RCP_OUT_LD_PADDED (-1)
 RCP_API int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
                                const rcp_plan_opts* opts, rcp_plan** out);
 RCP_API int rcp_plan_destroy(rcp_plan* plan);

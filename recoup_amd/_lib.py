@@ -67,7 +67,7 @@ class PlanInfo(ctypes.Structure):
 
 class PlanOpts(ctypes.Structure):
     _fields_ = [("pileup_kernel", ctypes.c_int32), ("heavy_threshold", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 6)]
+                ("out_ld", ctypes.c_int64), ("reserved", ctypes.c_int32 * 4)]
 
 
 # every symbol include/recoup_amd.h declares: (name, restype, argtypes)

@@ -359,14 +359,14 @@ def profileMatrix(input, flank, binParams, rc=None, keep_on_device=False):
     for s, cv in zip(input, cvs):
         bins = _profile_bins(binParams, flank, equal, _base_size(cv) if equal else 0)
         bins.scale = cv.scale
-        plan = Plan(cv.readset, cv.rows, bins)
+        plan = Plan(cv.readset, cv.rows, bins, out_ld="padded")
         out = plan.empty_output()
         valid = torch.empty(max(plan.n_rows, 1), dtype=torch.uint8, device=out.device)
         plan.execute(out, valid)
         plan.status()
-        s["profile"] = RMatrix(out.cpu().numpy().T, cv.names)
+        s["profile"] = RMatrix(out[:, :plan.n_rows].cpu().numpy().T, cv.names)
         if keep_on_device:
-            s["profile_device"] = out
+            s["profile_device"] = out[:, :plan.n_rows]
     return input
 
 
@@ -408,16 +408,16 @@ def recoupProfiles(input, genomeRanges, region, flank, binParams, keep_on_device
         fuse = heat is not None and prof.interp == heat.interp and prof.stat == heat.stat
         bins = Bins(parts + (heat.parts if fuse else []), flank=(f1, f2), stat=prof.stat, interp=prof.interp,
                     scale=cv.scale)
-        plan = Plan(cv.readset, cv.rows, bins)
+        plan = Plan(cv.readset, cv.rows, bins, out_ld="padded")
         out = plan.empty_output()
         valid = torch.empty(max(plan.n_rows, 1), dtype=torch.uint8, device=out.device)
         plan.execute(out, valid)
         plan.status()
-        full = out.cpu().numpy().T
+        full = out[:, :plan.n_rows].cpu().numpy().T
         npc = prof.n_cols
         s["profile"] = RMatrix(full[:, :npc], cv.names)
         if keep_on_device:
-            s["profile_device"] = out
+            s["profile_device"] = out[:, :plan.n_rows]
         if heat is not None:
             if fuse:
                 s["heatmap"] = RMatrix(full[:, npc:], cv.names)

@@ -112,6 +112,7 @@ struct RcpPlanDev {
     int32_t stat;               // 0 mean, 1 median
     double scale;
     int64_t n_cols;
+    int64_t out_ld;             // column stride of out / binsum in doubles (>= n_rows; rcp_plan_opts.out_ld)
     // interpolation rows
     int32_t n_interp;
     const int32_t* interp_row;  // [n_interp]

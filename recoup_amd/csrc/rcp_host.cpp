@@ -399,6 +399,7 @@ struct rcp_plan {
     DevBuf work;       // seg_lo / seg_hi / valid / status
     DevBuf scratch;    // interpolation scratch
     int32_t max_row_len = 0;
+    int64_t out_ld = 0;
 };
 
 namespace {
@@ -534,7 +535,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
                                   const rcp_plan_opts* opts, rcp_plan** out) {
     RCP_TRY
     if (!rs || !rows || !out) return fail(RCP_EINVAL, "NULL argument");
-    const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, {0, 0, 0, 0, 0, 0}};
+    const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, 0, {0, 0, 0, 0}};
     if (!opts) opts = &default_opts;
     if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_LEAN_ANY)
         return fail(RCP_EINVAL, "pileup_kernel = %d", opts->pileup_kernel);
@@ -716,6 +717,11 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     }
     P.n_cols = col;
     plan->n_cols = col;
+    if (opts->out_ld == RCP_OUT_LD_PADDED) P.out_ld = ((int64_t)R + 15) & ~int64_t(15);
+    else if (opts->out_ld == 0) P.out_ld = R;
+    else if (opts->out_ld >= R) P.out_ld = opts->out_ld;
+    else return fail(RCP_EINVAL, "out_ld = %lld < n_rows = %d", (long long)opts->out_ld, R);
+    plan->out_ld = P.out_ld;
     wave_geometry(chunk_cap, &P.wave_words, &P.chunk_cap);
     P.stage_cap = stage_cap;
     P.interp_cap = std::max(max_interp_len, 1);
@@ -1068,12 +1074,15 @@ extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, con
                            uint8_t* row_valid) {
     RCP_TRY
     rcp_plan* plan = nullptr;
-    int rc = rcp_plan_create(rs, rows, bins, &plan);
+    // padded column stride on the device (whole 128-B lines per 16-row column segment); the
+    // staged copy drops the padding on the way into R's n_rows x n_cols matrix
+    rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, {0, 0, 0, 0}};
+    int rc = rcp_plan_create_ex(rs, rows, bins, &opts, &plan);
     if (rc) return rc;
     std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
     DeviceGuard g(rs->device);
     HIP_TRY(g.err);
-    const size_t cells = (size_t)plan->n_rows * (size_t)plan->n_cols;
+    const size_t cells = (size_t)plan->out_ld * (size_t)plan->n_cols;
     DevBuf d_out, d_valid;
     HIP_TRY(d_out.alloc(8 * std::max<size_t>(cells, 1)));
     HIP_TRY(d_valid.alloc(std::max<int32_t>(plan->n_rows, 1)));
@@ -1082,7 +1091,9 @@ extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, con
     rc = rcp_plan_status(plan, nullptr);
     if (rc) return rc;
     // into R's allocMatrix memory (pageable): pinned double-buffered staging (rcp_stage.h)
-    if (out && cells) HIP_TRY(rcp::stage_d2h(out, d_out.p, 8 * cells, rs->device, nullptr));
+    if (out && plan->n_rows && plan->n_cols)
+        HIP_TRY(rcp::stage_d2h_2d(out, 8 * (size_t)plan->n_rows, d_out.p, 8 * (size_t)plan->out_ld,
+                                  8 * (size_t)plan->n_rows, (size_t)plan->n_cols, rs->device, nullptr));
     if (row_valid && plan->n_rows) HIP_TRY(hipMemcpy(row_valid, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost));
     return RCP_OK;
     RCP_CATCH

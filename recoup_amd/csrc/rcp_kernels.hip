@@ -1351,7 +1351,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
         const RowMeta& mr = meta[rbase + ii];
         const int32_t flag = mr.flag, kend = mr.kend, bs = mr.bs, lay = mr.lay;
         if (r >= P.n_rows || flag == 2) return;
-        const size_t R = (size_t)P.n_rows;
+        const size_t R = (size_t)P.out_ld;  // column stride of the output (>= n_rows)
         constexpr int kQuads = kPBlock / T;  // column quads per pass
         constexpr int kStep = 4 * kQuads;    // columns per pass
         const int32_t kq = k0 + 4 * (tid / T);
@@ -1965,7 +1965,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         const int st = tid - 64 * kPWaves;
         const int ii = st & (T - 1);
         const int qd = st / T;
-        const size_t R = (size_t)P.n_rows;
+        const size_t R = (size_t)P.out_ld;  // column stride of the output (>= n_rows)
         const double sc = P.scale;
         const int npass = (P.stage_cap + 4 * kLQuads - 1) / (4 * kLQuads);
         constexpr int kPass = GEN ? kLMaxPassGen : kLMaxPass;
@@ -2256,7 +2256,7 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
     const int r = P.interp_row[e];
     const RcpPart part = P.part[P.interp_part[e]];
     const int n = part.n_bins;
-    const size_t R = (size_t)P.n_rows;
+    const size_t R = (size_t)P.out_ld;  // column stride of the output (>= n_rows)
     if (!P.valid[r]) {
         for (int k = threadIdx.x; k < n; k += kBlock) out[(size_t)(part.col_off + k) * R + r] = 0.0;
         return;

@@ -165,26 +165,32 @@ hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipSt
     return e != hipSuccess ? e : e2;
 }
 
-hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t width, size_t height, int device,
-                        hipStream_t stream) {
-    const size_t bytes = width * height;
-    if (bytes == 0) return hipSuccess;
+hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
+                        int device, hipStream_t stream) {
+    if (width == 0 || height == 0) return hipSuccess;
+    // the device bytes moved: rows with their padding, except after the last row
+    const size_t bytes = spitch * (height - 1) + width;
     Stager* st = stager(device);
     if (bytes < kDirect || !st) {
-        hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, width, width, height, hipMemcpyDeviceToHost, stream);
+        hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost, stream);
         return e == hipSuccess ? hipStreamSynchronize(stream) : e;
     }
     std::lock_guard<std::mutex> g(st->mu);
     if (!ready(st)) {
-        hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, width, width, height, hipMemcpyDeviceToHost, stream);
+        hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost, stream);
         return e == hipSuccess ? hipStreamSynchronize(stream) : e;
     }
     const char* s = static_cast<const char*>(src);
     char* d = static_cast<char*>(dst);
-    // source bytes [a, z) of the linear (contiguous) device block -> their host rows
+    // device bytes [a, z) of the linear span -> their host rows (padding bytes skipped)
     auto scatter = [&](const char* pin, size_t base, size_t a, size_t z) {
         while (a < z) {
-            const size_t row = a / width, off = a % width, n = std::min(z - a, width - off);
+            const size_t row = a / spitch, off = a % spitch;
+            if (off >= width) {
+                a = (row + 1) * spitch;
+                continue;
+            }
+            const size_t n = std::min(z - a, width - off);
             std::memcpy(d + row * dpitch + off, pin + (a - base), n);
             a += n;
         }

@@ -18,13 +18,14 @@ namespace rcp {
 hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipStream_t stream);
 
 // dst (host) <- src (device), after everything enqueued on `stream` so far; blocks until done.
-// Rows of `width` bytes: src rows are contiguous (src pitch = width), dst rows `dpitch` apart --
-// e.g. one GPU's block of rows of an R column-major matrix (height = columns).
-hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t width, size_t height, int device,
-                        hipStream_t stream);
+// `height` rows of `width` bytes, `spitch` apart on the device and `dpitch` apart on the host --
+// e.g. a column-major matrix with a padded device leading dimension, or one GPU's block of rows
+// of the caller's R matrix (rows = columns of the matrix).
+hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
+                        int device, hipStream_t stream);
 
 inline hipError_t stage_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t stream) {
-    return stage_d2h_2d(dst, bytes, src, bytes, 1, device, stream);
+    return stage_d2h_2d(dst, bytes, src, bytes, bytes, 1, device, stream);
 }
 
 }  // namespace rcp

@@ -146,15 +146,18 @@ class Bins:
 class Plan:
     """One fused coverage -> profile pass of ``rows`` over ``readset`` with ``bins``."""
 
-    def __init__(self, readset, rows, bins, kernel="auto", heavy_threshold=-1):
+    def __init__(self, readset, rows, bins, kernel="auto", heavy_threshold=-1, out_ld=0):
         """``kernel``: "auto" | "general" | "lean_any" (rcp_plan_opts.pileup_kernel; every choice
-        gives bit-identical results); ``heavy_threshold``: -1 default, 0 off."""
+        gives bit-identical results); ``heavy_threshold``: -1 default, 0 off; ``out_ld``: the
+        output's column stride, 0 = n_rows, "padded" = the next multiple of 16 (whole 128-B
+        lines per 16-row column segment), or any value >= n_rows."""
         self.readset = readset  # keeps the device reads alive
         self.rows = rows
         self.bins = bins
         rd = rows.desc()
         bd = ctypes.byref(bins.desc()) if bins is not None else None
-        opts = _lib.PlanOpts(KERNEL[kernel] if isinstance(kernel, str) else int(kernel), int(heavy_threshold))
+        ld = -1 if out_ld == "padded" else int(out_ld)
+        opts = _lib.PlanOpts(KERNEL[kernel] if isinstance(kernel, str) else int(kernel), int(heavy_threshold), ld)
         h = ctypes.c_void_p()
         with torch.cuda.device(readset.device):
             check(_lib.lib().rcp_plan_create_ex(readset.h, ctypes.byref(rd), bd, ctypes.byref(opts),
@@ -165,6 +168,7 @@ class Plan:
         self.info = {k: getattr(info, k) for k, _ in _lib.PlanInfo._fields_}
         self.n_rows = rows.n_rows
         self.n_cols = int(info.n_cols)
+        self.out_ld = ((self.n_rows + 15) // 16 * 16 if ld == -1 else (ld or self.n_rows))
         self.device = readset.device
 
     def row_lengths(self):
@@ -173,7 +177,8 @@ class Plan:
         return out
 
     def empty_output(self):
-        return torch.empty((self.n_cols, self.n_rows), dtype=torch.float64, device=f"cuda:{self.device}")
+        """The device output: (n_cols, out_ld) float64; columns [:, :n_rows] are the R matrix."""
+        return torch.empty((self.n_cols, self.out_ld), dtype=torch.float64, device=f"cuda:{self.device}")
 
     def execute(self, out=None, valid=None, binsum=None, stream=None):
         """Enqueue the pass.  ``out`` is a CUDA float64 tensor holding the R column-major
@@ -236,10 +241,10 @@ class Plan:
         bs = torch.empty_like(out, dtype=torch.int64) if binsum else None
         self.execute(out, valid, bs, stream)
         self.status(stream)
-        mat = out.cpu().numpy().T  # (n_rows, n_cols) view of the column-major buffer: F order
+        mat = out[:, :self.n_rows].cpu().numpy().T  # (n_rows, n_cols) view of the column-major buffer
         v = valid[:self.n_rows].cpu().numpy().astype(bool)
         if binsum:
-            return mat, v, bs.cpu().numpy().T
+            return mat, v, bs[:, :self.n_rows].cpu().numpy().T
         return mat, v
 
     def close(self):

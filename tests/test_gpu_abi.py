@@ -96,3 +96,22 @@ def test_readset_info_and_strand_filter(c1):
     st[10:20] = 5
     r = ReadSet(bad, s["start"], s["end"], st, s["seqlengths"])
     assert r.n == len(s["start"]) - 20
+
+
+@pytest.mark.parametrize("n_rows,n_bins", [(20_003, 200), (4_099, 4000)])
+def test_rcp_profile_staged_copy(gpu, n_rows, n_bins):
+    """rcp_profile's output above the 4 MB direct-copy limit travels through the pinned
+    double-buffered stager (64 MB chunks, 4 host threads) from a padded device column stride
+    (n_rows rounded up to 16) into R's n_rows x n_cols matrix: bit-equal to the device result."""
+    from recoup_amd.engine import ReadSet
+    from tests.test_gpu_random import CHROM_LEN, make_reads, single_rows
+    rng = np.random.default_rng(n_rows)
+    reads = make_reads(rng, 300_000)
+    rows = single_rows(rng, n_rows, 4000)
+    bins = Bins([("whole", n_bins)])
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    ref, rv = Plan(rs, rows, bins).run()
+    rc, out, valid = _profile(rs, rows, bins)
+    assert rc == 0 and out.nbytes > (4 << 20)
+    assert np.array_equal(out.view(np.uint64), np.asfortranarray(ref).view(np.uint64))
+    np.testing.assert_array_equal(valid.astype(bool), rv)

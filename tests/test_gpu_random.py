@@ -342,3 +342,33 @@ def test_empty_inputs(gpu):
                      np.zeros(0, np.int8))
     mat, valid = Plan(rs, empty, Bins([("whole", 10)])).run()
     assert mat.shape == (0, 10)
+
+
+@pytest.mark.parametrize("kernel,n_bins,stat", [("auto", 1000, "mean"), ("general", 150, "mean"),
+                                                ("general", 64, "median"), ("auto", 0, "mean")])
+def test_output_leading_dimension(gpu, kernel, n_bins, stat):
+    """rcp_plan_opts.out_ld: a padded column stride (multiple of 16 rows) or any ld >= n_rows
+    gives the same bits in columns [:, :n_rows] as the plain R layout; interpolated rows
+    (700-bp rows, 1000 bins) write through the same stride.  The padding is never written."""
+    import torch
+    from recoup_amd.engine import Bins, Plan, ReadSet
+    rng = np.random.default_rng(91)
+    reads = make_reads(rng, 80_000)
+    rows = single_rows(rng, 333, 2000)
+    rows.end[::7] = rows.start[::7] + 699  # L < n bins: the interpolation kernel
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    bins = Bins([("whole", n_bins)], stat=stat) if n_bins else Bins([("whole", 0, 2000)])
+    if n_bins == 0:
+        rows.end[::7] = rows.start[::7] + 1999
+    ref = Plan(rs, rows, bins, kernel=kernel).run()
+    for ld in ("padded", 341, 400):
+        plan = Plan(rs, rows, bins, kernel=kernel, out_ld=ld)
+        out = torch.full((plan.n_cols, plan.out_ld), -7.0, dtype=torch.float64, device="cuda:0")
+        valid = torch.empty(333, dtype=torch.uint8, device="cuda:0")
+        plan.execute(out, valid)
+        plan.status()
+        assert plan.out_ld == (336 if ld == "padded" else ld)
+        got = out[:, :333].cpu().numpy().T
+        assert np.array_equal(got.view(np.uint64), ref[0].view(np.uint64))
+        np.testing.assert_array_equal(valid.cpu().numpy().astype(bool), ref[1])
+        assert bool(torch.all(out[:, 333:] == -7.0))

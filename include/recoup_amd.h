@@ -207,6 +207,28 @@ RCP_API int rcp_plan_row_lengths(const rcp_plan* plan, int64_t* out_len);
 RCP_API int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
                 double* out, uint8_t* row_valid);
 
+/* Profiles of a coverage list the caller holds as run-length encoded vectors -- the reference's
+ * own `$coverage` object, a named list of S4Vectors::Rle (R/coverage.R:171-173) -- as
+ * binCoverageMatrix / baseCoverageMatrix consume it (R/profile.R:100-212) when recoup() reuses a
+ * stored or sliced coverage (R/recoup.R:126-135, R/util.R:209-210, :311-320).  Row r's runs are
+ * run_off[r] .. run_off[r+1]-1 (runValue / runLength of the Rle); exactly one of ivalues (an
+ * integer Rle, as calcCoverage returns it) and dvalues (a numeric Rle, e.g. after
+ * normalize = "linear", R/recoup.R:559-577) is given.  is_null[r] = 1 marks a NULL list element
+ * (a zero row, row_valid = 0).  bins as for rcp_profile (parts, stat, interpolation, R-RNG bin
+ * layouts, scale); out: host R column-major n_rows x n_cols.  Integer Rle rows give the same
+ * bits as the read path (numerators in int64, mean = numerator * scale / width); numeric Rle
+ * means are double-double sums / width (within 1e-15 relative of R's long-double mean). */
+typedef struct {
+    int32_t n_rows;
+    const int64_t* run_off;     /* [n_rows + 1], run_off[0] = 0 */
+    const int32_t* lengths;     /* [n_runs] > 0 */
+    const int32_t* ivalues;     /* [n_runs] or NULL */
+    const double* dvalues;      /* [n_runs] or NULL */
+    const uint8_t* is_null;     /* [n_rows] or NULL (no NULL elements) */
+} rcp_rle_desc;
+RCP_API int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out,
+                            uint8_t* row_valid);
+
 /* calcCoverage: per-row integer depth vectors (CSR).  out_off is the host prefix sum of
  * rcp_plan_row_lengths(); d_cov (device int32 [out_off[n_rows]]) receives each valid row's
  * depth at its offset; d_valid (device) the NULL mask.  Rows are in the row's own

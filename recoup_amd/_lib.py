@@ -65,6 +65,11 @@ class PlanInfo(ctypes.Structure):
                 ("chunk_positions", ctypes.c_int32), ("pileup_kernel", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class RleDesc(ctypes.Structure):
+    _fields_ = [("n_rows", ctypes.c_int32), ("run_off", _i64p), ("lengths", _i32p), ("ivalues", _i32p),
+                ("dvalues", _dp), ("is_null", _u8p)]
+
+
 class PlanOpts(ctypes.Structure):
     _fields_ = [("pileup_kernel", ctypes.c_int32), ("heavy_threshold", ctypes.c_int32),
                 ("out_ld", ctypes.c_int64), ("reserved", ctypes.c_int32 * 4)]
@@ -91,6 +96,7 @@ SIGNATURES = [
     ("rcp_plan_row_lengths", ctypes.c_int, [_vp, _i64p]),
     ("rcp_profile", ctypes.c_int, [_vp, ctypes.POINTER(RowsDesc), ctypes.POINTER(BinsDesc), _dp, _u8p]),
     ("rcp_calc_coverage", ctypes.c_int, [_vp, _i64p, _vp, _vp, _vp]),
+    ("rcp_profile_rle", ctypes.c_int, [ctypes.POINTER(RleDesc), ctypes.POINTER(BinsDesc), ctypes.c_int, _dp, _u8p]),
     ("rcp_rle_encode", ctypes.c_int, [ctypes.c_int32, _i64p, _vp, ctypes.c_int, _vp, _vp, _i64p, _i64p, _vp]),
     ("rcp_bam_read", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                     ctypes.POINTER(_vp)]),

@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .engine import Bins, Plan, ReadSet, RowTable
+from .engine import Bins, Plan, ReadSet, RowTable, profile_rle
 from .granges import GRanges, GRangesList, getFlankingRanges, getRegionalRanges
 
 
@@ -65,6 +65,11 @@ class Rle:
 
     def decode(self):
         return np.repeat(self.values, self.lengths)
+
+    def __mul__(self, k):  # Rle * numeric -> numeric Rle (normalize = "linear", R/recoup.R:559-577)
+        return Rle(self.values * k, self.lengths)
+
+    __rmul__ = __mul__
 
     def __repr__(self):
         return f"Rle({len(self)} positions in {len(self.values)} runs)"
@@ -271,30 +276,43 @@ def coverageRnaRef(input, genomeRanges, helperRanges, flank=(2000, 2000), strand
 
 
 # ------------------------------------------------------------------------------ profile
-def _as_device_coverage(cvrg):
+def _as_coverage(cvrg):
+    """A DeviceCoverage (reads in HBM + row table: the fused pass), or a host coverage list --
+    the reference's own ``$coverage`` object: a list of Rle / vectors / None (profiled from its
+    runs by rcp_profile_rle)."""
     if isinstance(cvrg, DeviceCoverage):
         return cvrg
-    raise _lib.UnsupportedError(-4, "profiles are computed from a DeviceCoverage (coverageRef / coverageRnaRef); "
-                                    "materialised coverage lists are not re-uploaded")
+    if isinstance(cvrg, (list, tuple)):
+        return cvrg if isinstance(cvrg, CoverageList) else CoverageList(list(cvrg), getattr(cvrg, "names", None))
+    raise TypeError("a coverage must be a DeviceCoverage or a list of Rle / vectors / None")
 
 
-def _run(cv, bins):
-    plan = Plan(cv.readset, cv.rows, bins)
-    mat, _ = plan.run()
+def _run(cv, bins, device=None):
+    if isinstance(cv, DeviceCoverage):
+        plan = Plan(cv.readset, cv.rows, bins)
+        mat, _ = plan.run()
+        return RMatrix(mat, cv.names)
+    mat, _ = profile_rle(cv, bins, device=_device(device))
     return RMatrix(mat, cv.names)
 
 
-def binCoverageMatrix(cvrg, binSize=1000, stat="mean", interpolation="auto", flank=None, where="center", rc=None):
-    """R/profile.R:153-212: splitVector of each (sliced) coverage vector into binSize bins."""
-    cv = _as_device_coverage(cvrg)
+def _scale_of(cv):
+    return cv.scale if isinstance(cv, DeviceCoverage) else 1.0  # a host list holds scaled values
+
+
+def binCoverageMatrix(cvrg, binSize=1000, stat="mean", interpolation="auto", flank=None, where="center", rc=None,
+                      device=None):
+    """R/profile.R:153-212: splitVector of each (sliced) coverage vector into binSize bins.
+    ``cvrg``: a DeviceCoverage or the reference's list of Rle (None = NULL)."""
+    cv = _as_coverage(cvrg)
     stat = str(_first(stat, "mean")).lower()
     interpolation = _first(interpolation, "auto")
     where = _first(where, "center")
     if flank is None:
-        bins = Bins([("whole", int(binSize))], stat=stat, interp=interpolation, scale=cv.scale)
+        bins = Bins([("whole", int(binSize))], stat=stat, interp=interpolation, scale=_scale_of(cv))
     else:
-        bins = Bins([(where, int(binSize))], flank=flank, stat=stat, interp=interpolation, scale=cv.scale)
-    return _run(cv, bins)
+        bins = Bins([(where, int(binSize))], flank=flank, stat=stat, interp=interpolation, scale=_scale_of(cv))
+    return _run(cv, bins, device)
 
 
 def _base_size(cv):
@@ -304,16 +322,17 @@ def _base_size(cv):
     return int(ln[0]) if len(ln) and ln[0] > 0 else (int(nz[0]) if len(nz) else 0)
 
 
-def baseCoverageMatrix(cvrg, flank=None, where="upstream", rc=None):
-    """R/profile.R:100-151: per-base coverage rows (NULL -> zeros)."""
-    cv = _as_device_coverage(cvrg)
+def baseCoverageMatrix(cvrg, flank=None, where="upstream", rc=None, device=None):
+    """R/profile.R:100-151: per-base coverage rows (NULL -> zeros); ``cvrg`` as for
+    binCoverageMatrix."""
+    cv = _as_coverage(cvrg)
     where = _first(where, "upstream")
     if flank is None:
-        bins = Bins([("whole", 0, _base_size(cv))], scale=cv.scale)
+        bins = Bins([("whole", 0, _base_size(cv))], scale=_scale_of(cv))
     else:
         size = int(flank[0]) if where == "upstream" else int(flank[1])
-        bins = Bins([(where, 0, size)], flank=flank, scale=cv.scale)
-    return _run(cv, bins)
+        bins = Bins([(where, 0, size)], flank=flank, scale=_scale_of(cv))
+    return _run(cv, bins, device)
 
 
 def _profile_bins(binParams, flank, equal, size):
@@ -344,6 +363,22 @@ def _profile_bins(binParams, flank, equal, size):
     return Bins(parts, flank=(f1, f2), stat=stat, interp=interp)
 
 
+def _profile_pass(cv, bins, keep_on_device=False, device=None):
+    """One fused pass over a coverage: (R x n_cols host matrix, device (n_cols, R) view or None).
+    A DeviceCoverage runs the read plan (padded column stride); a host list the Rle path."""
+    if isinstance(cv, DeviceCoverage):
+        bins.scale = cv.scale
+        plan = Plan(cv.readset, cv.rows, bins, out_ld="padded")
+        out = plan.empty_output()
+        valid = torch.empty(max(plan.n_rows, 1), dtype=torch.uint8, device=out.device)
+        plan.execute(out, valid)
+        plan.status()
+        return out[:, :plan.n_rows].cpu().numpy().T, (out[:, :plan.n_rows] if keep_on_device else None)
+    mat, _ = profile_rle(cv, bins, device=_device(device))
+    return mat, (torch.from_numpy(np.ascontiguousarray(mat.T)).to(f"cuda:{_device(device)}")
+                 if keep_on_device else None)
+
+
 def profileMatrix(input, flank, binParams, rc=None, keep_on_device=False):
     """R/profile.R:1-98: per-sample R x B double matrix in ``sample["profile"]``.
 
@@ -352,21 +387,16 @@ def profileMatrix(input, flank, binParams, rc=None, keep_on_device=False):
     ``sample["profile_device"]`` (shape (B, R) in torch terms)."""
     if not _needs(input, "profile"):
         return input
-    cvs = [_as_device_coverage(s["coverage"]) for s in input]
+    cvs = [_as_coverage(s["coverage"]) for s in input]
     ln = cvs[0].lengths()
     ln = ln[ln != 0]
     equal = bool(np.all(ln == ln[0])) if len(ln) else True
     for s, cv in zip(input, cvs):
         bins = _profile_bins(binParams, flank, equal, _base_size(cv) if equal else 0)
-        bins.scale = cv.scale
-        plan = Plan(cv.readset, cv.rows, bins, out_ld="padded")
-        out = plan.empty_output()
-        valid = torch.empty(max(plan.n_rows, 1), dtype=torch.uint8, device=out.device)
-        plan.execute(out, valid)
-        plan.status()
-        s["profile"] = RMatrix(out[:, :plan.n_rows].cpu().numpy().T, cv.names)
+        mat, dev = _profile_pass(cv, bins, keep_on_device)
+        s["profile"] = RMatrix(mat, cv.names)
         if keep_on_device:
-            s["profile_device"] = out[:, :plan.n_rows]
+            s["profile_device"] = dev
     return input
 
 
@@ -392,7 +422,7 @@ def recoupProfiles(input, genomeRanges, region, flank, binParams, keep_on_device
         raise _lib.SemanticError(-5, "recoup.R:703: object 'forcedBinSize' not found (the reference's forced "
                                      "heatmap binning of a non-base region)")
     fbs = bp.get("forcedBinSize", (50, 200))
-    cvs = [_as_device_coverage(s["coverage"]) for s in input]
+    cvs = [_as_coverage(s["coverage"]) for s in input]
     ln = cvs[0].lengths()
     ln = ln[ln != 0]
     equal = bool(np.all(ln == ln[0])) if len(ln) else True
@@ -406,23 +436,17 @@ def recoupProfiles(input, genomeRanges, region, flank, binParams, keep_on_device
             # interpolation "auto" (R/recoup.R:664-668)
             heat = Bins([("whole", int(fbs[1]))], stat=stat, interp="auto")
         fuse = heat is not None and prof.interp == heat.interp and prof.stat == heat.stat
-        bins = Bins(parts + (heat.parts if fuse else []), flank=(f1, f2), stat=prof.stat, interp=prof.interp,
-                    scale=cv.scale)
-        plan = Plan(cv.readset, cv.rows, bins, out_ld="padded")
-        out = plan.empty_output()
-        valid = torch.empty(max(plan.n_rows, 1), dtype=torch.uint8, device=out.device)
-        plan.execute(out, valid)
-        plan.status()
-        full = out[:, :plan.n_rows].cpu().numpy().T
+        bins = Bins(parts + (heat.parts if fuse else []), flank=(f1, f2), stat=prof.stat, interp=prof.interp)
+        full, dev = _profile_pass(cv, bins, keep_on_device)
         npc = prof.n_cols
         s["profile"] = RMatrix(full[:, :npc], cv.names)
         if keep_on_device:
-            s["profile_device"] = out[:, :plan.n_rows]
+            s["profile_device"] = dev
         if heat is not None:
             if fuse:
                 s["heatmap"] = RMatrix(full[:, npc:], cv.names)
             else:
-                heat.scale = cv.scale
+                heat.scale = _scale_of(cv)
                 s["heatmap"] = _run(cv, heat)
     return input
 

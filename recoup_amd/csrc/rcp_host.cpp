@@ -21,6 +21,7 @@
 
 #include "../../include/recoup_amd.h"
 #include "rcp_device.h"
+#include "rcp_rle.h"
 #include "rcp_rng.h"
 #include "rcp_stage.h"
 
@@ -1172,6 +1173,236 @@ extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int3
     HIP_TRY(hipMemcpyAsync(run_off, d_run_off.p, 8 * ((size_t)n_rows + 1), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     *n_runs = nr;
+    return RCP_OK;
+    RCP_CATCH
+}
+
+// =====================================================================================
+// profiles of a host coverage list of Rle (the reference's $coverage object)
+// =====================================================================================
+namespace {
+
+// R/profile.R slices: where -> [lo, hi) relative to the row length (see RcpPart)
+bool part_slice_spec(int where, int32_t f1, int32_t f2, RcpPart* pt) {
+    switch (where) {
+        case RCP_WHERE_WHOLE: pt->lo_off = 0; pt->lo_end = 0; pt->hi_off = 0; pt->hi_end = 1; return true;
+        case RCP_WHERE_CENTER: pt->lo_off = f1; pt->lo_end = 0; pt->hi_off = -f2; pt->hi_end = 1; return true;
+        case RCP_WHERE_UPSTREAM: pt->lo_off = 0; pt->lo_end = 0; pt->hi_off = f1; pt->hi_end = 0; return true;
+        case RCP_WHERE_DOWNSTREAM: pt->lo_off = -f2; pt->lo_end = 1; pt->hi_off = 0; pt->hi_end = 1; return true;
+        default: return false;
+    }
+}
+
+}  // namespace
+
+extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out,
+                               uint8_t* row_valid) {
+    RCP_TRY
+    if (!cov || !bins) return fail(RCP_EINVAL, "NULL argument");
+    const int32_t R = cov->n_rows;
+    if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
+    if (R > 0 && !cov->run_off) return fail(RCP_EINVAL, "NULL run_off");
+    if (bins->n_parts < 1 || bins->n_parts > RCP_MAX_PARTS) return fail(RCP_EINVAL, "n_parts = %d", bins->n_parts);
+    if (bins->stat != RCP_STAT_MEAN && bins->stat != RCP_STAT_MEDIAN) return fail(RCP_EINVAL, "stat = %d", bins->stat);
+    if (bins->interp < 0 || bins->interp > 3) return fail(RCP_EINVAL, "interp = %d", bins->interp);
+    if (bins->flank[0] < 0 || bins->flank[1] < 0) return fail(RCP_EINVAL, "negative flank");
+    const bool dbl = cov->dvalues != nullptr;
+    const int64_t n_runs = R > 0 ? cov->run_off[R] : 0;
+    if (R > 0 && cov->run_off[0] != 0) return fail(RCP_EINVAL, "run_off[0] != 0");
+    for (int32_t r = 0; r < R; ++r)
+        if (cov->run_off[r + 1] < cov->run_off[r]) return fail(RCP_EINVAL, "run_off decreases at row %d", r);
+    if (n_runs > 0 && (!cov->lengths || (!cov->ivalues && !cov->dvalues)))
+        return fail(RCP_EINVAL, "NULL lengths / values");
+    if (cov->ivalues && cov->dvalues) return fail(RCP_EINVAL, "both integer and numeric values given");
+    // Rle lengths are positive and every row fits int32 positions
+    {
+        std::vector<int64_t> rl(std::max(R, 1), 0);
+        for (int32_t r = 0; r < R; ++r) {
+            int64_t acc = 0;
+            int32_t mn = INT32_MAX;
+            for (int64_t j = cov->run_off[r]; j < cov->run_off[r + 1]; ++j) {
+                acc += cov->lengths[j];
+                mn = std::min(mn, cov->lengths[j]);
+            }
+            if (mn <= 0) return fail(RCP_EINVAL, "row %d: an Rle run length <= 0", r);
+            if (acc >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "row %d: %lld positions", r, (long long)acc);
+        }
+    }
+    if (n_runs >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "%lld runs", (long long)n_runs);
+    int rc = check_device(device);
+    if (rc) return rc;
+    DeviceGuard g(device);
+    HIP_TRY(g.err);
+    hipStream_t s = nullptr;
+    // ---- runs to the device: lengths (+ a 0 pad for the scan), values, row offsets
+    DevBuf d_len, d_val, d_off, d_gstart, d_start, d_rowlen, temp;
+    HIP_TRY(d_len.alloc(4 * ((size_t)n_runs + 1)));
+    HIP_TRY(d_val.alloc((dbl ? 8 : 4) * std::max<size_t>((size_t)n_runs, 1)));
+    HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
+    HIP_TRY(d_gstart.alloc(8 * ((size_t)n_runs + 1)));
+    HIP_TRY(d_start.alloc(4 * std::max<size_t>((size_t)n_runs, 1)));
+    HIP_TRY(d_rowlen.alloc(4 * std::max<size_t>((size_t)R, 1)));
+    if (n_runs) {
+        HIP_TRY(rcp::stage_h2d(d_len.p, cov->lengths, 4 * (size_t)n_runs, device, s));
+        HIP_TRY(rcp::stage_h2d(d_val.p, dbl ? (const void*)cov->dvalues : (const void*)cov->ivalues,
+                               (dbl ? 8 : 4) * (size_t)n_runs, device, s));
+    }
+    HIP_TRY(hipMemsetAsync(d_len.as<int32_t>() + n_runs, 0, 4, s));
+    if (R > 0) HIP_TRY(rcp::stage_h2d(d_off.p, cov->run_off, 8 * ((size_t)R + 1), device, s));
+    size_t tb = 0;
+    HIP_TRY(rcp_rle_scan(d_len.as<int32_t>(), n_runs, d_gstart.as<int64_t>(), nullptr, &tb, s));
+    HIP_TRY(temp.alloc(std::max<size_t>(tb, 1)));
+    HIP_TRY(rcp_rle_scan(d_len.as<int32_t>(), n_runs, d_gstart.as<int64_t>(), temp.p, &tb, s));
+    HIP_TRY(rcp_rle_starts(R, d_off.as<int64_t>(), d_gstart.as<int64_t>(), d_start.as<int32_t>(),
+                           d_rowlen.as<int32_t>(), s));
+    std::vector<int32_t> row_len(std::max(R, 1), 0);
+    if (R) HIP_TRY(hipMemcpyAsync(row_len.data(), d_rowlen.p, 4 * (size_t)R, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    temp.reset();
+    d_gstart.reset();
+    d_len.reset();
+    // ---- tasks: one per (row, part), with the read path's splitVector decisions
+    const bool rounding = bins->rng_kind == RCP_RNG_ROUNDING;
+    RcpRleDev P{};
+    std::vector<RcpRleTask> tasks;
+    tasks.reserve((size_t)R * bins->n_parts);
+    std::vector<int32_t> lay_cnt, nb_pos;
+    std::map<std::pair<int, int>, int32_t> layout_cache, nb_cache;
+    int64_t col = 0;
+    int32_t max_interp_len = 0, max_interp_bins = 0, n_scratch = 0;
+    for (int p = 0; p < bins->n_parts; ++p) {
+        RcpPart pt{};
+        if (!part_slice_spec(bins->where ? bins->where[p] : RCP_WHERE_WHOLE, bins->flank[0], bins->flank[1], &pt))
+            return fail(RCP_EINVAL, "where[%d] = %d", p, bins->where[p]);
+        const int nb = bins->n_bins[p];
+        if (nb < 0) return fail(RCP_EINVAL, "n_bins[%d] < 0", p);
+        const bool per_base = nb == 0;
+        const int32_t ncol = per_base ? (bins->per_base_width ? bins->per_base_width[p] : 0) : nb;
+        if (ncol <= 0) return fail(RCP_EINVAL, "part %d has no columns", p);
+        P.part_col0[p] = (int32_t)col;
+        P.part_cols[p] = ncol;
+        col += ncol;
+        for (int32_t r = 0; r < R; ++r) {
+            RcpRleTask t{};
+            t.row = r;
+            t.part = p;
+            t.lay = t.nbpos = t.scratch = -1;
+            if (cov->is_null && cov->is_null[r]) {
+                t.mode = RCP_RLE_ZERO;
+                tasks.push_back(t);
+                continue;
+            }
+            int32_t head, L;
+            rcp_part_slice(pt, row_len[r], &head, &L);
+            if (L < 0 || head < 0 || head + L > row_len[r])
+                return fail(RCP_EUNSUPPORTED, "row %d: part %d slice out of its %d-long coverage", r, p, row_len[r]);
+            t.head = head;
+            t.L = L;
+            if (per_base) {
+                if (L != ncol)
+                    return fail(RCP_EUNSUPPORTED, "a per-base part met a row whose slice width differs from the column count");
+                t.mode = RCP_RLE_BASE;
+            } else if (L < nb) {
+                int mode = bins->interp;
+                if (mode == RCP_INTERP_AUTO)
+                    mode = ((double)(nb - L) / nb < 0.2) ? RCP_INTERP_NEIGHBORHOOD : RCP_INTERP_SPLINE;
+                if (mode == RCP_INTERP_NEIGHBORHOOD) {
+                    const auto key = std::make_pair(nb, L);
+                    auto it = nb_cache.find(key);
+                    if (it == nb_cache.end()) {
+                        std::vector<int32_t> pos;
+                        if (!rcp::neighborhood_positions(nb, L, rounding, &pos))
+                            return fail(RCP_ESEMANTIC,
+                                        "splitVector neighborhood interpolation of %d values into %d bins: R raises an error",
+                                        L, nb);
+                        t.nbpos = (int32_t)nb_pos.size();
+                        nb_pos.insert(nb_pos.end(), pos.begin(), pos.end());
+                        nb_cache[key] = t.nbpos;
+                    } else {
+                        t.nbpos = it->second;
+                    }
+                } else if (mode == RCP_INTERP_SPLINE && L < 1) {
+                    return fail(RCP_ESEMANTIC, "spline() of zero points: R raises an error");
+                } else if (mode == RCP_INTERP_LINEAR && L < 1) {
+                    return fail(RCP_EUNSUPPORTED, "empty slice with the 'linear' interpolation");
+                }
+                t.mode = RCP_RLE_INTERP + mode;
+                t.scratch = n_scratch++;
+                max_interp_len = std::max(max_interp_len, L);
+                max_interp_bins = std::max(max_interp_bins, nb);
+            } else {
+                t.mode = RCP_RLE_BINNED;
+                t.bs = L / nb;
+                const int32_t dif = L - t.bs * nb;
+                if (dif) {
+                    const auto key = std::make_pair(nb, dif);
+                    auto it = layout_cache.find(key);
+                    if (it == layout_cache.end()) {
+                        const std::vector<int32_t> cnt = rcp::bin_layout_counts(nb, dif, rounding);
+                        t.lay = (int32_t)lay_cnt.size();
+                        lay_cnt.insert(lay_cnt.end(), cnt.begin(), cnt.end());
+                        layout_cache[key] = t.lay;
+                    } else {
+                        t.lay = it->second;
+                    }
+                }
+            }
+            tasks.push_back(t);
+        }
+    }
+    if (max_interp_len > kChunkMax)
+        return fail(RCP_EUNSUPPORTED, "interpolated slice of %d positions exceeds %d", max_interp_len, kChunkMax);
+    // fmm pivots (as rcp_plan_create)
+    std::vector<double> spl_tb(2 * ((size_t)std::max(max_interp_len, 1) + 1), 0.0);
+    {
+        double bp = -1.0;
+        spl_tb[1] = bp;
+        for (size_t i = 1; 2 * i + 1 < spl_tb.size(); ++i) {
+            const double t = 1.0 / bp;
+            bp = 4.0 - t;
+            spl_tb[2 * i] = t;
+            spl_tb[2 * i + 1] = bp;
+        }
+    }
+    // interpolation working set: x (L+1) | y (n+1) | b, c, d (3 (L+1)) | n ints
+    // (the neighborhood fill's n pre-fill values reuse b.., as in rcp_plan_create)
+    const int64_t stride = 2 * ((int64_t)max_interp_bins + 1) + 4 * ((int64_t)max_interp_len + 1) + 8;
+    const size_t lds = n_scratch ? 8 * (size_t)stride : 0;
+    P.interp_lds = lds <= 160 * 1024 ? 1 : 0;
+    P.interp_stride = stride;
+    std::vector<char> blob;
+    const size_t o_tasks = put(blob, tasks);
+    const size_t o_lay = put(blob, lay_cnt);
+    const size_t o_nb = put(blob, nb_pos);
+    const size_t o_spl = put(blob, spl_tb);
+    DevBuf d_tab, d_scratch, d_out;
+    HIP_TRY(d_tab.alloc(blob.size()));
+    HIP_TRY(rcp::stage_h2d(d_tab.p, blob.data(), blob.size(), device, s));
+    if (n_scratch && !P.interp_lds) HIP_TRY(d_scratch.alloc(8 * (size_t)stride * n_scratch));
+    const int64_t ld = ((int64_t)R + 15) & ~int64_t(15);
+    HIP_TRY(d_out.alloc(8 * std::max<size_t>((size_t)ld * (size_t)col, 1)));
+    char* base = d_tab.as<char>();
+    P.run_off = d_off.as<int64_t>();
+    P.run_start = d_start.as<int32_t>();
+    P.row_len = d_rowlen.as<int32_t>();
+    P.ivals = dbl ? nullptr : d_val.as<int32_t>();
+    P.dvals = dbl ? d_val.as<double>() : nullptr;
+    P.tasks = reinterpret_cast<const RcpRleTask*>(base + o_tasks);
+    P.n_tasks = (int64_t)tasks.size();
+    P.lay_cnt = reinterpret_cast<const int32_t*>(base + o_lay);
+    P.nb_pos = reinterpret_cast<const int32_t*>(base + o_nb);
+    P.spl_tb = reinterpret_cast<const double*>(base + o_spl);
+    P.out = d_out.as<double>();
+    P.ld = ld;
+    P.stat = bins->stat;
+    P.scale = bins->scale;
+    P.scratch = d_scratch.as<double>();
+    HIP_TRY(rcp_rle_profile_launch(&P, dbl ? 1 : 0, P.interp_lds ? lds : 0, s));
+    if (out && R && col)
+        HIP_TRY(rcp::stage_d2h_2d(out, 8 * (size_t)R, d_out.p, 8 * (size_t)ld, 8 * (size_t)R, (size_t)col, device, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (row_valid)
+        for (int32_t r = 0; r < R; ++r) row_valid[r] = (cov->is_null && cov->is_null[r]) ? 0 : 1;
     return RCP_OK;
     RCP_CATCH
 }

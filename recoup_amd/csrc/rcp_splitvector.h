@@ -1,0 +1,230 @@
+// rcp_splitvector.h -- device restatement of splitVector's interpolation (R/util.R:17-73) for
+// one row whose slice is shorter than its bin count (length(x) < n), shared by the read-pileup
+// interpolation kernel (rcp_kernels.hip) and the Rle-input profile kernel (rcp_rle.hip).
+// Included by HIP sources only; everything lives in an anonymous namespace.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+#pragma clang fp contract(off)
+// stats::spline method "fmm" (R splines.c fmm_spline) on knots x = 1..n: every knot spacing
+// d[i] is 1.0, so the operations below are the original ones with the multiplications and
+// divisions by d[i] = 1.0 (exact) dropped.  With unit spacing the elimination's pivots
+// b_i and multipliers t_i = 1 / b_{i-1} do not depend on y: the host tabulates them once
+// per plan (P.spl_tb, same operations in the same order), so the forward elimination is
+// the dependent chain c_i = c_i - t_i c_{i-1} alone (one multiply, one subtract per step)
+// and the back substitution divides by tabulated pivots; both chains run on thread 0 with
+// the next 8 table / LDS values loaded ahead.  Data-parallel loops run over the block.
+// Same operations in the same order per element as R: bit-equal.
+// Call from all threads of the block; y, b, c, d in LDS (or global), 0-based.
+__device__ void fmm_spline_block(int n, const double* y, double* b, double* __restrict__ c, double* d,
+                                 const double* __restrict__ tb) {
+    const int t = threadIdx.x;
+    if (n < 3) {
+        if (t == 0) {
+            if (n == 2) {
+                b[0] = b[1] = y[1] - y[0];
+            } else if (n == 1) {
+                b[0] = 0.0;
+            }
+            for (int i = 0; i < n; ++i) c[i] = d[i] = 0.0;
+        }
+        __syncthreads();
+        return;
+    }
+    // 1-based i = 2 .. n-1 (0-based i - 1): c[i] = (y[i+1] - y[i]) - (y[i] - y[i-1])
+    for (int i = 1 + t; i < n - 1; i += blockDim.x) c[i] = (y[i + 1] - y[i]) - (y[i] - y[i - 1]);
+    __syncthreads();
+    if (t == 0) {
+        double c1 = 0.0, cn = 0.0;
+        if (n > 3) {
+            c1 = c[2] / 2.0 - c[1] / 2.0;
+            cn = c[n - 2] / 2.0 - c[n - 3] / 2.0;
+            c1 = c1 / 3.0;  // * d[1] * d[1] (= 1) / 3
+            cn = -cn / 3.0;
+        }
+        c[0] = c1;
+        c[n - 1] = cn;
+        // forward elimination: t = d[i-1] / b[i-1]; b[i] -= t d[i-1]; c[i] -= t c[i-1]
+        double cp = c1;
+        int i = 1;
+        for (; i + 8 <= n; i += 8) {
+            double cv[8], tv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cv[u] = c[i + u];
+                tv[u] = tb[2 * (i + u)];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cp = cv[u] - tv[u] * cp;
+                c[i + u] = cp;
+            }
+        }
+        for (; i < n; ++i) {
+            cp = c[i] - tb[2 * i] * cp;
+            c[i] = cp;
+        }
+        const double bn = -1.0 - tb[2 * (n - 1)];  // b[n-1] = -1 - t_{n-1}
+        // back substitution: c[i] = (c[i] - c[i+1]) / b[i]
+        double cnext = cp / bn;
+        c[n - 1] = cnext;
+        i = n - 2;
+        for (; i >= 7; i -= 8) {
+            double cv[8], bv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cv[u] = c[i - u];
+                bv[u] = tb[2 * (i - u) + 1];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cnext = (cv[u] - cnext) / bv[u];
+                c[i - u] = cnext;
+            }
+        }
+        for (; i >= 0; --i) {
+            cnext = (c[i] - cnext) / tb[2 * i + 1];
+            c[i] = cnext;
+        }
+        b[n - 1] = (y[n - 1] - y[n - 2]) + (c[n - 2] + 2.0 * c[n - 1]);
+    }
+    __syncthreads();
+    // coefficients: b[i] = (y[i+1] - y[i]) - (c[i+1] + 2 c[i]); d[i] = c[i+1] - c[i]; c[i] *= 3
+    for (int i = t; i < n - 1; i += blockDim.x) {
+        const double ci = c[i], cn1 = c[i + 1];
+        b[i] = (y[i + 1] - y[i]) - (cn1 + 2.0 * ci);
+        d[i] = cn1 - ci;
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += blockDim.x) c[i] = 3.0 * c[i];
+    if (t == 0) d[n - 1] = d[n - 2];
+    __syncthreads();
+}
+
+__device__ double seq_point(int L, int n, int i) {
+    // seq.int(1, L, length.out = n)[i] as do_seq computes it
+    if (i == 0) return 1.0;
+    if (i == n - 1) return (double)L;
+    const double by = ((double)L - 1.0) / (double)(n - 1);
+    return (i < n / 2) ? 1.0 + (double)i * by : (double)L - (double)(n - 1 - i) * by;
+}
+
+// spline_eval's interval for each output point, in R's order: the previous interval is kept
+// while x[i] <= u <= x[i+1], else bisection (knots x = 1..n) -- integer-only, on thread 0.
+__device__ void spline_intervals(int L, int n, int32_t* iv) {
+    int i = 0;
+    const int n_1 = L - 1;
+    for (int k = 0; k < n; ++k) {
+        const double u = seq_point(L, n, k);
+        if (u < (double)(i + 1) || (i < n_1 && (double)(i + 2) < u)) {
+            i = 0;
+            int j = L;
+            do {
+                const int m = (i + j) / 2;
+                if (u < (double)(m + 1)) j = m; else i = m;
+            } while (j > i + 1);
+        }
+        iv[k] = i;
+    }
+}
+
+__device__ __forceinline__ int spline_bisect(int L, double u) {
+    int i = 0, j = L;
+    do {
+        const int m = (i + j) / 2;
+        if (u < (double)(m + 1)) j = m; else i = m;
+    } while (j > i + 1);
+    return i;
+}
+
+// The same interval for point k alone, for interpolated rows (L < n: output points closer
+// than one knot apart).  spline_intervals keeps interval i for u in [i+1, i+2] and bisects
+// otherwise; the bisection lands on floor(u) - 1, so the two differ only at a point sitting
+// exactly on a knot m = i + 2 just after a point of interval i (it keeps i, the evaluation
+// runs at dx = 1).  Because consecutive points are less than 1 apart, the interval held at
+// point k - 1 is bisect(u_{k-1}) whenever it matters, and each point is decided alone.
+__device__ __forceinline__ int spline_interval_at(int L, int n, int k) {
+    const double u = seq_point(L, n, k);
+    const int prev = k == 0 ? 0 : spline_bisect(L, seq_point(L, n, k - 1));
+    if (u < (double)(prev + 1) || (prev < L - 1 && (double)(prev + 2) < u)) return spline_bisect(L, u);
+    return prev;
+}
+
+// spline_eval's cubic on interval i (no FMA contraction: R's rounding)
+__device__ double spline_eval_at(const double* y, const double* b, const double* c, const double* d, int i,
+                                 double u) {
+    const double dx = u - (double)(i + 1);
+    return y[i] + dx * (b[i] + dx * (c[i] + dx * d[i]));
+}
+#pragma clang fp contract(on)
+
+
+// splitVector of a row slice x[0 .. L) (doubles, already x * scale) into n > L bins, written to
+// out[k * ld] (k = 0 .. n - 1).  mode 1: spline(x, n)$y clipped at 0 (auto with (n - L) / n >= 0.2,
+// or "spline"); 3: neighborhood fill with the R-RNG positions nb_pos (1-based, sorted,
+// set.seed(42); sort(sample(3:(n - 2), L - 4))); otherwise "linear", whose switch arm is spelled
+// "inear" (util.R:49): x stays short and rbind recycles it.  Scratch follows x: y = x + L + 1
+// (n + 1), b, c, d (L + 1 each), then n ints.  Call with every thread of the block.
+__device__ void interp_finish(int mode, int L, int n, double* x, const int32_t* nb_pos, const double* spl_tb,
+                              double* out, size_t ld) {
+    double* y = x + L + 1;
+    double* b = y + n + 1;
+    if (mode == 1) {  // spline(x, n = n)$y, then x[x < 0] <- 0
+        double* c = b + L + 1;
+        double* d = c + L + 1;
+        int32_t* iv = reinterpret_cast<int32_t*>(d + L + 1);
+        fmm_spline_block(L, x, b, c, d, spl_tb);
+        if (L < n) {  // always, for rows of this kernel; the sequential walk stays as the rule
+            for (int k = threadIdx.x; k < n; k += (int)blockDim.x) iv[k] = spline_interval_at(L, n, k);
+        } else if (threadIdx.x == 0) {
+            spline_intervals(L, n, iv);
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < n; k += (int)blockDim.x) {
+            double v;
+            if (L == 1) {
+                v = x[0];
+            } else {
+                v = spline_eval_at(x, b, c, d, iv[k], seq_point(L, n, k));
+            }
+            y[k] = v < 0 ? 0.0 : v;
+        }
+    } else if (mode == 3) {  // neighborhood fill (util.R:53-69), from the pre-fill vector
+        const int32_t* pos = nb_pos;
+        double* pre = b;
+        for (int i = threadIdx.x; i < n; i += (int)blockDim.x) pre[i] = __builtin_nan("");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            pre[0] = x[0];
+            pre[1] = x[1];
+            pre[n - 2] = x[L - 2];
+            pre[n - 1] = x[L - 1];
+        }
+        for (int i = threadIdx.x; i < L - 4; i += (int)blockDim.x) pre[pos[i] - 1] = x[2 + i];
+        __syncthreads();
+        for (int z = threadIdx.x; z < n; z += (int)blockDim.x) {
+            if (!isnan(pre[z])) {
+                y[z] = pre[z];
+                continue;
+            }
+            double sm = 0.0;
+            int m = 0;
+            const int nb[4] = {z - 2, z - 1, z + 1, z + 2};
+            for (int q = 0; q < 4; ++q)
+                if (nb[q] >= 0 && nb[q] < n && !isnan(pre[nb[q]])) {
+                    sm += pre[nb[q]];
+                    ++m;
+                }
+            y[z] = m ? sm / m : __builtin_nan("");
+        }
+    } else {  // "linear": the switch arm is spelled "inear" -> x unchanged; rbind recycles
+        for (int i = threadIdx.x; i < n; i += (int)blockDim.x) y[i] = x[i % L];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < n; k += blockDim.x) out[(size_t)k * ld] = y[k];
+}
+
+}  // namespace

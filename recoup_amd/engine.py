@@ -272,3 +272,60 @@ def profile_host(readset, rows, bins, out, valid=None):
         check(_lib.lib().rcp_profile(readset.h, ctypes.byref(rd), ctypes.byref(bd), cptr(out, _lib._dp),
                                      None if valid is None else cptr(valid, _lib._u8p)))
     return out
+
+
+def rle_arrays(coverages):
+    """Flatten a coverage list (None = R's NULL, an ``Rle``-like object with ``values`` /
+    ``lengths``, or a dense vector) into the run arrays of rcp_rle_desc: (run_off int64,
+    lengths int32, values int32 or float64, is_null uint8).  Dense vectors are run-length
+    encoded here; the values are integer when every element is (an integer Rle), else float64
+    (a numeric Rle)."""
+    vals, lens, nulls, counts = [], [], [], []
+    for x in coverages:
+        if x is None:
+            nulls.append(1)
+            counts.append(0)
+            continue
+        nulls.append(0)
+        if hasattr(x, "values") and hasattr(x, "lengths"):
+            v, ln = np.asarray(x.values), np.asarray(x.lengths, dtype=np.int64)
+        else:
+            d = np.asarray(x)
+            if d.size == 0:
+                v, ln = d[:0], np.zeros(0, np.int64)
+            else:
+                cut = np.flatnonzero(d[1:] != d[:-1]) + 1
+                starts = np.concatenate([[0], cut])
+                v = d[starts]
+                ln = np.diff(np.concatenate([starts, [d.size]]))
+        vals.append(v)
+        lens.append(ln)
+        counts.append(len(ln))
+    run_off = np.zeros(len(counts) + 1, dtype=np.int64)
+    run_off[1:] = np.cumsum(counts)
+    lengths = np.ascontiguousarray(np.concatenate(lens) if lens else np.zeros(0), dtype=np.int32)
+    allv = np.concatenate(vals) if vals else np.zeros(0, np.int32)
+    integer = allv.dtype.kind in "iub" or (allv.dtype.kind == "f" and allv.size and
+                                           np.all(np.isfinite(allv)) and np.all(allv == np.round(allv)) and
+                                           np.all(np.abs(allv) < 2 ** 31))
+    values = np.ascontiguousarray(allv, dtype=np.int32 if integer else np.float64)
+    return run_off, lengths, values, np.asarray(nulls, dtype=np.uint8)
+
+
+def profile_rle(coverages, bins, device=0):
+    """rcp_profile_rle: binCoverageMatrix / baseCoverageMatrix of a host coverage list (the
+    reference's list of Rle).  Returns (R x n_cols float64 matrix in R column-major (F) order,
+    valid bool)."""
+    run_off, lengths, values, nulls = rle_arrays(coverages)
+    R = len(nulls)
+    integer = values.dtype == np.int32
+    d = _lib.RleDesc(R, cptr(run_off, _lib._i64p), cptr(lengths, _lib._i32p),
+                     cptr(values, _lib._i32p) if integer else None,
+                     None if integer else cptr(values, _lib._dp), cptr(nulls, _lib._u8p))
+    out = np.zeros((R, bins.n_cols), order="F")
+    valid = np.zeros(max(R, 1), np.uint8)
+    bd = bins.desc()
+    with torch.cuda.device(int(device)):
+        check(_lib.lib().rcp_profile_rle(ctypes.byref(d), ctypes.byref(bd), int(device), cptr(out, _lib._dp),
+                                         cptr(valid, _lib._u8p)))
+    return out, valid[:R].astype(bool)

@@ -73,6 +73,34 @@ static int abi() {
     EXPECT(rcp_calc_coverage(nullptr, nullptr, nullptr, nullptr, nullptr) == RCP_EINVAL);
     int64_t off[2] = {0, 0}, run_off[2], nruns;
     EXPECT(rcp_rle_encode(-1, off, nullptr, 0, nullptr, nullptr, run_off, &nruns, nullptr) == RCP_EINVAL);
+    {  // rcp_profile_rle: host-side validation of the run arrays before any device work
+        const int32_t where = RCP_WHERE_WHOLE, nb = 4, w = 0;
+        rcp_bins_desc bins{};
+        bins.n_parts = 1;
+        bins.where = &where;
+        bins.n_bins = &nb;
+        bins.per_base_width = &w;
+        bins.scale = 1.0;
+        const int64_t ro[3] = {0, 2, 3};
+        const int32_t len_ok[3] = {3, 2, 4}, len_bad[3] = {3, -2, 4}, vals[3] = {1, 0, 5};
+        rcp_rle_desc c{2, ro, len_ok, vals, nullptr, nullptr};
+        double out[8];
+        EXPECT(rcp_profile_rle(nullptr, &bins, 0, out, nullptr) == RCP_EINVAL);
+        EXPECT(rcp_profile_rle(&c, nullptr, 0, out, nullptr) == RCP_EINVAL);
+        c.lengths = len_bad;
+        EXPECT(rcp_profile_rle(&c, &bins, 0, out, nullptr) == RCP_EINVAL);
+        const int64_t ro_bad[3] = {0, 3, 2};
+        c.lengths = len_ok;
+        c.run_off = ro_bad;
+        EXPECT(rcp_profile_rle(&c, &bins, 0, out, nullptr) == RCP_EINVAL);
+        c.run_off = ro;
+        const double dv[3] = {1, 2, 3};
+        c.dvalues = dv;  // both value arrays
+        EXPECT(rcp_profile_rle(&c, &bins, 0, out, nullptr) == RCP_EINVAL);
+        c.dvalues = nullptr;
+        const int rc2 = rcp_profile_rle(&c, &bins, 0, out, nullptr);
+        EXPECT(nd > 0 ? rc2 == RCP_OK : rc2 == RCP_ENODEVICE);
+    }
     EXPECT(rcp_bam_read(nullptr, 0, 0.5, 1, nullptr) == RCP_EINVAL);
     rcp_bam* b = nullptr;
     EXPECT(rcp_bam_read("/nonexistent/x.bam", 0, 0.5, 1, &b) == RCP_EINVAL && b == nullptr);

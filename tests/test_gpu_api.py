@@ -139,11 +139,16 @@ def test_normalize_linear(c1):
         np.testing.assert_allclose(s["profile"], c1["gold"][f"tss_heat_s{k}"] * f[k], rtol=1e-12, atol=0)
 
 
-def test_profile_needs_device_coverage(c1):
+def test_profile_from_host_coverage_list(c1):
+    """The reference reuses a stored $coverage (a list of Rle, R/recoup.R:126-135): profileMatrix
+    of coverageRef's materialised list equals the fused device pass and the C1 golden matrix."""
     inp = ra.coverageRef(_input(c1), c1["genome"], "tss", FLANK)
-    inp[0]["coverage"] = inp[0]["coverage"].to_list()
-    with pytest.raises(ra.UnsupportedError):
-        ra.profileMatrix(inp, FLANK, {"regionBinSize": 200})
+    for s in inp:
+        s["coverage"] = s["coverage"].to_list(rle=True)
+    inp = ra.profileMatrix(inp, FLANK, {"flankBinSize": 0, "regionBinSize": 200})
+    for k, s in enumerate(inp):
+        np.testing.assert_allclose(s["profile"], c1["gold"][f"tss_heat_s{k}"], rtol=1e-12, atol=0)
+        assert s["profile"].rownames == list(c1["G"]["names"])
 
 
 def test_missing_chromosome_rows_are_null(c1):

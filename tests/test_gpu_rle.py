@@ -1,0 +1,147 @@
+"""Profiles of the reference's own coverage object -- a list of Rle (R/coverage.R:171-173) --
+through rcp_profile_rle (R/profile.R:100-212 on a stored or sliced $coverage,
+R/recoup.R:126-135, R/util.R:209-210).  coverageRef -> to_list(rle=True) -> profileMatrix must
+equal the fused device pass (DeviceCoverage) bit for bit for integer Rle and the oracle on
+random cases: uniform and R-RNG bins, interpolation (spline / neighborhood / "inear"),
+median, per-base flanks, NULL rows, numeric (normalised) Rle, dense vectors, slices."""
+import numpy as np
+import pytest
+
+import recoup_amd as ra
+from recoup_amd.engine import Bins, profile_rle
+from tests import helpers, oracle_rows
+from tests.test_gpu_random import CHROM_LEN, make_reads, single_rows
+
+pytestmark = pytest.mark.gpu
+FLANK = (2000, 2000)
+
+
+def _c1_inputs(region, flank):
+    """coverageRef of test.input over test.genome twice: one sample list keeps the
+    DeviceCoverage, the other the materialised list of Rle (as a saved recoup object has it)."""
+    from tests.golden import c1_cases
+    from tests.test_gpu_api import _input
+    d = c1_cases.load_inputs()
+    G = c1_cases.genome(d)
+    genome = ra.GRanges(G["chrom"], G["start"], G["end"], G["strand"], names=G["names"])
+    inp_dev = ra.coverageRef(_input({"d": d}), genome, region, flank)
+    inp_rle = ra.coverageRef(_input({"d": d}), genome, region, flank)
+    for s in inp_rle:
+        s["coverage"] = s["coverage"].to_list(rle=True)
+    return genome, inp_dev, inp_rle
+
+
+def _bits(a, b):
+    assert a.shape == b.shape
+    assert np.array_equal(np.ascontiguousarray(a).view(np.uint64), np.ascontiguousarray(b).view(np.uint64))
+
+
+@pytest.mark.parametrize("region,bp", [("tss", {"flankBinSize": 0, "regionBinSize": 200}),
+                                       ("tss", {"flankBinSize": 0, "regionBinSize": 0}),
+                                       ("tss", {"flankBinSize": 0, "regionBinSize": 150}),
+                                       ("genebody", {"flankBinSize": 50, "regionBinSize": 150}),
+                                       ("genebody", {"flankBinSize": 0, "regionBinSize": 150, "sumStat": "median"}),
+                                       ("genebody", {"flankBinSize": 50, "regionBinSize": 150, "interpolation": "spline"})])
+def test_rle_list_equals_device_pass(gpu, region, bp):
+    genome, inp_dev, inp_rle = _c1_inputs(region, FLANK)
+    ra.profileMatrix(inp_dev, FLANK, bp)
+    ra.profileMatrix(inp_rle, FLANK, bp)
+    for a, b in zip(inp_dev, inp_rle):
+        if bp.get("interpolation") == "spline" or bp.get("sumStat") == "median":
+            np.testing.assert_allclose(b["profile"], a["profile"], rtol=1e-12, atol=0)
+        else:
+            _bits(np.asarray(a["profile"]), np.asarray(b["profile"]))
+        assert a["profile"].rownames == b["profile"].rownames
+
+
+def test_sliced_coverage(gpu):
+    """sliceObj subsets the stored coverage list (R/util.R:209-210); its profile is the same
+    rows of the full profile."""
+    genome, inp_dev, inp_rle = _c1_inputs("genebody", FLANK)
+    bp = {"flankBinSize": 50, "regionBinSize": 150}
+    ra.profileMatrix(inp_dev, FLANK, bp)
+    idx = [3, 0, 17, 42, 42, 99]
+    for s in inp_rle:
+        cov = s["coverage"]
+        s["coverage"] = ra.CoverageList([cov[i] for i in idx], [cov.names[i] for i in idx])
+    ra.profileMatrix(inp_rle, FLANK, bp)
+    for a, b in zip(inp_dev, inp_rle):
+        _bits(np.asarray(a["profile"])[idx], np.asarray(b["profile"]))
+
+
+def test_numeric_rle_after_linear_normalisation(gpu):
+    """normalize = "linear" multiplies the stored coverage (a numeric Rle afterwards)."""
+    genome, inp_dev, inp_rle = _c1_inputs("tss", FLANK)
+    f = ra.calcLinearFactors(inp_dev)
+    assert (f != 1).any()
+    ra.normalizeLinear(inp_dev)
+    ra.normalizeLinear(inp_rle)
+    for bp in ({"flankBinSize": 0, "regionBinSize": 200}, {"flankBinSize": 0, "regionBinSize": 150, "sumStat": "median"}):
+        a = ra.profileMatrix([dict(s, profile=None) for s in inp_dev], FLANK, bp)
+        b = ra.profileMatrix([dict(s, profile=None) for s in inp_rle], FLANK, bp)
+        for x, y in zip(a, b):
+            np.testing.assert_allclose(y["profile"], x["profile"], rtol=1e-13, atol=1e-300)
+
+
+@pytest.mark.parametrize("stat", ["mean", "median"])
+@pytest.mark.parametrize("interp", ["auto", "spline", "neighborhood", "linear"])
+def test_random_rle_vs_oracle(gpu, stat, interp):
+    """Random rows of mixed lengths (some shorter than the bins: interpolation; R-RNG layouts;
+    NULL rows) as integer Rle, dense vectors and a numeric Rle: vs the oracle's splitVector."""
+    rng = np.random.default_rng(7 + len(interp) + (stat == "median"))
+    reads = make_reads(rng, 60_000)
+    R = 180
+    rows = single_rows(rng, R, 1000)
+    rows.end[:] = rows.start + rng.integers(40, 3000, R)  # mixed lengths
+    rows.end[::11] = rows.start[::11] + 30                # short rows (< 100 bins)
+    ix = oracle_rows.index_for(reads, CHROM_LEN)
+    cov = oracle_rows.row_coverage(ix, rows)
+    cov[5] = None
+    bins = Bins([("whole", 100)], stat=stat, interp=interp)
+    exp, ev = oracle_rows.profile(cov, bins)
+    rle = [None if x is None else ra.Rle(*_runs(x)) for x in cov]
+    for inp in (rle, cov):
+        mat, valid = profile_rle(inp, bins)
+        np.testing.assert_array_equal(valid, ev.astype(bool))
+        np.testing.assert_allclose(mat, exp, rtol=1e-9, atol=1e-12, equal_nan=True)
+    # numeric Rle: x * 0.37 as doubles; the oracle bins the same doubles
+    covd = [None if x is None else x * 0.37 for x in cov]
+    rled = [None if x is None else ra.Rle(*_runs(x)) for x in covd]
+    exp_d = np.vstack([np.zeros(100) if x is None else
+                       _row(x, 100, interp, stat) for x in covd])
+    mat, _ = profile_rle(rled, bins)
+    np.testing.assert_allclose(mat, exp_d, rtol=1e-12, atol=1e-12, equal_nan=True)
+
+
+def _row(x, n, interp, stat):
+    from oracle import oracle as o
+    r = o.split_vector(x, n, interp=interp, stat=stat)
+    return np.resize(r, n)  # rbind recycles a short row ("inear")
+
+
+def _runs(x):
+    x = np.asarray(x)
+    if x.size == 0:
+        return x[:0], np.zeros(0, np.int64)
+    cut = np.flatnonzero(x[1:] != x[:-1]) + 1
+    st = np.concatenate([[0], cut])
+    return x[st], np.diff(np.concatenate([st, [x.size]]))
+
+
+def test_flanks_per_base_and_errors(gpu):
+    """Per-base flanks + binned centre (profile.R:58-77) and the reference's errors."""
+    rng = np.random.default_rng(3)
+    reads = make_reads(rng, 50_000)
+    rows = single_rows(rng, 60, 6000)
+    ix = oracle_rows.index_for(reads, CHROM_LEN)
+    cov = oracle_rows.row_coverage(ix, rows)
+    bins = helpers.unequal_bins((1000, 1000), 0, 150)
+    exp, ev = oracle_rows.profile(cov, bins)
+    mat, valid = profile_rle([None if x is None else ra.Rle(*_runs(x)) for x in cov], bins)
+    np.testing.assert_allclose(mat, exp, rtol=1e-12, atol=0)
+    # a per-base part whose width differs from the slice: refused like the device path
+    with pytest.raises(ra.UnsupportedError):
+        profile_rle(cov, Bins([("whole", 0, 5999)]))
+    # neighborhood of fewer than 4 values: R raises an error
+    with pytest.raises(ra.SemanticError):
+        profile_rle([np.arange(3, dtype=np.int32)], Bins([("whole", 4)], interp="neighborhood"))

@@ -23,7 +23,7 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_err
 
 @pytest.fixture(scope="module")
 def driver():
-    if not os.path.exists(os.path.join(ROOT, "recoup_amd", "build", "rcp_kernels.hip.o")):
+    if not all(os.path.exists(os.path.join(ROOT, "recoup_amd", "build", f)) for f in ("rcp_kernels.hip.o", "rcp_rle.hip.o")):
         from recoup_amd import build
         build.build(verbose=False)
     subprocess.check_call(["make", "-s", "-C", SAN], stdout=subprocess.DEVNULL)

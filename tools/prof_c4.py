@@ -23,7 +23,7 @@ else:
     reg = d["regions"]
     rows = RowTable.from_ranges(reg["chrom"], reg["start"], reg["end"], reg["strand"])
     bins = Bins([("whole", d["n_bins"])]) if d["n_bins"] else Bins([("whole", 0, sum(d["flank"]))])
-plan = Plan(rs, rows, bins)
+plan = Plan(rs, rows, bins, out_ld="padded")  # as bench.py
 out = plan.empty_output()
 for _ in range(int(os.environ.get("ITERS", "3"))):
     plan.execute(out)

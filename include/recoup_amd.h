@@ -207,6 +207,21 @@ RCP_API int rcp_plan_row_lengths(const rcp_plan* plan, int64_t* out_len);
 RCP_API int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
                 double* out, uint8_t* row_valid);
 
+/* Several GPUs in one call: the reference parallelises the per-region
+ * work over host cores with cmclapply (R/util.R:364-382, used by R/coverage.R:147-154 and
+ * R/profile.R:84-96); here the rows are cut into n_devices contiguous blocks (balanced by a
+ * per-row weight: output + genomic width) and one host thread per GPU builds the plan for its
+ * block, executes it and copies its rows of every column straight into the caller's R
+ * column-major n_rows x n_cols matrix -- no collective, no host reassembly.
+ * rcp_readset_create_multi makes one readset of the same reads on each listed device (in
+ * parallel, one thread per device); readsets[i] lives on its own device and may be reused
+ * across calls, as R keeps input$ranges.  row_split (may be NULL) receives the n_devices + 1
+ * block boundaries.  The result is bit-identical to rcp_profile on one device. */
+RCP_API int rcp_readset_create_multi(const rcp_reads_desc* desc, const int32_t* device_ids, int32_t n_devices,
+                                     rcp_readset** out);
+RCP_API int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices, const rcp_rows_desc* rows,
+                              const rcp_bins_desc* bins, double* out, uint8_t* row_valid, int32_t* row_split);
+
 /* Profiles of a coverage list the caller holds as run-length encoded vectors -- the reference's
  * own `$coverage` object, a named list of S4Vectors::Rle (R/coverage.R:171-173) -- as
  * binCoverageMatrix / baseCoverageMatrix consume it (R/profile.R:100-212) when recoup() reuses a

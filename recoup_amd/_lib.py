@@ -95,6 +95,10 @@ SIGNATURES = [
     ("rcp_plan_heavy_rows", ctypes.c_int, [_vp, _vp, _i32p]),
     ("rcp_plan_row_lengths", ctypes.c_int, [_vp, _i64p]),
     ("rcp_profile", ctypes.c_int, [_vp, ctypes.POINTER(RowsDesc), ctypes.POINTER(BinsDesc), _dp, _u8p]),
+    ("rcp_readset_create_multi", ctypes.c_int, [ctypes.POINTER(ReadsDesc), _i32p, ctypes.c_int32,
+                                                ctypes.POINTER(_vp)]),
+    ("rcp_profile_multi", ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int32, ctypes.POINTER(RowsDesc),
+                                         ctypes.POINTER(BinsDesc), _dp, _u8p, _i32p]),
     ("rcp_calc_coverage", ctypes.c_int, [_vp, _i64p, _vp, _vp, _vp]),
     ("rcp_profile_rle", ctypes.c_int, [ctypes.POINTER(RleDesc), ctypes.POINTER(BinsDesc), ctypes.c_int, _dp, _u8p]),
     ("rcp_rle_encode", ctypes.c_int, [ctypes.c_int32, _i64p, _vp, ctypes.c_int, _vp, _vp, _i64p, _i64p, _vp]),

@@ -16,6 +16,7 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -1096,6 +1097,135 @@ extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, con
         HIP_TRY(rcp::stage_d2h_2d(out, 8 * (size_t)plan->n_rows, d_out.p, 8 * (size_t)plan->out_ld,
                                   8 * (size_t)plan->n_rows, (size_t)plan->n_cols, rs->device, nullptr));
     if (row_valid && plan->n_rows) HIP_TRY(hipMemcpy(row_valid, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost));
+    return RCP_OK;
+    RCP_CATCH
+}
+
+namespace {
+
+// Run fn(i) for i in [0, n) on one host thread each (one per GPU), collecting the first failure's
+// code and message into the calling thread's rcp_last_error().
+template <class F>
+int run_per_device(int n, F fn) {
+    std::vector<int> rc(n, RCP_OK);
+    std::vector<std::string> msg(n);
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (int i = 0; i < n; ++i)
+        th.emplace_back([&, i] {
+            try {
+                rc[i] = fn(i);
+            } catch (const std::bad_alloc&) {
+                rc[i] = fail(RCP_ENOMEM, "host memory exhausted (device thread %d)", i);
+            } catch (...) {
+                rc[i] = fail(RCP_EINVAL, "unexpected C++ exception (device thread %d)", i);
+            }
+            if (rc[i]) msg[i] = g_err;  // g_err is thread-local
+        });
+    for (auto& t : th) t.join();
+    for (int i = 0; i < n; ++i)
+        if (rc[i]) return fail(rc[i], "device %d: %s", i, msg[i].c_str());
+    return RCP_OK;
+}
+
+}  // namespace
+
+extern "C" int rcp_readset_create_multi(const rcp_reads_desc* desc, const int32_t* device_ids, int32_t n_devices,
+                                        rcp_readset** out) {
+    RCP_TRY
+    if (!desc || !device_ids || !out) return fail(RCP_EINVAL, "NULL argument");
+    if (n_devices < 1 || n_devices > 64) return fail(RCP_EINVAL, "n_devices = %d", n_devices);
+    for (int i = 0; i < n_devices; ++i) {
+        out[i] = nullptr;
+        const int rc = check_device(device_ids[i]);
+        if (rc) return rc;
+    }
+    const int rc = run_per_device(n_devices, [&](int i) {
+        rcp_reads_desc d = *desc;
+        d.device = device_ids[i];
+        return rcp_readset_create(&d, nullptr, &out[i]);
+    });
+    if (rc) {
+        for (int i = 0; i < n_devices; ++i) {
+            rcp_readset_destroy(out[i]);
+            out[i] = nullptr;
+        }
+    }
+    return rc;
+    RCP_CATCH
+}
+
+extern "C" int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices, const rcp_rows_desc* rows,
+                                 const rcp_bins_desc* bins, double* out, uint8_t* row_valid, int32_t* row_split) {
+    RCP_TRY
+    if (!readsets || !rows || !bins) return fail(RCP_EINVAL, "NULL argument");
+    if (n_devices < 1 || n_devices > 64) return fail(RCP_EINVAL, "n_devices = %d", n_devices);
+    for (int i = 0; i < n_devices; ++i)
+        if (!readsets[i]) return fail(RCP_EINVAL, "readsets[%d] is NULL", i);
+    const int32_t R = rows->n_rows;
+    if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
+    if (R > 0 && !rows->seg_off) return fail(RCP_EINVAL, "NULL seg_off");
+    // contiguous row blocks balanced by a per-row weight: the row's output (the same for every
+    // row) plus its genomic width (the reads it can touch grow with it)
+    std::vector<double> cum(R + 1, 0.0);
+    for (int32_t r = 0; r < R; ++r) {
+        double w = 0;
+        for (int64_t j = rows->seg_off[r]; j < rows->seg_off[r + 1]; ++j)
+            w += std::max<double>(0.0, (double)rows->seg_end[j] - rows->seg_start[j] + 1);
+        cum[r + 1] = cum[r] + 2048.0 + w;
+    }
+    std::vector<int32_t> split(n_devices + 1, 0);
+    split[n_devices] = R;
+    for (int i = 1; i < n_devices; ++i) {
+        const double target = cum[R] * i / n_devices;
+        split[i] = (int32_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+        split[i] = std::min(std::max(split[i], split[i - 1]), R);
+    }
+    if (row_split) std::copy(split.begin(), split.end(), row_split);
+    std::vector<int64_t> n_cols(n_devices, -1);
+    const int rc = run_per_device(n_devices, [&](int i) {
+        const int32_t r0 = split[i], r1 = split[i + 1];
+        if (r1 <= r0) return (int)RCP_OK;
+        rcp_rows_desc sub = *rows;  // seg_off indexes the shared segment arrays directly
+        sub.n_rows = r1 - r0;
+        sub.seg_off = rows->seg_off + r0;
+        const rcp_readset* rs = readsets[i];
+        rcp_plan* plan = nullptr;
+        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, {0, 0, 0, 0}};
+        int e = rcp_plan_create_ex(rs, &sub, bins, &opts, &plan);
+        if (e) return e;
+        std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
+        DeviceGuard g(rs->device);
+        HIP_TRY(g.err);
+        n_cols[i] = plan->n_cols;
+        hipStream_t s = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(s, hipStreamDestroy);
+        const size_t cells = (size_t)plan->out_ld * (size_t)plan->n_cols;
+        DevBuf d_out, d_valid;
+        HIP_TRY(d_out.alloc(8 * std::max<size_t>(cells, 1)));
+        HIP_TRY(d_valid.alloc(std::max<int32_t>(plan->n_rows, 1)));
+        e = rcp_plan_execute(plan, d_out.as<double>(), d_valid.as<uint8_t>(), nullptr, s);
+        if (e) return e;
+        e = rcp_plan_status(plan, s);
+        if (e) return e;
+        // this device's block of rows of every column of the caller's R matrix
+        if (out && plan->n_cols)
+            HIP_TRY(rcp::stage_d2h_2d(out + r0, 8 * (size_t)R, d_out.p, 8 * (size_t)plan->out_ld,
+                                      8 * (size_t)plan->n_rows, (size_t)plan->n_cols, rs->device, s));
+        if (row_valid) {
+            HIP_TRY(hipMemcpyAsync(row_valid + r0, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        }
+        return (int)RCP_OK;
+    });
+    if (rc) return rc;
+    int64_t nc = -1;
+    for (int i = 0; i < n_devices; ++i) {
+        if (n_cols[i] < 0) continue;
+        if (nc >= 0 && n_cols[i] != nc) return fail(RCP_EINVAL, "row blocks disagree on the column count");
+        nc = n_cols[i];
+    }
     return RCP_OK;
     RCP_CATCH
 }

@@ -67,6 +67,31 @@ class ReadSet:
         check(lib.rcp_readset_info(self.h, ctypes.byref(nk), cptr(self.stream_off, _lib._i64p)))
         self.n = nk.value
 
+    @classmethod
+    def multi(cls, chrom, start, end, strand, seqlengths, devices, strand_filter=None):
+        """rcp_readset_create_multi: one readset of the same host reads on each of ``devices``
+        (one host thread per GPU), for profile_multi."""
+        lib = _lib.lib()
+        seql = np.ascontiguousarray(seqlengths, dtype=np.int64)
+        keep = [np.ascontiguousarray(chrom, dtype=np.int32), np.ascontiguousarray(start, dtype=np.int32),
+                np.ascontiguousarray(end, dtype=np.int32), np.ascontiguousarray(strand, dtype=np.int8)]
+        sf = -1 if strand_filter is None else STRAND.get(strand_filter, strand_filter)
+        d = _lib.ReadsDesc(int(keep[1].shape[0]), ptr(keep[0]), ptr(keep[1]), ptr(keep[2]), ptr(keep[3]),
+                           len(seql), cptr(seql, _lib._i64p), 0, 0, int(sf))
+        dev = np.ascontiguousarray(devices, dtype=np.int32)
+        hs = (ctypes.c_void_p * len(dev))()
+        check(lib.rcp_readset_create_multi(ctypes.byref(d), cptr(dev, _lib._i32p), len(dev), hs))
+        out = []
+        for h, dv in zip(hs, dev):
+            rs = cls.__new__(cls)
+            rs.device, rs.seqlengths, rs.h = int(dv), seql, ctypes.c_void_p(h)
+            nk = ctypes.c_int64()
+            rs.stream_off = np.zeros(3 * len(seql) + 1, dtype=np.int64)
+            check(lib.rcp_readset_info(rs.h, ctypes.byref(nk), cptr(rs.stream_off, _lib._i64p)))
+            rs.n = nk.value
+            out.append(rs)
+        return out
+
     @property
     def chrom_has_reads(self):
         so = self.stream_off
@@ -272,6 +297,22 @@ def profile_host(readset, rows, bins, out, valid=None):
         check(_lib.lib().rcp_profile(readset.h, ctypes.byref(rd), ctypes.byref(bd), cptr(out, _lib._dp),
                                      None if valid is None else cptr(valid, _lib._u8p)))
     return out
+
+
+def profile_multi(readsets, rows, bins):
+    """rcp_profile_multi: rows cut into one contiguous block per readset (each on its own GPU),
+    one host thread per GPU, every block copied straight into the R column-major host matrix.
+    Returns (matrix (n_rows, n_cols) float64, validity bool, block boundaries)."""
+    rd = rows.desc()
+    bd = bins.desc()
+    n = len(readsets)
+    hs = (ctypes.c_void_p * n)(*[r.h.value for r in readsets])
+    out = np.zeros((bins.n_cols, rows.n_rows), np.float64)
+    valid = np.zeros(rows.n_rows, np.uint8)
+    split = np.zeros(n + 1, np.int32)
+    check(_lib.lib().rcp_profile_multi(hs, n, ctypes.byref(rd), ctypes.byref(bd), cptr(out, _lib._dp),
+                                       cptr(valid, _lib._u8p), cptr(split, _lib._i32p)))
+    return out.T, valid.astype(bool), split
 
 
 def rle_arrays(coverages):

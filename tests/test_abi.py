@@ -70,6 +70,10 @@ def test_no_device_fails_loudly():
     h = ctypes.c_void_p()
     assert L.rcp_readset_create(ctypes.byref(d), None, ctypes.byref(h)) == -6  # RCP_ENODEVICE
     assert not h.value
+    dev = np.zeros(2, np.int32)
+    hs = (ctypes.c_void_p * 2)()
+    assert L.rcp_readset_create_multi(ctypes.byref(d), _lib.cptr(dev, _lib._i32p), 2, hs) == -6
+    assert not hs[0] and not hs[1]
     with pytest.raises(_lib.RcpError):
         from recoup_amd.engine import ReadSet
         ReadSet(c, s, e, st, sl)
@@ -84,4 +88,6 @@ def test_null_arguments_are_rejected():
     L = _lib.lib()
     assert L.rcp_readset_create(None, None, None) == -1
     assert L.rcp_plan_create(None, None, None, None) == -1
+    assert L.rcp_profile_multi(None, 1, None, None, None, None, None) == -1
+    assert L.rcp_readset_create_multi(None, None, 1, None) == -1
     assert L.rcp_plan_destroy(None) == 0 or L.rcp_plan_destroy(None) == -1

@@ -115,3 +115,26 @@ def test_rcp_profile_staged_copy(gpu, n_rows, n_bins):
     assert rc == 0 and out.nbytes > (4 << 20)
     assert np.array_equal(out.view(np.uint64), np.asfortranarray(ref).view(np.uint64))
     np.testing.assert_array_equal(valid.astype(bool), rv)
+
+
+@pytest.mark.parametrize("n_dev,R,nb", [(3, 500, 100), (2, 300, 1000), (4, 3, 40)])
+def test_profile_multi_bit_equal(gpu, n_dev, R, nb):
+    """rcp_profile_multi (one host thread per device, row blocks copied into the caller's matrix)
+    gives the bits of the single-device pass.  The box has one GPU, so the 'devices' are n_dev
+    readsets on device 0 driven by n_dev concurrent host threads (R = 3 < 4 devices: an empty
+    block)."""
+    from recoup_amd.engine import ReadSet, profile_multi
+    from tests.test_gpu_random import CHROM_LEN, make_reads, single_rows
+    rng = np.random.default_rng(11 + n_dev)
+    reads = make_reads(rng, 80_000)
+    rows = single_rows(rng, R, 2000, edge=R > 10)
+    bins = Bins([("whole", nb)])
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    ref, rvalid = Plan(rs, rows, bins).run()
+    multi = ReadSet.multi(*reads, CHROM_LEN, [0] * n_dev)
+    mat, valid, split = profile_multi(multi, rows, bins)
+    assert split[0] == 0 and split[-1] == R and (np.diff(split) >= 0).all()
+    np.testing.assert_array_equal(valid, rvalid)
+    assert np.array_equal(mat.view(np.uint64), np.ascontiguousarray(ref).view(np.uint64))
+    for r in multi:
+        r.close()

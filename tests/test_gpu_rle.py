@@ -16,16 +16,23 @@ pytestmark = pytest.mark.gpu
 FLANK = (2000, 2000)
 
 
-def _c1_inputs(region, flank):
+def _c1_inputs(region, flank, keep=None):
     """coverageRef of test.input over test.genome twice: one sample list keeps the
-    DeviceCoverage, the other the materialised list of Rle (as a saved recoup object has it)."""
+    DeviceCoverage, the other the materialised list of Rle (as a saved recoup object has it).
+    keep: number of reads kept of sample 2 (unequal library sizes)."""
     from tests.golden import c1_cases
     from tests.test_gpu_api import _input
     d = c1_cases.load_inputs()
     G = c1_cases.genome(d)
     genome = ra.GRanges(G["chrom"], G["start"], G["end"], G["strand"], names=G["names"])
-    inp_dev = ra.coverageRef(_input({"d": d}), genome, region, flank)
-    inp_rle = ra.coverageRef(_input({"d": d}), genome, region, flank)
+
+    def inputs():
+        inp = _input({"d": d})
+        if keep is not None:
+            inp[1]["ranges"] = inp[1]["ranges"][np.arange(keep)]
+        return inp
+    inp_dev = ra.coverageRef(inputs(), genome, region, flank)
+    inp_rle = ra.coverageRef(inputs(), genome, region, flank)
     for s in inp_rle:
         s["coverage"] = s["coverage"].to_list(rle=True)
     return genome, inp_dev, inp_rle
@@ -71,7 +78,7 @@ def test_sliced_coverage(gpu):
 
 def test_numeric_rle_after_linear_normalisation(gpu):
     """normalize = "linear" multiplies the stored coverage (a numeric Rle afterwards)."""
-    genome, inp_dev, inp_rle = _c1_inputs("tss", FLANK)
+    genome, inp_dev, inp_rle = _c1_inputs("tss", FLANK, keep=37_000)
     f = ra.calcLinearFactors(inp_dev)
     assert (f != 1).any()
     ra.normalizeLinear(inp_dev)

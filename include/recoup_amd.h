@@ -142,7 +142,8 @@ typedef struct {
     int64_t grid;               /* workgroups of the pileup kernel */
     int32_t tile_rows;
     int32_t chunk_positions;
-    int32_t pileup_kernel;   /* 0: general pileup kernel; 1: lean kernel (pile + store waves) */
+    int32_t pileup_kernel;   /* 0: general pileup kernel; 1: lean kernel (pile + store waves);
+                              * 2: lean kernel, general bins; 3: row-wave kernel */
     int32_t reserved;
 } rcp_plan_info;
 
@@ -155,10 +156,11 @@ RCP_API int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows, co
  * (pile + store waves) where every row is one plain range with uniform power-of-two bins,
  * else the general kernel; RCP_KERNEL_GENERAL forces the general kernel; RCP_KERNEL_LEAN_ANY
  * also routes other mean plans whose chunks fit one wave pass through the lean kernel's
- * general-bins mode.  All choices give bit-identical results.  heavy_threshold: candidate
+ * general-bins mode; RCP_KERNEL_ROWS forces the row-wave kernel (whole rows per wave: AUTO takes
+ * it for mean plans with multi-range rows).  All choices give bit-identical results.  heavy_threshold: candidate
  * reads per column chunk above which a skewed row is piled by many workgroups first
  * (-1 = default 4096, 0 = never).  out_ld: see the field. */
-enum { RCP_KERNEL_AUTO = 0, RCP_KERNEL_GENERAL = 1, RCP_KERNEL_LEAN_ANY = 2 };
+enum { RCP_KERNEL_AUTO = 0, RCP_KERNEL_GENERAL = 1, RCP_KERNEL_LEAN_ANY = 2, RCP_KERNEL_ROWS = 3 };
 typedef struct {
     int32_t pileup_kernel;
     int32_t heavy_threshold;

@@ -26,6 +26,10 @@
 #include "rcp_rng.h"
 #include "rcp_stage.h"
 
+#ifndef RCP_ROWS_AUTO
+#define RCP_ROWS_AUTO 1  // plans with multi-range rows take the row-wave pileup kernel
+#endif
+
 extern "C" {
 hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
                           int32_t* vout, int64_t n, int end_bit, hipStream_t stream);
@@ -43,6 +47,8 @@ void rcp_tile_geometry(int* tile, int* rounds_max);
 int rcp_lean_max_bins(void);
 int rcp_lean_gen_max_bins(void);
 size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
+size_t rcp_pileup_rows_lds_bytes(void);
+int rcp_rows_window_cap(void);
 hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
                               const int8_t* strand, int32_t n_chrom, int32_t strand_filter, int merge, uint64_t* keys,
                               int32_t* vals, hipStream_t stream);
@@ -539,7 +545,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     if (!rs || !rows || !out) return fail(RCP_EINVAL, "NULL argument");
     const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, 0, {0, 0, 0, 0}};
     if (!opts) opts = &default_opts;
-    if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_LEAN_ANY)
+    if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_ROWS)
         return fail(RCP_EINVAL, "pileup_kernel = %d", opts->pileup_kernel);
     *out = nullptr;
     const rcp_bins_desc coverage_only{};  // bins == NULL: a calcCoverage-only plan
@@ -777,6 +783,15 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         }
         const bool gen = !lean && base && kind == RCP_KERNEL_LEAN_ANY && stage_cap <= rcp_lean_gen_max_bins();
         P.lean = lean ? 1 : (gen ? 2 : 0);
+        // row-wave kernel (lean == 3): mean bins of any layout, every bin inside one window;
+        // AUTO takes it for plans with multi-range rows (coverageRnaRef, genebody + flanks)
+        bool rows_ok = !cov_only && bins->stat == RCP_STAT_MEAN && kind != RCP_KERNEL_GENERAL && !lean;
+        for (int p = 0; rows_ok && p < P.n_parts; ++p)
+            if (!P.part[p].per_base && part_max_bin[p] > rcp_rows_window_cap()) rows_ok = false;
+        bool multi_rows = false;
+        for (int r = 0; !multi_rows && r < R; ++r) multi_rows = B.row_seg[r + 1] - B.row_seg[r] > 1;
+        if (rows_ok && (kind == RCP_KERNEL_ROWS || (kind == RCP_KERNEL_AUTO && multi_rows && RCP_ROWS_AUTO)))
+            P.lean = 3;
     }
 
     // ---- skewed rows: heavy slots sized for the eligible (short enough) rows
@@ -938,7 +953,8 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.interp_scratch = plan->scratch.as<double>();
     P.csr_off = nullptr;
     P.csr_out = nullptr;
-    plan->lds = P.lean ? rcp_pileup_lean_lds_bytes(&P) : rcp_pileup_lds_bytes(&P, cov_only ? 1 : 0);
+    plan->lds = P.lean == 3 ? rcp_pileup_rows_lds_bytes()
+                            : (P.lean ? rcp_pileup_lean_lds_bytes(&P) : rcp_pileup_lds_bytes(&P, cov_only ? 1 : 0));
     // general kernel: 2 rounds (32 rows) per workgroup (C3: 0.88 ms vs 0.91 with 4 rounds, 0.89
     // with 1), 1 when the row table is small, so that the grid still holds two workgroups per
     // CU (C2: 10k rows -> 625 workgroups instead of 157; pileup 0.076 -> 0.063 ms)

@@ -198,6 +198,98 @@ __device__ __forceinline__ void pileup_row(const RcpPlanDev& P, int r, int32_t P
     }
 }
 
+// Stream the candidate reads of the (segment, stream) pairs held one per lane -- lane t: segment
+// `sg`, genomic piece [gps, gpe] of the row window starting at row position P0, candidate reads
+// [lo, hi) (empty: lo == hi) -- into the window's difference array.  A wave scan lays the pairs'
+// candidates end to end; batches of 256 candidates cross pair boundaries, so a row window costs
+// one round trip per 256 candidates with the next batch in flight while the current one is
+// added.  The per-pair data a candidate needs is picked by a scalar loop over the (few) pairs a
+// batch spans.
+__device__ __forceinline__ void pile_pairs(const RcpPlanDev& P, const RcpSeg& sg, int32_t gps, int32_t gpe,
+                                           uint32_t lo, uint32_t hi, int32_t P0, int32_t* diff, int sh) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t cnt = hi - lo;
+    const uint32_t incl = wave_inclusive_scan(cnt);
+    const uint32_t start = incl - cnt;
+    const uint32_t N = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (N == 0) return;  // wave-uniform
+    const uint32_t delta = lo - start;  // candidate q of this pair is read lo + (q - start)
+    const uint64_t nz = __ballot(cnt > 0);
+    // pairs a batch [q0, q0 + 256) spans: nonempty pairs from the one holding q0
+    int pl = __builtin_ctzll(nz);  // pair holding the next batch's first candidate (loads)
+    auto load_batch = [&](uint32_t q0, int2 (&dst)[4], int (&sel)[4]) {
+        while ((uint32_t)__builtin_amdgcn_readlane((int)incl, pl) <= q0) ++pl;
+        uint32_t qc[4], d[4];
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)delta, pl);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            qc[u] = min(q0 + lane + 64u * u, N - 1);
+            sel[u] = pl;
+            d[u] = d0;
+        }
+        const uint32_t qe = min(q0 + 256u, N);
+        uint64_t m = pl < 63 ? nz & (~0ull << (pl + 1)) : 0ull;
+        while (m) {
+            const int p = __builtin_ctzll(m);
+            const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)start, p);
+            if (sp >= qe) break;
+            const uint32_t dp = (uint32_t)__builtin_amdgcn_readlane((int)delta, p);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (qc[u] >= sp) {
+                    sel[u] = p;
+                    d[u] = dp;
+                }
+            m &= m - 1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dst[u] = P.se[qc[u] + d[u]];
+    };
+    int pa = pl;  // pair holding the current batch's first candidate (adds)
+    auto add_batch = [&](uint32_t q0, const int2 (&rd)[4], const int (&sel)[4]) {
+        while ((uint32_t)__builtin_amdgcn_readlane((int)incl, pa) <= q0) ++pa;
+        const uint32_t qe = min(q0 + 256u, N);
+        uint64_t m = nz & (~0ull << pa);
+        while (m) {
+            const int p = __builtin_ctzll(m);
+            if ((uint32_t)__builtin_amdgcn_readlane((int)start, p) >= qe) break;
+            RcpSeg o;
+            o.lo = __builtin_amdgcn_readlane(sg.lo, p);
+            o.hi = __builtin_amdgcn_readlane(sg.hi, p);
+            o.off = __builtin_amdgcn_readlane(sg.off, p);
+            o.gfirst = __builtin_amdgcn_readlane(sg.gfirst, p);
+            o.gcount = (int16_t)__builtin_amdgcn_readlane((int)sg.gcount, p);
+            o.rev = (uint8_t)__builtin_amdgcn_readlane((int)sg.rev, p);
+            o.multi = (uint8_t)__builtin_amdgcn_readlane((int)sg.multi, p);
+            o.nb_lo = __builtin_amdgcn_readlane(sg.nb_lo, p);
+            o.nb_hi = __builtin_amdgcn_readlane(sg.nb_hi, p);
+            const int32_t ps = __builtin_amdgcn_readlane(gps, p);
+            const int32_t pe = __builtin_amdgcn_readlane(gpe, p);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (sel[u] == p && q0 + lane + 64u * u < N) add_read(P, o, rd[u], ps, pe, P0, diff, sh);
+            m &= m - 1;
+        }
+    };
+    int2 cur[4];
+    int scur[4];
+    load_batch(0, cur, scur);
+    for (uint32_t q0 = 0; q0 < N; q0 += 256) {
+        int2 nx[4];
+        int snx[4];
+        if (q0 + 256 < N) load_batch(q0 + 256, nx, snx);
+        add_batch(q0, cur, scur);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            cur[u] = nx[u];
+            scur[u] = snx[u];
+        }
+    }
+}
+
+#ifndef RCP_MR_DIR
+#define RCP_MR_DIR 1
+#endif
 // One wave piles row r (any number of segments x strand streams, e.g. a coverageRnaRef
 // c(flank, exons, flank) row) over row positions [P0, P0 + npos).  pileup_row walks the
 // (segment, stream) pairs one after the other -- one HBM round trip per pair, a dozen per
@@ -212,6 +304,12 @@ __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int3
     const int32_t P1 = P0 + npos;
     const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
     const int n_all = (j1 - j0) * 3;
+#if RCP_MR_DIR
+    // directory of the row's chromosome stream c*3 (all pairs in the merged layout, pair
+    // stream 0 in the stranded one)
+    const int64_t d0 = P.row_info[r].d0;
+    const int32_t dnb = P.row_info[r].nb;
+#endif
     for (int t0 = 0; t0 < n_all; t0 += 64) {
         // ---- lane t: pair (segment j, stream s)
         const int t = t0 + lane;
@@ -235,6 +333,17 @@ __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int3
                 lo = P.seg_lo[j * 3 + s];
                 hi = P.seg_hi[j * 3 + s];
                 const bool full = (a == sg.off) && (b == sg.off + len);
+#if RCP_MR_DIR
+                // a piece of the segment (the chunk window cuts it): its reads lie inside the
+                // directory buckets of its ends -- one load per bound, no bisection, at most a
+                // bucket (~8 reads) of extra candidates at each end, which add_read drops
+                if (lo < hi && !full && (P.merged || s == 0)) {
+                    const int32_t bl = min(max(gps, 0) >> P.dir_shift, dnb - 1);
+                    const int32_t bu = min(max(gpe, 0) >> P.dir_shift, dnb - 1);
+                    lo = max(lo, (uint32_t)P.dir_l[2 * (d0 + bl)]);
+                    hi = min(hi, (uint32_t)P.dir_u[2 * (d0 + bu + 1)]);
+                } else
+#endif
                 if (lo < hi && !full && hi - lo > 1024) {
                     lo = lower_bound_pmax(P.pmax, lo, hi, gps);
                     hi = upper_bound_start(P.se, lo, hi, gpe);
@@ -242,83 +351,7 @@ __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int3
                 if (hi < lo) hi = lo;
             }
         }
-        const uint32_t cnt = hi - lo;
-        const uint32_t incl = wave_inclusive_scan(cnt);
-        const uint32_t start = incl - cnt;
-        const uint32_t N = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        if (N == 0) continue;  // wave-uniform
-        const uint32_t delta = lo - start;  // candidate q of this pair is read lo + (q - start)
-        const uint64_t nz = __ballot(cnt > 0);
-        // pairs a batch [q0, q0 + 256) spans: nonempty pairs from the one holding q0
-        int pl = __builtin_ctzll(nz);  // pair holding the next batch's first candidate (loads)
-        auto load_batch = [&](uint32_t q0, int2 (&dst)[4], int (&sel)[4]) {
-            while ((uint32_t)__builtin_amdgcn_readlane((int)incl, pl) <= q0) ++pl;
-            uint32_t qc[4], d[4];
-            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)delta, pl);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                qc[u] = min(q0 + lane + 64u * u, N - 1);
-                sel[u] = pl;
-                d[u] = d0;
-            }
-            const uint32_t qe = min(q0 + 256u, N);
-            uint64_t m = pl < 63 ? nz & (~0ull << (pl + 1)) : 0ull;
-            while (m) {
-                const int p = __builtin_ctzll(m);
-                const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)start, p);
-                if (sp >= qe) break;
-                const uint32_t dp = (uint32_t)__builtin_amdgcn_readlane((int)delta, p);
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (qc[u] >= sp) {
-                        sel[u] = p;
-                        d[u] = dp;
-                    }
-                m &= m - 1;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) dst[u] = P.se[qc[u] + d[u]];
-        };
-        int pa = pl;  // pair holding the current batch's first candidate (adds)
-        auto add_batch = [&](uint32_t q0, const int2 (&rd)[4], const int (&sel)[4]) {
-            while ((uint32_t)__builtin_amdgcn_readlane((int)incl, pa) <= q0) ++pa;
-            const uint32_t qe = min(q0 + 256u, N);
-            uint64_t m = nz & (~0ull << pa);
-            while (m) {
-                const int p = __builtin_ctzll(m);
-                if ((uint32_t)__builtin_amdgcn_readlane((int)start, p) >= qe) break;
-                RcpSeg o;
-                o.lo = __builtin_amdgcn_readlane(sg.lo, p);
-                o.hi = __builtin_amdgcn_readlane(sg.hi, p);
-                o.off = __builtin_amdgcn_readlane(sg.off, p);
-                o.gfirst = __builtin_amdgcn_readlane(sg.gfirst, p);
-                o.gcount = (int16_t)__builtin_amdgcn_readlane((int)sg.gcount, p);
-                o.rev = (uint8_t)__builtin_amdgcn_readlane((int)sg.rev, p);
-                o.multi = (uint8_t)__builtin_amdgcn_readlane((int)sg.multi, p);
-                o.nb_lo = __builtin_amdgcn_readlane(sg.nb_lo, p);
-                o.nb_hi = __builtin_amdgcn_readlane(sg.nb_hi, p);
-                const int32_t ps = __builtin_amdgcn_readlane(gps, p);
-                const int32_t pe = __builtin_amdgcn_readlane(gpe, p);
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (sel[u] == p && q0 + lane + 64u * u < N) add_read(P, o, rd[u], ps, pe, P0, diff, sh);
-                m &= m - 1;
-            }
-        };
-        int2 cur[4];
-        int scur[4];
-        load_batch(0, cur, scur);
-        for (uint32_t q0 = 0; q0 < N; q0 += 256) {
-            int2 nx[4];
-            int snx[4];
-            if (q0 + 256 < N) load_batch(q0 + 256, nx, snx);
-            add_batch(q0, cur, scur);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                cur[u] = nx[u];
-                scur[u] = snx[u];
-            }
-        }
+        pile_pairs(P, sg, gps, gpe, lo, hi, P0, diff, sh);
     }
 }
 
@@ -1582,6 +1615,247 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
 
 
 // ---------------------------------------------------------------------------------
+// Row-wave pileup kernel (mean bins; P.lean == 3): every wave owns whole rows.  For plans
+// whose rows are lists of ranges (coverageRnaRef's c(flank, exons, flank), genebody rows with
+// flanks) the (row tile, column chunk) work items of the general kernel cost a dependent chain
+// of round trips per chunk (pair table -> piece bounds -> first reads) and a workgroup barrier
+// per round that waits for the round's longest row.  Here a wave claims a row (per-XCD
+// counters, then the other XCDs' leftovers), loads its (segment, stream) pair table once, and
+// walks the row's parts in windows of <= kRWCap positions -- usually one window per part --
+// streaming each pair's reads once (pieces cut by a window edge are narrowed by the bucket
+// directory, no bisection), then scans the window and writes its bins straight to the R
+// column-major output.  No barrier anywhere: waves are independent, so the row-length skew
+// of exon lists only costs the wave that drew the long row.
+// ---------------------------------------------------------------------------------
+constexpr int kRWaves = 4;                       // waves per workgroup (independent)
+constexpr int kRWSh = 5;                         // 32 positions per lane at most
+constexpr int kRWCap = 64 * (1 << kRWSh) - 1;    // positions per window (+1 sentinel)
+constexpr int kRWWords = 8 + 64 * ((1 << kRWSh) + 4);  // per wave: 8 zero words + padded array
+
+extern "C" int rcp_rows_window_cap(void) { return kRWCap; }
+
+// A wave writes one row's bins: 8 bytes per 128-B line of each column.  The 16 rows of a line are
+// claimed together by waves of one XCD, so plain stores meet in that L2 and leave it as whole
+// lines; non-temporal stores would go out as partial-line writes.
+#ifndef RCP_ROWS_NT
+#define RCP_ROWS_NT 0
+#endif
+__device__ __forceinline__ void rows_store(double x, double* p) {
+#if RCP_ROWS_NT
+    __builtin_nontemporal_store(x, p);
+#else
+    *p = x;
+#endif
+}
+
+__global__ void __launch_bounds__(64 * kRWaves) __attribute__((amdgpu_waves_per_eu(4)))
+rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restrict__ binsum) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * kRWWords + 8;
+    if (lane < 8) diff[lane - 8] = 0;  // cum[lp(-1)] == 0
+    const int xcd = blockIdx.x & 7;
+    const int n_tiles = (P.n_rows + kTile - 1) / kTile;
+    const size_t R = (size_t)P.out_ld;
+    const int ns = P.merged ? 1 : 3;
+    const double sc = P.scale;
+    // Work: tiles of 16 rows (one 128-B line of every output column).  Workgroups on XCD x take
+    // tiles x, x + 8, ... from that XCD's counter (then the other XCDs' leftovers): one global
+    // atomic per tile.  Inside the workgroup the four waves take the tile's rows one at a time
+    // from a 64-bit LDS word (tile << 32 | next row); the wave that draws row index 16 fetches
+    // the next tile and publishes it, waves drawing past 16 wait for the new tile.
+    unsigned long long* queue = reinterpret_cast<unsigned long long*>(smem + 4 * kRWaves * kRWWords);
+    constexpr uint32_t kEmpty = 0xFFFFFFFEu, kDone = 0xFFFFFFFFu;
+    if (threadIdx.x == 0) *queue = ((unsigned long long)kEmpty << 32) | kTile;
+    __syncthreads();
+    auto fetch_tile = [&]() -> uint32_t {
+        for (int k = 0; k < 8; ++k) {
+            const int xs = (xcd + k) & 7;
+            const uint32_t nt = (uint32_t)max((n_tiles - xs + 7) / 8, 0);
+            if (nt == 0) continue;
+            uint32_t j = 0;
+            if (lane == 0) j = atomicAdd(&P.status[8 + xs], 1u);
+            j = __builtin_amdgcn_readfirstlane(j);
+            if (j < nt) return j * 8 + xs;
+        }
+        return kDone;
+    };
+    auto claim = [&]() -> int {
+        while (true) {
+            unsigned long long w = 0;
+            if (lane == 0) w = atomicAdd(queue, 1ull);
+            const uint32_t tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(w >> 32));
+            const uint32_t idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w);
+            if (tile == kDone) return -1;
+            if (idx < (uint32_t)kTile && tile != kEmpty) {
+                const int r = (int)tile * kTile + (int)idx;
+                if (r < P.n_rows) return r;
+                continue;  // the short last tile
+            }
+            if (idx == (uint32_t)kTile) {
+                const uint32_t t = fetch_tile();
+                if (lane == 0) atomicExch(queue, ((unsigned long long)t << 32));
+                continue;
+            }
+            // another wave is fetching the next tile
+            while ((uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(*(volatile unsigned long long*)queue >> 32)) == tile)
+                __builtin_amdgcn_s_sleep(2);
+        }
+    };
+    auto zero_cols = [&](int r, const RcpPart& part, int32_t n) {
+        for (int32_t k = lane; k < n; k += 64) {
+            rows_store(0.0, out + (size_t)(part.col_off + k) * R + r);
+            if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = 0;
+        }
+    };
+    for (int r = claim(); r >= 0; r = claim()) {
+        const uint4 rc = *reinterpret_cast<const uint4*>(P.rec + r);  // flags, row_len, heavy, off
+        const int32_t flags = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.x);
+        const int32_t nr = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.y);
+        const int32_t heavy = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.z);
+        if (!(flags & RCP_REC_VALID)) {  // NULL row -> zeros (profile.R:191-197)
+            for (int p = 0; p < P.n_parts; ++p) zero_cols(r, P.part[p], P.part[p].n_bins);
+            continue;
+        }
+        const int j0 = P.row_info[r].j0, j1 = P.row_info[r].j1;
+        const int64_t d0 = P.row_info[r].d0;
+        const int32_t dnb = P.row_info[r].nb;
+        const int n_all = (j1 - j0) * ns;
+        // lane t: pair t of the row (pairs 64.. are reloaded per window)
+        auto load_pair = [&](int t, RcpSeg& sg, uint32_t& lo, uint32_t& hi, int& st) {
+            sg = RcpSeg{};
+            lo = hi = 0;
+            st = 0;
+            if (t < n_all) {
+                const int j = j0 + t / ns;
+                st = t % ns;
+                sg = P.segs[j];
+                lo = P.seg_lo[j * 3 + st];
+                hi = P.seg_hi[j * 3 + st];
+                if (!sg.query_ok || !((sg.streams >> st) & 1)) hi = lo;
+            }
+        };
+        RcpSeg sg0;
+        uint32_t plo0, phi0;
+        int pst0;
+        load_pair(lane, sg0, plo0, phi0, pst0);
+        for (int p = 0; p < P.n_parts; ++p) {
+            const RcpPart part = P.part[p];
+            int32_t head, L;
+            rcp_part_slice(part, nr, &head, &L);
+            const int32_t n = part.n_bins;
+            if (!part.per_base && L < n) continue;  // interpolation row: rcp_interp_kernel
+            if (part.per_base && L != n) {
+                if (lane == 0) atomicOr(P.status, RCP_STATUS_WIDTH);
+                zero_cols(r, part, n);
+                continue;
+            }
+            int32_t bs = 1, lay = -1;
+            if (!part.per_base) {
+                bs = L / n;
+                const int32_t dif = L - bs * n;
+                if (dif) {
+                    lay = P.lay_index[part.lay_base + dif];
+                    if (lay < 0) {
+                        if (lane == 0) atomicOr(P.status, RCP_STATUS_INTERP);
+                        lay = -1;
+                    }
+                }
+            }
+            const int32_t kw = max(1, kRWCap / (bs + (lay >= 0 ? 1 : 0)));  // bins per window
+            const bool pow2 = lay < 0 && (bs & (bs - 1)) == 0;
+            const double dd = (double)bs, rdd = 1.0 / dd;
+            for (int32_t k0 = 0; k0 < n; k0 += kw) {
+                const int32_t k1 = min(n, k0 + kw);
+                const int32_t e0 = bin_edge(bs, lay, P.lay_cnt, k0);
+                const int32_t npos = bin_edge(bs, lay, P.lay_cnt, k1) - e0;
+                const int32_t W0 = head + e0, W1 = W0 + npos;
+                const int need = (npos + 1 + 63) >> 6;
+                const int sh = need <= 4 ? 2 : 32 - __clz(need - 1);
+                const int per = 1 << sh;
+                {
+                    int4* d4 = reinterpret_cast<int4*>(diff);
+                    for (int q = lane; q < (per + 4) * 16; q += 64) d4[q] = make_int4(0, 0, 0, 0);
+                }
+                lds_order();
+                if (heavy >= 0) {
+                    // skewed row: its difference array was piled up by rcp_heavy_pileup_kernel
+                    const int32_t* g = P.heavy_gdiff + (size_t)heavy * P.heavy_stride;
+                    int32_t carry = 0;
+                    for (int q = lane; q < W0; q += 64) carry += g[q];
+                    carry = wave_sum(carry);
+                    for (int q = lane; q <= npos; q += 64) diff[lp(q, sh)] = g[W0 + q] + (q == 0 ? carry : 0);
+                } else {
+                    for (int t0 = 0; t0 < n_all; t0 += 64) {
+                        RcpSeg sg = sg0;
+                        uint32_t lo = plo0, hi = phi0;
+                        int st = pst0;
+                        if (t0 > 0) load_pair(t0 + lane, sg, lo, hi, st);
+                        // this pair's piece of the window
+                        const int32_t len = sg.hi - sg.lo + 1;
+                        const int32_t a = max(W0, sg.off), b = min(W1, sg.off + len);
+                        int32_t gps = 0, gpe = -1;
+                        if (a < b && lo < hi) {
+                            if (!sg.rev) {
+                                gps = sg.lo + (a - sg.off);
+                                gpe = sg.lo + (b - 1 - sg.off);
+                            } else {
+                                gpe = sg.hi - (a - sg.off);
+                                gps = sg.hi - (b - 1 - sg.off);
+                            }
+                            const bool full = (a == sg.off) && (b == sg.off + len);
+                            if (!full && (P.merged || st == 0)) {
+                                // reads of the piece lie inside the directory buckets of its ends
+                                const int32_t bl = min(max(gps, 0) >> P.dir_shift, dnb - 1);
+                                const int32_t bu = min(max(gpe, 0) >> P.dir_shift, dnb - 1);
+                                lo = max(lo, (uint32_t)P.dir_l[2 * (d0 + bl)]);
+                                hi = min(hi, (uint32_t)P.dir_u[2 * (d0 + bu + 1)]);
+                            } else if (!full && hi - lo > 1024) {
+                                lo = lower_bound_pmax(P.pmax, lo, hi, gps);
+                                hi = upper_bound_start(P.se, lo, hi, gpe);
+                            }
+                            if (hi < lo) hi = lo;
+                        } else {
+                            hi = lo;
+                        }
+                        pile_pairs(P, sg, gps, gpe, lo, hi, W0, diff, sh);
+                    }
+                }
+                lds_order();
+                scan_wave<true>(diff, per);
+                lds_order();
+                // bins [k0, k1): numerator = cum[b - 1] - cum[a - 1] (exact integers; the same
+                // divisions as the general kernel's epilogue, so the same bits)
+                const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
+                for (int32_t k = k0 + lane; k < k1; k += 64) {
+                    const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
+                    const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
+                    const uint32_t num = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
+                    double x;
+                    if (pow2) x = ((double)num * sc) * rdd;
+                    else if (lay < 0) x = ((double)num * sc) / dd;
+                    else x = ((double)num * sc) / (double)(b - a);
+                    rows_store(x, out + (size_t)(part.col_off + k) * R + r);
+                    if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = (int64_t)num;
+                }
+                lds_order();
+            }
+        }
+    }
+    // the last workgroup out resets the tile counters for the next launch
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const uint32_t done = atomicAdd(&P.status[16], 1u);
+        if (done == gridDim.x - 1) {
+            for (int x = 0; x < 8; ++x) atomicExch(&P.status[8 + x], 0u);
+            atomicExch(&P.status[16], 0u);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // Lean pileup kernel: persistent workgroups of pile waves + store waves.
 // For plans whose every row is one plain range with uniform power-of-two bins of one
 // wave chunk (C4 peaks, C5 per-base, TSS/TES windows: rcp_plan decides, `P.lean`), the
@@ -2280,11 +2554,25 @@ static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* bin
     return hipGetLastError();
 }
 
+extern "C" size_t rcp_pileup_rows_lds_bytes(void) { return 4 * (size_t)kRWaves * kRWWords + 16; }
+
+static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* binsum, hipStream_t s) {
+    // persistent: four workgroups (16 waves) per CU, a multiple of 8 (workgroup b serves XCD
+    // b % 8), never more workgroups than tiles
+    const int cus = std::max(1, P->n_cus);
+    const int64_t tiles = ((int64_t)P->n_rows + kTile - 1) / kTile;  // at least a tile per workgroup
+    const int64_t grid = std::min<int64_t>(((int64_t)4 * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
+    hipLaunchKernelGGL(rcp_pileup_rows_kernel, dim3((unsigned)grid), dim3(64 * kRWaves), rcp_pileup_rows_lds_bytes(), s,
+                       *P, out, binsum);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_t* binsum, int csr,
                                         hipStream_t stream) {
     if (P->n_rows == 0) return hipSuccess;
+    if (!csr && P->lean == 3 && P->stat == 0) return launch_pileup_rows(P, out, binsum, stream);
     const size_t lds = rcp_pileup_lds_bytes(P, csr);
-    if (!csr && P->lean && P->stat == 0 && !binsum) return launch_pileup_lean(P, out, stream);
+    if (!csr && (P->lean == 1 || P->lean == 2) && P->stat == 0 && !binsum) return launch_pileup_lean(P, out, stream);
     if (csr) return launch_pileup_t<false, true>(P, out, binsum, lds, stream);
     if (P->stat == 1) return launch_pileup_t<true, false>(P, out, binsum, lds, stream);
     return launch_pileup_t<false, false>(P, out, binsum, lds, stream);

@@ -116,7 +116,7 @@ def test_lean_heavy_rows(gpu):
 
 def test_lean_kernel_choice(gpu):
     """Power-of-two uniform bins of single-range rows take the lean kernel (1); R-RNG layouts,
-    other widths and exon lists stay on the general kernel (0) unless the general-bins mode is
+    other widths stay on the general kernel (0), exon lists take the row-wave kernel (3), unless the general-bins mode is
     opted in (kernel="lean_any"); medians always stay on the general kernel."""
     from recoup_amd.engine import Bins, Plan, ReadSet, RowTable
     rng = np.random.default_rng(71)
@@ -129,7 +129,8 @@ def test_lean_kernel_choice(gpu):
     for mode, other in (("auto", 0), ("lean_any", 2)):
         assert Plan(rs, rows, Bins([("whole", 150)]), kernel=mode).info["pileup_kernel"] == other   # dif != 0
         assert Plan(rs, rows, Bins([("whole", 200)]), kernel=mode).info["pileup_kernel"] == other   # bs = 10
-        assert Plan(rs, exons, Bins([("whole", 100)]), kernel=mode).info["pileup_kernel"] == other
+        # exon lists: the row-wave kernel under auto (tests/test_gpu_rows.py)
+        assert Plan(rs, exons, Bins([("whole", 100)]), kernel=mode).info["pileup_kernel"] == (3 if mode == "auto" else 2)
         assert Plan(rs, rows, Bins([("whole", 1000)], stat="median"), kernel=mode).info["pileup_kernel"] == 0
         assert Plan(rs, rows, Bins([("whole", 1000)]), kernel=mode).info["pileup_kernel"] == 1
         assert Plan(rs, rows, Bins([("whole", 1000)]), kernel="general").info["pileup_kernel"] == 0

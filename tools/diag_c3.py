@@ -47,11 +47,14 @@ def main():
     for name, parts in cases:
         if only and name.split()[0] not in only:
             continue
-        plan = Plan(rs, rows, Bins(parts, flank=fl))
+        plan = Plan(rs, rows, Bins(parts, flank=fl), kernel=os.environ.get("DIAG_KERNEL", "auto"),
+                    heavy_threshold=int(os.environ.get("DIAG_HEAVY", "-1")))
         out = plan.empty_output()
         t = timed(plan, out)
-        info = {k: plan.info[k] for k in ("n_cols", "n_interp_rows", "lds_bytes", "grid", "chunk_positions",
-                                          "pileup_kernel")}
+        plan.execute(out)
+        info = {"heavy_rows": plan.heavy_rows()}
+        info.update({k: plan.info[k] for k in ("n_cols", "n_interp_rows", "lds_bytes", "grid", "chunk_positions",
+                                          "pileup_kernel")})
         print(f"{name:16s} locate {t[0]:.3f}  pileup {t[1]:.3f}  interp {t[2]:.3f} ms  {info}", flush=True)
         del plan, out
 

@@ -14,7 +14,7 @@ if [ "$mode" = build ]; then
         mkdir -p "$OUT/$name"
         (
         objs=""
-        for src in rcp_kernels.hip rcp_host.cpp rcp_stage.cpp rcp_bam.cpp; do
+        for src in rcp_kernels.hip rcp_rle.hip rcp_host.cpp rcp_stage.cpp rcp_bam.cpp; do
             /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wno-unused-result $defs \
                 -c "$ROOT/recoup_amd/csrc/$src" -o "$OUT/$name/$src.o" || exit 1
             objs="$objs $OUT/$name/$src.o"

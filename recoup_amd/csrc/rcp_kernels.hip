@@ -198,93 +198,115 @@ __device__ __forceinline__ void pileup_row(const RcpPlanDev& P, int r, int32_t P
     }
 }
 
-// Stream the candidate reads of the (segment, stream) pairs held one per lane -- lane t: segment
-// `sg`, genomic piece [gps, gpe] of the row window starting at row position P0, candidate reads
-// [lo, hi) (empty: lo == hi) -- into the window's difference array.  A wave scan lays the pairs'
-// candidates end to end; batches of 256 candidates cross pair boundaries, so a row window costs
-// one round trip per 256 candidates with the next batch in flight while the current one is
-// added.  The per-pair data a candidate needs is picked by a scalar loop over the (few) pairs a
-// batch spans.
+// The candidate reads of the (segment, stream) pairs held one per lane -- lane t: segment `sg`,
+// genomic piece [gps, gpe] of a row window, candidate reads [lo, hi) (empty: lo == hi) -- as one
+// stream: a wave scan lays the pairs' candidates end to end, and batches of 256 candidates
+// cross pair boundaries, so a window costs one round trip per 256 candidates with the next
+// batch in flight while the current one is added.  The per-pair data a candidate needs is
+// picked by a scalar loop over the (few) pairs a batch spans.
+struct PairStream {
+    int32_t gps, gpe;
+    uint32_t incl, start, delta;  // per lane: inclusive / exclusive candidate scan, lo - start
+    uint32_t N;                   // candidates of the window (uniform)
+    uint64_t nz;                  // lanes with candidates
+    int pl, pa;                   // pair holding the next batch to load / to add
+};
+
+__device__ __forceinline__ void ps_prepare(PairStream& ps, int32_t gps, int32_t gpe, uint32_t lo, uint32_t hi) {
+    ps.gps = gps;
+    ps.gpe = gpe;
+    const uint32_t cnt = hi - lo;
+    ps.incl = wave_inclusive_scan(cnt);
+    ps.start = ps.incl - cnt;
+    ps.N = (uint32_t)__builtin_amdgcn_readlane((int)ps.incl, 63);
+    ps.delta = lo - ps.start;  // candidate q of this pair is read lo + (q - start)
+    ps.nz = __ballot(cnt > 0);
+    ps.pl = ps.nz ? __builtin_ctzll(ps.nz) : 0;
+    ps.pa = ps.pl;
+}
+
+// Issue the loads of batch [q0, q0 + 256) (q0 < N; lanes past N load the last candidate again).
+__device__ __forceinline__ void ps_load(const RcpPlanDev& P, PairStream& ps, uint32_t q0, int2 (&dst)[4]) {
+    const int lane = threadIdx.x & 63;
+    while ((uint32_t)__builtin_amdgcn_readlane((int)ps.incl, ps.pl) <= q0) ++ps.pl;
+    uint32_t qc[4], d[4];
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)ps.delta, ps.pl);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        qc[u] = min(q0 + lane + 64u * u, ps.N - 1);
+        d[u] = d0;
+    }
+    const uint32_t qe = min(q0 + 256u, ps.N);
+    uint64_t m = ps.pl < 63 ? ps.nz & (~0ull << (ps.pl + 1)) : 0ull;
+    while (m) {
+        const int p = __builtin_ctzll(m);
+        const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)ps.start, p);
+        if (sp >= qe) break;
+        const uint32_t dp = (uint32_t)__builtin_amdgcn_readlane((int)ps.delta, p);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (qc[u] >= sp) d[u] = dp;
+        m &= m - 1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dst[u] = P.se[qc[u] + d[u]];
+}
+
+// Add batch [q0, q0 + 256) (loaded by ps_load) to the difference array of the window at row
+// position P0; lane t holds pair t's segment `sg`.  Candidate q belongs to the pair p with
+// start_p <= q < incl_p.
+__device__ __forceinline__ void ps_add(const RcpPlanDev& P, const RcpSeg& sg, PairStream& ps, uint32_t q0,
+                                       const int2 (&rd)[4], int32_t P0, int32_t* diff, int sh) {
+    const int lane = threadIdx.x & 63;
+    while ((uint32_t)__builtin_amdgcn_readlane((int)ps.incl, ps.pa) <= q0) ++ps.pa;
+    const uint32_t qe = min(q0 + 256u, ps.N);
+    uint64_t m = ps.nz & (~0ull << ps.pa);
+    while (m) {
+        const int p = __builtin_ctzll(m);
+        const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)ps.start, p);
+        if (sp >= qe) break;
+        const uint32_t ep = (uint32_t)__builtin_amdgcn_readlane((int)ps.incl, p);
+        RcpSeg o;
+        o.lo = __builtin_amdgcn_readlane(sg.lo, p);
+        o.hi = __builtin_amdgcn_readlane(sg.hi, p);
+        o.off = __builtin_amdgcn_readlane(sg.off, p);
+        o.gfirst = __builtin_amdgcn_readlane(sg.gfirst, p);
+        o.gcount = (int16_t)__builtin_amdgcn_readlane((int)sg.gcount, p);
+        o.rev = (uint8_t)__builtin_amdgcn_readlane((int)sg.rev, p);
+        o.multi = (uint8_t)__builtin_amdgcn_readlane((int)sg.multi, p);
+        o.nb_lo = __builtin_amdgcn_readlane(sg.nb_lo, p);
+        o.nb_hi = __builtin_amdgcn_readlane(sg.nb_hi, p);
+        const int32_t gs = __builtin_amdgcn_readlane(ps.gps, p);
+        const int32_t ge = __builtin_amdgcn_readlane(ps.gpe, p);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t q = q0 + lane + 64u * u;
+            if (q >= sp && q < ep) add_read(P, o, rd[u], gs, ge, P0, diff, sh);
+        }
+        m &= m - 1;
+    }
+}
+
+// Pile a prepared stream whose first batch is in `cur` (loaded by ps_load(.., 0, ..)).
+__device__ __forceinline__ void ps_pile(const RcpPlanDev& P, const RcpSeg& sg, PairStream& ps, int2 (&cur)[4],
+                                        int32_t P0, int32_t* diff, int sh) {
+    for (uint32_t q0 = 0; q0 < ps.N; q0 += 256) {
+        int2 nx[4];
+        if (q0 + 256 < ps.N) ps_load(P, ps, q0 + 256, nx);
+        ps_add(P, sg, ps, q0, cur, P0, diff, sh);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = nx[u];
+    }
+}
+
 __device__ __forceinline__ void pile_pairs(const RcpPlanDev& P, const RcpSeg& sg, int32_t gps, int32_t gpe,
                                            uint32_t lo, uint32_t hi, int32_t P0, int32_t* diff, int sh) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t cnt = hi - lo;
-    const uint32_t incl = wave_inclusive_scan(cnt);
-    const uint32_t start = incl - cnt;
-    const uint32_t N = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    if (N == 0) return;  // wave-uniform
-    const uint32_t delta = lo - start;  // candidate q of this pair is read lo + (q - start)
-    const uint64_t nz = __ballot(cnt > 0);
-    // pairs a batch [q0, q0 + 256) spans: nonempty pairs from the one holding q0
-    int pl = __builtin_ctzll(nz);  // pair holding the next batch's first candidate (loads)
-    auto load_batch = [&](uint32_t q0, int2 (&dst)[4], int (&sel)[4]) {
-        while ((uint32_t)__builtin_amdgcn_readlane((int)incl, pl) <= q0) ++pl;
-        uint32_t qc[4], d[4];
-        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)delta, pl);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            qc[u] = min(q0 + lane + 64u * u, N - 1);
-            sel[u] = pl;
-            d[u] = d0;
-        }
-        const uint32_t qe = min(q0 + 256u, N);
-        uint64_t m = pl < 63 ? nz & (~0ull << (pl + 1)) : 0ull;
-        while (m) {
-            const int p = __builtin_ctzll(m);
-            const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)start, p);
-            if (sp >= qe) break;
-            const uint32_t dp = (uint32_t)__builtin_amdgcn_readlane((int)delta, p);
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (qc[u] >= sp) {
-                    sel[u] = p;
-                    d[u] = dp;
-                }
-            m &= m - 1;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) dst[u] = P.se[qc[u] + d[u]];
-    };
-    int pa = pl;  // pair holding the current batch's first candidate (adds)
-    auto add_batch = [&](uint32_t q0, const int2 (&rd)[4], const int (&sel)[4]) {
-        while ((uint32_t)__builtin_amdgcn_readlane((int)incl, pa) <= q0) ++pa;
-        const uint32_t qe = min(q0 + 256u, N);
-        uint64_t m = nz & (~0ull << pa);
-        while (m) {
-            const int p = __builtin_ctzll(m);
-            if ((uint32_t)__builtin_amdgcn_readlane((int)start, p) >= qe) break;
-            RcpSeg o;
-            o.lo = __builtin_amdgcn_readlane(sg.lo, p);
-            o.hi = __builtin_amdgcn_readlane(sg.hi, p);
-            o.off = __builtin_amdgcn_readlane(sg.off, p);
-            o.gfirst = __builtin_amdgcn_readlane(sg.gfirst, p);
-            o.gcount = (int16_t)__builtin_amdgcn_readlane((int)sg.gcount, p);
-            o.rev = (uint8_t)__builtin_amdgcn_readlane((int)sg.rev, p);
-            o.multi = (uint8_t)__builtin_amdgcn_readlane((int)sg.multi, p);
-            o.nb_lo = __builtin_amdgcn_readlane(sg.nb_lo, p);
-            o.nb_hi = __builtin_amdgcn_readlane(sg.nb_hi, p);
-            const int32_t ps = __builtin_amdgcn_readlane(gps, p);
-            const int32_t pe = __builtin_amdgcn_readlane(gpe, p);
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (sel[u] == p && q0 + lane + 64u * u < N) add_read(P, o, rd[u], ps, pe, P0, diff, sh);
-            m &= m - 1;
-        }
-    };
+    PairStream ps;
+    ps_prepare(ps, gps, gpe, lo, hi);
+    if (ps.N == 0) return;  // wave-uniform
     int2 cur[4];
-    int scur[4];
-    load_batch(0, cur, scur);
-    for (uint32_t q0 = 0; q0 < N; q0 += 256) {
-        int2 nx[4];
-        int snx[4];
-        if (q0 + 256 < N) load_batch(q0 + 256, nx, snx);
-        add_batch(q0, cur, scur);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            cur[u] = nx[u];
-            scur[u] = snx[u];
-        }
-    }
+    ps_load(P, ps, 0, cur);
+    ps_pile(P, sg, ps, cur, P0, diff, sh);
 }
 
 #ifndef RCP_MR_DIR

@@ -253,6 +253,18 @@ RCP_API int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bins, 
 RCP_API int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t* d_cov, uint8_t* d_valid,
                       void* hip_stream);
 
+/* calcCoverage one-shot for host callers (the R .Call shim): the coverage of every row of
+ * `rows` over the readset (R/coverage.R:126-226), run-length encoded on the GPU and held on the
+ * host -- exactly the values / lengths of the reference's named list of Rle (NULL rows:
+ * valid[r] = 0 and no runs).  rcp_cov_info gives the sizes; rcp_cov_copy fills caller arrays
+ * (run_off [n_rows + 1]: runs of row r are run_off[r] .. run_off[r+1]-1; values / lengths
+ * [n_runs]; valid [n_rows]; any may be NULL); rcp_cov_free releases it. */
+typedef struct rcp_cov rcp_cov;
+RCP_API int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows, rcp_cov** out);
+RCP_API int rcp_cov_info(const rcp_cov* c, int32_t* n_rows, int64_t* n_runs);
+RCP_API int rcp_cov_copy(const rcp_cov* c, int64_t* run_off, int32_t* values, int32_t* lengths, uint8_t* valid);
+RCP_API int rcp_cov_free(rcp_cov* c);
+
 /* ------------------------------------------------------------------ BAM ingest */
 /* readBam (R/ranges.R:111-146) on the host: BGZF blocks inflated by n_threads threads, mapped
  * alignments (readGAlignments) turned into 1-based ranges on their reference and strand:

@@ -1,0 +1,369 @@
+/* recoup_amd_shim.c -- the .Call shim a recoup maintainer compiles into the R package
+ * (src/ of recoup, linked with -lrecoup_amd) so that the R functions on the hot path run on the
+ * MI355X through the C ABI of include/recoup_amd.h.  r/R/rcp.R holds the R side.
+ *
+ *   R function (reference file:line)                      .Call entry point here
+ *   splitBySeqname + strand filter (R/util.R:1-13,           rcp_R_readset / rcp_R_readsets
+ *       R/coverage.R:141-144)
+ *   calcCoverage / coverageFromRanges (R/coverage.R:126-226) rcp_R_coverage -> list of Rle pieces
+ *   binCoverageMatrix / baseCoverageMatrix / splitVector     rcp_R_profile_rle (the stored $coverage,
+ *       (R/profile.R:100-212, R/util.R:15-85)                    a list of Rle, as R keeps it)
+ *   profileMatrix straight from the reads (fused, one call   rcp_R_profile / rcp_R_profile_multi
+ *       per sample; R/profile.R:1-98)
+ *   readBam (R/ranges.R:111-146)                             rcp_R_read_bam
+ *   preprocessRanges downsample / sampleto (R/ranges.R:32-62) rcp_R_sample_sorted
+ *
+ * Errors: every library call returns an RCP_E* code and is checked only AFTER it returned, so
+ * Rf_error never longjmps through the library's C++ frames.  Memory R hands in is read in
+ * place (INTEGER / REAL vectors); results are written straight into R-allocated vectors (the
+ * profile matrix is R column-major, as rcp_profile writes it).  Not fork-safe: call it from the
+ * R main process, not inside cmclapply's forked workers (R/util.R:364-382). */
+#include <R.h>
+#include <Rinternals.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "recoup_amd.h"
+
+static void check(int rc) {
+    if (rc != RCP_OK) Rf_error("recoup_amd: %s", rcp_last_error());
+}
+
+/* ------------------------------------------------------------------ reads */
+static void readset_finalizer(SEXP p) {
+    rcp_readset* rs = (rcp_readset*)R_ExternalPtrAddr(p);
+    if (rs) {
+        rcp_readset_destroy(rs);
+        R_ClearExternalPtr(p);
+    }
+}
+
+static SEXP wrap_readset(rcp_readset* rs) {
+    SEXP p = PROTECT(R_MakeExternalPtr(rs, R_NilValue, R_NilValue));
+    R_RegisterCFinalizerEx(p, readset_finalizer, TRUE);
+    UNPROTECT(1);
+    return p;
+}
+
+static rcp_reads_desc reads_of(SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP seqlen, SEXP sfilter) {
+    R_xlen_t n = XLENGTH(start);
+    int nchr = LENGTH(seqlen);
+    int64_t* sl = (int64_t*)R_alloc(nchr > 0 ? nchr : 1, sizeof(int64_t));
+    for (int c = 0; c < nchr; ++c) sl[c] = ISNA(REAL(seqlen)[c]) ? -1 : (int64_t)REAL(seqlen)[c];
+    int8_t* st = (int8_t*)R_alloc(n > 0 ? n : 1, 1);
+    for (R_xlen_t i = 0; i < n; ++i) st[i] = (int8_t)INTEGER(strand)[i];
+    rcp_reads_desc d;
+    memset(&d, 0, sizeof d);
+    d.n = (int64_t)n;
+    d.chrom = INTEGER(chrom);
+    d.start = INTEGER(start);
+    d.end = INTEGER(end);
+    d.strand = st;
+    d.n_chrom = nchr;
+    d.seqlen = sl;
+    d.device = 0;
+    d.on_device = 0;
+    d.strand_filter = asInteger(sfilter);
+    return d;
+}
+
+/* .Call("rcp_R_readset", chromCode, start, end, strandCode, seqlengths, strandFilter, device)
+ * chromCode: 0-based seqlevel index; strandCode 0 '+', 1 '-', 2 '*'; seqlengths numeric (NA ok) */
+SEXP rcp_R_readset(SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP seqlen, SEXP sfilter, SEXP dev) {
+    rcp_reads_desc d = reads_of(chrom, start, end, strand, seqlen, sfilter);
+    d.device = asInteger(dev);
+    rcp_readset* rs = NULL;
+    check(rcp_readset_create(&d, NULL, &rs));
+    return wrap_readset(rs);
+}
+
+/* .Call("rcp_R_readsets", <as rcp_R_readset>, devices) -> list of readsets, one per GPU */
+SEXP rcp_R_readsets(SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP seqlen, SEXP sfilter, SEXP devs) {
+    rcp_reads_desc d = reads_of(chrom, start, end, strand, seqlen, sfilter);
+    int nd = LENGTH(devs);
+    rcp_readset** rs = (rcp_readset**)R_alloc(nd > 0 ? nd : 1, sizeof(rcp_readset*));
+    check(rcp_readset_create_multi(&d, INTEGER(devs), nd, rs));
+    SEXP res = PROTECT(allocVector(VECSXP, nd));
+    for (int i = 0; i < nd; ++i) SET_VECTOR_ELT(res, i, wrap_readset(rs[i]));
+    UNPROTECT(1);
+    return res;
+}
+
+/* ------------------------------------------------------------------ rows / bins */
+/* rows: segOff (numeric, n_rows + 1), chrom (0-based, NA = absent chromosome), start, end,
+ * strand, group (0..3 per segment), isList (logical[4]), ignoreStrand (logical) */
+static rcp_rows_desc rows_of(SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
+                             SEXP isList, SEXP ignoreStrand) {
+    int nseg = LENGTH(start), nrow = LENGTH(segOff) - 1;
+    int64_t* off = (int64_t*)R_alloc(nrow + 1, sizeof(int64_t));
+    for (int r = 0; r <= nrow; ++r) off[r] = (int64_t)REAL(segOff)[r];
+    int8_t* st = (int8_t*)R_alloc(nseg > 0 ? nseg : 1, 1);
+    int8_t* gr = (int8_t*)R_alloc(nseg > 0 ? nseg : 1, 1);
+    int32_t* ch = (int32_t*)R_alloc(nseg > 0 ? nseg : 1, sizeof(int32_t));
+    for (int i = 0; i < nseg; ++i) {
+        st[i] = (int8_t)INTEGER(strand)[i];
+        gr[i] = (int8_t)INTEGER(group)[i];
+        ch[i] = INTEGER(chrom)[i] == NA_INTEGER ? -1 : INTEGER(chrom)[i];
+    }
+    uint8_t* il = (uint8_t*)R_alloc(4, 1);
+    for (int g = 0; g < 4; ++g) il[g] = (uint8_t)(g < LENGTH(isList) ? LOGICAL(isList)[g] : 0);
+    rcp_rows_desc rd;
+    memset(&rd, 0, sizeof rd);
+    rd.n_rows = nrow;
+    rd.seg_off = off;
+    rd.seg_chrom = ch;
+    rd.seg_start = INTEGER(start);
+    rd.seg_end = INTEGER(end);
+    rd.seg_strand = st;
+    rd.seg_group = gr;
+    rd.group_is_list = il;
+    rd.ignore_strand = asLogical(ignoreStrand);
+    return rd;
+}
+
+/* bins: where (RCP_WHERE_* per part), flank (2 ints), nBins (per part, 0 = per base),
+ * perBaseWidth (per part), stat (0 mean / 1 median), interp (0 auto .. 3 neighborhood),
+ * rngKind (0 Rejection / 1 Rounding: RNGkind()[3]), scale (linear factor) */
+static rcp_bins_desc bins_of(SEXP where, SEXP flank, SEXP nBins, SEXP pbw, SEXP stat, SEXP interp, SEXP rng,
+                             SEXP scale, int* ncol) {
+    rcp_bins_desc bd;
+    memset(&bd, 0, sizeof bd);
+    bd.n_parts = LENGTH(where);
+    bd.where = INTEGER(where);
+    bd.flank[0] = INTEGER(flank)[0];
+    bd.flank[1] = INTEGER(flank)[1];
+    bd.n_bins = INTEGER(nBins);
+    bd.per_base_width = INTEGER(pbw);
+    bd.stat = asInteger(stat);
+    bd.interp = asInteger(interp);
+    bd.rng_kind = asInteger(rng);
+    bd.scale = asReal(scale);
+    *ncol = 0;
+    for (int p = 0; p < bd.n_parts; ++p) *ncol += INTEGER(nBins)[p] ? INTEGER(nBins)[p] : INTEGER(pbw)[p];
+    return bd;
+}
+
+static SEXP profile_result(SEXP mat, const uint8_t* valid, int nrow) {
+    SEXP v = PROTECT(allocVector(LGLSXP, nrow));
+    for (int r = 0; r < nrow; ++r) LOGICAL(v)[r] = valid[r];
+    SEXP res = PROTECT(allocVector(VECSXP, 2));
+    SET_VECTOR_ELT(res, 0, mat);
+    SET_VECTOR_ELT(res, 1, v);
+    SEXP nm = PROTECT(allocVector(STRSXP, 2));
+    SET_STRING_ELT(nm, 0, mkChar("profile"));
+    SET_STRING_ELT(nm, 1, mkChar("valid"));
+    setAttrib(res, R_NamesSymbol, nm);
+    UNPROTECT(3);
+    return res;
+}
+
+/* ------------------------------------------------------------------ profiles */
+/* .Call("rcp_R_profile", readset, <rows: 8 args>, <bins: 8 args>)
+ * -> list(profile = n_rows x n_cols double matrix, valid = logical) */
+SEXP rcp_R_profile(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
+                   SEXP isList, SEXP ignoreStrand, SEXP where, SEXP flank, SEXP nBins, SEXP pbw, SEXP stat,
+                   SEXP interp, SEXP rng, SEXP scale) {
+    rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
+    int ncol = 0;
+    rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
+    SEXP out = PROTECT(allocMatrix(REALSXP, rd.n_rows, ncol)); /* R column-major, filled in place */
+    uint8_t* valid = (uint8_t*)R_alloc(rd.n_rows ? rd.n_rows : 1, 1);
+    int rc = rcp_profile((const rcp_readset*)R_ExternalPtrAddr(rsp), &rd, &bd, REAL(out), valid);
+    if (rc != RCP_OK) {
+        UNPROTECT(1);
+        check(rc);
+    }
+    SEXP res = profile_result(out, valid, rd.n_rows);
+    UNPROTECT(1);
+    return res;
+}
+
+/* .Call("rcp_R_profile_multi", list of readsets (one per GPU, rcp_R_readsets), <rows>, <bins>):
+ * row blocks on every GPU at once (the reference's cmclapply over regions) */
+SEXP rcp_R_profile_multi(SEXP rsl, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
+                         SEXP isList, SEXP ignoreStrand, SEXP where, SEXP flank, SEXP nBins, SEXP pbw,
+                         SEXP stat, SEXP interp, SEXP rng, SEXP scale) {
+    rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
+    int ncol = 0;
+    rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
+    int nd = LENGTH(rsl);
+    rcp_readset** rs = (rcp_readset**)R_alloc(nd > 0 ? nd : 1, sizeof(rcp_readset*));
+    for (int i = 0; i < nd; ++i) rs[i] = (rcp_readset*)R_ExternalPtrAddr(VECTOR_ELT(rsl, i));
+    SEXP out = PROTECT(allocMatrix(REALSXP, rd.n_rows, ncol));
+    uint8_t* valid = (uint8_t*)R_alloc(rd.n_rows ? rd.n_rows : 1, 1);
+    int rc = rcp_profile_multi(rs, nd, &rd, &bd, REAL(out), valid, NULL);
+    if (rc != RCP_OK) {
+        UNPROTECT(1);
+        check(rc);
+    }
+    SEXP res = profile_result(out, valid, rd.n_rows);
+    UNPROTECT(1);
+    return res;
+}
+
+/* .Call("rcp_R_profile_rle", runOff (numeric, n_rows + 1), values (integer or double),
+ *       lengths (integer), isNull (logical), <bins: 8 args>, device)
+ * binCoverageMatrix / baseCoverageMatrix of the stored coverage list (list of Rle flattened
+ * by .rcpRleArrays); -> list(profile, valid) */
+SEXP rcp_R_profile_rle(SEXP runOff, SEXP values, SEXP lengths, SEXP isNull, SEXP where, SEXP flank, SEXP nBins,
+                       SEXP pbw, SEXP stat, SEXP interp, SEXP rng, SEXP scale, SEXP dev) {
+    int nrow = LENGTH(runOff) - 1;
+    int64_t* off = (int64_t*)R_alloc(nrow + 1, sizeof(int64_t));
+    for (int r = 0; r <= nrow; ++r) off[r] = (int64_t)REAL(runOff)[r];
+    uint8_t* nul = (uint8_t*)R_alloc(nrow > 0 ? nrow : 1, 1);
+    for (int r = 0; r < nrow; ++r) nul[r] = (uint8_t)(LOGICAL(isNull)[r] != 0);
+    rcp_rle_desc cd;
+    memset(&cd, 0, sizeof cd);
+    cd.n_rows = nrow;
+    cd.run_off = off;
+    cd.lengths = INTEGER(lengths);
+    if (TYPEOF(values) == INTSXP) cd.ivalues = INTEGER(values);
+    else cd.dvalues = REAL(values);
+    cd.is_null = nul;
+    int ncol = 0;
+    rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
+    SEXP out = PROTECT(allocMatrix(REALSXP, nrow, ncol));
+    uint8_t* valid = (uint8_t*)R_alloc(nrow ? nrow : 1, 1);
+    int rc = rcp_profile_rle(&cd, &bd, asInteger(dev), REAL(out), valid);
+    if (rc != RCP_OK) {
+        UNPROTECT(1);
+        check(rc);
+    }
+    SEXP res = profile_result(out, valid, nrow);
+    UNPROTECT(1);
+    return res;
+}
+
+/* ------------------------------------------------------------------ coverage */
+/* .Call("rcp_R_coverage", readset, <rows: 8 args>)
+ * -> list(runOff = numeric n_rows + 1, values = integer, lengths = integer, valid = logical):
+ * the pieces of calcCoverage's named list of Rle (R/coverage.R:171-173), from which the R side
+ * builds S4Vectors::Rle(values, lengths) per valid row without expanding it */
+SEXP rcp_R_coverage(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
+                    SEXP isList, SEXP ignoreStrand) {
+    rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
+    rcp_cov* cov = NULL;
+    check(rcp_coverage_rle((const rcp_readset*)R_ExternalPtrAddr(rsp), &rd, &cov));
+    int32_t nrow = 0;
+    int64_t nruns = 0;
+    int rc = rcp_cov_info(cov, &nrow, &nruns);
+    if (rc != RCP_OK) {
+        rcp_cov_free(cov);
+        check(rc);
+    }
+    SEXP off = PROTECT(allocVector(REALSXP, nrow + 1));
+    SEXP val = PROTECT(allocVector(INTSXP, (R_xlen_t)nruns));
+    SEXP len = PROTECT(allocVector(INTSXP, (R_xlen_t)nruns));
+    SEXP ok = PROTECT(allocVector(LGLSXP, nrow));
+    int64_t* o64 = (int64_t*)R_alloc(nrow + 1, sizeof(int64_t));
+    uint8_t* v8 = (uint8_t*)R_alloc(nrow > 0 ? nrow : 1, 1);
+    rc = rcp_cov_copy(cov, o64, INTEGER(val), INTEGER(len), v8);
+    rcp_cov_free(cov);
+    if (rc != RCP_OK) {
+        UNPROTECT(4);
+        check(rc);
+    }
+    for (int r = 0; r <= nrow; ++r) REAL(off)[r] = (double)o64[r];
+    for (int r = 0; r < nrow; ++r) LOGICAL(ok)[r] = v8[r];
+    SEXP res = PROTECT(allocVector(VECSXP, 4));
+    SET_VECTOR_ELT(res, 0, off);
+    SET_VECTOR_ELT(res, 1, val);
+    SET_VECTOR_ELT(res, 2, len);
+    SET_VECTOR_ELT(res, 3, ok);
+    SEXP nm = PROTECT(allocVector(STRSXP, 4));
+    SET_STRING_ELT(nm, 0, mkChar("runOff"));
+    SET_STRING_ELT(nm, 1, mkChar("values"));
+    SET_STRING_ELT(nm, 2, mkChar("lengths"));
+    SET_STRING_ELT(nm, 3, mkChar("valid"));
+    setAttrib(res, R_NamesSymbol, nm);
+    UNPROTECT(6);
+    return res;
+}
+
+/* ------------------------------------------------------------------ BAM, RNG */
+/* .Call("rcp_R_read_bam", path, spliceAction (0 keep / 1 remove / 2 split), removeQ, threads)
+ * -> list(seqnames = character, seqlengths = numeric, chrom = integer (0-based), start, end,
+ *         strand = integer (0 '+', 1 '-')) */
+SEXP rcp_R_read_bam(SEXP path, SEXP splice, SEXP q, SEXP threads) {
+    rcp_bam* bam = NULL;
+    check(rcp_bam_read(CHAR(STRING_ELT(path, 0)), asInteger(splice), asReal(q), asInteger(threads), &bam));
+    int64_t n = 0, nal = 0;
+    int32_t nref = 0;
+    int rc = rcp_bam_info(bam, &n, &nref, &nal);
+    if (rc != RCP_OK) {
+        rcp_bam_free(bam);
+        check(rc);
+    }
+    SEXP nm = PROTECT(allocVector(STRSXP, nref));
+    for (int32_t i = 0; i < nref; ++i) SET_STRING_ELT(nm, i, mkChar(rcp_bam_ref_name(bam, i)));
+    SEXP sl = PROTECT(allocVector(REALSXP, nref));
+    SEXP ch = PROTECT(allocVector(INTSXP, (R_xlen_t)n));
+    SEXP st = PROTECT(allocVector(INTSXP, (R_xlen_t)n));
+    SEXP en = PROTECT(allocVector(INTSXP, (R_xlen_t)n));
+    SEXP sd = PROTECT(allocVector(INTSXP, (R_xlen_t)n));
+    int64_t* rl = (int64_t*)R_alloc(nref > 0 ? nref : 1, sizeof(int64_t));
+    int8_t* s8 = (int8_t*)R_alloc(n > 0 ? (size_t)n : 1, 1);
+    rc = rcp_bam_copy(bam, rl, INTEGER(ch), INTEGER(st), INTEGER(en), s8);
+    rcp_bam_free(bam);
+    if (rc != RCP_OK) {
+        UNPROTECT(6);
+        check(rc);
+    }
+    for (int32_t i = 0; i < nref; ++i) REAL(sl)[i] = (double)rl[i];
+    for (int64_t i = 0; i < n; ++i) INTEGER(sd)[i] = s8[i];
+    SEXP res = PROTECT(allocVector(VECSXP, 6));
+    SEXP names = PROTECT(allocVector(STRSXP, 6));
+    const char* keys[6] = {"seqnames", "seqlengths", "chrom", "start", "end", "strand"};
+    SEXP vals[6] = {nm, sl, ch, st, en, sd};
+    for (int k = 0; k < 6; ++k) {
+        SET_VECTOR_ELT(res, k, vals[k]);
+        SET_STRING_ELT(names, k, mkChar(keys[k]));
+    }
+    setAttrib(res, R_NamesSymbol, names);
+    UNPROTECT(8);
+    return res;
+}
+
+/* .Call("rcp_R_sample_sorted", seed, kind, libSizes (numeric), size)
+ * set.seed(seed); lapply(libSizes, function(x) sort(sample(x, size))) in R's RNG stream order
+ * (R/ranges.R:32-62) -> list of 1-based read indices (numeric) */
+SEXP rcp_R_sample_sorted(SEXP seed, SEXP kind, SEXP libSizes, SEXP size) {
+    rcp_rng* g = NULL;
+    check(rcp_rng_create((uint32_t)asInteger(seed), asInteger(kind), &g));
+    int ns = LENGTH(libSizes);
+    int64_t k = (int64_t)asReal(size);
+    SEXP res = PROTECT(allocVector(VECSXP, ns));
+    int64_t* idx = (int64_t*)R_alloc(k > 0 ? (size_t)k : 1, sizeof(int64_t));
+    for (int i = 0; i < ns; ++i) {
+        int rc = rcp_rng_sample_sorted(g, (int64_t)REAL(libSizes)[i], k, idx);
+        if (rc != RCP_OK) {
+            rcp_rng_free(g);
+            UNPROTECT(1);
+            check(rc);
+        }
+        SEXP v = PROTECT(allocVector(REALSXP, (R_xlen_t)k));
+        for (int64_t j = 0; j < k; ++j) REAL(v)[j] = (double)idx[j];
+        SET_VECTOR_ELT(res, i, v);
+        UNPROTECT(1);
+    }
+    rcp_rng_free(g);
+    UNPROTECT(1);
+    return res;
+}
+
+/* ------------------------------------------------------------------ registration */
+static const R_CallMethodDef call_methods[] = {
+    {"rcp_R_readset", (DL_FUNC)&rcp_R_readset, 7},
+    {"rcp_R_readsets", (DL_FUNC)&rcp_R_readsets, 7},
+    {"rcp_R_profile", (DL_FUNC)&rcp_R_profile, 17},
+    {"rcp_R_profile_multi", (DL_FUNC)&rcp_R_profile_multi, 17},
+    {"rcp_R_profile_rle", (DL_FUNC)&rcp_R_profile_rle, 13},
+    {"rcp_R_coverage", (DL_FUNC)&rcp_R_coverage, 9},
+    {"rcp_R_read_bam", (DL_FUNC)&rcp_R_read_bam, 4},
+    {"rcp_R_sample_sorted", (DL_FUNC)&rcp_R_sample_sorted, 4},
+    {NULL, NULL, 0}};
+
+void R_init_recoup(DllInfo* dll) {
+    R_registerRoutines(dll, NULL, call_methods, NULL, NULL);
+    R_useDynamicSymbols(dll, FALSE);
+}

@@ -102,6 +102,10 @@ SIGNATURES = [
     ("rcp_calc_coverage", ctypes.c_int, [_vp, _i64p, _vp, _vp, _vp]),
     ("rcp_profile_rle", ctypes.c_int, [ctypes.POINTER(RleDesc), ctypes.POINTER(BinsDesc), ctypes.c_int, _dp, _u8p]),
     ("rcp_rle_encode", ctypes.c_int, [ctypes.c_int32, _i64p, _vp, ctypes.c_int, _vp, _vp, _i64p, _i64p, _vp]),
+    ("rcp_coverage_rle", ctypes.c_int, [_vp, ctypes.POINTER(RowsDesc), ctypes.POINTER(_vp)]),
+    ("rcp_cov_info", ctypes.c_int, [_vp, _i32p, _i64p]),
+    ("rcp_cov_copy", ctypes.c_int, [_vp, _i64p, _i32p, _i32p, _u8p]),
+    ("rcp_cov_free", ctypes.c_int, [_vp]),
     ("rcp_bam_read", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                     ctypes.POINTER(_vp)]),
     ("rcp_bam_info", ctypes.c_int, [_vp, _i64p, _i32p, _i64p]),

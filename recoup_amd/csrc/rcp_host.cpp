@@ -1324,6 +1324,86 @@ extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int3
 }
 
 // =====================================================================================
+// calcCoverage for host callers: the Rle list on the host (what the R shim hands back)
+// =====================================================================================
+struct rcp_cov {
+    int32_t n_rows = 0;
+    std::vector<int64_t> run_off;
+    std::vector<int32_t> values, lengths;
+    std::vector<uint8_t> valid;
+};
+
+extern "C" int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows, rcp_cov** out) {
+    RCP_TRY
+    if (!rs || !rows || !out) return fail(RCP_EINVAL, "NULL argument");
+    *out = nullptr;
+    rcp_plan* plan = nullptr;
+    int rc = rcp_plan_create(rs, rows, nullptr, &plan);
+    if (rc) return rc;
+    std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
+    DeviceGuard g(rs->device);
+    HIP_TRY(g.err);
+    const int32_t R = plan->n_rows;
+    auto res = std::make_unique<rcp_cov>();
+    res->n_rows = R;
+    std::vector<int64_t> off((size_t)R + 1, 0);
+    for (int32_t r = 0; r < R; ++r) off[r + 1] = off[r] + plan->row_len[r];
+    const int64_t n = off[R];
+    if (n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "%lld coverage positions", (long long)n);
+    DevBuf d_cov, d_valid, d_values, d_lengths;
+    HIP_TRY(d_cov.alloc(4 * std::max<int64_t>(n, 1)));
+    HIP_TRY(d_valid.alloc(std::max<int32_t>(R, 1)));
+    HIP_TRY(d_values.alloc(4 * std::max<int64_t>(n, 1)));
+    HIP_TRY(d_lengths.alloc(4 * std::max<int64_t>(n, 1)));
+    rc = rcp_calc_coverage(plan, off.data(), d_cov.as<int32_t>(), d_valid.as<uint8_t>(), nullptr);
+    if (rc) return rc;
+    rc = rcp_plan_status(plan, nullptr);
+    if (rc) return rc;
+    res->run_off.assign((size_t)R + 1, 0);
+    int64_t n_runs = 0;
+    rc = rcp_rle_encode(R, off.data(), d_cov.as<int32_t>(), rs->device, d_values.as<int32_t>(),
+                        d_lengths.as<int32_t>(), res->run_off.data(), &n_runs, nullptr);
+    if (rc) return rc;
+    res->values.resize((size_t)std::max<int64_t>(n_runs, 0));
+    res->lengths.resize((size_t)std::max<int64_t>(n_runs, 0));
+    res->valid.resize((size_t)R);
+    if (n_runs > 0) {
+        HIP_TRY(hipMemcpy(res->values.data(), d_values.p, 4 * (size_t)n_runs, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(res->lengths.data(), d_lengths.p, 4 * (size_t)n_runs, hipMemcpyDeviceToHost));
+    }
+    if (R > 0) HIP_TRY(hipMemcpy(res->valid.data(), d_valid.p, (size_t)R, hipMemcpyDeviceToHost));
+    *out = res.release();
+    return RCP_OK;
+    RCP_CATCH
+}
+
+extern "C" int rcp_cov_info(const rcp_cov* c, int32_t* n_rows, int64_t* n_runs) {
+    RCP_TRY
+    if (!c) return fail(RCP_EINVAL, "NULL coverage");
+    if (n_rows) *n_rows = c->n_rows;
+    if (n_runs) *n_runs = (int64_t)c->values.size();
+    return RCP_OK;
+    RCP_CATCH
+}
+
+extern "C" int rcp_cov_copy(const rcp_cov* c, int64_t* run_off, int32_t* values, int32_t* lengths,
+                            uint8_t* valid) {
+    RCP_TRY
+    if (!c) return fail(RCP_EINVAL, "NULL coverage");
+    if (run_off) std::copy(c->run_off.begin(), c->run_off.end(), run_off);
+    if (values) std::copy(c->values.begin(), c->values.end(), values);
+    if (lengths) std::copy(c->lengths.begin(), c->lengths.end(), lengths);
+    if (valid) std::copy(c->valid.begin(), c->valid.end(), valid);
+    return RCP_OK;
+    RCP_CATCH
+}
+
+extern "C" int rcp_cov_free(rcp_cov* c) {
+    delete c;
+    return RCP_OK;
+}
+
+// =====================================================================================
 // profiles of a host coverage list of Rle (the reference's $coverage object)
 // =====================================================================================
 namespace {

@@ -138,3 +138,31 @@ def test_profile_multi_bit_equal(gpu, n_dev, R, nb):
     assert np.array_equal(mat.view(np.uint64), np.ascontiguousarray(ref).view(np.uint64))
     for r in multi:
         r.close()
+
+
+def test_coverage_rle_host_one_shot(c1):
+    """rcp_coverage_rle (what the R shim binds for calcCoverage): the host Rle list equals the
+    device calcCoverage + rcp_rle_encode path, NULL rows included."""
+    from recoup_amd.engine import Plan
+    rows = helpers.tss_rows(c1["G"])
+    L = _lib.lib()
+    for rs in c1["rs"]:
+        ref = Plan(rs, rows, None).coverage(rle=True)
+        rd = rows.desc()
+        h = ctypes.c_void_p()
+        assert L.rcp_coverage_rle(rs.h, ctypes.byref(rd), ctypes.byref(h)) == 0
+        nr, nruns = ctypes.c_int32(), ctypes.c_int64()
+        assert L.rcp_cov_info(h, ctypes.byref(nr), ctypes.byref(nruns)) == 0
+        assert nr.value == rows.n_rows
+        off = np.zeros(nr.value + 1, np.int64)
+        vals = np.zeros(max(nruns.value, 1), np.int32)
+        lens = np.zeros(max(nruns.value, 1), np.int32)
+        valid = np.zeros(nr.value, np.uint8)
+        assert L.rcp_cov_copy(h, off.ctypes.data_as(_lib._i64p), vals.ctypes.data_as(_lib._i32p),
+                              lens.ctypes.data_as(_lib._i32p), valid.ctypes.data_as(_lib._u8p)) == 0
+        assert L.rcp_cov_free(h) == 0
+        for r, e in enumerate(ref):
+            assert bool(valid[r]) == (e is not None)
+            if e is not None:
+                np.testing.assert_array_equal(vals[off[r]:off[r + 1]], e[0])
+                np.testing.assert_array_equal(lens[off[r]:off[r + 1]], e[1])

@@ -168,7 +168,11 @@ typedef struct {
                                  * 0 = n_rows (plain R column-major); >= n_rows otherwise.  A multiple
                                  * of 16 keeps every 16-row column segment on whole 128-B lines
                                  * (RCP_OUT_LD_PADDED picks the next multiple of 16) */
-    int32_t reserved[4];        /* zero */
+    int32_t min_col_chunks;     /* lean plans: cut each part into at least this many column chunks
+                                 * (0 = auto: enough (row tile, chunk) work items for the persistent
+                                 * grid -- small row tables, e.g. one GPU's shard, get more chunks so
+                                 * the last items do not leave most workgroups idle) */
+    int32_t reserved[3];        /* zero */
 } rcp_plan_opts;
 #define RCP_OUT_LD_PADDED (-1)
 RCP_API int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,

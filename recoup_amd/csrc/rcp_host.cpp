@@ -26,6 +26,15 @@
 #include "rcp_rng.h"
 #include "rcp_stage.h"
 
+// auto split off: on one GPU's 1/8, 1/4, 1/2 shard of C4, 4 and 8 column chunks instead of 2
+// were slower (1/8: pileup 0.109 -> 0.143 / 0.203 ms; profiles/r02c/lean_chunk_split_ab.log) --
+// an item's time is set by its 64 rows' read round trips, not by its width
+#ifndef RCP_LEAN_ITEMS_PER_WG
+#define RCP_LEAN_ITEMS_PER_WG 0
+#endif
+constexpr int kLeanItemsPerWg = RCP_LEAN_ITEMS_PER_WG;  // work items per persistent workgroup, at least
+constexpr int kLeanMinChunkBins = 64;                   // no column chunks narrower than this
+
 #ifndef RCP_ROWS_AUTO
 #define RCP_ROWS_AUTO 1  // plans with multi-range rows take the row-wave pileup kernel
 #endif
@@ -543,7 +552,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
                                   const rcp_plan_opts* opts, rcp_plan** out) {
     RCP_TRY
     if (!rs || !rows || !out) return fail(RCP_EINVAL, "NULL argument");
-    const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, 0, {0, 0, 0, 0}};
+    const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, 0, 0, {0, 0, 0}};
     if (!opts) opts = &default_opts;
     if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_ROWS)
         return fail(RCP_EINVAL, "pileup_kernel = %d", opts->pileup_kernel);
@@ -792,6 +801,39 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         for (int r = 0; !multi_rows && r < R; ++r) multi_rows = B.row_seg[r + 1] - B.row_seg[r] > 1;
         if (rows_ok && (kind == RCP_KERNEL_ROWS || (kind == RCP_KERNEL_AUTO && multi_rows && RCP_ROWS_AUTO)))
             P.lean = 3;
+    }
+    // ---- lean plans with few row tiles (one GPU's shard of a region table): the persistent
+    // grid (two workgroups per CU) takes (row tile, column chunk) items; with few items per
+    // workgroup the last ones leave most workgroups idle, so cut the parts into more column
+    // chunks (each streams only its reads: crange) until there are >= kLeanItemsPerWg per
+    // workgroup, or opts->min_col_chunks asks for more
+    if (P.lean == 1 && R > 0) {
+        int cus = 256;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, rs->device) != hipSuccess || cus <= 0)
+            cus = 256;
+        const int64_t grid = (2 * (int64_t)cus + 7) / 8 * 8;
+        const int64_t tiles = ((int64_t)R + rcp_tile_rows() - 1) / rcp_tile_rows();
+        auto can_split = [&]() {
+            if (P.n_chunks_total * 2 > RCP_MAX_CRANGE_CHUNKS) return false;
+            for (int p = 0; p < P.n_parts; ++p)
+                if (P.part[p].chunk_bins < 2 * kLeanMinChunkBins) return false;
+            return true;
+        };
+        auto split = [&]() {
+            P.n_chunks_total = 0;
+            for (int p = 0; p < P.n_parts; ++p) {
+                RcpPart& pt = P.part[p];
+                const int32_t nch = 2 * pt.n_chunks;
+                pt.chunk_bins = (pt.n_bins + nch - 1) / nch;
+                pt.n_chunks = (pt.n_bins + pt.chunk_bins - 1) / pt.chunk_bins;
+                P.n_chunks_total += pt.n_chunks;
+            }
+        };
+        while (can_split() && (tiles * P.n_chunks_total < kLeanItemsPerWg * grid ||
+                               P.n_chunks_total < opts->min_col_chunks))
+            split();
+        P.stage_cap = 1;
+        for (int p = 0; p < P.n_parts; ++p) P.stage_cap = std::max(P.stage_cap, P.part[p].chunk_bins);
     }
 
     // ---- skewed rows: heavy slots sized for the eligible (short enough) rows
@@ -1094,7 +1136,7 @@ extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, con
     rcp_plan* plan = nullptr;
     // padded column stride on the device (whole 128-B lines per 16-row column segment); the
     // staged copy drops the padding on the way into R's n_rows x n_cols matrix
-    rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, {0, 0, 0, 0}};
+    rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, {0, 0, 0}};
     int rc = rcp_plan_create_ex(rs, rows, bins, &opts, &plan);
     if (rc) return rc;
     std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
@@ -1207,7 +1249,7 @@ extern "C" int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices
         sub.seg_off = rows->seg_off + r0;
         const rcp_readset* rs = readsets[i];
         rcp_plan* plan = nullptr;
-        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, {0, 0, 0, 0}};
+        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, {0, 0, 0}};
         int e = rcp_plan_create_ex(rs, &sub, bins, &opts, &plan);
         if (e) return e;
         std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);

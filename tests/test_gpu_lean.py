@@ -182,3 +182,18 @@ def test_lean_general_exon_lists(gpu, stranded):
     assert kind == 2
     check(lean, exp, rtol=1e-9, atol=1e-12)
     same(lean, gen)
+
+
+@pytest.mark.parametrize("chunks", [4, 8])
+def test_lean_more_column_chunks(gpu, chunks):
+    """rcp_plan_opts.min_col_chunks: the lean plan cut into more column chunks (each streaming
+    only its reads through crange) gives the same bits."""
+    from recoup_amd.engine import Bins, Plan, ReadSet
+    rng = np.random.default_rng(900 + chunks)
+    reads = make_reads(rng, 100_000)
+    rows = single_rows(rng, 300, 2000)
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    base = Plan(rs, rows, Bins([("whole", 1000)]))
+    more = Plan(rs, rows, Bins([("whole", 1000)]), min_col_chunks=chunks)
+    assert base.info["pileup_kernel"] == 1 and more.info["pileup_kernel"] == 1
+    same(more.run(), base.run())

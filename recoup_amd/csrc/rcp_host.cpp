@@ -222,6 +222,22 @@ struct rcp_readset {
     ReadLayout stranded, merged;
 };
 
+// tools-only phase timing of rcp_plan_create_ex (build with -DRCP_PLAN_TIMING=1)
+#if RCP_PLAN_TIMING
+#include <chrono>
+struct PlanTimer {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), t = t0;
+    void mark(const char* what) {
+        const auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "[plan] %-14s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+#define PLAN_MARK(what) ptimer.mark(what)
+#else
+#define PLAN_MARK(what) ((void)0)
+#endif
+
 int rcp_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
 
 extern "C" const char* rcp_version(void) { return "recoup_amd 0.1.0 (gfx950)"; }
@@ -349,6 +365,9 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     if (d->seqlen)
         for (int c = 0; c < d->n_chrom; ++c) rs->seqlen[c] = d->seqlen[c] < 0 ? -1 : d->seqlen[c];
     const int64_t n = d->n;
+#if RCP_PLAN_TIMING
+    PlanTimer ptimer;
+#endif
 
     // inputs on device
     DevBuf in_chrom, in_start, in_end, in_strand;
@@ -369,10 +388,13 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
         pe = in_end.as<int32_t>();
         pst = in_strand.as<int8_t>();
     }
+    PLAN_MARK("reads H2D");
     rc = build_layout(rs.get(), d, pc, ps, pe, pst, 0, &rs->stranded, s);
     if (rc) return rc;
+    PLAN_MARK("stranded layout");
     rc = build_layout(rs.get(), d, pc, ps, pe, pst, 1, &rs->merged, s);
     if (rc) return rc;
+    PLAN_MARK("merged layout");
     HIP_TRY(rs->d_seqlen.alloc(8 * d->n_chrom));
     HIP_TRY(hipMemcpyAsync(rs->d_seqlen.p, rs->seqlen.data(), 8 * d->n_chrom, hipMemcpyHostToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -539,6 +561,32 @@ size_t put(std::vector<char>& blob, const std::vector<T>& v) {
     return off;
 }
 
+// The plan's device tables as one arena: pieces are laid out (256-B aligned) and then copied
+// straight from the host vectors through the pinned staging buffers (rcp_stage.h) -- no host
+// blob to assemble (C4: 26 MB, ~15 ms of host copies and page faults into a fresh vector).
+struct Arena {
+    struct Piece {
+        const void* p;
+        size_t bytes, off;
+    };
+    std::vector<Piece> pieces;
+    size_t total = 0;
+    template <class T>
+    size_t add(const std::vector<T>& v) {
+        const size_t off = (total + 255) & ~size_t(255);
+        if (!v.empty()) pieces.push_back({v.data(), sizeof(T) * v.size(), off});
+        total = off + sizeof(T) * std::max<size_t>(v.size(), 1);
+        return off;
+    }
+    hipError_t upload(void* dev, int device, hipStream_t s) const {
+        for (const Piece& q : pieces) {
+            const hipError_t e = rcp::stage_h2d(static_cast<char*>(dev) + q.off, q.p, q.bytes, device, s);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+};
+
 }  // namespace
 
 extern "C" int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
@@ -571,12 +619,16 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     DeviceGuard g(rs->device);
     HIP_TRY(g.err);
 
+#if RCP_PLAN_TIMING
+    PlanTimer ptimer;
+#endif
     auto plan = std::make_unique<rcp_plan>();
     plan->rs = rs;
     Builder B;
     int rc = build_rows(rs, rows, &B);
     if (rc) return rc;
     const int R = rows->n_rows;
+    PLAN_MARK("build_rows");
     plan->n_rows = R;
     plan->n_seg = (int64_t)B.segs.size();
     plan->row_len.assign(B.row_len.begin(), B.row_len.end());
@@ -836,6 +888,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         for (int p = 0; p < P.n_parts; ++p) P.stage_cap = std::max(P.stage_cap, P.part[p].chunk_bins);
     }
 
+    PLAN_MARK("parts+geometry");
     // ---- skewed rows: heavy slots sized for the eligible (short enough) rows
     const int32_t heavy_thr = opts->heavy_threshold < 0 ? kHeavyThreshold : opts->heavy_threshold;
     int32_t eligible_len = 0;
@@ -849,19 +902,19 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     if (heavy_thr <= 0 || R == 0) P.heavy_threshold = 0;
 
     // ---- upload tables (one arena)
-    std::vector<char> blob;
-    const size_t o_row_chrom = put(blob, B.row_chrom);
-    const size_t o_row_seg = put(blob, B.row_seg);
-    const size_t o_row_len = put(blob, B.row_len);
-    const size_t o_row_static = put(blob, B.row_static);
-    const size_t o_segs = put(blob, B.segs);
-    const size_t o_lay_index = put(blob, B.lay_index);
-    const size_t o_lay_cnt = put(blob, B.lay_cnt);
-    const size_t o_irow = put(blob, B.interp_row);
-    const size_t o_ipart = put(blob, B.interp_part);
-    const size_t o_imode = put(blob, B.interp_mode);
-    const size_t o_ipos = put(blob, B.interp_pos);
-    const size_t o_nb = put(blob, B.nb_pos);
+    Arena blob;
+    const size_t o_row_chrom = blob.add(B.row_chrom);
+    const size_t o_row_seg = blob.add(B.row_seg);
+    const size_t o_row_len = blob.add(B.row_len);
+    const size_t o_row_static = blob.add(B.row_static);
+    const size_t o_segs = blob.add(B.segs);
+    const size_t o_lay_index = blob.add(B.lay_index);
+    const size_t o_lay_cnt = blob.add(B.lay_cnt);
+    const size_t o_irow = blob.add(B.interp_row);
+    const size_t o_ipart = blob.add(B.interp_part);
+    const size_t o_imode = blob.add(B.interp_mode);
+    const size_t o_ipos = blob.add(B.interp_pos);
+    const size_t o_nb = blob.add(B.nb_pos);
     // locate's per-row input (RcpRowInfo)
     std::vector<RcpRowInfo> row_info((size_t)std::max(R, 1));
     {
@@ -883,7 +936,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
             if (ri.j1 > ri.j0) ri.seg0 = B.segs[ri.j0];
         }
     }
-    const size_t o_rinfo = put(blob, row_info);
+    const size_t o_rinfo = blob.add(row_info);
     // fmm pivots (see RcpPlanDev::spl_tb): the elimination of R's fmm_spline with d[i] = 1
     std::vector<double> spl_tb(2 * ((size_t)std::max(max_interp_len, 1) + 1), 0.0);
     {
@@ -896,9 +949,11 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
             spl_tb[2 * i + 1] = bp;
         }
     }
-    const size_t o_spl = put(blob, spl_tb);
-    HIP_TRY(plan->tables.alloc(blob.size()));
-    HIP_TRY(hipMemcpy(plan->tables.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    const size_t o_spl = blob.add(spl_tb);
+    PLAN_MARK("tables (host)");
+    HIP_TRY(plan->tables.alloc(blob.total));
+    HIP_TRY(blob.upload(plan->tables.p, rs->device, nullptr));
+    PLAN_MARK("tables upload");
     char* base = plan->tables.as<char>();
     // ---- work arena: locate outputs, heavy-row state, status words
     const int64_t S = std::max<int64_t>(plan->n_seg, 1);
@@ -917,6 +972,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     const size_t w_crange = al(w_rec + sizeof(RcpRowRec) * Rw);
     const size_t w_status = al(w_crange + (keep_crange ? sizeof(uint2) * 3 * (size_t)P.n_chunks_total * Rw : 0));
     HIP_TRY(plan->work.alloc(w_status + 256));
+    PLAN_MARK("work alloc");
     char* wb = plan->work.as<char>();
     P.ncand = reinterpret_cast<uint32_t*>(wb + w_ncand);
     P.heavy_slot = reinterpret_cast<int32_t*>(wb + w_hslot);
@@ -1015,7 +1071,12 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     }
     plan->grid = (int64_t)((R + plan->tile_rows - 1) / plan->tile_rows) * P.n_chunks_total;
     if (plan->lds > 160 * 1024) return fail(RCP_EUNSUPPORTED, "plan needs %zu B of LDS", plan->lds);
+    PLAN_MARK("rest");
     HIP_TRY(hipMemset(plan->work.p, 0, plan->work.bytes));
+#if RCP_PLAN_TIMING
+    HIP_TRY(hipDeviceSynchronize());
+    PLAN_MARK("memset");
+#endif
     *out = plan.release();
     return RCP_OK;
     RCP_CATCH

@@ -181,8 +181,8 @@ RCP_API int rcp_plan_destroy(rcp_plan* plan);
 RCP_API int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info);
 
 /* Device work only (stream-ordered, no host sync, capturable in a hipGraph):
- *   reset kernel (clears the skewed-row state the previous execution of this plan left),
- *   locate kernel (per segment/stream read ranges + NULL semantics; writes d_valid),
+ *   locate kernel (per segment/stream read ranges + NULL semantics; writes d_valid; also
+ *     clears the skewed-row state the previous execution of this plan left),
  *   skewed-row slice kernel,
  *   pileup-bin kernel (LDS difference array -> scans -> bins -> column-major out),
  *   interpolation kernel for rows with fewer positions than bins.

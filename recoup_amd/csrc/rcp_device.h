@@ -160,11 +160,16 @@ struct RcpPlanDev {
     int32_t* heavy_rows;        // [heavy_cap]
     uint32_t* heavy_nslice;     // [heavy_cap] slices of each slot (locate output)
     int32_t* heavy_gdiff;       // [heavy_cap * heavy_stride]; the slots the last execution used
-                                //    are cleared by the next one's reset kernel
-    // status (status[0]), heavy slot counter (status[1]), reset ticket (status[3]), lean work
-    // counters (status[8 .. 16])
+                                //    are cleared by the next one's locate kernel
+    // Status words of this execution: status (status[0]), heavy slot counter (status[1]), locate
+    // ticket (status[3]), lean work counters (status[8 .. 16]).  Executions alternate between
+    // two sets of RCP_STATUS_WORDS words (the plan's epoch parity): an execution's locate kernel
+    // reads the previous execution's slot count from status_prev[1], clears those slots, and its
+    // last block zeroes status_prev -- the set the next execution uses.  No reset launch.
     uint32_t* status;           // bit 0: numerator overflow, bit 1: per-base width mismatch
+    uint32_t* status_prev;
 };
+#define RCP_STATUS_WORDS 32
 
 __host__ __device__ inline void rcp_part_slice(const RcpPart& p, int32_t nr, int32_t* lo, int32_t* len) {
     *lo = (p.lo_end ? nr : 0) + p.lo_off;

@@ -46,7 +46,6 @@ hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, u
                            hipStream_t stream);
 hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream);
 hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_t stream);
-hipError_t rcp_launch_exec_reset(const RcpPlanDev* P, hipStream_t stream);
 hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_t* binsum, int csr, hipStream_t stream);
 hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStream_t stream);
 size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr);
@@ -234,8 +233,10 @@ struct PlanTimer {
     }
 };
 #define PLAN_MARK(what) ptimer.mark(what)
+#define LAYOUT_MARK(what) (void)hipStreamSynchronize(s), ltimer.mark(what)
 #else
 #define PLAN_MARK(what) ((void)0)
+#define LAYOUT_MARK(what) ((void)0)
 #endif
 
 int rcp_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
@@ -259,6 +260,9 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
                  const int8_t* pst, int merge, ReadLayout* L, hipStream_t s) {
     const int64_t n = d->n;
     const int64_t n_streams = (int64_t)d->n_chrom * 3;  // + 1 sentinel stream (dropped reads)
+#if RCP_PLAN_TIMING
+    PlanTimer ltimer;
+#endif
     DevBuf keys, keys2, vals, vals2, scan_in, scan_out, temp;
     HIP_TRY(keys.alloc(8 * std::max<int64_t>(n, 1)));
     HIP_TRY(keys2.alloc(8 * std::max<int64_t>(n, 1)));
@@ -266,6 +270,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     HIP_TRY(vals2.alloc(4 * std::max<int64_t>(n, 1)));
     HIP_TRY(rcp_launch_readset(n, pc, ps, pe, pst, d->n_chrom, d->strand_filter, merge, keys.as<uint64_t>(),
                                vals.as<int32_t>(), s));
+    LAYOUT_MARK("  keys");
     int end_bit = 32;
     while ((int64_t(1) << (end_bit - 32)) <= n_streams) ++end_bit;
     size_t tb = 0;
@@ -276,6 +281,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
         HIP_TRY(rcp_sort_pairs(temp.p, &tb, keys.as<uint64_t>(), keys2.as<uint64_t>(), vals.as<int32_t>(),
                                vals2.as<int32_t>(), n, end_bit, s));
     }
+    LAYOUT_MARK("  sort");
     keys.reset();
     vals.reset();
     HIP_TRY(L->stream_off.alloc(8 * (n_streams + 2)));
@@ -283,6 +289,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     HIP_TRY(scan_in.alloc(8 * std::max<int64_t>(n, 1)));
     HIP_TRY(rcp_launch_streams(n, keys2.as<uint64_t>(), vals2.as<int32_t>(), L->stream_off.as<int64_t>(),
                                n_streams + 2, L->se.as<int2>(), scan_in.as<uint64_t>(), s));
+    LAYOUT_MARK("  streams+pack");
     keys2.reset();
     vals2.reset();
     HIP_TRY(scan_out.alloc(8 * std::max<int64_t>(n, 1)));
@@ -294,9 +301,11 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     }
     HIP_TRY(L->pmax.alloc(4 * std::max<int64_t>(n, 1)));
     HIP_TRY(rcp_launch_unpack_pmax(n, scan_out.as<uint64_t>(), L->pmax.as<int32_t>(), s));
+    LAYOUT_MARK("  pmax scan");
     scan_in.reset();
     scan_out.reset();
     temp.reset();
+    LAYOUT_MARK("  frees");
     L->h_stream_off.resize(n_streams + 2);
     HIP_TRY(hipMemcpyAsync(L->h_stream_off.data(), L->stream_off.p, 8 * (n_streams + 2), hipMemcpyDeviceToHost, s));
     // ---- bucket directory: ~32 reads of a stream per bucket on average
@@ -339,6 +348,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
                            L->pmax.as<int32_t>(), L->se.as<int2>(), shift, L->dir_l.as<int32_t>(),
                            L->dir_l.as<int32_t>() + 1, s));
     HIP_TRY(hipStreamSynchronize(s));
+    LAYOUT_MARK("  directory");
     rs->n = kept;
     return RCP_OK;
 }
@@ -439,9 +449,19 @@ struct rcp_plan {
     DevBuf scratch;    // interpolation scratch
     int32_t max_row_len = 0;
     int64_t out_ld = 0;
+    uint32_t* status_sets = nullptr;  // 2 x RCP_STATUS_WORDS words in `work`
+    int epoch = 1;                    // parity of the last execution (the first one uses set 0)
 };
 
 namespace {
+
+// A new execution: alternate the status sets (RcpPlanDev::status / status_prev); the locate
+// kernel clears the previous execution's heavy slots and zeroes its set.
+void begin_exec(rcp_plan* plan) {
+    plan->epoch ^= 1;
+    plan->dev.status = plan->status_sets + RCP_STATUS_WORDS * plan->epoch;
+    plan->dev.status_prev = plan->status_sets + RCP_STATUS_WORDS * (plan->epoch ^ 1);
+}
 
 struct Builder {
     // host copies of the device tables
@@ -971,6 +991,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     const bool keep_crange = P.n_chunks_total > 1 && P.n_chunks_total <= RCP_MAX_CRANGE_CHUNKS;
     const size_t w_crange = al(w_rec + sizeof(RcpRowRec) * Rw);
     const size_t w_status = al(w_crange + (keep_crange ? sizeof(uint2) * 3 * (size_t)P.n_chunks_total * Rw : 0));
+    static_assert(2 * RCP_STATUS_WORDS * 4 <= 256, "two status sets");
     HIP_TRY(plan->work.alloc(w_status + 256));
     PLAN_MARK("work alloc");
     char* wb = plan->work.as<char>();
@@ -1038,7 +1059,9 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.seg_lo = reinterpret_cast<uint32_t*>(wb + w_lo);
     P.seg_hi = reinterpret_cast<uint32_t*>(wb + w_hi);
     P.valid = reinterpret_cast<uint8_t*>(wb + w_valid);
-    P.status = reinterpret_cast<uint32_t*>(wb + w_status);
+    plan->status_sets = reinterpret_cast<uint32_t*>(wb + w_status);
+    P.status = plan->status_sets;  // set by begin_exec per execution
+    P.status_prev = plan->status_sets + RCP_STATUS_WORDS;
     P.lay_index = reinterpret_cast<const int32_t*>(base + o_lay_index);
     P.lay_cnt = reinterpret_cast<const int32_t*>(base + o_lay_cnt);
     P.n_interp = n_interp;
@@ -1121,10 +1144,12 @@ extern "C" int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_str
     DeviceGuard g(plan->rs->device);
     HIP_TRY(g.err);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    begin_exec(plan);
     RcpPlanDev Q = plan->dev;
     Q.valid_out = d_valid;
-    HIP_TRY(rcp_launch_exec_reset(&Q, s));
     HIP_TRY(rcp_launch_locate(&Q, s));
+    Q.heavy_threshold = 0;  // no slices: the heavy launch only zeroes the previous status set
+    HIP_TRY(rcp_launch_heavy(&Q, kHeavyGrid, s));
     return RCP_OK;
     RCP_CATCH
 }
@@ -1139,11 +1164,11 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
     HIP_TRY(g.err);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     if (stages & RCP_STAGE_LOCATE) {
-        // reset (the previous execution's heavy slots, status words), locate (also writes the
-        // caller's validity vector), heavy slices
+        // locate (also clears the previous execution's heavy slots and status words, and writes
+        // the caller's validity vector), heavy slices
+        begin_exec(plan);
         RcpPlanDev Q = plan->dev;
         Q.valid_out = d_valid;
-        HIP_TRY(rcp_launch_exec_reset(&Q, s));
         HIP_TRY(rcp_launch_locate(&Q, s));
         HIP_TRY(rcp_launch_heavy(&Q, kHeavyGrid, s));
     }
@@ -1360,6 +1385,7 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
         if (out_off[r + 1] - out_off[r] != plan->row_len[r])
             return fail(RCP_EINVAL, "out_off does not match the row lengths at row %d", r);
     // one per-base part over the whole row, chunked by the plan's chunk capacity
+    begin_exec(plan);
     RcpPlanDev P = plan->dev;
     P.n_parts = 1;
     RcpPart& pt = P.part[0];
@@ -1378,7 +1404,6 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
     P.csr_off = d_off.as<int64_t>();
     P.csr_out = d_cov;
     P.valid_out = d_valid;
-    HIP_TRY(rcp_launch_exec_reset(&P, s));
     HIP_TRY(rcp_launch_locate(&P, s));
     HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));

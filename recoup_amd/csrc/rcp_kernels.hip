@@ -649,10 +649,12 @@ __device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32
 #ifndef RCP_LOC_WPE
 #define RCP_LOC_WPE 1
 #endif
-__global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlanDev P) {
+#ifndef RCP_CEDGE_DIR
+#define RCP_CEDGE_DIR 0
+#endif
+__device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres)[2 * RCP_MAX_CRANGE_CHUNKS]) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
     constexpr int KS = 4;                  // searches of one lockstep round
-    __shared__ uint32_t xres[kBlock / LPR][2 * RCP_MAX_CRANGE_CHUNKS];  // per row: chunk bounds
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = t / LPR;
     const int q = t % LPR;
@@ -768,6 +770,15 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
                     need = (task & 1) ? gpe < sg0.hi : gps > sg0.lo;  // a row end: the row's own bound
                     x = (task & 1) ? gpe : gps;
                 }
+#if RCP_CEDGE_DIR
+                // chunk edge bounded by its directory bucket alone (a superset of the exact range:
+                // the pileup's piece test drops the extra reads)
+                if (need) {
+                    const int32_t b = min(max(x, 0) >> P.dir_shift, ri.nb - 1);
+                    xr[task] = (task & 1) ? (uint32_t)P.dir_u[2 * (ri.d0 + b + 1)] : (uint32_t)P.dir_l[2 * (ri.d0 + b)];
+                    continue;
+                }
+#endif
             }
             if (!need) continue;
 #pragma unroll
@@ -878,8 +889,8 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
             bool empty;
             uint32_t clo = lo0, chi = hi0;
             if (piece(c, &gps, &gpe, &empty)) {
-                clo = gps > sg0.lo ? xr[2 * c] : lo0;
-                chi = max(clo, gpe < sg0.hi ? xr[2 * c + 1] : hi0);
+                clo = gps > sg0.lo ? max(lo0, xr[2 * c]) : lo0;
+                chi = max(clo, gpe < sg0.hi ? min(hi0, xr[2 * c + 1]) : hi0);
             } else if (empty) {
                 chi = clo;
             }
@@ -925,34 +936,27 @@ __global__ void __launch_bounds__(kBlock, RCP_LOC_WPE) rcp_locate_kernel(RcpPlan
     for (int u = 0; u < 4; ++u) dst[u] = src[u];
 }
 
-// =================================================================================
-// heavy rows: execution reset (clears the previous execution's slots), slice pileup
-// =================================================================================
-// First kernel of every execution (it replaces a status memset before locate and a clear
-// kernel after the pileup): zeroes the difference arrays of the slots the previous execution
-// claimed -- the pileup kernels read them across column chunks, so no reader can clear them
-// -- and, once every block has read the slot count, the status words (last block's ticket).
-__global__ void __launch_bounds__(kBlock) rcp_exec_reset_kernel(RcpPlanDev P) {
-    __shared__ uint32_t sn;
-    if (threadIdx.x == 0) sn = P.heavy_threshold > 0 ? min(P.status[1], (uint32_t)P.heavy_cap) : 0u;
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RCP_LOC_WPE))) rcp_locate_kernel(RcpPlanDev P) {
+    constexpr int LPR = 4;                 // lanes per row (a quad)
+    __shared__ uint32_t xres[kBlock / LPR][2 * RCP_MAX_CRANGE_CHUNKS];  // per row: chunk bounds
+    __shared__ uint32_t n_prev;
+    // ---- the previous execution's heavy slots (its pileup kernels read them across column
+    // chunks, so they are cleared here, before this execution's heavy kernel adds into them)
+    if (threadIdx.x == 0) n_prev = P.heavy_threshold > 0 ? min(P.status_prev[1], (uint32_t)P.heavy_cap) : 0u;
     __syncthreads();
-    const uint32_t n = sn;
-    for (uint32_t s = blockIdx.x; s < n; s += gridDim.x) {
-        // 16-byte stores: a slot is heavy_stride (a multiple of 64) ints, 16-byte aligned
-        int4* g4 = reinterpret_cast<int4*>(P.heavy_gdiff + (size_t)s * P.heavy_stride);
-        const int32_t n4 = (P.row_len[P.heavy_rows[s]] + 1 + 3) >> 2;
-        for (int q = threadIdx.x; q < n4; q += blockDim.x) g4[q] = make_int4(0, 0, 0, 0);
+    for (uint32_t s = blockIdx.x; s < n_prev; s += gridDim.x) {
+        int4* g4 = reinterpret_cast<int4*>(P.heavy_gdiff + (size_t)s * P.heavy_stride);  // stride: multiple of 64
+        for (int i = threadIdx.x; i < (P.heavy_stride >> 2); i += blockDim.x) g4[i] = make_int4(0, 0, 0, 0);
     }
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(&P.status[3], 1u) == gridDim.x - 1) {
-            atomicExch(&P.status[0], 0u);
-            atomicExch(&P.status[1], 0u);
-            atomicExch(&P.status[3], 0u);
-        }
-    }
+    locate_rows(P, xres);
+    // (status_prev is zeroed by the next launch, rcp_heavy_pileup_kernel, once every block here
+    // has read it: a last-block ticket over this grid's thousands of blocks cost ~150 us)
 }
 
+
+// =================================================================================
+// heavy rows: slice pileup
+// =================================================================================
 #ifndef RCP_HEAVY_LOADS
 #define RCP_HEAVY_LOADS 16
 #endif
@@ -965,7 +969,10 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) 
     uint32_t* scratch = reinterpret_cast<uint32_t*>(smem);
     int32_t* diff = reinterpret_cast<int32_t*>(smem) + 16;
     uint32_t* offs = reinterpret_cast<uint32_t*>(diff) + (P.heavy_max_len + 1 + 64);  // [heavy_cap + 1]
-    const uint32_t n = min(P.status[1], (uint32_t)P.heavy_cap);
+    // every locate block has read the previous execution's status set: zero it for the next
+    // execution (launched with one block when the plan has no heavy path)
+    if (blockIdx.x == 0 && threadIdx.x < RCP_STATUS_WORDS) P.status_prev[threadIdx.x] = 0u;
+    const uint32_t n = P.heavy_threshold > 0 ? min(P.status[1], (uint32_t)P.heavy_cap) : 0u;
     if (n == 0) return;
     // slice offsets of the slots: every block scans the per-slot slice counts locate stored
     // when it claimed them (no separate one-block planning kernel between the two)
@@ -2489,8 +2496,12 @@ extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream)
     return hipGetLastError();
 }
 
+// Always launched after locate (one block without a heavy path): it also zeroes status_prev.
 extern "C" hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_t stream) {
-    if (P->n_rows == 0 || P->heavy_threshold <= 0) return hipSuccess;
+    if (P->n_rows == 0 || P->heavy_threshold <= 0) {
+        hipLaunchKernelGGL(rcp_heavy_pileup_kernel, dim3(1), dim3(kBlock), 64, stream, *P);
+        return hipGetLastError();
+    }
     {
         const hipError_t e = allow_big_lds(rcp_heavy_pileup_kernel);
         if (e != hipSuccess) return e;
@@ -2498,16 +2509,6 @@ extern "C" hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_
     // difference array of one row + the slots' slice offsets
     const size_t lds = 4 * (16 + (size_t)P->heavy_max_len + 1 + 64) + 4 * ((size_t)P->heavy_cap + 1);
     hipLaunchKernelGGL(rcp_heavy_pileup_kernel, dim3(grid), dim3(kBlock), lds, stream, *P);
-    return hipGetLastError();
-}
-
-// before every locate: see rcp_exec_reset_kernel
-extern "C" hipError_t rcp_launch_exec_reset(const RcpPlanDev* P, hipStream_t stream) {
-#ifndef RCP_RESET_GRID
-#define RCP_RESET_GRID 64  // fewer last-block tickets: C2 0.093 -> 0.089 ms, C4 -0.005 ms (vs 256)
-#endif
-    const unsigned grid = (P->n_rows > 0 && P->heavy_threshold > 0) ? (unsigned)RCP_RESET_GRID : 1u;
-    hipLaunchKernelGGL(rcp_exec_reset_kernel, dim3(grid), dim3(kBlock), 0, stream, *P);
     return hipGetLastError();
 }
 

@@ -275,9 +275,10 @@ def test_heavy_duplicate_stacks_match(gpu):
 
 
 def test_heavy_repeated_executions(gpu):
-    """Each execution starts with the reset kernel, which clears the heavy slots the previous
-    call left (there is no clear after the pileup): one plan run repeatedly, with validity-only
-    and coverage calls in between, gives the oracle's matrix every time."""
+    """Each execution's locate kernel clears the heavy slots the previous call left and zeroes
+    the previous call's status words (executions alternate between two sets; there is no reset
+    launch and no clear after the pileup): one plan run repeatedly, with validity-only and
+    coverage calls in between, gives the oracle's matrix every time."""
     from recoup_amd.engine import Bins, Plan, ReadSet
     rng = np.random.default_rng(31)
     reads = make_reads(rng, 200_000, widths=(100, 200))

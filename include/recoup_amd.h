@@ -71,8 +71,8 @@ RCP_API int rcp_device_count(int* n);
 typedef struct rcp_readset rcp_readset;
 
 typedef struct {
-    int64_t n;              /* number of reads (< 2^32) */
-    const int32_t* chrom;   /* [n] chromosome code 0..n_chrom-1 (seqnames)            */
+    int64_t n;              /* number of reads (< 2^31) */
+    const int32_t* chrom;   /* [n] chromosome code 0..n_chrom-1 (seqnames); NULL: runs below */
     const int32_t* start;   /* [n] 1-based start                                       */
     const int32_t* end;     /* [n] 1-based end (inclusive)                             */
     const int8_t* strand;   /* [n] strand code                                         */
@@ -81,6 +81,12 @@ typedef struct {
     int32_t device;         /* HIP device ordinal                                      */
     int32_t on_device;      /* 1: chrom/start/end/strand are device pointers           */
     int32_t strand_filter;  /* -1 none, else keep only reads of that strand (calcCoverage strand=) */
+    /* seqnames as runs, GRanges' own Rle (runValue / runLength of seqnames(x)), used when
+     * chrom is NULL: a coordinate-sorted BAM's reads are a few dozen runs, so the 4 bytes per
+     * read of an expanded chromosome vector never cross PCIe.  Host pointers in both modes. */
+    int32_t n_chrom_runs;
+    const int32_t* chrom_run_value;   /* [n_chrom_runs] chromosome code of each run          */
+    const int64_t* chrom_run_length;  /* [n_chrom_runs] > 0, summing to n                    */
 } rcp_reads_desc;
 
 /* Upload (or adopt device arrays), sort by (chrom, strand, start) on the GPU, and build

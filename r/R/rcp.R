@@ -29,7 +29,8 @@
 # the reads go to the GPU once, sorted there by (chromosome, strand, start)
 .rcpReads <- function(input, strand = NULL, devices = .rcpDevices()) {
     lv <- seqlevels(input)
-    args <- list(as.integer(seqnames(input)) - 1L, start(input), end(input),
+    sn <- seqnames(input)  # an Rle: its runs go to the GPU, not one code per read
+    args <- list(list(as.integer(runValue(sn)) - 1L, as.numeric(runLength(sn))), start(input), end(input),
         .rcpStrandCode(strand(input)), as.numeric(seqlengths(input)[lv]),
         if (is.null(strand)) -1L else .rcpStrandCode(strand))
     if (length(devices) > 1)

@@ -55,7 +55,19 @@ static rcp_reads_desc reads_of(SEXP chrom, SEXP start, SEXP end, SEXP strand, SE
     rcp_reads_desc d;
     memset(&d, 0, sizeof d);
     d.n = (int64_t)n;
-    d.chrom = INTEGER(chrom);
+    if (TYPEOF(chrom) == VECSXP) {
+        /* list(runValue, runLength) of seqnames(reads): expanded on the GPU */
+        SEXP rv = VECTOR_ELT(chrom, 0), rl = VECTOR_ELT(chrom, 1);
+        int nr = LENGTH(rv);
+        int64_t* len = (int64_t*)R_alloc(nr > 0 ? nr : 1, sizeof(int64_t));
+        for (int k = 0; k < nr; ++k) len[k] = (int64_t)REAL(rl)[k];
+        d.chrom = NULL;
+        d.n_chrom_runs = nr;
+        d.chrom_run_value = INTEGER(rv);
+        d.chrom_run_length = len;
+    } else {
+        d.chrom = INTEGER(chrom);
+    }
     d.start = INTEGER(start);
     d.end = INTEGER(end);
     d.strand = st;
@@ -68,7 +80,8 @@ static rcp_reads_desc reads_of(SEXP chrom, SEXP start, SEXP end, SEXP strand, SE
 }
 
 /* .Call("rcp_R_readset", chromCode, start, end, strandCode, seqlengths, strandFilter, device)
- * chromCode: 0-based seqlevel index; strandCode 0 '+', 1 '-', 2 '*'; seqlengths numeric (NA ok) */
+ * chromCode: 0-based seqlevel index per read, or list(runValue - 1L, as.numeric(runLength)) of
+ * the seqnames Rle; strandCode 0 '+', 1 '-', 2 '*'; seqlengths numeric (NA ok) */
 SEXP rcp_R_readset(SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP seqlen, SEXP sfilter, SEXP dev) {
     rcp_reads_desc d = reads_of(chrom, start, end, strand, seqlen, sfilter);
     d.device = asInteger(dev);

@@ -41,7 +41,10 @@ constexpr int kLeanMinChunkBins = 64;                   // no column chunks narr
 
 extern "C" {
 hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
-                          int32_t* vout, int64_t n, int end_bit, hipStream_t stream);
+                          int32_t* vout, int64_t n, int begin_bit, int end_bit, hipStream_t stream);
+hipError_t rcp_launch_unsorted(int64_t n, const uint64_t* keys, uint32_t* flag, hipStream_t stream);
+hipError_t rcp_launch_expand_runs(int64_t n, int32_t n_runs, const int64_t* run_start, const int32_t* run_value,
+                                  int32_t* out, hipStream_t stream);
 hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
                            hipStream_t stream);
 hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream);
@@ -219,6 +222,7 @@ struct rcp_readset {
     std::vector<int64_t> seqlen;
     DevBuf d_seqlen;
     ReadLayout stranded, merged;
+    bool presorted = false;  // the reads came in (chromosome, start) order (no full radix sort)
 };
 
 // tools-only phase timing of rcp_plan_create_ex (build with -DRCP_PLAN_TIMING=1)
@@ -256,8 +260,12 @@ extern "C" int rcp_device_count(int* n) {
 namespace {
 
 // Sort the reads into layout L (merge = strands share stream c*3) and build its search index.
+// `presorted` (in/out): the merged layout, built first, reports whether the reads already came in
+// (chromosome, start) order -- a coordinate-sorted BAM's readGAlignments does -- and then skips its
+// radix sort; the stranded layout of such reads is a stable sort on the stream id alone (one
+// 8-bit pass instead of five: the start order inside each stream is already there).
 int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, const int32_t* ps, const int32_t* pe,
-                 const int8_t* pst, int merge, ReadLayout* L, hipStream_t s) {
+                 const int8_t* pst, int merge, ReadLayout* L, hipStream_t s, bool* presorted) {
     const int64_t n = d->n;
     const int64_t n_streams = (int64_t)d->n_chrom * 3;  // + 1 sentinel stream (dropped reads)
 #if RCP_PLAN_TIMING
@@ -273,15 +281,36 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     LAYOUT_MARK("  keys");
     int end_bit = 32;
     while ((int64_t(1) << (end_bit - 32)) <= n_streams) ++end_bit;
+    bool sorted_in = false;
+    if (merge && n > 1) {
+        // keys are (stream, start): non-decreasing <=> (chromosome, start) order, no dropped read
+        // (the sentinel stream) before a kept one
+        DevBuf flag;
+        HIP_TRY(flag.alloc(4));
+        HIP_TRY(hipMemsetAsync(flag.p, 0, 4, s));
+        HIP_TRY(rcp_launch_unsorted(n, keys.as<uint64_t>(), flag.as<uint32_t>(), s));
+        uint32_t h = 1;
+        HIP_TRY(hipMemcpyAsync(&h, flag.p, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        sorted_in = h == 0;
+        *presorted = sorted_in;
+    }
+    const int begin_bit = (!merge && *presorted) ? 32 : 0;
     size_t tb = 0;
-    if (n > 0) {
+    if (n > 0 && !sorted_in) {
         HIP_TRY(rcp_sort_pairs(nullptr, &tb, keys.as<uint64_t>(), keys2.as<uint64_t>(), vals.as<int32_t>(),
-                               vals2.as<int32_t>(), n, end_bit, s));
+                               vals2.as<int32_t>(), n, begin_bit, end_bit, s));
         HIP_TRY(temp.alloc(tb));
         HIP_TRY(rcp_sort_pairs(temp.p, &tb, keys.as<uint64_t>(), keys2.as<uint64_t>(), vals.as<int32_t>(),
-                               vals2.as<int32_t>(), n, end_bit, s));
+                               vals2.as<int32_t>(), n, begin_bit, end_bit, s));
     }
     LAYOUT_MARK("  sort");
+    if (sorted_in) {
+        std::swap(keys.p, keys2.p);
+        std::swap(keys.bytes, keys2.bytes);
+        std::swap(vals.p, vals2.p);
+        std::swap(vals.bytes, vals2.bytes);
+    }
     keys.reset();
     vals.reset();
     HIP_TRY(L->stream_off.alloc(8 * (n_streams + 2)));
@@ -363,7 +392,19 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     if (rc) return rc;
     if (d->n < 0 || d->n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "read count %lld outside [0, 2^31)", (long long)d->n);
     if (d->n_chrom <= 0 || d->n_chrom > (1 << 20)) return fail(RCP_EINVAL, "n_chrom = %d", d->n_chrom);
-    if (d->n > 0 && (!d->chrom || !d->start || !d->end || !d->strand)) return fail(RCP_EINVAL, "NULL read array");
+    if (d->n > 0 && (!d->start || !d->end || !d->strand)) return fail(RCP_EINVAL, "NULL read array");
+    if (d->n > 0 && !d->chrom) {
+        if (d->n_chrom_runs <= 0 || !d->chrom_run_value || !d->chrom_run_length)
+            return fail(RCP_EINVAL, "chrom is NULL and no chromosome runs are given");
+        int64_t tot = 0;
+        for (int32_t k = 0; k < d->n_chrom_runs; ++k) {
+            if (d->chrom_run_length[k] <= 0) return fail(RCP_EINVAL, "chromosome run %d has length %lld", k,
+                                                         (long long)d->chrom_run_length[k]);
+            tot += d->chrom_run_length[k];
+        }
+        if (tot != d->n) return fail(RCP_EINVAL, "chromosome runs cover %lld reads, not %lld", (long long)tot,
+                                     (long long)d->n);
+    }
     if (d->strand_filter < -1 || d->strand_filter > 2) return fail(RCP_EINVAL, "strand_filter = %d", d->strand_filter);
     DeviceGuard g(d->device);
     HIP_TRY(g.err);
@@ -380,16 +421,29 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
 #endif
 
     // inputs on device
-    DevBuf in_chrom, in_start, in_end, in_strand;
+    DevBuf in_chrom, in_start, in_end, in_strand, runs;
     const int32_t *pc = d->chrom, *ps = d->start, *pe = d->end;
     const int8_t* pst = d->strand;
-    if (!d->on_device && n > 0) {
+    if (!d->chrom && n > 0) {
+        // seqnames as runs: expanded on the device (never crosses PCIe)
+        std::vector<int64_t> rstart(d->n_chrom_runs + 1, 0);
+        for (int32_t k = 0; k < d->n_chrom_runs; ++k) rstart[k + 1] = rstart[k] + d->chrom_run_length[k];
+        HIP_TRY(runs.alloc(8 * rstart.size() + 4 * (size_t)d->n_chrom_runs));
+        HIP_TRY(hipMemcpyAsync(runs.p, rstart.data(), 8 * rstart.size(), hipMemcpyHostToDevice, s));
+        int32_t* rv = reinterpret_cast<int32_t*>(runs.as<char>() + 8 * rstart.size());
+        HIP_TRY(hipMemcpyAsync(rv, d->chrom_run_value, 4 * (size_t)d->n_chrom_runs, hipMemcpyHostToDevice, s));
         HIP_TRY(in_chrom.alloc(4 * n));
+        HIP_TRY(rcp_launch_expand_runs(n, d->n_chrom_runs, runs.as<int64_t>(), rv, in_chrom.as<int32_t>(), s));
+        HIP_TRY(hipStreamSynchronize(s));  // rstart is released on return
+        pc = in_chrom.as<int32_t>();
+    }
+    if (!d->on_device && n > 0) {
+        if (d->chrom) HIP_TRY(in_chrom.alloc(4 * n));
         HIP_TRY(in_start.alloc(4 * n));
         HIP_TRY(in_end.alloc(4 * n));
         HIP_TRY(in_strand.alloc(n));
         // caller-owned pageable arrays (R vectors): pinned double-buffered staging (rcp_stage.h)
-        HIP_TRY(rcp::stage_h2d(in_chrom.p, d->chrom, 4 * n, d->device, s));
+        if (d->chrom) HIP_TRY(rcp::stage_h2d(in_chrom.p, d->chrom, 4 * n, d->device, s));
         HIP_TRY(rcp::stage_h2d(in_start.p, d->start, 4 * n, d->device, s));
         HIP_TRY(rcp::stage_h2d(in_end.p, d->end, 4 * n, d->device, s));
         HIP_TRY(rcp::stage_h2d(in_strand.p, d->strand, n, d->device, s));
@@ -399,12 +453,14 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
         pst = in_strand.as<int8_t>();
     }
     PLAN_MARK("reads H2D");
-    rc = build_layout(rs.get(), d, pc, ps, pe, pst, 0, &rs->stranded, s);
-    if (rc) return rc;
-    PLAN_MARK("stranded layout");
-    rc = build_layout(rs.get(), d, pc, ps, pe, pst, 1, &rs->merged, s);
+    bool presorted = false;
+    rc = build_layout(rs.get(), d, pc, ps, pe, pst, 1, &rs->merged, s, &presorted);
     if (rc) return rc;
     PLAN_MARK("merged layout");
+    rc = build_layout(rs.get(), d, pc, ps, pe, pst, 0, &rs->stranded, s, &presorted);
+    if (rc) return rc;
+    PLAN_MARK("stranded layout");
+    rs->presorted = presorted;
     HIP_TRY(rs->d_seqlen.alloc(8 * d->n_chrom));
     HIP_TRY(hipMemcpyAsync(rs->d_seqlen.p, rs->seqlen.data(), 8 * d->n_chrom, hipMemcpyHostToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));

@@ -496,8 +496,29 @@ struct SegMaxOp {
 };
 
 extern "C" hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, uint64_t* kout,
-                                     const int32_t* vin, int32_t* vout, int64_t n, int end_bit, hipStream_t stream) {
-    return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, kin, kout, vin, vout, (int)n, 0, end_bit, stream);
+                                     const int32_t* vin, int32_t* vout, int64_t n, int begin_bit, int end_bit,
+                                     hipStream_t stream) {
+    return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, kin, kout, vin, vout, (int)n, begin_bit, end_bit,
+                                              stream);
+}
+
+// flag = 1 when some key is smaller than its predecessor
+__global__ void rcp_unsorted_kernel(int64_t n, const uint64_t* __restrict__ keys, uint32_t* __restrict__ flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+    if (i < n && keys[i] < keys[i - 1]) *flag = 1u;
+}
+
+// chromosome code of read i from the seqnames runs (run_start: prefix sums, n_runs + 1 entries)
+__global__ void rcp_expand_runs_kernel(int64_t n, int32_t n_runs, const int64_t* __restrict__ run_start,
+                                       const int32_t* __restrict__ run_value, int32_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t a = 0, b = n_runs;  // last run with run_start <= i
+    while (b - a > 1) {
+        const int32_t m = (a + b) >> 1;
+        if (run_start[m] <= i) a = m; else b = m;
+    }
+    out[i] = run_value[a];
 }
 
 extern "C" hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
@@ -2633,6 +2654,21 @@ extern "C" hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const 
     const int64_t grid = (n + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(rcp_make_keys_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, chrom, start, end,
                        strand, n_chrom, strand_filter, merge, keys, vals);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rcp_launch_unsorted(int64_t n, const uint64_t* keys, uint32_t* flag, hipStream_t stream) {
+    if (n < 2) return hipSuccess;
+    hipLaunchKernelGGL(rcp_unsorted_kernel, dim3((unsigned)((n - 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, n,
+                       keys, flag);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rcp_launch_expand_runs(int64_t n, int32_t n_runs, const int64_t* run_start,
+                                             const int32_t* run_value, int32_t* out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rcp_expand_runs_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, n,
+                       n_runs, run_start, run_value, out);
     return hipGetLastError();
 }
 

@@ -1,0 +1,7 @@
+#!/bin/bash
+OUT=gpurun_out/r02j
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
+tail -2 $OUT/gpu_tests.log
+bash tools/gpu_ab.sh $OUT "c4 c5" nocedge base nocedge base || exit 1

@@ -2109,7 +2109,10 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     };
     if (wave == kPWaves) claim(0);
-    if (tid == 0) item[2] = 0;  // the pile waves' row counter (RCP_LEAN_DYN)
+    if (tid == 0) {
+        item[1] = -1;  // (always written by a claim before it is read; defined anyway)
+        item[2] = 0;   // the pile waves' row counter (RCP_LEAN_DYN)
+    }
     lds_barrier();
 
     if (wave < kPWaves) {

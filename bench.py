@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--verify-gather", action="store_true",
                     help="N > 1: rank 0 also runs the whole workload alone and checks the gathered matrix bit for bit")
     ap.add_argument("--no-e2e", action="store_true", help="skip the one-off host-to-host timing")
+    ap.add_argument("--inflight", default="auto", choices=["auto", "1", "2"],
+                    help="passes in flight on separate HIP streams (D plans over the same readset and region "
+                         "table, like D sample slots); auto: the faster of 1 and 2, timed after the warmup")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default profiles/traffic_<config>.json")
     return ap.parse_args()
@@ -238,18 +241,46 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] readset + plan in {time.time() - t1:.1f}s (plan {plan_s * 1e3:.1f} ms), info {plan.info}")
 
+    # ---- passes in flight: D plans of the same workload (same readset, rows, bins) on D HIP
+    # streams; step k is one complete pass by plan k % D.  Passes are independent, so with D = 2
+    # one pass's locate / heavy launches and its pileup's tail overlap the other's pileup (small
+    # shards and C5 leave the persistent pileup grid partly idle at its start and end).
+    plans, outs, valids = [plan], [out], [valid]
+    streams = [torch.cuda.current_stream()]
+    if args.inflight != "1":
+        p2 = Plan(rs, rows, bins, out_ld="padded")
+        plans.append(p2)
+        outs.append(p2.empty_output())
+        valids.append(torch.empty(max(R, 1), dtype=torch.uint8, device=dev))
+        streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+
+    def passes(D, n):
+        for k in range(n):
+            i = k % D
+            plans[i].execute(outs[i], valids[i], stream=streams[i] if D > 1 else streams[0])
+
     # ---- warmup + correctness gate
-    for _ in range(args.warmup):
-        plan.execute(out, valid)
-    plan.status()
+    passes(len(plans), max(args.warmup, len(plans)))
+    for p in plans:
+        p.status()
+    tune = None
+    D = len(plans)
+    if args.inflight == "auto":
+        tune = {}
+        for d in (1, 2):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            passes(d, max(args.steps, 10))
+            torch.cuda.synchronize()
+            tune[d] = (time.perf_counter() - t) / max(args.steps, 10) * 1e3
+        D = min(tune, key=tune.get)
 
     # ---- timed region: exactly K steps between barrier + synchronize
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
     ts = time.perf_counter()
-    for _ in range(args.steps):
-        plan.execute(out, valid)
+    passes(D, args.steps)
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
@@ -258,7 +289,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
-    plan.status()
+    for p in plans:
+        p.status()
+    # (bitwise: a row the reference maps to NaN -- e.g. a spline through one knot -- is NaN in both)
+    if D == 2 and not torch.equal(outs[0][:, :R].view(torch.int64), outs[1][:, :R].view(torch.int64)):
+        raise SystemExit("passes in flight disagree")
 
     # ---- per-kernel durations with HIP events on the launch stream
     stream = torch.cuda.current_stream()
@@ -345,6 +380,10 @@ def main():
                 "parallelism": f"region-sharded x{world}: one contiguous region shard per GPU, balanced by "
                                f"overlapping reads; no data-path collective",
                 "rank0_shard": {"regions": R, "reads": n_reads, "sim_shard": args.sim_shard},
+                "inflight": D,
+                "inflight_note": "passes in flight on separate HIP streams (plans of the same workload); every "
+                                 "step is a complete pass; rank 0's ms per pass when tuned: "
+                                 + (json.dumps({str(k): round(v, 4) for k, v in tune.items()}) if tune else "not tuned"),
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,

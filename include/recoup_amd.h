@@ -234,6 +234,18 @@ RCP_API int rcp_readset_create_multi(const rcp_reads_desc* desc, const int32_t* 
 RCP_API int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices, const rcp_rows_desc* rows,
                               const rcp_bins_desc* bins, double* out, uint8_t* row_valid, int32_t* row_split);
 
+/* Several samples over one region table -- profileMatrix's loop over the samples of a recoup
+ * input list (R/profile.R:13-98, `for (n in names(input))`) -- in one call: one plan per sample
+ * (all readsets on one device), passes kept `inflight` deep on as many HIP streams (1..3; 0 =
+ * 2), so one sample's locate / heavy launches and the tail of its persistent pileup grid overlap
+ * another's pileup, and each finished sample's matrix is copied (staged) into outs[s] -- the
+ * caller's R column-major n_rows x n_cols matrix -- while later samples compute.  row_valid may
+ * be NULL, or hold n_samples pointers (each may be NULL).  Bit-identical to rcp_profile per
+ * sample. */
+RCP_API int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_samples, const rcp_rows_desc* rows,
+                                const rcp_bins_desc* bins, int32_t inflight, double* const* outs,
+                                uint8_t* const* row_valid);
+
 /* Profiles of a coverage list the caller holds as run-length encoded vectors -- the reference's
  * own `$coverage` object, a named list of S4Vectors::Rle (R/coverage.R:171-173) -- as
  * binCoverageMatrix / baseCoverageMatrix consume it (R/profile.R:100-212) when recoup() reuses a

@@ -136,6 +136,29 @@ baseCoverageMatrix <- function(cvrg, flank = NULL, where = c("upstream", "downst
 
 # profileMatrix (R/profile.R:1-98) with every column part of a sample in ONE library call:
 # the same parts, in the same order (left, center, right), as the reference's cbind
+# the column parts of profileMatrix: one whole part when all rows have one length, else
+# (upstream,) center (, downstream) with the flank bin counts of R/profile.R:24-60
+.rcpParts <- function(equal, len1, flank, binParams) {
+    if (equal)
+        return(list(where = 0L, nBins = binParams$regionBinSize,
+            perBase = if (binParams$regionBinSize == 0) len1 else 0L))
+    where <- 1L
+    nb <- binParams$regionBinSize
+    pb <- 0L
+    r <- flank / sum(flank)
+    for (k in 1:2) {
+        if (flank[k] == 0)
+            next
+        fb <- if (binParams$flankBinSize != 0) round(2 * binParams$flankBinSize * r[k]) else 0
+        if (k == 1) {
+            where <- c(2L, where); nb <- c(fb, nb); pb <- c(if (fb) 0L else flank[1], pb)
+        } else {
+            where <- c(where, 3L); nb <- c(nb, fb); pb <- c(pb, if (fb) 0L else flank[2])
+        }
+    }
+    list(where = where, nBins = nb, perBase = pb)
+}
+
 profileMatrixFused <- function(input, flank, binParams, rc = NULL) {
     len <- lengths(input[[1]]$coverage)
     len <- len[len != 0]
@@ -143,31 +166,47 @@ profileMatrixFused <- function(input, flank, binParams, rc = NULL) {
     for (n in names(input)) {
         if (!is.null(input[[n]]$profile))
             next
-        if (equal) {
-            parts <- list(where = 0L, nBins = binParams$regionBinSize,
-                perBase = if (binParams$regionBinSize == 0) len[1] else 0L)
-        } else {
-            where <- 1L
-            nb <- binParams$regionBinSize
-            pb <- 0L
-            r <- flank / sum(flank)
-            for (k in 1:2) {
-                if (flank[k] == 0)
-                    next
-                fb <- if (binParams$flankBinSize != 0) round(2 * binParams$flankBinSize * r[k]) else 0
-                if (k == 1) {
-                    where <- c(2L, where); nb <- c(fb, nb); pb <- c(if (fb) 0L else flank[1], pb)
-                } else {
-                    where <- c(where, 3L); nb <- c(nb, fb); pb <- c(pb, if (fb) 0L else flank[2])
-                }
-            }
-            parts <- list(where = where, nBins = nb, perBase = pb)
-        }
+        parts <- .rcpParts(equal, len[1], flank, binParams)
         # the equal-length branch calls binCoverageMatrix without interpolation= (its default)
         interp <- if (equal) "auto" else binParams$interpolation
         input[[n]]$profile <- .rcpProfileRle(input[[n]]$coverage, parts$where, flank,
             parts$nBins, parts$perBase, binParams$sumStat, interp)
         rownames(input[[n]]$profile) <- names(input[[n]]$coverage)
+    }
+    return(input)
+}
+
+# profileMatrix straight from the reads, for a caller that does not keep $coverage: the mask's
+# rows over every sample's reads.  One GPU: all samples in ONE library call, passes kept two
+# deep on separate HIP streams (one sample's locate and pileup tail overlap another's pileup);
+# several GPUs (options(recoup.devices)): each sample's rows split over them.
+profileMatrixFromReads <- function(input, mask, flank, binParams, ignore.strand = TRUE) {
+    len <- width(mask)
+    equal <- all(len == len[1])
+    parts <- .rcpParts(equal, len[1], flank, binParams)
+    interp <- if (equal) "auto" else binParams$interpolation
+    rows <- .rcpRows(mask, seqlevels(input[[1]]$ranges), ignore.strand)
+    binArgs <- list(as.integer(parts$where), as.integer(if (is.null(flank)) c(0, 0) else flank),
+        as.integer(parts$nBins), as.integer(parts$perBase), .rcpStat(binParams$sumStat),
+        .rcpInterp(interp), .rcpRngKind(), 1.0)
+    devs <- .rcpDevices()
+    todo <- which(vapply(input, function(x) is.null(x$profile), TRUE))
+    if (length(devs) > 1) {
+        for (i in todo) {
+            rs <- .rcpReads(input[[i]]$ranges, NULL, devs)
+            res <- do.call(.Call, c(list("rcp_R_profile_multi", rs), .rcpRowArgs(rows), binArgs,
+                list(PACKAGE = "recoup")))
+            input[[i]]$profile <- res$profile
+            rownames(input[[i]]$profile) <- names(mask)
+        }
+        return(input)
+    }
+    rsl <- lapply(input[todo], function(x) .rcpReads(x$ranges, NULL, devs[1]))
+    res <- do.call(.Call, c(list("rcp_R_profile_samples", rsl), .rcpRowArgs(rows), binArgs,
+        list(2L, PACKAGE = "recoup")))
+    for (k in seq_along(todo)) {
+        input[[todo[k]]]$profile <- res[[k]]$profile
+        rownames(input[[todo[k]]]$profile) <- names(mask)
     }
     return(input)
 }

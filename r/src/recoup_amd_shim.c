@@ -8,8 +8,8 @@
  *   calcCoverage / coverageFromRanges (R/coverage.R:126-226) rcp_R_coverage -> list of Rle pieces
  *   binCoverageMatrix / baseCoverageMatrix / splitVector     rcp_R_profile_rle (the stored $coverage,
  *       (R/profile.R:100-212, R/util.R:15-85)                    a list of Rle, as R keeps it)
- *   profileMatrix straight from the reads (fused, one call   rcp_R_profile / rcp_R_profile_multi
- *       per sample; R/profile.R:1-98)
+ *   profileMatrix straight from the reads (fused, one call   rcp_R_profile / rcp_R_profile_multi /
+ *       per sample, or all samples at once; R/profile.R:1-98)   rcp_R_profile_samples
  *   readBam (R/ranges.R:111-146)                             rcp_R_read_bam
  *   preprocessRanges downsample / sampleto (R/ranges.R:32-62) rcp_R_sample_sorted
  *
@@ -188,6 +188,38 @@ SEXP rcp_R_profile(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP
     }
     SEXP res = profile_result(out, valid, rd.n_rows);
     UNPROTECT(1);
+    return res;
+}
+
+/* .Call("rcp_R_profile_samples", list of readsets (one per sample, one GPU), <rows: 8 args>,
+ * <bins: 8 args>, inflight) -> list (per sample) of list(profile, valid): profileMatrix's loop
+ * over the samples of a recoup input list (R/profile.R:13-98) in one call, passes kept
+ * `inflight` deep on separate HIP streams */
+SEXP rcp_R_profile_samples(SEXP rsl, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
+                           SEXP isList, SEXP ignoreStrand, SEXP where, SEXP flank, SEXP nBins, SEXP pbw,
+                           SEXP stat, SEXP interp, SEXP rng, SEXP scale, SEXP inflight) {
+    rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
+    int ncol = 0;
+    rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
+    int ns = LENGTH(rsl);
+    rcp_readset** rs = (rcp_readset**)R_alloc(ns > 0 ? ns : 1, sizeof(rcp_readset*));
+    double** outs = (double**)R_alloc(ns > 0 ? ns : 1, sizeof(double*));
+    uint8_t** valid = (uint8_t**)R_alloc(ns > 0 ? ns : 1, sizeof(uint8_t*));
+    SEXP mats = PROTECT(allocVector(VECSXP, ns));
+    for (int i = 0; i < ns; ++i) {
+        rs[i] = (rcp_readset*)R_ExternalPtrAddr(VECTOR_ELT(rsl, i));
+        SET_VECTOR_ELT(mats, i, allocMatrix(REALSXP, rd.n_rows, ncol));
+        outs[i] = REAL(VECTOR_ELT(mats, i));
+        valid[i] = (uint8_t*)R_alloc(rd.n_rows ? rd.n_rows : 1, 1);
+    }
+    int rc = rcp_profile_samples(rs, ns, &rd, &bd, asInteger(inflight), outs, valid);
+    if (rc != RCP_OK) {
+        UNPROTECT(1);
+        check(rc);
+    }
+    SEXP res = PROTECT(allocVector(VECSXP, ns));
+    for (int i = 0; i < ns; ++i) SET_VECTOR_ELT(res, i, profile_result(VECTOR_ELT(mats, i), valid[i], rd.n_rows));
+    UNPROTECT(2);
     return res;
 }
 
@@ -370,6 +402,7 @@ static const R_CallMethodDef call_methods[] = {
     {"rcp_R_readsets", (DL_FUNC)&rcp_R_readsets, 7},
     {"rcp_R_profile", (DL_FUNC)&rcp_R_profile, 17},
     {"rcp_R_profile_multi", (DL_FUNC)&rcp_R_profile_multi, 17},
+    {"rcp_R_profile_samples", (DL_FUNC)&rcp_R_profile_samples, 18},
     {"rcp_R_profile_rle", (DL_FUNC)&rcp_R_profile_rle, 13},
     {"rcp_R_coverage", (DL_FUNC)&rcp_R_coverage, 9},
     {"rcp_R_read_bam", (DL_FUNC)&rcp_R_read_bam, 4},

@@ -100,6 +100,9 @@ SIGNATURES = [
                                                 ctypes.POINTER(_vp)]),
     ("rcp_profile_multi", ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int32, ctypes.POINTER(RowsDesc),
                                          ctypes.POINTER(BinsDesc), _dp, _u8p, _i32p]),
+    ("rcp_profile_samples", ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int32, ctypes.POINTER(RowsDesc),
+                                           ctypes.POINTER(BinsDesc), ctypes.c_int32, ctypes.POINTER(_dp),
+                                           ctypes.POINTER(_u8p)]),
     ("rcp_calc_coverage", ctypes.c_int, [_vp, _i64p, _vp, _vp, _vp]),
     ("rcp_profile_rle", ctypes.c_int, [ctypes.POINTER(RleDesc), ctypes.POINTER(BinsDesc), ctypes.c_int, _dp, _u8p]),
     ("rcp_rle_encode", ctypes.c_int, [ctypes.c_int32, _i64p, _vp, ctypes.c_int, _vp, _vp, _i64p, _i64p, _vp]),

@@ -1355,6 +1355,82 @@ extern "C" int rcp_readset_create_multi(const rcp_reads_desc* desc, const int32_
     RCP_CATCH
 }
 
+extern "C" int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_samples, const rcp_rows_desc* rows,
+                                   const rcp_bins_desc* bins, int32_t inflight, double* const* outs,
+                                   uint8_t* const* row_valid) {
+    RCP_TRY
+    if (!readsets || !rows || !bins) return fail(RCP_EINVAL, "NULL argument");
+    if (n_samples < 0) return fail(RCP_EINVAL, "n_samples = %d", n_samples);
+    if (inflight < 0 || inflight > 3) return fail(RCP_EINVAL, "inflight = %d (0..3)", inflight);
+    if (n_samples == 0) return RCP_OK;
+    for (int i = 0; i < n_samples; ++i) {
+        if (!readsets[i]) return fail(RCP_EINVAL, "readsets[%d] is NULL", i);
+        if (readsets[i]->device != readsets[0]->device)
+            return fail(RCP_EINVAL, "readsets[%d] is on device %d, readsets[0] on %d (one device per call)", i,
+                        readsets[i]->device, readsets[0]->device);
+    }
+    const int dev = readsets[0]->device;
+    const int D = std::min(n_samples, inflight == 0 ? 2 : inflight);
+    // plans first (host work and small uploads), so the passes below are launches only
+    std::vector<std::unique_ptr<rcp_plan, int (*)(rcp_plan*)>> plans;
+    plans.reserve(n_samples);
+    for (int i = 0; i < n_samples; ++i) {
+        rcp_plan* plan = nullptr;
+        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, {0, 0, 0}};
+        const int e = rcp_plan_create_ex(readsets[i], rows, bins, &opts, &plan);
+        if (e) return e;
+        plans.emplace_back(plan, rcp_plan_destroy);
+    }
+    DeviceGuard g(dev);
+    HIP_TRY(g.err);
+    const rcp_plan* p0 = plans[0].get();
+    const size_t cells = (size_t)p0->out_ld * (size_t)p0->n_cols;
+    std::vector<DevBuf> d_out(D), d_valid(D);
+    std::vector<hipStream_t> st(D, nullptr);
+    struct Streams {
+        std::vector<hipStream_t>& v;
+        ~Streams() {
+            for (hipStream_t x : v)
+                if (x) (void)hipStreamDestroy(x);
+        }
+    } sguard{st};
+    for (int k = 0; k < D; ++k) {
+        HIP_TRY(d_out[k].alloc(8 * std::max<size_t>(cells, 1)));
+        HIP_TRY(d_valid[k].alloc(std::max<int32_t>(p0->n_rows, 1)));
+        HIP_TRY(hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking));
+    }
+    // sample j's pass ran on slot j % D: wait for it, check its status, copy its matrix out
+    auto finish = [&](int j) -> int {
+        const int k = j % D;
+        rcp_plan* plan = plans[j].get();
+        int e = rcp_plan_status(plan, st[k]);
+        if (e) return e;
+        if (outs && outs[j] && plan->n_rows && plan->n_cols)
+            HIP_TRY(rcp::stage_d2h_2d(outs[j], 8 * (size_t)plan->n_rows, d_out[k].p, 8 * (size_t)plan->out_ld,
+                                      8 * (size_t)plan->n_rows, (size_t)plan->n_cols, dev, st[k]));
+        if (row_valid && row_valid[j] && plan->n_rows) {
+            HIP_TRY(hipMemcpyAsync(row_valid[j], d_valid[k].p, plan->n_rows, hipMemcpyDeviceToHost, st[k]));
+            HIP_TRY(hipStreamSynchronize(st[k]));
+        }
+        return RCP_OK;
+    };
+    for (int i = 0; i < n_samples; ++i) {
+        if (i >= D) {
+            const int e = finish(i - D);  // frees slot i % D
+            if (e) return e;
+        }
+        const int k = i % D;
+        const int e = rcp_plan_execute(plans[i].get(), d_out[k].as<double>(), d_valid[k].as<uint8_t>(), nullptr, st[k]);
+        if (e) return e;
+    }
+    for (int j = std::max(0, n_samples - D); j < n_samples; ++j) {
+        const int e = finish(j);
+        if (e) return e;
+    }
+    return RCP_OK;
+    RCP_CATCH
+}
+
 extern "C" int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices, const rcp_rows_desc* rows,
                                  const rcp_bins_desc* bins, double* out, uint8_t* row_valid, int32_t* row_split) {
     RCP_TRY

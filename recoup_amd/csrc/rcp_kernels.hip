@@ -1690,6 +1690,9 @@ extern "C" int rcp_rows_window_cap(void) { return kRWCap; }
 #ifndef RCP_ROWS_NT
 #define RCP_ROWS_NT 0
 #endif
+#ifndef RCP_ROWS_ABL
+#define RCP_ROWS_ABL 0
+#endif
 __device__ __forceinline__ void rows_store(double x, double* p) {
 #if RCP_ROWS_NT
     __builtin_nontemporal_store(x, p);
@@ -1886,7 +1889,13 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     if (pow2) x = ((double)num * sc) * rdd;
                     else if (lay < 0) x = ((double)num * sc) / dd;
                     else x = ((double)num * sc) / (double)(b - a);
+#if RCP_ROWS_ABL == 1
+                    if (x == -12345.0) rows_store(x, out + (size_t)(part.col_off + k) * R + r);  // (timing ablation: no stores)
+#elif RCP_ROWS_ABL == 2
+                    rows_store(x, out + (size_t)r * P.n_cols + (part.col_off + k));  // (timing ablation: row-major)
+#else
                     rows_store(x, out + (size_t)(part.col_off + k) * R + r);
+#endif
                     if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = (int64_t)num;
                 }
                 lds_order();

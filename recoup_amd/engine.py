@@ -342,6 +342,23 @@ def profile_multi(readsets, rows, bins):
     return out.T, valid.astype(bool), split
 
 
+def profile_samples(readsets, rows, bins, inflight=0):
+    """rcp_profile_samples: one region table over several samples' readsets (one GPU), passes
+    kept ``inflight`` deep on separate HIP streams (0 = the library's default, 2), each matrix
+    copied into its own host array.  Returns [(matrix (n_rows, n_cols) float64, validity bool)]."""
+    rd = rows.desc()
+    bd = bins.desc()
+    n = len(readsets)
+    hs = (ctypes.c_void_p * n)(*[r.h.value for r in readsets])
+    outs = [np.zeros((bins.n_cols, rows.n_rows), np.float64) for _ in range(n)]
+    valids = [np.zeros(max(rows.n_rows, 1), np.uint8) for _ in range(n)]
+    po = (_lib._dp * n)(*[cptr(o, _lib._dp) for o in outs])
+    pv = (_lib._u8p * n)(*[cptr(v, _lib._u8p) for v in valids])
+    with torch.cuda.device(readsets[0].device if n else 0):
+        check(_lib.lib().rcp_profile_samples(hs, n, ctypes.byref(rd), ctypes.byref(bd), int(inflight), po, pv))
+    return [(o.T, v[:rows.n_rows].astype(bool)) for o, v in zip(outs, valids)]
+
+
 def rle_arrays(coverages):
     """Flatten a coverage list (None = R's NULL, an ``Rle``-like object with ``values`` /
     ``lengths``, or a dense vector) into the run arrays of rcp_rle_desc: (run_off int64,

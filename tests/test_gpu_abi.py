@@ -166,3 +166,31 @@ def test_coverage_rle_host_one_shot(c1):
             if e is not None:
                 np.testing.assert_array_equal(vals[off[r]:off[r + 1]], e[0])
                 np.testing.assert_array_equal(lens[off[r]:off[r + 1]], e[1])
+
+
+@pytest.mark.parametrize("n_samples,inflight,nb", [(4, 2, 100), (5, 3, 1000), (3, 1, 40), (2, 0, 0)])
+def test_profile_samples_bit_equal(gpu, n_samples, inflight, nb):
+    """rcp_profile_samples (profileMatrix's loop over a recoup input list's samples, passes kept
+    `inflight` deep on separate HIP streams, each matrix staged into its own host array) gives
+    every sample the bits of its own single pass; nb = 0 is a per-base part."""
+    from recoup_amd.engine import ReadSet, profile_samples
+    from tests.test_gpu_random import CHROM_LEN, make_reads, single_rows
+    rng = np.random.default_rng(40 + n_samples)
+    rows = single_rows(rng, 700, 2000, edge=nb > 0)  # (a per-base part needs equal row widths)
+    bins = Bins([("whole", nb)]) if nb else Bins([("whole", 0, 2000)])
+    rss = [ReadSet(*make_reads(rng, 60_000 + 5_000 * i, star_frac=0.1), CHROM_LEN, device=0)
+           for i in range(n_samples)]
+    got = profile_samples(rss, rows, bins, inflight=inflight)
+    assert len(got) == n_samples
+    for rs, (mat, valid) in zip(rss, got):
+        ref, rvalid = Plan(rs, rows, bins).run()
+        np.testing.assert_array_equal(valid, rvalid)
+        assert np.array_equal(mat.view(np.uint64), np.ascontiguousarray(ref).view(np.uint64))
+
+
+def test_profile_samples_errors(c1):
+    from recoup_amd.engine import profile_samples
+    rows = helpers.tss_rows(c1["G"])
+    with pytest.raises(_lib.RcpError, match="inflight"):
+        profile_samples(c1["rs"], rows, Bins([("whole", 20)]), inflight=4)
+    assert profile_samples([], rows, Bins([("whole", 20)])) == []

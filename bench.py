@@ -57,9 +57,9 @@ def parse():
     ap.add_argument("--verify-gather", action="store_true",
                     help="N > 1: rank 0 also runs the whole workload alone and checks the gathered matrix bit for bit")
     ap.add_argument("--no-e2e", action="store_true", help="skip the one-off host-to-host timing")
-    ap.add_argument("--inflight", default="auto", choices=["auto", "1", "2"],
+    ap.add_argument("--inflight", default="auto", choices=["auto", "1", "2", "3"],
                     help="passes in flight on separate HIP streams (D plans over the same readset and region "
-                         "table, like D sample slots); auto: the faster of 1 and 2, timed after the warmup")
+                         "table, like D sample slots); auto: the fastest of 1, 2, 3, timed after the warmup")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default profiles/traffic_<config>.json")
     return ap.parse_args()
@@ -247,12 +247,14 @@ def main():
     # shards and C5 leave the persistent pileup grid partly idle at its start and end).
     plans, outs, valids = [plan], [out], [valid]
     streams = [torch.cuda.current_stream()]
-    if args.inflight != "1":
-        p2 = Plan(rs, rows, bins, out_ld="padded")
-        plans.append(p2)
-        outs.append(p2.empty_output())
-        valids.append(torch.empty(max(R, 1), dtype=torch.uint8, device=dev))
-        streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+    dmax = 3 if args.inflight == "auto" else int(args.inflight)
+    if dmax > 1:
+        for _ in range(dmax - 1):
+            p2 = Plan(rs, rows, bins, out_ld="padded")
+            plans.append(p2)
+            outs.append(p2.empty_output())
+            valids.append(torch.empty(max(R, 1), dtype=torch.uint8, device=dev))
+        streams = [torch.cuda.Stream(device=dev) for _ in range(dmax)]
 
     def passes(D, n):
         for k in range(n):
@@ -267,7 +269,7 @@ def main():
     D = len(plans)
     if args.inflight == "auto":
         tune = {}
-        for d in (1, 2):
+        for d in range(1, dmax + 1):
             torch.cuda.synchronize()
             t = time.perf_counter()
             passes(d, max(args.steps, 10))
@@ -292,8 +294,9 @@ def main():
     for p in plans:
         p.status()
     # (bitwise: a row the reference maps to NaN -- e.g. a spline through one knot -- is NaN in both)
-    if D == 2 and not torch.equal(outs[0][:, :R].view(torch.int64), outs[1][:, :R].view(torch.int64)):
-        raise SystemExit("passes in flight disagree")
+    for i in range(1, D):
+        if not torch.equal(outs[0][:, :R].view(torch.int64), outs[i][:, :R].view(torch.int64)):
+            raise SystemExit("passes in flight disagree")
 
     # ---- per-kernel durations with HIP events on the launch stream
     stream = torch.cuda.current_stream()

@@ -503,6 +503,7 @@ struct rcp_plan {
     DevBuf tables;     // read-only tables
     DevBuf work;       // seg_lo / seg_hi / valid / status
     DevBuf scratch;    // interpolation scratch
+    DevBuf rm;         // row-wave kernel: row-major staging of the matrix
     int32_t max_row_len = 0;
     int64_t out_ld = 0;
     uint32_t* status_sets = nullptr;  // 2 x RCP_STATUS_WORDS words in `work`
@@ -1130,6 +1131,12 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.interp_scratch = plan->scratch.as<double>();
     P.csr_off = nullptr;
     P.csr_out = nullptr;
+    // row-wave plans stage their bins row-major (whole lines per row) and transpose once
+    P.rm = nullptr;
+    if (P.lean == 3 && R > 0 && P.n_cols > 0) {
+        HIP_TRY(plan->rm.alloc(8 * (size_t)R * (size_t)P.n_cols));
+        P.rm = plan->rm.as<double>();
+    }
     plan->lds = P.lean == 3 ? rcp_pileup_rows_lds_bytes()
                             : (P.lean ? rcp_pileup_lean_lds_bytes(&P) : rcp_pileup_lds_bytes(&P, cov_only ? 1 : 0));
     // general kernel: 2 rounds (32 rows) per workgroup (C3: 0.88 ms vs 0.91 with 4 rounds, 0.89

@@ -1690,9 +1690,7 @@ extern "C" int rcp_rows_window_cap(void) { return kRWCap; }
 #ifndef RCP_ROWS_NT
 #define RCP_ROWS_NT 0
 #endif
-#ifndef RCP_ROWS_ABL
-#define RCP_ROWS_ABL 0
-#endif
+
 __device__ __forceinline__ void rows_store(double x, double* p) {
 #if RCP_ROWS_NT
     __builtin_nontemporal_store(x, p);
@@ -1756,9 +1754,15 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                 __builtin_amdgcn_s_sleep(2);
         }
     };
+    // the matrix cell (row r, column c): row-major staging (P.rm, transposed after the kernel:
+    // a row's bins are whole lines) or, with binsum, the column-major output itself
+    double* const rm = binsum ? nullptr : P.rm;
+    auto cell = [&](int r, int64_t c) -> double* {
+        return rm ? rm + (size_t)r * (size_t)P.n_cols + (size_t)c : out + (size_t)c * R + r;
+    };
     auto zero_cols = [&](int r, const RcpPart& part, int32_t n) {
         for (int32_t k = lane; k < n; k += 64) {
-            rows_store(0.0, out + (size_t)(part.col_off + k) * R + r);
+            rows_store(0.0, cell(r, part.col_off + k));
             if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = 0;
         }
     };
@@ -1889,13 +1893,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     if (pow2) x = ((double)num * sc) * rdd;
                     else if (lay < 0) x = ((double)num * sc) / dd;
                     else x = ((double)num * sc) / (double)(b - a);
-#if RCP_ROWS_ABL == 1
-                    if (x == -12345.0) rows_store(x, out + (size_t)(part.col_off + k) * R + r);  // (timing ablation: no stores)
-#elif RCP_ROWS_ABL == 2
-                    rows_store(x, out + (size_t)r * P.n_cols + (part.col_off + k));  // (timing ablation: row-major)
-#else
-                    rows_store(x, out + (size_t)(part.col_off + k) * R + r);
-#endif
+                    rows_store(x, cell(r, part.col_off + k));
                     if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = (int64_t)num;
                 }
                 lds_order();
@@ -2612,6 +2610,27 @@ static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* bin
 
 extern "C" size_t rcp_pileup_rows_lds_bytes(void) { return 4 * (size_t)kRWaves * kRWWords + 16; }
 
+// The row-wave kernel's row-major matrix (P.rm) -> the R column-major output: 64 x 64 tiles
+// through LDS, 512-byte row segments in, 512-byte column segments out.
+__global__ void __launch_bounds__(256) rcp_rm_transpose_kernel(const double* __restrict__ rm, double* __restrict__ out,
+                                                               int32_t n_rows, int64_t n_cols, int64_t ld) {
+    __shared__ double t[64][65];
+    const int64_t c0 = (int64_t)blockIdx.x * 64;
+    const int32_t r0 = (int32_t)blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int i = ty; i < 64; i += 4) {
+        const int32_t r = r0 + i;
+        const int64_t c = c0 + tx;
+        if (r < n_rows && c < n_cols) t[i][tx] = rm[(size_t)r * (size_t)n_cols + (size_t)c];
+    }
+    __syncthreads();
+    for (int j = ty; j < 64; j += 4) {
+        const int64_t c = c0 + j;
+        const int32_t r = r0 + tx;
+        if (r < n_rows && c < n_cols) __builtin_nontemporal_store(t[tx][j], out + (size_t)c * (size_t)ld + r);
+    }
+}
+
 static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* binsum, hipStream_t s) {
     // persistent: four workgroups (16 waves) per CU, a multiple of 8 (workgroup b serves XCD
     // b % 8), never more workgroups than tiles
@@ -2620,6 +2639,10 @@ static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* 
     const int64_t grid = std::min<int64_t>(((int64_t)4 * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
     hipLaunchKernelGGL(rcp_pileup_rows_kernel, dim3((unsigned)grid), dim3(64 * kRWaves), rcp_pileup_rows_lds_bytes(), s,
                        *P, out, binsum);
+    if (P->rm && !binsum && P->n_cols > 0) {
+        const dim3 tg((unsigned)((P->n_cols + 63) / 64), (unsigned)((P->n_rows + 63) / 64));
+        hipLaunchKernelGGL(rcp_rm_transpose_kernel, tg, dim3(256), 0, s, P->rm, out, P->n_rows, P->n_cols, P->out_ld);
+    }
     return hipGetLastError();
 }
 
@@ -2640,6 +2663,8 @@ static size_t interp_int_bytes(const RcpPlanDev* P) {
 }
 
 static bool interp_in_lds(const RcpPlanDev* P) {
+    // (the spline's arrays in global scratch instead, which lets every row's block be resident
+    // at once, measured slower on C3: 0.128 vs 0.123 ms, profiles/r02h/c3_transpose_interp_ab.log)
     return interp_int_bytes(P) + 8 * (size_t)P->interp_stride + 16 <= 160 * 1024;
 }
 

@@ -29,7 +29,7 @@ def per_launch(path, counter):
                 if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
                     vals.append(float(row["Counter_Value"]) * 1024.0)
         if vals:
-            return sum(vals) / len(vals), len(vals), kernel.rstrip("<")
+            return sum(vals) / len(vals), len(vals), kernel.rstrip("<(")
     raise SystemExit(f"no {counter} rows for {KERNELS} under {path}")
 
 

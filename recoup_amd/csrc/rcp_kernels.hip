@@ -2612,18 +2612,21 @@ extern "C" size_t rcp_pileup_rows_lds_bytes(void) { return 4 * (size_t)kRWaves *
 
 // The row-wave kernel's row-major matrix (P.rm) -> the R column-major output: 64 x 64 tiles
 // through LDS, 512-byte row segments in, 512-byte column segments out.
+// (128-row tiles -- 66 KB of LDS -- measured slower: profiles/r02h/c3_transpose_variants_ab.log)
 __global__ void __launch_bounds__(256) rcp_rm_transpose_kernel(const double* __restrict__ rm, double* __restrict__ out,
                                                                int32_t n_rows, int64_t n_cols, int64_t ld) {
     __shared__ double t[64][65];
     const int64_t c0 = (int64_t)blockIdx.x * 64;
     const int32_t r0 = (int32_t)blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
     for (int i = ty; i < 64; i += 4) {
         const int32_t r = r0 + i;
         const int64_t c = c0 + tx;
-        if (r < n_rows && c < n_cols) t[i][tx] = rm[(size_t)r * (size_t)n_cols + (size_t)c];
+        if (r < n_rows && c < n_cols) t[i][tx] = __builtin_nontemporal_load(rm + (size_t)r * (size_t)n_cols + (size_t)c);
     }
     __syncthreads();
+#pragma unroll
     for (int j = ty; j < 64; j += 4) {
         const int64_t c = c0 + j;
         const int32_t r = r0 + tx;

@@ -91,3 +91,32 @@ def test_null_arguments_are_rejected():
     assert L.rcp_profile_multi(None, 1, None, None, None, None, None) == -1
     assert L.rcp_readset_create_multi(None, None, 1, None) == -1
     assert L.rcp_plan_destroy(None) == 0 or L.rcp_plan_destroy(None) == -1
+
+
+# header struct -> ctypes mirror in recoup_amd/_lib.py
+STRUCTS = {"rcp_reads_desc": "ReadsDesc", "rcp_rows_desc": "RowsDesc", "rcp_bins_desc": "BinsDesc",
+           "rcp_plan_info": "PlanInfo", "rcp_plan_opts": "PlanOpts", "rcp_rle_desc": "RleDesc"}
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """Every descriptor struct the ctypes binding passes has the header's size and field offsets
+    (a C probe compiled with gcc against include/recoup_amd.h prints them)."""
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "recoup_amd.h"', "int main(void) {"]
+    for c, py in STRUCTS.items():
+        lines.append(f'  printf("{c} size %zu\\n", sizeof({c}));')
+        for name, _ in getattr(_lib, py)._fields_:
+            lines.append(f'  printf("{c} {name} %zu\\n", offsetof({c}, {name}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for ln in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        c, f, v = ln.split()
+        got[(c, f)] = int(v)
+    for c, py in STRUCTS.items():
+        cls = getattr(_lib, py)
+        assert ctypes.sizeof(cls) == got[(c, "size")], c
+        for name, _ in cls._fields_:
+            assert getattr(cls, name).offset == got[(c, name)], (c, name)

@@ -142,8 +142,9 @@ struct RcpPlanDev {
     int32_t lean;               // 1: every row is one plain range with uniform power-of-two bins
                                 //    of one wave chunk -> rcp_pileup_lean_kernel
     // row-wave kernel (lean == 3): its rows' bins go row-major into rm (n_rows x n_cols, whole
-    // lines per row) and one transpose launch writes them into the R column-major output; a
-    // row-wave store straight into the column-major matrix is 8 bytes per 128-B line
+    // lines per row); the last wave to finish a 16-row tile writes the tile's rows of every
+    // column into the R column-major output as whole 128-B lines (a row-wave store straight
+    // into the column-major matrix is 8 bytes per 128-B line)
     double* rm;                 // nullptr: direct column-major stores
     // coverage (CSR) mode
     const int64_t* csr_off;     // non-null: write per-row depth into csr (calcCoverage)

@@ -1684,12 +1684,13 @@ constexpr int kRWWords = 8 + 64 * ((1 << kRWSh) + 4);  // per wave: 8 zero words
 
 extern "C" int rcp_rows_window_cap(void) { return kRWCap; }
 
-// A wave writes one row's bins: 8 bytes per 128-B line of each column.  The 16 rows of a line are
-// claimed together by waves of one XCD, so plain stores meet in that L2 and leave it as whole
-// lines; non-temporal stores would go out as partial-line writes.
+// Stores of a row's bins: row-major into the staging (P.rm, whole lines per row), or -- with
+// binsum, which keeps the column-major layout -- 8 bytes per 128-B column line; the 16 rows of a
+// line are claimed together by waves of one XCD, so plain stores meet in that L2.
 #ifndef RCP_ROWS_NT
 #define RCP_ROWS_NT 0
 #endif
+
 
 __device__ __forceinline__ void rows_store(double x, double* p) {
 #if RCP_ROWS_NT
@@ -1718,8 +1719,21 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     // the next tile and publishes it, waves drawing past 16 wait for the new tile.
     unsigned long long* queue = reinterpret_cast<unsigned long long*>(smem + 4 * kRWaves * kRWWords);
     constexpr uint32_t kEmpty = 0xFFFFFFFEu, kDone = 0xFFFFFFFFu;
+    // tile slots of the flush: tile id, rows finished (kFree: flushed),
+    // and the workgroup's tile sequence number (slot = seq % kSlots)
+    constexpr int kSlots = 4;
+    constexpr uint32_t kFree = 0xFFFFFFFFu;
+    uint32_t* slot_tile = reinterpret_cast<uint32_t*>(queue + 1);
+    uint32_t* slot_cnt = slot_tile + kSlots;
+    uint32_t* seq = slot_cnt + kSlots;
     if (threadIdx.x == 0) *queue = ((unsigned long long)kEmpty << 32) | kTile;
+    if (threadIdx.x < kSlots) {
+        slot_tile[threadIdx.x] = kDone;
+        slot_cnt[threadIdx.x] = kFree;
+    }
+    if (threadIdx.x == 0) *seq = 0;
     __syncthreads();
+    double* const rm = binsum ? nullptr : P.rm;
     auto fetch_tile = [&]() -> uint32_t {
         for (int k = 0; k < 8; ++k) {
             const int xs = (xcd + k) & 7;
@@ -1746,6 +1760,19 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             }
             if (idx == (uint32_t)kTile) {
                 const uint32_t t = fetch_tile();
+                if (rm && t != kDone) {
+                    // the tile's slot: free once the tile kSlots before it has been flushed (its
+                    // last rows are in progress on other waves, which never wait on this one)
+                    const uint32_t sl = *(volatile uint32_t*)seq % kSlots;
+                    while ((uint32_t)__builtin_amdgcn_readfirstlane((int)*(volatile uint32_t*)&slot_cnt[sl]) != kFree)
+                        __builtin_amdgcn_s_sleep(2);
+                    if (lane == 0) {
+                        slot_tile[sl] = t;
+                        slot_cnt[sl] = 0;
+                        *seq = *seq + 1;
+                    }
+                    lds_order();
+                }
                 if (lane == 0) atomicExch(queue, ((unsigned long long)t << 32));
                 continue;
             }
@@ -1754,9 +1781,8 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                 __builtin_amdgcn_s_sleep(2);
         }
     };
-    // the matrix cell (row r, column c): row-major staging (P.rm, transposed after the kernel:
-    // a row's bins are whole lines) or, with binsum, the column-major output itself
-    double* const rm = binsum ? nullptr : P.rm;
+    // the matrix cell (row r, column c): row-major staging (P.rm, written into the column-major
+    // output tile by tile: a row's bins are whole lines) or, with binsum, the output itself
     auto cell = [&](int r, int64_t c) -> double* {
         return rm ? rm + (size_t)r * (size_t)P.n_cols + (size_t)c : out + (size_t)c * R + r;
     };
@@ -1766,15 +1792,55 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = 0;
         }
     };
-    for (int r = claim(); r >= 0; r = claim()) {
+    // the last wave to finish a row of tile T writes the tile's 16 rows of every column from the
+    // row-major staging as whole 128-B column lines (release / acquire: the other waves' staging
+    // stores are visible to it); lane = (row i, column quarter): 4 columns x 16 rows per store
+    auto flush = [&](uint32_t T) {
+        const int32_t t16 = (int32_t)T * kTile;
+        const int32_t nrow = min(kTile, P.n_rows - t16);
+        const int i = lane & 15, cq = lane >> 4;
+        const int64_t nc = P.n_cols;
+        const double* src = rm + (size_t)(t16 + i) * (size_t)nc;
+        for (int64_t c0 = 0; c0 < nc; c0 += 32) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t c = c0 + 4 * u + cq;
+                v[u] = (i < nrow && c < nc) ? src[c] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t c = c0 + 4 * u + cq;
+                if (i < nrow && c < nc) __builtin_nontemporal_store(v[u], out + (size_t)c * R + (size_t)(t16 + i));
+            }
+        }
+    };
+    auto row_done = [&](int r) {
+        const uint32_t T = (uint32_t)(r / kTile);
+        int sl = 0;
+        for (int k = 1; k < kSlots; ++k)
+            if (slot_tile[k] == T) sl = k;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        uint32_t old = 0;
+        if (lane == 0) old = atomicAdd(&slot_cnt[sl], 1u);
+        old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+        if ((int32_t)old + 1 == min(kTile, P.n_rows - (int32_t)T * kTile)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            flush(T);
+            lds_order();
+            if (lane == 0) atomicExch(&slot_cnt[sl], kFree);
+        }
+    };
+    auto row_body = [&](int r) {
         const uint4 rc = *reinterpret_cast<const uint4*>(P.rec + r);  // flags, row_len, heavy, off
         const int32_t flags = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.x);
         const int32_t nr = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.y);
         const int32_t heavy = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.z);
         if (!(flags & RCP_REC_VALID)) {  // NULL row -> zeros (profile.R:191-197)
             for (int p = 0; p < P.n_parts; ++p) zero_cols(r, P.part[p], P.part[p].n_bins);
-            continue;
+            return;
         }
+
         const int j0 = P.row_info[r].j0, j1 = P.row_info[r].j1;
         const int64_t d0 = P.row_info[r].d0;
         const int32_t dnb = P.row_info[r].nb;
@@ -1899,6 +1965,10 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                 lds_order();
             }
         }
+    };
+    for (int r = claim(); r >= 0; r = claim()) {
+        row_body(r);
+        if (rm) row_done(r);
     }
     // the last workgroup out resets the tile counters for the next launch
     __syncthreads();
@@ -2608,31 +2678,7 @@ static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* bin
     return hipGetLastError();
 }
 
-extern "C" size_t rcp_pileup_rows_lds_bytes(void) { return 4 * (size_t)kRWaves * kRWWords + 16; }
-
-// The row-wave kernel's row-major matrix (P.rm) -> the R column-major output: 64 x 64 tiles
-// through LDS, 512-byte row segments in, 512-byte column segments out.
-// (128-row tiles -- 66 KB of LDS -- measured slower: profiles/r02h/c3_transpose_variants_ab.log)
-__global__ void __launch_bounds__(256) rcp_rm_transpose_kernel(const double* __restrict__ rm, double* __restrict__ out,
-                                                               int32_t n_rows, int64_t n_cols, int64_t ld) {
-    __shared__ double t[64][65];
-    const int64_t c0 = (int64_t)blockIdx.x * 64;
-    const int32_t r0 = (int32_t)blockIdx.y * 64;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-#pragma unroll
-    for (int i = ty; i < 64; i += 4) {
-        const int32_t r = r0 + i;
-        const int64_t c = c0 + tx;
-        if (r < n_rows && c < n_cols) t[i][tx] = __builtin_nontemporal_load(rm + (size_t)r * (size_t)n_cols + (size_t)c);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = ty; j < 64; j += 4) {
-        const int64_t c = c0 + j;
-        const int32_t r = r0 + tx;
-        if (r < n_rows && c < n_cols) __builtin_nontemporal_store(t[tx][j], out + (size_t)c * (size_t)ld + r);
-    }
-}
+extern "C" size_t rcp_pileup_rows_lds_bytes(void) { return 4 * (size_t)kRWaves * kRWWords + 16 + 48; }
 
 static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* binsum, hipStream_t s) {
     // persistent: four workgroups (16 waves) per CU, a multiple of 8 (workgroup b serves XCD
@@ -2642,10 +2688,6 @@ static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* 
     const int64_t grid = std::min<int64_t>(((int64_t)4 * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
     hipLaunchKernelGGL(rcp_pileup_rows_kernel, dim3((unsigned)grid), dim3(64 * kRWaves), rcp_pileup_rows_lds_bytes(), s,
                        *P, out, binsum);
-    if (P->rm && !binsum && P->n_cols > 0) {
-        const dim3 tg((unsigned)((P->n_cols + 63) / 64), (unsigned)((P->n_rows + 63) / 64));
-        hipLaunchKernelGGL(rcp_rm_transpose_kernel, tg, dim3(256), 0, s, P->rm, out, P->n_rows, P->n_cols, P->out_ld);
-    }
     return hipGetLastError();
 }
 

@@ -590,32 +590,17 @@ __device__ __forceinline__ bool chunk_window(const RcpPlanDev& P, const RcpPart&
 template <int CTRL>
 __device__ __forceinline__ int qperm(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false); }
 
-// lower_bound(pmax >= v) (upper = false) or upper_bound(start > v) (upper = true) of stream
-// `st`, confined to the reads of v's directory bucket (rcp_device.h), as ONE instruction
-// stream: first index of the bucket with key >= thr, key = pmax or start.  Lanes of a quad
-// that look for different bounds then search in lockstep, their loads in flight together
-// (two separate functions would run one after the other under the exec mask).  (An 8-ary
+// Up to K searches of one lane bisecting in lockstep: search u is lower_bound(pmax >= v[u])
+// or, when dst[u] == -1 or dst[u] is odd (the locate task numbering), upper_bound(start >
+// v[u]), confined to the reads of v[u]'s bucket of the directory at entry d0[u] (nb[u]
+// buckets; rcp_device.h).  Both bounds are one instruction stream (first index of the bucket
+// with key >= thr, key = pmax or start), and each step issues the probes of all unfinished
+// searches before using any, so they cost one chain of round trips together.  (An 8-ary
 // variant -- 7 probes in flight per step -- measured slower on C4: 0.099 vs 0.082 ms.)
-__device__ __forceinline__ uint32_t dir_bound_at(const RcpPlanDev& P, int64_t d0, int32_t nb, int32_t v, bool upper) {
-    const int32_t b = min(max(v, 0) >> P.dir_shift, nb - 1);
-    const int32_t* dir = upper ? P.dir_u : P.dir_l;  // interleaved (l, u) pairs: stride 2
-    uint32_t lo = (uint32_t)dir[2 * (d0 + b)], hi = (uint32_t)dir[2 * (d0 + b + 1)];
-    const int32_t* key = upper ? reinterpret_cast<const int32_t*>(P.se) : P.pmax;
-    const int ksh = upper ? 1 : 0;                      // start of read m is word 2m of se
-    const int64_t thr = (int64_t)v + (upper ? 1 : 0);  // start > v  <=>  start >= v + 1
-    while (lo < hi) {
-        const uint32_t m = lo + ((hi - lo) >> 1);
-        if ((int64_t)key[(size_t)m << ksh] < thr) lo = m + 1; else hi = m;
-    }
-    return lo;
-}
-
-// Up to K searches of one lane (search u: v[u], upper when dst[u] == -1 or dst[u] is odd, as
-// the locate task numbering has it) bisecting in lockstep: each step issues the probes of all
-// unfinished searches before using any, so they cost one chain of round trips together.
 template <int K>
-__device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0, int32_t nb, const int32_t (&v)[K],
-                                                const int (&dst)[K], int cnt, uint32_t (&res)[K]) {
+__device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64_t (&d0)[K], const int32_t (&nb)[K],
+                                                const int32_t (&v)[K], const int (&dst)[K], int cnt,
+                                                uint32_t (&res)[K]) {
     uint32_t lo[K], hi[K];
     int64_t thr[K];
     bool up[K];
@@ -625,10 +610,10 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0,
         lo[u] = hi[u] = 0;
         thr[u] = (int64_t)v[u] + (up[u] ? 1 : 0);
         if (u < cnt) {
-            const int32_t b = min(max(v[u], 0) >> P.dir_shift, nb - 1);
+            const int32_t b = min(max(v[u], 0) >> P.dir_shift, nb[u] - 1);
             const int32_t* dir = up[u] ? P.dir_u : P.dir_l;  // interleaved: stride 2
-            lo[u] = (uint32_t)dir[2 * (d0 + b)];
-            hi[u] = (uint32_t)dir[2 * (d0 + b + 1)];
+            lo[u] = (uint32_t)dir[2 * (d0[u] + b)];
+            hi[u] = (uint32_t)dir[2 * (d0[u] + b + 1)];
         }
     }
     const int32_t* se = reinterpret_cast<const int32_t*>(P.se);
@@ -656,10 +641,6 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, int64_t d0,
     for (int u = 0; u < K; ++u) res[u] = lo[u];
 }
 
-__device__ __forceinline__ uint32_t dir_bound(const RcpPlanDev& P, int st, int32_t v, bool upper) {
-    const int64_t d0 = P.dir_off[st];
-    return dir_bound_at(P, d0, (int32_t)(P.dir_off[st + 1] - d0) - 1, v, upper);
-}
 
 // LPR = 4 lanes per row: the row's (segment, stream) searches are dealt round-robin to the
 // quad's lanes (one stream per segment in the merged layout, three in the stranded one), so
@@ -768,7 +749,14 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
         // C2 has 8 searches per row -> 2 per lane, C5 16 -> 4); a 5th starts a second round
         auto run = [&]() {
             uint32_t w[KS];
-            dir_bound_multi<KS>(P, ri.d0, ri.nb, sx, sdst, cnt, w);
+            int64_t dd[KS];
+            int32_t dn[KS];
+#pragma unroll
+            for (int u = 0; u < KS; ++u) {
+                dd[u] = ri.d0;
+                dn[u] = ri.nb;
+            }
+            dir_bound_multi<KS>(P, dd, dn, sx, sdst, cnt, w);
 #pragma unroll
             for (int u = 0; u < KS; ++u)
                 if (u < cnt) {
@@ -824,28 +812,66 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
         }
         if (q != 0) lo = hi = 0;  // the quad combine below reads (lo, hi) from lane 0
     }
-    for (int pi = split1 ? npairs : q; pi < npairs; pi += LPR) {
-        const int j = j0 + pi / ns;
-        const int s = pi % ns;
-        const RcpSeg sg = P.segs[j];
-        const int g = sg.group & 3;
-        present |= 1u << g;
-        maxpos[g] = max(maxpos[g], sg.hi);
-        lo = 0;
-        hi = 0;
-        if (ok && sg.query_ok && ((sg.streams >> s) & 1)) {
-            lo = dir_bound(P, chrom * 3 + s, sg.lo, false);
-            hi = max(lo, dir_bound(P, chrom * 3 + s, sg.hi, true));
-            if (lo < hi) {
-                hit |= 1u << g;
-                if (sl < 0) maxend[g] = max(maxend[g], P.pmax[hi - 1]);  // only NA seqlengths need it
-                ncand += hi - lo;
+    // (segment, stream) pairs dealt round-robin to the quad; a lane's two pairs of one round
+    // (pi, pi + LPR) search their lower and upper bounds in lockstep: one chain of dependent
+    // loads for four searches (an exon list of ~10 segments: 2 rounds instead of 6 chains)
+    for (int pb = split1 ? npairs : q; pb < npairs; pb += 2 * LPR) {
+        int32_t sv[4] = {0, 0, 0, 0};
+        int sd[4] = {-2, -1, -2, -1};
+        int64_t sd0[4] = {0, 0, 0, 0};
+        int32_t snb[4] = {1, 1, 1, 1};
+        bool use[2] = {false, false};
+        int cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int pi = pb + k * LPR;
+            if (pi >= npairs) continue;
+            const int j = j0 + pi / ns;
+            const int s = pi % ns;
+            const RcpSeg sg = P.segs[j];
+            const int g = sg.group & 3;
+            present |= 1u << g;
+            maxpos[g] = max(maxpos[g], sg.hi);
+            if (ok && sg.query_ok && ((sg.streams >> s) & 1)) {
+                use[k] = true;
+                int64_t d0 = ri.d0;
+                int32_t nb = ri.nb;
+                if (!P.merged) {
+                    d0 = P.dir_off[chrom * 3 + s];
+                    nb = (int32_t)(P.dir_off[chrom * 3 + s + 1] - d0) - 1;
+                }
+                sv[2 * k] = sg.lo;
+                sv[2 * k + 1] = sg.hi;
+                sd0[2 * k] = sd0[2 * k + 1] = d0;
+                snb[2 * k] = snb[2 * k + 1] = nb;
+                cnt = 2 * k + 2;
             }
         }
-        P.seg_lo[j * 3 + s] = lo;
-        P.seg_hi[j * 3 + s] = hi;
-        // (merged layout: the entries of streams 1, 2 -- and their crange words -- stay as the
-        // plan zeroed them; no read lives there)
+        uint32_t res[4];
+        dir_bound_multi<4>(P, sd0, snb, sv, sd, cnt, res);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int pi = pb + k * LPR;
+            if (pi >= npairs) continue;
+            const int j = j0 + pi / ns;
+            const int s = pi % ns;
+            const int g = P.segs[j].group & 3;
+            lo = 0;
+            hi = 0;
+            if (use[k]) {
+                lo = res[2 * k];
+                hi = max(lo, res[2 * k + 1]);
+                if (lo < hi) {
+                    hit |= 1u << g;
+                    if (sl < 0) maxend[g] = max(maxend[g], P.pmax[hi - 1]);  // only NA seqlengths need it
+                    ncand += hi - lo;
+                }
+            }
+            P.seg_lo[j * 3 + s] = lo;
+            P.seg_hi[j * 3 + s] = hi;
+            // (merged layout: the entries of streams 1, 2 -- and their crange words -- stay as
+            // the plan zeroed them; no read lives there)
+        }
     }
     // ---- combine the quad (all lanes active: DPP reads neighbours)
     {

@@ -1090,9 +1090,8 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         if (ok) P.cw_len = nr;
     }
     const int32_t n_interp = (int32_t)B.interp_row.size();
-    // x (L+1) | y (n+1) | b, c, d (3 (L+1)) | interval index per output point (n ints); the
-    // neighborhood fill's n pre-fill values reuse b..
-    P.interp_stride = 2 * (max_interp_bins + 1) + 4 * (max_interp_len + 1) + 8;
+    // x (L+1) | b, c, d (3 (L+1)) for the spline, or the neighborhood fill's n pre-fill values
+    P.interp_stride = (max_interp_len + 1) + std::max(max_interp_bins, 3 * (max_interp_len + 1)) + 8;
     if (n_interp) HIP_TRY(plan->scratch.alloc(8 * (size_t)n_interp * P.interp_stride));
 
     const ReadLayout& RL = rows->ignore_strand ? rs->merged : rs->stranded;
@@ -1859,7 +1858,8 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     }
     // interpolation working set: x (L+1) | y (n+1) | b, c, d (3 (L+1)) | n ints
     // (the neighborhood fill's n pre-fill values reuse b.., as in rcp_plan_create)
-    const int64_t stride = 2 * ((int64_t)max_interp_bins + 1) + 4 * ((int64_t)max_interp_len + 1) + 8;
+    const int64_t stride = ((int64_t)max_interp_len + 1) +
+                           std::max<int64_t>(max_interp_bins, 3 * ((int64_t)max_interp_len + 1)) + 8;
     const size_t lds = n_scratch ? 8 * (size_t)stride : 0;
     P.interp_lds = lds <= 160 * 1024 ? 1 : 0;
     P.interp_stride = stride;

@@ -112,25 +112,8 @@ __device__ double seq_point(int L, int n, int i) {
     return (i < n / 2) ? 1.0 + (double)i * by : (double)L - (double)(n - 1 - i) * by;
 }
 
-// spline_eval's interval for each output point, in R's order: the previous interval is kept
-// while x[i] <= u <= x[i+1], else bisection (knots x = 1..n) -- integer-only, on thread 0.
-__device__ void spline_intervals(int L, int n, int32_t* iv) {
-    int i = 0;
-    const int n_1 = L - 1;
-    for (int k = 0; k < n; ++k) {
-        const double u = seq_point(L, n, k);
-        if (u < (double)(i + 1) || (i < n_1 && (double)(i + 2) < u)) {
-            i = 0;
-            int j = L;
-            do {
-                const int m = (i + j) / 2;
-                if (u < (double)(m + 1)) j = m; else i = m;
-            } while (j > i + 1);
-        }
-        iv[k] = i;
-    }
-}
-
+// spline_eval's interval walk (R splines.c): the previous interval i is kept while
+// x[i] <= u <= x[i+1], else bisection (knots x = 1..n)
 __device__ __forceinline__ int spline_bisect(int L, double u) {
     int i = 0, j = L;
     do {
@@ -141,7 +124,7 @@ __device__ __forceinline__ int spline_bisect(int L, double u) {
 }
 
 // The same interval for point k alone, for interpolated rows (L < n: output points closer
-// than one knot apart).  spline_intervals keeps interval i for u in [i+1, i+2] and bisects
+// than one knot apart).  The walk keeps interval i for u in [i+1, i+2] and bisects
 // otherwise; the bisection lands on floor(u) - 1, so the two differ only at a point sitting
 // exactly on a knot m = i + 2 just after a point of interval i (it keeps i, the evaluation
 // runs at dx = 1).  Because consecutive points are less than 1 apart, the interval held at
@@ -166,31 +149,31 @@ __device__ double spline_eval_at(const double* y, const double* b, const double*
 // out[k * ld] (k = 0 .. n - 1).  mode 1: spline(x, n)$y clipped at 0 (auto with (n - L) / n >= 0.2,
 // or "spline"); 3: neighborhood fill with the R-RNG positions nb_pos (1-based, sorted,
 // set.seed(42); sort(sample(3:(n - 2), L - 4))); otherwise "linear", whose switch arm is spelled
-// "inear" (util.R:49): x stays short and rbind recycles it.  Scratch follows x: y = x + L + 1
-// (n + 1), b, c, d (L + 1 each), then n ints.  Call with every thread of the block.
+// "inear" (util.R:49): x stays short and rbind recycles it.  Scratch follows x: b, c, d (L + 1
+// each) for the spline, or the n pre-fill values of the neighborhood fill; every output point is
+// computed and stored by its own thread (no staging of the n outputs: the block's scratch stays
+// small enough for every interpolated row's block to be resident at once).  Call with every
+// thread of the block.
 __device__ void interp_finish(int mode, int L, int n, double* x, const int32_t* nb_pos, const double* spl_tb,
                               double* out, size_t ld) {
-    double* y = x + L + 1;
-    double* b = y + n + 1;
+    double* b = x + L + 1;
     if (mode == 1) {  // spline(x, n = n)$y, then x[x < 0] <- 0
         double* c = b + L + 1;
         double* d = c + L + 1;
-        int32_t* iv = reinterpret_cast<int32_t*>(d + L + 1);
         fmm_spline_block(L, x, b, c, d, spl_tb);
+        auto put = [&](int k, int iv) {
+            const double v = L == 1 ? x[0] : spline_eval_at(x, b, c, d, iv, seq_point(L, n, k));
+            out[(size_t)k * ld] = v < 0 ? 0.0 : v;
+        };
         if (L < n) {  // always, for rows of this kernel; the sequential walk stays as the rule
-            for (int k = threadIdx.x; k < n; k += (int)blockDim.x) iv[k] = spline_interval_at(L, n, k);
+            for (int k = threadIdx.x; k < n; k += (int)blockDim.x) put(k, spline_interval_at(L, n, k));
         } else if (threadIdx.x == 0) {
-            spline_intervals(L, n, iv);
-        }
-        __syncthreads();
-        for (int k = threadIdx.x; k < n; k += (int)blockDim.x) {
-            double v;
-            if (L == 1) {
-                v = x[0];
-            } else {
-                v = spline_eval_at(x, b, c, d, iv[k], seq_point(L, n, k));
+            int i = 0;  // spline_eval's walk, point by point
+            for (int k = 0; k < n; ++k) {
+                const double u = seq_point(L, n, k);
+                if (u < (double)(i + 1) || (i < L - 1 && (double)(i + 2) < u)) i = spline_bisect(L, u);
+                put(k, i);
             }
-            y[k] = v < 0 ? 0.0 : v;
         }
     } else if (mode == 3) {  // neighborhood fill (util.R:53-69), from the pre-fill vector
         const int32_t* pos = nb_pos;
@@ -206,25 +189,25 @@ __device__ void interp_finish(int mode, int L, int n, double* x, const int32_t* 
         for (int i = threadIdx.x; i < L - 4; i += (int)blockDim.x) pre[pos[i] - 1] = x[2 + i];
         __syncthreads();
         for (int z = threadIdx.x; z < n; z += (int)blockDim.x) {
+            double v;
             if (!isnan(pre[z])) {
-                y[z] = pre[z];
-                continue;
+                v = pre[z];
+            } else {
+                double sm = 0.0;
+                int m = 0;
+                const int nb[4] = {z - 2, z - 1, z + 1, z + 2};
+                for (int q = 0; q < 4; ++q)
+                    if (nb[q] >= 0 && nb[q] < n && !isnan(pre[nb[q]])) {
+                        sm += pre[nb[q]];
+                        ++m;
+                    }
+                v = m ? sm / m : __builtin_nan("");
             }
-            double sm = 0.0;
-            int m = 0;
-            const int nb[4] = {z - 2, z - 1, z + 1, z + 2};
-            for (int q = 0; q < 4; ++q)
-                if (nb[q] >= 0 && nb[q] < n && !isnan(pre[nb[q]])) {
-                    sm += pre[nb[q]];
-                    ++m;
-                }
-            y[z] = m ? sm / m : __builtin_nan("");
+            out[(size_t)z * ld] = v;
         }
     } else {  // "linear": the switch arm is spelled "inear" -> x unchanged; rbind recycles
-        for (int i = threadIdx.x; i < n; i += (int)blockDim.x) y[i] = x[i % L];
+        for (int i = threadIdx.x; i < n; i += (int)blockDim.x) out[(size_t)i * ld] = x[i % L];
     }
-    __syncthreads();
-    for (int k = threadIdx.x; k < n; k += blockDim.x) out[(size_t)k * ld] = y[k];
 }
 
 }  // namespace

@@ -174,3 +174,17 @@ def test_preprocess_sampleto_on_bam_fixtures():
     ds = ra.preprocessRanges([{"id": "a", "file": bams[0]}, {"id": "b", "file": bams[1]}],
                              {"normalize": "downsample"})
     assert [len(s["ranges"]) for s in ds] == [50000, 50000]
+
+
+def test_product_rng_matches_independent_python_restatement():
+    """The library's R RNG (recoup_amd/csrc/rcp_rng.h) against tests/rrng.py (pure Python, written
+    from R's RNG.c / random.c, independent of both C copies): sort(sample(n, k)) streams continued
+    across calls, both sample.kind values, and the n > 1e7 hash variant."""
+    from tests.rrng import RRng
+    for kind in ("Rejection", "Rounding"):
+        for seed in (42, 3, 99991):
+            g, py = ra.RRng(seed, kind), RRng(seed, kind)
+            for n, k in [(50_000, 700), (1234, 1234), (99, 3), (70_000, 5)]:
+                np.testing.assert_array_equal(g.sample_sorted(n, k), np.sort(py.sample_int(n, k)))
+    g, py = ra.RRng(11), RRng(11)
+    np.testing.assert_array_equal(g.sample_sorted(20_000_001, 50), np.sort(py.sample_int(20_000_001, 50)))

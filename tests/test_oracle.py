@@ -282,3 +282,34 @@ def test_spline_fmm_reproduces_cubics():
 def test_split_vector_neighborhood_too_short_errors():
     with pytest.raises(ValueError):
         o.split_vector(np.ones(3), 4, "neighborhood", "mean")
+
+
+# ----------------------------------------------------------------------------- R RNG, independent
+@pytest.mark.parametrize("kind", ["Rejection", "Rounding"])
+def test_rng_matches_independent_python_restatement(kind):
+    """The oracle's C R-RNG (rcp_oracle.c) against tests/rrng.py, a pure-Python restatement of
+    R's set.seed / MT19937 / unif_rand / sample.int written from R's RNG.c and random.c alone:
+    the same draws for many seeds and sizes -- one and two 16-bit chunks per index (n above
+    65536), powers of two, whole permutations, and several calls continuing one stream."""
+    from tests.rrng import RRng
+    for seed in (42, 1, 7, 123456, 2 ** 31 - 1, -5):
+        py = RRng(seed, kind)
+        o.set_seed(seed)
+        np.testing.assert_array_equal(o.runif(5), py.runif(5))
+        for n, k in [(10, 10), (200, 37), (4096, 4096), (4097, 150), (65536, 300), (65537, 300),
+                     (1_000_003, 500), (3, 1), (1, 1)]:
+            np.testing.assert_array_equal(o.sample_int(n, k, kind), py.sample_int(n, k), err_msg=f"{seed} {n} {k}")
+
+
+def test_split_vector_layout_against_independent_rng():
+    """splitVector's enlarged bins (R/util.R:74-80) from the independent RNG: the oracle's bins of
+    (L, n) are floor(L / n) + 1 wide exactly on sample(1:n, L %% n) after set.seed(42)."""
+    from tests.rrng import RRng
+    for L, n in [(4000, 150), (29594, 150), (1001, 7), (523, 50), (2049, 1000)]:
+        x = np.arange(L, dtype=np.float64)
+        sizes = np.full(n, L // n)
+        add = RRng(42).sample_int(n, L - (L // n) * n)
+        sizes[np.array(add, dtype=np.int64) - 1] += 1
+        cuts = np.concatenate([[0], np.cumsum(sizes)])
+        exp = np.array([x[a:b].mean() for a, b in zip(cuts[:-1], cuts[1:])])
+        np.testing.assert_allclose(o.split_vector(x, n, "auto", "mean", "Rejection"), exp, rtol=1e-15)

@@ -373,3 +373,41 @@ def test_output_leading_dimension(gpu, kernel, n_bins, stat):
         assert np.array_equal(got.view(np.uint64), ref[0].view(np.uint64))
         np.testing.assert_array_equal(valid.cpu().numpy().astype(bool), ref[1])
         assert bool(torch.all(out[:, 333:] == -7.0))
+
+
+@pytest.mark.parametrize("ignore_strand", [True, False])
+def test_coordinates_near_int32_max(gpu, ignore_strand):
+    """A chromosome of 2,147,483,000 bp (just under the int32 coordinate limit the C ABI
+    states): reads and rows at its far end, a row ending on its last base (valid), one running
+    past it (NULL, coverage.R:217-222), a hot spot taking the heavy path, a second small
+    chromosome; lean (2-bp bins), general (40 bins) and per-base plans, merged and stranded
+    read layouts, known and NA seqlengths -- all against the oracle."""
+    from recoup_amd.engine import Bins, RowTable
+    rng = np.random.default_rng(47)
+    L0 = 2_147_483_000
+    n0, n1, nh = 60_000, 20_000, 20_000
+    s0 = rng.integers(L0 - 1_000_000, L0 - 179, n0)
+    sh = rng.integers(L0 - 500_000, L0 - 499_000, nh)             # hot spot: heavy rows
+    s1 = rng.integers(1, 99_000, n1)
+    start = np.concatenate([s0, sh, s1]).astype(np.int64)
+    width = rng.integers(20, 181, start.size)
+    end = np.minimum(start + width - 1, np.where(np.arange(start.size) < n0 + nh, L0, 100_000))
+    chrom = np.concatenate([np.zeros(n0 + nh, np.int32), np.ones(n1, np.int32)])
+    strand = rng.integers(0, 3, start.size).astype(np.int8)
+    reads = (chrom, start.astype(np.int32), end.astype(np.int32), strand)
+    R = 300
+    rc = np.zeros(R, np.int32)
+    rs_ = rng.integers(L0 - 990_000, L0 - 2000, R).astype(np.int64)
+    rs_[:8] = L0 - 500_800 + 100 * np.arange(8)                    # on the hot spot
+    rs_[8] = L0 - 1999                                             # ends on the last base
+    rs_[9] = L0 - 1500                                             # runs past the chromosome
+    rc[10:20] = 1
+    rs_[10:20] = rng.integers(1, 97_000, 10)
+    st = rng.integers(0, 3, R).astype(np.int8)
+    rows = RowTable.from_ranges(rc, rs_, rs_ + 1999, st, ignore_strand=ignore_strand)
+    for seqlen in (np.array([L0, 100_000], np.int64), np.array([-1, -1], np.int64)):
+        for bins in (Bins([("whole", 1000)]), Bins([("whole", 40)]), Bins([("whole", 0, 2000)])):
+            res, exp = run_case(reads, seqlen, rows, bins, heavy_threshold=64)
+            check(res, exp)
+            if seqlen[0] > 0:
+                assert res[1][8] and not res[1][9]

@@ -70,7 +70,12 @@ calcCoverage <- function(input, mask, strand = NULL, ignore.strand = TRUE, rc = 
     if (is.character(input) && file.exists(input)) {
         if (length(grep("\\.bam$", input, ignore.case = TRUE, perl = TRUE)) == 0)
             stop("recoup_amd reads BAM files; BigWig input is not on the GPU path")
+        # coverageFromBam (R/coverage.R:228-295): every mapped alignment overlapping the region
+        # ("keep" spans); calcCoverage skips the strand filter for a BAM (:141) and
+        # coverageFromBam never reads ignore.strand
         input <- .rcpReadBam(input)
+        strand <- NULL
+        ignore.strand <- TRUE
     }
     if (!is(input, "GRanges"))
         stop("The input argument must be a GenomicRanges object or a valid BAM file")

@@ -17,6 +17,9 @@ vectors are only materialised when asked for (``.to_list()``), because profileMa
 coverage and binning in one pass over the reads (no per-base vector ever reaches HBM).
 Every call runs on the GPU through librecoup_amd.so; there is no CPU path.
 """
+import os
+import re
+
 import numpy as np
 import torch
 
@@ -194,9 +197,42 @@ class DeviceCoverage:
 
 
 # ------------------------------------------------------------------------------ coverage
+def _bam_reads(path):
+    """calcCoverage's file input (R/coverage.R:127-140): a BAM path is read by coverageFromBam
+    (:228-295), one region at a time, as every mapped alignment overlapping it
+    (``ScanBamParam(which=)``, spliceAction "keep": the alignment's reference span).  Reading
+    the whole file once (readBam, "keep") and locating each region's reads on the GPU gives
+    the same reads per region; the BAM header's lengths are the seqlengths."""
+    path = os.fspath(path)
+    if not os.path.exists(path):
+        raise ValueError("The input argument must be a GenomicRanges object or a valid BAM/BigWig file "
+                         "or a list of GenomicRanges")
+    if re.search(r"\.bam$", path, re.IGNORECASE) is None:
+        if re.search(r"\.(bigwig|bw|wig|bg)$", path, re.IGNORECASE):
+            raise _lib.UnsupportedError(-4, "BigWig input (coverageFromBigWig) is not on the GPU path")
+        raise ValueError("The input argument must be a GenomicRanges object or a valid BAM/BigWig file "
+                         "or a list of GenomicRanges")
+    return readBam(path, "keep")
+
+
+def _sample_reads(s, strand, ignore_strand):
+    """A sample's reads for coverageRef / coverageRnaRef: ``ranges`` when present, else its
+    ``file`` -- the reference passes ``input[[n]]$file`` to calcCoverage (coverage.R:35-39,
+    58-62, 93-96), whose BAM branch skips the strand filter (:141) and never reads
+    ``ignore.strand`` (coverageFromBam takes every overlapping alignment)."""
+    if s.get("ranges") is not None:
+        return s["ranges"], strand, ignore_strand
+    if s.get("file") is not None:
+        return _bam_reads(s["file"]), None, True
+    raise ValueError(f"sample {s.get('id')!r} has neither ranges nor a file")
+
+
 def calcCoverage(input, mask, strand=None, ignore_strand=True, device=None, rc=None, rle=False):
     """R/coverage.R:126-174: one coverage vector per mask element (None = R's NULL); with
-    ``rle`` the elements are ``Rle`` objects, the form the reference returns."""
+    ``rle`` the elements are ``Rle`` objects, the form the reference returns.  ``input`` may
+    also be a BAM file path (coverageFromBam semantics: no strand filter, strand ignored)."""
+    if isinstance(input, (str, os.PathLike)):
+        input, strand, ignore_strand = _bam_reads(input), None, True
     dev = _device(device)
     rs, levels = _readset(input, dev, strand)
     rows = _rows_from_mask(mask, levels, ignore_strand)
@@ -223,8 +259,9 @@ def coverageRef(input, genomeRanges, region="tss", flank=(2000, 2000), strandedP
     strand, ign = _strand_params(strandedParams)
     dev = _device(device)
     for s in input:
-        rs, levels = _readset(s["ranges"], dev, strand)
-        s["coverage"] = DeviceCoverage(rs, _rows_from_mask(main, levels, ign), genomeRanges.names)
+        reads, st, ig = _sample_reads(s, strand, ign)
+        rs, levels = _readset(reads, dev, st)
+        s["coverage"] = DeviceCoverage(rs, _rows_from_mask(main, levels, ig), genomeRanges.names)
     return input
 
 
@@ -269,8 +306,9 @@ def coverageRnaRef(input, genomeRanges, helperRanges, flank=(2000, 2000), strand
     strand, ign = _strand_params(strandedParams)
     dev = _device(device)
     for s in input:
-        rs, levels = _readset(s["ranges"], dev, strand)
-        s["coverage"] = DeviceCoverage(rs, _rna_rows(genomeRanges, helperRanges, flank, levels, ign),
+        reads, st, ig = _sample_reads(s, strand, ign)
+        rs, levels = _readset(reads, dev, st)
+        s["coverage"] = DeviceCoverage(rs, _rna_rows(genomeRanges, helperRanges, flank, levels, ig),
                                        genomeRanges.names)
     return input
 

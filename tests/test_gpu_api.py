@@ -231,3 +231,41 @@ def test_bam_ingest_to_profile(c1):
         ref, rv = o.profile_part(ix, mask, 100)
         np.testing.assert_allclose(s["profile"], ref, rtol=1e-12, atol=0)
         assert s["profile"].sum() > 0
+
+
+def test_bam_path_input(c1):
+    """calcCoverage / coverageRef / coverageRnaRef with a BAM path (R/coverage.R:127-140,
+    35-39, 93-96 -> coverageFromBam, :228-295): every mapped alignment overlapping a region,
+    strand filter skipped and ignore.strand unused -- the same lists as the readBam reads with
+    no filter and strands ignored, whatever strand arguments are passed; the oracle agrees."""
+    bam = os.path.join(os.path.dirname(__file__), "golden", "bam", "WT_H4K20me1_50kr.bam")
+    reads = ra.readBam(bam)
+    win = ra.getRegionalRanges(c1["genome"], "tss", FLANK)
+    got = ra.calcCoverage(bam, win, strand="+", ignore_strand=False)
+    ref = ra.calcCoverage(reads, win)
+    ix = o.Index(reads.seqcodes, reads.start, reads.end, reads.strand, reads.seqlengths)
+    mask = o.Mask.from_ranges(win.codes_in(reads.seqlevels), win.start, win.end, win.strand)
+    exp = o.coverage(ix, mask, ignore_strand=True)
+    assert len(got) == len(ref) == len(exp) == len(win)
+    n_valid = 0
+    for g, r, e in zip(got, ref, exp):
+        assert (g is None) == (r is None) == (e is None)
+        if g is not None:
+            np.testing.assert_array_equal(g, r)
+            np.testing.assert_array_equal(g, e)
+            n_valid += 1
+    assert n_valid > 0
+    # coverageRef / coverageRnaRef on samples that carry only the file
+    inp = ra.coverageRef([{"id": "s0", "name": "WT", "file": bam}], c1["genome"], "tss", FLANK,
+                         strandedParams={"strand": "-", "ignoreStrand": False})
+    inp = ra.profileMatrix(inp, FLANK, {"flankBinSize": 0, "regionBinSize": 100})
+    ref_p, _ = o.profile_part(ix, mask, 100)
+    np.testing.assert_allclose(inp[0]["profile"], ref_p, rtol=1e-12, atol=0)
+    rna_f = ra.coverageRnaRef([{"id": "s0", "name": "WT", "file": bam}], c1["exons"], c1["genome"], FLANK)
+    rna_r = ra.coverageRnaRef([{"id": "s0", "name": "WT", "ranges": reads}], c1["exons"], c1["genome"], FLANK)
+    for g, r in zip(rna_f[0]["coverage"].to_list(), rna_r[0]["coverage"].to_list()):
+        assert (g is None) == (r is None)
+        if g is not None:
+            np.testing.assert_array_equal(g, r)
+    with pytest.raises(ValueError):
+        ra.calcCoverage(os.path.join(os.path.dirname(__file__), "golden", "nope.bam"), win)

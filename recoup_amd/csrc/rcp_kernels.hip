@@ -654,6 +654,7 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
 #ifndef RCP_CEDGE_DIR
 #define RCP_CEDGE_DIR 0
 #endif
+
 __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres)[2 * RCP_MAX_CRANGE_CHUNKS]) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
     constexpr int KS = 4;                  // searches of one lockstep round
@@ -869,7 +870,7 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
             }
             P.seg_lo[j * 3 + s] = lo;
             P.seg_hi[j * 3 + s] = hi;
-            // (merged layout: the entries of streams 1, 2 -- and their crange words -- stay as
+            // (merged layout: the entries of streams 1, 2 stay as
             // the plan zeroed them; no read lives there)
         }
     }
@@ -941,7 +942,9 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
             } else if (empty) {
                 chi = clo;
             }
-            P.crange[((size_t)r * nc + c) * 3] = make_uint2(clo, chi);
+            // merged layout: one stream, so dense (row, chunk) words -- a wave's writes are
+            // whole lines (stride 3, as the stranded layout below, measured ~1 us slower on C4)
+            P.crange[(size_t)r * nc + c] = make_uint2(clo, chi);
         }
     } else if (cr && q < 3) {
         // stranded layout: lane q refines its own stream's range chunk by chunk
@@ -1361,11 +1364,18 @@ __device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart
                     const bool refine = !full && all > 4096;
                     if (rec.flags & RCP_REC_CRANGE) {
                         // exact ranges for this chunk from the locate kernel
-                        const uint2* cr = P.crange + ((size_t)r * P.n_chunks_total + cidx) * 3;
-                        for (int s = 0; s < 3; ++s) {
-                            const uint2 v = cr[s];
-                            m.lo[s] = v.x;
-                            m.hi[s] = v.y;
+                        if (P.merged) {  // one stream: dense (row, chunk) words
+                            const uint2 v = P.crange[(size_t)r * P.n_chunks_total + cidx];
+                            m.lo[0] = v.x;
+                            m.hi[0] = v.y;
+                            m.lo[1] = m.hi[1] = m.lo[2] = m.hi[2] = 0;
+                        } else {
+                            const uint2* cr = P.crange + ((size_t)r * P.n_chunks_total + cidx) * 3;
+                            for (int s = 0; s < 3; ++s) {
+                                const uint2 v = cr[s];
+                                m.lo[s] = v.x;
+                                m.hi[s] = v.y;
+                            }
                         }
                     } else
                     for (int s = 0; s < 3; ++s) {

@@ -447,7 +447,9 @@ def end_to_end(reads, seqlen, rows, bins, local, units, reps=3):
     memory, already touched as R's allocMatrix result is).  Two input forms:
       * "sorted_runs" -- what R holds for a coordinate-sorted BAM (readGAlignments keeps file
         order, R/ranges.R:111-132): reads in (chromosome, start) order, seqnames as the runs of
-        its Rle (the shim passes runValue / runLength) -- the headline e2e;
+        its Rle (the shim passes runValue / runLength) and the widths as runs of Rle(width(x))
+        when they are few (r/R/rcp.R: at most one run per 4 reads, else the end vector) --
+        the headline e2e;
       * "any_order" -- the same reads in generation order, one chromosome code per read.
     `reps` calls each; `ms` is the median call, `first_call_ms` the first (it also pays the
     pinned staging buffers and the first big device allocations).  Reported beside `value`,
@@ -457,12 +459,17 @@ def end_to_end(reads, seqlen, rows, bins, local, units, reps=3):
     order = torch.argsort((chrom.to(torch.int64) << 32) | start.to(torch.int64))
     sc = chrom[order]
     rv, rl = torch.unique_consecutive(sc, return_counts=True)
+    sw = (end[order] - start[order] + 1).to(torch.int32)
+    wv, wl = torch.unique_consecutive(sw, return_counts=True)
+    ends = ((wv.cpu().numpy(), wl.to(torch.int64).cpu().numpy()) if wv.numel() <= sw.numel() // 4
+            else end[order].cpu().numpy())
     forms = {
-        "sorted_runs": [(rv.to(torch.int32).cpu().numpy(), rl.to(torch.int64).cpu().numpy())]
-                       + [x[order].cpu().numpy() for x in (start, end, strand)],
+        "sorted_runs": [(rv.to(torch.int32).cpu().numpy(), rl.to(torch.int64).cpu().numpy()),
+                        start[order].cpu().numpy(), ends, strand[order].cpu().numpy()],
         "any_order": [x.cpu().numpy() for x in reads],
     }
-    del order, sc
+    n_wruns = int(wv.numel()) if isinstance(ends, tuple) else None
+    del order, sc, sw, wv, wl
     out = np.zeros((bins.n_cols, rows.n_rows))  # R's matrix: allocated + touched before the call
     valid = np.zeros(max(rows.n_rows, 1), np.uint8)
     res = {}
@@ -483,8 +490,10 @@ def end_to_end(reads, seqlen, rows, bins, local, units, reps=3):
                      "first_call_ms": calls[0][0], "calls_ms": [round(c[0], 2) for c in calls]}
     e2e = dict(res["sorted_runs"])
     e2e["any_order"] = res["any_order"]
+    e2e["width_runs"] = n_wruns
     e2e["note"] = ("C ABI: rcp_readset_create from host arrays + rcp_profile into a host matrix; PCIe both ways; "
-                   "reads coordinate-sorted with seqnames runs (a sorted BAM); any_order: unsorted, one code per read")
+                   "reads coordinate-sorted with seqnames runs (a sorted BAM) and width runs when few "
+                   "(width_runs: their count; null = per-read ends); any_order: unsorted, one code and one end per read")
     return e2e
 
 

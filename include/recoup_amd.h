@@ -87,6 +87,13 @@ typedef struct {
     int32_t n_chrom_runs;
     const int32_t* chrom_run_value;   /* [n_chrom_runs] chromosome code of each run          */
     const int64_t* chrom_run_length;  /* [n_chrom_runs] > 0, summing to n                    */
+    /* widths as runs (IRanges holds start and width; width(x) as an Rle), used when end is
+     * NULL: end = start + width - 1 is formed on the device, so reads of one length (a
+     * sequencing run's fixed read length) send no end vector over PCIe.  Host pointers in
+     * both modes. */
+    int32_t n_width_runs;
+    const int32_t* width_run_value;   /* [n_width_runs] >= 0                                  */
+    const int64_t* width_run_length;  /* [n_width_runs] > 0, summing to n                    */
 } rcp_reads_desc;
 
 /* Upload (or adopt device arrays), sort by (chrom, strand, start) on the GPU, and build

@@ -30,7 +30,11 @@
 .rcpReads <- function(input, strand = NULL, devices = .rcpDevices()) {
     lv <- seqlevels(input)
     sn <- seqnames(input)  # an Rle: its runs go to the GPU, not one code per read
-    args <- list(list(as.integer(runValue(sn)) - 1L, as.numeric(runLength(sn))), start(input), end(input),
+    # IRanges holds start and width: reads of a few lengths send width runs, not an end vector
+    w <- Rle(width(input))
+    ends <- if (nrun(w) <= length(input) %/% 4)
+        list(as.integer(runValue(w)), as.numeric(runLength(w))) else end(input)
+    args <- list(list(as.integer(runValue(sn)) - 1L, as.numeric(runLength(sn))), start(input), ends,
         .rcpStrandCode(strand(input)), as.numeric(seqlengths(input)[lv]),
         if (is.null(strand)) -1L else .rcpStrandCode(strand))
     if (length(devices) > 1)

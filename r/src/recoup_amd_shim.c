@@ -69,7 +69,19 @@ static rcp_reads_desc reads_of(SEXP chrom, SEXP start, SEXP end, SEXP strand, SE
         d.chrom = INTEGER(chrom);
     }
     d.start = INTEGER(start);
-    d.end = INTEGER(end);
+    if (TYPEOF(end) == VECSXP) {
+        /* list(runValue, runLength) of width(reads): end = start + width - 1 formed on the GPU */
+        SEXP wv = VECTOR_ELT(end, 0), wl = VECTOR_ELT(end, 1);
+        int nw = LENGTH(wv);
+        int64_t* wlen = (int64_t*)R_alloc(nw > 0 ? nw : 1, sizeof(int64_t));
+        for (int k = 0; k < nw; ++k) wlen[k] = (int64_t)REAL(wl)[k];
+        d.end = NULL;
+        d.n_width_runs = nw;
+        d.width_run_value = INTEGER(wv);
+        d.width_run_length = wlen;
+    } else {
+        d.end = INTEGER(end);
+    }
     d.strand = st;
     d.n_chrom = nchr;
     d.seqlen = sl;
@@ -81,7 +93,8 @@ static rcp_reads_desc reads_of(SEXP chrom, SEXP start, SEXP end, SEXP strand, SE
 
 /* .Call("rcp_R_readset", chromCode, start, end, strandCode, seqlengths, strandFilter, device)
  * chromCode: 0-based seqlevel index per read, or list(runValue - 1L, as.numeric(runLength)) of
- * the seqnames Rle; strandCode 0 '+', 1 '-', 2 '*'; seqlengths numeric (NA ok) */
+ * the seqnames Rle; end: per read, or list(runValue, as.numeric(runLength)) of the width Rle;
+ * strandCode 0 '+', 1 '-', 2 '*'; seqlengths numeric (NA ok) */
 SEXP rcp_R_readset(SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP seqlen, SEXP sfilter, SEXP dev) {
     rcp_reads_desc d = reads_of(chrom, start, end, strand, seqlen, sfilter);
     d.device = asInteger(dev);

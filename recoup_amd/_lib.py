@@ -45,7 +45,8 @@ class ReadsDesc(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("chrom", _vp), ("start", _vp), ("end", _vp), ("strand", _vp),
                 ("n_chrom", ctypes.c_int32), ("seqlen", _i64p), ("device", ctypes.c_int32),
                 ("on_device", ctypes.c_int32), ("strand_filter", ctypes.c_int32), ("n_chrom_runs", ctypes.c_int32),
-                ("chrom_run_value", _i32p), ("chrom_run_length", _i64p)]
+                ("chrom_run_value", _i32p), ("chrom_run_length", _i64p), ("n_width_runs", ctypes.c_int32),
+                ("width_run_value", _i32p), ("width_run_length", _i64p)]
 
 
 class RowsDesc(ctypes.Structure):

@@ -10,11 +10,14 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdint>
 #include <cstring>
 #include <exception>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <new>
+#include <set>
 #include <string>
 #include <thread>
 #include <utility>
@@ -43,6 +46,7 @@ extern "C" {
 hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
                           int32_t* vout, int64_t n, int begin_bit, int end_bit, hipStream_t stream);
 hipError_t rcp_launch_unsorted(int64_t n, const uint64_t* keys, uint32_t* flag, hipStream_t stream);
+hipError_t rcp_launch_width_end(int64_t n, const int32_t* start, int32_t* width_end, hipStream_t stream);
 hipError_t rcp_launch_expand_runs(int64_t n, int32_t n_runs, const int64_t* run_start, const int32_t* run_value,
                                   int32_t* out, hipStream_t stream);
 hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
@@ -176,6 +180,54 @@ struct DevBuf {
     }
 };
 
+// Stream-ordered temporaries from the device's default memory pool, which keeps freed memory
+// mapped (release threshold raised once per device): the multi-GB sort and scan buffers of a
+// readset build cost a hipMalloc / hipFree pair each, and on the box those took 0.3-6 s now
+// and then (C5, 500 M reads: a 0.19 s build became 1.4 s and 7.4 s, tools/diag_readset.py);
+// from the pool the same memory is handed out again.  Allocated and freed on the stream that
+// uses it, so the reuse is ordered after the last kernel touching it.
+hipError_t keep_pool_mapped() {
+    static std::mutex mu;
+    static std::set<int> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count(dev)) return hipSuccess;
+    hipMemPool_t pool;
+    e = hipDeviceGetDefaultMemPool(&pool, dev);
+    if (e != hipSuccess) return e;
+    uint64_t thr = UINT64_MAX;
+    e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    if (e == hipSuccess) done.insert(dev);
+    return e;
+}
+
+struct PoolBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipStream_t s;
+    explicit PoolBuf(hipStream_t st) : s(st) {}
+    PoolBuf(const PoolBuf&) = delete;
+    PoolBuf& operator=(const PoolBuf&) = delete;
+    ~PoolBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFreeAsync(p, s);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t alloc(size_t n) {
+        reset();
+        bytes = n;
+        if (n == 0) return hipSuccess;
+        return hipMallocAsync(&p, n, s);
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
 // Switch to a device for the scope of an API call, restoring the caller's device.
 struct DeviceGuard {
     int prev = -1;
@@ -207,11 +259,39 @@ int check_device(int dev) {
 // `stranded` (stream c*3 + strand, for findOverlaps with strand compatibility) and `merged`
 // (all strands in stream c*3, streams c*3+1, c*3+2 empty: ignore.strand = TRUE, the default),
 // so the default path searches and streams one range per segment instead of three.
+// A readset's own arrays, from the same pool (a 4 GB hipMalloc of C5's packed reads once took
+// 5.9 s on the box, tools/diag_readset.py with -DRCP_PLAN_TIMING=1), allocated on the build
+// stream and released after a device synchronisation -- what hipFree did implicitly, so a
+// readset destroyed with work still queued on it stays safe -- back into the pool.
+struct PoolArr {
+    void* p = nullptr;
+    size_t bytes = 0;
+    PoolArr() = default;
+    PoolArr(const PoolArr&) = delete;
+    PoolArr& operator=(const PoolArr&) = delete;
+    ~PoolArr() {
+        if (p) {
+            (void)hipDeviceSynchronize();
+            (void)hipFreeAsync(p, nullptr);
+        }
+    }
+    hipError_t alloc(size_t n, hipStream_t s) {
+        if (p) return hipErrorInvalidValue;  // allocated once
+        bytes = n;
+        if (n == 0) return hipSuccess;
+        return hipMallocAsync(&p, n, s);
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
 struct ReadLayout {
     std::vector<int64_t> h_stream_off;  // n_chrom*3 + 1
     std::vector<int64_t> h_dir_off;     // n_chrom*3 + 1
-    DevBuf se, pmax, stream_off;
-    DevBuf dir_l, dir_u, dir_off;
+    PoolArr se, pmax, stream_off;
+    PoolArr dir_l, dir_off;
     int32_t dir_shift = 12;
 };
 
@@ -271,7 +351,8 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
 #if RCP_PLAN_TIMING
     PlanTimer ltimer;
 #endif
-    DevBuf keys, keys2, vals, vals2, scan_in, scan_out, temp;
+    HIP_TRY(keep_pool_mapped());
+    PoolBuf keys(s), keys2(s), vals(s), vals2(s), scan_in(s), scan_out(s), temp(s);
     HIP_TRY(keys.alloc(8 * std::max<int64_t>(n, 1)));
     HIP_TRY(keys2.alloc(8 * std::max<int64_t>(n, 1)));
     HIP_TRY(vals.alloc(4 * std::max<int64_t>(n, 1)));
@@ -285,7 +366,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     if (merge && n > 1) {
         // keys are (stream, start): non-decreasing <=> (chromosome, start) order, no dropped read
         // (the sentinel stream) before a kept one
-        DevBuf flag;
+        PoolBuf flag(s);
         HIP_TRY(flag.alloc(4));
         HIP_TRY(hipMemsetAsync(flag.p, 0, 4, s));
         HIP_TRY(rcp_launch_unsorted(n, keys.as<uint64_t>(), flag.as<uint32_t>(), s));
@@ -313,8 +394,8 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     }
     keys.reset();
     vals.reset();
-    HIP_TRY(L->stream_off.alloc(8 * (n_streams + 2)));
-    HIP_TRY(L->se.alloc(8 * std::max<int64_t>(n, 1)));
+    HIP_TRY(L->stream_off.alloc(8 * (n_streams + 2), s));
+    HIP_TRY(L->se.alloc(8 * std::max<int64_t>(n, 1), s));
     HIP_TRY(scan_in.alloc(8 * std::max<int64_t>(n, 1)));
     HIP_TRY(rcp_launch_streams(n, keys2.as<uint64_t>(), vals2.as<int32_t>(), L->stream_off.as<int64_t>(),
                                n_streams + 2, L->se.as<int2>(), scan_in.as<uint64_t>(), s));
@@ -328,7 +409,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
         if (tb2 > temp.bytes) HIP_TRY(temp.alloc(tb2));
         HIP_TRY(rcp_segmax_scan(temp.p, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
     }
-    HIP_TRY(L->pmax.alloc(4 * std::max<int64_t>(n, 1)));
+    HIP_TRY(L->pmax.alloc(4 * std::max<int64_t>(n, 1), s));
     HIP_TRY(rcp_launch_unpack_pmax(n, scan_out.as<uint64_t>(), L->pmax.as<int32_t>(), s));
     LAYOUT_MARK("  pmax scan");
     scan_in.reset();
@@ -338,7 +419,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     L->h_stream_off.resize(n_streams + 2);
     HIP_TRY(hipMemcpyAsync(L->h_stream_off.data(), L->stream_off.p, 8 * (n_streams + 2), hipMemcpyDeviceToHost, s));
     // ---- bucket directory: ~32 reads of a stream per bucket on average
-    DevBuf maxend;
+    PoolBuf maxend(s);
     HIP_TRY(maxend.alloc(4 * std::max<int64_t>(n_streams, 1)));
     HIP_TRY(rcp_launch_stream_maxend(n_streams, L->stream_off.as<int64_t>(), L->pmax.as<int32_t>(),
                                      maxend.as<int32_t>(), s));
@@ -369,8 +450,8 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
         }
     }
     const int64_t ne = doff[n_streams];
-    HIP_TRY(L->dir_off.alloc(8 * (n_streams + 1)));
-    HIP_TRY(L->dir_l.alloc(8 * std::max<int64_t>(ne, 1)));  // interleaved (l, u) per entry
+    HIP_TRY(L->dir_off.alloc(8 * (n_streams + 1), s));
+    HIP_TRY(L->dir_l.alloc(8 * std::max<int64_t>(ne, 1), s));  // interleaved (l, u) per entry
     HIP_TRY(hipMemcpyAsync(L->dir_off.p, doff.data(), 8 * (n_streams + 1), hipMemcpyHostToDevice, s));
     L->h_dir_off = doff;
     HIP_TRY(rcp_launch_dir(ne, n_streams, L->dir_off.as<int64_t>(), L->stream_off.as<int64_t>(),
@@ -392,7 +473,7 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     if (rc) return rc;
     if (d->n < 0 || d->n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "read count %lld outside [0, 2^31)", (long long)d->n);
     if (d->n_chrom <= 0 || d->n_chrom > (1 << 20)) return fail(RCP_EINVAL, "n_chrom = %d", d->n_chrom);
-    if (d->n > 0 && (!d->start || !d->end || !d->strand)) return fail(RCP_EINVAL, "NULL read array");
+    if (d->n > 0 && (!d->start || !d->strand)) return fail(RCP_EINVAL, "NULL read array");
     if (d->n > 0 && !d->chrom) {
         if (d->n_chrom_runs <= 0 || !d->chrom_run_value || !d->chrom_run_length)
             return fail(RCP_EINVAL, "chrom is NULL and no chromosome runs are given");
@@ -403,6 +484,19 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
             tot += d->chrom_run_length[k];
         }
         if (tot != d->n) return fail(RCP_EINVAL, "chromosome runs cover %lld reads, not %lld", (long long)tot,
+                                     (long long)d->n);
+    }
+    if (d->n > 0 && !d->end) {
+        if (d->n_width_runs <= 0 || !d->width_run_value || !d->width_run_length)
+            return fail(RCP_EINVAL, "end is NULL and no width runs are given");
+        int64_t tot = 0;
+        for (int32_t k = 0; k < d->n_width_runs; ++k) {
+            if (d->width_run_length[k] <= 0) return fail(RCP_EINVAL, "width run %d has length %lld", k,
+                                                         (long long)d->width_run_length[k]);
+            if (d->width_run_value[k] < 0) return fail(RCP_EINVAL, "width run %d has width %d", k, d->width_run_value[k]);
+            tot += d->width_run_length[k];
+        }
+        if (tot != d->n) return fail(RCP_EINVAL, "width runs cover %lld reads, not %lld", (long long)tot,
                                      (long long)d->n);
     }
     if (d->strand_filter < -1 || d->strand_filter > 2) return fail(RCP_EINVAL, "strand_filter = %d", d->strand_filter);
@@ -421,7 +515,7 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
 #endif
 
     // inputs on device
-    DevBuf in_chrom, in_start, in_end, in_strand, runs;
+    DevBuf in_chrom, in_start, in_end, in_strand, runs, wruns;
     const int32_t *pc = d->chrom, *ps = d->start, *pe = d->end;
     const int8_t* pst = d->strand;
     if (!d->chrom && n > 0) {
@@ -440,17 +534,31 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     if (!d->on_device && n > 0) {
         if (d->chrom) HIP_TRY(in_chrom.alloc(4 * n));
         HIP_TRY(in_start.alloc(4 * n));
-        HIP_TRY(in_end.alloc(4 * n));
+        if (d->end) HIP_TRY(in_end.alloc(4 * n));
         HIP_TRY(in_strand.alloc(n));
         // caller-owned pageable arrays (R vectors): pinned double-buffered staging (rcp_stage.h)
         if (d->chrom) HIP_TRY(rcp::stage_h2d(in_chrom.p, d->chrom, 4 * n, d->device, s));
         HIP_TRY(rcp::stage_h2d(in_start.p, d->start, 4 * n, d->device, s));
-        HIP_TRY(rcp::stage_h2d(in_end.p, d->end, 4 * n, d->device, s));
+        if (d->end) HIP_TRY(rcp::stage_h2d(in_end.p, d->end, 4 * n, d->device, s));
         HIP_TRY(rcp::stage_h2d(in_strand.p, d->strand, n, d->device, s));
         pc = in_chrom.as<int32_t>();
         ps = in_start.as<int32_t>();
-        pe = in_end.as<int32_t>();
+        if (d->end) pe = in_end.as<int32_t>();
         pst = in_strand.as<int8_t>();
+    }
+    if (!d->end && n > 0) {
+        // widths as runs: expanded on the device, end = start + width - 1 formed there
+        std::vector<int64_t> rstart(d->n_width_runs + 1, 0);
+        for (int32_t k = 0; k < d->n_width_runs; ++k) rstart[k + 1] = rstart[k] + d->width_run_length[k];
+        HIP_TRY(wruns.alloc(8 * rstart.size() + 4 * (size_t)d->n_width_runs));
+        HIP_TRY(hipMemcpyAsync(wruns.p, rstart.data(), 8 * rstart.size(), hipMemcpyHostToDevice, s));
+        int32_t* wv = reinterpret_cast<int32_t*>(wruns.as<char>() + 8 * rstart.size());
+        HIP_TRY(hipMemcpyAsync(wv, d->width_run_value, 4 * (size_t)d->n_width_runs, hipMemcpyHostToDevice, s));
+        HIP_TRY(in_end.alloc(4 * n));
+        HIP_TRY(rcp_launch_expand_runs(n, d->n_width_runs, wruns.as<int64_t>(), wv, in_end.as<int32_t>(), s));
+        HIP_TRY(rcp_launch_width_end(n, ps, in_end.as<int32_t>(), s));
+        HIP_TRY(hipStreamSynchronize(s));  // rstart is released on return
+        pe = in_end.as<int32_t>();
     }
     PLAN_MARK("reads H2D");
     bool presorted = false;

@@ -508,6 +508,12 @@ __global__ void rcp_unsorted_kernel(int64_t n, const uint64_t* __restrict__ keys
     if (i < n && keys[i] < keys[i - 1]) *flag = 1u;
 }
 
+// end = start + width - 1 in place over the expanded widths (IRanges: width >= 0, end fits int32)
+__global__ void rcp_width_end_kernel(int64_t n, const int32_t* __restrict__ start, int32_t* __restrict__ width_end) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) width_end[i] = start[i] + (width_end[i] - 1);
+}
+
 // chromosome code of read i from the seqnames runs (run_start: prefix sums, n_runs + 1 entries)
 __global__ void rcp_expand_runs_kernel(int64_t n, int32_t n_runs, const int64_t* __restrict__ run_start,
                                        const int32_t* __restrict__ run_value, int32_t* __restrict__ out) {
@@ -2779,6 +2785,13 @@ extern "C" hipError_t rcp_launch_unsorted(int64_t n, const uint64_t* keys, uint3
     if (n < 2) return hipSuccess;
     hipLaunchKernelGGL(rcp_unsorted_kernel, dim3((unsigned)((n - 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, n,
                        keys, flag);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rcp_launch_width_end(int64_t n, const int32_t* start, int32_t* width_end, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rcp_width_end_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, n,
+                       start, width_end);
     return hipGetLastError();
 }
 

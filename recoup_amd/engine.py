@@ -32,24 +32,30 @@ def _stream(device, stream):
 
 
 def _chrom_runs(chrom):
-    """(run_values int32, run_lengths int64) when ``chrom`` is given as seqnames runs, else None."""
+    """(run_values int32, run_lengths int64) when ``chrom`` (or ``end``) is given as the runs of
+    an R Rle (seqnames(x), width(x)), else None."""
     if isinstance(chrom, tuple) and len(chrom) == 2:
         v = np.ascontiguousarray(chrom[0], dtype=np.int32)
         n = np.ascontiguousarray(chrom[1], dtype=np.int64)
         if v.shape != n.shape:
-            raise ValueError("seqnames runs: values and lengths differ in length")
+            raise ValueError("runs: values and lengths differ in length")
         return v, n
     return None
 
 
-def _reads_desc(n, keep, runs, seql, device, on_dev, sf):
-    d = _lib.ReadsDesc(n, ptr(keep[0]) if keep[0] is not None else None, ptr(keep[1]), ptr(keep[2]), ptr(keep[3]),
+def _reads_desc(n, keep, runs, seql, device, on_dev, sf, wruns=None):
+    d = _lib.ReadsDesc(n, ptr(keep[0]) if keep[0] is not None else None, ptr(keep[1]),
+                       ptr(keep[2]) if keep[2] is not None else None, ptr(keep[3]),
                        len(seql), cptr(seql, _lib._i64p), device, on_dev, sf)
     if runs is not None:
         d.n_chrom_runs = len(runs[0])
         d.chrom_run_value = cptr(runs[0], _lib._i32p)
         d.chrom_run_length = cptr(runs[1], _lib._i64p)
-    d._keep = (keep, runs)  # the arrays outlive the call
+    if wruns is not None:
+        d.n_width_runs = len(wruns[0])
+        d.width_run_value = cptr(wruns[0], _lib._i32p)
+        d.width_run_length = cptr(wruns[1], _lib._i64p)
+    d._keep = (keep, runs, wruns)  # the arrays outlive the call
     return d
 
 
@@ -63,7 +69,9 @@ class ReadSet:
 
     def __init__(self, chrom, start, end, strand, seqlengths, device=0, strand_filter=None, stream=None):
         """``chrom`` is one code per read, or the runs of R's ``seqnames(x)`` Rle as a tuple
-        ``(run_values, run_lengths)`` (expanded on the GPU, never copied per read)."""
+        ``(run_values, run_lengths)`` (expanded on the GPU, never copied per read); likewise
+        ``end`` is one end per read, or the runs of ``width(x)`` as a tuple ``(run_values,
+        run_lengths)`` (end = start + width - 1 formed on the GPU)."""
         lib = _lib.lib()
         if _lib.device_count() == 0:
             raise _lib.RcpError(-6, "no GPU visible: recoup_amd runs only on the GPU")
@@ -71,18 +79,21 @@ class ReadSet:
         self.seqlengths = np.ascontiguousarray(seqlengths, dtype=np.int64)
         on_dev = isinstance(start, torch.Tensor)
         runs = _chrom_runs(chrom)
+        wruns = _chrom_runs(end)
         if on_dev:
-            keep = [None if runs else chrom.contiguous()] + [t.contiguous() for t in (start, end, strand)]
+            keep = ([None if runs else chrom.contiguous(), start.contiguous(), None if wruns else end.contiguous(),
+                     strand.contiguous()])
             for t, dt in zip(keep, (torch.int32, torch.int32, torch.int32, torch.int8)):
                 if t is not None and (t.dtype != dt or t.device.type != "cuda"):
                     raise TypeError("device reads must be int32/int32/int32/int8 CUDA tensors")
         else:
             keep = [None if runs else np.ascontiguousarray(chrom, dtype=np.int32),
-                    np.ascontiguousarray(start, dtype=np.int32), np.ascontiguousarray(end, dtype=np.int32),
+                    np.ascontiguousarray(start, dtype=np.int32),
+                    None if wruns else np.ascontiguousarray(end, dtype=np.int32),
                     np.ascontiguousarray(strand, dtype=np.int8)]
         n = int(keep[1].shape[0])
         sf = -1 if strand_filter is None else STRAND.get(strand_filter, strand_filter)
-        d = _reads_desc(n, keep, runs, self.seqlengths, self.device, int(on_dev), int(sf))
+        d = _reads_desc(n, keep, runs, self.seqlengths, self.device, int(on_dev), int(sf), wruns)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             check(lib.rcp_readset_create(ctypes.byref(d), _stream(self.device, stream), ctypes.byref(h)))
@@ -99,11 +110,13 @@ class ReadSet:
         lib = _lib.lib()
         seql = np.ascontiguousarray(seqlengths, dtype=np.int64)
         runs = _chrom_runs(chrom)
+        wruns = _chrom_runs(end)
         keep = [None if runs else np.ascontiguousarray(chrom, dtype=np.int32),
-                np.ascontiguousarray(start, dtype=np.int32), np.ascontiguousarray(end, dtype=np.int32),
+                np.ascontiguousarray(start, dtype=np.int32),
+                None if wruns else np.ascontiguousarray(end, dtype=np.int32),
                 np.ascontiguousarray(strand, dtype=np.int8)]
         sf = -1 if strand_filter is None else STRAND.get(strand_filter, strand_filter)
-        d = _reads_desc(int(keep[1].shape[0]), keep, runs, seql, 0, 0, int(sf))
+        d = _reads_desc(int(keep[1].shape[0]), keep, runs, seql, 0, 0, int(sf), wruns)
         dev = np.ascontiguousarray(devices, dtype=np.int32)
         hs = (ctypes.c_void_p * len(dev))()
         check(lib.rcp_readset_create_multi(ctypes.byref(d), cptr(dev, _lib._i32p), len(dev), hs))

@@ -101,3 +101,51 @@ def test_seqnames_runs_errors(gpu):
     # a run code outside the seqlevels drops its reads, as an unknown per-read code does
     rs = ReadSet((np.array([0, 9], np.int32), np.array([600, 400], np.int64)), start, end, strand, CHROM_LEN)
     assert rs.n == 600
+
+
+@pytest.mark.parametrize("sort", [False, True])
+def test_width_runs(gpu, sort):
+    """end as the runs of width(x) (IRanges holds start and width): end = start + width - 1 is
+    formed on the GPU.  Fixed-length reads (one run), mixed lengths (many runs), zero-width
+    reads, seqnames runs together with width runs, host and device starts: the same profile bit
+    for bit as the per-read ends, and the oracle's."""
+    import torch
+    from recoup_amd.engine import Bins, Plan, ReadSet
+    rng = np.random.default_rng(19)
+    chrom, start, _, strand = make_reads(rng, 60_000)
+    for width in (np.full(len(start), 180, np.int32),                                  # one run
+                  np.repeat(rng.integers(0, 300, 600), 100).astype(np.int32)):          # 600 runs, zeros
+        end = (start.astype(np.int64) + width - 1).astype(np.int32)
+        reads = (chrom, start, end, strand)
+        if sort:
+            o = np.lexsort((start, chrom))
+            reads = tuple(x[o] for x in reads)
+            width = width[o]
+        rows = single_rows(rng, 200, 2000)
+        bins = Bins([("whole", 1000)])
+        _, ref = _profile(reads, rows, bins)
+        exp = oracle_rows.profile(oracle_rows.row_coverage(oracle_rows.index_for(reads, CHROM_LEN), rows), bins)
+        check(ref, exp)
+        wr = _runs(width)
+        assert wr[1].sum() == len(width)
+        for ch in (reads[0], _runs(reads[0])):
+            _, got = _profile((ch, reads[1], wr, reads[3]), rows, bins)
+            np.testing.assert_array_equal(got[1], ref[1])
+            np.testing.assert_array_equal(got[0].view(np.uint64), ref[0].view(np.uint64))
+        dev = [torch.as_tensor(x, device="cuda:0") for x in (reads[0], reads[1], reads[3])]
+        rs = ReadSet(dev[0], dev[1], wr, dev[2], CHROM_LEN, device=0)
+        got = Plan(rs, rows, bins).run()
+        np.testing.assert_array_equal(got[0].view(np.uint64), ref[0].view(np.uint64))
+
+
+def test_width_runs_errors(gpu):
+    from recoup_amd import _lib
+    from recoup_amd.engine import ReadSet
+    rng = np.random.default_rng(20)
+    chrom, start, end, strand = make_reads(rng, 1000)
+    with pytest.raises(_lib.RcpError, match="cover"):
+        ReadSet(chrom, start, (np.array([50, 60], np.int32), np.array([500, 400], np.int64)), strand, CHROM_LEN)
+    with pytest.raises(_lib.RcpError, match="length"):
+        ReadSet(chrom, start, (np.array([50, 60], np.int32), np.array([1000, 0], np.int64)), strand, CHROM_LEN)
+    with pytest.raises(_lib.RcpError, match="width"):
+        ReadSet(chrom, start, (np.array([50, -1], np.int32), np.array([500, 500], np.int64)), strand, CHROM_LEN)

@@ -180,8 +180,9 @@ struct DevBuf {
     }
 };
 
-// Stream-ordered temporaries from the device's default memory pool, which keeps freed memory
-// mapped (release threshold raised once per device): the multi-GB sort and scan buffers of a
+// Stream-ordered temporaries from the device's default memory pool, which keeps up to 64 GB of
+// freed memory mapped (release threshold raised once per device; memory beyond it goes back at
+// synchronisation points, and torch's own allocator does not draw on this pool): the multi-GB sort and scan buffers of a
 // readset build cost a hipMalloc / hipFree pair each, and on the box those took 0.3-6 s now
 // and then (C5, 500 M reads: a 0.19 s build became 1.4 s and 7.4 s, tools/diag_readset.py);
 // from the pool the same memory is handed out again.  Allocated and freed on the stream that
@@ -197,7 +198,7 @@ hipError_t keep_pool_mapped() {
     hipMemPool_t pool;
     e = hipDeviceGetDefaultMemPool(&pool, dev);
     if (e != hipSuccess) return e;
-    uint64_t thr = UINT64_MAX;
+    uint64_t thr = uint64_t(64) << 30;  // up to 64 GB kept mapped (C5's build peaks near 40 GB)
     e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
     if (e == hipSuccess) done.insert(dev);
     return e;

@@ -309,9 +309,6 @@ __device__ __forceinline__ void pile_pairs(const RcpPlanDev& P, const RcpSeg& sg
     ps_pile(P, sg, ps, cur, P0, diff, sh);
 }
 
-#ifndef RCP_MR_DIR
-#define RCP_MR_DIR 1
-#endif
 // One wave piles row r (any number of segments x strand streams, e.g. a coverageRnaRef
 // c(flank, exons, flank) row) over row positions [P0, P0 + npos).  pileup_row walks the
 // (segment, stream) pairs one after the other -- one HBM round trip per pair, a dozen per
@@ -326,12 +323,10 @@ __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int3
     const int32_t P1 = P0 + npos;
     const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
     const int n_all = (j1 - j0) * 3;
-#if RCP_MR_DIR
     // directory of the row's chromosome stream c*3 (all pairs in the merged layout, pair
     // stream 0 in the stranded one)
     const int64_t d0 = P.row_info[r].d0;
     const int32_t dnb = P.row_info[r].nb;
-#endif
     for (int t0 = 0; t0 < n_all; t0 += 64) {
         // ---- lane t: pair (segment j, stream s)
         const int t = t0 + lane;
@@ -355,7 +350,6 @@ __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int3
                 lo = P.seg_lo[j * 3 + s];
                 hi = P.seg_hi[j * 3 + s];
                 const bool full = (a == sg.off) && (b == sg.off + len);
-#if RCP_MR_DIR
                 // a piece of the segment (the chunk window cuts it): its reads lie inside the
                 // directory buckets of its ends -- one load per bound, no bisection, at most a
                 // bucket (~8 reads) of extra candidates at each end, which add_read drops
@@ -364,9 +358,7 @@ __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int3
                     const int32_t bu = min(max(gpe, 0) >> P.dir_shift, dnb - 1);
                     lo = max(lo, (uint32_t)P.dir_l[2 * (d0 + bl)]);
                     hi = min(hi, (uint32_t)P.dir_u[2 * (d0 + bu + 1)]);
-                } else
-#endif
-                if (lo < hi && !full && hi - lo > 1024) {
+                } else if (lo < hi && !full && hi - lo > 1024) {
                     lo = lower_bound_pmax(P.pmax, lo, hi, gps);
                     hi = upper_bound_start(P.se, lo, hi, gpe);
                 }
@@ -657,9 +649,6 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
 #ifndef RCP_LOC_WPE
 #define RCP_LOC_WPE 1
 #endif
-#ifndef RCP_CEDGE_DIR
-#define RCP_CEDGE_DIR 0
-#endif
 
 __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres)[2 * RCP_MAX_CRANGE_CHUNKS]) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
@@ -786,15 +775,6 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
                     need = (task & 1) ? gpe < sg0.hi : gps > sg0.lo;  // a row end: the row's own bound
                     x = (task & 1) ? gpe : gps;
                 }
-#if RCP_CEDGE_DIR
-                // chunk edge bounded by its directory bucket alone (a superset of the exact range:
-                // the pileup's piece test drops the extra reads)
-                if (need) {
-                    const int32_t b = min(max(x, 0) >> P.dir_shift, ri.nb - 1);
-                    xr[task] = (task & 1) ? (uint32_t)P.dir_u[2 * (ri.d0 + b + 1)] : (uint32_t)P.dir_l[2 * (ri.d0 + b)];
-                    continue;
-                }
-#endif
             }
             if (!need) continue;
 #pragma unroll
@@ -1729,18 +1709,7 @@ extern "C" int rcp_rows_window_cap(void) { return kRWCap; }
 // Stores of a row's bins: row-major into the staging (P.rm, whole lines per row), or -- with
 // binsum, which keeps the column-major layout -- 8 bytes per 128-B column line; the 16 rows of a
 // line are claimed together by waves of one XCD, so plain stores meet in that L2.
-#ifndef RCP_ROWS_NT
-#define RCP_ROWS_NT 0
-#endif
-
-
-__device__ __forceinline__ void rows_store(double x, double* p) {
-#if RCP_ROWS_NT
-    __builtin_nontemporal_store(x, p);
-#else
-    *p = x;
-#endif
-}
+__device__ __forceinline__ void rows_store(double x, double* p) { *p = x; }
 
 __global__ void __launch_bounds__(64 * kRWaves) __attribute__((amdgpu_waves_per_eu(4)))
 rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restrict__ binsum) {

@@ -1,0 +1,11 @@
+#!/bin/bash
+# the driver's round-end commands on the committed tree: GPU tests, smoke, default bench line
+OUT=gpurun_out/r04x
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
+tail -1 $OUT/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 1; }
+tail -2 $OUT/smoke.log
+timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.log || { tail $OUT/bench.log; exit 1; }
+cat $OUT/bench.json

@@ -74,7 +74,7 @@ typedef struct {
     int64_t n;              /* number of reads (< 2^31) */
     const int32_t* chrom;   /* [n] chromosome code 0..n_chrom-1 (seqnames); NULL: runs below */
     const int32_t* start;   /* [n] 1-based start                                       */
-    const int32_t* end;     /* [n] 1-based end (inclusive)                             */
+    const int32_t* end;     /* [n] 1-based end (inclusive); NULL: width runs below     */
     const int8_t* strand;   /* [n] strand code                                         */
     int32_t n_chrom;        /* seqlevels                                               */
     const int64_t* seqlen;  /* [n_chrom] host pointer; -1 = NA seqlength               */

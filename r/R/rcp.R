@@ -26,21 +26,78 @@
     match(interpolation[1], c("auto", "spline", "linear", "neighborhood")) - 1L
 
 # splitBySeqname (R/util.R:1-13) + the strand filter of calcCoverage (R/coverage.R:141-144):
-# the reads go to the GPU once, sorted there by (chromosome, strand, start)
-.rcpReads <- function(input, strand = NULL, devices = .rcpDevices()) {
-    lv <- seqlevels(input)
-    sn <- seqnames(input)  # an Rle: its runs go to the GPU, not one code per read
+# the reads go to the GPU once, sorted there by (chromosome, strand, start).  `input` is what
+# calcCoverage accepts (R/coverage.R:126-146): a GRanges of reads, or the per-chromosome list
+# of GRanges that splitBySeqname makes (coverageAreaRef / coverageRnaRef pass that list,
+# R/coverage.R:54-57,94-103): its elements are laid end to end with their merged seqinfo,
+# which is what coverage() of a list element sees (the elements keep the whole seqinfo)
+.rcpReadArgs <- function(input, levels = NULL) {
+    if (is(input, "GRanges"))
+        input <- list(input)
+    input <- input[!vapply(input, is.null, TRUE)]
+    if (!all(vapply(input, is, TRUE, "GRanges")))
+        stop("The input argument must be a GenomicRanges object or a valid BAM/BigWig file ",
+            "or a list of GenomicRanges")
+    si <- if (length(input) == 0) Seqinfo() else if (length(input) == 1) seqinfo(input[[1]]) else
+        Reduce(merge, lapply(unname(input), seqinfo))
+    # `levels`: a code space shared with other samples (profileMatrixFromReads' one row table)
+    lv <- if (is.null(levels)) seqlevels(si) else levels
+    if (length(lv) == 0) # no reads and no seqlevels: one empty chromosome
+        return(list(levels = ".", args = list(integer(0), integer(0), integer(0), integer(0), NA_real_)))
+    # seqnames as their Rle runs (recoded into the merged levels): never one code per read
+    sn <- lapply(input, function(g) {
+        s <- seqnames(g)
+        list(match(as.character(runValue(s)), lv) - 1L, as.numeric(runLength(s)))
+    })
+    chrom <- list(unlist(lapply(sn, `[[`, 1), use.names = FALSE),
+        unlist(lapply(sn, `[[`, 2), use.names = FALSE))
+    if (sum(chrom[[2]]) == 0)
+        chrom <- integer(0)
     # IRanges holds start and width: reads of a few lengths send width runs, not an end vector
-    w <- Rle(width(input))
-    ends <- if (nrun(w) <= length(input) %/% 4)
-        list(as.integer(runValue(w)), as.numeric(runLength(w))) else end(input)
-    args <- list(list(as.integer(runValue(sn)) - 1L, as.numeric(runLength(sn))), start(input), ends,
-        .rcpStrandCode(strand(input)), as.numeric(seqlengths(input)[lv]),
-        if (is.null(strand)) -1L else .rcpStrandCode(strand))
-    if (length(devices) > 1)
-        return(do.call(.Call, c(list("rcp_R_readsets"), args, list(devices),
-            list(PACKAGE = "recoup"))))
-    do.call(.Call, c(list("rcp_R_readset"), args, list(devices[1]), list(PACKAGE = "recoup")))
+    one <- length(input) == 1
+    w <- Rle(if (one) width(input[[1]]) else unlist(lapply(input, width), use.names = FALSE))
+    n <- length(w)
+    ends <- if (n > 0 && nrun(w) <= n %/% 4)
+        list(as.integer(runValue(w)), as.numeric(runLength(w))) else
+        if (one) end(input[[1]]) else unlist(lapply(input, end), use.names = FALSE)
+    st <- if (one) start(input[[1]]) else unlist(lapply(input, start), use.names = FALSE)
+    sd <- if (one) .rcpStrandCode(strand(input[[1]])) else
+        unlist(lapply(input, function(g) .rcpStrandCode(strand(g))), use.names = FALSE)
+    list(levels = lv, args = list(chrom, st, ends, sd, as.numeric(seqlengths(si)[lv])))
+}
+
+# A sample's reads on the GPU: an "rcpReadSet" (the library's readset as an external pointer,
+# freed by .rcpFree or by the garbage collector, plus the seqlevels its chromosome codes index).
+# Built once per sample by coverageBaseRef / coverageAreaRef / coverageRnaRef below, so one
+# sample's reads cross PCIe once per recoup() call whatever the number of masks.
+.rcpReadSet <- function(input, strand = NULL, devices = .rcpDevices(), levels = NULL) {
+    ra <- .rcpReadArgs(input, levels)
+    sf <- if (is.null(strand)) -1L else .rcpStrandCode(strand)
+    args <- c(ra$args, list(sf))
+    ptr <- if (length(devices) > 1)
+        do.call(.Call, c(list("rcp_R_readsets"), args, list(devices), list(PACKAGE = "recoup"))) else
+        do.call(.Call, c(list("rcp_R_readset"), args, list(devices[1]), list(PACKAGE = "recoup")))
+    structure(list(ptr = ptr, levels = ra$levels, strand = strand), class = "rcpReadSet")
+}
+
+.rcpIsReadSet <- function(x) inherits(x, "rcpReadSet")
+
+# release the device arrays now instead of at the next garbage collection
+.rcpFree <- function(rs) {
+    if (.rcpIsReadSet(rs))
+        for (p in if (is.list(rs$ptr)) rs$ptr else list(rs$ptr))
+            .Call("rcp_R_free", p, PACKAGE = "recoup")
+    invisible(NULL)
+}
+
+# what calcCoverage reads for a sample of a recoup input list (R/coverage.R:32-39,53-62,94-97):
+# its reads (strand filter, findOverlaps' ignore.strand), or its BAM file -- whose branch skips
+# the strand filter (:141) and never reads ignore.strand (coverageFromBam, :228-295)
+.rcpSampleReadSet <- function(x, strandedParams) {
+    if (!is.null(x$ranges))
+        return(list(rs = .rcpReadSet(x$ranges, strandedParams$strand),
+            ignore.strand = strandedParams$ignoreStrand))
+    list(rs = .rcpReadSet(.rcpReadBam(x$file), NULL), ignore.strand = TRUE)
 }
 
 # One row per mask element: a GRanges element is one segment; a GRangesList element (the exon
@@ -65,35 +122,128 @@
     list(rows$segOff, rows$chrom, rows$start, rows$end, rows$strand, rows$group, rows$isList,
         rows$ignoreStrand)
 
-# calcCoverage (R/coverage.R:126-174): the named list of Rle (NULL where findOverlaps finds no
-# read, the chromosome is absent or the region runs past the chromosome), computed on the GPU
-# and run-length encoded there
-calcCoverage <- function(input, mask, strand = NULL, ignore.strand = TRUE, rc = NULL) {
-    if (!is(mask, "GRanges") && !is(mask, "GRangesList"))
-        stop("The mask argument must be a GRanges or GRangesList object")
-    if (is.character(input) && file.exists(input)) {
-        if (length(grep("\\.bam$", input, ignore.case = TRUE, perl = TRUE)) == 0)
-            stop("recoup_amd reads BAM files; BigWig input is not on the GPU path")
-        # coverageFromBam (R/coverage.R:228-295): every mapped alignment overlapping the region
-        # ("keep" spans); calcCoverage skips the strand filter for a BAM (:141) and
-        # coverageFromBam never reads ignore.strand
-        input <- .rcpReadBam(input)
-        strand <- NULL
-        ignore.strand <- TRUE
-    }
-    if (!is(input, "GRanges"))
-        stop("The input argument must be a GenomicRanges object or a valid BAM file")
-    rs <- .rcpReads(input, strand, .rcpDevices()[1])
-    rows <- .rcpRows(mask, seqlevels(input), ignore.strand)
-    res <- do.call(.Call, c(list("rcp_R_coverage", rs), .rcpRowArgs(rows), list(PACKAGE = "recoup")))
+# rcp_R_coverage over a readset and a row table -> calcCoverage's named list of Rle
+# (R/coverage.R:171-173; NULL where findOverlaps finds no read, the chromosome is absent or a
+# subscript fails), run-length encoded on the GPU and rebuilt here without expanding it
+.rcpCoverage <- function(rs, rows, names) {
+    ptr <- if (is.list(rs$ptr)) rs$ptr[[1]] else rs$ptr
+    res <- do.call(.Call, c(list("rcp_R_coverage", ptr), .rcpRowArgs(rows), list(PACKAGE = "recoup")))
     cov <- lapply(seq_along(res$valid), function(r) {
         if (!res$valid[r])
             return(NULL)
         i <- seq.int(res$runOff[r] + 1, length.out = res$runOff[r + 1] - res$runOff[r])
         Rle(res$values[i], res$lengths[i])
     })
-    names(cov) <- names(mask)
-    return(cov)
+    names(cov) <- names
+    cov
+}
+
+# calcCoverage (R/coverage.R:126-174): the named list of Rle, computed on the GPU.  `input` is
+# any input the reference takes -- a GRanges of reads, splitBySeqname's per-chromosome list of
+# GRanges (coverageAreaRef / coverageRnaRef, R/coverage.R:54-57,94-103), or a BAM file -- or a
+# readset the caller prepared with .rcpReadSet (then `strand` must be the one it was built with)
+calcCoverage <- function(input, mask, strand = NULL, ignore.strand = TRUE, rc = NULL) {
+    if (!.rcpIsReadSet(input) && !is(input, "GRanges") && !is.list(input) && is.character(input)
+        && !file.exists(input))
+        stop("The input argument must be a GenomicRanges object or a valid ",
+            "BAM/BigWig file or a list of GenomicRanges")
+    if (!is(mask, "GRanges") && !is(mask, "GRangesList"))
+        stop("The mask argument must be a GRanges or GRangesList object")
+    own <- !.rcpIsReadSet(input)
+    if (!own) {
+        if (!identical(strand, input$strand))
+            stop("the readset was prepared with another strand filter")
+        rs <- input
+    } else if (is.character(input)) {
+        if (length(grep("\\.bam$", input, ignore.case = TRUE, perl = TRUE)) == 0)
+            stop("recoup_amd reads BAM files; BigWig input is not on the GPU path")
+        # coverageFromBam (R/coverage.R:228-295): every mapped alignment overlapping the region
+        # ("keep" spans); calcCoverage skips the strand filter for a BAM (:141) and
+        # coverageFromBam never reads ignore.strand
+        rs <- .rcpReadSet(.rcpReadBam(input), NULL, .rcpDevices()[1])
+        ignore.strand <- TRUE
+    } else {
+        # a GRanges, or a list of them; the reference's strand filter (:141-144) is the
+        # readset's (applied to every element of a list)
+        rs <- .rcpReadSet(input, strand, .rcpDevices()[1])
+    }
+    if (own)
+        on.exit(.rcpFree(rs))
+    .rcpCoverage(rs, .rcpRows(mask, rs$levels, ignore.strand), names(mask))
+}
+
+# coverageBaseRef / coverageAreaRef (R/coverage.R:26-77): per sample one readset and one
+# calcCoverage over the regional ranges; coverageAreaRef's splitBySeqname (:54) is the
+# readset's own chromosome index, so the reads are not split in R
+.rcpCoverageRef <- function(input, genomeRanges, region, flank, strandedParams) {
+    mainRanges <- getRegionalRanges(genomeRanges, region, flank)
+    names(input) <- sapply(input, function(x) return(x$id))
+    for (n in names(input)) {
+        message("Calculating ", region, " coverage for ", input[[n]]$name)
+        s <- .rcpSampleReadSet(input[[n]], strandedParams)
+        input[[n]]$coverage <- .rcpCoverage(s$rs, .rcpRows(mainRanges, s$rs$levels, s$ignore.strand),
+            names(mainRanges))
+        .rcpFree(s$rs)
+    }
+    return(input)
+}
+
+coverageBaseRef <- function(input, genomeRanges, region, flank, strandedParams, rc = NULL)
+    .rcpCoverageRef(input, genomeRanges, region, flank, strandedParams)
+
+coverageAreaRef <- function(input, genomeRanges, region, flank, strandedParams, bamParams = NULL,
+    rc = NULL)
+    .rcpCoverageRef(input, genomeRanges, region, flank, strandedParams)
+
+# coverageRnaRef's rows (R/coverage.R:84-121): per gene c(upstream flank, the gene's exon list,
+# downstream flank) as groups 0 / 1 / 2 of ONE row -- each group is one calcCoverage element
+# (oriented by its own first range's strand, reads counted once per exon they overlap in the
+# list group), and the row is NULL when any group is NULL, as the reference's merge is
+.rcpRnaRows <- function(left, exons, right, levels, ignore.strand = TRUE) {
+    G <- length(exons)
+    if (length(left) != G || length(right) != G)
+        stop("helperRanges and genomeRanges differ in length")
+    nex <- lengths(exons)
+    flat <- unlist(exons, use.names = FALSE)
+    segOff <- c(0, cumsum(as.numeric(nex + 2)))
+    n <- segOff[G + 1]
+    first <- segOff[-(G + 1)] + 1
+    last <- segOff[-1]
+    isEx <- rep(TRUE, n)
+    isEx[c(first, last)] <- FALSE
+    code <- function(g) match(as.character(seqnames(g)), levels) - 1L
+    chrom <- st <- en <- sd <- integer(n)
+    grp <- rep(1L, n)
+    chrom[first] <- code(left); st[first] <- start(left); en[first] <- end(left)
+    sd[first] <- .rcpStrandCode(strand(left)); grp[first] <- 0L
+    chrom[last] <- code(right); st[last] <- start(right); en[last] <- end(right)
+    sd[last] <- .rcpStrandCode(strand(right)); grp[last] <- 2L
+    chrom[isEx] <- code(flat); st[isEx] <- start(flat); en[isEx] <- end(flat)
+    sd[isEx] <- .rcpStrandCode(strand(flat))
+    list(segOff = segOff, chrom = chrom, start = st, end = en, strand = sd, group = grp,
+        isList = c(FALSE, TRUE, FALSE, FALSE), ignoreStrand = as.logical(ignore.strand))
+}
+
+# coverageRnaRef (R/coverage.R:79-124): the three calcCoverage passes per sample (center over
+# the exon lists, upstream and downstream flanks) and the per-gene c(le, ce, ri) merge become
+# ONE pass over the sample's readset with 3-group rows
+coverageRnaRef <- function(input, genomeRanges, helperRanges, flank,
+    strandedParams = list(strand = NULL, ignoreStrand = TRUE), bamParams = NULL, rc = NULL) {
+    hasCoverage <- sapply(input, function(x) is.null(x$coverage))
+    if (!any(hasCoverage))
+        return(input)
+    # flank[1] == 0 gives 1-bp flanks on both sides: the reference tests flank[1] twice (:84-91)
+    leftRanges <- getFlankingRanges(helperRanges, if (flank[1] == 0) 1 else flank[1], "upstream")
+    rightRanges <- getFlankingRanges(helperRanges, if (flank[1] == 0) 1 else flank[2], "downstream")
+    names(input) <- sapply(input, function(x) return(x$id))
+    for (n in names(input)) {
+        message("Calculating genebody coverage for ", input[[n]]$name)
+        s <- .rcpSampleReadSet(input[[n]], strandedParams)
+        rows <- .rcpRnaRows(leftRanges, genomeRanges, rightRanges, s$rs$levels, s$ignore.strand)
+        input[[n]]$coverage <- .rcpCoverage(s$rs, rows, names(genomeRanges))
+        .rcpFree(s$rs)
+    }
+    return(input)
 }
 
 # The stored coverage list -> run arrays (runValue / runLength of every Rle element; anything
@@ -194,25 +344,29 @@ profileMatrixFromReads <- function(input, mask, flank, binParams, ignore.strand 
     equal <- all(len == len[1])
     parts <- .rcpParts(equal, len[1], flank, binParams)
     interp <- if (equal) "auto" else binParams$interpolation
-    rows <- .rcpRows(mask, seqlevels(input[[1]]$ranges), ignore.strand)
     binArgs <- list(as.integer(parts$where), as.integer(if (is.null(flank)) c(0, 0) else flank),
         as.integer(parts$nBins), as.integer(parts$perBase), .rcpStat(binParams$sumStat),
         .rcpInterp(interp), .rcpRngKind(), 1.0)
     devs <- .rcpDevices()
     todo <- which(vapply(input, function(x) is.null(x$profile), TRUE))
+    # one row table for every sample: chromosome codes index the union of their seqlevels
+    lv <- unique(unlist(lapply(input[todo], function(x) seqlevels(x$ranges)), use.names = FALSE))
+    rows <- .rcpRows(mask, lv, ignore.strand)
     if (length(devs) > 1) {
         for (i in todo) {
-            rs <- .rcpReads(input[[i]]$ranges, NULL, devs)
-            res <- do.call(.Call, c(list("rcp_R_profile_multi", rs), .rcpRowArgs(rows), binArgs,
+            rs <- .rcpReadSet(input[[i]]$ranges, NULL, devs, lv)
+            res <- do.call(.Call, c(list("rcp_R_profile_multi", rs$ptr), .rcpRowArgs(rows), binArgs,
                 list(PACKAGE = "recoup")))
+            .rcpFree(rs)
             input[[i]]$profile <- res$profile
             rownames(input[[i]]$profile) <- names(mask)
         }
         return(input)
     }
-    rsl <- lapply(input[todo], function(x) .rcpReads(x$ranges, NULL, devs[1]))
-    res <- do.call(.Call, c(list("rcp_R_profile_samples", rsl), .rcpRowArgs(rows), binArgs,
-        list(2L, PACKAGE = "recoup")))
+    rsl <- lapply(input[todo], function(x) .rcpReadSet(x$ranges, NULL, devs[1], lv))
+    on.exit(lapply(rsl, .rcpFree))
+    res <- do.call(.Call, c(list("rcp_R_profile_samples", lapply(rsl, `[[`, "ptr")), .rcpRowArgs(rows),
+        binArgs, list(2L, PACKAGE = "recoup")))
     for (k in seq_along(todo)) {
         input[[todo[k]]]$profile <- res[[k]]$profile
         rownames(input[[todo[k]]]$profile) <- names(mask)

@@ -12,6 +12,7 @@
  *       per sample, or all samples at once; R/profile.R:1-98)   rcp_R_profile_samples
  *   readBam (R/ranges.R:111-146)                             rcp_R_read_bam
  *   preprocessRanges downsample / sampleto (R/ranges.R:32-62) rcp_R_sample_sorted
+ *   (release a readset's device arrays now)                  rcp_R_free
  *
  * Errors: every library call returns an RCP_E* code and is checked only AFTER it returned, so
  * Rf_error never longjmps through the library's C++ frames.  Memory R hands in is read in
@@ -38,9 +39,37 @@ static void readset_finalizer(SEXP p) {
     }
 }
 
-static SEXP wrap_readset(rcp_readset* rs) {
-    SEXP p = PROTECT(R_MakeExternalPtr(rs, R_NilValue, R_NilValue));
-    R_RegisterCFinalizerEx(p, readset_finalizer, TRUE);
+static void cov_finalizer(SEXP p) {
+    rcp_cov* c = (rcp_cov*)R_ExternalPtrAddr(p);
+    if (c) {
+        rcp_cov_free(c);
+        R_ClearExternalPtr(p);
+    }
+}
+
+static void bam_finalizer(SEXP p) {
+    rcp_bam* b = (rcp_bam*)R_ExternalPtrAddr(p);
+    if (b) {
+        rcp_bam_free(b);
+        R_ClearExternalPtr(p);
+    }
+}
+
+static void rng_finalizer(SEXP p) {
+    rcp_rng* g = (rcp_rng*)R_ExternalPtrAddr(p);
+    if (g) {
+        rcp_rng_free(g);
+        R_ClearExternalPtr(p);
+    }
+}
+
+/* An external pointer with a finalizer, made BEFORE the library hands out the handle it will
+ * hold: the handle goes into it (R_SetExternalPtrAddr, no allocation) the moment the library
+ * returns, so an R allocation failure (a longjmp) after that point can only leak to the
+ * garbage collector, which runs the finalizer. */
+static SEXP new_guard(R_CFinalizer_t fin) {
+    SEXP p = PROTECT(R_MakeExternalPtr(NULL, R_NilValue, R_NilValue));
+    R_RegisterCFinalizerEx(p, fin, TRUE);
     UNPROTECT(1);
     return p;
 }
@@ -98,9 +127,13 @@ static rcp_reads_desc reads_of(SEXP chrom, SEXP start, SEXP end, SEXP strand, SE
 SEXP rcp_R_readset(SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP seqlen, SEXP sfilter, SEXP dev) {
     rcp_reads_desc d = reads_of(chrom, start, end, strand, seqlen, sfilter);
     d.device = asInteger(dev);
+    SEXP p = PROTECT(new_guard(readset_finalizer));
     rcp_readset* rs = NULL;
-    check(rcp_readset_create(&d, NULL, &rs));
-    return wrap_readset(rs);
+    int rc = rcp_readset_create(&d, NULL, &rs);
+    R_SetExternalPtrAddr(p, rs);
+    check(rc);
+    UNPROTECT(1);
+    return p;
 }
 
 /* .Call("rcp_R_readsets", <as rcp_R_readset>, devices) -> list of readsets, one per GPU */
@@ -108,11 +141,23 @@ SEXP rcp_R_readsets(SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP seqlen, 
     rcp_reads_desc d = reads_of(chrom, start, end, strand, seqlen, sfilter);
     int nd = LENGTH(devs);
     rcp_readset** rs = (rcp_readset**)R_alloc(nd > 0 ? nd : 1, sizeof(rcp_readset*));
-    check(rcp_readset_create_multi(&d, INTEGER(devs), nd, rs));
     SEXP res = PROTECT(allocVector(VECSXP, nd));
-    for (int i = 0; i < nd; ++i) SET_VECTOR_ELT(res, i, wrap_readset(rs[i]));
+    for (int i = 0; i < nd; ++i) {
+        rs[i] = NULL;
+        SET_VECTOR_ELT(res, i, new_guard(readset_finalizer));
+    }
+    int rc = rcp_readset_create_multi(&d, INTEGER(devs), nd, rs);
+    for (int i = 0; i < nd; ++i) R_SetExternalPtrAddr(VECTOR_ELT(res, i), rc == RCP_OK ? rs[i] : NULL);
+    check(rc);
     UNPROTECT(1);
     return res;
+}
+
+/* .Call("rcp_R_free", readset) releases a readset's device arrays now (the finalizer then finds
+ * nothing to do) */
+SEXP rcp_R_free(SEXP p) {
+    readset_finalizer(p);
+    return R_NilValue;
 }
 
 /* ------------------------------------------------------------------ rows / bins */
@@ -300,15 +345,14 @@ SEXP rcp_R_profile_rle(SEXP runOff, SEXP values, SEXP lengths, SEXP isNull, SEXP
 SEXP rcp_R_coverage(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
                     SEXP isList, SEXP ignoreStrand) {
     rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
+    SEXP guard = PROTECT(new_guard(cov_finalizer));
     rcp_cov* cov = NULL;
-    check(rcp_coverage_rle((const rcp_readset*)R_ExternalPtrAddr(rsp), &rd, &cov));
+    int rc = rcp_coverage_rle((const rcp_readset*)R_ExternalPtrAddr(rsp), &rd, &cov);
+    R_SetExternalPtrAddr(guard, cov);
+    check(rc);
     int32_t nrow = 0;
     int64_t nruns = 0;
-    int rc = rcp_cov_info(cov, &nrow, &nruns);
-    if (rc != RCP_OK) {
-        rcp_cov_free(cov);
-        check(rc);
-    }
+    check(rcp_cov_info(cov, &nrow, &nruns));
     SEXP off = PROTECT(allocVector(REALSXP, nrow + 1));
     SEXP val = PROTECT(allocVector(INTSXP, (R_xlen_t)nruns));
     SEXP len = PROTECT(allocVector(INTSXP, (R_xlen_t)nruns));
@@ -316,11 +360,8 @@ SEXP rcp_R_coverage(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEX
     int64_t* o64 = (int64_t*)R_alloc(nrow + 1, sizeof(int64_t));
     uint8_t* v8 = (uint8_t*)R_alloc(nrow > 0 ? nrow : 1, 1);
     rc = rcp_cov_copy(cov, o64, INTEGER(val), INTEGER(len), v8);
-    rcp_cov_free(cov);
-    if (rc != RCP_OK) {
-        UNPROTECT(4);
-        check(rc);
-    }
+    cov_finalizer(guard); /* the runs are in R's vectors now */
+    check(rc);
     for (int r = 0; r <= nrow; ++r) REAL(off)[r] = (double)o64[r];
     for (int r = 0; r < nrow; ++r) LOGICAL(ok)[r] = v8[r];
     SEXP res = PROTECT(allocVector(VECSXP, 4));
@@ -334,7 +375,7 @@ SEXP rcp_R_coverage(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEX
     SET_STRING_ELT(nm, 2, mkChar("lengths"));
     SET_STRING_ELT(nm, 3, mkChar("valid"));
     setAttrib(res, R_NamesSymbol, nm);
-    UNPROTECT(6);
+    UNPROTECT(7);
     return res;
 }
 
@@ -343,15 +384,14 @@ SEXP rcp_R_coverage(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEX
  * -> list(seqnames = character, seqlengths = numeric, chrom = integer (0-based), start, end,
  *         strand = integer (0 '+', 1 '-')) */
 SEXP rcp_R_read_bam(SEXP path, SEXP splice, SEXP q, SEXP threads) {
+    SEXP guard = PROTECT(new_guard(bam_finalizer));
     rcp_bam* bam = NULL;
-    check(rcp_bam_read(CHAR(STRING_ELT(path, 0)), asInteger(splice), asReal(q), asInteger(threads), &bam));
+    int rc = rcp_bam_read(CHAR(STRING_ELT(path, 0)), asInteger(splice), asReal(q), asInteger(threads), &bam);
+    R_SetExternalPtrAddr(guard, bam);
+    check(rc);
     int64_t n = 0, nal = 0;
     int32_t nref = 0;
-    int rc = rcp_bam_info(bam, &n, &nref, &nal);
-    if (rc != RCP_OK) {
-        rcp_bam_free(bam);
-        check(rc);
-    }
+    check(rcp_bam_info(bam, &n, &nref, &nal));
     SEXP nm = PROTECT(allocVector(STRSXP, nref));
     for (int32_t i = 0; i < nref; ++i) SET_STRING_ELT(nm, i, mkChar(rcp_bam_ref_name(bam, i)));
     SEXP sl = PROTECT(allocVector(REALSXP, nref));
@@ -362,11 +402,8 @@ SEXP rcp_R_read_bam(SEXP path, SEXP splice, SEXP q, SEXP threads) {
     int64_t* rl = (int64_t*)R_alloc(nref > 0 ? nref : 1, sizeof(int64_t));
     int8_t* s8 = (int8_t*)R_alloc(n > 0 ? (size_t)n : 1, 1);
     rc = rcp_bam_copy(bam, rl, INTEGER(ch), INTEGER(st), INTEGER(en), s8);
-    rcp_bam_free(bam);
-    if (rc != RCP_OK) {
-        UNPROTECT(6);
-        check(rc);
-    }
+    bam_finalizer(guard);
+    check(rc);
     for (int32_t i = 0; i < nref; ++i) REAL(sl)[i] = (double)rl[i];
     for (int64_t i = 0; i < n; ++i) INTEGER(sd)[i] = s8[i];
     SEXP res = PROTECT(allocVector(VECSXP, 6));
@@ -378,7 +415,7 @@ SEXP rcp_R_read_bam(SEXP path, SEXP splice, SEXP q, SEXP threads) {
         SET_STRING_ELT(names, k, mkChar(keys[k]));
     }
     setAttrib(res, R_NamesSymbol, names);
-    UNPROTECT(8);
+    UNPROTECT(9);
     return res;
 }
 
@@ -386,26 +423,24 @@ SEXP rcp_R_read_bam(SEXP path, SEXP splice, SEXP q, SEXP threads) {
  * set.seed(seed); lapply(libSizes, function(x) sort(sample(x, size))) in R's RNG stream order
  * (R/ranges.R:32-62) -> list of 1-based read indices (numeric) */
 SEXP rcp_R_sample_sorted(SEXP seed, SEXP kind, SEXP libSizes, SEXP size) {
+    SEXP guard = PROTECT(new_guard(rng_finalizer));
     rcp_rng* g = NULL;
-    check(rcp_rng_create((uint32_t)asInteger(seed), asInteger(kind), &g));
+    int rc = rcp_rng_create((uint32_t)asInteger(seed), asInteger(kind), &g);
+    R_SetExternalPtrAddr(guard, g);
+    check(rc);
     int ns = LENGTH(libSizes);
     int64_t k = (int64_t)asReal(size);
     SEXP res = PROTECT(allocVector(VECSXP, ns));
     int64_t* idx = (int64_t*)R_alloc(k > 0 ? (size_t)k : 1, sizeof(int64_t));
     for (int i = 0; i < ns; ++i) {
-        int rc = rcp_rng_sample_sorted(g, (int64_t)REAL(libSizes)[i], k, idx);
-        if (rc != RCP_OK) {
-            rcp_rng_free(g);
-            UNPROTECT(1);
-            check(rc);
-        }
+        check(rcp_rng_sample_sorted(g, (int64_t)REAL(libSizes)[i], k, idx));
         SEXP v = PROTECT(allocVector(REALSXP, (R_xlen_t)k));
         for (int64_t j = 0; j < k; ++j) REAL(v)[j] = (double)idx[j];
         SET_VECTOR_ELT(res, i, v);
         UNPROTECT(1);
     }
-    rcp_rng_free(g);
-    UNPROTECT(1);
+    rng_finalizer(guard);
+    UNPROTECT(2);
     return res;
 }
 
@@ -420,6 +455,7 @@ static const R_CallMethodDef call_methods[] = {
     {"rcp_R_coverage", (DL_FUNC)&rcp_R_coverage, 9},
     {"rcp_R_read_bam", (DL_FUNC)&rcp_R_read_bam, 4},
     {"rcp_R_sample_sorted", (DL_FUNC)&rcp_R_sample_sorted, 4},
+    {"rcp_R_free", (DL_FUNC)&rcp_R_free, 1},
     {NULL, NULL, 0}};
 
 void R_init_recoup(DllInfo* dll) {

@@ -1,0 +1,301 @@
+"""Line-by-line Python transliterations of the R wrappers in r/R/rcp.R (test infrastructure).
+
+R is not installed here or on the GPU box, so the R functions themselves cannot run.  These
+mirrors build exactly the ``.Call`` arguments the R code builds -- same vectors, same types
+(integer / double / logical), same order -- from the Python GRanges stand-ins, and drive the
+real shim through tests/rmini (an emulation of the R C API).  Each function names the R
+function it mirrors; a change to rcp.R must be reflected here (tests/test_r_shim.py checks
+that every mirrored R function still exists).
+"""
+import numpy as np
+
+from recoup_amd.granges import GRanges, GRangesList, getFlankingRanges, getRegionalRanges
+
+MIRRORED = [".rcpReadArgs", ".rcpReadSet", ".rcpFree", ".rcpSampleReadSet", ".rcpRows", ".rcpRowArgs",
+            ".rcpCoverage", "calcCoverage", ".rcpCoverageRef", ".rcpRnaRows", "coverageRnaRef", ".rcpRleArrays",
+            ".rcpProfileRle", ".rcpParts", "profileMatrixFused", "profileMatrixFromReads"]
+
+
+def rle(x):
+    """S4Vectors::Rle(x): (runValue, runLength)."""
+    x = np.asarray(x)
+    if x.size == 0:
+        return x[:0], np.zeros(0, np.int64)
+    brk = np.nonzero(x[1:] != x[:-1])[0] + 1
+    starts = np.concatenate([[0], brk])
+    return x[starts], np.diff(np.concatenate([starts, [x.size]]))
+
+
+def split_by_seqname(gr):
+    """splitBySeqname (R/util.R:1-13): level -> reads on it (empty levels dropped); each
+    element keeps the whole seqinfo, as GRanges subsetting does."""
+    out = {}
+    for c, lv in enumerate(gr.seqlevels):
+        sel = gr.seqcodes == c
+        if sel.any():
+            out[lv] = gr[sel]
+    return out
+
+
+def merge_seqinfo(grs):
+    """Reduce(merge, lapply(input, seqinfo)): union of seqlevels in first-seen order; a length
+    known in one element and NA in another is known."""
+    levels, sl = [], {}
+    for g in grs:
+        for lv, n in zip(g.seqlevels, g.seqlengths):
+            if lv not in sl:
+                levels.append(lv)
+                sl[lv] = -1
+            if n >= 0:
+                if sl[lv] >= 0 and sl[lv] != n:
+                    raise ValueError(f"incompatible seqlengths for {lv}")
+                sl[lv] = int(n)
+    return levels, sl
+
+
+def rcp_read_args(inp, levels=None):
+    """.rcpReadArgs(input, levels): (levels, list(chrom, start, ends, strand, seqlengths))."""
+    if isinstance(inp, GRanges):
+        inp = [inp]
+    elif isinstance(inp, dict):
+        inp = list(inp.values())
+    inp = [g for g in inp if g is not None]
+    lv_all, sl = merge_seqinfo(inp)
+    lv = lv_all if levels is None else list(levels)
+    if len(lv) == 0:
+        return ["."], [np.zeros(0, np.int32)] * 4 + [np.array([np.nan])]
+    code = {c: i for i, c in enumerate(lv)}
+    rv, rl = [], []
+    for g in inp:
+        names = np.array(g.seqlevels, dtype=object)[g.seqcodes] if len(g) else np.array([], dtype=object)
+        v, l = rle(np.array([code[c] for c in names], dtype=np.int32))  # match(...) - 1L
+        rv.append(v)
+        rl.append(l)
+    chrom = [np.concatenate(rv).astype(np.int32) if rv else np.zeros(0, np.int32),
+             np.concatenate(rl).astype(np.float64) if rl else np.zeros(0)]
+    if chrom[1].sum() == 0:
+        chrom = np.zeros(0, np.int32)
+    width = np.concatenate([g.width for g in inp]).astype(np.int32) if inp else np.zeros(0, np.int32)
+    wv, wl = rle(width)
+    n = width.size
+    if n > 0 and wv.size <= n // 4:
+        ends = [wv.astype(np.int32), wl.astype(np.float64)]
+    else:
+        ends = np.concatenate([g.end for g in inp]).astype(np.int32) if inp else np.zeros(0, np.int32)
+    st = np.concatenate([g.start for g in inp]).astype(np.int32) if inp else np.zeros(0, np.int32)
+    sd = np.concatenate([g.strand for g in inp]).astype(np.int32) if inp else np.zeros(0, np.int32)
+    seqlen = np.array([sl[c] if sl.get(c, -1) >= 0 else np.nan for c in lv], dtype=np.float64)
+    return lv, [chrom, st, ends, sd, seqlen]
+
+
+class ReadSet:
+    """The R "rcpReadSet": list(ptr, levels, strand)."""
+
+    def __init__(self, ptr, levels, strand):
+        self.ptr, self.levels, self.strand = ptr, levels, strand
+
+
+STRAND = {"+": 0, "-": 1, "*": 2}
+
+
+def rcp_read_set(sh, inp, strand=None, devices=(0,), levels=None):
+    """.rcpReadSet(input, strand, devices, levels)."""
+    lv, args = rcp_read_args(inp, levels)
+    sf = -1 if strand is None else STRAND[strand]
+    if len(devices) > 1:
+        ptr = sh.call("rcp_R_readsets", *args, np.int32(sf), np.asarray(devices, np.int32), raw=False)
+    else:
+        ptr = sh.call("rcp_R_readset", *args, np.int32(sf), np.int32(devices[0]))
+    return ReadSet(ptr, lv, strand)
+
+
+def rcp_free(sh, rs):
+    """.rcpFree(rs)."""
+    for p in (rs.ptr if isinstance(rs.ptr, list) else [rs.ptr]):
+        sh.call("rcp_R_free", p)
+
+
+def rcp_rows(mask, levels, ignore_strand=True):
+    """.rcpRows(mask, levels, ignore.strand)."""
+    if isinstance(mask, GRangesList):
+        flat, n = mask.flat, np.diff(mask.offsets)
+    else:
+        flat, n = mask, np.ones(len(mask), np.int64)
+    seg_off = np.concatenate([[0.0], np.cumsum(n.astype(np.float64))])
+    codes = flat.codes_in(levels)  # match(..., levels) - 1L; NA -> R's NA_integer_
+    chrom = np.where(codes < 0, np.iinfo(np.int32).min, codes).astype(np.int32)
+    return dict(segOff=seg_off, chrom=chrom, start=flat.start.astype(np.int32), end=flat.end.astype(np.int32),
+                strand=flat.strand.astype(np.int32), group=np.zeros(len(flat), np.int32),
+                isList=np.array([isinstance(mask, GRangesList), False, False, False]),
+                ignoreStrand=np.array([bool(ignore_strand)]))
+
+
+def rcp_row_args(rows):
+    """.rcpRowArgs(rows)."""
+    return [rows[k] for k in ("segOff", "chrom", "start", "end", "strand", "group", "isList", "ignoreStrand")]
+
+
+def rcp_coverage(sh, rs, rows, names=None):
+    """.rcpCoverage(rs, rows, names): list of (values, lengths) runs or None."""
+    ptr = rs.ptr[0] if isinstance(rs.ptr, list) else rs.ptr
+    res = sh.call("rcp_R_coverage", ptr, *rcp_row_args(rows))
+    cov = []
+    for r in range(len(res["valid"])):
+        if not res["valid"][r]:
+            cov.append(None)
+            continue
+        a, b = int(res["runOff"][r]), int(res["runOff"][r + 1])
+        cov.append((res["values"][a:b], res["lengths"][a:b]))
+    return cov
+
+
+def calc_coverage(sh, inp, mask, strand=None, ignore_strand=True):
+    """calcCoverage(input, mask, strand, ignore.strand) for a GRanges or a split list."""
+    rs = rcp_read_set(sh, inp, strand)
+    try:
+        return rcp_coverage(sh, rs, rcp_rows(mask, rs.levels, ignore_strand), mask.names)
+    finally:
+        rcp_free(sh, rs)
+
+
+def coverage_ref(sh, input, genomeRanges, region, flank, strandedParams):
+    """.rcpCoverageRef (coverageBaseRef / coverageAreaRef)."""
+    main = getRegionalRanges(genomeRanges, region, flank)
+    for x in input:
+        rs = rcp_read_set(sh, x["ranges"], strandedParams.get("strand"))
+        x["coverage"] = rcp_coverage(sh, rs, rcp_rows(main, rs.levels, strandedParams.get("ignoreStrand", True)))
+        rcp_free(sh, rs)
+    return input
+
+
+def rcp_rna_rows(left, exons, right, levels, ignore_strand=True):
+    """.rcpRnaRows(left, exons, right, levels, ignore.strand)."""
+    G = len(exons)
+    if len(left) != G or len(right) != G:
+        raise ValueError("helperRanges and genomeRanges differ in length")
+    nex = np.diff(exons.offsets)
+    flat = exons.flat
+    seg_off = np.concatenate([[0.0], np.cumsum((nex + 2).astype(np.float64))])
+    n = int(seg_off[G])
+    first = seg_off[:-1].astype(np.int64)  # R's first - 1 (0-based here)
+    last = seg_off[1:].astype(np.int64) - 1
+    is_ex = np.ones(n, bool)
+    is_ex[np.concatenate([first, last])] = False
+
+    def code(g):
+        c = g.codes_in(levels)
+        return np.where(c < 0, np.iinfo(np.int32).min, c)
+
+    chrom, st, en, sd = (np.zeros(n, np.int32) for _ in range(4))
+    grp = np.ones(n, np.int32)
+    chrom[first], st[first], en[first], sd[first], grp[first] = code(left), left.start, left.end, left.strand, 0
+    chrom[last], st[last], en[last], sd[last], grp[last] = code(right), right.start, right.end, right.strand, 2
+    chrom[is_ex], st[is_ex], en[is_ex], sd[is_ex] = code(flat), flat.start, flat.end, flat.strand
+    return dict(segOff=seg_off, chrom=chrom, start=st, end=en, strand=sd, group=grp,
+                isList=np.array([False, True, False, False]), ignoreStrand=np.array([bool(ignore_strand)]))
+
+
+def coverage_rna_ref(sh, input, genomeRanges, helperRanges, flank, strandedParams=None):
+    """coverageRnaRef(input, genomeRanges, helperRanges, flank, strandedParams)."""
+    sp = strandedParams or {"strand": None, "ignoreStrand": True}
+    left = getFlankingRanges(helperRanges, 1 if flank[0] == 0 else flank[0], "upstream")
+    right = getFlankingRanges(helperRanges, 1 if flank[0] == 0 else flank[1], "downstream")
+    for x in input:
+        rs = rcp_read_set(sh, x["ranges"], sp.get("strand"))
+        rows = rcp_rna_rows(left, genomeRanges, right, rs.levels, sp.get("ignoreStrand", True))
+        x["coverage"] = rcp_coverage(sh, rs, rows)
+        rcp_free(sh, rs)
+    return input
+
+
+def rcp_rle_arrays(cvrg):
+    """.rcpRleArrays(cvrg): runOff, values, lengths, isNull."""
+    is_null = np.array([x is None for x in cvrg])
+    nr = np.array([0 if x is None else len(x[0]) for x in cvrg], np.float64)
+    vals = [x[0] for x in cvrg if x is not None]
+    values = np.concatenate(vals) if vals else np.zeros(0, np.int32)
+    values = values.astype(np.int32) if values.dtype.kind in "iu" else values.astype(np.float64)
+    lengths = np.concatenate([x[1] for x in cvrg if x is not None]).astype(np.int32) if vals else np.zeros(0, np.int32)
+    return dict(runOff=np.concatenate([[0.0], np.cumsum(nr)]), values=values, lengths=lengths, isNull=is_null)
+
+
+STAT = {"mean": 0, "median": 1}
+INTERP = {"auto": 0, "spline": 1, "linear": 2, "neighborhood": 3}
+
+
+def rcp_profile_rle(sh, cvrg, where, flank, n_bins, per_base, stat="mean", interpolation="auto", rng_kind=0,
+                    device=0):
+    """.rcpProfileRle(cvrg, where, flank, nBins, perBase, stat, interpolation)."""
+    a = rcp_rle_arrays(cvrg)
+    res = sh.call("rcp_R_profile_rle", a["runOff"], a["values"], a["lengths"], a["isNull"],
+                  np.asarray(where, np.int32), np.asarray((0, 0) if flank is None else flank, np.int32),
+                  np.asarray(n_bins, np.int32), np.asarray(per_base, np.int32), np.int32(STAT[stat]),
+                  np.int32(INTERP[interpolation]), np.int32(rng_kind), 1.0, np.int32(device))
+    return res["profile"]
+
+
+def rcp_parts(equal, len1, flank, binParams):
+    """.rcpParts(equal, len1, flank, binParams)."""
+    if equal:
+        rbs = binParams["regionBinSize"]
+        return dict(where=[0], nBins=[rbs], perBase=[len1 if rbs == 0 else 0])
+    where, nb, pb = [1], [binParams["regionBinSize"]], [0]
+    r = np.asarray(flank, np.float64) / sum(flank)
+    for k in (0, 1):
+        if flank[k] == 0:
+            continue
+        fb = int(np.round(2 * binParams["flankBinSize"] * r[k])) if binParams["flankBinSize"] != 0 else 0
+        if k == 0:
+            where, nb, pb = [2] + where, [fb] + nb, [0 if fb else flank[0]] + pb
+        else:
+            where, nb, pb = where + [3], nb + [fb], pb + [0 if fb else flank[1]]
+    return dict(where=where, nBins=nb, perBase=pb)
+
+
+def _lengths(cvrg):
+    return np.array([0 if x is None else int(np.sum(x[1])) for x in cvrg])
+
+
+def profile_matrix_fused(sh, input, flank, binParams):
+    """profileMatrixFused(input, flank, binParams)."""
+    ln = _lengths(input[0]["coverage"])
+    ln = ln[ln != 0]
+    equal = bool(np.all(ln == ln[0]))
+    for x in input:
+        if x.get("profile") is not None:
+            continue
+        parts = rcp_parts(equal, int(ln[0]), flank, binParams)
+        interp = "auto" if equal else binParams.get("interpolation", "auto")
+        x["profile"] = rcp_profile_rle(sh, x["coverage"], parts["where"], flank, parts["nBins"], parts["perBase"],
+                                       binParams.get("sumStat", "mean"), interp)
+    return input
+
+
+def profile_matrix_from_reads(sh, input, mask, flank, binParams, ignore_strand=True, devices=(0,)):
+    """profileMatrixFromReads(input, mask, flank, binParams, ignore.strand)."""
+    ln = mask.width
+    equal = bool(np.all(ln == ln[0]))
+    parts = rcp_parts(equal, int(ln[0]), flank, binParams)
+    interp = "auto" if equal else binParams.get("interpolation", "auto")
+    bin_args = [np.asarray(parts["where"], np.int32), np.asarray((0, 0) if flank is None else flank, np.int32),
+                np.asarray(parts["nBins"], np.int32), np.asarray(parts["perBase"], np.int32),
+                np.int32(STAT[binParams.get("sumStat", "mean")]), np.int32(INTERP[interp]), np.int32(0), 1.0]
+    todo = [i for i, x in enumerate(input) if x.get("profile") is None]
+    lv = list(dict.fromkeys(l for i in todo for l in input[i]["ranges"].seqlevels))
+    rows = rcp_rows(mask, lv, ignore_strand)
+    if len(devices) > 1:
+        for i in todo:
+            rs = rcp_read_set(sh, input[i]["ranges"], None, devices, lv)
+            res = sh.call("rcp_R_profile_multi", rs.ptr, *rcp_row_args(rows), *bin_args)
+            rcp_free(sh, rs)
+            input[i]["profile"] = res["profile"]
+        return input
+    rsl = [rcp_read_set(sh, input[i]["ranges"], None, devices[:1], lv) for i in todo]
+    try:
+        res = sh.call("rcp_R_profile_samples", [rs.ptr for rs in rsl], *rcp_row_args(rows), *bin_args, np.int32(2))
+    finally:
+        for rs in rsl:
+            rcp_free(sh, rs)
+    for k, i in enumerate(todo):
+        input[i]["profile"] = res[k]["profile"]
+    return input

@@ -1,6 +1,7 @@
-/* Minimal declarations of the R C API used by r/src/recoup_amd_shim.c -- for a compile-only
- * check of the shim against include/recoup_amd.h where R itself is not installed
- * (tests/test_r_shim.py).  Not R's header; nothing here is linked or run. */
+/* Minimal declarations of the R C API used by r/src/recoup_amd_shim.c -- for a compile check
+ * of the shim against include/recoup_amd.h where R itself is not installed
+ * (tests/test_r_shim.py), and for tests/rmini/rmini.c, a small emulation of these functions
+ * that lets the tests execute the shim.  Not R's header. */
 #ifndef RCP_RSTUB_R_H
 #define RCP_RSTUB_R_H
 #include <stddef.h>

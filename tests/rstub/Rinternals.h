@@ -29,6 +29,7 @@ SEXP setAttrib(SEXP, SEXP, SEXP);
 SEXP R_MakeExternalPtr(void*, SEXP, SEXP);
 void* R_ExternalPtrAddr(SEXP);
 void R_ClearExternalPtr(SEXP);
+void R_SetExternalPtrAddr(SEXP, void*);
 typedef void (*R_CFinalizer_t)(SEXP);
 void R_RegisterCFinalizerEx(SEXP, R_CFinalizer_t, int);
 typedef void* (*DL_FUNC)(void);

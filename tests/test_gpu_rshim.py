@@ -1,0 +1,195 @@
+"""The R production path, executed: the .Call shim (r/src/recoup_amd_shim.c) driven with the
+exact arguments r/R/rcp.R builds (tests/r_mirror.py, a line-by-line transliteration) through
+tests/rmini (an emulation of the R C API; R is not installed), on the reference's own fixture
+(C1, data/recoup_test_data.rda) and synthetic multi-chromosome reads.
+
+recoup() with rcp.R dropped in runs coverageRef / coverageRnaRef (R/recoup.R:551-556) ->
+calcCoverage's named list of Rle in $coverage -> profileMatrix (:597) -> binCoverageMatrix /
+baseCoverageMatrix of that list, plus the forced heatmap binning (:659-714).  Each step below is
+checked against the committed golden fixtures (tests/golden/c1_expected.npz) or the CPU oracle:
+integer coverage bit-exact, means within 1e-12 relative."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as o
+from tests import r_mirror as rm
+from tests.golden import c1_cases
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "c1_expected.npz")
+MEAN_RTOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def sh(gpu):
+    from tests.rmini import rmini
+    return rmini.shim()
+
+
+@pytest.fixture(scope="module")
+def c1():
+    from recoup_amd.granges import GRanges, GRangesList
+    d = c1_cases.load_inputs()
+    S, G, E = c1_cases.samples(d), c1_cases.genome(d), c1_cases.exons(d)
+    reads = [GRanges(np.full(len(s["start"]), "chr12"), s["start"], s["end"], s["strand"],
+                     seqlevels=list(s["seqlevels"]), seqlengths=s["seqlengths"]) for s in S]
+    genes = GRanges(G["chrom"], G["start"], G["end"], G["strand"], names=G["names"])
+    exons = GRangesList(GRanges(E["chrom"], E["start"], E["end"], E["strand"]), E["seg_off"], names=E["names"])
+    idx = [o.Index(np.zeros(len(s["start"]), np.int32), s["start"], s["end"], s["strand"], s["seqlengths"])
+           for s in S]
+    return dict(S=S, reads=reads, genes=genes, exons=exons, idx=idx, G=G, E=E, gold=dict(np.load(GOLD)))
+
+
+def _decode(cov):
+    return [None if x is None else np.repeat(x[0], x[1]) for x in cov]
+
+
+def _assert_cov_equal(got, want):
+    assert len(got) == len(want)
+    for r, (g, w) in enumerate(zip(got, want)):
+        assert (g is None) == (w is None), r
+        if g is not None:
+            np.testing.assert_array_equal(g, w, err_msg=f"row {r}")
+
+
+def _oracle_cov(ix, gr, ignore_strand=True):
+    m = o.Mask.from_ranges(np.zeros(len(gr), np.int32), gr.start, gr.end, gr.strand)
+    return o.coverage(ix, m, ignore_strand, 8)
+
+
+def _inputs(c1):
+    return [dict(id=s["id"], name=s["name"], ranges=g) for s, g in zip(c1["S"], c1["reads"])]
+
+
+def test_calc_coverage_of_a_split_list(sh, c1):
+    """coverageAreaRef's call (R/coverage.R:54-57): calcCoverage(splitBySeqname(reads), mask)."""
+    from recoup_amd.granges import getRegionalRanges
+    for region in ("tss", "genebody"):
+        mask = getRegionalRanges(c1["genes"], region, (2000, 2000))
+        for k in range(2):
+            got = _decode(rm.calc_coverage(sh, rm.split_by_seqname(c1["reads"][k]), mask))
+            _assert_cov_equal(got, _oracle_cov(c1["idx"][k], mask))
+    assert sh.live_handles() == 0  # every readset released (.rcpFree)
+
+
+def test_tss_recoup_path(sh, c1):
+    """coverageBaseRef -> $coverage -> profileMatrix (per base, regionBinSize = 0) and the forced
+    200-bin heatmap pass (inst/unitTests/test_recoup.R:4-13, R/recoup.R:659-671)."""
+    inp = rm.coverage_ref(sh, _inputs(c1), c1["genes"], "tss", (2000, 2000), {"strand": None, "ignoreStrand": True})
+    gold = c1["gold"]
+    for k, x in enumerate(inp):
+        valid = np.array([c is not None for c in x["coverage"]])
+        np.testing.assert_array_equal(valid, gold[f"tss_valid_s{k}"].astype(bool))
+    inp = rm.profile_matrix_fused(sh, inp, (2000, 2000), dict(flankBinSize=0, regionBinSize=0))
+    for k, x in enumerate(inp):
+        np.testing.assert_array_equal(x["profile"], gold[f"tss_base_s{k}"].astype(np.float64))
+        heat = rm.rcp_profile_rle(sh, x["coverage"], [0], None, [200], [0])
+        np.testing.assert_allclose(heat, gold[f"tss_heat_s{k}"], rtol=MEAN_RTOL, atol=0)
+        b150 = rm.rcp_profile_rle(sh, x["coverage"], [0], None, [150], [0])
+        np.testing.assert_allclose(b150, gold[f"tss150_s{k}"], rtol=MEAN_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("stat", ["mean", "median"])
+def test_genebody_recoup_path(sh, c1, stat):
+    """coverageAreaRef -> profileMatrix's unequal-length branch (test_recoup.R:15-26)."""
+    inp = rm.coverage_ref(sh, _inputs(c1), c1["genes"], "genebody", (2000, 2000),
+                          {"strand": None, "ignoreStrand": True})
+    inp = rm.profile_matrix_fused(sh, inp, (2000, 2000), dict(flankBinSize=50, regionBinSize=150, sumStat=stat,
+                                                              interpolation="auto"))
+    for k, x in enumerate(inp):
+        np.testing.assert_allclose(x["profile"], c1["gold"][f"gb_{stat}_s{k}"], rtol=1e-9 if stat == "median"
+                                   else MEAN_RTOL, atol=0)
+
+
+def test_rna_recoup_path(sh, c1):
+    """coverageRnaRef (R/coverage.R:79-124) as ONE 3-group pass per sample: its coverage is the
+    reference's three calcCoverage passes merged with c(le, ce, ri) (here: three oracle passes),
+    and profileMatrix of it matches the golden RNA profile (man/coverageRnaRef.Rd)."""
+    from recoup_amd.granges import getFlankingRanges
+    genes, exons = c1["genes"], c1["exons"]
+    inp = rm.coverage_rna_ref(sh, _inputs(c1), exons, genes, (2000, 2000))
+    left = getFlankingRanges(genes, 2000, "upstream")
+    right = getFlankingRanges(genes, 2000, "downstream")
+    E = c1["E"]
+    ex = o.Mask(E["seg_off"], np.zeros(len(E["start"]), np.int32), E["start"], E["end"], E["strand"])
+    for k, x in enumerate(inp):
+        ix = c1["idx"][k]
+        want = o.rna_merge(_oracle_cov(ix, left), o.coverage(ix, ex, True, 8), _oracle_cov(ix, right))
+        _assert_cov_equal(_decode(x["coverage"]), want)
+    inp = rm.profile_matrix_fused(sh, inp, (2000, 2000), dict(flankBinSize=50, regionBinSize=150,
+                                                              interpolation="auto"))
+    for k, x in enumerate(inp):
+        np.testing.assert_allclose(x["profile"], c1["gold"][f"rna_s{k}"], rtol=MEAN_RTOL, atol=0)
+
+
+def test_profile_from_reads(sh, c1):
+    """profileMatrixFromReads: every sample in one rcp_R_profile_samples call, and the rows
+    split over two device slots (rcp_R_readsets + rcp_R_profile_multi) bit-equal to it."""
+    from recoup_amd.granges import getRegionalRanges
+    mask = getRegionalRanges(c1["genes"], "tss", (2000, 2000))
+    bp = dict(flankBinSize=0, regionBinSize=200)
+    one = rm.profile_matrix_from_reads(sh, _inputs(c1), mask, (2000, 2000), bp)
+    two = rm.profile_matrix_from_reads(sh, _inputs(c1), mask, (2000, 2000), bp, devices=(0, 0))
+    for k in range(2):
+        np.testing.assert_allclose(one[k]["profile"], c1["gold"][f"tss_heat_s{k}"], rtol=MEAN_RTOL, atol=0)
+        np.testing.assert_array_equal(two[k]["profile"], one[k]["profile"])
+    assert sh.live_handles() == 0
+
+
+def test_split_list_with_merged_seqinfo_and_strands(sh):
+    """A list whose elements carry different seqinfo (one chromosome's length NA in one element,
+    known in another), reads in any order, the strand filter and ignore.strand = FALSE."""
+    from recoup_amd.granges import GRanges
+    rng = np.random.default_rng(11)
+    lv = ["chr1", "chr2", "chr3"]
+    L = {"chr1": 300000, "chr2": 200000, "chr3": 250000}
+    parts, codes, starts, ends, strands = {}, [], [], [], []
+    for c, name in enumerate(lv):
+        n = 4000 + 1000 * c
+        st = rng.integers(1, L[name] - 400, n)
+        en = st + rng.integers(20, 300, n)
+        sd = rng.integers(0, 3, n)
+        # chr2's element does not know its own length; chr3's element knows chr2's
+        sl = {name: L[name]} if name != "chr2" else {}
+        if name == "chr3":
+            sl["chr2"] = L["chr2"]
+        parts[name] = GRanges(np.full(n, name), st, en, sd, seqlevels=lv if name == "chr3" else [name],
+                              seqlengths=sl)
+        codes.append(np.full(n, c, np.int32))
+        starts.append(st)
+        ends.append(en)
+        strands.append(sd)
+    R = 120
+    rc = rng.integers(0, 3, R)
+    cen = np.array([rng.integers(3000, L[lv[c]] - 3000) for c in rc])
+    rs_ = rng.integers(0, 3, R)
+    mask = GRanges(np.array(lv)[rc], cen - 1500, cen + 1499, rs_, seqlevels=lv)
+    seqlen = np.array([L[c] for c in lv], np.int64)
+    for strand in (None, "+", "-"):
+        for ign in (True, False):
+            got = _decode(rm.calc_coverage(sh, parts, mask, strand, ign))
+            ix = o.Index(np.concatenate(codes), np.concatenate(starts), np.concatenate(ends),
+                         np.concatenate(strands).astype(np.int8), seqlen,
+                         strand_filter=None if strand is None else {"+": 0, "-": 1}[strand])
+            m = o.Mask.from_ranges(rc.astype(np.int32), mask.start, mask.end, mask.strand)
+            _assert_cov_equal(got, o.coverage(ix, m, ign, 8))
+
+
+def test_library_errors_unwind_without_leaks(sh, c1):
+    """A library error inside rcp_R_coverage (a row table the library rejects) is an R error
+    raised after the call returned: the protect stack is reset and the coverage handle, if any,
+    is held by a finalizer; the readset stays usable and is released by rcp_R_free."""
+    from tests.rmini import rmini
+    rs = rm.rcp_read_set(sh, c1["reads"][0])
+    rows = rm.rcp_rows(c1["genes"], rs.levels)
+    bad = dict(rows, segOff=rows["segOff"][::-1].copy())  # offsets running backwards
+    with pytest.raises(rmini.RError, match="recoup_amd"):
+        sh.call("rcp_R_coverage", rs.ptr, *rm.rcp_row_args(bad))
+    assert sh.unguarded_handles() == 0
+    cov = rm.rcp_coverage(sh, rs, rows)
+    _assert_cov_equal(_decode(cov), _oracle_cov(c1["idx"][0], c1["genes"]))
+    rm.rcp_free(sh, rs)
+    sh.run_finalizers()
+    assert sh.live_handles() == 0

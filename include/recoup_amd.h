@@ -158,6 +158,8 @@ typedef struct {
     int32_t pileup_kernel;   /* 0: general pileup kernel; 1: lean kernel (pile + store waves);
                               * 2: lean kernel, general bins; 3: row-wave kernel */
     int32_t reserved;
+    int64_t out_ld;          /* column stride of d_out / d_binsum (rcp_plan_opts.out_ld resolved):
+                              * both must hold out_ld * (n_cols - 1) + n_rows elements */
 } rcp_plan_info;
 
 /* Host work: orientation of segments, R-RNG bin layouts (set.seed(42); sample(1:n, dif)),
@@ -199,9 +201,11 @@ RCP_API int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info);
  *   skewed-row slice kernel,
  *   pileup-bin kernel (LDS difference array -> scans -> bins -> column-major out),
  *   interpolation kernel for rows with fewer positions than bins.
- * d_out: device [n_rows * n_cols] doubles.  d_valid (device, n_rows) and d_binsum
- * (device int64 numerators, same shape as d_out; median rows hold 2x the median) may be
- * NULL.  A device-side status word reports numerator overflow; rcp_plan_status() reads it. */
+ * d_out: device doubles, column c of the R matrix at d_out + c * out_ld (out_ld =
+ * rcp_plan_info.out_ld: n_rows unless the plan was created with a wider stride), so it holds
+ * out_ld * (n_cols - 1) + n_rows elements -- [n_rows * n_cols] for the default stride.
+ * d_valid (device, n_rows) and d_binsum (device int64 numerators, same shape and stride as
+ * d_out; median rows hold 2x the median) may be NULL.  A device-side status word reports numerator overflow; rcp_plan_status() reads it. */
 RCP_API int rcp_plan_execute(rcp_plan* plan, double* d_out, uint8_t* d_valid, int64_t* d_binsum,
                      void* hip_stream);
 /* The same pass split into its launches (for per-kernel timing with events between them):

@@ -46,7 +46,8 @@ extern "C" {
 hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
                           int32_t* vout, int64_t n, int begin_bit, int end_bit, hipStream_t stream);
 hipError_t rcp_launch_unsorted(int64_t n, const uint64_t* keys, uint32_t* flag, hipStream_t stream);
-hipError_t rcp_launch_width_end(int64_t n, const int32_t* start, int32_t* width_end, hipStream_t stream);
+hipError_t rcp_launch_width_end(int64_t n, const int32_t* start, int32_t* width_end, uint32_t* overflow,
+                                hipStream_t stream);
 hipError_t rcp_launch_expand_runs(int64_t n, int32_t n_runs, const int64_t* run_start, const int32_t* run_value,
                                   int32_t* out, hipStream_t stream);
 hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
@@ -262,8 +263,9 @@ int check_device(int dev) {
 // so the default path searches and streams one range per segment instead of three.
 // A readset's own arrays, from the same pool (a 4 GB hipMalloc of C5's packed reads once took
 // 5.9 s on the box, tools/diag_readset.py with -DRCP_PLAN_TIMING=1), allocated on the build
-// stream and released after a device synchronisation -- what hipFree did implicitly, so a
-// readset destroyed with work still queued on it stays safe -- back into the pool.
+// stream and released after one device synchronisation per readset (~rcp_readset) -- what
+// hipFree does implicitly, so a readset destroyed with work still queued on it stays safe --
+// back into the pool.
 struct PoolArr {
     void* p = nullptr;
     size_t bytes = 0;
@@ -271,10 +273,7 @@ struct PoolArr {
     PoolArr(const PoolArr&) = delete;
     PoolArr& operator=(const PoolArr&) = delete;
     ~PoolArr() {
-        if (p) {
-            (void)hipDeviceSynchronize();
-            (void)hipFreeAsync(p, nullptr);
-        }
+        if (p) (void)hipFreeAsync(p, nullptr);  // after rcp_readset's device synchronisation
     }
     hipError_t alloc(size_t n, hipStream_t s) {
         if (p) return hipErrorInvalidValue;  // allocated once
@@ -304,6 +303,9 @@ struct rcp_readset {
     DevBuf d_seqlen;
     ReadLayout stranded, merged;
     bool presorted = false;  // the reads came in (chromosome, start) order (no full radix sort)
+    // one device synchronisation before the members' arrays go back to the pool (what hipFree
+    // does implicitly): work still queued on any stream that reads them has finished
+    ~rcp_readset() { (void)hipDeviceSynchronize(); }
 };
 
 // tools-only phase timing of rcp_plan_create_ex (build with -DRCP_PLAN_TIMING=1)
@@ -551,14 +553,19 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
         // widths as runs: expanded on the device, end = start + width - 1 formed there
         std::vector<int64_t> rstart(d->n_width_runs + 1, 0);
         for (int32_t k = 0; k < d->n_width_runs; ++k) rstart[k + 1] = rstart[k] + d->width_run_length[k];
-        HIP_TRY(wruns.alloc(8 * rstart.size() + 4 * (size_t)d->n_width_runs));
+        HIP_TRY(wruns.alloc(8 * rstart.size() + 4 * (size_t)d->n_width_runs + 4));
         HIP_TRY(hipMemcpyAsync(wruns.p, rstart.data(), 8 * rstart.size(), hipMemcpyHostToDevice, s));
         int32_t* wv = reinterpret_cast<int32_t*>(wruns.as<char>() + 8 * rstart.size());
+        uint32_t* overflow = reinterpret_cast<uint32_t*>(wv + d->n_width_runs);
         HIP_TRY(hipMemcpyAsync(wv, d->width_run_value, 4 * (size_t)d->n_width_runs, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(overflow, 0, 4, s));
         HIP_TRY(in_end.alloc(4 * n));
         HIP_TRY(rcp_launch_expand_runs(n, d->n_width_runs, wruns.as<int64_t>(), wv, in_end.as<int32_t>(), s));
-        HIP_TRY(rcp_launch_width_end(n, ps, in_end.as<int32_t>(), s));
+        HIP_TRY(rcp_launch_width_end(n, ps, in_end.as<int32_t>(), overflow, s));
+        uint32_t h_over = 0;
+        HIP_TRY(hipMemcpyAsync(&h_over, overflow, 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));  // rstart is released on return
+        if (h_over) return fail(RCP_EUNSUPPORTED, "a read's start + width - 1 exceeds 2^31 - 1");
         pe = in_end.as<int32_t>();
     }
     PLAN_MARK("reads H2D");
@@ -1297,6 +1304,7 @@ extern "C" int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info) {
     info->chunk_positions = plan->dev.chunk_cap;
     info->pileup_kernel = plan->dev.lean;
     info->reserved = 0;
+    info->out_ld = plan->out_ld;
     return RCP_OK;
     RCP_CATCH
 }

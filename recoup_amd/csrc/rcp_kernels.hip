@@ -500,10 +500,15 @@ __global__ void rcp_unsorted_kernel(int64_t n, const uint64_t* __restrict__ keys
     if (i < n && keys[i] < keys[i - 1]) *flag = 1u;
 }
 
-// end = start + width - 1 in place over the expanded widths (IRanges: width >= 0, end fits int32)
-__global__ void rcp_width_end_kernel(int64_t n, const int32_t* __restrict__ start, int32_t* __restrict__ width_end) {
+// end = start + width - 1 in place over the expanded widths (IRanges: width >= 0, end fits
+// int32); an end past INT32_MAX sets *overflow (the host refuses the reads)
+__global__ void rcp_width_end_kernel(int64_t n, const int32_t* __restrict__ start, int32_t* __restrict__ width_end,
+                                     uint32_t* __restrict__ overflow) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) width_end[i] = start[i] + (width_end[i] - 1);
+    if (i >= n) return;
+    const int64_t e = (int64_t)start[i] + (int64_t)width_end[i] - 1;
+    if (e > INT32_MAX) *overflow = 1u;
+    width_end[i] = (int32_t)e;
 }
 
 // chromosome code of read i from the seqnames runs (run_start: prefix sums, n_runs + 1 entries)
@@ -2757,10 +2762,11 @@ extern "C" hipError_t rcp_launch_unsorted(int64_t n, const uint64_t* keys, uint3
     return hipGetLastError();
 }
 
-extern "C" hipError_t rcp_launch_width_end(int64_t n, const int32_t* start, int32_t* width_end, hipStream_t stream) {
+extern "C" hipError_t rcp_launch_width_end(int64_t n, const int32_t* start, int32_t* width_end, uint32_t* overflow,
+                                           hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(rcp_width_end_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, n,
-                       start, width_end);
+                       start, width_end, overflow);
     return hipGetLastError();
 }
 

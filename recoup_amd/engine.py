@@ -233,7 +233,7 @@ class Plan:
         self.info = {k: getattr(info, k) for k, _ in _lib.PlanInfo._fields_}
         self.n_rows = rows.n_rows
         self.n_cols = int(info.n_cols)
-        self.out_ld = ((self.n_rows + 15) // 16 * 16 if ld == -1 else (ld or self.n_rows))
+        self.out_ld = int(info.out_ld)
         self.device = readset.device
 
     def row_lengths(self):
@@ -245,16 +245,36 @@ class Plan:
         """The device output: (n_cols, out_ld) float64; columns [:, :n_rows] are the R matrix."""
         return torch.empty((self.n_cols, self.out_ld), dtype=torch.float64, device=f"cuda:{self.device}")
 
+    def _check_buffers(self, out, valid, binsum):
+        """The kernels write column c at out + c * out_ld: out (float64) and binsum (int64) must be
+        contiguous tensors on the plan's device holding out_ld * (n_cols - 1) + n_rows elements
+        (empty_output() gives (n_cols, out_ld)); valid (uint8) n_rows."""
+        need = self.out_ld * (self.n_cols - 1) + self.n_rows if self.n_cols else 0
+        for name, t, dt, n in (("out", out, torch.float64, need), ("binsum", binsum, torch.int64, need),
+                               ("valid", valid, torch.uint8, self.n_rows)):
+            if t is None:
+                continue
+            if not isinstance(t, torch.Tensor) or t.device != torch.device("cuda", self.device):
+                raise ValueError(f"{name} must be a tensor on cuda:{self.device}")
+            if t.dtype != dt or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous {dt} tensor")
+            if t.numel() < n:
+                raise ValueError(f"{name} holds {t.numel()} elements; the plan writes {n} "
+                                 f"(out_ld {self.out_ld} x {self.n_cols} columns)")
+
     def execute(self, out=None, valid=None, binsum=None, stream=None):
         """Enqueue the pass.  ``out`` is a CUDA float64 tensor holding the R column-major
-        matrix (shape (n_cols, n_rows) in torch's row-major terms).  No host sync."""
+        matrix with column stride ``out_ld``: shape (n_cols, out_ld) in torch's row-major terms
+        (``empty_output()``), the R matrix being ``out[:, :n_rows]``.  No host sync."""
         if out is None:
             out = self.empty_output()
+        self._check_buffers(out, valid, binsum)
         check(_lib.lib().rcp_plan_execute(self.h, ptr(out), ptr(valid), ptr(binsum), _stream(self.device, stream)))
         return out
 
     def execute_stages(self, stages, out, valid=None, binsum=None, stream=None):
         """Enqueue only some launches (1 locate, 2 pileup, 4 interpolation) -- for timing."""
+        self._check_buffers(out, valid, binsum)
         check(_lib.lib().rcp_plan_execute_stages(self.h, ptr(out), ptr(valid), ptr(binsum),
                                                  _stream(self.device, stream), int(stages)))
         return out

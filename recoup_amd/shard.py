@@ -99,7 +99,12 @@ def profile_sharded(reads, regions, compute, group=None, gather="all", per_regio
     if gather is None and world > 1:
         return mine, cm.T.cpu().numpy() if not as_tensor else cm, vt[0].cpu().numpy() != 0
     backend = dist.get_backend(group) if world > 1 else None
-    dev = cm.device if (backend in (None, "nccl")) else torch.device("cpu")
+    if backend == "nccl":  # RCCL gathers device tensors: host results are copied across
+        dev = torch.device("cuda", torch.cuda.current_device())
+    elif backend is None:
+        dev = cm.device
+    else:
+        dev = torch.device("cpu")
     nmax = max(len(s) for s in shards)
     # one padded block per rank: B rows of values + 1 row of validity, columns = the shard's regions
     blk = torch.zeros((B + 1, nmax), dtype=torch.float64, device=dev)

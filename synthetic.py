@@ -26,6 +26,11 @@ def _gen(device, seed):
     return g
 
 
+def _sample_seed(seed, sample):
+    """Seed of sample k's reads (k > 0): the same regions, an independent read set."""
+    return (int(seed) * 1_000_003 + 7_919 * int(sample)) % (2 ** 63)
+
+
 def _uniform_positions(n, lens_t, g, device, margin):
     """n positions: chromosome chosen proportional to length, uniform inside [margin, len - margin]."""
     p = lens_t.double() / lens_t.sum()
@@ -52,11 +57,15 @@ def _sorted_regions(chrom, pos):
 
 
 def c4(device="cuda:0", seed=20261015, n_regions=200_000, n_reads=200_000_000, enriched=0.30, width=180,
-       flank=1000, n_bins=1000):
+       flank=1000, n_bins=1000, sample=0):
+    """``sample`` k > 0: the same regions, another sample's reads (its own peak heights and
+    draws) -- what profileMatrix loops over (R/profile.R:13-98)."""
     g = _gen(device, seed)
     lens = torch.as_tensor(MM10, device=device)
     pc, pp = _uniform_positions(n_regions, lens, g, device, margin=2500)
     pc, pp = _sorted_regions(pc, pp)
+    if sample:
+        g = _gen(device, _sample_seed(seed, sample))
     n_enr = int(n_reads * enriched)
     # Pareto(alpha = 1.5) per-peak weights -> hot regions, truncated at 1000x the median weight
     # (an untruncated draw over 200k peaks can hand one 2 kb peak a third of all reads)
@@ -82,12 +91,14 @@ def c4(device="cuda:0", seed=20261015, n_regions=200_000, n_reads=200_000_000, e
 
 
 def c2(device="cuda:0", seed=20261015, n_regions=10_000, n_reads=10_000_000, enriched=0.30, width=180,
-       flank=2000, n_bins=200):
+       flank=2000, n_bins=200, sample=0):
     g = _gen(device, seed)
     lens = torch.as_tensor(MM10, device=device)
     tc, tp = _uniform_positions(n_regions, lens, g, device, margin=2500)
     tc, tp = _sorted_regions(tc, tp)
     tstrand = torch.randint(0, 2, (n_regions,), generator=g, device=device, dtype=torch.int8)
+    if sample:
+        g = _gen(device, _sample_seed(seed, sample))
     n_enr = int(n_reads * enriched)
     k = torch.randint(0, n_regions, (n_enr,), generator=g, device=device)
     off = (torch.randn(n_enr, generator=g, device=device, dtype=torch.float64) * 300).round().to(torch.int64)
@@ -106,9 +117,9 @@ def c2(device="cuda:0", seed=20261015, n_regions=10_000, n_reads=10_000_000, enr
 
 
 def c5(device="cuda:0", seed=20261015, n_regions=25_000, n_reads=500_000_000, enriched=0.40, width=50,
-       flank=2000):
+       flank=2000, sample=0):
     d = c2(device=device, seed=seed, n_regions=n_regions, n_reads=n_reads, enriched=enriched, width=width,
-           flank=flank, n_bins=0)
+           flank=flank, n_bins=0, sample=sample)
     d["name"] = "c5"
     return d
 
@@ -127,7 +138,7 @@ def n_overlaps(reads, regions, width, device="cuda:0"):
 
 
 def c3(device="cuda:0", seed=20261015, n_genes=25_000, n_pairs=50_000_000, width=100, exonic=0.70,
-       flank=2000, region_bins=500, flank_bins=50, short_frac=0.05, genome=None):
+       flank=2000, region_bins=500, flank_bins=50, short_frac=0.05, genome=None, sample=0):
     """coverageRnaRef spliced (C3): genes of 1 + Poisson(8) exons (lognormal widths, median 150 bp;
     lognormal introns, median 2 kb; ~5 % of genes with < 500 exonic bp -> interpolated centres),
     2 x n_pairs mate alignments of `width` bp (mates read independently, R/ranges.R:117-120),
@@ -166,8 +177,8 @@ def c3(device="cuda:0", seed=20261015, n_genes=25_000, n_pairs=50_000_000, width
     seg_off[1:] = np.cumsum(n_ex2)
     gstrand = rng.integers(0, 2, n_genes).astype(np.int8)
     gend = ex_e[seg_off[1:] - 1]
-    # ---- reads on the GPU
-    g = _gen(device, seed)
+    # ---- reads on the GPU (sample k > 0: the same genes, another sample's reads)
+    g = _gen(device, seed if not sample else _sample_seed(seed, sample))
     n = 2 * n_pairs
     n_ex_reads = int(n * exonic)
     dev = device

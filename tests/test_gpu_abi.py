@@ -76,6 +76,17 @@ def test_execute_contract(c1):
         cov_only.execute(torch.empty((1, rows.n_rows), dtype=torch.float64, device="cuda:0"))
     p = Plan(rs, rows, Bins([("whole", 200)]))
     assert _lib.lib().rcp_plan_execute(p.h, None, None, None, None) == -1  # NULL output
+    # the padded column stride needs out_ld * (n_cols - 1) + n_rows elements: the unpadded
+    # (n_cols, n_rows) shape, a float32 or a host buffer is refused before any launch
+    pp = Plan(rs, rows, Bins([("whole", 200)]), out_ld="padded")
+    assert pp.out_ld == pp.info["out_ld"] == 112
+    for bad in (torch.empty((200, rows.n_rows), dtype=torch.float64, device="cuda:0"),
+                torch.empty((200, 112), dtype=torch.float32, device="cuda:0"),
+                torch.empty((200, 112), dtype=torch.float64)):
+        with pytest.raises(ValueError):
+            pp.execute(bad)
+    with pytest.raises(ValueError):
+        pp.execute(pp.empty_output(), binsum=torch.empty((200, rows.n_rows), dtype=torch.int64, device="cuda:0"))
     np.testing.assert_array_equal(p.validity(), c1["gold"]["tss_valid_s0"].astype(bool))
     np.testing.assert_array_equal(p.row_lengths(), np.full(rows.n_rows, 4000))
 

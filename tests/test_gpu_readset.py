@@ -149,3 +149,12 @@ def test_width_runs_errors(gpu):
         ReadSet(chrom, start, (np.array([50, 60], np.int32), np.array([1000, 0], np.int64)), strand, CHROM_LEN)
     with pytest.raises(_lib.RcpError, match="width"):
         ReadSet(chrom, start, (np.array([50, -1], np.int32), np.array([500, 500], np.int64)), strand, CHROM_LEN)
+
+    # IRanges' ends fit int32: a width run pushing start + width - 1 past 2^31 - 1 is refused
+    # (not wrapped to a negative end)
+    big = start.copy()
+    big[7] = 2 ** 31 - 100
+    with pytest.raises(_lib.UnsupportedError, match="2\\^31"):
+        ReadSet(chrom, big, (np.array([180], np.int32), np.array([1000], np.int64)), strand, CHROM_LEN)
+    ok = ReadSet(chrom, big, (np.array([100], np.int32), np.array([1000], np.int64)), strand, CHROM_LEN)
+    assert ok.n == 1000

@@ -444,7 +444,7 @@ def gather_matrix(tdist, backend, out, R, B, cuts, dev, R_total, reps=3):
             "note": "all_gather_into_tensor of padded (B, R/N) blocks + placement; not part of value"}, full
 
 
-def end_to_end(reads, seqlen, rows, bins, local, units, reps=3):
+def end_to_end(reads, seqlen, rows, bins, local, units, reps=3, rle=True):
     """Host-to-host passes through the C ABI entry points the R shim binds, timed in two
     phases: rcp_readset_create from host read arrays (H2D + device sort + stream index), then
     rcp_profile (plan + one pass + D2H of the R column-major matrix into caller-owned host
@@ -494,11 +494,48 @@ def end_to_end(reads, seqlen, rows, bins, local, units, reps=3):
                      "first_call_ms": calls[0][0], "calls_ms": [round(c[0], 2) for c in calls]}
     e2e = dict(res["sorted_runs"])
     e2e["any_order"] = res["any_order"]
+    if rle:
+        e2e["rle_path"] = rle_path(forms["sorted_runs"], seqlen, rows, bins, local, units, out, reps)
     e2e["width_runs"] = n_wruns
     e2e["note"] = ("C ABI: rcp_readset_create from host arrays + rcp_profile into a host matrix; PCIe both ways; "
                    "reads coordinate-sorted with seqnames runs (a sorted BAM) and width runs when few "
                    "(width_runs: their count; null = per-read ends); any_order: unsorted, one code and one end per read")
     return e2e
+
+
+def rle_path(host, seqlen, rows, bins, local, units, fused, reps):
+    """The path recoup() takes through the R wrappers (r/R/rcp.R) with saveParams$coverage =
+    TRUE, the default (R/util.R:459-461): coverageRef -> calcCoverage -> rcp_coverage_rle (GPU
+    pileup + GPU run-length encoding, runs copied to the host: the `$coverage` list of Rle,
+    R/coverage.R:171-173), then profileMatrix -> binCoverageMatrix / baseCoverageMatrix ->
+    rcp_profile_rle over those host run arrays (R/recoup.R:551-597, R/profile.R:100-212).
+    Phases per call: readset_create, coverage_rle (incl. the D2H of the runs), profile_rle
+    (H2D of the runs, the profile kernel, D2H of the matrix).  The matrix is checked bit-equal
+    to the fused pass's (``fused``, the host matrix end_to_end just filled)."""
+    from recoup_amd.engine import ReadSet, coverage_rle_host, profile_rle_arrays
+    out = np.zeros((rows.n_rows, bins.n_cols), order="F")
+    calls = []
+    n_runs = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rs = ReadSet(*host, seqlen, device=local)
+        t1 = time.perf_counter()
+        run_off, values, lengths, valid = coverage_rle_host(rs, rows)
+        t2 = time.perf_counter()
+        profile_rle_arrays(run_off, lengths, values, (valid == 0).astype(np.uint8), bins, local, out)
+        t3 = time.perf_counter()
+        del rs
+        n_runs = int(run_off[-1])
+        calls.append(((t3 - t0) * 1e3, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3))
+    med = sorted(calls)[len(calls) // 2]
+    return {"ms": med[0], "region_bins_per_s": units / (med[0] * 1e-3),
+            "phases_ms": {"readset_create": med[1], "coverage_rle": med[2], "profile_rle": med[3]},
+            "calls_ms": [round(c[0], 2) for c in calls], "n_runs": n_runs,
+            "run_bytes": 8 * n_runs, "equal_fused": bool(np.array_equal(out.T.view(np.int64), fused.view(np.int64))),
+            "note": "recoup()'s default R path: rcp_coverage_rle (GPU pileup + RLE, runs to the host) then "
+                    "rcp_profile_rle of the host runs (H2D, profile kernel, D2H); equal_fused: bit-equal to "
+                    "the fused rcp_profile matrix"}
 
 
 def cpu_baseline(args, data, rows, bins, plan, B):

@@ -267,7 +267,8 @@ RCP_API int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_samples,
  * (a zero row, row_valid = 0).  bins as for rcp_profile (parts, stat, interpolation, R-RNG bin
  * layouts, scale); out: host R column-major n_rows x n_cols.  Integer Rle rows give the same
  * bits as the read path (numerators in int64, mean = numerator * scale / width); numeric Rle
- * means are double-double sums / width (within 1e-15 relative of R's long-double mean). */
+ * means are the exact sum (double-double of value x overlap) divided once with a remainder
+ * correction -- R's long-double mean of the same values except at double-rounding ties. */
 typedef struct {
     int32_t n_rows;
     const int64_t* run_off;     /* [n_rows + 1], run_off[0] = 0 */
@@ -287,11 +288,12 @@ RCP_API int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t* d
                       void* hip_stream);
 
 /* calcCoverage one-shot for host callers (the R .Call shim): the coverage of every row of
- * `rows` over the readset (R/coverage.R:126-226), run-length encoded on the GPU and held on the
- * host -- exactly the values / lengths of the reference's named list of Rle (NULL rows:
- * valid[r] = 0 and no runs).  rcp_cov_info gives the sizes; rcp_cov_copy fills caller arrays
- * (run_off [n_rows + 1]: runs of row r are run_off[r] .. run_off[r+1]-1; values / lengths
- * [n_runs]; valid [n_rows]; any may be NULL); rcp_cov_free releases it. */
+ * `rows` over the readset (R/coverage.R:126-226), run-length encoded on the GPU and held in
+ * device memory by the handle -- exactly the values / lengths of the reference's named list of
+ * Rle (NULL rows: valid[r] = 0 and no runs).  rcp_cov_info gives the sizes; rcp_cov_copy copies
+ * them straight into caller arrays (run_off [n_rows + 1]: runs of row r are run_off[r] ..
+ * run_off[r+1]-1; values / lengths [n_runs]; valid [n_rows]; any may be NULL; may be called
+ * again); rcp_cov_free releases the device memory. */
 typedef struct rcp_cov rcp_cov;
 RCP_API int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows, rcp_cov** out);
 RCP_API int rcp_cov_info(const rcp_cov* c, int32_t* n_rows, int64_t* n_runs);

@@ -71,10 +71,9 @@ hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* st
 hipError_t rcp_launch_streams(int64_t n, const uint64_t* keys, const int32_t* vals, int64_t* off, int64_t n_off,
                               int2* se, uint64_t* scan_in, hipStream_t stream);
 hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* pmax, hipStream_t stream);
-hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, int64_t n, const int32_t* d_cov, uint8_t* rowstart,
-                              uint32_t* flags, uint32_t* run, void* temp, size_t* temp_bytes, int32_t* d_values,
-                              int64_t* run_start, int32_t* d_lengths, int64_t* d_run_off, uint32_t* n_runs_host,
-                              hipStream_t stream);
+hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, int64_t* d_count,
+                              int64_t* d_run_off, void* temp, size_t* temp_bytes, int32_t* d_values,
+                              int32_t* d_lengths, int pass, hipStream_t stream);
 hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t* off, const int32_t* pmax, int32_t* out,
                                     hipStream_t stream);
 hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const int64_t* dir_off, const int64_t* off,
@@ -1667,6 +1666,31 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
     RCP_CATCH
 }
 
+namespace {
+
+// Run-length encoding of CSR coverage on the device (rcp_kernels.hip: count, scan, emit).
+// d_run_off: device [n_rows + 1]; the total run count is returned in *n_runs (one sync).
+// d_values / d_lengths: device arrays of at least n_runs entries, or null to only count
+// (then call again with them).
+int rle_encode_device(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, int64_t* d_run_off,
+                      int64_t* n_runs, hipStream_t s) {
+    PoolBuf count(s), temp(s);
+    HIP_TRY(count.alloc(8 * ((size_t)n_rows + 1)));
+    size_t tb = 0;
+    HIP_TRY(rcp_rle_encode_dev(n_rows, d_off, d_cov, count.as<int64_t>(), d_run_off, nullptr, &tb, nullptr, nullptr, 0,
+                               s));
+    HIP_TRY(temp.alloc(std::max<size_t>(tb, 1)));
+    HIP_TRY(rcp_rle_encode_dev(n_rows, d_off, d_cov, count.as<int64_t>(), d_run_off, temp.p, &tb, nullptr, nullptr, 1,
+                               s));
+    int64_t nr = 0;
+    HIP_TRY(hipMemcpyAsync(&nr, d_run_off + n_rows, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n_runs = nr;
+    return RCP_OK;
+}
+
+}  // namespace
+
 extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int32_t* d_cov, int device,
                               int32_t* d_values, int32_t* d_lengths, int64_t* run_off, int64_t* n_runs,
                               void* hip_stream) {
@@ -1675,30 +1699,24 @@ extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int3
     const int64_t n = out_off[n_rows];
     if (n < 0 || n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "%lld positions", (long long)n);
     if (n > 0 && (!d_cov || !d_values || !d_lengths)) return fail(RCP_EINVAL, "NULL device array");
+    if (out_off[0] != 0) return fail(RCP_EINVAL, "out_off[0] != 0");
     for (int32_t r = 0; r < n_rows; ++r)
         if (out_off[r + 1] < out_off[r]) return fail(RCP_EINVAL, "out_off decreases at row %d", r);
     int rc = check_device(device);
     if (rc) return rc;
     DeviceGuard g(device);
     HIP_TRY(g.err);
+    HIP_TRY(keep_pool_mapped());
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    const int64_t nn = std::max<int64_t>(n, 1);
-    DevBuf d_off, rowstart, flags, run, run_start, d_run_off, temp;
+    PoolBuf d_off(s), d_run_off(s);
     HIP_TRY(d_off.alloc(8 * ((size_t)n_rows + 1)));
-    HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * ((size_t)n_rows + 1), hipMemcpyHostToDevice, s));
-    HIP_TRY(rowstart.alloc(nn));
-    HIP_TRY(flags.alloc(4 * nn));
-    HIP_TRY(run.alloc(4 * nn));
-    HIP_TRY(run_start.alloc(8 * nn));
     HIP_TRY(d_run_off.alloc(8 * ((size_t)n_rows + 1)));
-    size_t tb = 0;
-    uint32_t nr = 0;
-    HIP_TRY(rcp_rle_encode_dev(n_rows, d_off.as<int64_t>(), n, d_cov, nullptr, flags.as<uint32_t>(), run.as<uint32_t>(),
-                               nullptr, &tb, nullptr, nullptr, nullptr, nullptr, &nr, s));
-    HIP_TRY(temp.alloc(std::max<size_t>(tb, 1)));
-    HIP_TRY(rcp_rle_encode_dev(n_rows, d_off.as<int64_t>(), n, d_cov, rowstart.as<uint8_t>(), flags.as<uint32_t>(),
-                               run.as<uint32_t>(), temp.p, &tb, d_values, run_start.as<int64_t>(), d_lengths,
-                               d_run_off.as<int64_t>(), &nr, s));
+    HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * ((size_t)n_rows + 1), hipMemcpyHostToDevice, s));
+    int64_t nr = 0;
+    rc = rle_encode_device(n_rows, d_off.as<int64_t>(), d_cov, d_run_off.as<int64_t>(), &nr, s);
+    if (rc) return rc;
+    HIP_TRY(rcp_rle_encode_dev(n_rows, d_off.as<int64_t>(), d_cov, nullptr, d_run_off.as<int64_t>(), nullptr, nullptr,
+                               d_values, d_lengths, 2, s));
     HIP_TRY(hipMemcpyAsync(run_off, d_run_off.p, 8 * ((size_t)n_rows + 1), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     *n_runs = nr;
@@ -1707,13 +1725,22 @@ extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int3
 }
 
 // =====================================================================================
-// calcCoverage for host callers: the Rle list on the host (what the R shim hands back)
+// calcCoverage for host callers: the Rle list (what the R shim hands back).  The runs stay
+// on the device until rcp_cov_copy moves them straight into the caller's arrays (R's
+// allocVector results): one PCIe transfer, no library-side host copy.
 // =====================================================================================
 struct rcp_cov {
     int32_t n_rows = 0;
-    std::vector<int64_t> run_off;
-    std::vector<int32_t> values, lengths;
-    std::vector<uint8_t> valid;
+    int64_t n_runs = 0;
+    int device = 0;
+    PoolBuf run_off{nullptr}, values{nullptr}, lengths{nullptr}, valid{nullptr};
+    ~rcp_cov() {
+        // the buffers go back to the pool after everything queued on the null stream
+        run_off.reset();
+        values.reset();
+        lengths.reset();
+        valid.reset();
+    }
 };
 
 extern "C" int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows, rcp_cov** out) {
@@ -1726,35 +1753,37 @@ extern "C" int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows
     std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
     DeviceGuard g(rs->device);
     HIP_TRY(g.err);
+    HIP_TRY(keep_pool_mapped());
     const int32_t R = plan->n_rows;
     auto res = std::make_unique<rcp_cov>();
     res->n_rows = R;
+    res->device = rs->device;
     std::vector<int64_t> off((size_t)R + 1, 0);
     for (int32_t r = 0; r < R; ++r) off[r + 1] = off[r] + plan->row_len[r];
     const int64_t n = off[R];
     if (n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "%lld coverage positions", (long long)n);
-    DevBuf d_cov, d_valid, d_values, d_lengths;
-    HIP_TRY(d_cov.alloc(4 * std::max<int64_t>(n, 1)));
-    HIP_TRY(d_valid.alloc(std::max<int32_t>(R, 1)));
-    HIP_TRY(d_values.alloc(4 * std::max<int64_t>(n, 1)));
-    HIP_TRY(d_lengths.alloc(4 * std::max<int64_t>(n, 1)));
-    rc = rcp_calc_coverage(plan, off.data(), d_cov.as<int32_t>(), d_valid.as<uint8_t>(), nullptr);
-    if (rc) return rc;
-    rc = rcp_plan_status(plan, nullptr);
-    if (rc) return rc;
-    res->run_off.assign((size_t)R + 1, 0);
-    int64_t n_runs = 0;
-    rc = rcp_rle_encode(R, off.data(), d_cov.as<int32_t>(), rs->device, d_values.as<int32_t>(),
-                        d_lengths.as<int32_t>(), res->run_off.data(), &n_runs, nullptr);
-    if (rc) return rc;
-    res->values.resize((size_t)std::max<int64_t>(n_runs, 0));
-    res->lengths.resize((size_t)std::max<int64_t>(n_runs, 0));
-    res->valid.resize((size_t)R);
-    if (n_runs > 0) {
-        HIP_TRY(hipMemcpy(res->values.data(), d_values.p, 4 * (size_t)n_runs, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(res->lengths.data(), d_lengths.p, 4 * (size_t)n_runs, hipMemcpyDeviceToHost));
+    hipStream_t s = nullptr;
+    {
+        PoolBuf d_cov(s), d_off(s);
+        HIP_TRY(d_cov.alloc(4 * std::max<int64_t>(n, 1)));
+        HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
+        HIP_TRY(res->valid.alloc(std::max<int32_t>(R, 1)));
+        HIP_TRY(res->run_off.alloc(8 * ((size_t)R + 1)));
+        rc = rcp_calc_coverage(plan, off.data(), d_cov.as<int32_t>(), res->valid.as<uint8_t>(), nullptr);
+        if (rc) return rc;
+        rc = rcp_plan_status(plan, nullptr);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(d_off.p, off.data(), 8 * ((size_t)R + 1), hipMemcpyHostToDevice, s));
+        int64_t nr = 0;
+        rc = rle_encode_device(R, d_off.as<int64_t>(), d_cov.as<int32_t>(), res->run_off.as<int64_t>(), &nr, s);
+        if (rc) return rc;
+        res->n_runs = nr;
+        HIP_TRY(res->values.alloc(4 * (size_t)std::max<int64_t>(nr, 1)));
+        HIP_TRY(res->lengths.alloc(4 * (size_t)std::max<int64_t>(nr, 1)));
+        HIP_TRY(rcp_rle_encode_dev(R, d_off.as<int64_t>(), d_cov.as<int32_t>(), nullptr, res->run_off.as<int64_t>(),
+                                   nullptr, nullptr, res->values.as<int32_t>(), res->lengths.as<int32_t>(), 2, s));
+        HIP_TRY(hipStreamSynchronize(s));
     }
-    if (R > 0) HIP_TRY(hipMemcpy(res->valid.data(), d_valid.p, (size_t)R, hipMemcpyDeviceToHost));
     *out = res.release();
     return RCP_OK;
     RCP_CATCH
@@ -1764,7 +1793,7 @@ extern "C" int rcp_cov_info(const rcp_cov* c, int32_t* n_rows, int64_t* n_runs) 
     RCP_TRY
     if (!c) return fail(RCP_EINVAL, "NULL coverage");
     if (n_rows) *n_rows = c->n_rows;
-    if (n_runs) *n_runs = (int64_t)c->values.size();
+    if (n_runs) *n_runs = c->n_runs;
     return RCP_OK;
     RCP_CATCH
 }
@@ -1773,16 +1802,22 @@ extern "C" int rcp_cov_copy(const rcp_cov* c, int64_t* run_off, int32_t* values,
                             uint8_t* valid) {
     RCP_TRY
     if (!c) return fail(RCP_EINVAL, "NULL coverage");
-    if (run_off) std::copy(c->run_off.begin(), c->run_off.end(), run_off);
-    if (values) std::copy(c->values.begin(), c->values.end(), values);
-    if (lengths) std::copy(c->lengths.begin(), c->lengths.end(), lengths);
-    if (valid) std::copy(c->valid.begin(), c->valid.end(), valid);
+    DeviceGuard g(c->device);
+    HIP_TRY(g.err);
+    // pinned double-buffered staging (rcp_stage.h) straight into the caller's arrays
+    if (run_off) HIP_TRY(rcp::stage_d2h(run_off, c->run_off.p, 8 * ((size_t)c->n_rows + 1), c->device, nullptr));
+    if (values && c->n_runs) HIP_TRY(rcp::stage_d2h(values, c->values.p, 4 * (size_t)c->n_runs, c->device, nullptr));
+    if (lengths && c->n_runs) HIP_TRY(rcp::stage_d2h(lengths, c->lengths.p, 4 * (size_t)c->n_runs, c->device, nullptr));
+    if (valid && c->n_rows) HIP_TRY(rcp::stage_d2h(valid, c->valid.p, (size_t)c->n_rows, c->device, nullptr));
     return RCP_OK;
     RCP_CATCH
 }
 
 extern "C" int rcp_cov_free(rcp_cov* c) {
-    delete c;
+    if (c) {
+        DeviceGuard g(c->device);
+        delete c;
+    }
     return RCP_OK;
 }
 
@@ -1823,18 +1858,36 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     if (n_runs > 0 && (!cov->lengths || (!cov->ivalues && !cov->dvalues)))
         return fail(RCP_EINVAL, "NULL lengths / values");
     if (cov->ivalues && cov->dvalues) return fail(RCP_EINVAL, "both integer and numeric values given");
-    // Rle lengths are positive and every row fits int32 positions
+    // Rle lengths are positive and every row fits int32 positions; row lengths (the slices of
+    // the parts).  One pass over the runs, rows split over host threads (C4: 100 M runs).
+    std::vector<int32_t> row_len(std::max(R, 1), 0);
     {
-        std::vector<int64_t> rl(std::max(R, 1), 0);
-        for (int32_t r = 0; r < R; ++r) {
-            int64_t acc = 0;
-            int32_t mn = INT32_MAX;
-            for (int64_t j = cov->run_off[r]; j < cov->run_off[r + 1]; ++j) {
-                acc += cov->lengths[j];
-                mn = std::min(mn, cov->lengths[j]);
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
+                                                                     n_runs / (1 << 20) + 1}));
+        std::vector<int32_t> bad(nt, -1), big(nt, -1);
+        auto work = [&](int k) {
+            for (int32_t r = (int32_t)((int64_t)R * k / nt); r < (int32_t)((int64_t)R * (k + 1) / nt); ++r) {
+                int64_t acc = 0;
+                int32_t mn = INT32_MAX;
+                for (int64_t j = cov->run_off[r]; j < cov->run_off[r + 1]; ++j) {
+                    acc += cov->lengths[j];
+                    mn = std::min(mn, cov->lengths[j]);
+                }
+                if (mn <= 0 && bad[k] < 0) bad[k] = r;
+                if (acc >= (int64_t(1) << 31) && big[k] < 0) big[k] = r;
+                row_len[r] = (int32_t)std::min<int64_t>(acc, INT32_MAX);
             }
-            if (mn <= 0) return fail(RCP_EINVAL, "row %d: an Rle run length <= 0", r);
-            if (acc >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "row %d: %lld positions", r, (long long)acc);
+        };
+        if (nt == 1) {
+            work(0);
+        } else {
+            std::vector<std::thread> th;
+            for (int k = 0; k < nt; ++k) th.emplace_back(work, k);
+            for (auto& t : th) t.join();
+        }
+        for (int k = 0; k < nt; ++k) {
+            if (bad[k] >= 0) return fail(RCP_EINVAL, "row %d: an Rle run length <= 0", bad[k]);
+            if (big[k] >= 0) return fail(RCP_EUNSUPPORTED, "row %d: 2^31 or more positions", big[k]);
         }
     }
     if (n_runs >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "%lld runs", (long long)n_runs);
@@ -1843,14 +1896,13 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     DeviceGuard g(device);
     HIP_TRY(g.err);
     hipStream_t s = nullptr;
-    // ---- runs to the device: lengths (+ a 0 pad for the scan), values, row offsets
-    DevBuf d_len, d_val, d_off, d_gstart, d_start, d_rowlen, temp;
+    // ---- runs to the device: lengths (+ a 0 pad for the scan), values, row offsets;
+    // the scan of the lengths gives every run's start (rcp_rle.h gstart)
+    DevBuf d_len, d_val, d_off, d_gstart, temp;
     HIP_TRY(d_len.alloc(4 * ((size_t)n_runs + 1)));
     HIP_TRY(d_val.alloc((dbl ? 8 : 4) * std::max<size_t>((size_t)n_runs, 1)));
     HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
     HIP_TRY(d_gstart.alloc(8 * ((size_t)n_runs + 1)));
-    HIP_TRY(d_start.alloc(4 * std::max<size_t>((size_t)n_runs, 1)));
-    HIP_TRY(d_rowlen.alloc(4 * std::max<size_t>((size_t)R, 1)));
     if (n_runs) {
         HIP_TRY(rcp::stage_h2d(d_len.p, cov->lengths, 4 * (size_t)n_runs, device, s));
         HIP_TRY(rcp::stage_h2d(d_val.p, dbl ? (const void*)cov->dvalues : (const void*)cov->ivalues,
@@ -1862,14 +1914,6 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     HIP_TRY(rcp_rle_scan(d_len.as<int32_t>(), n_runs, d_gstart.as<int64_t>(), nullptr, &tb, s));
     HIP_TRY(temp.alloc(std::max<size_t>(tb, 1)));
     HIP_TRY(rcp_rle_scan(d_len.as<int32_t>(), n_runs, d_gstart.as<int64_t>(), temp.p, &tb, s));
-    HIP_TRY(rcp_rle_starts(R, d_off.as<int64_t>(), d_gstart.as<int64_t>(), d_start.as<int32_t>(),
-                           d_rowlen.as<int32_t>(), s));
-    std::vector<int32_t> row_len(std::max(R, 1), 0);
-    if (R) HIP_TRY(hipMemcpyAsync(row_len.data(), d_rowlen.p, 4 * (size_t)R, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    temp.reset();
-    d_gstart.reset();
-    d_len.reset();
     // ---- tasks: one per (row, part), with the read path's splitVector decisions
     const bool rounding = bins->rng_kind == RCP_RNG_ROUNDING;
     RcpRleDev P{};
@@ -1980,8 +2024,19 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     const size_t lds = n_scratch ? 8 * (size_t)stride : 0;
     P.interp_lds = lds <= 160 * 1024 ? 1 : 0;
     P.interp_stride = stride;
+    std::vector<RcpRleTask> itasks;
+    for (int p = 0; p < bins->n_parts; ++p) P.part_dense[p] = dbl ? 0 : 1;
+    for (const RcpRleTask& t : tasks) {
+        if (t.mode >= RCP_RLE_INTERP) itasks.push_back(t);
+        // dense windows: integer means of uniform 1-, 2- or 4-position bins, or per-base values
+        const bool dense_ok = t.mode == RCP_RLE_ZERO || t.mode >= RCP_RLE_INTERP || t.mode == RCP_RLE_BASE ||
+                              (t.mode == RCP_RLE_BINNED && bins->stat == RCP_STAT_MEAN && t.lay < 0 &&
+                               (t.bs == 1 || t.bs == 2 || t.bs == 4));
+        if (!dense_ok) P.part_dense[t.part] = 0;
+    }
     std::vector<char> blob;
     const size_t o_tasks = put(blob, tasks);
+    const size_t o_itasks = put(blob, itasks);
     const size_t o_lay = put(blob, lay_cnt);
     const size_t o_nb = put(blob, nb_pos);
     const size_t o_spl = put(blob, spl_tb);
@@ -1993,12 +2048,14 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     HIP_TRY(d_out.alloc(8 * std::max<size_t>((size_t)ld * (size_t)col, 1)));
     char* base = d_tab.as<char>();
     P.run_off = d_off.as<int64_t>();
-    P.run_start = d_start.as<int32_t>();
-    P.row_len = d_rowlen.as<int32_t>();
+    P.gstart = d_gstart.as<int64_t>();
     P.ivals = dbl ? nullptr : d_val.as<int32_t>();
     P.dvals = dbl ? d_val.as<double>() : nullptr;
     P.tasks = reinterpret_cast<const RcpRleTask*>(base + o_tasks);
-    P.n_tasks = (int64_t)tasks.size();
+    P.n_rows = R;
+    P.n_parts = bins->n_parts;
+    P.itasks = reinterpret_cast<const RcpRleTask*>(base + o_itasks);
+    P.n_itasks = (int64_t)itasks.size();
     P.lay_cnt = reinterpret_cast<const int32_t*>(base + o_lay);
     P.nb_pos = reinterpret_cast<const int32_t*>(base + o_nb);
     P.spl_tb = reinterpret_cast<const double*>(base + o_spl);

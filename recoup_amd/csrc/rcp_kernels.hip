@@ -2809,63 +2809,105 @@ extern "C" hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const
 // =================================================================================
 // run-length encoding of CSR coverage (the Rle objects of calcCoverage, S4Vectors)
 // =================================================================================
-// run starts: a row's first position, or a value change inside a row
-__global__ void rcp_rle_flags_kernel(int64_t n, const int32_t* __restrict__ cov, const uint8_t* __restrict__ rowstart,
-                                     uint32_t* __restrict__ flags) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    flags[i] = (rowstart[i] || cov[i] != cov[i - 1 >= 0 ? i - 1 : 0]) ? 1u : 0u;
-}
+// One wave per row, 256 positions per step (lane: positions base + lane + 64 u, coalesced): a
+// run starts at the row's first position or where the value differs from the one before.
+// Pass 1 counts each row's runs; an exclusive scan of the counts gives the rows' run offsets;
+// pass 2 writes every run's value and length at its final place (run lengths from the next
+// run start in the same 64 positions, else carried as the wave's pending run).
+constexpr int kRleWaves = 4;
 
-__global__ void rcp_rle_rowstart_kernel(int32_t n_rows, const int64_t* __restrict__ off, uint8_t* __restrict__ rowstart) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < n_rows && off[r + 1] > off[r]) rowstart[off[r]] = 1;
-}
-
-__global__ void rcp_rle_scatter_kernel(int64_t n, const int32_t* __restrict__ cov, const uint32_t* __restrict__ flags,
-                                       const uint32_t* __restrict__ run, int32_t* __restrict__ values,
-                                       int64_t* __restrict__ run_start) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !flags[i]) return;
-    values[run[i]] = cov[i];
-    run_start[run[i]] = i;
-}
-
-__global__ void rcp_rle_finish_kernel(int32_t n_rows, int64_t n, uint32_t n_runs, const int64_t* __restrict__ off,
-                                      const uint32_t* __restrict__ run, const int64_t* __restrict__ run_start,
-                                      int32_t* __restrict__ lengths, int64_t* __restrict__ run_off) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < n_runs) lengths[t] = (int32_t)((t + 1 < n_runs ? run_start[t + 1] : n) - run_start[t]);
-    if (t <= n_rows) run_off[t] = off[t] < n ? (int64_t)run[off[t]] : (int64_t)n_runs;
-}
-
-extern "C" hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, int64_t n, const int32_t* d_cov,
-                                         uint8_t* rowstart, uint32_t* flags, uint32_t* run, void* temp, size_t* temp_bytes,
-                                         int32_t* d_values, int64_t* run_start, int32_t* d_lengths, int64_t* d_run_off,
-                                         uint32_t* n_runs_host, hipStream_t stream) {
-    if (!temp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, flags, run, (int)std::max<int64_t>(n, 1),
-                                                       stream);
-    hipError_t e;
-    const unsigned gn = (unsigned)((n + kBlock - 1) / kBlock);
-    if ((e = hipMemsetAsync(rowstart, 0, (size_t)std::max<int64_t>(n, 1), stream)) != hipSuccess) return e;
-    hipLaunchKernelGGL(rcp_rle_rowstart_kernel, dim3((n_rows + kBlock - 1) / kBlock + 1), dim3(kBlock), 0, stream,
-                       n_rows, d_off, rowstart);
-    uint32_t nr = 0;
-    if (n > 0) {
-        hipLaunchKernelGGL(rcp_rle_flags_kernel, dim3(gn), dim3(kBlock), 0, stream, n, d_cov, rowstart, flags);
-        if ((e = hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, flags, run, (int)n, stream)) != hipSuccess) return e;
-        uint32_t last[2];
-        if ((e = hipMemcpyAsync(&last[0], run + n - 1, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess) return e;
-        if ((e = hipMemcpyAsync(&last[1], flags + n - 1, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
-        nr = last[0] + last[1];
-        hipLaunchKernelGGL(rcp_rle_scatter_kernel, dim3(gn), dim3(kBlock), 0, stream, n, d_cov, flags, run, d_values,
-                           run_start);
+__global__ void __launch_bounds__(64 * kRleWaves) rcp_rle_count_kernel(int32_t n_rows, const int64_t* __restrict__ off,
+                                                                     const int32_t* __restrict__ cov,
+                                                                     int64_t* __restrict__ count) {
+    const int r = blockIdx.x * kRleWaves + (threadIdx.x >> 6);
+    if (r >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t a = off[r], b = off[r + 1];
+    int64_t c = 0;
+    for (int64_t base = a; base < b; base += 256) {
+        int32_t v[4], pv[4];
+        bool in[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = base + lane + 64 * u;
+            in[u] = i < b;
+            v[u] = in[u] ? cov[i] : 0;
+            pv[u] = (in[u] && i > a) ? cov[i - 1] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = base + lane + 64 * u;
+            c += __popcll(__ballot(in[u] && (i == a || v[u] != pv[u])));
+        }
     }
-    const int64_t work = std::max<int64_t>((int64_t)nr, (int64_t)n_rows + 1);
-    hipLaunchKernelGGL(rcp_rle_finish_kernel, dim3((unsigned)((work + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
-                       n_rows, n, nr, d_off, run, run_start, d_lengths, d_run_off);
-    *n_runs_host = nr;
+    if (lane == 0) count[r] = c;
+}
+
+__global__ void __launch_bounds__(64 * kRleWaves) rcp_rle_emit_kernel(int32_t n_rows, const int64_t* __restrict__ off,
+                                                                    const int32_t* __restrict__ cov,
+                                                                    const int64_t* __restrict__ run_off,
+                                                                    int32_t* __restrict__ values,
+                                                                    int32_t* __restrict__ lengths) {
+    const int r = blockIdx.x * kRleWaves + (threadIdx.x >> 6);
+    if (r >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t a = off[r], b = off[r + 1];
+    const uint64_t below = (1ull << lane) - 1;  // lanes < this one
+    int64_t k = run_off[r];                      // next run index
+    int64_t pend = -1, pstart = 0;               // the last run written, its length still open
+    for (int64_t base = a; base < b; base += 256) {
+        int32_t v[4], pv[4];
+        bool in[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = base + lane + 64 * u;
+            in[u] = i < b;
+            v[u] = in[u] ? cov[i] : 0;
+            pv[u] = (in[u] && i > a) ? cov[i - 1] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = base + lane + 64 * u;
+            const bool f = in[u] && (i == a || v[u] != pv[u]);
+            const uint64_t m = __ballot(f);
+            if (m == 0) continue;
+            const int first = __builtin_ctzll(m);
+            const int64_t s0 = base + 64 * u;  // position of lane 0 in this step
+            if (pend >= 0 && lane == first) lengths[pend] = (int32_t)(i - pstart);
+            if (f) {
+                const int64_t idx = k + __popcll(m & below);
+                values[idx] = v[u];
+                const uint64_t after = m & ~(below | (1ull << lane));
+                if (after) lengths[idx] = __builtin_ctzll(after) - lane;
+            }
+            const int last = 63 - __builtin_clzll(m);
+            k += __popcll(m);
+            pend = k - 1;
+            pstart = s0 + last;
+        }
+    }
+    if (pend >= 0 && lane == 0) lengths[pend] = (int32_t)(b - pstart);
+}
+
+extern "C" hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, int64_t* d_count,
+                                         int64_t* d_run_off, void* temp, size_t* temp_bytes, int32_t* d_values,
+                                         int32_t* d_lengths, int pass, hipStream_t stream) {
+    // pass 0: temp size of the scan; 1: count + scan (d_run_off[n_rows] = total); 2: emit
+    if (pass == 0)
+        return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, d_count, d_run_off, (int)n_rows + 1, stream);
+    const unsigned grid = (unsigned)((n_rows + kRleWaves - 1) / kRleWaves);
+    if (pass == 1) {
+        hipError_t e = hipMemsetAsync(d_count + n_rows, 0, 8, stream);
+        if (e != hipSuccess) return e;
+        if (n_rows > 0)
+            hipLaunchKernelGGL(rcp_rle_count_kernel, dim3(grid), dim3(64 * kRleWaves), 0, stream, n_rows, d_off, d_cov,
+                               d_count);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, d_count, d_run_off, (int)n_rows + 1, stream);
+    }
+    if (n_rows > 0)
+        hipLaunchKernelGGL(rcp_rle_emit_kernel, dim3(grid), dim3(64 * kRleWaves), 0, stream, n_rows, d_off, d_cov,
+                           d_run_off, d_values, d_lengths);
     return hipGetLastError();
 }
 

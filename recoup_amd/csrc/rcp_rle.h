@@ -1,5 +1,5 @@
 // rcp_rle.h -- device tables of the Rle-input profile (rcp_rle.hip, rcp_profile_rle in
-// rcp_host.cpp): one task per (row, column part).
+// rcp_host.cpp): one task per (row, column part), part-major.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -27,12 +27,14 @@ struct RcpRleTask {
 
 struct RcpRleDev {
     const int64_t* run_off;    // [n_rows + 1]
-    const int32_t* run_start;  // [n_runs] row-relative start (0-based) of each run
-    const int32_t* row_len;    // [n_rows]
+    const int64_t* gstart;     // [n_runs + 1] exclusive scan of the run lengths (row r's
+                               // positions start at gstart[run_off[r]])
     const int32_t* ivals;      // integer Rle values or null
     const double* dvals;       // numeric Rle values or null
-    const RcpRleTask* tasks;
-    int64_t n_tasks;
+    const RcpRleTask* tasks;   // [n_parts][n_rows]
+    int32_t n_rows, n_parts;
+    const RcpRleTask* itasks;  // the interpolation tasks (rcp_rle_interp_kernel)
+    int64_t n_itasks;
     const int32_t* lay_cnt;
     const int32_t* nb_pos;
     const double* spl_tb;      // fmm pivots (rcp_splitvector.h)
@@ -40,6 +42,7 @@ struct RcpRleDev {
     int64_t ld;
     int32_t part_col0[RCP_MAX_PARTS];
     int32_t part_cols[RCP_MAX_PARTS];
+    int32_t part_dense[RCP_MAX_PARTS];  // 1: every row of the part takes the dense-window tile path
     int32_t stat;              // 0 mean, 1 median
     double scale;
     double* scratch;           // interpolation rows whose working set exceeds LDS
@@ -50,7 +53,5 @@ struct RcpRleDev {
 extern "C" {
 hipError_t rcp_rle_scan(const int32_t* lengths, int64_t n_runs, int64_t* gstart, void* temp, size_t* temp_bytes,
                         hipStream_t stream);
-hipError_t rcp_rle_starts(int32_t n_rows, const int64_t* run_off, const int64_t* gstart, int32_t* run_start,
-                          int32_t* row_len, hipStream_t stream);
 hipError_t rcp_rle_profile_launch(const RcpRleDev* P, int dbl, size_t lds, hipStream_t stream);
 }

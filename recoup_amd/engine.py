@@ -434,16 +434,54 @@ def profile_rle(coverages, bins, device=0):
     """rcp_profile_rle: binCoverageMatrix / baseCoverageMatrix of a host coverage list (the
     reference's list of Rle).  Returns (R x n_cols float64 matrix in R column-major (F) order,
     valid bool)."""
-    run_off, lengths, values, nulls = rle_arrays(coverages)
+    return profile_rle_arrays(*rle_arrays(coverages), bins, device)
+
+
+def profile_rle_arrays(run_off, lengths, values, nulls, bins, device=0, out=None):
+    """rcp_profile_rle on run arrays as the R shim passes them (``.rcpRleArrays``: run_off int64
+    [R + 1], lengths int32, values int32 (integer Rle) or float64 (numeric Rle), is_null uint8
+    [R]).  ``out``: optional caller-owned (R, n_cols) float64 F-order matrix (R's allocMatrix)."""
     R = len(nulls)
     integer = values.dtype == np.int32
     d = _lib.RleDesc(R, cptr(run_off, _lib._i64p), cptr(lengths, _lib._i32p),
                      cptr(values, _lib._i32p) if integer else None,
                      None if integer else cptr(values, _lib._dp), cptr(nulls, _lib._u8p))
-    out = np.zeros((R, bins.n_cols), order="F")
+    if out is None:
+        out = np.zeros((R, bins.n_cols), order="F")
+    elif out.dtype != np.float64 or not out.flags.f_contiguous or out.shape != (R, bins.n_cols):
+        raise ValueError("out must be an F-ordered float64 array of n_rows x n_cols")
     valid = np.zeros(max(R, 1), np.uint8)
     bd = bins.desc()
     with torch.cuda.device(int(device)):
         check(_lib.lib().rcp_profile_rle(ctypes.byref(d), ctypes.byref(bd), int(device), cptr(out, _lib._dp),
                                          cptr(valid, _lib._u8p)))
     return out, valid[:R].astype(bool)
+
+
+def coverage_rle_host(readset, rows, timing=None):
+    """rcp_coverage_rle + rcp_cov_copy (what the R shim's rcp_R_coverage does for calcCoverage):
+    the named list of Rle as host run arrays -- (run_off int64 [R + 1], values int32, lengths
+    int32, valid uint8 [R]); a row with valid 0 is the reference's NULL."""
+    import time
+    L = _lib.lib()
+    rd = rows.desc()
+    h = ctypes.c_void_p()
+    t0 = time.perf_counter()
+    with torch.cuda.device(readset.device):
+        check(L.rcp_coverage_rle(readset.h, ctypes.byref(rd), ctypes.byref(h)))
+    t1 = time.perf_counter()
+    try:
+        nr, nruns = ctypes.c_int32(), ctypes.c_int64()
+        check(L.rcp_cov_info(h, ctypes.byref(nr), ctypes.byref(nruns)))
+        run_off = np.empty(nr.value + 1, np.int64)
+        values = np.empty(max(nruns.value, 1), np.int32)
+        lengths = np.empty(max(nruns.value, 1), np.int32)
+        valid = np.empty(max(nr.value, 1), np.uint8)
+        check(L.rcp_cov_copy(h, cptr(run_off, _lib._i64p), cptr(values, _lib._i32p), cptr(lengths, _lib._i32p),
+                             cptr(valid, _lib._u8p)))
+    finally:
+        L.rcp_cov_free(h)
+    if timing is not None:
+        timing["coverage_ms"] = round((t1 - t0) * 1e3, 2)
+        timing["copy_ms"] = round((time.perf_counter() - t1) * 1e3, 2)
+    return run_off, values[:nruns.value], lengths[:nruns.value], valid[:nr.value]

@@ -563,6 +563,9 @@ __global__ void rcp_dir_kernel(int64_t n_entries, int64_t n_streams, const int64
 // =================================================================================
 // locate: per (row, segment, stream) read ranges, the NULL rules, heavy-row slots
 // =================================================================================
+#ifndef RCP_LOC_ABL
+#define RCP_LOC_ABL 0  // timing ablations only (wrong results): 1 no side writes, 2 no bucket searches
+#endif
 // Row positions [*p0, *p0 + *np) that column chunk (part, first bin k0) piles up for a
 // valid row of nominal length nr, mirroring the pileup kernel's metadata stage; false when
 // that stage would not pile the chunk (interpolated, wide median, width mismatch, empty).
@@ -620,7 +623,7 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
         }
     }
     const int32_t* se = reinterpret_cast<const int32_t*>(P.se);
-    while (true) {
+    while (RCP_LOC_ABL != 2) {
         uint32_t m[K];
         int32_t kv[K];
         bool any = false;
@@ -798,10 +801,12 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
             if (sl < 0 && q == 0) maxend[g] = P.pmax[hi - 1];
             if (q == 0) ncand = hi - lo;
         }
+#if RCP_LOC_ABL != 1
         if (q == 0) {
             P.seg_lo[j0 * 3] = lo;
             P.seg_hi[j0 * 3] = hi;
         }
+#endif
         if (q != 0) lo = hi = 0;  // the quad combine below reads (lo, hi) from lane 0
     }
     // (segment, stream) pairs dealt round-robin to the quad; a lane's two pairs of one round
@@ -897,9 +902,11 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
     }
     int32_t slot = -1;
     if (in_row && q == 0) {
+#if RCP_LOC_ABL != 1
         P.valid[r] = valid ? 1 : 0;
         if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
         P.ncand[r] = ncand;
+#endif
         // skewed rows only: many candidates per column chunk (each chunk of a row is one
         // wave's work) AND a deep pileup (> 2 reads per position), so a long row with
         // proportionally many reads stays on the workgroup path
@@ -914,7 +921,9 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
                 P.heavy_nslice[u] = (ncand + (uint32_t)P.heavy_slice - 1) / (uint32_t)P.heavy_slice;
             }
         }
+#if RCP_LOC_ABL != 1
         P.heavy_slot[r] = slot;
+#endif
     }
     slot = qperm<0x00>(slot);
     const bool cr = P.crange != nullptr && fast && valid && slot < 0;
@@ -980,16 +989,16 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RCP_LOC_WPE))) rcp_locate_kernel(RcpPlanDev P) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
     __shared__ uint32_t xres[kBlock / LPR][2 * RCP_MAX_CRANGE_CHUNKS];  // per row: chunk bounds
-    __shared__ uint32_t n_prev;
+    locate_rows(P, xres);
     // ---- the previous execution's heavy slots (its pileup kernels read them across column
-    // chunks, so they are cleared here, before this execution's heavy kernel adds into them)
-    if (threadIdx.x == 0) n_prev = P.heavy_threshold > 0 ? min(P.status_prev[1], (uint32_t)P.heavy_cap) : 0u;
-    __syncthreads();
+    // chunks, so they are cleared here, before this execution's heavy kernel adds into them).
+    // After the rows, each wave reading the count itself: no block-wide wait on that load
+    // before the rows' own chains start (neutral on C4 / C2, profiles/r03/pipeline/locate_ablation_ab.log).
+    const uint32_t n_prev = P.heavy_threshold > 0 ? min(P.status_prev[1], (uint32_t)P.heavy_cap) : 0u;
     for (uint32_t s = blockIdx.x; s < n_prev; s += gridDim.x) {
         int4* g4 = reinterpret_cast<int4*>(P.heavy_gdiff + (size_t)s * P.heavy_stride);  // stride: multiple of 64
         for (int i = threadIdx.x; i < (P.heavy_stride >> 2); i += blockDim.x) g4[i] = make_int4(0, 0, 0, 0);
     }
-    locate_rows(P, xres);
     // (status_prev is zeroed by the next launch, rcp_heavy_pileup_kernel, once every block here
     // has read it: a last-block ticket over this grid's thousands of blocks cost ~150 us)
 }

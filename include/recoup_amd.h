@@ -72,7 +72,10 @@ typedef struct rcp_readset rcp_readset;
 
 typedef struct {
     int64_t n;              /* number of reads (< 2^31) */
-    const int32_t* chrom;   /* [n] chromosome code 0..n_chrom-1 (seqnames); NULL: runs below */
+    const int32_t* chrom;   /* [n] chromosome code 0..n_chrom-1 (seqnames); NULL: runs below.
+                             * A code outside [0, n_chrom) (R's NA from match()) or a strand
+                             * code outside 0..2 drops the read (it joins no stream), as a
+                             * read on a seqlevel the mask never names is never a hit. */
     const int32_t* start;   /* [n] 1-based start                                       */
     const int32_t* end;     /* [n] 1-based end (inclusive); NULL: width runs below     */
     const int8_t* strand;   /* [n] strand code                                         */
@@ -100,6 +103,9 @@ typedef struct {
  * the per-(chrom, strand) stream offsets plus the prefix-max-of-end search index. */
 RCP_API int rcp_readset_create(const rcp_reads_desc* desc, void* hip_stream, rcp_readset** out);
 RCP_API int rcp_readset_destroy(rcp_readset* rs);
+/* The library's device memory pool (readset arrays, build and encode temporaries) keeps up to
+ * 64 GB of freed memory mapped for the next build; this returns what no live object uses. */
+RCP_API int rcp_release_pool(int device);
 /* n_reads kept, and stream offsets (host array of n_chrom*3+1, may be NULL). */
 RCP_API int rcp_readset_info(const rcp_readset* rs, int64_t* n_reads, int64_t* stream_off);
 

@@ -86,6 +86,7 @@ SIGNATURES = [
     ("rcp_readset_create", ctypes.c_int, [ctypes.POINTER(ReadsDesc), _vp, ctypes.POINTER(_vp)]),
     ("rcp_readset_destroy", ctypes.c_int, [_vp]),
     ("rcp_readset_info", ctypes.c_int, [_vp, _i64p, _i64p]),
+    ("rcp_release_pool", ctypes.c_int, [ctypes.c_int]),
     ("rcp_plan_create", ctypes.c_int, [_vp, ctypes.POINTER(RowsDesc), ctypes.POINTER(BinsDesc), ctypes.POINTER(_vp)]),
     ("rcp_plan_create_ex", ctypes.c_int, [_vp, ctypes.POINTER(RowsDesc), ctypes.POINTER(BinsDesc),
                                           ctypes.POINTER(PlanOpts), ctypes.POINTER(_vp)]),
@@ -135,7 +136,12 @@ def lib():
             raise ImportError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`"
                               " (hipcc --offload-arch=gfx950); recoup_amd has no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
+        # an A/B variant library (RCP_LIB_PATH, tools/gpu_ab.sh) built from an older tree may
+        # lack entry points added since; the in-tree library must export every one
+        variant = "RCP_LIB_PATH" in os.environ
         for name, res, args in SIGNATURES:
+            if variant and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -180,28 +180,47 @@ struct DevBuf {
     }
 };
 
-// Stream-ordered temporaries from the device's default memory pool, which keeps up to 64 GB of
-// freed memory mapped (release threshold raised once per device; memory beyond it goes back at
-// synchronisation points, and torch's own allocator does not draw on this pool): the multi-GB sort and scan buffers of a
-// readset build cost a hipMalloc / hipFree pair each, and on the box those took 0.3-6 s now
-// and then (C5, 500 M reads: a 0.19 s build became 1.4 s and 7.4 s, tools/diag_readset.py);
+// Stream-ordered temporaries from the library's own memory pool on each device (not the
+// process-wide default pool, whose settings other users of hipMallocAsync in the process would
+// inherit), which keeps up to 64 GB of freed memory mapped: the multi-GB sort and scan buffers
+// of a readset build cost a hipMalloc / hipFree pair each, and on the box those took 0.3-6 s
+// now and then (C5, 500 M reads: a 0.19 s build became 1.4 s and 7.4 s, tools/diag_readset.py);
 // from the pool the same memory is handed out again.  Allocated and freed on the stream that
-// uses it, so the reuse is ordered after the last kernel touching it.
-hipError_t keep_pool_mapped() {
-    static std::mutex mu;
-    static std::set<int> done;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    std::lock_guard<std::mutex> lock(mu);
-    if (done.count(dev)) return hipSuccess;
+// uses it, so the reuse is ordered after the last kernel touching it.  rcp_release_pool()
+// returns the cached memory (e.g. to torch's caching allocator in the same process).
+std::mutex g_pool_mu;
+std::map<int, hipMemPool_t> g_pools;
+
+hipError_t device_pool(int dev, hipMemPool_t* out) {
+    std::lock_guard<std::mutex> lock(g_pool_mu);
+    auto it = g_pools.find(dev);
+    if (it != g_pools.end()) {
+        *out = it->second;
+        return hipSuccess;
+    }
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
     hipMemPool_t pool;
-    e = hipDeviceGetDefaultMemPool(&pool, dev);
+    hipError_t e = hipMemPoolCreate(&pool, &props);
     if (e != hipSuccess) return e;
     uint64_t thr = uint64_t(64) << 30;  // up to 64 GB kept mapped (C5's build peaks near 40 GB)
     e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-    if (e == hipSuccess) done.insert(dev);
-    return e;
+    if (e != hipSuccess) return e;
+    g_pools[dev] = pool;
+    *out = pool;
+    return hipSuccess;
+}
+
+hipError_t pool_alloc(void** p, size_t n, hipStream_t s) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    hipMemPool_t pool;
+    if ((e = device_pool(dev, &pool)) != hipSuccess) return e;
+    return hipMallocFromPoolAsync(p, n, pool, s);
 }
 
 struct PoolBuf {
@@ -221,7 +240,7 @@ struct PoolBuf {
         reset();
         bytes = n;
         if (n == 0) return hipSuccess;
-        return hipMallocAsync(&p, n, s);
+        return pool_alloc(&p, n, s);
     }
     template <class T>
     T* as() const {
@@ -278,7 +297,7 @@ struct PoolArr {
         if (p) return hipErrorInvalidValue;  // allocated once
         bytes = n;
         if (n == 0) return hipSuccess;
-        return hipMallocAsync(&p, n, s);
+        return pool_alloc(&p, n, s);
     }
     template <class T>
     T* as() const {
@@ -353,7 +372,6 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
 #if RCP_PLAN_TIMING
     PlanTimer ltimer;
 #endif
-    HIP_TRY(keep_pool_mapped());
     PoolBuf keys(s), keys2(s), vals(s), vals2(s), scan_in(s), scan_out(s), temp(s);
     HIP_TRY(keys.alloc(8 * std::max<int64_t>(n, 1)));
     HIP_TRY(keys2.alloc(8 * std::max<int64_t>(n, 1)));
@@ -589,6 +607,25 @@ extern "C" int rcp_readset_destroy(rcp_readset* rs) {
     if (!rs) return RCP_OK;
     DeviceGuard g(rs->device);
     delete rs;
+    return RCP_OK;
+    RCP_CATCH
+}
+
+extern "C" int rcp_release_pool(int device) {
+    RCP_TRY
+    int rc = check_device(device);
+    if (rc) return rc;
+    DeviceGuard g(device);
+    HIP_TRY(g.err);
+    hipMemPool_t pool;
+    {
+        std::lock_guard<std::mutex> lock(g_pool_mu);
+        auto it = g_pools.find(device);
+        if (it == g_pools.end()) return RCP_OK;
+        pool = it->second;
+    }
+    HIP_TRY(hipDeviceSynchronize());  // frees still queued on streams land first
+    HIP_TRY(hipMemPoolTrimTo(pool, 0));
     return RCP_OK;
     RCP_CATCH
 }
@@ -1706,7 +1743,6 @@ extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int3
     if (rc) return rc;
     DeviceGuard g(device);
     HIP_TRY(g.err);
-    HIP_TRY(keep_pool_mapped());
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     PoolBuf d_off(s), d_run_off(s);
     HIP_TRY(d_off.alloc(8 * ((size_t)n_rows + 1)));
@@ -1753,7 +1789,6 @@ extern "C" int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows
     std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
     DeviceGuard g(rs->device);
     HIP_TRY(g.err);
-    HIP_TRY(keep_pool_mapped());
     const int32_t R = plan->n_rows;
     auto res = std::make_unique<rcp_cov>();
     res->n_rows = R;

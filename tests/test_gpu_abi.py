@@ -205,3 +205,23 @@ def test_profile_samples_errors(c1):
     with pytest.raises(_lib.RcpError, match="inflight"):
         profile_samples(c1["rs"], rows, Bins([("whole", 20)]), inflight=4)
     assert profile_samples([], rows, Bins([("whole", 20)])) == []
+
+
+def test_release_pool_then_rebuild(c1):
+    """rcp_release_pool returns the library pool's cached device memory; readsets built before
+    and after give the same profiles (the pool only recycles memory)."""
+    L = _lib.lib()
+    rows = helpers.tss_rows(c1["G"])
+    bins = Bins([("whole", 200)])
+    s = c1["S"][0]
+    rs = helpers.readset(s)
+    rc, before, vb = _profile(rs, rows, bins)
+    assert rc == 0
+    del rs
+    assert L.rcp_release_pool(0) == 0
+    assert L.rcp_release_pool(0) == 0  # nothing cached: still fine
+    rs = helpers.readset(s)
+    rc, after, va = _profile(rs, rows, bins)
+    assert rc == 0
+    assert np.array_equal(before.view(np.int64), after.view(np.int64)) and np.array_equal(vb, va)
+    assert L.rcp_release_pool(-1) != 0  # a device that does not exist

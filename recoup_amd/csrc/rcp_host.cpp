@@ -1937,7 +1937,6 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     HIP_TRY(d_len.alloc(4 * ((size_t)n_runs + 1)));
     HIP_TRY(d_val.alloc((dbl ? 8 : 4) * std::max<size_t>((size_t)n_runs, 1)));
     HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
-    HIP_TRY(d_gstart.alloc(8 * ((size_t)n_runs + 1)));
     if (n_runs) {
         HIP_TRY(rcp::stage_h2d(d_len.p, cov->lengths, 4 * (size_t)n_runs, device, s));
         HIP_TRY(rcp::stage_h2d(d_val.p, dbl ? (const void*)cov->dvalues : (const void*)cov->ivalues,
@@ -1945,10 +1944,6 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     }
     HIP_TRY(hipMemsetAsync(d_len.as<int32_t>() + n_runs, 0, 4, s));
     if (R > 0) HIP_TRY(rcp::stage_h2d(d_off.p, cov->run_off, 8 * ((size_t)R + 1), device, s));
-    size_t tb = 0;
-    HIP_TRY(rcp_rle_scan(d_len.as<int32_t>(), n_runs, d_gstart.as<int64_t>(), nullptr, &tb, s));
-    HIP_TRY(temp.alloc(std::max<size_t>(tb, 1)));
-    HIP_TRY(rcp_rle_scan(d_len.as<int32_t>(), n_runs, d_gstart.as<int64_t>(), temp.p, &tb, s));
     // ---- tasks: one per (row, part), with the read path's splitVector decisions
     const bool rounding = bins->rng_kind == RCP_RNG_ROUNDING;
     RcpRleDev P{};
@@ -2060,6 +2055,15 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     P.interp_lds = lds <= 160 * 1024 ? 1 : 0;
     P.interp_stride = stride;
     std::vector<RcpRleTask> itasks;
+    // run starts: from the lengths inside the tile kernel when every part's slice starts at the
+    // row's first position and no row is interpolated or a median (each row is streamed from
+    // its first run); else one device scan of the lengths (the starts the searches need)
+    bool from_lengths = bins->stat == RCP_STAT_MEAN;
+    for (int p = 0; p < bins->n_parts; ++p) {
+        RcpPart pt{};
+        part_slice_spec(bins->where ? bins->where[p] : RCP_WHERE_WHOLE, bins->flank[0], bins->flank[1], &pt);
+        if (pt.lo_end != 0 || pt.lo_off != 0) from_lengths = false;
+    }
     for (int p = 0; p < bins->n_parts; ++p) P.part_dense[p] = dbl ? 0 : 1;
     for (const RcpRleTask& t : tasks) {
         if (t.mode >= RCP_RLE_INTERP) itasks.push_back(t);
@@ -2072,6 +2076,14 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     std::vector<char> blob;
     const size_t o_tasks = put(blob, tasks);
     const size_t o_itasks = put(blob, itasks);
+    if (!itasks.empty()) from_lengths = false;
+    if (!from_lengths) {
+        size_t tb = 0;
+        HIP_TRY(d_gstart.alloc(8 * ((size_t)n_runs + 1)));
+        HIP_TRY(rcp_rle_scan(d_len.as<int32_t>(), n_runs, d_gstart.as<int64_t>(), nullptr, &tb, s));
+        HIP_TRY(temp.alloc(std::max<size_t>(tb, 1)));
+        HIP_TRY(rcp_rle_scan(d_len.as<int32_t>(), n_runs, d_gstart.as<int64_t>(), temp.p, &tb, s));
+    }
     const size_t o_lay = put(blob, lay_cnt);
     const size_t o_nb = put(blob, nb_pos);
     const size_t o_spl = put(blob, spl_tb);
@@ -2083,7 +2095,8 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     HIP_TRY(d_out.alloc(8 * std::max<size_t>((size_t)ld * (size_t)col, 1)));
     char* base = d_tab.as<char>();
     P.run_off = d_off.as<int64_t>();
-    P.gstart = d_gstart.as<int64_t>();
+    P.gstart = from_lengths ? nullptr : d_gstart.as<int64_t>();
+    P.lengths = d_len.as<int32_t>();
     P.ivals = dbl ? nullptr : d_val.as<int32_t>();
     P.dvals = dbl ? d_val.as<double>() : nullptr;
     P.tasks = reinterpret_cast<const RcpRleTask*>(base + o_tasks);

@@ -28,7 +28,9 @@ struct RcpRleTask {
 struct RcpRleDev {
     const int64_t* run_off;    // [n_rows + 1]
     const int64_t* gstart;     // [n_runs + 1] exclusive scan of the run lengths (row r's
-                               // positions start at gstart[run_off[r]])
+                               // positions start at gstart[run_off[r]]); null: starts are formed
+                               // from the lengths in the tile kernel (slices start at position 0)
+    const int32_t* lengths;    // [n_runs] run lengths
     const int32_t* ivals;      // integer Rle values or null
     const double* dvals;       // numeric Rle values or null
     const RcpRleTask* tasks;   // [n_parts][n_rows]

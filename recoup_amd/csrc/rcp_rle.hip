@@ -199,38 +199,70 @@ __device__ __forceinline__ double dd_div(double hi, double lo, double w) {
 // A batch of runs in registers: runs j + lane and j + 64 + lane (value, and the low word of
 // their global start), and the low word of run j + 128's start.  Row-relative starts fit int32,
 // so start = (int32)(low word - low word of the row's base): the subtraction waits until the
-// batch is used, and the loads stay in flight meanwhile.
+// batch is used, and the loads stay in flight meanwhile.  LEN (parts whose slices start at the
+// row's first position, no interpolation or median rows: the host then skips the scan of the
+// lengths): g0 / g1 are the runs' lengths (0 past the row) and the starts are a wave scan of
+// them from the batch's first start, when the batch is used.
 template <class VT>
 struct RunBatch {
     uint32_t g0, g1, g2;
     VT v0, v1;
 };
 
-template <bool DBL, class VT>
+template <bool DBL, bool LEN, class VT>
 __device__ __forceinline__ RunBatch<VT> load_batch(const RcpRleDev& P, int64_t j, int64_t j1) {
     // indices clamped instead of branched (no divergent loads): gstart[j1] - base is the row
     // length, and values past the row are never used
     const int lane = threadIdx.x & 63;
-    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(P.gstart);
     RunBatch<VT> b;
     const int64_t i0 = min(j + lane, j1), i1 = min(j + 64 + lane, j1), i2 = min(j + kTBatch, j1);
-    b.g0 = g32[2 * i0];
-    b.g1 = g32[2 * i1];
-    b.g2 = g32[2 * i2];
-    if constexpr (DBL) {
-        b.v0 = P.dvals[min(i0, j1 - 1)];
-        b.v1 = P.dvals[min(i1, j1 - 1)];
+    const int64_t c0 = min(i0, j1 - 1), c1 = min(i1, j1 - 1);
+    if constexpr (LEN) {
+        const uint32_t l0 = (uint32_t)P.lengths[c0], l1 = (uint32_t)P.lengths[c1];
+        b.g0 = i0 < j1 ? l0 : 0u;
+        b.g1 = i1 < j1 ? l1 : 0u;
+        b.g2 = 0;
     } else {
-        b.v0 = P.ivals[min(i0, j1 - 1)];
-        b.v1 = P.ivals[min(i1, j1 - 1)];
+        const uint32_t* g32 = reinterpret_cast<const uint32_t*>(P.gstart);
+        b.g0 = g32[2 * i0];
+        b.g1 = g32[2 * i1];
+        b.g2 = g32[2 * i2];
+    }
+    if constexpr (DBL) {
+        b.v0 = P.dvals[c0];
+        b.v1 = P.dvals[c1];
+    } else {
+        b.v0 = P.ivals[c0];
+        b.v1 = P.ivals[c1];
     }
     return b;
 }
 
+// the batch's starts into rs[0 .. 128] (row-relative); cst = start of its first run (LEN)
+template <bool LEN, class VT>
+__device__ __forceinline__ void batch_starts(const RunBatch<VT>& b, uint32_t gbl, int32_t cst, int32_t* rs,
+                                             int32_t* s0, int32_t* s1) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (LEN) {
+        const uint32_t i0 = wave_incl_scan(b.g0), i1 = wave_incl_scan(b.g1);
+        const int32_t t0 = __builtin_amdgcn_readlane((int)i0, 63), t1 = __builtin_amdgcn_readlane((int)i1, 63);
+        *s0 = cst + (int32_t)(i0 - b.g0);
+        *s1 = cst + t0 + (int32_t)(i1 - b.g1);
+        if (lane == 0) rs[kTBatch] = cst + t0 + t1;
+    } else {
+        *s0 = (int32_t)(b.g0 - gbl);
+        *s1 = (int32_t)(b.g1 - gbl);
+        if (lane == 0) rs[kTBatch] = (int32_t)(b.g2 - gbl);
+    }
+    rs[lane] = *s0;
+    rs[lane + 64] = *s1;
+}
+
 // KIND 0: means (binned or per base) by per-column searches of the run batch; 1: median bins;
 // 2: dense windows (integer Rle; per base, or uniform bins of 1, 2 or 4 positions; the host
-// picks it per part when every row of the part qualifies)
-template <bool DBL, int KIND>
+// picks it per part when every row of the part qualifies).  LEN: starts from the lengths
+// (load_batch).
+template <bool DBL, int KIND, bool LEN>
 __global__ void __launch_bounds__(kTBlock) __attribute__((amdgpu_waves_per_eu(RCP_RLE_WPE)))
 rcp_rle_tile_kernel(RcpRleDev P, int p) {
     constexpr bool MEDIAN = KIND == 1, DENSE = !DBL && KIND == 2;
@@ -262,7 +294,7 @@ rcp_rle_tile_kernel(RcpRleDev P, int p) {
     const bool base = t.mode == RCP_RLE_BASE;
     const bool median = MEDIAN && !base;
     const int64_t j0 = zero ? 0 : P.run_off[r], j1 = zero ? 0 : P.run_off[r + 1];
-    const int64_t gb = zero ? 0 : P.gstart[j0];
+    const int64_t gb = (zero || LEN) ? 0 : P.gstart[j0];
     const uint32_t gbl = (uint32_t)gb;
     const int32_t* cnt = (!zero && !base && t.lay >= 0) ? P.lay_cnt + t.lay : nullptr;
     // the run containing the next chunk's first position, and its batch (prefetched during the
@@ -272,11 +304,13 @@ rcp_rle_tile_kernel(RcpRleDev P, int p) {
     const int32_t dbs = base ? 1 : t.bs;
     int32_t* dn = dn_l[DENSE ? q : 0];
     int64_t j = 0;
+    int32_t cst = 0;  // LEN: start of run j
     RunBatch<VT> nb_regs{};
     const bool streamed = !zero && !median;
     if (streamed) {
-        j = wave_run_search(P, j0, j1, gb, base ? t.head : bin_lo(t, cnt, 0));
-        nb_regs = load_batch<DBL, VT>(P, j, j1);
+        if constexpr (LEN) j = j0;  // every slice starts at position 0: run j0
+        else j = wave_run_search(P, j0, j1, gb, base ? t.head : bin_lo(t, cnt, 0));
+        nb_regs = load_batch<DBL, LEN, VT>(P, j, j1);
     }
     for (int32_t c0 = 0; c0 < ncol; c0 += kTCols) {
         const int32_t cc = min(kTCols, ncol - c0);
@@ -297,10 +331,8 @@ rcp_rle_tile_kernel(RcpRleDev P, int p) {
             for (int i = lane; i < (W + 3) >> 2; i += 64) reinterpret_cast<int4*>(dn)[i] = make_int4(0, 0, 0, 0);
             uint32_t carry = 0;  // value of the run before the batch's first run (0 before the window)
             for (;;) {
-                const int32_t s0 = (int32_t)(nb_regs.g0 - gbl), s1 = (int32_t)(nb_regs.g1 - gbl);
-                rs[lane] = s0;
-                rs[lane + 64] = s1;
-                if (lane == 0) rs[kTBatch] = (int32_t)(nb_regs.g2 - gbl);
+                int32_t s0, s1;
+                batch_starts<LEN>(nb_regs, gbl, cst, rs, &s0, &s1);
                 rv[lane] = nb_regs.v0;
                 rv[lane + 64] = nb_regs.v1;
                 const int n = __popcll(__ballot(s0 < pb)) + __popcll(__ballot(s1 < pb));
@@ -309,8 +341,10 @@ rcp_rle_tile_kernel(RcpRleDev P, int p) {
                 const bool more = be < pb;
                 // the next batch: the rest of this window, or the next chunk's first (the run
                 // containing pb); in flight while this one is added
-                const int64_t jn = (more || rs[n] == pb) ? j + n : j + n - 1;
-                nb_regs = load_batch<DBL, VT>(P, jn, j1);
+                const bool at = more || rs[n] == pb;
+                const int64_t jn = at ? j + n : j + n - 1;
+                cst = at ? rs[n] : rs[n - 1];
+                nb_regs = load_batch<DBL, LEN, VT>(P, jn, j1);
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const int k = lane + 64 * u;
@@ -372,18 +406,18 @@ rcp_rle_tile_kernel(RcpRleDev P, int p) {
             int32_t pos = pa;
             for (;;) {
                 // the batch: runs j .. j + 127 and the start of run j + 128
-                const int32_t s0 = (int32_t)(nb_regs.g0 - gbl), s1 = (int32_t)(nb_regs.g1 - gbl);
-                rs[lane] = s0;
-                rs[lane + 64] = s1;
-                if (lane == 0) rs[kTBatch] = (int32_t)(nb_regs.g2 - gbl);
+                int32_t s0, s1;
+                batch_starts<LEN>(nb_regs, gbl, cst, rs, &s0, &s1);
                 rv[lane] = nb_regs.v0;
                 rv[lane + 64] = nb_regs.v1;
                 const int n = __popcll(__ballot(s0 < pb)) + __popcll(__ballot(s1 < pb));
                 wave_lds_order();
                 const int32_t be = min(pb, rs[n]);  // this batch covers positions [pos, be)
                 const bool more = be < pb;          // then n == 128 and run j + 128 starts at be
-                const int64_t jn = (more || rs[n] == pb) ? j + n : j + n - 1;  // next batch's first run
-                nb_regs = load_batch<DBL, VT>(P, jn, j1);
+                const bool at = more || rs[n] == pb;
+                const int64_t jn = at ? j + n : j + n - 1;  // next batch's first run
+                cst = at ? rs[n] : rs[n - 1];
+                nb_regs = load_batch<DBL, LEN, VT>(P, jn, j1);
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const int32_t lo = max(ca[u], pos), hi = min(cb[u], be);
@@ -442,9 +476,9 @@ extern "C" hipError_t rcp_rle_scan(const int32_t* lengths, int64_t n_runs, int64
     return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, in, gstart, (int)(n_runs + 1), stream);
 }
 
-template <bool DBL, int KIND>
+template <bool DBL, int KIND, bool LEN>
 static void launch_tiles(const RcpRleDev* P, int p, int64_t grid, hipStream_t stream) {
-    hipLaunchKernelGGL((rcp_rle_tile_kernel<DBL, KIND>), dim3((unsigned)grid), dim3(kTBlock), 0, stream, *P, p);
+    hipLaunchKernelGGL((rcp_rle_tile_kernel<DBL, KIND, LEN>), dim3((unsigned)grid), dim3(kTBlock), 0, stream, *P, p);
 }
 
 extern "C" hipError_t rcp_rle_profile_launch(const RcpRleDev* P, int dbl, size_t lds, hipStream_t stream) {
@@ -453,11 +487,23 @@ extern "C" hipError_t rcp_rle_profile_launch(const RcpRleDev* P, int dbl, size_t
     if (P->n_rows > 0 && P->n_parts > 0) {
         if ((P->ld & (kTRows - 1)) != 0) return hipErrorInvalidValue;  // tiles write whole 16-row segments
         const int64_t grid = (P->n_rows + kTRows - 1) / kTRows;
+        const bool len = P->gstart == nullptr;  // starts from the lengths (the host skipped the scan)
         for (int p = 0; p < P->n_parts; ++p) {
             const int kind = (!dbl && P->part_dense[p]) ? 2 : (P->stat == 1 ? 1 : 0);
-            if (dbl) kind == 1 ? launch_tiles<true, 1>(P, p, grid, stream) : launch_tiles<true, 0>(P, p, grid, stream);
-            else if (kind == 2) launch_tiles<false, 2>(P, p, grid, stream);
-            else kind == 1 ? launch_tiles<false, 1>(P, p, grid, stream) : launch_tiles<false, 0>(P, p, grid, stream);
+            if (kind == 1 && len) return hipErrorInvalidValue;  // median bins search the scanned starts
+            if (dbl) {
+                if (kind == 1) launch_tiles<true, 1, false>(P, p, grid, stream);
+                else if (len) launch_tiles<true, 0, true>(P, p, grid, stream);
+                else launch_tiles<true, 0, false>(P, p, grid, stream);
+            } else if (kind == 2) {
+                if (len) launch_tiles<false, 2, true>(P, p, grid, stream);
+                else launch_tiles<false, 2, false>(P, p, grid, stream);
+            } else if (kind == 1) {
+                launch_tiles<false, 1, false>(P, p, grid, stream);
+            } else {
+                if (len) launch_tiles<false, 0, true>(P, p, grid, stream);
+                else launch_tiles<false, 0, false>(P, p, grid, stream);
+            }
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

@@ -162,6 +162,16 @@ struct DevBuf {
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) {
+            reset();
+            p = o.p;
+            bytes = o.bytes;
+            o.p = nullptr;
+            o.bytes = 0;
+        }
+        return *this;
+    }
     ~DevBuf() { reset(); }
     void reset() {
         if (p) (void)hipFree(p);
@@ -321,6 +331,16 @@ struct rcp_readset {
     DevBuf d_seqlen;
     ReadLayout stranded, merged;
     bool presorted = false;  // the reads came in (chromosome, start) order (no full radix sort)
+    // The stranded layout serves only ignore.strand = FALSE (findOverlaps with strand
+    // compatibility); the default TRUE reads the merged one.  Reads uploaded from the host keep
+    // their device copies here and the stranded layout is built at its first use
+    // (ensure_stranded: a plan with ignore_strand == 0, rcp_readset_info), not by every create.
+    std::mutex mu;
+    bool stranded_ready = false;
+    rcp_reads_desc desc{};  // n, n_chrom, strand_filter of the build
+    DevBuf keep_chrom, keep_start, keep_end, keep_strand;
+    const int32_t *kc = nullptr, *ks = nullptr, *ke = nullptr;
+    const int8_t* kst = nullptr;
     // one device synchronisation before the members' arrays go back to the pool (what hipFree
     // does implicitly): work still queued on any stream that reads them has finished
     ~rcp_readset() { (void)hipDeviceSynchronize(); }
@@ -485,6 +505,33 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
 
 }  // namespace
 
+namespace {
+
+// The stranded layout of a readset whose reads were uploaded from the host, built once at its
+// first use from the kept device copies (which are then released).
+int ensure_stranded(const rcp_readset* crs) {
+    rcp_readset* rs = const_cast<rcp_readset*>(crs);
+    std::lock_guard<std::mutex> lock(rs->mu);
+    if (rs->stranded_ready) return RCP_OK;
+    DeviceGuard g(rs->device);
+    HIP_TRY(g.err);
+    bool presorted = rs->presorted;
+    const int64_t kept = rs->n;
+    const int rc = build_layout(rs, &rs->desc, rs->kc, rs->ks, rs->ke, rs->kst, 0, &rs->stranded, nullptr, &presorted);
+    if (rc) return rc;
+    rs->n = kept;
+    rs->keep_chrom.reset();
+    rs->keep_start.reset();
+    rs->keep_end.reset();
+    rs->keep_strand.reset();
+    rs->kc = rs->ks = rs->ke = nullptr;
+    rs->kst = nullptr;
+    rs->stranded_ready = true;
+    return RCP_OK;
+}
+
+}  // namespace
+
 extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp_readset** out) {
     RCP_TRY
     if (!d || !out) return fail(RCP_EINVAL, "NULL argument");
@@ -590,10 +637,25 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     rc = build_layout(rs.get(), d, pc, ps, pe, pst, 1, &rs->merged, s, &presorted);
     if (rc) return rc;
     PLAN_MARK("merged layout");
-    rc = build_layout(rs.get(), d, pc, ps, pe, pst, 0, &rs->stranded, s, &presorted);
-    if (rc) return rc;
-    PLAN_MARK("stranded layout");
     rs->presorted = presorted;
+    rs->desc = *d;
+    if (d->on_device) {
+        // the caller's device arrays are not ours to keep: the stranded layout now
+        rc = build_layout(rs.get(), d, pc, ps, pe, pst, 0, &rs->stranded, s, &presorted);
+        if (rc) return rc;
+        rs->stranded_ready = true;
+        PLAN_MARK("stranded layout");
+    } else {
+        // keep the uploaded copies for a later stranded layout (ensure_stranded)
+        rs->keep_chrom = std::move(in_chrom);
+        rs->keep_start = std::move(in_start);
+        rs->keep_end = std::move(in_end);
+        rs->keep_strand = std::move(in_strand);
+        rs->kc = pc;
+        rs->ks = ps;
+        rs->ke = pe;
+        rs->kst = pst;
+    }
     HIP_TRY(rs->d_seqlen.alloc(8 * d->n_chrom));
     HIP_TRY(hipMemcpyAsync(rs->d_seqlen.p, rs->seqlen.data(), 8 * d->n_chrom, hipMemcpyHostToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -634,7 +696,11 @@ extern "C" int rcp_readset_info(const rcp_readset* rs, int64_t* n_reads, int64_t
     RCP_TRY
     if (!rs) return fail(RCP_EINVAL, "NULL readset");
     if (n_reads) *n_reads = rs->n;
-    if (stream_off) std::memcpy(stream_off, rs->stranded.h_stream_off.data(), 8 * rs->stranded.h_stream_off.size());
+    if (stream_off) {
+        const int rc = ensure_stranded(rs);
+        if (rc) return rc;
+        std::memcpy(stream_off, rs->stranded.h_stream_off.data(), 8 * rs->stranded.h_stream_off.size());
+    }
     return RCP_OK;
     RCP_CATCH
 }
@@ -851,6 +917,10 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
 #if RCP_PLAN_TIMING
     PlanTimer ptimer;
 #endif
+    if (!rows->ignore_strand) {  // findOverlaps with strand compatibility: the stranded layout
+        const int rc0 = ensure_stranded(rs);
+        if (rc0) return rc0;
+    }
     auto plan = std::make_unique<rcp_plan>();
     plan->rs = rs;
     Builder B;

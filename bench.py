@@ -57,11 +57,12 @@ def parse():
     ap.add_argument("--verify-gather", action="store_true",
                     help="N > 1: rank 0 also runs the whole workload alone and checks the gathered matrix bit for bit")
     ap.add_argument("--no-e2e", action="store_true", help="skip the one-off host-to-host timing")
-    ap.add_argument("--inflight", default="1", choices=["auto", "1", "2", "3"],
+    ap.add_argument("--inflight", default="auto", choices=["auto", "1", "2", "3"],
                     help="samples in flight: D DISTINCT samples (independent read sets over the same region "
                          "table, as profileMatrix loops over a recoup input list) on D HIP streams, step k "
-                         "= one complete pass of sample k %% D; auto: the fastest of 1, 2, 3.  The one-sample "
-                         "pass time is always reported beside it (single_pass_ms)")
+                         "= one complete pass of sample k %% D; auto (default): the fastest of 1, 2, 3, "
+                         "timed on every rank (max over ranks) so all ranks run the same D.  The "
+                         "one-sample pass time is always reported beside it (single_pass_ms)")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default profiles/traffic_<config>.json")
     return ap.parse_args()
@@ -280,6 +281,11 @@ def main():
         passes(d, max(args.steps, 10))
         torch.cuda.synchronize()
         tune[d] = (time.perf_counter() - t) / max(args.steps, 10) * 1e3
+    if dist and len(tune) > 1:  # one D for every rank: the per-D times, max over ranks
+        tt = torch.tensor([tune[k] for k in sorted(tune)], dtype=torch.float64,
+                          device=dev if backend == "nccl" else "cpu")
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        tune = {k: float(v) for k, v in zip(sorted(tune), tt.tolist())}
     D = min(tune, key=tune.get) if args.inflight == "auto" else len(plans)
 
     # ---- timed region: exactly K steps between barrier + synchronize

@@ -174,14 +174,17 @@ typedef struct {
 RCP_API int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
                     rcp_plan** out);
 /* Plan options (NULL = defaults).  pileup_kernel: RCP_KERNEL_AUTO picks the lean kernel
- * (pile + store waves) where every row is one plain range with uniform power-of-two bins,
- * else the general kernel; RCP_KERNEL_GENERAL forces the general kernel; RCP_KERNEL_LEAN_ANY
+ * (pile + store waves) where every row is one plain range with uniform power-of-two bins
+ * (binned plans: from 36000 rows up; fewer rows, e.g. one GPU's 1/8 of a region table, run
+ * faster on the general kernel's smaller workgroup tiles), else the general kernel;
+ * RCP_KERNEL_LEAN takes the lean kernel wherever AUTO's shape rule allows, at any row count;
+ * RCP_KERNEL_GENERAL forces the general kernel; RCP_KERNEL_LEAN_ANY
  * also routes other mean plans whose chunks fit one wave pass through the lean kernel's
  * general-bins mode; RCP_KERNEL_ROWS forces the row-wave kernel (whole rows per wave: AUTO takes
  * it for mean plans with multi-range rows).  All choices give bit-identical results.  heavy_threshold: candidate
  * reads per column chunk above which a skewed row is piled by many workgroups first
  * (-1 = default 4096, 0 = never).  out_ld: see the field. */
-enum { RCP_KERNEL_AUTO = 0, RCP_KERNEL_GENERAL = 1, RCP_KERNEL_LEAN_ANY = 2, RCP_KERNEL_ROWS = 3 };
+enum { RCP_KERNEL_AUTO = 0, RCP_KERNEL_GENERAL = 1, RCP_KERNEL_LEAN_ANY = 2, RCP_KERNEL_ROWS = 3, RCP_KERNEL_LEAN = 4 };
 typedef struct {
     int32_t pileup_kernel;
     int32_t heavy_threshold;

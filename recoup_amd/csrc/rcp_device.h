@@ -149,6 +149,10 @@ struct RcpPlanDev {
     // coverage (CSR) mode
     const int64_t* csr_off;     // non-null: write per-row depth into csr (calcCoverage)
     int32_t* csr_out;
+    // non-null: each wave adds the Rle run starts inside its sub-chunk to csr_runs[row] (a
+    // sub-chunk's first position counts only at the row's position 0; rcp_rle_seams_kernel
+    // adds the seams between sub-chunks): the run counts of calcCoverage's Rle list
+    unsigned long long* csr_runs;
     // skewed depth: rows with more than heavy_threshold candidate reads are piled up
     // first by many workgroups (heavy slices) into a global difference array
     uint32_t* ncand;            // [n_rows] candidate reads (locate output)

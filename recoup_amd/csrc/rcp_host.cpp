@@ -37,6 +37,12 @@
 #endif
 constexpr int kLeanItemsPerWg = RCP_LEAN_ITEMS_PER_WG;  // work items per persistent workgroup, at least
 constexpr int kLeanMinChunkBins = 64;                   // no column chunks narrower than this
+// AUTO keeps binned plans of fewer rows on the general kernel: a lean item is 64 rows, the
+// general kernel's workgroup 32, and with about one item per workgroup the item's read round
+// trips set the pass.  C4 shards (1000 bins of 2 bp), ms per pass lean / general: 25 k rows
+// 0.141 / 0.133, 33 k 0.160 / 0.154, 40 k 0.187 / 0.197, 50 k 0.217 / 0.232; per-base C5
+// shards stay lean (12.5 k rows: 0.317 / 0.435).  profiles/r03/pipeline/small_shard_kernels.log
+constexpr int kLeanMinRowsBinned = 36000;
 
 #ifndef RCP_ROWS_AUTO
 #define RCP_ROWS_AUTO 1  // plans with multi-range rows take the row-wave pileup kernel
@@ -74,6 +80,8 @@ hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* 
 hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, int64_t* d_count,
                               int64_t* d_run_off, void* temp, size_t* temp_bytes, int32_t* d_values,
                               int32_t* d_lengths, int pass, hipStream_t stream);
+hipError_t rcp_rle_seams_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, const uint8_t* d_valid,
+                             int32_t chunk_bins, int32_t chunk_cap, int64_t* d_count, hipStream_t stream);
 hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t* off, const int32_t* pmax, int32_t* out,
                                     hipStream_t stream);
 hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const int64_t* dir_off, const int64_t* off,
@@ -897,7 +905,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     if (!rs || !rows || !out) return fail(RCP_EINVAL, "NULL argument");
     const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, 0, 0, {0, 0, 0}};
     if (!opts) opts = &default_opts;
-    if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_ROWS)
+    if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_LEAN)
         return fail(RCP_EINVAL, "pileup_kernel = %d", opts->pileup_kernel);
     *out = nullptr;
     const rcp_bins_desc coverage_only{};  // bins == NULL: a calcCoverage-only plan
@@ -1136,6 +1144,11 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
             if ((int64_t)pt.chunk_bins * w > P.chunk_cap) base = false;
         }
         bool lean = base && lean_ok && stage_cap <= rcp_lean_max_bins();
+        if (lean && kind == RCP_KERNEL_AUTO && R < kLeanMinRowsBinned) {
+            bool binned = true;
+            for (int p = 0; p < P.n_parts; ++p) binned = binned && !P.part[p].per_base;
+            if (binned) lean = false;
+        }
         for (int r = 0; lean && r < R; ++r) {
             const int32_t j0 = B.row_seg[r], j1 = B.row_seg[r + 1];
             if (j1 - j0 > 1) lean = false;
@@ -1352,6 +1365,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.interp_scratch = plan->scratch.as<double>();
     P.csr_off = nullptr;
     P.csr_out = nullptr;
+    P.csr_runs = nullptr;
     // row-wave plans stage their bins row-major (whole lines per row) and transpose once
     P.rm = nullptr;
     if (P.lean == 3 && R > 0 && P.n_cols > 0) {
@@ -1735,16 +1749,12 @@ extern "C" int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices
     RCP_CATCH
 }
 
-extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t* d_cov, uint8_t* d_valid,
-                                 void* hip_stream) {
-    RCP_TRY
-    if (!plan || !out_off) return fail(RCP_EINVAL, "NULL argument");
-    DeviceGuard g(plan->rs->device);
-    HIP_TRY(g.err);
-    hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    for (int r = 0; r < plan->n_rows; ++r)
-        if (out_off[r + 1] - out_off[r] != plan->row_len[r])
-            return fail(RCP_EINVAL, "out_off does not match the row lengths at row %d", r);
+namespace {
+
+// calcCoverage of every row into CSR depth (d_off: device [n_rows + 1]); with d_runs (device
+// [n_rows + 1], zeroed here) also each row's Rle run count, 0 for NULL rows
+int calc_coverage_dev(rcp_plan* plan, const int64_t* d_off, int32_t* d_cov, uint8_t* d_valid, int64_t* d_runs,
+                      hipStream_t s) {
     // one per-base part over the whole row, chunked by the plan's chunk capacity
     begin_exec(plan);
     RcpPlanDev P = plan->dev;
@@ -1759,15 +1769,36 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
     P.n_chunks_total = pt.n_chunks;
     P.crange = nullptr;  // sized for the plan's chunks, not these
     P.cw_len = -1;
-    DevBuf d_off;
-    HIP_TRY(d_off.alloc(8 * (plan->n_rows + 1)));
-    HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * (plan->n_rows + 1), hipMemcpyHostToDevice, s));
-    P.csr_off = d_off.as<int64_t>();
+    P.csr_off = d_off;
     P.csr_out = d_cov;
     P.valid_out = d_valid;
+    P.csr_runs = reinterpret_cast<unsigned long long*>(d_runs);
+    if (d_runs) HIP_TRY(hipMemsetAsync(d_runs, 0, 8 * ((size_t)plan->n_rows + 1), s));
     HIP_TRY(rcp_launch_locate(&P, s));
     HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
+    if (d_runs) HIP_TRY(rcp_rle_seams_dev(plan->n_rows, d_off, d_cov, d_valid, pt.chunk_bins, P.chunk_cap, d_runs, s));
+    return RCP_OK;
+}
+
+}  // namespace
+
+
+extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t* d_cov, uint8_t* d_valid,
+                                 void* hip_stream) {
+    RCP_TRY
+    if (!plan || !out_off) return fail(RCP_EINVAL, "NULL argument");
+    DeviceGuard g(plan->rs->device);
+    HIP_TRY(g.err);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    for (int r = 0; r < plan->n_rows; ++r)
+        if (out_off[r + 1] - out_off[r] != plan->row_len[r])
+            return fail(RCP_EINVAL, "out_off does not match the row lengths at row %d", r);
+    DevBuf d_off;
+    HIP_TRY(d_off.alloc(8 * (plan->n_rows + 1)));
+    HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * (plan->n_rows + 1), hipMemcpyHostToDevice, s));
+    const int rc = calc_coverage_dev(plan, d_off.as<int64_t>(), d_cov, d_valid, nullptr, s);
+    if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s));  // d_off is released on return
     return RCP_OK;
     RCP_CATCH
@@ -1869,19 +1900,29 @@ extern "C" int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows
     if (n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "%lld coverage positions", (long long)n);
     hipStream_t s = nullptr;
     {
-        PoolBuf d_cov(s), d_off(s);
+        // the pileup counts each row's runs as it writes the depth (csr_runs, + the seams
+        // between its wave sub-chunks); a scan of the counts places every row's runs
+        PoolBuf d_cov(s), d_off(s), d_count(s), temp(s);
         HIP_TRY(d_cov.alloc(4 * std::max<int64_t>(n, 1)));
         HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
+        HIP_TRY(d_count.alloc(8 * ((size_t)R + 1)));
         HIP_TRY(res->valid.alloc(std::max<int32_t>(R, 1)));
         HIP_TRY(res->run_off.alloc(8 * ((size_t)R + 1)));
-        rc = rcp_calc_coverage(plan, off.data(), d_cov.as<int32_t>(), res->valid.as<uint8_t>(), nullptr);
+        HIP_TRY(hipMemcpyAsync(d_off.p, off.data(), 8 * ((size_t)R + 1), hipMemcpyHostToDevice, s));
+        rc = calc_coverage_dev(plan, d_off.as<int64_t>(), d_cov.as<int32_t>(), res->valid.as<uint8_t>(),
+                               d_count.as<int64_t>(), s);
         if (rc) return rc;
         rc = rcp_plan_status(plan, nullptr);
         if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(d_off.p, off.data(), 8 * ((size_t)R + 1), hipMemcpyHostToDevice, s));
+        size_t tb = 0;
+        HIP_TRY(rcp_rle_encode_dev(R, nullptr, nullptr, d_count.as<int64_t>(), res->run_off.as<int64_t>(), nullptr, &tb,
+                                   nullptr, nullptr, 0, s));
+        HIP_TRY(temp.alloc(std::max<size_t>(tb, 1)));
+        HIP_TRY(rcp_rle_encode_dev(R, nullptr, nullptr, d_count.as<int64_t>(), res->run_off.as<int64_t>(), temp.p, &tb,
+                                   nullptr, nullptr, 3, s));
         int64_t nr = 0;
-        rc = rle_encode_device(R, d_off.as<int64_t>(), d_cov.as<int32_t>(), res->run_off.as<int64_t>(), &nr, s);
-        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(&nr, res->run_off.as<int64_t>() + R, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
         res->n_runs = nr;
         HIP_TRY(res->values.alloc(4 * (size_t)std::max<int64_t>(nr, 1)));
         HIP_TRY(res->lengths.alloc(4 * (size_t)std::max<int64_t>(nr, 1)));

@@ -1623,8 +1623,23 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
                 scan_wave<!(MEDIAN || CSR)>(diff, per);
                 lds_order();
                 if (CSR) {
-                    for (int32_t k = k0 + s0 + lane; k < k0 + s0 + sn; k += 64)
-                        P.csr_out[P.csr_off[r] + k] = diff[lp(k - k0 - s0, sh)];
+                    int32_t* orow = P.csr_out + P.csr_off[r];
+                    // run starts after this sub-chunk's first position: position q - 1 is the
+                    // lane below (wave_shr:1), lane 0's the last lane of the step before
+                    int32_t runs = 0, carry = 0;
+                    for (int32_t q0 = 0; q0 < sn; q0 += 64) {
+                        const int32_t q = q0 + lane;
+                        const bool in = q < sn;
+                        const int32_t v = in ? diff[lp(q, sh)] : 0;
+                        if (in) orow[k0 + s0 + q] = v;
+                        const int32_t pv = __builtin_amdgcn_update_dpp(carry, v, 0x138, 0xf, 0xf, false);
+                        runs += (in && q > 0 && v != pv) ? 1 : 0;
+                        carry = __builtin_amdgcn_readlane(v, 63);
+                    }
+                    if (P.csr_runs) {  // kernel argument: scalar branch
+                        runs = wave_sum(runs) + (k0 + s0 == 0 ? 1 : 0);
+                        if (lane == 0) atomicAdd(P.csr_runs + r, (unsigned long long)runs);
+                    }
                 } else if (MEDIAN) {
                     for (int32_t k = k0 + lane; k < kend; k += 64) {
                         const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
@@ -2860,6 +2875,7 @@ __global__ void __launch_bounds__(64 * kRleWaves) rcp_rle_emit_kernel(int32_t n_
     const int r = blockIdx.x * kRleWaves + (threadIdx.x >> 6);
     if (r >= n_rows) return;
     const int lane = threadIdx.x & 63;
+    if (run_off[r + 1] == run_off[r]) return;  // no runs: an empty or NULL row
     const int64_t a = off[r], b = off[r + 1];
     const uint64_t below = (1ull << lane) - 1;  // lanes < this one
     int64_t k = run_off[r];                      // next run index
@@ -2898,12 +2914,45 @@ __global__ void __launch_bounds__(64 * kRleWaves) rcp_rle_emit_kernel(int32_t n_
     if (pend >= 0 && lane == 0) lengths[pend] = (int32_t)(b - pstart);
 }
 
+// The run starts the coverage pileup could not see (rcp_pileup_kernel's csr_runs): the seams
+// between the wave sub-chunks of chunk_cap positions inside the column chunks of chunk_bins
+// positions, a thread per row (most rows have one or two seams); NULL rows (valid 0) keep no
+// runs.
+__global__ void __launch_bounds__(kBlock) rcp_rle_seams_kernel(int32_t n_rows, const int64_t* __restrict__ off,
+                                                             const int32_t* __restrict__ cov,
+                                                             const uint8_t* __restrict__ valid, int32_t chunk_bins,
+                                                             int32_t chunk_cap, unsigned long long* __restrict__ count) {
+    const int r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= n_rows || !valid[r]) return;
+    const int64_t a = off[r];
+    const int64_t L = off[r + 1] - a;
+    unsigned long long c = 0;
+    for (int64_t k0 = 0; k0 < L; k0 += chunk_bins)
+        for (int64_t p = k0 == 0 ? chunk_cap : k0; p < k0 + chunk_bins && p < L; p += chunk_cap)
+            c += cov[a + p] != cov[a + p - 1] ? 1 : 0;
+    if (c) count[r] += c;  // the pileup's atomics have completed (earlier launch)
+}
+
+extern "C" hipError_t rcp_rle_seams_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov,
+                                        const uint8_t* d_valid, int32_t chunk_bins, int32_t chunk_cap,
+                                        int64_t* d_count, hipStream_t stream) {
+    if (n_rows <= 0) return hipSuccess;
+    if (chunk_bins <= 0 || chunk_cap <= 0) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)((n_rows + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(rcp_rle_seams_kernel, dim3(grid), dim3(kBlock), 0, stream, n_rows, d_off, d_cov, d_valid,
+                       chunk_bins, chunk_cap, reinterpret_cast<unsigned long long*>(d_count));
+    return hipGetLastError();
+}
+
 extern "C" hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, int64_t* d_count,
                                          int64_t* d_run_off, void* temp, size_t* temp_bytes, int32_t* d_values,
                                          int32_t* d_lengths, int pass, hipStream_t stream) {
-    // pass 0: temp size of the scan; 1: count + scan (d_run_off[n_rows] = total); 2: emit
+    // pass 0: temp size of the scan; 1: count + scan (d_run_off[n_rows] = total); 2: emit;
+    // 3: scan of counts made elsewhere (d_count[n_rows] must be 0)
     if (pass == 0)
         return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, d_count, d_run_off, (int)n_rows + 1, stream);
+    if (pass == 3)
+        return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, d_count, d_run_off, (int)n_rows + 1, stream);
     const unsigned grid = (unsigned)((n_rows + kRleWaves - 1) / kRleWaves);
     if (pass == 1) {
         hipError_t e = hipMemsetAsync(d_count + n_rows, 0, 8, stream);

@@ -20,7 +20,7 @@ STRAND = {"+": 0, "-": 1, "*": 2}
 STAT = {"mean": 0, "median": 1}
 INTERP = {"auto": 0, "spline": 1, "linear": 2, "neighborhood": 3}
 RNG = {"Rejection": 0, "Rounding": 1}
-KERNEL = {"auto": 0, "general": 1, "lean_any": 2, "rows": 3}
+KERNEL = {"auto": 0, "general": 1, "lean_any": 2, "rows": 3, "lean": 4}
 
 
 def _stream(device, stream):
@@ -211,7 +211,7 @@ class Plan:
     """One fused coverage -> profile pass of ``rows`` over ``readset`` with ``bins``."""
 
     def __init__(self, readset, rows, bins, kernel="auto", heavy_threshold=-1, out_ld=0, min_col_chunks=0):
-        """``kernel``: "auto" | "general" | "lean_any" | "rows" (rcp_plan_opts.pileup_kernel; every choice
+        """``kernel``: "auto" | "general" | "lean" | "lean_any" | "rows" (rcp_plan_opts.pileup_kernel; every choice
         gives bit-identical results); ``heavy_threshold``: -1 default, 0 off; ``out_ld``: the
         output's column stride, 0 = n_rows, "padded" = the next multiple of 16 (whole 128-B
         lines per 16-row column segment), or any value >= n_rows."""

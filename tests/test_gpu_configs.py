@@ -80,7 +80,7 @@ def test_c4_reduced_heavy_rows(gpu):
     d = synthetic.c4(device=DEV, n_regions=20_000, n_reads=20_000_000)
     reg = d["regions"]
     rows = single_rows(reg)
-    plan, out, valid = run(d["reads"], d["seqlen"], rows, Bins([("whole", d["n_bins"])]))
+    plan, out, valid = run(d["reads"], d["seqlen"], rows, Bins([("whole", d["n_bins"])]), kernel="lean")
     assert plan.info["pileup_kernel"] == 1  # the lean kernel, as in the bench
     assert plan.heavy_rows() > 0            # Pareto hot peaks go through the heavy slices
     ix = host_index(d["reads"], d["seqlen"])

@@ -15,12 +15,13 @@ pytestmark = pytest.mark.gpu
 
 
 def plans(reads, seqlen, rows, bins, strand_filter=None, lean_mode=None, heavy_threshold=-1):
-    """(lean result, general result, lean kernel id, expected) for one configuration;
+    """(lean result, general result, lean kernel id, expected) for one configuration; the lean
+    kernel is forced ("lean": these row tables are below AUTO's row floor for binned plans);
     lean_mode "lean_any" opts in to the general-bins mode."""
     from recoup_amd.engine import Plan, ReadSet
     from tests import oracle_rows
     rs = ReadSet(*reads, seqlen, device=0, strand_filter=strand_filter)
-    lean = Plan(rs, rows, bins, kernel=lean_mode or "auto", heavy_threshold=heavy_threshold)
+    lean = Plan(rs, rows, bins, kernel=lean_mode or "lean", heavy_threshold=heavy_threshold)
     general = Plan(rs, rows, bins, kernel="general", heavy_threshold=heavy_threshold)
     assert general.info["pileup_kernel"] == 0
     r_lean, r_gen = lean.run(), general.run()
@@ -126,14 +127,19 @@ def test_lean_kernel_choice(gpu):
     seg_off = np.array([0, 2, 3], np.int64)
     exons = RowTable(seg_off, np.zeros(3, np.int32), np.array([1000, 3000, 9000]), np.array([1999, 3999, 10999]),
                      np.zeros(3, np.int8), seg_group=np.zeros(3, np.int8), group_is_list=np.array([1, 0, 0, 0], np.uint8))
-    for mode, other in (("auto", 0), ("lean_any", 2)):
+    for mode, other in (("lean", 0), ("lean_any", 2)):
         assert Plan(rs, rows, Bins([("whole", 150)]), kernel=mode).info["pileup_kernel"] == other   # dif != 0
         assert Plan(rs, rows, Bins([("whole", 200)]), kernel=mode).info["pileup_kernel"] == other   # bs = 10
         # exon lists: the row-wave kernel under auto (tests/test_gpu_rows.py)
-        assert Plan(rs, exons, Bins([("whole", 100)]), kernel=mode).info["pileup_kernel"] == (3 if mode == "auto" else 2)
+        assert Plan(rs, exons, Bins([("whole", 100)]), kernel=mode).info["pileup_kernel"] == (0 if mode == "lean" else 2)
         assert Plan(rs, rows, Bins([("whole", 1000)], stat="median"), kernel=mode).info["pileup_kernel"] == 0
         assert Plan(rs, rows, Bins([("whole", 1000)]), kernel=mode).info["pileup_kernel"] == 1
         assert Plan(rs, rows, Bins([("whole", 1000)]), kernel="general").info["pileup_kernel"] == 0
+    # AUTO: exon lists take the row-wave kernel; binned single-range plans below 36000 rows the
+    # general kernel, per-base ones the lean kernel at any row count
+    assert Plan(rs, exons, Bins([("whole", 100)])).info["pileup_kernel"] == 3
+    assert Plan(rs, rows, Bins([("whole", 1000)])).info["pileup_kernel"] == 0
+    assert Plan(rs, rows, Bins([("whole", 0, 2000)])).info["pileup_kernel"] == 1
 
 
 @pytest.mark.parametrize("width,n_bins", [(2000, 150), (4000, 200), (1500, 256), (3000, 64), (2000, 1000)])
@@ -193,7 +199,7 @@ def test_lean_more_column_chunks(gpu, chunks):
     reads = make_reads(rng, 100_000)
     rows = single_rows(rng, 300, 2000)
     rs = ReadSet(*reads, CHROM_LEN, device=0)
-    base = Plan(rs, rows, Bins([("whole", 1000)]))
-    more = Plan(rs, rows, Bins([("whole", 1000)]), min_col_chunks=chunks)
+    base = Plan(rs, rows, Bins([("whole", 1000)]), kernel="lean")
+    more = Plan(rs, rows, Bins([("whole", 1000)]), kernel="lean", min_col_chunks=chunks)
     assert base.info["pileup_kernel"] == 1 and more.info["pileup_kernel"] == 1
     same(more.run(), base.run())

@@ -152,3 +152,42 @@ def test_flanks_per_base_and_errors(gpu):
     # neighborhood of fewer than 4 values: R raises an error
     with pytest.raises(ra.SemanticError):
         profile_rle([np.arange(3, dtype=np.int32)], Bins([("whole", 4)], interp="neighborhood"))
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_coverage_rle_runs_across_sub_chunk_seams(gpu, seed):
+    """rcp_coverage_rle counts each row's runs inside the coverage pileup (a wave per sub-chunk
+    of the row's positions) plus the seams between sub-chunks: rows shorter than, equal to and
+    many times one wave chunk (1023 / 2047 / 4095 positions), flat rows (no reads: one run),
+    deep hot spots and NULL rows give the oracle's runs exactly; a NULL row keeps no runs."""
+    from recoup_amd.engine import ReadSet, RowTable, coverage_rle_host
+    rng = np.random.default_rng(100 + seed)
+    reads = make_reads(rng, 80_000, widths=(5, 300))
+    gap = ~((reads[0] == 0) & (reads[2] >= 100_000) & (reads[1] <= 110_000))
+    reads = tuple(x[gap] for x in reads)
+    lens = np.array([1, 2, 63, 64, 1023, 1024, 1025, 2046, 2047, 2048, 2049, 4095, 4096, 4097, 8191, 12_000,
+                     30_000, 65_537], np.int64)
+    R = 120
+    w = np.concatenate([lens, rng.integers(1, 9000, R - len(lens))])
+    rng.shuffle(w)
+    chrom = rng.integers(0, 2, R).astype(np.int32)
+    start = np.array([rng.integers(1, CHROM_LEN[c] - x + 1) for c, x in zip(chrom, w)], np.int64)
+    start[0], start[1] = -50, 0                     # negative index -> NULL; 0 -> dropped index
+    start[2] = CHROM_LEN[chrom[2]] - w[2] // 2 + 1  # runs past the chromosome -> NULL
+    chrom[3], start[3], w[3] = 0, 101_000, 5000     # no reads there: one run of 0
+    strand = rng.integers(0, 3, R).astype(np.int8)
+    rows = RowTable.from_ranges(chrom, start, start + w - 1, strand)
+    ix = oracle_rows.index_for(reads, CHROM_LEN)
+    cov = oracle_rows.row_coverage(ix, rows)
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    run_off, values, lengths, valid = coverage_rle_host(rs, rows)
+    assert len(run_off) == R + 1 and run_off[0] == 0
+    for r in range(R):
+        a, b = run_off[r], run_off[r + 1]
+        if cov[r] is None:
+            assert not valid[r] and a == b
+            continue
+        assert valid[r]
+        v, ln = _runs(cov[r])
+        np.testing.assert_array_equal(values[a:b], v)
+        np.testing.assert_array_equal(lengths[a:b], ln)

@@ -149,5 +149,5 @@ def test_repeated_executions_and_kernel_choice(gpu):
     assert Plan(rs, rows, med).info["pileup_kernel"] == 0
     single = single_rows(rng, 50, 2000)
     assert Plan(rs, single, Bins([("whole", 150)])).info["pileup_kernel"] == 0
-    assert Plan(rs, single, Bins([("whole", 1000)])).info["pileup_kernel"] == 1
+    assert Plan(rs, single, Bins([("whole", 1000)]), kernel="lean").info["pileup_kernel"] == 1
     assert Plan(rs, rows, bins, kernel="general").info["pileup_kernel"] == 0

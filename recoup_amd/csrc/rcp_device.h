@@ -141,6 +141,7 @@ struct RcpPlanDev {
                                 //    fewer for small row tables, so more workgroups fill the chip)
     int32_t lean;               // 1: every row is one plain range with uniform power-of-two bins
                                 //    of one wave chunk -> rcp_pileup_lean_kernel
+    int32_t lean_rounds;        // lean kernel: rounds of 16 rows per work item (2; else kRounds)
     // row-wave kernel (lean == 3): its rows' bins go row-major into rm (n_rows x n_cols, whole
     // lines per row); the last wave to finish a 16-row tile writes the tile's rows of every
     // column into the R column-major output as whole 128-B lines (a row-wave store straight

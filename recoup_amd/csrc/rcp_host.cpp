@@ -42,7 +42,21 @@ constexpr int kLeanMinChunkBins = 64;                   // no column chunks narr
 // trips set the pass.  C4 shards (1000 bins of 2 bp), ms per pass lean / general: 25 k rows
 // 0.141 / 0.133, 33 k 0.160 / 0.154, 40 k 0.187 / 0.197, 50 k 0.217 / 0.232; per-base C5
 // shards stay lean (12.5 k rows: 0.317 / 0.435).  profiles/r03/pipeline/small_shard_kernels.log
-constexpr int kLeanMinRowsBinned = 36000;
+#ifndef RCP_LEAN_MIN_ROWS_BINNED
+#define RCP_LEAN_MIN_ROWS_BINNED 36000
+#endif
+constexpr int kLeanMinRowsBinned = RCP_LEAN_MIN_ROWS_BINNED;
+// Per-base lean plans (baseCoverageMatrix: every part one column per position) take work items
+// of two 16-row rounds instead of four: ms per pass four / two rounds, C5 0.752 / 0.673, its
+// 1/8 shard 0.272 / 0.253, 1/4 0.319 / 0.290; binned C4 is slower with them (0.553 / 0.563
+// pileup; 1/8 shard 0.107 / 0.115).  profiles/r03/pipeline/lean_rounds_ab.log
+#ifndef RCP_LEAN_ROUNDS2
+#define RCP_LEAN_ROUNDS2 1  // 0: four rounds for every lean plan, 2: two for every lean plan (A/B)
+#endif
+
+#ifndef RCP_AUTO_GEN
+#define RCP_AUTO_GEN 0  // 1: AUTO also takes the lean kernel's general-bins mode (A/B only)
+#endif
 
 #ifndef RCP_ROWS_AUTO
 #define RCP_ROWS_AUTO 1  // plans with multi-range rows take the row-wave pileup kernel
@@ -1154,8 +1168,14 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
             if (j1 - j0 > 1) lean = false;
             else if (j1 == j0 + 1 && (B.segs[j0].multi || !B.segs[j0].query_ok)) lean = false;
         }
-        const bool gen = !lean && base && kind == RCP_KERNEL_LEAN_ANY && stage_cap <= rcp_lean_gen_max_bins();
+        const bool gen = !lean && base && (kind == RCP_KERNEL_LEAN_ANY || (RCP_AUTO_GEN && kind == RCP_KERNEL_AUTO)) &&
+                         stage_cap <= rcp_lean_gen_max_bins();
         P.lean = lean ? 1 : (gen ? 2 : 0);
+        {
+            bool per_base = true;
+            for (int p = 0; p < P.n_parts; ++p) per_base = per_base && P.part[p].per_base;
+            P.lean_rounds = P.lean && ((RCP_LEAN_ROUNDS2 == 1 && per_base) || RCP_LEAN_ROUNDS2 == 2) ? 2 : 0;
+        }
         // row-wave kernel (lean == 3): mean bins of any layout, every bin inside one window;
         // AUTO takes it for plans with multi-range rows (coverageRnaRef, genebody + flanks)
         bool rows_ok = !cov_only && bins->stat == RCP_STAT_MEAN && kind != RCP_KERNEL_GENERAL && !lean;
@@ -1176,7 +1196,8 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, rs->device) != hipSuccess || cus <= 0)
             cus = 256;
         const int64_t grid = (2 * (int64_t)cus + 7) / 8 * 8;
-        const int64_t tiles = ((int64_t)R + rcp_tile_rows() - 1) / rcp_tile_rows();
+        const int64_t trows = P.lean_rounds == 2 ? 32 : rcp_tile_rows();
+        const int64_t tiles = ((int64_t)R + trows - 1) / trows;
         auto can_split = [&]() {
             if (P.n_chunks_total * 2 > RCP_MAX_CRANGE_CHUNKS) return false;
             for (int p = 0; p < P.n_parts; ++p)
@@ -1388,7 +1409,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         while (P.rounds > 1 &&
                (int64_t)((R + tile * P.rounds - 1) / (tile * P.rounds)) * P.n_chunks_total < 2 * (int64_t)cus)
             P.rounds /= 2;
-        plan->tile_rows = P.lean ? rcp_tile_rows() : tile * P.rounds;
+        plan->tile_rows = P.lean ? (P.lean_rounds == 2 ? 2 * tile : rcp_tile_rows()) : tile * P.rounds;
     }
     plan->grid = (int64_t)((R + plan->tile_rows - 1) / plan->tile_rows) * P.n_chunks_total;
     if (plan->lds > 160 * 1024) return fail(RCP_EUNSUPPORTED, "plan needs %zu B of LDS", plan->lds);

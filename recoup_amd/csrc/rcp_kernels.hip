@@ -1394,8 +1394,14 @@ __device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart
     return m;
 }
 
+#ifndef RCP_GEN_ABL
+#define RCP_GEN_ABL 0  // timing ablations only (wrong results): 1 no output stores, 2 no read loads / adds
+#endif
+#ifndef RCP_GEN_WPE
+#define RCP_GEN_WPE 4
+#endif
 template <bool MEDIAN, bool CSR>
-__global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4))) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
+__global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RCP_GEN_WPE))) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
                                                             int64_t* __restrict__ binsum) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int T = kTile;
@@ -1445,7 +1451,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     [[maybe_unused]] const int n_steps = kRowsPerWave * rounds;
     auto prefetch = [&](int i, int2* dst) {
         const RowMeta m = uniform_meta(meta[i]);
-        const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
+        const uint32_t n = (m.flag == 0 && m.fast && !(RCP_GEN_ABL & 2)) ? fast_candidates(m) : 0;
         if (n) {  // wave-uniform
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -1464,6 +1470,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     // and column quads t / 16, t / 16 + 32, ...: one 16-B stage read feeds four stores, and
     // the 16 lanes of a quad column write 16 consecutive rows (128 B) of one column.
     auto flush = [&](int rd) {
+        if (RCP_GEN_ABL & 1) return;
         const int rbase = rd * T;
         const int ii = tid & (T - 1);
         const int r = row0 + rbase + ii;
@@ -1584,7 +1591,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
                     carry = wave_sum(carry);
                     for (int q = lane; q <= sn; q += 64) diff[lp(q, sh)] = g[base + q] + (q == 0 ? carry : 0);
                 } else if (m.fast && whole) {
-                    const uint32_t n = fast_candidates(m);
+                    const uint32_t n = (RCP_GEN_ABL & 2) ? 0u : fast_candidates(m);
                     // batch q0 + 256 is loaded while batch q0 is added
                     for (uint32_t q0 = 0; q0 < n; q0 += 256) {
                         int2 nx[4];
@@ -2057,8 +2064,7 @@ constexpr int kLStoreWaves = RCP_LSTORE_WAVES;
 constexpr int kLBlock = 64 * (kPWaves + kLStoreWaves);
 constexpr int kLQuads = 64 * kLStoreWaves / kTile;  // column quads per store pass
 constexpr int kLMaxPass = 8;                        // stage_cap <= 4 * kLQuads * kLMaxPass
-static_assert(kRows == 64 && kRounds >= 2, "store wave 0 decodes one row per lane; the next item's "
-                                            "metadata is published one round before it is read");
+static_assert(kRows == 64 && kRounds >= 2, "store wave 0 decodes one row per lane");
 
 // Row metadata of the lean kernel (64 B): w0 = flag | fast << 2 | rev << 3 | log2(bin) << 4
 // | (heavy slot + 1) << 9; the read -> chunk position offset `k` folds orientation and origin.
@@ -2182,12 +2188,14 @@ constexpr int kLMaxPassGen = 4;  // general-bins mode: <= 4 * kLQuads * 4 = 256 
 #ifndef RCP_LWPE_GEN
 #define RCP_LWPE_GEN RCP_LWPE
 #endif
-template <int MAXPER, bool GEN>
+template <int MAXPER, bool GEN, int LR>
 __global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(GEN ? RCP_LWPE_GEN : RCP_LWPE)))
 rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int T = kTile;
-    [[maybe_unused]] constexpr int kSteps = kRowsPerWave * kRounds;  // rows of one wave per item
+    // LR rounds of T rows per item (kIRows rows); the metadata buffers keep kRows slots
+    constexpr int kIRows = LR * kTile;
+    static_assert(LR >= 2 && LR <= kRounds, "the next item's metadata is published a round before it is read");
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int lane = tid & 63;
@@ -2197,7 +2205,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     LeanMeta* lmeta = reinterpret_cast<LeanMeta*>(emask + (GEN ? T * 16 : 0));  // [2][kRows]
     int32_t* item = reinterpret_cast<int32_t*>(lmeta + 2 * kRows);  // [2]: item code or -1
     const int xcd = blockIdx.x & 7;
-    const int n_tiles = (P.n_rows + kRows - 1) / kRows;
+    const int n_tiles = (P.n_rows + kIRows - 1) / kIRows;
     auto n_items_of = [&](int x) { return (uint32_t)((n_tiles - x + 7) / 8) * (uint32_t)P.n_chunks_total; };
 
     // store wave 0: claim the next item of this XCD, decode its rows into buffer buf; once
@@ -2217,8 +2225,9 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             const int tl = (int)(j / P.n_chunks_total);
             code = (tl * 8 + xs) * P.n_chunks_total + (int)(j - (uint32_t)tl * P.n_chunks_total);
             const LeanItem it = lean_item(P, code);
-            lmeta[buf * kRows + lane] =
-                lean_pack(decode_row<false, false>(P, P.part[it.p], it.k0, it.cidx, it.tile * kRows + lane));
+            if (lane < kIRows)
+                lmeta[buf * kRows + lane] =
+                    lean_pack(decode_row<false, false>(P, P.part[it.p], it.k0, it.cidx, it.tile * kIRows + lane));
         }
         if (lane == 0) item[buf] = code;
         // nothing of the claim stays in flight: later register writes of this wave never
@@ -2277,7 +2286,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 for (int q = lane; q <= npos; q += 64) diff[lp(q, sh)] = g[m.P0 + q] + (q == 0 ? carry : 0);
             } else if (GEN && !m.fast) {
                 // several ranges (exon list): the wave streams the row's (segment, stream) pairs
-                pileup_row_wave(P, it.tile * kRows + i, m.P0, npos, diff, sh);
+                pileup_row_wave(P, it.tile * kIRows + i, m.P0, npos, diff, sh);
             } else {
                 const uint32_t n = lean_candidates(m);
                 // batches of 256 reads, three in flight: `cur` (prefetched with the previous
@@ -2370,11 +2379,11 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             return __builtin_amdgcn_readfirstlane(v);
         };
         auto fetch = [&](uint32_t rel, int2 (&dst)[4]) {  // rel: row number relative to this item
-            if (rel < (uint32_t)kRows) {
+            if (rel < (uint32_t)kIRows) {
                 prefetch(lmeta[buf * kRows + rel], dst);
             } else {
                 const int nc = item[buf ^ 1];
-                if (nc >= 0) prefetch(lmeta[(buf ^ 1) * kRows + (rel - kRows)], dst);
+                if (nc >= 0) prefetch(lmeta[(buf ^ 1) * kRows + (rel - kIRows)], dst);
             }
         };
         uint32_t base = 0;       // first row number of the current item
@@ -2383,7 +2392,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         if (code >= 0) fetch(g, bufA);
         while (code >= 0) {
             const LeanItem it = lean_item(P, code);
-            for (int rd = 0; rd < kRounds; ++rd) {
+            for (int rd = 0; rd < LR; ++rd) {
                 const uint32_t lim = base + (uint32_t)(T * (rd + 1));
                 while (g < lim) {
                     const uint32_t gn = take();
@@ -2400,7 +2409,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 lds_barrier();  // A: the round's stage rows are complete
                 lds_barrier();  // B: the store waves hold them in registers
             }
-            base += kRows;
+            base += kIRows;
             buf ^= 1;
             code = item[buf];
         }
@@ -2418,12 +2427,17 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         while (code >= 0) {
             const LeanItem it = lean_item(P, code);
             const int32_t col0 = P.part[it.p].col_off + it.k0 + 4 * qd;
-            for (int rd = 0; rd < kRounds; ++rd) {
+            for (int rd = 0; rd < LR; ++rd) {
+                // two rounds per item: the next item is claimed before the first round's barrier A
+                // (pile waves prefetch its first rows during the second round; every wave read
+                // the buffer it overwrites before the previous item's last barrier B)
+                if (LR == 2 && rd == 0 && wave == kPWaves) claim(buf ^ 1);
                 lds_barrier();  // A
                 const int rb = rd * T + ii;
-                const int r = it.tile * kRows + rb;
+                const int r = it.tile * kIRows + rb;
                 const LeanMeta& mr = lmeta[buf * kRows + rb];
                 const int32_t w0 = mr.w0, kend = mr.kend;
+                const int32_t bsr = GEN ? mr.bs : 1;  // (all metadata reads before barrier B)
                 const int32_t flag = w0 & 3;
                 const bool live = r < P.n_rows && flag != 2;
                 // the round's stage -> registers (uniform pass count; the reads past a row's
@@ -2452,7 +2466,6 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                     const double scf = flag == 0 ? sc : 0.0;
                     const int32_t nk = kend - (it.k0 + 4 * qd);  // columns left from this thread's first quad
                     double* o = out + (size_t)col0 * R + (size_t)r;
-                    const int32_t bsr = GEN ? mr.bs : 1;
 #pragma unroll
                     for (int j = 0; j < kPass; ++j) {
                         constexpr int kStep = 4 * kLQuads;
@@ -2485,7 +2498,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 // the next item: claimed and decoded after round 0's stores were issued (its
                 // loads wait for them, with a whole round of pile work to hide that); read
                 // by the pile waves from round 2 on, after this wave has passed barrier A(1)
-                if (rd == 0 && wave == kPWaves) claim(buf ^ 1);
+                if (LR > 2 && rd == 0 && wave == kPWaves) claim(buf ^ 1);
             }
             buf ^= 1;
             code = item[buf];
@@ -2658,7 +2671,7 @@ extern "C" size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr) {
     return 4 * ((size_t)kPWaves * (P->wave_words + 8) + stage_words + (size_t)kRows * kMetaWords + 8);
 }
 
-extern "C" int rcp_tile_rows(void) { return kRows; }
+extern "C" int rcp_tile_rows(void) { return kRows; }  // lean items of kRounds rounds (lean_rounds 0)
 
 // rows per round of the general pileup kernel and its maximum rounds per workgroup
 extern "C" void rcp_tile_geometry(int* tile, int* rounds_max) {
@@ -2672,10 +2685,10 @@ extern "C" int rcp_lean_gen_max_bins(void) { return 4 * kLQuads * kLMaxPassGen; 
 
 extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
 
-template <int MAXPER, bool GEN>
+template <int MAXPER, bool GEN, int LR>
 static hipError_t launch_pileup_lean_t(const RcpPlanDev* P, double* out, hipStream_t s) {
     {
-        const hipError_t e = allow_big_lds(rcp_pileup_lean_kernel<MAXPER, GEN>);
+        const hipError_t e = allow_big_lds(rcp_pileup_lean_kernel<MAXPER, GEN, LR>);
         if (e != hipSuccess) return e;
     }
     // [pile waves' difference arrays | one stage | row metadata x 2 | item codes x 2]
@@ -2684,11 +2697,18 @@ static hipError_t launch_pileup_lean_t(const RcpPlanDev* P, double* out, hipStre
     // (workgroup b serves XCD b % 8), never more than there are work items
     const int cus = std::max(1, P->n_cus);  // of the plan's device (rcp_plan_create)
     const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
-    const int tiles = (P->n_rows + kRows - 1) / kRows;
+    const int tiles = (P->n_rows + LR * kTile - 1) / (LR * kTile);
     const int64_t items = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
     const int64_t grid = std::min<int64_t>(((int64_t)per_cu * cus + 7) / 8 * 8, items);
-    hipLaunchKernelGGL((rcp_pileup_lean_kernel<MAXPER, GEN>), dim3((unsigned)grid), dim3(kLBlock), lds, s, *P, out);
+    hipLaunchKernelGGL((rcp_pileup_lean_kernel<MAXPER, GEN, LR>), dim3((unsigned)grid), dim3(kLBlock), lds, s, *P,
+                       out);
     return hipGetLastError();
+}
+
+template <int MAXPER, bool GEN>
+static hipError_t launch_pileup_lean_r(const RcpPlanDev* P, double* out, hipStream_t s) {
+    return P->lean_rounds == 2 ? launch_pileup_lean_t<MAXPER, GEN, 2>(P, out, s)
+                               : launch_pileup_lean_t<MAXPER, GEN, kRounds>(P, out, s);
 }
 
 extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P) {
@@ -2701,8 +2721,8 @@ extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P) {
 
 static hipError_t launch_pileup_lean(const RcpPlanDev* P, double* out, hipStream_t s) {
     if (P->lean == 2)
-        return P->chunk_cap <= 511 ? launch_pileup_lean_t<8, true>(P, out, s) : launch_pileup_lean_t<16, true>(P, out, s);
-    return P->chunk_cap <= 511 ? launch_pileup_lean_t<8, false>(P, out, s) : launch_pileup_lean_t<16, false>(P, out, s);
+        return P->chunk_cap <= 511 ? launch_pileup_lean_r<8, true>(P, out, s) : launch_pileup_lean_r<16, true>(P, out, s);
+    return P->chunk_cap <= 511 ? launch_pileup_lean_r<8, false>(P, out, s) : launch_pileup_lean_r<16, false>(P, out, s);
 }
 
 template <bool MEDIAN, bool CSR>

@@ -564,7 +564,8 @@ __global__ void rcp_dir_kernel(int64_t n_entries, int64_t n_streams, const int64
 // locate: per (row, segment, stream) read ranges, the NULL rules, heavy-row slots
 // =================================================================================
 #ifndef RCP_LOC_ABL
-#define RCP_LOC_ABL 0  // timing ablations only (wrong results): 1 no side writes, 2 no bucket searches
+#define RCP_LOC_ABL 0  // timing ablations only (wrong results), bits: 1 no side writes, 2 no bucket searches,
+                       // 4 no crange / record writes, 8 nothing after the row_info load
 #endif
 // Row positions [*p0, *p0 + *np) that column chunk (part, first bin k0) piles up for a
 // valid row of nominal length nr, mirroring the pileup kernel's metadata stage; false when
@@ -623,7 +624,7 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
         }
     }
     const int32_t* se = reinterpret_cast<const int32_t*>(P.se);
-    while (RCP_LOC_ABL != 2) {
+    while (!(RCP_LOC_ABL & 2)) {
         uint32_t m[K];
         int32_t kv[K];
         bool any = false;
@@ -678,6 +679,10 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
 #pragma unroll
             for (int u = 0; u < (int)(sizeof(RcpRowInfo) / 16); ++u) d[u] = make_uint4(0u, 0u, 0u, 0u);
         }
+    }
+    if (RCP_LOC_ABL & 8) {
+        if (in_row && ri.j0 == -12345) P.rec[r].flags = ri.j1;  // keeps the load
+        return;
     }
     const int j0 = ri.j0, j1 = ri.j1;
     const int32_t chrom = in_row ? ri.chrom : -1;
@@ -801,7 +806,7 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
             if (sl < 0 && q == 0) maxend[g] = P.pmax[hi - 1];
             if (q == 0) ncand = hi - lo;
         }
-#if RCP_LOC_ABL != 1
+#if !(RCP_LOC_ABL & 1)
         if (q == 0) {
             P.seg_lo[j0 * 3] = lo;
             P.seg_hi[j0 * 3] = hi;
@@ -902,7 +907,7 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
     }
     int32_t slot = -1;
     if (in_row && q == 0) {
-#if RCP_LOC_ABL != 1
+#if !(RCP_LOC_ABL & 1)
         P.valid[r] = valid ? 1 : 0;
         if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
         P.ncand[r] = ncand;
@@ -921,7 +926,7 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
                 P.heavy_nslice[u] = (ncand + (uint32_t)P.heavy_slice - 1) / (uint32_t)P.heavy_slice;
             }
         }
-#if RCP_LOC_ABL != 1
+#if !(RCP_LOC_ABL & 1)
         P.heavy_slot[r] = slot;
 #endif
     }
@@ -944,7 +949,7 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
             }
             // merged layout: one stream, so dense (row, chunk) words -- a wave's writes are
             // whole lines (stride 3, as the stranded layout below, measured ~1 us slower on C4)
-            P.crange[(size_t)r * nc + c] = make_uint2(clo, chi);
+            if (!(RCP_LOC_ABL & 4)) P.crange[(size_t)r * nc + c] = make_uint2(clo, chi);
         }
     } else if (cr && q < 3) {
         // stranded layout: lane q refines its own stream's range chunk by chunk
@@ -982,6 +987,10 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
     }
     const uint4* src = reinterpret_cast<const uint4*>(&rec);
     uint4* dst = reinterpret_cast<uint4*>(P.rec + r);
+    if (RCP_LOC_ABL & 4) {
+        if (rec.lo[0] == 0x7fffffffu) dst[0] = src[0];  // keeps the computation
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) dst[u] = src[u];
 }

@@ -143,59 +143,28 @@ __device__ __forceinline__ void add_read(const RcpPlanDev& P, const RcpSeg& sg, 
     atomicAdd(&diff[lp(o1 - P0 + 1, sh)], -w);
 }
 
-// Pile the candidate reads of row r over row positions [P0, P0 + npos) into `diff`
-// (npos + 1 words, zeroed by the caller).  Threads `t` of `nt` (a wave or a block) split
-// the reads; each keeps 4 coalesced loads in flight.
-__device__ __forceinline__ void pileup_row(const RcpPlanDev& P, int r, int32_t P0, int32_t npos, int32_t* diff,
-                                           int t, int nt, int sh) {
-    const int32_t P1 = P0 + npos;
-    const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
-    for (int j = j0; j < j1; ++j) {
-        const RcpSeg sg = P.segs[j];
-        const int32_t len = sg.hi - sg.lo + 1;
-        const int32_t a = max(P0, sg.off);
-        const int32_t b = min(P1, sg.off + len);
-        if (a >= b || !sg.query_ok) continue;
-        const bool full = (a == sg.off) && (b == sg.off + len);
-        int32_t gps, gpe;  // genomic piece
-        if (!sg.rev) {
-            gps = sg.lo + (a - sg.off);
-            gpe = sg.lo + (b - 1 - sg.off);
-        } else {
-            gpe = sg.hi - (a - sg.off);
-            gps = sg.hi - (b - 1 - sg.off);
-        }
-        for (int s = 0; s < 3; ++s) {
-            if (!((sg.streams >> s) & 1)) continue;
-            uint32_t lo = P.seg_lo[j * 3 + s];
-            uint32_t hi = P.seg_hi[j * 3 + s];
-            if (lo >= hi) continue;
-            // narrowing a partly covered segment costs two dependent binary searches; below a
-            // few batches of reads it is cheaper to stream them all (the piece test drops the rest)
-            if (!full && hi - lo > 1024) {
-                lo = lower_bound_pmax(P.pmax, lo, hi, gps);
-                hi = upper_bound_start(P.se, lo, hi, gpe);
-                if (lo >= hi) continue;
-            }
-            // batch base + 4 nt is loaded while batch base is added
-            int2 rd[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) rd[u] = P.se[min(lo + t + u * nt, hi - 1)];  // clamped: no branch
-            for (uint32_t base = lo + t; base < hi; base += 4 * nt) {
-                int2 nx[4];
-                const uint32_t nb = base + 4 * nt;
-                if (nb - t < hi) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) nx[u] = P.se[min(nb + u * nt, hi - 1)];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (base + u * nt < hi) add_read(P, sg, rd[u], gps, gpe, P0, diff, sh);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) rd[u] = nx[u];
-            }
+// add_read for a read of segment sg with the row offset folded: window index of genomic
+// position x is x + k (forward; k = off - lo - P0) or k - x (reversed; k = off + hi - P0)
+template <bool REV>
+__device__ __forceinline__ void add_read_k(const RcpPlanDev& P, const RcpSeg& sg, int32_t k, int2 rd, int32_t gps,
+                                           int32_t gpe, int32_t* diff, int sh, bool act) {
+    if (!act || rd.y < gps || rd.x > gpe) return;
+    int32_t w = 1;
+    if (sg.multi && !(rd.x > sg.nb_lo && rd.y < sg.nb_hi)) {
+        // subjectHits repeats a read once per range of the list it overlaps
+        // (R/coverage.R:190-192): weight = number of overlapped ranges.
+        w = 0;
+        for (int g = sg.gfirst; g < sg.gfirst + sg.gcount; ++g) {
+            const RcpSeg o = P.segs[g];
+            w += (o.query_ok && o.lo <= rd.y && o.hi >= rd.x) ? 1 : 0;
         }
     }
+    const int32_t x0 = max(rd.x, gps);
+    const int32_t x1 = min(rd.y, gpe);
+    const int32_t a = REV ? k - x1 : x0 + k;
+    const int32_t b = REV ? k - x0 + 1 : x1 + k + 1;
+    atomicAdd(&diff[lp(a, sh)], w);
+    atomicSub(&diff[lp(b, sh)], w);
 }
 
 // The candidate reads of the (segment, stream) pairs held one per lane -- lane t: segment `sg`,
@@ -278,21 +247,35 @@ __device__ __forceinline__ void ps_add(const RcpPlanDev& P, const RcpSeg& sg, Pa
         o.nb_hi = __builtin_amdgcn_readlane(sg.nb_hi, p);
         const int32_t gs = __builtin_amdgcn_readlane(ps.gps, p);
         const int32_t ge = __builtin_amdgcn_readlane(ps.gpe, p);
+        // the pair's orientation and origin folded into one offset (SGPR): a read's two adds
+        // take a clip (max / min), an add and the lane padding each
+        if (o.rev) {
+            const int32_t k = o.off + o.hi - P0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t q = q0 + lane + 64u * u;
-            if (q >= sp && q < ep) add_read(P, o, rd[u], gs, ge, P0, diff, sh);
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t q = q0 + lane + 64u * u;
+                add_read_k<true>(P, o, k, rd[u], gs, ge, diff, sh, q >= sp && q < ep);
+            }
+        } else {
+            const int32_t k = o.off - o.lo - P0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t q = q0 + lane + 64u * u;
+                add_read_k<false>(P, o, k, rd[u], gs, ge, diff, sh, q >= sp && q < ep);
+            }
         }
         m &= m - 1;
     }
 }
 
-// Pile a prepared stream whose first batch is in `cur` (loaded by ps_load(.., 0, ..)).
+// Pile a prepared stream whose batch `first` is in `cur` (loaded by ps_load(.., 256 first, ..)):
+// batches first, first + step, ... (step > 1: the waves of a block share one stream)
 __device__ __forceinline__ void ps_pile(const RcpPlanDev& P, const RcpSeg& sg, PairStream& ps, int2 (&cur)[4],
-                                        int32_t P0, int32_t* diff, int sh) {
-    for (uint32_t q0 = 0; q0 < ps.N; q0 += 256) {
+                                        int32_t P0, int32_t* diff, int sh, int first = 0, int step = 1) {
+    const uint32_t st = 256u * (uint32_t)step;
+    for (uint32_t q0 = 256u * (uint32_t)first; q0 < ps.N; q0 += st) {
         int2 nx[4];
-        if (q0 + 256 < ps.N) ps_load(P, ps, q0 + 256, nx);
+        if (q0 + st < ps.N) ps_load(P, ps, q0 + st, nx);
         ps_add(P, sg, ps, q0, cur, P0, diff, sh);
 #pragma unroll
         for (int u = 0; u < 4; ++u) cur[u] = nx[u];
@@ -300,25 +283,28 @@ __device__ __forceinline__ void ps_pile(const RcpPlanDev& P, const RcpSeg& sg, P
 }
 
 __device__ __forceinline__ void pile_pairs(const RcpPlanDev& P, const RcpSeg& sg, int32_t gps, int32_t gpe,
-                                           uint32_t lo, uint32_t hi, int32_t P0, int32_t* diff, int sh) {
+                                           uint32_t lo, uint32_t hi, int32_t P0, int32_t* diff, int sh,
+                                           int first = 0, int step = 1) {
     PairStream ps;
     ps_prepare(ps, gps, gpe, lo, hi);
-    if (ps.N == 0) return;  // wave-uniform
+    if (256u * (uint32_t)first >= ps.N) return;  // wave-uniform
     int2 cur[4];
-    ps_load(P, ps, 0, cur);
-    ps_pile(P, sg, ps, cur, P0, diff, sh);
+    ps_load(P, ps, 256u * (uint32_t)first, cur);
+    ps_pile(P, sg, ps, cur, P0, diff, sh, first, step);
 }
 
 // One wave piles row r (any number of segments x strand streams, e.g. a coverageRnaRef
-// c(flank, exons, flank) row) over row positions [P0, P0 + npos).  pileup_row walks the
-// (segment, stream) pairs one after the other -- one HBM round trip per pair, a dozen per
-// gene.  Here lane t owns pair t (its candidate range, narrowed by its own binary searches
+// c(flank, exons, flank) row) over row positions [P0, P0 + npos).  Walking the (segment,
+// stream) pairs one after the other costs one HBM round trip per pair, a dozen per gene.
+// Here lane t owns pair t (its candidate range, narrowed by its own binary searches
 // in parallel with the other lanes'); a wave scan lays the pairs' candidates end to end, and
 // batches of 256 candidates cross pair boundaries, so a row costs one round trip per 256
 // candidates with the next batch in flight while the current one is added.  The per-pair
 // data each candidate needs is picked by a scalar loop over the (few) pairs a batch spans.
+// (first, step): this wave adds batches first, first + step, ... of each stream of 64 pairs
+// (the waves of a block splitting one row: block_window_depth)
 __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int32_t P0, int32_t npos, int32_t* diff,
-                                                int sh) {
+                                                int sh, int first = 0, int step = 1) {
     const int lane = threadIdx.x & 63;
     const int32_t P1 = P0 + npos;
     const int j0 = P.row_seg[r], j1 = P.row_seg[r + 1];
@@ -365,7 +351,7 @@ __device__ __forceinline__ void pileup_row_wave(const RcpPlanDev& P, int r, int3
                 if (hi < lo) hi = lo;
             }
         }
-        pile_pairs(P, sg, gps, gpe, lo, hi, P0, diff, sh);
+        pile_pairs(P, sg, gps, gpe, lo, hi, P0, diff, sh, first, step);
     }
 }
 
@@ -2547,7 +2533,10 @@ __device__ void block_window_depth(const RcpPlanDev& P, int r, int32_t w0, int32
         __syncthreads();
         for (int q = threadIdx.x; q <= wn; q += kBlock) diff[q] += g[w0 + q];
     } else {
-        pileup_row(P, r, w0, wn, diff, threadIdx.x, kBlock, 30);
+        // the row's (segment, stream) pairs as one stream of candidate batches, dealt to the
+        // block's waves (pileup_row walked the pairs one after the other: one round trip each,
+        // a dozen per interpolated C3 gene)
+        if (!(RCP_INTERP_ABL & 2)) pileup_row_wave(P, r, w0, wn, diff, 30, (int)(threadIdx.x >> 6), kWaves);
     }
     __syncthreads();
     scan_block_depth(diff, per, scratch);

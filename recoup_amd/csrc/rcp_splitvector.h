@@ -36,8 +36,20 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
     }
     // 1-based i = 2 .. n-1 (0-based i - 1): c[i] = (y[i+1] - y[i]) - (y[i] - y[i-1])
     for (int i = 1 + t; i < n - 1; i += blockDim.x) c[i] = (y[i + 1] - y[i]) - (y[i] - y[i - 1]);
+    // the tabulated multipliers t_i and pivots b_i staged next to the data (b and d are free
+    // until the coefficients below): thread 0's chains read them at LDS latency, not the
+    // global table's (one round trip per 8 steps: 0.116 ms of C3's interpolation kernel)
+    double* tt = b;
+    double* tp = d;
+    for (int i = t; i < n; i += blockDim.x) {
+        tt[i] = tb[2 * i];
+        tp[i] = tb[2 * i + 1];
+    }
     __syncthreads();
-    if (t == 0) {
+#ifndef RCP_INTERP_ABL
+#define RCP_INTERP_ABL 0  // timing ablations only (wrong results): 1 no elimination chains, 2 no reads
+#endif
+    if (t == 0 && !(RCP_INTERP_ABL & 1)) {
         double c1 = 0.0, cn = 0.0;
         if (n > 3) {
             c1 = c[2] / 2.0 - c[1] / 2.0;
@@ -55,7 +67,7 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 cv[u] = c[i + u];
-                tv[u] = tb[2 * (i + u)];
+                tv[u] = tt[i + u];
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -64,10 +76,10 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
             }
         }
         for (; i < n; ++i) {
-            cp = c[i] - tb[2 * i] * cp;
+            cp = c[i] - tt[i] * cp;
             c[i] = cp;
         }
-        const double bn = -1.0 - tb[2 * (n - 1)];  // b[n-1] = -1 - t_{n-1}
+        const double bn = -1.0 - tt[n - 1];  // b[n-1] = -1 - t_{n-1}
         // back substitution: c[i] = (c[i] - c[i+1]) / b[i]
         double cnext = cp / bn;
         c[n - 1] = cnext;
@@ -77,7 +89,7 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 cv[u] = c[i - u];
-                bv[u] = tb[2 * (i - u) + 1];
+                bv[u] = tp[i - u];
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -86,7 +98,7 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
             }
         }
         for (; i >= 0; --i) {
-            cnext = (c[i] - cnext) / tb[2 * i + 1];
+            cnext = (c[i] - cnext) / tp[i];
             c[i] = cnext;
         }
         b[n - 1] = (y[n - 1] - y[n - 2]) + (c[n - 2] + 2.0 * c[n - 1]);

@@ -1,7 +1,9 @@
 #!/bin/bash
-# PMC SQ passes of the C4 pass (locate / heavy / lean pileup counters)
+# general kernel occupancy at C4 shapes: stage of <= 256 bins (two workgroups per CU) or a
+# single-buffered stage, vs base; 1/8 and 1/4 C4 shards (general kernel) and full C4 (lean)
 OUT=gpurun_out/r3g
 mkdir -p $OUT
 export TMPDIR=/tmp
-PASSES=sq bash tools/pmc.sh $OUT/pmc c4
-python3 tools/pmc_kernels.py $OUT/pmc rcp_locate rcp_heavy rcp_pileup_lean > $OUT/sq_c4.txt; cat $OUT/sq_c4.txt
+BENCH_ARGS="--inflight 1 --sim-shard 0/8" TAG=_s8 bash tools/gpu_ab.sh $OUT c4 base sb256 buf1 base sb256 buf1 || exit 1
+BENCH_ARGS="--inflight 1 --sim-shard 0/4" TAG=_s4 bash tools/gpu_ab.sh $OUT c4 base sb256 buf1 || exit 1
+BENCH_ARGS="--inflight 1" bash tools/gpu_ab.sh $OUT "c4 c2" base sb256 buf1 || exit 1

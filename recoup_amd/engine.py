@@ -98,9 +98,9 @@ class ReadSet:
         with torch.cuda.device(self.device):
             check(lib.rcp_readset_create(ctypes.byref(d), _stream(self.device, stream), ctypes.byref(h)))
         self.h = h
+        self._stream_off = None
         nk = ctypes.c_int64()
-        self.stream_off = np.zeros(3 * len(self.seqlengths) + 1, dtype=np.int64)
-        check(lib.rcp_readset_info(self.h, ctypes.byref(nk), cptr(self.stream_off, _lib._i64p)))
+        check(lib.rcp_readset_info(self.h, ctypes.byref(nk), None))
         self.n = nk.value
 
     @classmethod
@@ -124,12 +124,25 @@ class ReadSet:
         for h, dv in zip(hs, dev):
             rs = cls.__new__(cls)
             rs.device, rs.seqlengths, rs.h = int(dv), seql, ctypes.c_void_p(h)
+            rs._stream_off = None
             nk = ctypes.c_int64()
-            rs.stream_off = np.zeros(3 * len(seql) + 1, dtype=np.int64)
-            check(lib.rcp_readset_info(rs.h, ctypes.byref(nk), cptr(rs.stream_off, _lib._i64p)))
+            check(lib.rcp_readset_info(rs.h, ctypes.byref(nk), None))
             rs.n = nk.value
             out.append(rs)
         return out
+
+    @property
+    def stream_off(self):
+        """Start of each (chromosome, strand) stream of the strand-split layout, [3 * n_chrom + 1]
+        (rcp_readset_info; the library builds that layout on its first use, so a readset only
+        ever used with ignore.strand = TRUE rows never pays for it)."""
+        if self._stream_off is None:
+            so = np.zeros(3 * len(self.seqlengths) + 1, dtype=np.int64)
+            nk = ctypes.c_int64()
+            with torch.cuda.device(self.device):
+                check(_lib.lib().rcp_readset_info(self.h, ctypes.byref(nk), cptr(so, _lib._i64p)))
+            self._stream_off = so
+        return self._stream_off
 
     @property
     def chrom_has_reads(self):

@@ -1,0 +1,14 @@
+#!/bin/bash
+# lazy stream offsets in the Python ReadSet (no stranded layout for ignore.strand = TRUE callers):
+# GPU suite + C5 / C4 e2e legs
+OUT=gpurun_out/r3e2e
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 900 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
+tail -1 $OUT/gpu_tests.log
+for c in c5 c4; do
+timeout -k 10 600 python3 bench.py --config $c --no-cpu --steps 10 > $OUT/$c.json 2> $OUT/$c.err || { tail $OUT/$c.err; exit 1; }
+python3 -c "
+import json; d=json.load(open('$OUT/$c.json')); e=d['e2e']
+print('$c', round(e['ms'],1), {k: round(v,1) for k,v in e['phases_ms'].items()}, 'any', round(e['any_order']['ms'],1), 'rle', round(e['rle_path']['ms'],1), {k: round(v,1) for k,v in e['rle_path']['phases_ms'].items()})"
+done

@@ -76,6 +76,10 @@ struct RcpPart {
 struct RcpPlanDev {
     // reads
     const int2* se;            // sorted (start, end) pairs
+    // reads of one width (ChIP-seq fragments extended to fragLen, fixed read lengths): their
+    // starts alone, end = start + st_w (the lean kernel streams these; null = not uniform)
+    const int32_t* st;
+    int32_t st_w;
     const int32_t* pmax;       // prefix max of end inside each stream
     const int64_t* stream_off; // [n_chrom*3 + 1]
     const int64_t* seqlen;     // [n_chrom] (-1 = NA)

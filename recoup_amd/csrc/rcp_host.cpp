@@ -94,6 +94,8 @@ hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* 
 hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, int64_t* d_count,
                               int64_t* d_run_off, void* temp, size_t* temp_bytes, int32_t* d_values,
                               int32_t* d_lengths, int pass, hipStream_t stream);
+hipError_t rcp_launch_width_range(int64_t n, const int2* se, int32_t* mm, hipStream_t stream);
+hipError_t rcp_launch_starts(int64_t n, const int2* se, int32_t* st, hipStream_t stream);
 hipError_t rcp_rle_seams_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, const uint8_t* d_valid,
                              int32_t chunk_bins, int32_t chunk_cap, int64_t* d_count, hipStream_t stream);
 hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t* off, const int32_t* pmax, int32_t* out,
@@ -343,6 +345,8 @@ struct ReadLayout {
     PoolArr se, pmax, stream_off;
     PoolArr dir_l, dir_off;
     int32_t dir_shift = 12;
+    PoolArr st;         // the starts alone when every read has one width (st_w = end - start)
+    int32_t st_w = 0;
 };
 
 struct rcp_readset {
@@ -474,6 +478,23 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     HIP_TRY(L->pmax.alloc(4 * std::max<int64_t>(n, 1), s));
     HIP_TRY(rcp_launch_unpack_pmax(n, scan_out.as<uint64_t>(), L->pmax.as<int32_t>(), s));
     LAYOUT_MARK("  pmax scan");
+    // reads of one width: keep their starts alone for the lean pileup (half its read bytes)
+    if (n > 0) {
+        PoolBuf mm(s);
+        HIP_TRY(mm.alloc(8));
+        const int32_t seed[2] = {INT32_MAX, INT32_MIN};
+        HIP_TRY(hipMemcpyAsync(mm.p, seed, 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(rcp_launch_width_range(n, L->se.as<int2>(), mm.as<int32_t>(), s));
+        int32_t h_mm[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(h_mm, mm.p, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (h_mm[0] == h_mm[1] && h_mm[0] >= 0) {
+            HIP_TRY(L->st.alloc(4 * (size_t)n, s));
+            HIP_TRY(rcp_launch_starts(n, L->se.as<int2>(), L->st.as<int32_t>(), s));
+            L->st_w = h_mm[0];
+        }
+    }
+    LAYOUT_MARK("  uniform starts");
     scan_in.reset();
     scan_out.reset();
     temp.reset();
@@ -1352,6 +1373,8 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
 
     const ReadLayout& RL = rows->ignore_strand ? rs->merged : rs->stranded;
     P.se = RL.se.as<int2>();
+    P.st = RL.st.p ? RL.st.as<int32_t>() : nullptr;  // uniform-width reads (the lean kernel)
+    P.st_w = RL.st_w;
     P.pmax = RL.pmax.as<int32_t>();
     P.stream_off = RL.stream_off.as<int64_t>();
     P.seqlen = rs->d_seqlen.as<int64_t>();

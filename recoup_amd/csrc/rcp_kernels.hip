@@ -23,6 +23,7 @@
 // a column (128 B) per 16 lanes of the R column-major matrix (64-B segments write at ~60 %
 // of the 128-B rate: tools/write_bench.hip).
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <hipcub/hipcub.hpp>
 
 #include <mutex>
@@ -2183,7 +2184,7 @@ constexpr int kLMaxPassGen = 4;  // general-bins mode: <= 4 * kLQuads * 4 = 256 
 #ifndef RCP_LWPE_GEN
 #define RCP_LWPE_GEN RCP_LWPE
 #endif
-template <int MAXPER, bool GEN, int LR>
+template <int MAXPER, bool GEN, int LR, bool UNI>
 __global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(GEN ? RCP_LWPE_GEN : RCP_LWPE)))
 rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2191,6 +2192,11 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     // LR rounds of T rows per item (kIRows rows); the metadata buffers keep kRows slots
     constexpr int kIRows = LR * kTile;
     static_assert(LR >= 2 && LR <= kRounds, "the next item's metadata is published a round before it is read");
+    // UNI (plan st != null): reads of one width -- the candidate streams are their starts alone
+    // (4 B per read instead of the (start, end) pair: half the pile's read traffic); the end
+    // is formed when the read is added, so the prefetched loads stay in flight until then
+    static_assert(!(UNI && GEN), "uniform-width reads: single-range mode only");
+    using RdT = typename std::conditional<UNI, int32_t, int2>::type;
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int lane = tid & 63;
@@ -2240,14 +2246,22 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         // ================= pile waves
         int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * P.wave_words;
         [[maybe_unused]] auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
-        auto prefetch = [&](const LeanMeta& mm, int2* dst) {
+        auto rd_load = [&](uint32_t idx) -> RdT {
+            if constexpr (UNI) return P.st[idx];
+            else return P.se[idx];
+        };
+        auto rd_pair = [&](RdT v) -> int2 {
+            if constexpr (UNI) return make_int2(v, v + P.st_w);
+            else return v;
+        };
+        auto prefetch = [&](const LeanMeta& mm, RdT* dst) {
             const LeanRow m = lean_row(mm);
             const uint32_t n = (m.flag == 0 && m.fast) ? lean_candidates(m) : 0;
             if (n) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const uint32_t q = lane + 64 * u;
-                    dst[u] = P.se[lean_index(m, q < n ? q : n - 1)];
+                    dst[u] = rd_load(lean_index(m, q < n ? q : n - 1));
                 }
             }
         };
@@ -2257,7 +2271,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         // one row: `cur` holds its first reads; the next row's (possibly the next item's
         // first row) go to `nxt`
         // pile row i of the item (tile row), its first reads in `cur`; bin sums -> stage
-        auto pile_row = [&](const LeanItem& it, int i, int2 (&cur)[4]) __attribute__((always_inline)) {
+        auto pile_row = [&](const LeanItem& it, int i, RdT (&cur)[4]) __attribute__((always_inline)) {
             const LeanRow m = lean_row(lmeta[buf * kRows + i]);
             if (m.flag != 0) return;
             if (!GEN && !m.fast && m.heavy < 0) {  // the plan promised single-range rows
@@ -2286,12 +2300,12 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 const uint32_t n = lean_candidates(m);
                 // batches of 256 reads, three in flight: `cur` (prefetched with the previous
                 // row), b1, b2; the loop is unrolled over the ring so no buffer is copied
-                auto load_batch = [&](uint32_t q0, int2 (&dst)[4]) {
+                auto load_batch = [&](uint32_t q0, RdT (&dst)[4]) {
                     if (q0 < n) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             const uint32_t q = q0 + lane + 64 * u;
-                            dst[u] = P.se[lean_index(m, q < n ? q : n - 1)];
+                            dst[u] = rd_load(lean_index(m, q < n ? q : n - 1));
                         }
                     }
                 };
@@ -2299,27 +2313,27 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 #define RCP_LDENSE 1
 #endif
                 const bool dense = RCP_LDENSE && n >= (uint32_t)npos;  // wave-uniform
-                auto add_batch = [&](uint32_t q0, const int2 (&src)[4]) {
+                auto add_batch = [&](uint32_t q0, const RdT (&src)[4]) {
                     if (dense) {
                         if (m.rev) {
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) lean_add_runs<true>(m, src[u], q0 + lane + 64u * u < n, diff, sh);
+                            for (int u = 0; u < 4; ++u) lean_add_runs<true>(m, rd_pair(src[u]), q0 + lane + 64u * u < n, diff, sh);
                         } else {
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) lean_add_runs<false>(m, src[u], q0 + lane + 64u * u < n, diff, sh);
+                            for (int u = 0; u < 4; ++u) lean_add_runs<false>(m, rd_pair(src[u]), q0 + lane + 64u * u < n, diff, sh);
                         }
                     } else if (m.rev) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            if (q0 + lane + 64u * u < n) lean_add<true>(m, src[u], diff, sh);
+                            if (q0 + lane + 64u * u < n) lean_add<true>(m, rd_pair(src[u]), diff, sh);
                     } else {
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            if (q0 + lane + 64u * u < n) lean_add<false>(m, src[u], diff, sh);
+                            if (q0 + lane + 64u * u < n) lean_add<false>(m, rd_pair(src[u]), diff, sh);
                     }
                 };
                 for (uint32_t q0 = 0; q0 < n; q0 += 256) {
-                    int2 nx[4];
+                    RdT nx[4];
                     load_batch(q0 + 256, nx);
                     add_batch(q0, cur);
 #pragma unroll
@@ -2358,7 +2372,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             }
             lds_order();
         };
-        int2 bufA[4], bufB[4];
+        RdT bufA[4], bufB[4];
         // Rows are dealt dynamically: a wave takes the workgroup's next row number g from an
         // LDS counter (rows 64 q .. 64 q + 63 = the q-th item of this workgroup, 16 per round)
         // when it starts its current row, and prefetches g's first reads.  A round ends when
@@ -2373,7 +2387,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             if (lane == 0) v = atomicAdd(ctr, 1u);
             return __builtin_amdgcn_readfirstlane(v);
         };
-        auto fetch = [&](uint32_t rel, int2 (&dst)[4]) {  // rel: row number relative to this item
+        auto fetch = [&](uint32_t rel, RdT (&dst)[4]) {  // rel: row number relative to this item
             if (rel < (uint32_t)kIRows) {
                 prefetch(lmeta[buf * kRows + rel], dst);
             } else {
@@ -2683,10 +2697,10 @@ extern "C" int rcp_lean_gen_max_bins(void) { return 4 * kLQuads * kLMaxPassGen; 
 
 extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
 
-template <int MAXPER, bool GEN, int LR>
+template <int MAXPER, bool GEN, int LR, bool UNI>
 static hipError_t launch_pileup_lean_t(const RcpPlanDev* P, double* out, hipStream_t s) {
     {
-        const hipError_t e = allow_big_lds(rcp_pileup_lean_kernel<MAXPER, GEN, LR>);
+        const hipError_t e = allow_big_lds(rcp_pileup_lean_kernel<MAXPER, GEN, LR, UNI>);
         if (e != hipSuccess) return e;
     }
     // [pile waves' difference arrays | one stage | row metadata x 2 | item codes x 2]
@@ -2698,15 +2712,20 @@ static hipError_t launch_pileup_lean_t(const RcpPlanDev* P, double* out, hipStre
     const int tiles = (P->n_rows + LR * kTile - 1) / (LR * kTile);
     const int64_t items = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
     const int64_t grid = std::min<int64_t>(((int64_t)per_cu * cus + 7) / 8 * 8, items);
-    hipLaunchKernelGGL((rcp_pileup_lean_kernel<MAXPER, GEN, LR>), dim3((unsigned)grid), dim3(kLBlock), lds, s, *P,
+    hipLaunchKernelGGL((rcp_pileup_lean_kernel<MAXPER, GEN, LR, UNI>), dim3((unsigned)grid), dim3(kLBlock), lds, s, *P,
                        out);
     return hipGetLastError();
 }
 
 template <int MAXPER, bool GEN>
 static hipError_t launch_pileup_lean_r(const RcpPlanDev* P, double* out, hipStream_t s) {
-    return P->lean_rounds == 2 ? launch_pileup_lean_t<MAXPER, GEN, 2>(P, out, s)
-                               : launch_pileup_lean_t<MAXPER, GEN, kRounds>(P, out, s);
+    if constexpr (!GEN) {
+        if (P->st)
+            return P->lean_rounds == 2 ? launch_pileup_lean_t<MAXPER, false, 2, true>(P, out, s)
+                                       : launch_pileup_lean_t<MAXPER, false, kRounds, true>(P, out, s);
+    }
+    return P->lean_rounds == 2 ? launch_pileup_lean_t<MAXPER, GEN, 2, false>(P, out, s)
+                               : launch_pileup_lean_t<MAXPER, GEN, kRounds, false>(P, out, s);
 }
 
 extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P) {
@@ -2984,6 +3003,52 @@ extern "C" hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, c
     if (n_rows > 0)
         hipLaunchKernelGGL(rcp_rle_emit_kernel, dim3(grid), dim3(64 * kRleWaves), 0, stream, n_rows, d_off, d_cov,
                            d_run_off, d_values, d_lengths);
+    return hipGetLastError();
+}
+
+// Uniform-width readsets: the range of end - start over the layout's reads (mm[0] min, mm[1]
+// max; the caller seeds INT32_MAX / INT32_MIN), then, when it is one value, the starts alone.
+__global__ void __launch_bounds__(kBlock) rcp_width_range_kernel(int64_t n, const int2* __restrict__ se,
+                                                                int32_t* __restrict__ mm) {
+    __shared__ int32_t bmin, bmax;
+    if (threadIdx.x == 0) {
+        bmin = INT32_MAX;
+        bmax = INT32_MIN;
+    }
+    __syncthreads();
+    int32_t lo = INT32_MAX, hi = INT32_MIN;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        const int2 r = se[i];
+        const int32_t w = r.y - r.x;
+        lo = min(lo, w);
+        hi = max(hi, w);
+    }
+    atomicMin(&bmin, lo);
+    atomicMax(&bmax, hi);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicMin(&mm[0], bmin);
+        atomicMax(&mm[1], bmax);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) rcp_starts_kernel(int64_t n, const int2* __restrict__ se,
+                                                           int32_t* __restrict__ st) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        st[i] = se[i].x;
+}
+
+extern "C" hipError_t rcp_launch_width_range(int64_t n, const int2* se, int32_t* mm, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const int64_t grid = std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);
+    hipLaunchKernelGGL(rcp_width_range_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, se, mm);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rcp_launch_starts(int64_t n, const int2* se, int32_t* st, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const int64_t grid = std::min<int64_t>((n + kBlock - 1) / kBlock, 16384);
+    hipLaunchKernelGGL(rcp_starts_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, se, st);
     return hipGetLastError();
 }
 

@@ -1,5 +1,6 @@
 // PMC calibration for the pileup kernel's access shapes (MI355X_MICROARCH.md documents the
-// FETCH_SIZE correction only for 16-B-per-lane reads; the pileup streams 8-B int2 reads and
+// FETCH_SIZE correction only for 16-B-per-lane reads; the pileup streams 8-B int2 reads (4-B
+// starts for uniform-width readsets) and
 // writes 8-B fp64 non-temporal stores in 128-B column segments).
 //
 //   fetch_calib          runs each kernel 3 times over a 2 GiB buffer (far beyond L2 + MALL)
@@ -39,6 +40,14 @@ __global__ void read8_plain(const int2* __restrict__ in, size_t n, int* __restri
     if (acc == 0x7fffffff) sink[0] = acc;
 }
 
+// plain int32 loads (the lean pileup over a uniform-width readset's starts: global_load_dword)
+__global__ void read4_plain(const int* __restrict__ in, size_t n, int* __restrict__ sink) {
+    int acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        acc += in[i];
+    if (acc == 0x7fffffff) sink[0] = acc;
+}
+
 // column-major fp64 matrix, 16-row column segments, non-temporal 8-B stores (the epilogue)
 __global__ void write8_seg16(double* out, int R, int B) {
     const int r = blockIdx.x * 16 + threadIdx.x % 16;
@@ -57,6 +66,7 @@ int main() {
         hipLaunchKernelGGL(read8, dim3(4096), dim3(256), 0, 0, (const int2*)buf, bytes / 8, sink);
         hipLaunchKernelGGL(read8_plain, dim3(4096), dim3(256), 0, 0, (const int2*)buf, bytes / 8, sink);
         hipLaunchKernelGGL(read16, dim3(4096), dim3(256), 0, 0, (const int4*)buf, bytes / 16, sink);
+        hipLaunchKernelGGL(read4_plain, dim3(4096), dim3(256), 0, 0, (const int*)buf, bytes / 4, sink);
         hipLaunchKernelGGL(write8_seg16, dim3(R / 16), dim3(256), 0, 0, (double*)buf, R, B);
     }
     if (hipDeviceSynchronize() != hipSuccess) return 1;

@@ -7,7 +7,7 @@ OUT=${1:-gpurun_out/round}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 PASSES=traffic bash tools/pmc.sh "$OUT/pmc" c4
-python3 tools/pmc_traffic.py "$OUT/pmc" "$OUT/traffic_c4.json"
+python3 tools/pmc_traffic.py "$OUT/pmc" "$OUT/traffic_c4.json" "${CALIB:-profiles/fetch_calib.json}"
 timeout -k 10 600 python3 bench.py --traffic "$OUT/traffic_c4.json" > "$OUT/c4_bench.json" 2> "$OUT/c4_bench.err"
 cat "$OUT/c4_bench.json"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \

@@ -11,7 +11,7 @@ python3 tools/pmc_traffic.py "$OUT/pmc" "$OUT/traffic_c4.json" "${CALIB:-profile
 timeout -k 10 600 python3 bench.py --traffic "$OUT/traffic_c4.json" > "$OUT/c4_bench.json" 2> "$OUT/c4_bench.err"
 cat "$OUT/c4_bench.json"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
-    python3 bench.py --no-cpu --no-e2e --traffic "$OUT/traffic_c4.json" > "$OUT/c4_bench_under_rocprof.json" 2> "$OUT/prof.err"
+    python3 bench.py --no-cpu --no-e2e --inflight 1 --traffic "$OUT/traffic_c4.json" > "$OUT/c4_bench_under_rocprof.json" 2> "$OUT/prof.err"
 for c in c2 c3 c5; do
     timeout -k 10 600 python3 bench.py --config $c > "$OUT/${c}_bench.json" 2> "$OUT/${c}_bench.err"
     cat "$OUT/${c}_bench.json"

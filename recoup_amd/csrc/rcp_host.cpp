@@ -1373,7 +1373,10 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
 
     const ReadLayout& RL = rows->ignore_strand ? rs->merged : rs->stranded;
     P.se = RL.se.as<int2>();
-    P.st = RL.st.p ? RL.st.as<int32_t>() : nullptr;  // uniform-width reads (the lean kernel)
+#ifndef RCP_NO_UNI
+#define RCP_NO_UNI 0  // 1: never stream starts alone (A/B only)
+#endif
+    P.st = RL.st.p && !RCP_NO_UNI ? RL.st.as<int32_t>() : nullptr;  // uniform-width reads
     P.st_w = RL.st_w;
     P.pmax = RL.pmax.as<int32_t>();
     P.stream_off = RL.stream_off.as<int64_t>();

@@ -1396,9 +1396,20 @@ __device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart
 #ifndef RCP_GEN_WPE
 #define RCP_GEN_WPE 4
 #endif
-template <bool MEDIAN, bool CSR>
+template <bool MEDIAN, bool CSR, bool UNI>
 __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RCP_GEN_WPE))) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
                                                             int64_t* __restrict__ binsum) {
+    // UNI (plan st != null): reads of one width, streamed as their starts alone (the lean kernel's
+    // start-only stream): 4-B loads, end = start + st_w formed when a read is added
+    using RdT = typename std::conditional<UNI, int32_t, int2>::type;
+    auto rd_load = [&](uint32_t idx) -> RdT {
+        if constexpr (UNI) return P.st[idx];
+        else return P.se[idx];
+    };
+    auto rd_pair = [&](RdT v) -> int2 {
+        if constexpr (UNI) return make_int2(v, v + P.st_w);
+        else return v;
+    };
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int T = kTile;
     const int tid = threadIdx.x;
@@ -1445,7 +1456,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
     // software pipeline: the first 256 candidate reads of the next kAhead rows are in flight
     // while a row is piled up (registers are free: LDS, not VGPRs, limits occupancy)
     [[maybe_unused]] const int n_steps = kRowsPerWave * rounds;
-    auto prefetch = [&](int i, int2* dst) {
+    auto prefetch = [&](int i, RdT* dst) {
         const RowMeta m = uniform_meta(meta[i]);
         const uint32_t n = (m.flag == 0 && m.fast && !(RCP_GEN_ABL & 2)) ? fast_candidates(m) : 0;
         if (n) {  // wave-uniform
@@ -1453,7 +1464,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
             for (int u = 0; u < 4; ++u) {
                 // unconditional (clamped) loads: no divergent branch, no early vmcnt wait
                 const uint32_t q = lane + 64 * u;
-                dst[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+                dst[u] = rd_load(fast_index(m, q < n ? q : n - 1));
             }
         }
     };
@@ -1461,7 +1472,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
     // Two read buffers used alternately (no register copies across steps): a copy at the loop
     // back-edge would need the prefetched reads to have landed right after the epilogue's
     // stores, and gfx9's single in-order vmcnt would make that wait for the stores too.
-    int2 bufA[4], bufB[4];
+    RdT bufA[4], bufB[4];
     // ---- round epilogue: stage row -> out[col * n_rows + row].  Thread t serves row t % 16
     // and column quads t / 16, t / 16 + 32, ...: one 16-B stage read feeds four stores, and
     // the 16 lanes of a quad column write 16 consecutive rows (128 B) of one column.
@@ -1546,7 +1557,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
     int clean_sh = -1;
     // one row of this wave: `cur` holds its first reads; the next row's go to `nxt`
     // pile row i of the workgroup (round i / T), its first reads in `cur`
-    auto pile_row = [&](int i, int2 (&cur)[4]) __attribute__((always_inline)) {
+    auto pile_row = [&](int i, RdT (&cur)[4]) __attribute__((always_inline)) {
         const RowMeta m = uniform_meta(meta[i]);
         uint32_t* sbuf = stage + ((i / T) % kStageBufs) * T * RS;  // this round's stage
         if (m.flag == 0) {  // wave-uniform: scalar branch
@@ -1590,22 +1601,22 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
                     const uint32_t n = (RCP_GEN_ABL & 2) ? 0u : fast_candidates(m);
                     // batch q0 + 256 is loaded while batch q0 is added
                     for (uint32_t q0 = 0; q0 < n; q0 += 256) {
-                        int2 nx[4];
+                        RdT nx[4];
                         if (q0 + 256 < n) {
 #pragma unroll
                             for (int u = 0; u < 4; ++u) {
                                 const uint32_t q = q0 + 256 + lane + 64 * u;
-                                nx[u] = P.se[fast_index(m, q < n ? q : n - 1)];
+                                nx[u] = rd_load(fast_index(m, q < n ? q : n - 1));
                             }
                         }
                         if (m.rev) {  // wave-uniform orientation
 #pragma unroll
                             for (int u = 0; u < 4; ++u)
-                                if (q0 + lane + 64u * u < n) add_read_fast_t<true>(m, cur[u], diff, sh);
+                                if (q0 + lane + 64u * u < n) add_read_fast_t<true>(m, rd_pair(cur[u]), diff, sh);
                         } else {
 #pragma unroll
                             for (int u = 0; u < 4; ++u)
-                                if (q0 + lane + 64u * u < n) add_read_fast_t<false>(m, cur[u], diff, sh);
+                                if (q0 + lane + 64u * u < n) add_read_fast_t<false>(m, rd_pair(cur[u]), diff, sh);
                         }
 #pragma unroll
                         for (int u = 0; u < 4; ++u) cur[u] = nx[u];
@@ -1691,7 +1702,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
             }
         }
     };
-    auto pile_step = [&](int step, int2 (&cur)[4], int2 (&nxt)[4]) __attribute__((always_inline)) {
+    auto pile_step = [&](int step, RdT (&cur)[4], RdT (&nxt)[4]) __attribute__((always_inline)) {
         if (step + 1 < n_steps) prefetch(row_of(step + 1), nxt);
         pile_row(row_of(step), cur);
     };
@@ -2742,17 +2753,24 @@ static hipError_t launch_pileup_lean(const RcpPlanDev* P, double* out, hipStream
     return P->chunk_cap <= 511 ? launch_pileup_lean_r<8, false>(P, out, s) : launch_pileup_lean_r<16, false>(P, out, s);
 }
 
-template <bool MEDIAN, bool CSR>
-static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* binsum, size_t lds, hipStream_t s) {
+template <bool MEDIAN, bool CSR, bool UNI>
+static hipError_t launch_pileup_u(const RcpPlanDev* P, double* out, int64_t* binsum, size_t lds, hipStream_t s) {
     {
-        const hipError_t e = allow_big_lds(rcp_pileup_kernel<MEDIAN, CSR>);
+        const hipError_t e = allow_big_lds(rcp_pileup_kernel<MEDIAN, CSR, UNI>);
         if (e != hipSuccess) return e;
     }
     const int rows_wg = kTile * P->rounds;
     const int tiles = (P->n_rows + rows_wg - 1) / rows_wg;
     const int64_t grid = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
-    hipLaunchKernelGGL((rcp_pileup_kernel<MEDIAN, CSR>), dim3((unsigned)grid), dim3(kPBlock), lds, s, *P, out, binsum);
+    hipLaunchKernelGGL((rcp_pileup_kernel<MEDIAN, CSR, UNI>), dim3((unsigned)grid), dim3(kPBlock), lds, s, *P, out,
+                       binsum);
     return hipGetLastError();
+}
+
+template <bool MEDIAN, bool CSR>
+static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* binsum, size_t lds, hipStream_t s) {
+    return P->st ? launch_pileup_u<MEDIAN, CSR, true>(P, out, binsum, lds, s)
+                 : launch_pileup_u<MEDIAN, CSR, false>(P, out, binsum, lds, s);
 }
 
 extern "C" size_t rcp_pileup_rows_lds_bytes(void) { return 4 * (size_t)kRWaves * kRWWords + 16 + 48; }

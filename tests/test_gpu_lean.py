@@ -205,9 +205,9 @@ def test_lean_more_column_chunks(gpu, chunks):
     same(more.run(), base.run())
 
 
-@pytest.mark.parametrize("stranded", [False, True])
+@pytest.mark.parametrize("stranded,strand_filter", [(False, None), (True, None), (True, "+")])
 @pytest.mark.parametrize("width", [1, 180])
-def test_lean_uniform_width_reads(gpu, stranded, width):
+def test_lean_uniform_width_reads(gpu, stranded, strand_filter, width):
     """Reads of one width (fragments extended to fragLen, fixed read lengths): the layout keeps
     their starts alone and the lean kernel streams those (end = start + width - 1 formed when
     added); binned, per-base and heavy rows, both row orientations, edge rows -- bit-equal to
@@ -220,12 +220,12 @@ def test_lean_uniform_width_reads(gpu, stranded, width):
     r0.start[1], r0.end[1] = 1, 2000  # (a start at 0 shortens its row: an R-RNG layout)
     rows = RowTable(r0.seg_off, r0.chrom, r0.start, r0.end, r0.strand, ignore_strand=not stranded)
     for bins in (Bins([("whole", 1000)]), Bins([("whole", 0, 2000)]), Bins([("whole", 250)])):
-        lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, bins, heavy_threshold=64)
+        lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, bins, strand_filter, heavy_threshold=64)
         assert kind == 1
         check(lean, exp)
         same(lean, gen)
     mixed = (reads[0], reads[1], reads[2].copy(), reads[3])
     mixed[2][7] += 1
-    lean, gen, kind, exp = plans(mixed, CHROM_LEN, rows, Bins([("whole", 1000)]))
+    lean, gen, kind, exp = plans(mixed, CHROM_LEN, rows, Bins([("whole", 1000)]), strand_filter)
     check(lean, exp)
     same(lean, gen)

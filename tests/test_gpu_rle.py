@@ -154,15 +154,16 @@ def test_flanks_per_base_and_errors(gpu):
         profile_rle([np.arange(3, dtype=np.int32)], Bins([("whole", 4)], interp="neighborhood"))
 
 
-@pytest.mark.parametrize("seed", [0, 1])
-def test_coverage_rle_runs_across_sub_chunk_seams(gpu, seed):
+@pytest.mark.parametrize("seed,widths", [(0, (5, 300)), (1, (5, 300)), (2, (150, 150))])
+def test_coverage_rle_runs_across_sub_chunk_seams(gpu, seed, widths):
     """rcp_coverage_rle counts each row's runs inside the coverage pileup (a wave per sub-chunk
     of the row's positions) plus the seams between sub-chunks: rows shorter than, equal to and
     many times one wave chunk (1023 / 2047 / 4095 positions), flat rows (no reads: one run),
-    deep hot spots and NULL rows give the oracle's runs exactly; a NULL row keeps no runs."""
+    deep hot spots and NULL rows give the oracle's runs exactly; a NULL row keeps no runs.
+    Reads of one width (150) take the start-only stream."""
     from recoup_amd.engine import ReadSet, RowTable, coverage_rle_host
     rng = np.random.default_rng(100 + seed)
-    reads = make_reads(rng, 80_000, widths=(5, 300))
+    reads = make_reads(rng, 80_000, widths=widths)
     gap = ~((reads[0] == 0) & (reads[2] >= 100_000) & (reads[1] <= 110_000))
     reads = tuple(x[gap] for x in reads)
     lens = np.array([1, 2, 63, 64, 1023, 1024, 1025, 2046, 2047, 2048, 2049, 4095, 4096, 4097, 8191, 12_000,

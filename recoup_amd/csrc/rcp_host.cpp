@@ -94,8 +94,9 @@ hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* 
 hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, int64_t* d_count,
                               int64_t* d_run_off, void* temp, size_t* temp_bytes, int32_t* d_values,
                               int32_t* d_lengths, int pass, hipStream_t stream);
-hipError_t rcp_launch_width_range(int64_t n, const int2* se, int32_t* mm, hipStream_t stream);
-hipError_t rcp_launch_starts(int64_t n, const int2* se, int32_t* st, hipStream_t stream);
+hipError_t rcp_launch_width_range(int64_t n, const uint64_t* keys, const int32_t* vals, int32_t* mm,
+                                  hipStream_t stream);
+hipError_t rcp_launch_split_uniform(int64_t n, const int2* se, int32_t* st, int32_t* pmax, hipStream_t stream);
 hipError_t rcp_rle_seams_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, const uint8_t* d_valid,
                              int32_t chunk_bins, int32_t chunk_cap, int64_t* d_count, hipStream_t stream);
 hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t* off, const int32_t* pmax, int32_t* out,
@@ -460,41 +461,46 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     }
     keys.reset();
     vals.reset();
-    HIP_TRY(L->stream_off.alloc(8 * (n_streams + 2), s));
-    HIP_TRY(L->se.alloc(8 * std::max<int64_t>(n, 1), s));
-    HIP_TRY(scan_in.alloc(8 * std::max<int64_t>(n, 1)));
-    HIP_TRY(rcp_launch_streams(n, keys2.as<uint64_t>(), vals2.as<int32_t>(), L->stream_off.as<int64_t>(),
-                               n_streams + 2, L->se.as<int2>(), scan_in.as<uint64_t>(), s));
-    LAYOUT_MARK("  streams+pack");
-    keys2.reset();
-    vals2.reset();
-    HIP_TRY(scan_out.alloc(8 * std::max<int64_t>(n, 1)));
-    if (n > 0) {
-        size_t tb2 = 0;
-        HIP_TRY(rcp_segmax_scan(nullptr, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
-        if (tb2 > temp.bytes) HIP_TRY(temp.alloc(tb2));
-        HIP_TRY(rcp_segmax_scan(temp.p, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
-    }
-    HIP_TRY(L->pmax.alloc(4 * std::max<int64_t>(n, 1), s));
-    HIP_TRY(rcp_launch_unpack_pmax(n, scan_out.as<uint64_t>(), L->pmax.as<int32_t>(), s));
-    LAYOUT_MARK("  pmax scan");
-    // reads of one width: keep their starts alone for the lean pileup (half its read bytes)
+    // reads of one width (fixed read lengths, fragments extended to fragLen): their ends ascend
+    // with the starts inside a stream, so pmax = end (no segmented scan) and the pileup
+    // kernels stream the starts alone (half their read bytes)
+    bool uniform = false;
     if (n > 0) {
         PoolBuf mm(s);
         HIP_TRY(mm.alloc(8));
         const int32_t seed[2] = {INT32_MAX, INT32_MIN};
         HIP_TRY(hipMemcpyAsync(mm.p, seed, 8, hipMemcpyHostToDevice, s));
-        HIP_TRY(rcp_launch_width_range(n, L->se.as<int2>(), mm.as<int32_t>(), s));
+        HIP_TRY(rcp_launch_width_range(n, keys2.as<uint64_t>(), vals2.as<int32_t>(), mm.as<int32_t>(), s));
         int32_t h_mm[2] = {0, 0};
         HIP_TRY(hipMemcpyAsync(h_mm, mm.p, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (h_mm[0] == h_mm[1] && h_mm[0] >= 0) {
-            HIP_TRY(L->st.alloc(4 * (size_t)n, s));
-            HIP_TRY(rcp_launch_starts(n, L->se.as<int2>(), L->st.as<int32_t>(), s));
-            L->st_w = h_mm[0];
-        }
+        uniform = h_mm[0] == h_mm[1] && h_mm[0] >= 0;
+        if (uniform) L->st_w = h_mm[0];
     }
-    LAYOUT_MARK("  uniform starts");
+    LAYOUT_MARK("  width range");
+    HIP_TRY(L->stream_off.alloc(8 * (n_streams + 2), s));
+    HIP_TRY(L->se.alloc(8 * std::max<int64_t>(n, 1), s));
+    if (!uniform) HIP_TRY(scan_in.alloc(8 * std::max<int64_t>(n, 1)));
+    HIP_TRY(rcp_launch_streams(n, keys2.as<uint64_t>(), vals2.as<int32_t>(), L->stream_off.as<int64_t>(),
+                               n_streams + 2, L->se.as<int2>(), uniform ? nullptr : scan_in.as<uint64_t>(), s));
+    LAYOUT_MARK("  streams+pack");
+    keys2.reset();
+    vals2.reset();
+    HIP_TRY(L->pmax.alloc(4 * std::max<int64_t>(n, 1), s));
+    if (uniform) {
+        HIP_TRY(L->st.alloc(4 * (size_t)n, s));
+        HIP_TRY(rcp_launch_split_uniform(n, L->se.as<int2>(), L->st.as<int32_t>(), L->pmax.as<int32_t>(), s));
+    } else {
+        HIP_TRY(scan_out.alloc(8 * std::max<int64_t>(n, 1)));
+        if (n > 0) {
+            size_t tb2 = 0;
+            HIP_TRY(rcp_segmax_scan(nullptr, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
+            if (tb2 > temp.bytes) HIP_TRY(temp.alloc(tb2));
+            HIP_TRY(rcp_segmax_scan(temp.p, &tb2, scan_in.as<uint64_t>(), scan_out.as<uint64_t>(), n, s));
+        }
+        HIP_TRY(rcp_launch_unpack_pmax(n, scan_out.as<uint64_t>(), L->pmax.as<int32_t>(), s));
+    }
+    LAYOUT_MARK("  pmax");
     scan_in.reset();
     scan_out.reset();
     temp.reset();

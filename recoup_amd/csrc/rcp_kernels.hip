@@ -458,7 +458,7 @@ __global__ void rcp_pack_kernel(int64_t n, const uint64_t* __restrict__ keys, co
     const int32_t start = (int32_t)((uint32_t)k ^ 0x80000000u);
     const int32_t end = vals[i];
     se[i] = make_int2(start, end);
-    scan_in[i] = (k & 0xFFFFFFFF00000000ull) | (uint64_t)((uint32_t)end ^ 0x80000000u);
+    if (scan_in) scan_in[i] = (k & 0xFFFFFFFF00000000ull) | (uint64_t)((uint32_t)end ^ 0x80000000u);
 }
 
 __global__ void rcp_unpack_pmax_kernel(int64_t n, const uint64_t* __restrict__ scan_out, int32_t* __restrict__ pmax) {
@@ -3024,9 +3024,12 @@ extern "C" hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, c
     return hipGetLastError();
 }
 
-// Uniform-width readsets: the range of end - start over the layout's reads (mm[0] min, mm[1]
-// max; the caller seeds INT32_MAX / INT32_MIN), then, when it is one value, the starts alone.
-__global__ void __launch_bounds__(kBlock) rcp_width_range_kernel(int64_t n, const int2* __restrict__ se,
+// Uniform-width readsets: the range of end - start over the layout's sorted (key, end) pairs
+// (mm[0] min, mm[1] max; the caller seeds INT32_MAX / INT32_MIN).  When it is one value the
+// ends ascend with the starts inside every stream, so the prefix max of the ends is the end
+// itself (no segmented scan), and the starts are kept alone for the pileup kernels.
+__global__ void __launch_bounds__(kBlock) rcp_width_range_kernel(int64_t n, const uint64_t* __restrict__ keys,
+                                                                const int32_t* __restrict__ vals,
                                                                 int32_t* __restrict__ mm) {
     __shared__ int32_t bmin, bmax;
     if (threadIdx.x == 0) {
@@ -3036,8 +3039,8 @@ __global__ void __launch_bounds__(kBlock) rcp_width_range_kernel(int64_t n, cons
     __syncthreads();
     int32_t lo = INT32_MAX, hi = INT32_MIN;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-        const int2 r = se[i];
-        const int32_t w = r.y - r.x;
+        const int32_t start = (int32_t)((uint32_t)keys[i] ^ 0x80000000u);
+        const int32_t w = (int32_t)((int64_t)vals[i] - (int64_t)start);  // ends >= start - 1
         lo = min(lo, w);
         hi = max(hi, w);
     }
@@ -3050,23 +3053,30 @@ __global__ void __launch_bounds__(kBlock) rcp_width_range_kernel(int64_t n, cons
     }
 }
 
-__global__ void __launch_bounds__(kBlock) rcp_starts_kernel(int64_t n, const int2* __restrict__ se,
-                                                           int32_t* __restrict__ st) {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
-        st[i] = se[i].x;
+// se -> starts alone (st) and the prefix max of the ends (= the ends, reads of one width)
+__global__ void __launch_bounds__(kBlock) rcp_split_uniform_kernel(int64_t n, const int2* __restrict__ se,
+                                                                  int32_t* __restrict__ st,
+                                                                  int32_t* __restrict__ pmax) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        const int2 r = se[i];
+        st[i] = r.x;
+        pmax[i] = r.y;
+    }
 }
 
-extern "C" hipError_t rcp_launch_width_range(int64_t n, const int2* se, int32_t* mm, hipStream_t stream) {
+extern "C" hipError_t rcp_launch_width_range(int64_t n, const uint64_t* keys, const int32_t* vals, int32_t* mm,
+                                             hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const int64_t grid = std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);
-    hipLaunchKernelGGL(rcp_width_range_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, se, mm);
+    hipLaunchKernelGGL(rcp_width_range_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, keys, vals, mm);
     return hipGetLastError();
 }
 
-extern "C" hipError_t rcp_launch_starts(int64_t n, const int2* se, int32_t* st, hipStream_t stream) {
+extern "C" hipError_t rcp_launch_split_uniform(int64_t n, const int2* se, int32_t* st, int32_t* pmax,
+                                               hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const int64_t grid = std::min<int64_t>((n + kBlock - 1) / kBlock, 16384);
-    hipLaunchKernelGGL(rcp_starts_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, se, st);
+    hipLaunchKernelGGL(rcp_split_uniform_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, se, st, pmax);
     return hipGetLastError();
 }
 

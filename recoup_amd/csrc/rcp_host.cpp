@@ -1382,7 +1382,13 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
 #ifndef RCP_NO_UNI
 #define RCP_NO_UNI 0  // 1: never stream starts alone (A/B only)
 #endif
-    P.st = RL.st.p && !RCP_NO_UNI ? RL.st.as<int32_t>() : nullptr;  // uniform-width reads
+    // uniform-width reads: the general kernel and per-base lean plans stream the starts alone;
+    // binned lean plans keep the (start, end) pairs -- C4's latency-bound pile measured 4 % slower
+    // with starts (pileup 0.578 vs 0.555 ms, same box), C5's dense per-base rows 6 % faster
+    // (0.58 vs 0.62), the 1/8 C4 shard's general kernel 4 % (profiles/r03/pipeline/general_starts_ab.log,
+    // lean_starts_c4_ab.log)
+    const bool use_st = RL.st.p && !RCP_NO_UNI && (P.lean != 1 || P.lean_rounds == 2);
+    P.st = use_st ? RL.st.as<int32_t>() : nullptr;
     P.st_w = RL.st_w;
     P.pmax = RL.pmax.as<int32_t>();
     P.stream_off = RL.stream_off.as<int64_t>();

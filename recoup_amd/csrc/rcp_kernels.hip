@@ -2064,6 +2064,12 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
 #endif
 // 1: three batches of reads in flight per row instead of two (measured neutral on C4 / C5 /
 // C3, tools/ab_variants.sh: kept as a build option, off by default)
+#ifndef RCP_LUNI_RUNS
+#define RCP_LUNI_RUNS 1  // start-only dense rows: one run detection for both atomics (0: per key)
+#endif
+#ifndef RCP_LEAN_ABL
+#define RCP_LEAN_ABL 0  // timing ablations only (wrong results): 1 no LDS adds (loads kept), 2 no output stores
+#endif
 #ifndef RCP_LWPE
 #define RCP_LWPE 6
 #endif
@@ -2164,6 +2170,28 @@ __device__ __forceinline__ void lean_add_runs(const LeanRow& m, int2 rd, bool ac
     const int32_t b = REV ? m.k - x0 + 1 : x1 + m.k + 1;
     run_add(diff, lp(a, sh), act, 1);
     run_add(diff, lp(b, sh), act, -1);
+}
+
+// lean_add_runs for reads of one width w (the start-only stream): a read covers window
+// positions [u, u + w] with u = s + k (forward) or k - s - w (reversed), so its two keys are
+// functions of u alone -- one run detection over u serves both atomics (clipped to the
+// chunk's window [lo_w, hi_w]); equal u gives equal keys, as the pair path's runs would.
+template <bool REV>
+__device__ __forceinline__ void lean_add_runs_uni(const LeanRow& m, int32_t s, int32_t w, int32_t lo_w, int32_t hi_w,
+                                                  bool act, int32_t* diff, int sh) {
+    const int lane = threadIdx.x & 63;
+    const int32_t u = REV ? m.k - s - w : s + m.k;
+    act = act && u <= hi_w && u + w >= lo_w;
+    const int32_t key = act ? u : INT32_MIN;  // never a window position
+    const int32_t prev = __builtin_amdgcn_update_dpp(INT32_MIN + 1, key, 0x138, 0xf, 0xf, false);  // wave_shr:1
+    const bool head = lane == 0 || key != prev;
+    const uint64_t heads = __ballot(head);
+    const uint64_t above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+    const int len = (above ? __builtin_ctzll(above) : 64) - lane;
+    if (head && act) {
+        atomicAdd(&diff[lp(max(u, lo_w), sh)], len);
+        atomicSub(&diff[lp(min(u + w, hi_w) + 1, sh)], len);
+    }
 }
 
 // (tile, chunk) of an item code, its part and first bin
@@ -2325,6 +2353,28 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 #endif
                 const bool dense = RCP_LDENSE && n >= (uint32_t)npos;  // wave-uniform
                 auto add_batch = [&](uint32_t q0, const RdT (&src)[4]) {
+                    if (RCP_LEAN_ABL & 1) {  // timing ablation: loads kept, no adds
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) asm volatile("" ::"v"(src[u]));
+                        return;
+                    }
+                    if constexpr (UNI) {
+                        if (dense && RCP_LUNI_RUNS) {
+                            const int32_t w = P.st_w;
+                            const int32_t lo_w = m.rev ? m.k - m.gpe : m.gps + m.k;
+                            const int32_t hi_w = m.rev ? m.k - m.gps : m.gpe + m.k;
+                            if (m.rev) {
+#pragma unroll
+                                for (int u = 0; u < 4; ++u)
+                                    lean_add_runs_uni<true>(m, src[u], w, lo_w, hi_w, q0 + lane + 64u * u < n, diff, sh);
+                            } else {
+#pragma unroll
+                                for (int u = 0; u < 4; ++u)
+                                    lean_add_runs_uni<false>(m, src[u], w, lo_w, hi_w, q0 + lane + 64u * u < n, diff, sh);
+                            }
+                            return;
+                        }
+                    }
                     if (dense) {
                         if (m.rev) {
 #pragma unroll
@@ -2479,7 +2529,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 #pragma unroll
                 for (int j = 0; j < kPass; ++j)
                     if (j < npass) asm volatile("" : "+v"(v[j].x), "+v"(v[j].y), "+v"(v[j].z), "+v"(v[j].w));
-                if (live) {
+                if (live && !(RCP_LEAN_ABL & 2)) {
                     // power-of-two bin width: multiplying by its reciprocal is exact; a NULL row
                     // (flag 1) scales its (unwritten) stage words by 0.0 -> zeros
                     const double rdd = 1.0 / (double)(1 << ((w0 >> 4) & 31));

@@ -57,10 +57,10 @@ def parse():
     ap.add_argument("--verify-gather", action="store_true",
                     help="N > 1: rank 0 also runs the whole workload alone and checks the gathered matrix bit for bit")
     ap.add_argument("--no-e2e", action="store_true", help="skip the one-off host-to-host timing")
-    ap.add_argument("--inflight", default="auto", choices=["auto", "1", "2", "3"],
+    ap.add_argument("--inflight", default="auto", choices=["auto", "1", "2", "3", "4"],
                     help="samples in flight: D DISTINCT samples (independent read sets over the same region "
                          "table, as profileMatrix loops over a recoup input list) on D HIP streams, step k "
-                         "= one complete pass of sample k %% D; auto (default): the fastest of 1, 2, 3, "
+                         "= one complete pass of sample k %% D; auto (default): the fastest of 1, 2, 3, 4, "
                          "timed on every rank (max over ranks) so all ranks run the same D.  The "
                          "one-sample pass time is always reported beside it (single_pass_ms)")
     ap.add_argument("--traffic", default=None,
@@ -252,7 +252,7 @@ def main():
     # pileup.  D = 1 (the default) is one sample, pass after pass.
     plans, outs, valids, rsets = [plan], [out], [valid], [rs]
     streams = [torch.cuda.current_stream()]
-    dmax = 3 if args.inflight == "auto" else int(args.inflight)
+    dmax = 4 if args.inflight == "auto" else int(args.inflight)
     if dmax > 1:
         for k in range(1, dmax):
             dk = workload(args, dev, sample=k)[0]
@@ -275,7 +275,7 @@ def main():
     for p in plans:
         p.status()
     tune = {}
-    for d in ([1] + ([2, 3] if args.inflight == "auto" else [])):
+    for d in ([1] + ([2, 3, 4] if args.inflight == "auto" else [])):
         torch.cuda.synchronize()
         t = time.perf_counter()
         passes(d, max(args.steps, 10))

@@ -195,6 +195,16 @@ __device__ __forceinline__ void ps_prepare(PairStream& ps, int32_t gps, int32_t 
     ps.pa = ps.pl;
 }
 
+// Candidate slot u of a lane in a batch: lane + 64 u, or (RCP_PS_INTERLEAVE) 4 lane + u, so the
+// 64 adds of one instruction are 4 reads apart (fewer same-bank / same-address LDS atomics on
+// start-sorted reads)
+#ifndef RCP_PS_INTERLEAVE
+#define RCP_PS_INTERLEAVE 1  // C3 pass 0.760-0.770 -> 0.753-0.755 ms (interp kernel 0.112 -> 0.106), profiles/r03/pipeline/ps_interleave_ab.log
+#endif
+__device__ __forceinline__ uint32_t ps_slot(int lane, int u) {
+    return RCP_PS_INTERLEAVE ? 4u * (uint32_t)lane + (uint32_t)u : (uint32_t)lane + 64u * (uint32_t)u;
+}
+
 // Issue the loads of batch [q0, q0 + 256) (q0 < N; lanes past N load the last candidate again).
 __device__ __forceinline__ void ps_load(const RcpPlanDev& P, PairStream& ps, uint32_t q0, int2 (&dst)[4]) {
     const int lane = threadIdx.x & 63;
@@ -203,7 +213,7 @@ __device__ __forceinline__ void ps_load(const RcpPlanDev& P, PairStream& ps, uin
     const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)ps.delta, ps.pl);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        qc[u] = min(q0 + lane + 64u * u, ps.N - 1);
+        qc[u] = min(q0 + ps_slot(lane, u), ps.N - 1);
         d[u] = d0;
     }
     const uint32_t qe = min(q0 + 256u, ps.N);
@@ -254,14 +264,14 @@ __device__ __forceinline__ void ps_add(const RcpPlanDev& P, const RcpSeg& sg, Pa
             const int32_t k = o.off + o.hi - P0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const uint32_t q = q0 + lane + 64u * u;
+                const uint32_t q = q0 + ps_slot(lane, u);
                 add_read_k<true>(P, o, k, rd[u], gs, ge, diff, sh, q >= sp && q < ep);
             }
         } else {
             const int32_t k = o.off - o.lo - P0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const uint32_t q = q0 + lane + 64u * u;
+                const uint32_t q = q0 + ps_slot(lane, u);
                 add_read_k<false>(P, o, k, rd[u], gs, ge, diff, sh, q >= sp && q < ep);
             }
         }

@@ -91,6 +91,11 @@ struct RcpPlanDev {
     const int32_t* dir_l;
     const int32_t* dir_u;
     const int64_t* dir_off;    // [n_chrom*3 + 1]
+    // the same directory with each bucket's first keys inline, one 128-byte line per entry e:
+    // words 0..15 = dir_l[e], dir_l[e+1], pmax[dir_l[e] + i] (i < 14); words 16..31 = dir_u[e],
+    // dir_u[e+1], start[dir_u[e] + i] -- a bound search whose answer lies among a bucket's first
+    // 14 reads reads this one line (null = not built)
+    const int32_t* dir_k;
     int32_t dir_shift;
     int32_t merged;            // 1: the strand-merged layout (all reads in stream chrom*3)
     // rows

@@ -104,6 +104,8 @@ hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t* off, const
 hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const int64_t* dir_off, const int64_t* off,
                           const int32_t* pmax, const int2* se, int shift, int32_t* dir_l, int32_t* dir_u,
                           hipStream_t stream);
+hipError_t rcp_launch_dirk(int64_t n_entries, const int32_t* dir_lu, const int32_t* pmax, const int2* se,
+                           int32_t* dir_k, hipStream_t stream);
 }
 
 namespace {
@@ -122,6 +124,9 @@ constexpr int kHeavyThreshold = 4096;  // candidate reads per column chunk above
                                         // (8192 before the lean kernel dealt rows dynamically; C4 0.647 -> 0.633 ms)
 #ifndef RCP_DIR_READS
 #define RCP_DIR_READS 8  // mean reads per directory bucket (the locate kernel's search depth)
+#endif
+#ifndef RCP_DIR_INLINE
+#define RCP_DIR_INLINE 1  // build the inline-key directory (one line per locate search)
 #endif
 #ifndef RCP_HEAVY_SLICE
 #define RCP_HEAVY_SLICE 4096
@@ -345,6 +350,7 @@ struct ReadLayout {
     std::vector<int64_t> h_dir_off;     // n_chrom*3 + 1
     PoolArr se, pmax, stream_off;
     PoolArr dir_l, dir_off;
+    PoolArr dir_k;      // inline-key directory (128 bytes per entry; rcp_device.h)
     int32_t dir_shift = 12;
     PoolArr st;         // the starts alone when every read has one width (st_w = end - start)
     int32_t st_w = 0;
@@ -546,6 +552,11 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     HIP_TRY(rcp_launch_dir(ne, n_streams, L->dir_off.as<int64_t>(), L->stream_off.as<int64_t>(),
                            L->pmax.as<int32_t>(), L->se.as<int2>(), shift, L->dir_l.as<int32_t>(),
                            L->dir_l.as<int32_t>() + 1, s));
+    if (RCP_DIR_INLINE) {
+        HIP_TRY(L->dir_k.alloc(128 * std::max<int64_t>(ne, 1), s));
+        HIP_TRY(rcp_launch_dirk(ne, L->dir_l.as<int32_t>(), L->pmax.as<int32_t>(), L->se.as<int2>(),
+                                L->dir_k.as<int32_t>(), s));
+    }
     HIP_TRY(hipStreamSynchronize(s));
     LAYOUT_MARK("  directory");
     rs->n = kept;
@@ -1396,6 +1407,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.dir_l = RL.dir_l.as<int32_t>();
     P.dir_u = RL.dir_l.as<int32_t>() + 1;  // interleaved with dir_l (stride 2)
     P.dir_off = RL.dir_off.as<int64_t>();
+    P.dir_k = RL.dir_k.as<int32_t>();
     P.dir_shift = RL.dir_shift;
     P.merged = rows->ignore_strand ? 1 : 0;
     P.n_chrom = rs->n_chrom;

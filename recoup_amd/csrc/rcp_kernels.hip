@@ -557,6 +557,29 @@ __global__ void rcp_dir_kernel(int64_t n_entries, int64_t n_streams, const int64
     dir_u[2 * e] = (int32_t)upper_bound_start(se, so, eo, (int32_t)min(v - 1, (int64_t)INT32_MAX));
 }
 
+// Inline-key directory (rcp_device.h dir_k): thread t fills half t & 1 of entry t >> 1 from the
+// interleaved (dir_l, dir_u) entries e and e + 1 of the same directory.
+constexpr int kDirKeys = 14;
+__global__ void rcp_dirk_kernel(int64_t n_entries, const int32_t* __restrict__ dir_lu, const int32_t* __restrict__ pmax,
+                                const int2* __restrict__ se, int32_t* __restrict__ dir_k) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * n_entries) return;
+    const int64_t e = t >> 1;
+    const int h = (int)(t & 1);
+    const int32_t a = dir_lu[2 * e + h];
+    // the last entry of a stream is never a bucket's first edge (its successor is the next
+    // stream's): any count is fine there, but stay inside the arrays
+    const int32_t b = e + 1 < n_entries ? max(dir_lu[2 * (e + 1) + h], a) : a;
+    int32_t w[16];
+    w[0] = a;
+    w[1] = b;
+#pragma unroll
+    for (int i = 0; i < kDirKeys; ++i) w[2 + i] = a + i < b ? (h ? se[a + i].x : pmax[a + i]) : 0;
+    int4* dst = reinterpret_cast<int4*>(dir_k + 32 * e + 16 * h);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
 // =================================================================================
 // locate: per (row, segment, stream) read ranges, the NULL rules, heavy-row slots
 // =================================================================================
@@ -613,11 +636,41 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
         up[u] = dst[u] == -1 || (dst[u] >= 0 && (dst[u] & 1));
         lo[u] = hi[u] = 0;
         thr[u] = (int64_t)v[u] + (up[u] ? 1 : 0);
-        if (u < cnt) {
+        if (u < cnt && !P.dir_k) {
             const int32_t b = min(max(v[u], 0) >> P.dir_shift, nb[u] - 1);
             const int32_t* dir = up[u] ? P.dir_u : P.dir_l;  // interleaved: stride 2
             lo[u] = (uint32_t)dir[2 * (d0[u] + b)];
             hi[u] = (uint32_t)dir[2 * (d0[u] + b + 1)];
+        }
+    }
+    if (P.dir_k) {
+        // one line per search: the bucket's edges and first keys; the answer is the number of
+        // those keys below the threshold unless all of them are (then bisect the rest)
+#ifndef RCP_DIRK_QUADS
+#define RCP_DIRK_QUADS 4  // 16-byte words of the entry half read per search (keys: 4 q - 2)
+#endif
+        constexpr int kQ = RCP_DIRK_QUADS, kKeys = 4 * kQ - 2;
+        int4 w[K][kQ];
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            if (u < cnt) {
+                const int32_t b = min(max(v[u], 0) >> P.dir_shift, nb[u] - 1);
+                const int4* src = reinterpret_cast<const int4*>(P.dir_k + 32 * (d0[u] + b) + (up[u] ? 16 : 0));
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) w[u][q] = src[q];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            if (u < cnt) {
+                const int32_t* x = reinterpret_cast<const int32_t*>(w[u]);
+                const int32_t n = x[1] - x[0];
+                uint32_t c = 0;
+#pragma unroll
+                for (int i = 0; i < kKeys; ++i) c += (i < n && (int64_t)x[2 + i] < thr[u]) ? 1u : 0u;
+                lo[u] = (uint32_t)x[0] + c;
+                hi[u] = c < (uint32_t)kKeys ? lo[u] : (uint32_t)x[1];
+            }
         }
     }
     const int32_t* se = reinterpret_cast<const int32_t*>(P.se);
@@ -2933,6 +2986,14 @@ extern "C" hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t*
     if (n_streams == 0) return hipSuccess;
     hipLaunchKernelGGL(rcp_stream_maxend_kernel, dim3((unsigned)((n_streams + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        stream, n_streams, off, pmax, out);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rcp_launch_dirk(int64_t n_entries, const int32_t* dir_lu, const int32_t* pmax, const int2* se,
+                                      int32_t* dir_k, hipStream_t stream) {
+    if (n_entries == 0) return hipSuccess;
+    hipLaunchKernelGGL(rcp_dirk_kernel, dim3((unsigned)((2 * n_entries + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                       n_entries, dir_lu, pmax, se, dir_k);
     return hipGetLastError();
 }
 

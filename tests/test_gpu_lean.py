@@ -229,3 +229,31 @@ def test_lean_uniform_width_reads(gpu, stranded, strand_filter, width):
     lean, gen, kind, exp = plans(mixed, CHROM_LEN, rows, Bins([("whole", 1000)]), strand_filter)
     check(lean, exp)
     same(lean, gen)
+
+
+@pytest.mark.parametrize("kernel", ["lean", "general"])
+def test_dense_bucket_bounds(gpu, kernel):
+    """Row edges inside stacks of duplicate reads: the locate searches' buckets hold hundreds of
+    reads, so their answers lie past the directory's inline keys (rcp_device.h dir_k) and the
+    bisection continues in the read arrays."""
+    from recoup_amd.engine import Bins, Plan, ReadSet, RowTable
+    from tests import oracle_rows
+    rng = np.random.default_rng(77)
+    chrom, start, end, strand = make_reads(rng, 20_000)
+    piles = np.sort(rng.choice(np.arange(5_000, 80_000, 700), 40, replace=False))
+    pc = np.repeat(np.int32(2), 40 * 150)
+    ps = np.repeat(piles, 150).astype(np.int32) + rng.integers(0, 3, 40 * 150).astype(np.int32)
+    pe = ps + rng.integers(10, 90, ps.size).astype(np.int32)
+    pst = rng.integers(0, 2, ps.size).astype(np.int8)
+    reads = (np.concatenate([chrom, pc]), np.concatenate([start, ps]), np.concatenate([end, pe]),
+             np.concatenate([strand, pst]))
+    # rows starting / ending a few bases around each pile (both edges searched inside it)
+    off = rng.integers(-60, 60, 4 * 40)
+    s = np.repeat(piles, 4) + off
+    rows = RowTable.from_ranges(np.full(s.size, 2, np.int32), s, s + 1023, rng.integers(0, 3, s.size).astype(np.int8))
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    ix = oracle_rows.index_for(reads, CHROM_LEN, None)
+    cov = oracle_rows.row_coverage(ix, rows)
+    for bins in (Bins([("whole", 1024)]), Bins([("whole", 256)])):
+        res = Plan(rs, rows, bins, kernel=kernel, heavy_threshold=0).run()
+        check(res, oracle_rows.profile(cov, bins))

@@ -120,7 +120,10 @@ constexpr int kStageMaxBins = RCP_STAGE_MAX_BINS;  // bins per chunk (LDS stage 
 #define RCP_LDS_BUDGET (80 * 1024)
 #endif
 constexpr size_t kLdsBudget = RCP_LDS_BUDGET;  // pileup LDS per workgroup (80 KB: two per CU)
-constexpr int kHeavyThreshold = 4096;  // candidate reads per column chunk above which a row is split across workgroups
+#ifndef RCP_HEAVY_THRESHOLD
+#define RCP_HEAVY_THRESHOLD 4096
+#endif
+constexpr int kHeavyThreshold = RCP_HEAVY_THRESHOLD;  // candidate reads per column chunk above which a row is split across workgroups
                                         // (8192 before the lean kernel dealt rows dynamically; C4 0.647 -> 0.633 ms)
 #ifndef RCP_DIR_READS
 #define RCP_DIR_READS 8  // mean reads per directory bucket (the locate kernel's search depth)

@@ -1462,6 +1462,9 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         while (P.rounds > 1 &&
                (int64_t)((R + tile * P.rounds - 1) / (tile * P.rounds)) * P.n_chunks_total < 2 * (int64_t)cus)
             P.rounds /= 2;
+#ifdef RCP_GEN_ROUNDS_FIX  // A/B only: force the general kernel's rounds per workgroup
+        P.rounds = std::min(rmax, (int)RCP_GEN_ROUNDS_FIX);
+#endif
         plan->tile_rows = P.lean ? (P.lean_rounds == 2 ? 2 * tile : rcp_tile_rows()) : tile * P.rounds;
     }
     plan->grid = (int64_t)((R + plan->tile_rows - 1) / plan->tile_rows) * P.n_chunks_total;

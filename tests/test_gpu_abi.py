@@ -109,6 +109,30 @@ def test_readset_info_and_strand_filter(c1):
     assert r.n == len(s["start"]) - 20
 
 
+@pytest.mark.parametrize("n", [13, 1_001, 17_000_003])
+def test_strand_codes_cross_pcie(gpu, n):
+    """Host strand codes through both upload paths (rcp_stage.h: the direct copy below 4 MB,
+    the pinned staging above it): each (chromosome, strand) stream holds exactly the reads of
+    that code, and codes outside 0..2 (-1, 3, 5, -128) drop their reads."""
+    from recoup_amd.engine import ReadSet
+    rng = np.random.default_rng(n)
+    codes = np.array([0, 1, 2, 0, 1, 2, 0, 1, 2, -1, 3, 5, -128], np.int8)
+    strand = codes[rng.integers(0, len(codes), n)]
+    chrom = rng.integers(0, 2, n).astype(np.int32)
+    start = rng.integers(1, 1_000_000, n).astype(np.int32)
+    end = start + 49
+    seql = np.array([2_000_000, 2_000_000], np.int64)
+    rs = ReadSet(chrom, start, end, strand, seql)
+    keep = (strand >= 0) & (strand <= 2)
+    assert rs.n == int(keep.sum())
+    so = rs.stream_off
+    for c in range(2):
+        for q in range(3):
+            assert so[3 * c + q + 1] - so[3 * c + q] == int(((chrom == c) & (strand == q)).sum()), (c, q)
+    plus = ReadSet(chrom, start, end, strand, seql, strand_filter="+")
+    assert plus.n == int((strand == 0).sum())
+
+
 @pytest.mark.parametrize("n_rows,n_bins", [(20_003, 200), (4_099, 4000)])
 def test_rcp_profile_staged_copy(gpu, n_rows, n_bins):
     """rcp_profile's output above the 4 MB direct-copy limit travels through the pinned

@@ -1,6 +1,6 @@
 #!/bin/bash
 # re-entry check of the committed tree on a fresh box: GPU suite, smoke, the default bench line
-OUT=gpurun_out/r3f1
+OUT=gpurun_out/${OUTD:-r3f1}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }

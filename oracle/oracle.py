@@ -9,6 +9,8 @@ the hot path so the tests can call it like the reference's own API:
 * ``profile_matrix``     R/profile.R:1-98 (equal-length test on sample 1, per-base vs
                          binned, center/upstream/downstream + cbind)
 * ``rna_merge``          R/coverage.R:115-121 (c(left, center, right), NULL if any NULL)
+* ``profile_dimnames``   the dimnames of profileMatrix's matrix (rbind of a named list,
+                         unlist of llply's bins, cbind + rownames<-)
 """
 import ctypes
 import os
@@ -317,6 +319,38 @@ def profile_matrix(covs, flank, bin_params, scales=None, kind="Rejection"):
             else:
                 out.append(_base_matrix(cov, None, None, sc))
     return out
+
+
+def bin_colnames(n, stat):
+    """Names of a binned row, unlist(llply(split(x, f), stat)) (R/util.R:81-84, R/profile.R:208):
+    split names the bins by the factor levels "1".."n"; llply hands a function given by NAME
+    to plyr::each, whose one-function closure sets names(res) <- the function's name on a
+    length-1 result, so unlist joins the two: "1.mean", "2.mean", ..."""
+    return [f"{k}.{stat}" for k in range(1, int(n) + 1)]
+
+
+def profile_dimnames(names, flank, bin_params, equal):
+    """dimnames(input[[s]]$profile) after profileMatrix (R/profile.R:1-98) of a coverage list
+    named ``names`` (None = unnamed): None, or (rownames, colnames).
+
+    * equal lengths: the matrix is do.call("rbind", <list named like the coverage>) -- rownames
+      = names (R/profile.R:112-115,159-162,198-208); binned rows bring bin_colnames, per-base
+      rows (as.numeric of an Rle) none;
+    * unequal: cbind(left, center, right) of slices mapped over 1:length(cvrg) (unnamed rows):
+      colnames the parts' own, "" for a per-base flank; then rownames(...) <- names (:78-79)."""
+    fbs = int(bin_params.get("flankBinSize", 0))
+    rbs = int(bin_params.get("regionBinSize", 0))
+    stat = bin_params.get("sumStat", "mean")
+    rn = None if names is None else [str(x) for x in names]
+    if equal:
+        cn = bin_colnames(rbs, stat) if rbs != 0 else None
+    else:
+        f1, f2 = int(flank[0]), int(flank[1])
+        r = np.asarray([f1, f2], dtype=float) / (f1 + f2)
+        side = [bin_colnames(r_round(2 * fbs * r[k]), stat) if fbs != 0 else [""] * (f1, f2)[k]
+                for k in (0, 1)]
+        cn = (side[0] if f1 else []) + bin_colnames(rbs, stat) + (side[1] if f2 else [])
+    return None if rn is None and cn is None else (rn, cn)
 
 
 # ---------------------------------------------------------------- region windows

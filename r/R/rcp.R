@@ -261,40 +261,46 @@ coverageRnaRef <- function(input, genomeRanges, helperRanges, flank,
         lengths = as.integer(unlist(rl, use.names = FALSE)), isNull = isNull)
 }
 
-# parts: where codes 0 whole, 1 center, 2 upstream, 3 downstream; nBins 0 = per base
+# parts: where codes 0 whole, 1 center, 2 upstream, 3 downstream; nBins 0 = per base.
+# rowNames: the rownames the reference's matrix carries (NULL: none).  The shim sets the
+# matrix's dimnames as the reference's rbind / cbind leave them (r/src/recoup_amd_shim.c,
+# set_dimnames): rownames = rowNames, colnames "<bin>.<stat>" for binned parts, "" for per-base
+# parts, none when no part is binned
 .rcpProfileRle <- function(cvrg, where, flank, nBins, perBase, stat = "mean",
-    interpolation = "auto") {
+    interpolation = "auto", rowNames = NULL) {
     a <- .rcpRleArrays(cvrg)
     res <- .Call("rcp_R_profile_rle", a$runOff, a$values, a$lengths, a$isNull,
         as.integer(where), as.integer(if (is.null(flank)) c(0, 0) else flank),
         as.integer(nBins), as.integer(perBase), .rcpStat(stat), .rcpInterp(interpolation),
-        .rcpRngKind(), 1.0, .rcpDevices()[1], PACKAGE = "recoup")
+        .rcpRngKind(), 1.0, .rcpDevices()[1], rowNames, PACKAGE = "recoup")
     res$profile
 }
 
 # binCoverageMatrix (R/profile.R:153-212): splitVector of each element (or of its
-# center / upstream / downstream slice), NULL -> zeros
+# center / upstream / downstream slice), NULL -> zeros.  The reference's rbind is named by
+# names(cvrg) when it maps over cvrg itself (:159), unnamed when it maps over 1:length(cvrg)
+# (the slices, :167-187)
 binCoverageMatrix <- function(cvrg, binSize = 1000, stat = c("mean", "median"),
     interpolation = c("auto", "spline", "linear", "neighborhood"), flank = NULL,
     where = c("center", "upstream", "downstream"), rc = NULL) {
     w <- if (is.null(flank)) 0L else match(where[1], c("center", "upstream", "downstream"))
-    .rcpProfileRle(cvrg, w, flank, binSize, 0L, stat, interpolation)
+    .rcpProfileRle(cvrg, w, flank, binSize, 0L, stat, interpolation,
+        if (is.null(flank)) names(cvrg) else NULL)
 }
 
-# baseCoverageMatrix (R/profile.R:100-151): per-base rows (whole, or the flank slices)
+# baseCoverageMatrix (R/profile.R:100-151): per-base rows (whole, or the flank slices); rows
+# named as binCoverageMatrix's, no colnames (as.numeric of an Rle has none)
 baseCoverageMatrix <- function(cvrg, flank = NULL, where = c("upstream", "downstream"),
     rc = NULL) {
     if (is.null(flank)) {
         ok <- which(vapply(cvrg, function(x) length(x) > 0, TRUE))
         size <- if (length(ok)) length(cvrg[[ok[1]]]) else 0L
-        return(.rcpProfileRle(cvrg, 0L, NULL, 0L, size))
+        return(.rcpProfileRle(cvrg, 0L, NULL, 0L, size, rowNames = names(cvrg)))
     }
     w <- match(where[1], c("upstream", "downstream"))
     .rcpProfileRle(cvrg, w + 1L, flank, 0L, flank[w])
 }
 
-# profileMatrix (R/profile.R:1-98) with every column part of a sample in ONE library call:
-# the same parts, in the same order (left, center, right), as the reference's cbind
 # the column parts of profileMatrix: one whole part when all rows have one length, else
 # (upstream,) center (, downstream) with the flank bin counts of R/profile.R:24-60
 .rcpParts <- function(equal, len1, flank, binParams) {
@@ -309,6 +315,9 @@ baseCoverageMatrix <- function(cvrg, flank = NULL, where = c("upstream", "downst
         if (flank[k] == 0)
             next
         fb <- if (binParams$flankBinSize != 0) round(2 * binParams$flankBinSize * r[k]) else 0
+        # binCoverageMatrix(binSize = 0) stops in splitVector's sample() (R/util.R:74-79)
+        if (binParams$flankBinSize != 0 && fb == 0)
+            stop("invalid 'size' argument")
         if (k == 1) {
             where <- c(2L, where); nb <- c(fb, nb); pb <- c(if (fb) 0L else flank[1], pb)
         } else {
@@ -318,19 +327,32 @@ baseCoverageMatrix <- function(cvrg, flank = NULL, where = c("upstream", "downst
     list(where = where, nBins = nb, perBase = pb)
 }
 
-profileMatrixFused <- function(input, flank, binParams, rc = NULL) {
+# profileMatrix (R/profile.R:1-98), same signature and result: every sample's profile in ONE
+# library call -- the unequal-length branch's upstream / center / downstream parts (three
+# binCoverageMatrix or baseCoverageMatrix calls, :13-77) are one plan whose columns are their
+# cbind (:78), rownames = names of the coverage list (:79).  The equal-length branch is the
+# reference's own single binCoverageMatrix / baseCoverageMatrix call (:83-96), whose rows are
+# named by rbind.  As in the reference, every sample is (re)profiled once any sample lacks one
+profileMatrix <- function(input, flank, binParams, rc = NULL) {
+    hasProfile <- sapply(input, function(x) is.null(x$profile))
+    if (!any(hasProfile))
+        return(input)
     len <- lengths(input[[1]]$coverage)
     len <- len[len != 0]
     equal <- all(len == len[1])
     for (n in names(input)) {
-        if (!is.null(input[[n]]$profile))
+        message("Calculating profile for ", input[[n]]$name)
+        cvrg <- input[[n]]$coverage
+        if (equal) {
+            input[[n]]$profile <- if (binParams$regionBinSize != 0)
+                binCoverageMatrix(cvrg, binSize = binParams$regionBinSize,
+                    stat = binParams$sumStat, rc = rc) else
+                baseCoverageMatrix(cvrg, rc = rc)
             next
-        parts <- .rcpParts(equal, len[1], flank, binParams)
-        # the equal-length branch calls binCoverageMatrix without interpolation= (its default)
-        interp <- if (equal) "auto" else binParams$interpolation
-        input[[n]]$profile <- .rcpProfileRle(input[[n]]$coverage, parts$where, flank,
-            parts$nBins, parts$perBase, binParams$sumStat, interp)
-        rownames(input[[n]]$profile) <- names(input[[n]]$coverage)
+        }
+        parts <- .rcpParts(FALSE, NA, flank, binParams)
+        input[[n]]$profile <- .rcpProfileRle(cvrg, parts$where, flank, parts$nBins,
+            parts$perBase, binParams$sumStat, binParams$interpolation, names(cvrg))
     }
     return(input)
 }
@@ -347,6 +369,8 @@ profileMatrixFromReads <- function(input, mask, flank, binParams, ignore.strand 
     binArgs <- list(as.integer(parts$where), as.integer(if (is.null(flank)) c(0, 0) else flank),
         as.integer(parts$nBins), as.integer(parts$perBase), .rcpStat(binParams$sumStat),
         .rcpInterp(interp), .rcpRngKind(), 1.0)
+    # dimnames as profileMatrix leaves them: rows named by the mask (rbind of the named coverage
+    # list, or rownames<- after the cbind)
     devs <- .rcpDevices()
     todo <- which(vapply(input, function(x) is.null(x$profile), TRUE))
     # one row table for every sample: chromosome codes index the union of their seqlevels
@@ -356,21 +380,18 @@ profileMatrixFromReads <- function(input, mask, flank, binParams, ignore.strand 
         for (i in todo) {
             rs <- .rcpReadSet(input[[i]]$ranges, NULL, devs, lv)
             res <- do.call(.Call, c(list("rcp_R_profile_multi", rs$ptr), .rcpRowArgs(rows), binArgs,
-                list(PACKAGE = "recoup")))
+                list(names(mask), PACKAGE = "recoup")))
             .rcpFree(rs)
             input[[i]]$profile <- res$profile
-            rownames(input[[i]]$profile) <- names(mask)
         }
         return(input)
     }
     rsl <- lapply(input[todo], function(x) .rcpReadSet(x$ranges, NULL, devs[1], lv))
     on.exit(lapply(rsl, .rcpFree))
     res <- do.call(.Call, c(list("rcp_R_profile_samples", lapply(rsl, `[[`, "ptr")), .rcpRowArgs(rows),
-        binArgs, list(2L, PACKAGE = "recoup")))
-    for (k in seq_along(todo)) {
+        binArgs, list(2L, names(mask), PACKAGE = "recoup")))
+    for (k in seq_along(todo))
         input[[todo[k]]]$profile <- res[[k]]$profile
-        rownames(input[[todo[k]]]$profile) <- names(mask)
-    }
     return(input)
 }
 

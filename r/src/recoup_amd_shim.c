@@ -22,6 +22,7 @@
 #include <R.h>
 #include <Rinternals.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include "recoup_amd.h"
@@ -214,6 +215,45 @@ static rcp_bins_desc bins_of(SEXP where, SEXP flank, SEXP nBins, SEXP pbw, SEXP 
     return bd;
 }
 
+/* The dimnames the reference's profile matrices carry (R/profile.R:112-115,150,159-162,198-208):
+ * rbind of a NAMED list gives rownames = the list's names (the caller passes names(cvrg), or NULL
+ * where the reference's cmclapply runs over 1:length(cvrg) and the rows come back unnamed);
+ * a binned row is unlist(llply(split(x, f), stat)), whose names are "<bin>.<stat>" -- llply
+ * names each bin by its factor level "1".."n", and plyr::each, which llply applies to a
+ * function given by name, names a length-1 result by that name -- while a per-base row
+ * (as.numeric of an Rle) has none.  cbind of the parts (R/profile.R:78) keeps each part's
+ * colnames, "" for a part without them; no binned part -> no colnames at all. */
+static void set_dimnames(SEXP mat, SEXP rowNames, const rcp_bins_desc* bd, int nrow, int ncol) {
+    SEXP rn = R_NilValue, cn = R_NilValue;
+    int nprot = 0;
+    if (TYPEOF(rowNames) == STRSXP && XLENGTH(rowNames) == nrow) rn = rowNames;
+    int binned = 0;
+    for (int p = 0; p < bd->n_parts; ++p) binned |= bd->n_bins[p] != 0;
+    if (binned) {
+        const char* stat = bd->stat == RCP_STAT_MEDIAN ? "median" : "mean";
+        cn = PROTECT(allocVector(STRSXP, ncol));
+        ++nprot;
+        int c = 0;
+        char buf[64];
+        for (int p = 0; p < bd->n_parts; ++p) {
+            int nb = bd->n_bins[p], w = nb ? nb : bd->per_base_width[p];
+            for (int k = 1; k <= w; ++k, ++c) {
+                if (nb) snprintf(buf, sizeof buf, "%d.%s", k, stat);
+                else buf[0] = 0;
+                SET_STRING_ELT(cn, c, mkChar(buf));
+            }
+        }
+    }
+    if (rn != R_NilValue || cn != R_NilValue) {
+        SEXP dn = PROTECT(allocVector(VECSXP, 2));
+        ++nprot;
+        SET_VECTOR_ELT(dn, 0, rn);
+        SET_VECTOR_ELT(dn, 1, cn);
+        setAttrib(mat, R_DimNamesSymbol, dn);
+    }
+    UNPROTECT(nprot);
+}
+
 static SEXP profile_result(SEXP mat, const uint8_t* valid, int nrow) {
     SEXP v = PROTECT(allocVector(LGLSXP, nrow));
     for (int r = 0; r < nrow; ++r) LOGICAL(v)[r] = valid[r];
@@ -229,11 +269,11 @@ static SEXP profile_result(SEXP mat, const uint8_t* valid, int nrow) {
 }
 
 /* ------------------------------------------------------------------ profiles */
-/* .Call("rcp_R_profile", readset, <rows: 8 args>, <bins: 8 args>)
- * -> list(profile = n_rows x n_cols double matrix, valid = logical) */
+/* .Call("rcp_R_profile", readset, <rows: 8 args>, <bins: 8 args>, rowNames)
+ * -> list(profile = n_rows x n_cols double matrix with the reference's dimnames, valid = logical) */
 SEXP rcp_R_profile(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
                    SEXP isList, SEXP ignoreStrand, SEXP where, SEXP flank, SEXP nBins, SEXP pbw, SEXP stat,
-                   SEXP interp, SEXP rng, SEXP scale) {
+                   SEXP interp, SEXP rng, SEXP scale, SEXP rowNames) {
     rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
     int ncol = 0;
     rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
@@ -244,18 +284,19 @@ SEXP rcp_R_profile(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP
         UNPROTECT(1);
         check(rc);
     }
+    set_dimnames(out, rowNames, &bd, rd.n_rows, ncol);
     SEXP res = profile_result(out, valid, rd.n_rows);
     UNPROTECT(1);
     return res;
 }
 
 /* .Call("rcp_R_profile_samples", list of readsets (one per sample, one GPU), <rows: 8 args>,
- * <bins: 8 args>, inflight) -> list (per sample) of list(profile, valid): profileMatrix's loop
+ * <bins: 8 args>, inflight, rowNames) -> list (per sample) of list(profile, valid): profileMatrix's loop
  * over the samples of a recoup input list (R/profile.R:13-98) in one call, passes kept
  * `inflight` deep on separate HIP streams */
 SEXP rcp_R_profile_samples(SEXP rsl, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
                            SEXP isList, SEXP ignoreStrand, SEXP where, SEXP flank, SEXP nBins, SEXP pbw,
-                           SEXP stat, SEXP interp, SEXP rng, SEXP scale, SEXP inflight) {
+                           SEXP stat, SEXP interp, SEXP rng, SEXP scale, SEXP inflight, SEXP rowNames) {
     rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
     int ncol = 0;
     rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
@@ -276,16 +317,19 @@ SEXP rcp_R_profile_samples(SEXP rsl, SEXP segOff, SEXP chrom, SEXP start, SEXP e
         check(rc);
     }
     SEXP res = PROTECT(allocVector(VECSXP, ns));
-    for (int i = 0; i < ns; ++i) SET_VECTOR_ELT(res, i, profile_result(VECTOR_ELT(mats, i), valid[i], rd.n_rows));
+    for (int i = 0; i < ns; ++i) {
+        set_dimnames(VECTOR_ELT(mats, i), rowNames, &bd, rd.n_rows, ncol);
+        SET_VECTOR_ELT(res, i, profile_result(VECTOR_ELT(mats, i), valid[i], rd.n_rows));
+    }
     UNPROTECT(2);
     return res;
 }
 
-/* .Call("rcp_R_profile_multi", list of readsets (one per GPU, rcp_R_readsets), <rows>, <bins>):
+/* .Call("rcp_R_profile_multi", list of readsets (one per GPU, rcp_R_readsets), <rows>, <bins>, rowNames):
  * row blocks on every GPU at once (the reference's cmclapply over regions) */
 SEXP rcp_R_profile_multi(SEXP rsl, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
                          SEXP isList, SEXP ignoreStrand, SEXP where, SEXP flank, SEXP nBins, SEXP pbw,
-                         SEXP stat, SEXP interp, SEXP rng, SEXP scale) {
+                         SEXP stat, SEXP interp, SEXP rng, SEXP scale, SEXP rowNames) {
     rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
     int ncol = 0;
     rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
@@ -299,17 +343,18 @@ SEXP rcp_R_profile_multi(SEXP rsl, SEXP segOff, SEXP chrom, SEXP start, SEXP end
         UNPROTECT(1);
         check(rc);
     }
+    set_dimnames(out, rowNames, &bd, rd.n_rows, ncol);
     SEXP res = profile_result(out, valid, rd.n_rows);
     UNPROTECT(1);
     return res;
 }
 
 /* .Call("rcp_R_profile_rle", runOff (numeric, n_rows + 1), values (integer or double),
- *       lengths (integer), isNull (logical), <bins: 8 args>, device)
+ *       lengths (integer), isNull (logical), <bins: 8 args>, device, rowNames)
  * binCoverageMatrix / baseCoverageMatrix of the stored coverage list (list of Rle flattened
  * by .rcpRleArrays); -> list(profile, valid) */
 SEXP rcp_R_profile_rle(SEXP runOff, SEXP values, SEXP lengths, SEXP isNull, SEXP where, SEXP flank, SEXP nBins,
-                       SEXP pbw, SEXP stat, SEXP interp, SEXP rng, SEXP scale, SEXP dev) {
+                       SEXP pbw, SEXP stat, SEXP interp, SEXP rng, SEXP scale, SEXP dev, SEXP rowNames) {
     int nrow = LENGTH(runOff) - 1;
     int64_t* off = (int64_t*)R_alloc(nrow + 1, sizeof(int64_t));
     for (int r = 0; r <= nrow; ++r) off[r] = (int64_t)REAL(runOff)[r];
@@ -332,6 +377,7 @@ SEXP rcp_R_profile_rle(SEXP runOff, SEXP values, SEXP lengths, SEXP isNull, SEXP
         UNPROTECT(1);
         check(rc);
     }
+    set_dimnames(out, rowNames, &bd, nrow, ncol);
     SEXP res = profile_result(out, valid, nrow);
     UNPROTECT(1);
     return res;
@@ -448,10 +494,10 @@ SEXP rcp_R_sample_sorted(SEXP seed, SEXP kind, SEXP libSizes, SEXP size) {
 static const R_CallMethodDef call_methods[] = {
     {"rcp_R_readset", (DL_FUNC)&rcp_R_readset, 7},
     {"rcp_R_readsets", (DL_FUNC)&rcp_R_readsets, 7},
-    {"rcp_R_profile", (DL_FUNC)&rcp_R_profile, 17},
-    {"rcp_R_profile_multi", (DL_FUNC)&rcp_R_profile_multi, 17},
-    {"rcp_R_profile_samples", (DL_FUNC)&rcp_R_profile_samples, 18},
-    {"rcp_R_profile_rle", (DL_FUNC)&rcp_R_profile_rle, 13},
+    {"rcp_R_profile", (DL_FUNC)&rcp_R_profile, 18},
+    {"rcp_R_profile_multi", (DL_FUNC)&rcp_R_profile_multi, 18},
+    {"rcp_R_profile_samples", (DL_FUNC)&rcp_R_profile_samples, 19},
+    {"rcp_R_profile_rle", (DL_FUNC)&rcp_R_profile_rle, 14},
     {"rcp_R_coverage", (DL_FUNC)&rcp_R_coverage, 9},
     {"rcp_R_read_bam", (DL_FUNC)&rcp_R_read_bam, 4},
     {"rcp_R_sample_sorted", (DL_FUNC)&rcp_R_sample_sorted, 4},

@@ -79,15 +79,35 @@ class Rle:
 
 
 class RMatrix(np.ndarray):
-    """A numpy matrix that carries R's rownames (region names)."""
+    """A numpy matrix that carries R's dimnames: ``rownames`` (region names) and ``colnames``."""
 
-    def __new__(cls, a, rownames=None):
+    def __new__(cls, a, rownames=None, colnames=None):
         obj = np.asarray(a).view(cls)
-        obj.rownames = None if rownames is None else list(rownames)
+        obj.rownames = None if rownames is None else [str(x) for x in rownames]
+        obj.colnames = None if colnames is None else list(colnames)
         return obj
 
     def __array_finalize__(self, obj):
         self.rownames = getattr(obj, "rownames", None)
+        self.colnames = getattr(obj, "colnames", None)
+
+
+_STAT_NAME = {0: "mean", 1: "median"}
+
+
+def _colnames(bins):
+    """The colnames R's rbind / cbind give a profile with these column parts: "<bin>.<stat>"
+    per bin of a binned part -- unlist(llply(split(x, f), stat)) names each bin by its factor
+    level and plyr::each names the length-1 statistic by the function's name (R/util.R:81-84,
+    R/profile.R:208) -- and "" per column of a per-base part (as.numeric of an Rle has no
+    names); None when no part is binned."""
+    if not any(int(b) != 0 for b in bins.n_bins):
+        return None
+    stat = _STAT_NAME[bins.stat]
+    out = []
+    for b, w in zip(bins.n_bins, bins.width):
+        out += [f"{k}.{stat}" for k in range(1, int(b) + 1)] if b else [""] * int(w)
+    return out
 
 
 # ------------------------------------------------------------------------------ reads
@@ -325,13 +345,15 @@ def _as_coverage(cvrg):
     raise TypeError("a coverage must be a DeviceCoverage or a list of Rle / vectors / None")
 
 
-def _run(cv, bins, device=None):
+def _run(cv, bins, device=None, named=True):
+    """``named``: rows named by the coverage list (rbind of cmclapply(cvrg, ...)); False for the
+    flank / center slices, mapped over 1:length(cvrg) (R/profile.R:125-141,164-189)."""
     if isinstance(cv, DeviceCoverage):
         plan = Plan(cv.readset, cv.rows, bins)
         mat, _ = plan.run()
-        return RMatrix(mat, cv.names)
-    mat, _ = profile_rle(cv, bins, device=_device(device))
-    return RMatrix(mat, cv.names)
+    else:
+        mat, _ = profile_rle(cv, bins, device=_device(device))
+    return RMatrix(mat, cv.names if named else None, _colnames(bins))
 
 
 def _scale_of(cv):
@@ -350,7 +372,7 @@ def binCoverageMatrix(cvrg, binSize=1000, stat="mean", interpolation="auto", fla
         bins = Bins([("whole", int(binSize))], stat=stat, interp=interpolation, scale=_scale_of(cv))
     else:
         bins = Bins([(where, int(binSize))], flank=flank, stat=stat, interp=interpolation, scale=_scale_of(cv))
-    return _run(cv, bins, device)
+    return _run(cv, bins, device, named=flank is None)
 
 
 def _base_size(cv):
@@ -370,7 +392,7 @@ def baseCoverageMatrix(cvrg, flank=None, where="upstream", rc=None, device=None)
     else:
         size = int(flank[0]) if where == "upstream" else int(flank[1])
         bins = Bins([(where, 0, size)], flank=flank, scale=_scale_of(cv))
-    return _run(cv, bins, device)
+    return _run(cv, bins, device, named=flank is None)
 
 
 def _profile_bins(binParams, flank, equal, size):
@@ -387,11 +409,15 @@ def _profile_bins(binParams, flank, equal, size):
     parts = []
     if fbs != 0:
         r = np.asarray([f1, f2], dtype=float) / (f1 + f2)
+        nb = [int(np.round(2 * fbs * r[k])) for k in (0, 1)]
+        if any(f and b == 0 for f, b in zip((f1, f2), nb)):
+            # binCoverageMatrix(binSize = 0) stops in splitVector's sample() (R/util.R:74-79)
+            raise _lib.SemanticError(-5, "invalid 'size' argument (a flank rounds to 0 bins)")
         if f1:
-            parts.append(("upstream", int(np.round(2 * fbs * r[0]))))
+            parts.append(("upstream", nb[0]))
         parts.append(("center", rbs))
         if f2:
-            parts.append(("downstream", int(np.round(2 * fbs * r[1]))))
+            parts.append(("downstream", nb[1]))
     else:
         if f1:
             parts.append(("upstream", 0, f1))
@@ -432,7 +458,7 @@ def profileMatrix(input, flank, binParams, rc=None, keep_on_device=False):
     for s, cv in zip(input, cvs):
         bins = _profile_bins(binParams, flank, equal, _base_size(cv) if equal else 0)
         mat, dev = _profile_pass(cv, bins, keep_on_device)
-        s["profile"] = RMatrix(mat, cv.names)
+        s["profile"] = RMatrix(mat, cv.names, _colnames(bins))
         if keep_on_device:
             s["profile_device"] = dev
     return input
@@ -477,12 +503,12 @@ def recoupProfiles(input, genomeRanges, region, flank, binParams, keep_on_device
         bins = Bins(parts + (heat.parts if fuse else []), flank=(f1, f2), stat=prof.stat, interp=prof.interp)
         full, dev = _profile_pass(cv, bins, keep_on_device)
         npc = prof.n_cols
-        s["profile"] = RMatrix(full[:, :npc], cv.names)
+        s["profile"] = RMatrix(full[:, :npc], cv.names, _colnames(prof))
         if keep_on_device:
             s["profile_device"] = dev
         if heat is not None:
             if fuse:
-                s["heatmap"] = RMatrix(full[:, npc:], cv.names)
+                s["heatmap"] = RMatrix(full[:, npc:], cv.names, _colnames(heat))
             else:
                 heat.scale = _scale_of(cv)
                 s["heatmap"] = _run(cv, heat)

@@ -13,7 +13,22 @@ from recoup_amd.granges import GRanges, GRangesList, getFlankingRanges, getRegio
 
 MIRRORED = [".rcpReadArgs", ".rcpReadSet", ".rcpFree", ".rcpSampleReadSet", ".rcpRows", ".rcpRowArgs",
             ".rcpCoverage", "calcCoverage", ".rcpCoverageRef", ".rcpRnaRows", "coverageRnaRef", ".rcpRleArrays",
-            ".rcpProfileRle", ".rcpParts", "profileMatrixFused", "profileMatrixFromReads"]
+            ".rcpProfileRle", "binCoverageMatrix", "baseCoverageMatrix", ".rcpParts", "profileMatrix",
+            "profileMatrixFromReads"]
+
+
+class NamedList(list):
+    """An R list with names (None = no names attribute), e.g. calcCoverage's list of Rle."""
+
+    def __init__(self, items, names=None):
+        super().__init__(items)
+        self.names = None if names is None else [str(x) for x in names]
+
+
+def _rchar(names):
+    """An R character vector for the shim, or NULL."""
+    from tests.rmini.rmini import RChar
+    return None if names is None else RChar(names)
 
 
 def rle(x):
@@ -136,7 +151,7 @@ def rcp_row_args(rows):
 
 
 def rcp_coverage(sh, rs, rows, names=None):
-    """.rcpCoverage(rs, rows, names): list of (values, lengths) runs or None."""
+    """.rcpCoverage(rs, rows, names): named list of (values, lengths) runs or None."""
     ptr = rs.ptr[0] if isinstance(rs.ptr, list) else rs.ptr
     res = sh.call("rcp_R_coverage", ptr, *rcp_row_args(rows))
     cov = []
@@ -146,7 +161,7 @@ def rcp_coverage(sh, rs, rows, names=None):
             continue
         a, b = int(res["runOff"][r]), int(res["runOff"][r + 1])
         cov.append((res["values"][a:b], res["lengths"][a:b]))
-    return cov
+    return NamedList(cov, names)
 
 
 def calc_coverage(sh, inp, mask, strand=None, ignore_strand=True):
@@ -163,7 +178,8 @@ def coverage_ref(sh, input, genomeRanges, region, flank, strandedParams):
     main = getRegionalRanges(genomeRanges, region, flank)
     for x in input:
         rs = rcp_read_set(sh, x["ranges"], strandedParams.get("strand"))
-        x["coverage"] = rcp_coverage(sh, rs, rcp_rows(main, rs.levels, strandedParams.get("ignoreStrand", True)))
+        x["coverage"] = rcp_coverage(sh, rs, rcp_rows(main, rs.levels, strandedParams.get("ignoreStrand", True)),
+                                     main.names)
         rcp_free(sh, rs)
     return input
 
@@ -203,7 +219,7 @@ def coverage_rna_ref(sh, input, genomeRanges, helperRanges, flank, strandedParam
     for x in input:
         rs = rcp_read_set(sh, x["ranges"], sp.get("strand"))
         rows = rcp_rna_rows(left, genomeRanges, right, rs.levels, sp.get("ignoreStrand", True))
-        x["coverage"] = rcp_coverage(sh, rs, rows)
+        x["coverage"] = rcp_coverage(sh, rs, rows, genomeRanges.names)
         rcp_free(sh, rs)
     return input
 
@@ -224,14 +240,39 @@ INTERP = {"auto": 0, "spline": 1, "linear": 2, "neighborhood": 3}
 
 
 def rcp_profile_rle(sh, cvrg, where, flank, n_bins, per_base, stat="mean", interpolation="auto", rng_kind=0,
-                    device=0):
-    """.rcpProfileRle(cvrg, where, flank, nBins, perBase, stat, interpolation)."""
+                    device=0, row_names=None):
+    """.rcpProfileRle(cvrg, where, flank, nBins, perBase, stat, interpolation, rowNames): the
+    matrix (an rmini RArray carrying the dimnames the shim set)."""
     a = rcp_rle_arrays(cvrg)
     res = sh.call("rcp_R_profile_rle", a["runOff"], a["values"], a["lengths"], a["isNull"],
                   np.asarray(where, np.int32), np.asarray((0, 0) if flank is None else flank, np.int32),
                   np.asarray(n_bins, np.int32), np.asarray(per_base, np.int32), np.int32(STAT[stat]),
-                  np.int32(INTERP[interpolation]), np.int32(rng_kind), 1.0, np.int32(device))
+                  np.int32(INTERP[interpolation]), np.int32(rng_kind), 1.0, np.int32(device), _rchar(row_names))
     return res["profile"]
+
+
+def _names(cvrg):
+    return getattr(cvrg, "names", None)
+
+
+WHERE = {"center": 1, "upstream": 2, "downstream": 3}
+
+
+def bin_coverage_matrix(sh, cvrg, binSize=1000, stat="mean", interpolation="auto", flank=None, where="center"):
+    """binCoverageMatrix(cvrg, binSize, stat, interpolation, flank, where)."""
+    w = 0 if flank is None else WHERE[where]
+    return rcp_profile_rle(sh, cvrg, [w], flank, [binSize], [0], stat, interpolation,
+                           row_names=_names(cvrg) if flank is None else None)
+
+
+def base_coverage_matrix(sh, cvrg, flank=None, where="upstream"):
+    """baseCoverageMatrix(cvrg, flank, where)."""
+    if flank is None:
+        ok = [i for i, x in enumerate(cvrg) if x is not None and int(np.sum(x[1])) > 0]
+        size = int(np.sum(cvrg[ok[0]][1])) if ok else 0
+        return rcp_profile_rle(sh, cvrg, [0], None, [0], [size], row_names=_names(cvrg))
+    w = {"upstream": 1, "downstream": 2}[where]
+    return rcp_profile_rle(sh, cvrg, [w + 1], flank, [0], [flank[w - 1]])
 
 
 def rcp_parts(equal, len1, flank, binParams):
@@ -245,6 +286,8 @@ def rcp_parts(equal, len1, flank, binParams):
         if flank[k] == 0:
             continue
         fb = int(np.round(2 * binParams["flankBinSize"] * r[k])) if binParams["flankBinSize"] != 0 else 0
+        if binParams["flankBinSize"] != 0 and fb == 0:
+            raise ValueError("invalid 'size' argument")
         if k == 0:
             where, nb, pb = [2] + where, [fb] + nb, [0 if fb else flank[0]] + pb
         else:
@@ -256,21 +299,105 @@ def _lengths(cvrg):
     return np.array([0 if x is None else int(np.sum(x[1])) for x in cvrg])
 
 
-def profile_matrix_fused(sh, input, flank, binParams):
-    """profileMatrixFused(input, flank, binParams)."""
+def profile_matrix(sh, input, flank, binParams):
+    """profileMatrix(input, flank, binParams) of rcp.R (one library call per sample)."""
+    if not any(x.get("profile") is None for x in input):
+        return input
     ln = _lengths(input[0]["coverage"])
     ln = ln[ln != 0]
-    equal = bool(np.all(ln == ln[0]))
+    equal = bool(np.all(ln == ln[0])) if len(ln) else True
+    stat = binParams.get("sumStat", "mean")
     for x in input:
-        if x.get("profile") is not None:
+        cvrg = x["coverage"]
+        if equal:
+            x["profile"] = bin_coverage_matrix(sh, cvrg, binParams["regionBinSize"], stat) \
+                if binParams["regionBinSize"] != 0 else base_coverage_matrix(sh, cvrg)
             continue
-        parts = rcp_parts(equal, int(ln[0]), flank, binParams)
-        interp = "auto" if equal else binParams.get("interpolation", "auto")
-        x["profile"] = rcp_profile_rle(sh, x["coverage"], parts["where"], flank, parts["nBins"], parts["perBase"],
-                                       binParams.get("sumStat", "mean"), interp)
+        parts = rcp_parts(False, None, flank, binParams)
+        x["profile"] = rcp_profile_rle(sh, cvrg, parts["where"], flank, parts["nBins"], parts["perBase"], stat,
+                                       binParams.get("interpolation", "auto"), row_names=_names(cvrg))
     return input
 
 
+# ---------------------------------------------------------------------------------------------
+# The REFERENCE's own callers of binCoverageMatrix / baseCoverageMatrix, transliterated: with
+# rcp.R dropped in, a maintainer who keeps R/profile.R's profileMatrix, and recoup()'s forced
+# heatmap binning (R/recoup.R:659-714, which rcp.R does not replace), call the replacements above.
+# R's cbind and rownames<- are modelled on the dimnames the shim returns.
+
+def r_cbind(*mats):
+    """cbind(...) of matrices (NULL arguments dropped): rownames from the first argument that has
+    them; colnames the arguments' colnames, "" for an argument without; none if no argument has."""
+    mats = [m for m in mats if m is not None]
+    from tests.rmini.rmini import RArray
+    vals = np.concatenate([np.asarray(m) for m in mats], axis=1)
+    rn = next((m.rownames for m in mats if m.rownames is not None), None)
+    cn = None
+    if any(m.colnames is not None for m in mats):
+        cn = []
+        for m in mats:
+            cn += list(m.colnames) if m.colnames is not None else [""] * m.shape[1]
+    return RArray(vals, None if rn is None and cn is None else (rn, cn))
+
+
+def r_set_rownames(m, names):
+    """rownames(m) <- names."""
+    from tests.rmini.rmini import RArray
+    cn = m.colnames
+    rn = None if names is None else list(names)
+    return RArray(np.asarray(m), None if rn is None and cn is None else (rn, cn))
+
+
+def ref_profile_matrix(sh, input, flank, binParams):
+    """R/profile.R:1-98 as the reference wrote it, over rcp.R's binCoverageMatrix /
+    baseCoverageMatrix."""
+    if not any(x.get("profile") is None for x in input):
+        return input
+    ln = _lengths(input[0]["coverage"])
+    ln = ln[ln != 0]
+    equal = bool(np.all(ln == ln[0]))
+    stat = binParams.get("sumStat", "mean")
+    interp = binParams.get("interpolation", "auto")
+    for x in input:
+        cv = x["coverage"]
+        if not equal:
+            center = bin_coverage_matrix(sh, cv, binParams["regionBinSize"], stat, interp, flank, "center")
+            r = np.asarray(flank, np.float64) / sum(flank)
+            if binParams["flankBinSize"] != 0:
+                left = None if flank[0] == 0 else bin_coverage_matrix(
+                    sh, cv, int(np.round(2 * binParams["flankBinSize"] * r[0])), stat, interp, flank, "upstream")
+                right = None if flank[1] == 0 else bin_coverage_matrix(
+                    sh, cv, int(np.round(2 * binParams["flankBinSize"] * r[1])), stat, interp, flank, "downstream")
+            else:
+                left = None if flank[0] == 0 else base_coverage_matrix(sh, cv, flank, "upstream")
+                right = None if flank[1] == 0 else base_coverage_matrix(sh, cv, flank, "downstream")
+            x["profile"] = r_set_rownames(r_cbind(left, center, right), _names(cv))
+        elif binParams["regionBinSize"] != 0:
+            x["profile"] = bin_coverage_matrix(sh, cv, binParams["regionBinSize"], stat)
+        else:
+            x["profile"] = base_coverage_matrix(sh, cv)
+    return input
+
+
+def ref_forced_heatmap(sh, input, region, flank, binParams, customIsBase=False):
+    """R/recoup.R:659-714: the heatmap profiles (helpInput[[n]]$profile), or None when the
+    reference does not force binning.  A non-base region reaches :703, whose undefined
+    forcedBinSize raises "object 'forcedBinSize' not found" after the center and upstream passes."""
+    bp = dict(binParams)
+    fbs = bp.get("forcedBinSize", (50, 200))
+    if not (bp.get("forceHeatmapBinning", True) and (bp["regionBinSize"] == 0 or bp["flankBinSize"] == 0)):
+        return None
+    stat = bp.get("sumStat", "mean")
+    out = []
+    for x in input:
+        if region in ("tss", "tes") or customIsBase:
+            out.append(bin_coverage_matrix(sh, x["coverage"], fbs[1], stat))
+            continue
+        interp = bp.get("interpolation", "auto")
+        bin_coverage_matrix(sh, x["coverage"], fbs[1], stat, interp, flank, "center")
+        bin_coverage_matrix(sh, x["coverage"], fbs[0], stat, interp, flank, "upstream")
+        raise NameError("object 'forcedBinSize' not found")
+    return out
 def profile_matrix_from_reads(sh, input, mask, flank, binParams, ignore_strand=True, devices=(0,)):
     """profileMatrixFromReads(input, mask, flank, binParams, ignore.strand)."""
     ln = mask.width
@@ -280,19 +407,21 @@ def profile_matrix_from_reads(sh, input, mask, flank, binParams, ignore_strand=T
     bin_args = [np.asarray(parts["where"], np.int32), np.asarray((0, 0) if flank is None else flank, np.int32),
                 np.asarray(parts["nBins"], np.int32), np.asarray(parts["perBase"], np.int32),
                 np.int32(STAT[binParams.get("sumStat", "mean")]), np.int32(INTERP[interp]), np.int32(0), 1.0]
+    names = _rchar(mask.names)
     todo = [i for i, x in enumerate(input) if x.get("profile") is None]
     lv = list(dict.fromkeys(l for i in todo for l in input[i]["ranges"].seqlevels))
     rows = rcp_rows(mask, lv, ignore_strand)
     if len(devices) > 1:
         for i in todo:
             rs = rcp_read_set(sh, input[i]["ranges"], None, devices, lv)
-            res = sh.call("rcp_R_profile_multi", rs.ptr, *rcp_row_args(rows), *bin_args)
+            res = sh.call("rcp_R_profile_multi", rs.ptr, *rcp_row_args(rows), *bin_args, names)
             rcp_free(sh, rs)
             input[i]["profile"] = res["profile"]
         return input
     rsl = [rcp_read_set(sh, input[i]["ranges"], None, devices[:1], lv) for i in todo]
     try:
-        res = sh.call("rcp_R_profile_samples", [rs.ptr for rs in rsl], *rcp_row_args(rows), *bin_args, np.int32(2))
+        res = sh.call("rcp_R_profile_samples", [rs.ptr for rs in rsl], *rcp_row_args(rows), *bin_args, np.int32(2),
+                      names)
     finally:
         for rs in rsl:
             rcp_free(sh, rs)

@@ -4,7 +4,9 @@
  * tests/rmini/build/librmini_shim.so and driven from Python (tests/rmini/rmini.py).
  *
  * What it models of R, and what it checks:
- *   - vectors (integer, logical, double, character, list), matrices (dims kept), names;
+ *   - vectors (integer, logical, double, character, list), matrices (dims kept), names, and a
+ *     matrix's dimnames (a list of two: row names, column names; each NULL or character of the
+ *     dimension's length -- what R's dimnames<- insists on);
  *   - Rf_error as a longjmp back to rmini_call's setjmp (R's error unwinding), after which the
  *     protect stack is reset, as R resets it;
  *   - the PROTECT stack: rmini_call reports the depth a routine left behind (must be 0);
@@ -33,15 +35,18 @@ struct SEXPREC {
     R_xlen_t len;
     void* data;
     SEXP names;
+    SEXP dimnames;
     int nrow, ncol;
     void* addr;
     R_CFinalizer_t fin;
 };
 
-static struct SEXPREC nil_obj = {NILSXP, 0, NULL, NULL, 0, 0, NULL, NULL};
-static struct SEXPREC names_sym = {NILSXP, 0, NULL, NULL, 0, 0, NULL, NULL};
+static struct SEXPREC nil_obj = {NILSXP, 0, NULL, NULL, NULL, 0, 0, NULL, NULL};
+static struct SEXPREC names_sym = {NILSXP, 0, NULL, NULL, NULL, 0, 0, NULL, NULL};
+static struct SEXPREC dimnames_sym = {NILSXP, 0, NULL, NULL, NULL, 0, 0, NULL, NULL};
 SEXP R_NilValue = &nil_obj;
 SEXP R_NamesSymbol = &names_sym;
+SEXP R_DimNamesSymbol = &dimnames_sym;
 int R_NaInt = INT_MIN;
 
 static jmp_buf* err_jmp = NULL;
@@ -224,8 +229,25 @@ const char* CHAR(SEXP s) {
 }
 
 SEXP setAttrib(SEXP s, SEXP name, SEXP v) {
-    if (name != R_NamesSymbol) Rf_error("rmini: only names attributes are modelled");
-    s->names = v;
+    if (name == R_NamesSymbol) {
+        s->names = v;
+        return v;
+    }
+    if (name != R_DimNamesSymbol) Rf_error("rmini: only names and dimnames attributes are modelled");
+    if (s->nrow == 0 && s->ncol == 0 && s->len != 0) Rf_error("'dimnames' applied to non-array");
+    if (v->type != VECSXP || v->len != 2) Rf_error("length of 'dimnames' [%ld] must match that of 'dims' [2]",
+                                                   (long)v->len);
+    for (int k = 0; k < 2; ++k) {
+        SEXP d = ((SEXP*)v->data)[k];
+        int want = k == 0 ? s->nrow : s->ncol;
+        if (d->type == NILSXP) continue;
+        if (d->type != STRSXP) Rf_error("rmini: dimnames[[%d]] is neither NULL nor character", k + 1);
+        if (d->len != want)
+            Rf_error("length of 'dimnames' [%d] not equal to array extent", k + 1);
+        for (R_xlen_t i = 0; i < d->len; ++i)
+            if (!((SEXP*)d->data)[i]) Rf_error("rmini: dimnames[[%d]][%ld] unset", k + 1, (long)i + 1);
+    }
+    s->dimnames = v;
     return v;
 }
 
@@ -293,10 +315,13 @@ typedef SEXP (*F4)(SEXP, SEXP, SEXP, SEXP);
 typedef SEXP (*F7)(SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP);
 typedef SEXP (*F9)(SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP);
 typedef SEXP (*F13)(SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP);
+typedef SEXP (*F14)(SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP);
 typedef SEXP (*F17)(SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP,
                     SEXP, SEXP);
 typedef SEXP (*F18)(SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP,
                     SEXP, SEXP, SEXP);
+typedef SEXP (*F19)(SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP, SEXP,
+                    SEXP, SEXP, SEXP, SEXP);
 
 /* .Call(name, a[0], ..., a[nargs-1]): 0 and *out on success; 1 and the message
  * (rmini_error) when the routine raised an R error.  *depth: the protect stack depth the
@@ -325,6 +350,9 @@ int rmini_call(const char* name, int nargs, SEXP* a, SEXP* out, int* depth) {
     case 7: r = ((F7)f)(a[0], a[1], a[2], a[3], a[4], a[5], a[6]); break;
     case 9: r = ((F9)f)(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8]); break;
     case 13: r = ((F13)f)(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[11], a[12]); break;
+    case 14:
+        r = ((F14)f)(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[11], a[12], a[13]);
+        break;
     case 17:
         r = ((F17)f)(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[11], a[12], a[13], a[14],
                      a[15], a[16]);
@@ -332,6 +360,10 @@ int rmini_call(const char* name, int nargs, SEXP* a, SEXP* out, int* depth) {
     case 18:
         r = ((F18)f)(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[11], a[12], a[13], a[14],
                      a[15], a[16], a[17]);
+        break;
+    case 19:
+        r = ((F19)f)(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[11], a[12], a[13], a[14],
+                     a[15], a[16], a[17], a[18]);
         break;
     default:
         err_jmp = saved;
@@ -390,6 +422,17 @@ SEXP rmini_string(const char* c) {
     return s;
 }
 
+SEXP rmini_strings(int n, const char** c) {
+    SEXP s = new_obj(STRSXP, n);
+    for (int i = 0; i < n; ++i) {
+        size_t k = strlen(c[i]);
+        SEXP ch = new_obj(CHARSXP, (R_xlen_t)k);
+        memcpy(ch->data, c[i], k);
+        ((SEXP*)s->data)[i] = ch;
+    }
+    return s;
+}
+
 SEXP rmini_list(int n, const SEXP* elts) {
     SEXP s = new_obj(VECSXP, n);
     for (int i = 0; i < n; ++i) ((SEXP*)s->data)[i] = elts[i];
@@ -400,5 +443,6 @@ int rmini_type(SEXP s) { return s->type; }
 R_xlen_t rmini_length(SEXP s) { return s->len; }
 void* rmini_data(SEXP s) { return s->data; }
 SEXP rmini_names(SEXP s) { return s->names ? s->names : R_NilValue; }
+SEXP rmini_dimnames(SEXP s) { return s->dimnames ? s->dimnames : R_NilValue; }
 int rmini_dim(SEXP s, int k) { return k == 0 ? s->nrow : s->ncol; }
 SEXP rmini_nil(void) { return R_NilValue; }

@@ -3,8 +3,10 @@ emulation of the R C API (test infrastructure; R is not installed here or on the
 
 ``Shim().call(name, *args)`` is ``.Call(name, ...)``: Python values become R objects
 (``numpy`` int32 -> integer, float64 -> double, bool -> logical, ``str`` -> character,
-``list`` -> list, ``None`` -> NULL) and the result comes back as Python values (a named R list
--> ``dict``, a matrix -> 2-D ``numpy`` array in R's column-major order).  An R error raised by
+``list`` -> list, ``None`` -> NULL, ``RChar([...])`` -> a character vector) and the result comes
+back as Python values (a named R list -> ``dict``, a matrix -> ``RArray``: a 2-D ``numpy`` array in
+R's column-major order whose ``dimnames`` is R's ``dimnames(m)``: None, or (rownames, colnames),
+each None or a list of str).  An R error raised by
 the shim becomes ``RError``; the protect stack must be balanced on return.
 
 build() compiles the shim with rmini.c against include/recoup_amd.h and links
@@ -26,6 +28,30 @@ INTSXP, LGLSXP, REALSXP, STRSXP, VECSXP, CHARSXP, NILSXP, EXTPTRSXP = 13, 10, 14
 
 class RError(Exception):
     pass
+
+
+class RChar(list):
+    """An R character vector (``c("a", "b")``); a plain ``str`` is a length-1 one."""
+
+
+class RArray(np.ndarray):
+    """An R matrix: the values plus R's ``dimnames`` (None, or a (rownames, colnames) pair)."""
+
+    def __new__(cls, a, dimnames=None):
+        obj = np.asarray(a).view(cls)
+        obj.dimnames = dimnames
+        return obj
+
+    def __array_finalize__(self, obj):
+        self.dimnames = getattr(obj, "dimnames", None)
+
+    @property
+    def rownames(self):
+        return None if self.dimnames is None else self.dimnames[0]
+
+    @property
+    def colnames(self):
+        return None if self.dimnames is None else self.dimnames[1]
 
 
 def build(force=False):
@@ -70,6 +96,10 @@ class Shim:
         L.rmini_data.argtypes = [v]
         L.rmini_names.restype = v
         L.rmini_names.argtypes = [v]
+        L.rmini_dimnames.restype = v
+        L.rmini_dimnames.argtypes = [v]
+        L.rmini_strings.restype = v
+        L.rmini_strings.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
         L.rmini_nil.restype = v
         L.rmini_fail_alloc_after.argtypes = [ctypes.c_long]
         assert L.rmini_init() == 0, "R_init_recoup registered no routines"
@@ -83,6 +113,10 @@ class Shim:
             return L.rmini_nil()
         if isinstance(x, RObj):
             return x.ptr
+        if isinstance(x, RChar):
+            enc = [str(e).encode() for e in x]
+            arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+            return L.rmini_strings(len(enc), arr)
         if isinstance(x, str):
             return L.rmini_string(x.encode())
         if isinstance(x, (list, tuple)):
@@ -113,7 +147,9 @@ class Shim:
                 a = a.astype(bool)
             nr, nc = L.rmini_dim(p, 0), L.rmini_dim(p, 1)
             if nr or nc:
-                a = a.reshape((nr, nc), order="F")
+                dn = L.rmini_dimnames(p)
+                dn = None if L.rmini_type(dn) == NILSXP else tuple(self.from_r(e) for e in self.from_r(dn))
+                return RArray(a.reshape((nr, nc), order="F"), dn)
             return a
         if t == CHARSXP:
             return ctypes.string_at(L.rmini_data(p), n).decode()

@@ -3,7 +3,7 @@
 #define RCP_RSTUB_RINTERNALS_H
 #include "R.h"
 enum { INTSXP = 13, LGLSXP = 10, REALSXP = 14, STRSXP = 16, VECSXP = 19 };
-extern SEXP R_NilValue, R_NamesSymbol;
+extern SEXP R_NilValue, R_NamesSymbol, R_DimNamesSymbol;
 extern int R_NaInt;
 #define NA_INTEGER R_NaInt
 R_xlen_t XLENGTH(SEXP);

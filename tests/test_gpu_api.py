@@ -46,9 +46,14 @@ def test_tss_chipseq_per_base(c1):
         assert s["profile"].shape == (100, 4000)
         np.testing.assert_array_equal(np.asarray(s["profile"]), c1["gold"][f"tss_base_s{k}"].astype(np.float64))
         assert s["profile"].rownames == list(c1["G"]["names"])
+        assert s["profile"].colnames is None  # per-base rows: as.numeric(Rle) has no names
         # the forced heatmap pass (recoup.R:659-671): binCoverageMatrix(..., binSize = 200)
         heat = ra.binCoverageMatrix(s["coverage"], binSize=200, stat="mean")
         np.testing.assert_allclose(heat, c1["gold"][f"tss_heat_s{k}"], rtol=1e-12, atol=0)
+        assert heat.rownames == list(c1["G"]["names"]) and heat.colnames == o.bin_colnames(200, "mean")
+        # a flank slice is mapped over 1:length(cvrg): rbind leaves its rows unnamed
+        up = ra.baseCoverageMatrix(s["coverage"], flank=FLANK, where="upstream")
+        assert up.rownames is None and up.colnames is None
 
 
 def test_tss_profile_150_bins(c1):
@@ -65,9 +70,12 @@ def test_genebody_binned(c1, stat):
     inp = ra.coverageRef(_input(c1), c1["genome"], "genebody", FLANK)
     inp = ra.profileMatrix(inp, FLANK, {"flankBinSize": 50, "regionBinSize": 150, "sumStat": stat,
                                         "interpolation": "auto"})
+    bp = {"flankBinSize": 50, "regionBinSize": 150, "sumStat": stat}
     for k, s in enumerate(inp):
         assert s["profile"].shape == (100, 250)
         np.testing.assert_allclose(s["profile"], c1["gold"][f"gb_{stat}_s{k}"], rtol=1e-9, atol=1e-12)
+        assert (s["profile"].rownames, s["profile"].colnames) == \
+            o.profile_dimnames(list(c1["G"]["names"]), FLANK, bp, False)
 
 
 def test_rna_coverage_profile(c1):
@@ -77,7 +85,8 @@ def test_rna_coverage_profile(c1):
     for k, s in enumerate(inp):
         np.testing.assert_array_equal(s["coverage"].valid(), c1["gold"][f"rna_valid_s{k}"].astype(bool))
         np.testing.assert_allclose(s["profile"], c1["gold"][f"rna_s{k}"], rtol=1e-9, atol=1e-12)
-        assert s["profile"].rownames == list(c1["E"]["names"])
+        assert (s["profile"].rownames, s["profile"].colnames) == \
+            o.profile_dimnames(list(c1["E"]["names"]), FLANK, {"flankBinSize": 50, "regionBinSize": 150}, False)
 
 
 def _oracle_index(sample):

@@ -39,7 +39,10 @@ def c1():
     exons = GRangesList(GRanges(E["chrom"], E["start"], E["end"], E["strand"]), E["seg_off"], names=E["names"])
     idx = [o.Index(np.zeros(len(s["start"]), np.int32), s["start"], s["end"], s["strand"], s["seqlengths"])
            for s in S]
-    return dict(S=S, reads=reads, genes=genes, exons=exons, idx=idx, G=G, E=E, gold=dict(np.load(GOLD)))
+    design = {k: [str(v) for v in d[f"design_{k}"]] for k in ("rownames", "strand", "RNA_status")}
+    assert design["rownames"] == [str(n) for n in G["names"]]  # test.design rows = test.genome rows
+    return dict(S=S, reads=reads, genes=genes, exons=exons, idx=idx, G=G, E=E, gold=dict(np.load(GOLD)),
+                design=design)
 
 
 def _decode(cov):
@@ -74,39 +77,110 @@ def test_calc_coverage_of_a_split_list(sh, c1):
     assert sh.live_handles() == 0  # every readset released (.rcpFree)
 
 
+def _assert_dimnames(m, want, what):
+    got = m.dimnames
+    assert (got is None) == (want is None), f"{what}: dimnames {got is not None} vs {want is not None}"
+    if want is not None:
+        assert got[0] == want[0], f"{what}: rownames"
+        assert got[1] == want[1], f"{what}: colnames"
+
+
+def _assert_same_matrix(a, b, what):
+    """bit-equal values and identical dimnames (rcp.R's profileMatrix vs the reference's)."""
+    np.testing.assert_array_equal(np.asarray(a).view(np.int64), np.asarray(b).view(np.int64), err_msg=what)
+    _assert_dimnames(a, b.dimnames, what)
+
+
+def _design_split_selects_every_row(profile, design_col):
+    """R/plot.R:199-204 (and :728-733): split(rownames(x$profile), as.list(d), drop = TRUE), then
+    x$profile[splitter[[n]], , drop = FALSE] per design level: rownames must exist, and the
+    subsets together hold every row exactly once.  kmeansDesign (R/util.R:181-193) indexes the
+    clusters by rownames(design) -- the same names."""
+    rn = profile.rownames
+    assert rn is not None, "profile without rownames: plot.R:200 splits NULL"
+    assert len(set(rn)) == len(rn)
+    pos = {n: i for i, n in enumerate(rn)}
+    picked = []
+    for lvl in sorted(set(design_col)):
+        names = [n for n, d in zip(rn, design_col) if d == lvl]
+        picked += [pos[n] for n in names]  # profile[names, ] by name
+    assert sorted(picked) == list(range(len(rn)))
+
+
 def test_tss_recoup_path(sh, c1):
     """coverageBaseRef -> $coverage -> profileMatrix (per base, regionBinSize = 0) and the forced
-    200-bin heatmap pass (inst/unitTests/test_recoup.R:4-13, R/recoup.R:659-671)."""
+    200-bin heatmap pass (inst/unitTests/test_recoup.R:4-13, R/recoup.R:659-671), with the
+    dimnames the reference's rbind leaves: rownames = region names."""
     inp = rm.coverage_ref(sh, _inputs(c1), c1["genes"], "tss", (2000, 2000), {"strand": None, "ignoreStrand": True})
     gold = c1["gold"]
+    names = list(c1["G"]["names"])
     for k, x in enumerate(inp):
         valid = np.array([c is not None for c in x["coverage"]])
         np.testing.assert_array_equal(valid, gold[f"tss_valid_s{k}"].astype(bool))
-    inp = rm.profile_matrix_fused(sh, inp, (2000, 2000), dict(flankBinSize=0, regionBinSize=0))
+        assert x["coverage"].names == names
+    bp = dict(flankBinSize=0, regionBinSize=0)
+    inp = rm.profile_matrix(sh, inp, (2000, 2000), bp)
+    ref = rm.ref_profile_matrix(sh, [dict(coverage=x["coverage"]) for x in inp], (2000, 2000), bp)
+    heat = rm.ref_forced_heatmap(sh, inp, "tss", (2000, 2000), bp)
     for k, x in enumerate(inp):
         np.testing.assert_array_equal(x["profile"], gold[f"tss_base_s{k}"].astype(np.float64))
-        heat = rm.rcp_profile_rle(sh, x["coverage"], [0], None, [200], [0])
-        np.testing.assert_allclose(heat, gold[f"tss_heat_s{k}"], rtol=MEAN_RTOL, atol=0)
-        b150 = rm.rcp_profile_rle(sh, x["coverage"], [0], None, [150], [0])
+        _assert_dimnames(x["profile"], o.profile_dimnames(names, (2000, 2000), bp, True), "tss profile")
+        _assert_same_matrix(x["profile"], ref[k]["profile"], "tss: rcp.R profileMatrix vs R/profile.R's")
+        np.testing.assert_allclose(heat[k], gold[f"tss_heat_s{k}"], rtol=MEAN_RTOL, atol=0)
+        _assert_dimnames(heat[k], (names, o.bin_colnames(200, "mean")), "tss heatmap")
+        _design_split_selects_every_row(x["profile"], c1["design"]["RNA_status"])
+        _design_split_selects_every_row(heat[k], c1["design"]["strand"])
+        b150 = rm.bin_coverage_matrix(sh, x["coverage"], 150)  # man/profileMatrix.Rd:32-50
         np.testing.assert_allclose(b150, gold[f"tss150_s{k}"], rtol=MEAN_RTOL, atol=0)
+        _assert_dimnames(b150, (names, o.bin_colnames(150, "mean")), "tss 150 bins")
 
 
 @pytest.mark.parametrize("stat", ["mean", "median"])
 def test_genebody_recoup_path(sh, c1, stat):
-    """coverageAreaRef -> profileMatrix's unequal-length branch (test_recoup.R:15-26)."""
+    """coverageAreaRef -> profileMatrix's unequal-length branch (test_recoup.R:15-26) in one call
+    per sample, equal (values and dimnames) to the reference's three binCoverageMatrix calls +
+    cbind + rownames<-; the forced heatmap pass of a non-base region stops at R/recoup.R:703."""
     inp = rm.coverage_ref(sh, _inputs(c1), c1["genes"], "genebody", (2000, 2000),
                           {"strand": None, "ignoreStrand": True})
-    inp = rm.profile_matrix_fused(sh, inp, (2000, 2000), dict(flankBinSize=50, regionBinSize=150, sumStat=stat,
-                                                              interpolation="auto"))
+    bp = dict(flankBinSize=50, regionBinSize=150, sumStat=stat, interpolation="auto")
+    inp = rm.profile_matrix(sh, inp, (2000, 2000), bp)
+    ref = rm.ref_profile_matrix(sh, [dict(coverage=x["coverage"]) for x in inp], (2000, 2000), bp)
+    names = list(c1["G"]["names"])
     for k, x in enumerate(inp):
         np.testing.assert_allclose(x["profile"], c1["gold"][f"gb_{stat}_s{k}"], rtol=1e-9 if stat == "median"
                                    else MEAN_RTOL, atol=0)
+        _assert_dimnames(x["profile"], o.profile_dimnames(names, (2000, 2000), bp, False), "genebody")
+        assert x["profile"].colnames[:2] == ["1." + stat, "2." + stat] and len(x["profile"].colnames) == 250
+        _assert_same_matrix(x["profile"], ref[k]["profile"], "genebody: rcp.R profileMatrix vs R/profile.R's")
+        _design_split_selects_every_row(x["profile"], c1["design"]["RNA_status"])
+    with pytest.raises(NameError, match="forcedBinSize"):
+        rm.ref_forced_heatmap(sh, inp, "genebody", (2000, 2000), dict(bp, flankBinSize=0))
+
+
+def test_genebody_per_base_flanks(sh, c1):
+    """flankBinSize = 0 (R/profile.R:58-77): per-base flanks around the binned center; the
+    cbind's colnames are "" for the per-base columns."""
+    inp = rm.coverage_ref(sh, _inputs(c1), c1["genes"], "genebody", (1000, 500),
+                          {"strand": None, "ignoreStrand": True})
+    bp = dict(flankBinSize=0, regionBinSize=60, sumStat="mean", interpolation="auto")
+    inp = rm.profile_matrix(sh, inp, (1000, 500), bp)
+    ref = rm.ref_profile_matrix(sh, [dict(coverage=x["coverage"]) for x in inp], (1000, 500), bp)
+    names = list(c1["G"]["names"])
+    want = o.profile_matrix([[None if c is None else np.repeat(c[0], c[1]) for c in x["coverage"]] for x in inp],
+                            (1000, 500), bp)
+    for k, x in enumerate(inp):
+        np.testing.assert_allclose(x["profile"], want[k], rtol=MEAN_RTOL, atol=0)
+        dn = o.profile_dimnames(names, (1000, 500), bp, False)
+        assert dn[1][:1000] == [""] * 1000 and dn[1][1000] == "1.mean" and dn[1][-500:] == [""] * 500
+        _assert_dimnames(x["profile"], dn, "genebody per-base flanks")
+        _assert_same_matrix(x["profile"], ref[k]["profile"], "per-base flanks: rcp.R vs R/profile.R")
 
 
 def test_rna_recoup_path(sh, c1):
     """coverageRnaRef (R/coverage.R:79-124) as ONE 3-group pass per sample: its coverage is the
     reference's three calcCoverage passes merged with c(le, ce, ri) (here: three oracle passes),
-    and profileMatrix of it matches the golden RNA profile (man/coverageRnaRef.Rd)."""
+    and profileMatrix of it matches the golden RNA profile (man/coverageRnaRef.Rd), rows named
+    by the exon list (names(genomeRanges), :121)."""
     from recoup_amd.granges import getFlankingRanges
     genes, exons = c1["genes"], c1["exons"]
     inp = rm.coverage_rna_ref(sh, _inputs(c1), exons, genes, (2000, 2000))
@@ -118,10 +192,13 @@ def test_rna_recoup_path(sh, c1):
         ix = c1["idx"][k]
         want = o.rna_merge(_oracle_cov(ix, left), o.coverage(ix, ex, True, 8), _oracle_cov(ix, right))
         _assert_cov_equal(_decode(x["coverage"]), want)
-    inp = rm.profile_matrix_fused(sh, inp, (2000, 2000), dict(flankBinSize=50, regionBinSize=150,
-                                                              interpolation="auto"))
+    bp = dict(flankBinSize=50, regionBinSize=150, interpolation="auto")
+    inp = rm.profile_matrix(sh, inp, (2000, 2000), bp)
+    ref = rm.ref_profile_matrix(sh, [dict(coverage=x["coverage"]) for x in inp], (2000, 2000), bp)
     for k, x in enumerate(inp):
         np.testing.assert_allclose(x["profile"], c1["gold"][f"rna_s{k}"], rtol=MEAN_RTOL, atol=0)
+        _assert_dimnames(x["profile"], o.profile_dimnames(list(E["names"]), (2000, 2000), bp, False), "rna")
+        _assert_same_matrix(x["profile"], ref[k]["profile"], "rna: rcp.R profileMatrix vs R/profile.R's")
 
 
 def test_profile_from_reads(sh, c1):
@@ -134,7 +211,8 @@ def test_profile_from_reads(sh, c1):
     two = rm.profile_matrix_from_reads(sh, _inputs(c1), mask, (2000, 2000), bp, devices=(0, 0))
     for k in range(2):
         np.testing.assert_allclose(one[k]["profile"], c1["gold"][f"tss_heat_s{k}"], rtol=MEAN_RTOL, atol=0)
-        np.testing.assert_array_equal(two[k]["profile"], one[k]["profile"])
+        _assert_dimnames(one[k]["profile"], o.profile_dimnames(list(mask.names), (2000, 2000), bp, True), "reads")
+        _assert_same_matrix(two[k]["profile"], one[k]["profile"], "two device slots vs one")
     assert sh.live_handles() == 0
 
 

@@ -296,3 +296,56 @@ def test_mirror_read_args_of_a_split_list():
     order = np.argsort(g.seqcodes, kind="stable")
     np.testing.assert_array_equal(args[1], g.start[order])
     np.testing.assert_array_equal(args[3], g.strand[order])
+
+
+# ---------------------------------------------------------------- profile shapes (dimnames)
+def test_profile_dimnames_rules():
+    """The oracle's restatement of the dimnames R leaves on profileMatrix's matrix."""
+    from oracle import oracle as o
+    names = ["g1", "g2", "g3"]
+    assert o.bin_colnames(3, "mean") == ["1.mean", "2.mean", "3.mean"]
+    # equal lengths: rbind of the named list
+    assert o.profile_dimnames(names, (2000, 2000), dict(regionBinSize=0), True) == (names, None)
+    assert o.profile_dimnames(names, (2000, 2000), dict(regionBinSize=2, sumStat="median"), True) == \
+        (names, ["1.median", "2.median"])
+    assert o.profile_dimnames(None, (2000, 2000), dict(regionBinSize=0), True) is None
+    assert o.profile_dimnames(None, (2000, 2000), dict(regionBinSize=1), True) == (None, ["1.mean"])
+    # unequal: cbind(left, center, right) + rownames<-; flank bins round(2 * fbs * f / sum(f))
+    dn = o.profile_dimnames(names, (3000, 1000), dict(flankBinSize=2, regionBinSize=2), False)
+    assert dn == (names, ["1.mean", "2.mean", "3.mean", "1.mean", "2.mean", "1.mean"])
+    dn = o.profile_dimnames(names, (2, 0), dict(flankBinSize=0, regionBinSize=1), False)
+    assert dn == (names, ["", "", "1.mean"])
+
+
+def test_r_cbind_model():
+    from tests import r_mirror as rm
+    from tests.rmini.rmini import RArray
+    a = RArray(np.zeros((2, 2)))
+    b = RArray(np.ones((2, 1)), (None, ["1.mean"]))
+    m = rm.r_cbind(None, a, b)
+    assert m.shape == (2, 3) and m.dimnames == (None, ["", "", "1.mean"])
+    assert rm.r_set_rownames(m, ["x", "y"]).dimnames == (["x", "y"], ["", "", "1.mean"])
+    assert rm.r_cbind(a, a).dimnames is None
+    assert rm.r_set_rownames(a, None).dimnames is None
+
+
+def test_rcp_replaces_profile_matrix():
+    """profileMatrix keeps the reference's signature (R/profile.R:1) and makes one library call
+    per sample in the unequal-length branch; the binning functions name rows as the reference's
+    rbind does: by names(cvrg) when mapping over cvrg itself, not over the slices."""
+    src = open(RSRC).read()
+    pm = _r_function(src, "profileMatrix")
+    assert pm.startswith("profileMatrix <- function(input, flank, binParams, rc = NULL) {")
+    assert "for (n in names(input))" in pm and "if (!any(hasProfile))" in pm
+    assert pm.count(".rcpProfileRle(") == 1 and "names(cvrg))" in pm
+    assert "binCoverageMatrix(cvrg, binSize = binParams$regionBinSize" in pm
+    bcm = _r_function(src, "binCoverageMatrix")
+    assert "if (is.null(flank)) names(cvrg) else NULL" in bcm
+    base = _r_function(src, "baseCoverageMatrix")
+    assert "rowNames = names(cvrg)" in base
+    assert "profileMatrixFused" not in src
+    shim = open(SHIM).read()
+    # every profile routine sets the dimnames of the matrix it returns
+    for name, body in _bodies(shim).items():
+        if "allocMatrix" in body:
+            assert "set_dimnames(" in body, name

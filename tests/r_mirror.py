@@ -13,7 +13,7 @@ from recoup_amd.granges import GRanges, GRangesList, getFlankingRanges, getRegio
 
 MIRRORED = [".rcpReadArgs", ".rcpReadSet", ".rcpFree", ".rcpSampleReadSet", ".rcpRows", ".rcpRowArgs",
             ".rcpCoverage", "calcCoverage", ".rcpCoverageRef", ".rcpRnaRows", "coverageRnaRef", ".rcpRleArrays",
-            ".rcpProfileRle", "binCoverageMatrix", "baseCoverageMatrix", ".rcpParts", "profileMatrix",
+            ".rcpProfileRle", ".rcpStrandOfListError", "binCoverageMatrix", "baseCoverageMatrix", ".rcpParts", "profileMatrix",
             "profileMatrixFromReads"]
 
 
@@ -164,8 +164,19 @@ def rcp_coverage(sh, rs, rows, names=None):
     return NamedList(cov, names)
 
 
+class RStop(Exception):
+    """An R stop() raised by the R code mirrored here."""
+
+
+def rcp_strand_of_list_error():
+    """.rcpStrandOfListError()."""
+    raise RStop("unable to find an inherited method for function 'strand' for signature '\"list\"'")
+
+
 def calc_coverage(sh, inp, mask, strand=None, ignore_strand=True):
     """calcCoverage(input, mask, strand, ignore.strand) for a GRanges or a split list."""
+    if strand is not None and not isinstance(inp, GRanges):
+        rcp_strand_of_list_error()
     rs = rcp_read_set(sh, inp, strand)
     try:
         return rcp_coverage(sh, rs, rcp_rows(mask, rs.levels, ignore_strand), mask.names)
@@ -173,10 +184,12 @@ def calc_coverage(sh, inp, mask, strand=None, ignore_strand=True):
         rcp_free(sh, rs)
 
 
-def coverage_ref(sh, input, genomeRanges, region, flank, strandedParams):
-    """.rcpCoverageRef (coverageBaseRef / coverageAreaRef)."""
+def coverage_ref(sh, input, genomeRanges, region, flank, strandedParams, split=False):
+    """.rcpCoverageRef (coverageBaseRef / coverageAreaRef: split = TRUE)."""
     main = getRegionalRanges(genomeRanges, region, flank)
     for x in input:
+        if split and x.get("ranges") is not None and strandedParams.get("strand") is not None:
+            rcp_strand_of_list_error()
         rs = rcp_read_set(sh, x["ranges"], strandedParams.get("strand"))
         x["coverage"] = rcp_coverage(sh, rs, rcp_rows(main, rs.levels, strandedParams.get("ignoreStrand", True)),
                                      main.names)
@@ -217,6 +230,8 @@ def coverage_rna_ref(sh, input, genomeRanges, helperRanges, flank, strandedParam
     left = getFlankingRanges(helperRanges, 1 if flank[0] == 0 else flank[0], "upstream")
     right = getFlankingRanges(helperRanges, 1 if flank[0] == 0 else flank[1], "downstream")
     for x in input:
+        if x.get("ranges") is not None and sp.get("strand") is not None:
+            rcp_strand_of_list_error()
         rs = rcp_read_set(sh, x["ranges"], sp.get("strand"))
         rows = rcp_rna_rows(left, genomeRanges, right, rs.levels, sp.get("ignoreStrand", True))
         x["coverage"] = rcp_coverage(sh, rs, rows, genomeRanges.names)

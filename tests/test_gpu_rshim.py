@@ -245,9 +245,15 @@ def test_split_list_with_merged_seqinfo_and_strands(sh):
     rs_ = rng.integers(0, 3, R)
     mask = GRanges(np.array(lv)[rc], cen - 1500, cen + 1499, rs_, seqlevels=lv)
     seqlen = np.array([L[c] for c in lv], np.int64)
+    whole = GRanges(np.concatenate([np.full(len(parts[c]), c) for c in lv]), np.concatenate(starts),
+                    np.concatenate(ends), np.concatenate(strands), seqlevels=lv, seqlengths=L)
     for strand in (None, "+", "-"):
+        if strand is not None:  # strand() of splitBySeqname's plain list stops in the reference
+            with pytest.raises(rm.RStop, match="strand"):
+                rm.calc_coverage(sh, parts, mask, strand)
         for ign in (True, False):
-            got = _decode(rm.calc_coverage(sh, parts, mask, strand, ign))
+            # the list (merged seqinfo) without a strand filter; the GRanges with one
+            got = _decode(rm.calc_coverage(sh, parts if strand is None else whole, mask, strand, ign))
             ix = o.Index(np.concatenate(codes), np.concatenate(starts), np.concatenate(ends),
                          np.concatenate(strands).astype(np.int8), seqlen,
                          strand_filter=None if strand is None else {"+": 0, "-": 1}[strand])

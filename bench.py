@@ -304,6 +304,16 @@ def main():
         elapsed = float(t.item())
     for p in plans:
         p.status()
+    # every sample the timed passes computed, checked bit for bit against an independent plan of
+    # its readset on the general pileup kernel (sample 0 is also checked against the oracle below)
+    inflight_check = []
+    for i in range(D):
+        ref_plan = Plan(rsets[i], rows, bins, kernel="general", out_ld="padded")
+        ref_out = ref_plan.execute()
+        ref_plan.status()
+        got = outs[i][:, :R]
+        inflight_check.append(bool(torch.equal(got.view(torch.int64), ref_out[:, :R].view(torch.int64))))
+        del ref_plan, ref_out
 
     # ---- per-kernel durations with HIP events on the launch stream
     stream = torch.cuda.current_stream()
@@ -412,6 +422,7 @@ def main():
             "n_overlaps": ovl,
             "plan_ms": plan_s * 1e3,
             "parity_sample": parity,
+            "inflight_check": {"samples": D, "equal_to_general_kernel": inflight_check},
         }
         print(json.dumps(res), flush=True)
     if dist:
@@ -549,6 +560,7 @@ def cpu_baseline(args, data, rows, bins, plan, B):
     regions like cmclapply with rc = NULL) on the first --cpu-regions rows, repeated for about
     --cpu-seconds; multi-range rows (C3) go through the oracle's per-group coverage + splitVector."""
     from oracle import oracle as o
+    from recoup_amd.engine import RowTable
     R = rows.n_rows
     m = min(args.cpu_regions, R)
     chrom, start, end, strand = data["reads"]
@@ -571,7 +583,6 @@ def cpu_baseline(args, data, rows, bins, plan, B):
                 return o.profile_part(ix, mask, nb, nthreads=threads)
             return o.profile_part(ix, mask, 0, ncol=B, nthreads=threads)
     else:
-        from recoup_amd.engine import RowTable
         sub = RowTable(rows.seg_off[:m + 1], rows.chrom[:rows.seg_off[m]], rows.start[:rows.seg_off[m]],
                        rows.end[:rows.seg_off[m]], rows.strand[:rows.seg_off[m]],
                        seg_group=None if rows.seg_group is None else rows.seg_group[:rows.seg_off[m]],
@@ -590,9 +601,37 @@ def cpu_baseline(args, data, rows, bins, plan, B):
             break
     dt = (time.perf_counter() - t) / reps
     parity = parity_check(plan, bins, ref, rvalid, m, single)
+    # the same restatement on ONE core (beside the all-cores figure), on the first
+    # tenth of the sample's rows so it stays within about --cpu-seconds / 2
+    m1 = max(1, m // 10)
+    if single:
+        mask1 = o.Mask.from_ranges(rows.chrom[:m1], rows.start[:m1], rows.end[:m1], rows.strand[:m1])
+
+        def run1():
+            if nb > 0:
+                return o.profile_part(ix, mask1, nb, nthreads=1)
+            return o.profile_part(ix, mask1, 0, ncol=B, nthreads=1)
+    else:
+        sub1 = RowTable(rows.seg_off[:m1 + 1], rows.chrom[:rows.seg_off[m1]], rows.start[:rows.seg_off[m1]],
+                        rows.end[:rows.seg_off[m1]], rows.strand[:rows.seg_off[m1]],
+                        seg_group=None if rows.seg_group is None else rows.seg_group[:rows.seg_off[m1]],
+                        group_is_list=rows.group_is_list, ignore_strand=rows.ignore_strand)
+
+        def run1():
+            return o.profile_rows(ix, sub1, bins, nthreads=1)
+    reps1 = 0
+    t = time.perf_counter()
+    while True:
+        run1()
+        reps1 += 1
+        if time.perf_counter() - t >= args.cpu_seconds / 2:
+            break
+    dt1 = (time.perf_counter() - t) / reps1
     cpu = {"value": m * B / dt, "unit": "region-bins/s", "cores": threads, "kind": "port",
            "sample": f"first {m} of {R} rows (all their reads), {B} columns; oracle/ C restatement, "
                      f"{threads} threads over regions ({basis}); mean of {reps} passes, {dt:.3f} s/pass",
+           "one_core": {"value": m1 * B / dt1, "cores": 1,
+                        "sample": f"first {m1} rows, 1 thread; mean of {reps1} passes, {dt1:.3f} s/pass"},
            "cpu_model": cpu_model()}
     return cpu, parity
 

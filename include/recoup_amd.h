@@ -106,7 +106,11 @@ RCP_API int rcp_readset_destroy(rcp_readset* rs);
 /* The library's device memory pool (readset arrays, build and encode temporaries) keeps up to
  * 64 GB of freed memory mapped for the next build; this returns what no live object uses. */
 RCP_API int rcp_release_pool(int device);
-/* n_reads kept, and stream offsets (host array of n_chrom*3+1, may be NULL). */
+/* n_reads kept, and stream offsets (host array of n_chrom*3+1, may be NULL) of the strand-split
+ * layout.  A readset made from host arrays builds that layout at its first use -- here when
+ * stream_off != NULL, or in a plan with ignore_strand == 0 -- a device build of the same size as
+ * rcp_readset_create's, which can fail with RCP_ENOMEM / RCP_EHIP; a failed build leaves the
+ * readset as it was (the next use tries again). */
 RCP_API int rcp_readset_info(const rcp_readset* rs, int64_t* n_reads, int64_t* stream_off);
 
 /* ------------------------------------------------------------------ rows */

@@ -333,6 +333,20 @@ struct PoolArr {
     PoolArr() = default;
     PoolArr(const PoolArr&) = delete;
     PoolArr& operator=(const PoolArr&) = delete;
+    PoolArr(PoolArr&& o) noexcept : p(o.p), bytes(o.bytes) {
+        o.p = nullptr;
+        o.bytes = 0;
+    }
+    PoolArr& operator=(PoolArr&& o) noexcept {
+        if (this != &o) {
+            if (p) (void)hipFreeAsync(p, nullptr);
+            p = o.p;
+            bytes = o.bytes;
+            o.p = nullptr;
+            o.bytes = 0;
+        }
+        return *this;
+    }
     ~PoolArr() {
         if (p) (void)hipFreeAsync(p, nullptr);  // after rcp_readset's device synchronisation
     }
@@ -421,8 +435,11 @@ namespace {
 // (chromosome, start) order -- a coordinate-sorted BAM's readGAlignments does -- and then skips its
 // radix sort; the stranded layout of such reads is a stable sort on the stream id alone (one
 // 8-bit pass instead of five: the start order inside each stream is already there).
-int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, const int32_t* ps, const int32_t* pe,
-                 const int8_t* pst, int merge, ReadLayout* L, hipStream_t s, bool* presorted) {
+// Builds one layout of the reads into *L (a fresh ReadLayout: PoolArr allocates once) and
+// returns the number of reads it kept in *kept.  Reads rs's seqlengths only.
+int build_layout(const rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, const int32_t* ps,
+                 const int32_t* pe, const int8_t* pst, int merge, ReadLayout* L, hipStream_t s, bool* presorted,
+                 int64_t* kept_out) {
     const int64_t n = d->n;
     const int64_t n_streams = (int64_t)d->n_chrom * 3;  // + 1 sentinel stream (dropped reads)
 #if RCP_PLAN_TIMING
@@ -562,7 +579,7 @@ int build_layout(rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, co
     }
     HIP_TRY(hipStreamSynchronize(s));
     LAYOUT_MARK("  directory");
-    rs->n = kept;
+    *kept_out = kept;
     return RCP_OK;
 }
 
@@ -579,10 +596,15 @@ int ensure_stranded(const rcp_readset* crs) {
     DeviceGuard g(rs->device);
     HIP_TRY(g.err);
     bool presorted = rs->presorted;
-    const int64_t kept = rs->n;
-    const int rc = build_layout(rs, &rs->desc, rs->kc, rs->ks, rs->ke, rs->kst, 0, &rs->stranded, nullptr, &presorted);
+    int64_t kept = 0;
+    // built into a local layout, moved in only when complete: a failed build (e.g. out of
+    // memory) leaves no half-allocated arrays behind, so a later call can build it again
+    ReadLayout L;
+    const int rc = build_layout(rs, &rs->desc, rs->kc, rs->ks, rs->ke, rs->kst, 0, &L, nullptr, &presorted, &kept);
     if (rc) return rc;
-    rs->n = kept;
+    if (kept != rs->n) return fail(RCP_EINVAL, "internal: stranded layout kept %lld reads, merged %lld",
+                                   (long long)kept, (long long)rs->n);
+    rs->stranded = std::move(L);
     rs->keep_chrom.reset();
     rs->keep_start.reset();
     rs->keep_end.reset();
@@ -697,14 +719,16 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     }
     PLAN_MARK("reads H2D");
     bool presorted = false;
-    rc = build_layout(rs.get(), d, pc, ps, pe, pst, 1, &rs->merged, s, &presorted);
+    int64_t kept = 0;
+    rc = build_layout(rs.get(), d, pc, ps, pe, pst, 1, &rs->merged, s, &presorted, &kept);
     if (rc) return rc;
+    rs->n = kept;
     PLAN_MARK("merged layout");
     rs->presorted = presorted;
     rs->desc = *d;
     if (d->on_device) {
         // the caller's device arrays are not ours to keep: the stranded layout now
-        rc = build_layout(rs.get(), d, pc, ps, pe, pst, 0, &rs->stranded, s, &presorted);
+        rc = build_layout(rs.get(), d, pc, ps, pe, pst, 0, &rs->stranded, s, &presorted, &kept);
         if (rc) return rc;
         rs->stranded_ready = true;
         PLAN_MARK("stranded layout");
@@ -1929,10 +1953,16 @@ extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int3
     int64_t nr = 0;
     rc = rle_encode_device(n_rows, d_off.as<int64_t>(), d_cov, d_run_off.as<int64_t>(), &nr, s);
     if (rc) return rc;
-    HIP_TRY(rcp_rle_encode_dev(n_rows, d_off.as<int64_t>(), d_cov, nullptr, d_run_off.as<int64_t>(), nullptr, nullptr,
+    PoolBuf bad(s);
+    HIP_TRY(bad.alloc(4));
+    HIP_TRY(hipMemsetAsync(bad.p, 0, 4, s));
+    HIP_TRY(rcp_rle_encode_dev(n_rows, d_off.as<int64_t>(), d_cov, nullptr, d_run_off.as<int64_t>(), bad.p, nullptr,
                                d_values, d_lengths, 2, s));
     HIP_TRY(hipMemcpyAsync(run_off, d_run_off.p, 8 * ((size_t)n_rows + 1), hipMemcpyDeviceToHost, s));
+    uint32_t h_bad = 0;
+    HIP_TRY(hipMemcpyAsync(&h_bad, bad.p, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (h_bad) return fail(RCP_EINVAL, "internal: run counts and emitted runs disagree");
     *n_runs = nr;
     return RCP_OK;
     RCP_CATCH
@@ -2003,9 +2033,13 @@ extern "C" int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows
         res->n_runs = nr;
         HIP_TRY(res->values.alloc(4 * (size_t)std::max<int64_t>(nr, 1)));
         HIP_TRY(res->lengths.alloc(4 * (size_t)std::max<int64_t>(nr, 1)));
+        HIP_TRY(hipMemsetAsync(d_count.p, 0, 4, s));  // the counts are scanned: their words are free
         HIP_TRY(rcp_rle_encode_dev(R, d_off.as<int64_t>(), d_cov.as<int32_t>(), nullptr, res->run_off.as<int64_t>(),
-                                   nullptr, nullptr, res->values.as<int32_t>(), res->lengths.as<int32_t>(), 2, s));
+                                   d_count.p, nullptr, res->values.as<int32_t>(), res->lengths.as<int32_t>(), 2, s));
+        uint32_t h_bad = 0;
+        HIP_TRY(hipMemcpyAsync(&h_bad, d_count.p, 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        if (h_bad) return fail(RCP_EINVAL, "internal: run counts and emitted runs disagree");
     }
     *out = res.release();
     return RCP_OK;

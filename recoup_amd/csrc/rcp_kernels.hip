@@ -3047,11 +3047,13 @@ __global__ void __launch_bounds__(64 * kRleWaves) rcp_rle_emit_kernel(int32_t n_
                                                                     const int32_t* __restrict__ cov,
                                                                     const int64_t* __restrict__ run_off,
                                                                     int32_t* __restrict__ values,
-                                                                    int32_t* __restrict__ lengths) {
+                                                                    int32_t* __restrict__ lengths,
+                                                                    uint32_t* __restrict__ bad) {
     const int r = blockIdx.x * kRleWaves + (threadIdx.x >> 6);
     if (r >= n_rows) return;
     const int lane = threadIdx.x & 63;
-    if (run_off[r + 1] == run_off[r]) return;  // no runs: an empty or NULL row
+    const int64_t end = run_off[r + 1];  // the row's runs, as the counts sized them
+    if (end == run_off[r]) return;        // no runs: an empty or NULL row
     const int64_t a = off[r], b = off[r + 1];
     const uint64_t below = (1ull << lane) - 1;  // lanes < this one
     int64_t k = run_off[r];                      // next run index
@@ -3074,12 +3076,14 @@ __global__ void __launch_bounds__(64 * kRleWaves) rcp_rle_emit_kernel(int32_t n_
             if (m == 0) continue;
             const int first = __builtin_ctzll(m);
             const int64_t s0 = base + 64 * u;  // position of lane 0 in this step
-            if (pend >= 0 && lane == first) lengths[pend] = (int32_t)(i - pstart);
+            if (pend >= 0 && pend < end && lane == first) lengths[pend] = (int32_t)(i - pstart);
             if (f) {
                 const int64_t idx = k + __popcll(m & below);
-                values[idx] = v[u];
-                const uint64_t after = m & ~(below | (1ull << lane));
-                if (after) lengths[idx] = __builtin_ctzll(after) - lane;
+                if (idx < end) {  // never past the row's runs, whatever the counts said
+                    values[idx] = v[u];
+                    const uint64_t after = m & ~(below | (1ull << lane));
+                    if (after) lengths[idx] = __builtin_ctzll(after) - lane;
+                }
             }
             const int last = 63 - __builtin_clzll(m);
             k += __popcll(m);
@@ -3087,7 +3091,8 @@ __global__ void __launch_bounds__(64 * kRleWaves) rcp_rle_emit_kernel(int32_t n_
             pstart = s0 + last;
         }
     }
-    if (pend >= 0 && lane == 0) lengths[pend] = (int32_t)(b - pstart);
+    if (pend >= 0 && pend < end && lane == 0) lengths[pend] = (int32_t)(b - pstart);
+    if (lane == 0 && k != end) atomicOr(bad, 1u);  // the counting pass and this one disagree
 }
 
 // The run starts the coverage pileup could not see (rcp_pileup_kernel's csr_runs): the seams
@@ -3123,8 +3128,9 @@ extern "C" hipError_t rcp_rle_seams_dev(int32_t n_rows, const int64_t* d_off, co
 extern "C" hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, int64_t* d_count,
                                          int64_t* d_run_off, void* temp, size_t* temp_bytes, int32_t* d_values,
                                          int32_t* d_lengths, int pass, hipStream_t stream) {
-    // pass 0: temp size of the scan; 1: count + scan (d_run_off[n_rows] = total); 2: emit;
-    // 3: scan of counts made elsewhere (d_count[n_rows] must be 0)
+    // pass 0: temp size of the scan; 1: count + scan (d_run_off[n_rows] = total); 2: emit
+    // (temp: a zeroed uint32 flag, set when a row's runs differ from its count); 3: scan of
+    // counts made elsewhere (d_count[n_rows] must be 0)
     if (pass == 0)
         return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, d_count, d_run_off, (int)n_rows + 1, stream);
     if (pass == 3)
@@ -3141,7 +3147,7 @@ extern "C" hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, c
     }
     if (n_rows > 0)
         hipLaunchKernelGGL(rcp_rle_emit_kernel, dim3(grid), dim3(64 * kRleWaves), 0, stream, n_rows, d_off, d_cov,
-                           d_run_off, d_values, d_lengths);
+                           d_run_off, d_values, d_lengths, static_cast<uint32_t*>(temp));
     return hipGetLastError();
 }
 

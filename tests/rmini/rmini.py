@@ -148,7 +148,7 @@ class Shim:
             nr, nc = L.rmini_dim(p, 0), L.rmini_dim(p, 1)
             if nr or nc:
                 dn = L.rmini_dimnames(p)
-                dn = None if L.rmini_type(dn) == NILSXP else tuple(self.from_r(e) for e in self.from_r(dn))
+                dn = None if L.rmini_type(dn) == NILSXP else tuple(self.from_r(dn))
                 return RArray(a.reshape((nr, nc), order="F"), dn)
             return a
         if t == CHARSXP:

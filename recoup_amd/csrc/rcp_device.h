@@ -198,3 +198,5 @@ __host__ __device__ inline void rcp_part_slice(const RcpPart& p, int32_t nr, int
 #define RCP_STATUS_OVERFLOW 1u
 #define RCP_STATUS_WIDTH 2u
 #define RCP_STATUS_INTERP 4u
+
+#include "rcp_divrn.h"

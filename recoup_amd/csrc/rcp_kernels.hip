@@ -558,8 +558,14 @@ __global__ void rcp_dir_kernel(int64_t n_entries, int64_t n_streams, const int64
 }
 
 // Inline-key directory (rcp_device.h dir_k): thread t fills half t & 1 of entry t >> 1 from the
-// interleaved (dir_l, dir_u) entries e and e + 1 of the same directory.
+// interleaved (dir_l, dir_u) entries e and e + 1 of the same directory.  A bucket of n <= 14
+// reads keeps its keys; a denser one (reads piled at a peak or a DNase site, far above the
+// genome-average density the bucket width is sized for) keeps the keys at bucket offsets
+// m_i = (i + 1) n / 15 (rcp_dirk_offset), so one line narrows any search to n / 15 reads.
 constexpr int kDirKeys = 14;
+__device__ __forceinline__ int32_t rcp_dirk_offset(int32_t n, int i) {
+    return n <= kDirKeys ? i : (int32_t)(((int64_t)(i + 1) * n) / (kDirKeys + 1));
+}
 __global__ void rcp_dirk_kernel(int64_t n_entries, const int32_t* __restrict__ dir_lu, const int32_t* __restrict__ pmax,
                                 const int2* __restrict__ se, int32_t* __restrict__ dir_k) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -574,7 +580,10 @@ __global__ void rcp_dirk_kernel(int64_t n_entries, const int32_t* __restrict__ d
     w[0] = a;
     w[1] = b;
 #pragma unroll
-    for (int i = 0; i < kDirKeys; ++i) w[2 + i] = a + i < b ? (h ? se[a + i].x : pmax[a + i]) : 0;
+    for (int i = 0; i < kDirKeys; ++i) {
+        const int32_t k = a + rcp_dirk_offset(b - a, i);
+        w[2 + i] = k < b ? (h ? se[k].x : pmax[k]) : 0;
+    }
     int4* dst = reinterpret_cast<int4*>(dir_k + 32 * e + 16 * h);
 #pragma unroll
     for (int q = 0; q < 4; ++q) dst[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
@@ -644,12 +653,15 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
         }
     }
     if (P.dir_k) {
-        // one line per search: the bucket's edges and first keys; the answer is the number of
-        // those keys below the threshold unless all of them are (then bisect the rest)
+        // one line per search: the bucket's edges and 14 keys -- its first ones (n <= 14: the
+        // answer is the number of keys below the threshold) or, in a denser bucket, the keys at
+        // offsets m_i = (i + 1) n / 15: c keys below the threshold put the answer in
+        // (m_{c-1}, m_c] (rcp_dirk_offset), searched below
 #ifndef RCP_DIRK_QUADS
 #define RCP_DIRK_QUADS 4  // 16-byte words of the entry half read per search (keys: 4 q - 2)
 #endif
         constexpr int kQ = RCP_DIRK_QUADS, kKeys = 4 * kQ - 2;
+        static_assert(kKeys == kDirKeys, "the search reads the keys rcp_dirk_kernel writes");
         int4 w[K][kQ];
 #pragma unroll
         for (int u = 0; u < K; ++u) {
@@ -668,12 +680,52 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
                 uint32_t c = 0;
 #pragma unroll
                 for (int i = 0; i < kKeys; ++i) c += (i < n && (int64_t)x[2 + i] < thr[u]) ? 1u : 0u;
-                lo[u] = (uint32_t)x[0] + c;
-                hi[u] = c < (uint32_t)kKeys ? lo[u] : (uint32_t)x[1];
+                if (n <= kKeys) {
+                    lo[u] = (uint32_t)x[0] + c;
+                    hi[u] = c < (uint32_t)kKeys ? lo[u] : (uint32_t)x[1];
+                } else {
+                    lo[u] = (uint32_t)x[0] + (c ? (uint32_t)rcp_dirk_offset(n, (int)c - 1) + 1u : 0u);
+                    hi[u] = c < (uint32_t)kKeys ? (uint32_t)x[0] + (uint32_t)rcp_dirk_offset(n, (int)c) : (uint32_t)x[1];
+                }
             }
         }
     }
     const int32_t* se = reinterpret_cast<const int32_t*>(P.se);
+    // wide ranges: 8-ary steps, the 7 probes of every unfinished search in flight together
+    // (p_j = lo + j len / 8; c probes below the threshold leave (p_c, p_{c+1}]), then bisection
+#ifndef RCP_LOC_KARY
+#define RCP_LOC_KARY 0  // 1: 8-ary steps (C4 / C5 locate slower: profiles/r04/locate_ab.log)
+#endif
+    while (RCP_LOC_KARY && !(RCP_LOC_ABL & 2)) {
+        constexpr int kP = 7;
+        int32_t kv[K][kP];
+        uint32_t len[K];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            len[u] = hi[u] - lo[u];
+            if (lo[u] < hi[u] && len[u] >= 32u) {
+                any = true;
+#pragma unroll
+                for (int j = 1; j <= kP; ++j) {
+                    const uint32_t m = lo[u] + (uint32_t)(((uint64_t)j * len[u]) >> 3);
+                    kv[u][j - 1] = up[u] ? se[(size_t)m << 1] : P.pmax[m];
+                }
+            }
+        }
+        if (!any) break;
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            if (lo[u] < hi[u] && len[u] >= 32u) {
+                int c = 0;
+#pragma unroll
+                for (int j = 0; j < kP; ++j) c += (int64_t)kv[u][j] < thr[u] ? 1 : 0;
+                const uint32_t l0 = lo[u];
+                if (c > 0) lo[u] = l0 + (uint32_t)(((uint64_t)c * len[u]) >> 3) + 1u;
+                if (c < kP) hi[u] = l0 + (uint32_t)(((uint64_t)(c + 1) * len[u]) >> 3);
+            }
+        }
+    }
     while (!(RCP_LOC_ABL & 2)) {
         uint32_t m[K];
         int32_t kv[K];
@@ -1584,23 +1636,29 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
                 put4(k, o, x);
             }
         } else if (MEDIAN || lay < 0) {
+            // RN(x / den) through the row's correctly rounded reciprocal (rcp_div_rn: bit-equal
+            // to the division, a third of its instructions)
             const uint32_t* st = st0;
             for (int32_t k = kq; k < kend; k += kStep, o += ostep, st += kStep) {
                 const uint4 q = *reinterpret_cast<const uint4*>(st);
-                const double x[4] = {((double)q.x * sc) / dd, ((double)q.y * sc) / dd,
-                                     ((double)q.z * sc) / dd, ((double)q.w * sc) / dd};
+                const double x[4] = {rcp_div_rn((double)q.x * sc, dd, rdd), rcp_div_rn((double)q.y * sc, dd, rdd),
+                                     rcp_div_rn((double)q.z * sc, dd, rdd), rcp_div_rn((double)q.w * sc, dd, rdd)};
                 put4(k, o, x);
             }
         } else {
+            // splitVector layout: bins of bs or bs + 1 positions, one reciprocal each
             const int32_t* cnt = P.lay_cnt + lay;
+            const double dd1 = (double)(bs + 1), rdd1 = 1.0 / dd1;
             const uint32_t* st = st0;
             for (int32_t k = kq; k < kend; k += kStep, o += ostep, st += kStep) {
                 const uint4 q = *reinterpret_cast<const uint4*>(st);
                 const uint32_t num[4] = {q.x, q.y, q.z, q.w};
                 double x[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    x[u] = k + u < kend ? ((double)num[u] * sc) / (double)(bs + cnt[k + u + 1] - cnt[k + u]) : 0.0;
+                for (int u = 0; u < 4; ++u) {
+                    const bool enl = k + u < kend && cnt[k + u + 1] != cnt[k + u];
+                    x[u] = k + u < kend ? rcp_div_rn((double)num[u] * sc, enl ? dd1 : dd, enl ? rdd1 : rdd) : 0.0;
+                }
                 put4(k, o, x);
             }
         }
@@ -2006,6 +2064,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             const int32_t kw = max(1, kRWCap / (bs + (lay >= 0 ? 1 : 0)));  // bins per window
             const bool pow2 = lay < 0 && (bs & (bs - 1)) == 0;
             const double dd = (double)bs, rdd = 1.0 / dd;
+            const double dd1 = (double)(bs + 1), rdd1 = 1.0 / dd1;  // an enlarged bin's width
             for (int32_t k0 = 0; k0 < n; k0 += kw) {
                 const int32_t k1 = min(n, k0 + kw);
                 const int32_t e0 = bin_edge(bs, lay, P.lay_cnt, k0);
@@ -2074,8 +2133,8 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     const uint32_t num = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
                     double x;
                     if (pow2) x = ((double)num * sc) * rdd;
-                    else if (lay < 0) x = ((double)num * sc) / dd;
-                    else x = ((double)num * sc) / (double)(b - a);
+                    else if (b - a == bs) x = rcp_div_rn((double)num * sc, dd, rdd);
+                    else x = rcp_div_rn((double)num * sc, dd1, rdd1);  // b - a == bs + 1
                     rows_store(x, cell(r, part.col_off + k));
                     if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = (int64_t)num;
                 }
@@ -2135,6 +2194,9 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
 #endif
 #ifndef RCP_LWPE
 #define RCP_LWPE 6
+#endif
+#ifndef RCP_LBATCH_UNI
+#define RCP_LBATCH_UNI 4  // reads per lane per batch of a start-only (uniform-width) lean plan
 #endif
 constexpr int kLStoreWaves = RCP_LSTORE_WAVES;
 constexpr int kLBlock = 64 * (kPWaves + kLStoreWaves);
@@ -2299,6 +2361,9 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     // is formed when the read is added, so the prefetched loads stay in flight until then
     static_assert(!(UNI && GEN), "uniform-width reads: single-range mode only");
     using RdT = typename std::conditional<UNI, int32_t, int2>::type;
+    // reads per lane per batch: start-only streams (4 B per read) keep RCP_LBATCH_UNI in flight
+    constexpr int BL = UNI ? RCP_LBATCH_UNI : 4;
+    constexpr uint32_t BQ = 64u * BL;  // reads per batch
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int lane = tid & 63;
@@ -2361,7 +2426,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             const uint32_t n = (m.flag == 0 && m.fast) ? lean_candidates(m) : 0;
             if (n) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < BL; ++u) {
                     const uint32_t q = lane + 64 * u;
                     dst[u] = rd_load(lean_index(m, q < n ? q : n - 1));
                 }
@@ -2373,7 +2438,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         // one row: `cur` holds its first reads; the next row's (possibly the next item's
         // first row) go to `nxt`
         // pile row i of the item (tile row), its first reads in `cur`; bin sums -> stage
-        auto pile_row = [&](const LeanItem& it, int i, RdT (&cur)[4]) __attribute__((always_inline)) {
+        auto pile_row = [&](const LeanItem& it, int i, RdT (&cur)[BL]) __attribute__((always_inline)) {
             const LeanRow m = lean_row(lmeta[buf * kRows + i]);
             if (m.flag != 0) return;
             if (!GEN && !m.fast && m.heavy < 0) {  // the plan promised single-range rows
@@ -2402,10 +2467,10 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 const uint32_t n = lean_candidates(m);
                 // batches of 256 reads, three in flight: `cur` (prefetched with the previous
                 // row), b1, b2; the loop is unrolled over the ring so no buffer is copied
-                auto load_batch = [&](uint32_t q0, RdT (&dst)[4]) {
+                auto load_batch = [&](uint32_t q0, RdT (&dst)[BL]) {
                     if (q0 < n) {
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
+                        for (int u = 0; u < BL; ++u) {
                             const uint32_t q = q0 + lane + 64 * u;
                             dst[u] = rd_load(lean_index(m, q < n ? q : n - 1));
                         }
@@ -2415,10 +2480,10 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 #define RCP_LDENSE 1
 #endif
                 const bool dense = RCP_LDENSE && n >= (uint32_t)npos;  // wave-uniform
-                auto add_batch = [&](uint32_t q0, const RdT (&src)[4]) {
+                auto add_batch = [&](uint32_t q0, const RdT (&src)[BL]) {
                     if (RCP_LEAN_ABL & 1) {  // timing ablation: loads kept, no adds
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) asm volatile("" ::"v"(src[u]));
+                        for (int u = 0; u < BL; ++u) asm volatile("" ::"v"(src[u]));
                         return;
                     }
                     if constexpr (UNI) {
@@ -2428,11 +2493,11 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                             const int32_t hi_w = m.rev ? m.k - m.gps : m.gpe + m.k;
                             if (m.rev) {
 #pragma unroll
-                                for (int u = 0; u < 4; ++u)
+                                for (int u = 0; u < BL; ++u)
                                     lean_add_runs_uni<true>(m, src[u], w, lo_w, hi_w, q0 + lane + 64u * u < n, diff, sh);
                             } else {
 #pragma unroll
-                                for (int u = 0; u < 4; ++u)
+                                for (int u = 0; u < BL; ++u)
                                     lean_add_runs_uni<false>(m, src[u], w, lo_w, hi_w, q0 + lane + 64u * u < n, diff, sh);
                             }
                             return;
@@ -2441,27 +2506,27 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                     if (dense) {
                         if (m.rev) {
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) lean_add_runs<true>(m, rd_pair(src[u]), q0 + lane + 64u * u < n, diff, sh);
+                            for (int u = 0; u < BL; ++u) lean_add_runs<true>(m, rd_pair(src[u]), q0 + lane + 64u * u < n, diff, sh);
                         } else {
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) lean_add_runs<false>(m, rd_pair(src[u]), q0 + lane + 64u * u < n, diff, sh);
+                            for (int u = 0; u < BL; ++u) lean_add_runs<false>(m, rd_pair(src[u]), q0 + lane + 64u * u < n, diff, sh);
                         }
                     } else if (m.rev) {
 #pragma unroll
-                        for (int u = 0; u < 4; ++u)
+                        for (int u = 0; u < BL; ++u)
                             if (q0 + lane + 64u * u < n) lean_add<true>(m, rd_pair(src[u]), diff, sh);
                     } else {
 #pragma unroll
-                        for (int u = 0; u < 4; ++u)
+                        for (int u = 0; u < BL; ++u)
                             if (q0 + lane + 64u * u < n) lean_add<false>(m, rd_pair(src[u]), diff, sh);
                     }
                 };
-                for (uint32_t q0 = 0; q0 < n; q0 += 256) {
-                    RdT nx[4];
-                    load_batch(q0 + 256, nx);
+                for (uint32_t q0 = 0; q0 < n; q0 += BQ) {
+                    RdT nx[BL];
+                    load_batch(q0 + BQ, nx);
                     add_batch(q0, cur);
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) cur[u] = nx[u];
+                    for (int u = 0; u < BL; ++u) cur[u] = nx[u];
                 }
             }
             lds_order();
@@ -2496,7 +2561,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             }
             lds_order();
         };
-        RdT bufA[4], bufB[4];
+        RdT bufA[BL], bufB[BL];
         // Rows are dealt dynamically: a wave takes the workgroup's next row number g from an
         // LDS counter (rows 64 q .. 64 q + 63 = the q-th item of this workgroup, 16 per round)
         // when it starts its current row, and prefetches g's first reads.  A round ends when
@@ -2511,7 +2576,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
             if (lane == 0) v = atomicAdd(ctr, 1u);
             return __builtin_amdgcn_readfirstlane(v);
         };
-        auto fetch = [&](uint32_t rel, RdT (&dst)[4]) {  // rel: row number relative to this item
+        auto fetch = [&](uint32_t rel, RdT (&dst)[BL]) {  // rel: row number relative to this item
             if (rel < (uint32_t)kIRows) {
                 prefetch(lmeta[buf * kRows + rel], dst);
             } else {
@@ -2607,11 +2672,15 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                         double x[4];
                         if (GEN) {
                             // mean of a bin = numerator * scale / width (profile.R via splitVector;
-                            // the general kernel's flush); a NULL row writes zeros
+                            // the general kernel's flush, rcp_div_rn); a NULL row writes zeros
                             const uint32_t q4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+                            const double d0 = (double)bsr, d1 = (double)(bsr + 1);
+                            const double r0 = 1.0 / d0, r1 = 1.0 / d1;
 #pragma unroll
-                            for (int u = 0; u < 4; ++u)
-                                x[u] = flag == 0 ? ((double)q4[u] * sc) / (double)(bsr + ((enl >> (4 * j + u)) & 1)) : 0.0;
+                            for (int u = 0; u < 4; ++u) {
+                                const bool e = (enl >> (4 * j + u)) & 1;
+                                x[u] = flag == 0 ? rcp_div_rn((double)q4[u] * sc, e ? d1 : d0, e ? r1 : r0) : 0.0;
+                            }
                         } else {
                             x[0] = ((double)v[j].x * scf) * rdd;
                             x[1] = ((double)v[j].y * scf) * rdd;

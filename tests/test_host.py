@@ -188,3 +188,16 @@ def test_product_rng_matches_independent_python_restatement():
                 np.testing.assert_array_equal(g.sample_sorted(n, k), np.sort(py.sample_int(n, k)))
     g, py = ra.RRng(11), RRng(11)
     np.testing.assert_array_equal(g.sample_sorted(20_000_001, 50), np.sort(py.sample_int(20_000_001, 50)))
+
+
+def test_reciprocal_division_is_correctly_rounded(tmp_path):
+    """rcp_div_rn (recoup_amd/csrc/rcp_divrn.h), the kernels' bin-mean division RN(x / width)
+    through RN(1 / width) and one FMA correction, equals IEEE division: every numerator below
+    2^18 over every width 1..600, and 2M random (numerator < 2^32, width < 2^20, scale) triples."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "div_rn_check")
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-I", os.path.join(root, "recoup_amd", "csrc"), "-o",
+                           exe, os.path.join(root, "tests", "native", "div_rn_check.c"), "-lm"])
+    r = subprocess.run([exe, "18", "600", "2000000"], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout + r.stderr

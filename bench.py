@@ -37,7 +37,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 # plan.info["pileup_kernel"] -> kernel name (as rocprofv3 lists it)
 PILEUP_KERNELS = {0: "rcp_pileup_kernel", 1: "rcp_pileup_lean_kernel", 2: "rcp_pileup_lean_kernel (general bins)",
-                  3: "rcp_pileup_rows_kernel"}
+                  3: "rcp_pileup_rows_kernel", 4: "rcp_pileup_bins_kernel"}
 
 
 def parse():

@@ -166,7 +166,7 @@ typedef struct {
     int32_t tile_rows;
     int32_t chunk_positions;
     int32_t pileup_kernel;   /* 0: general pileup kernel; 1: lean kernel (pile + store waves);
-                              * 2: lean kernel, general bins; 3: row-wave kernel */
+                              * 2: lean kernel, general bins; 3: row-wave kernel; 4: bin-difference kernel */
     int32_t reserved;
     int64_t out_ld;          /* column stride of d_out / d_binsum (rcp_plan_opts.out_ld resolved):
                               * both must hold out_ld * (n_cols - 1) + n_rows elements */
@@ -185,10 +185,14 @@ RCP_API int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows, co
  * RCP_KERNEL_GENERAL forces the general kernel; RCP_KERNEL_LEAN_ANY
  * also routes other mean plans whose chunks fit one wave pass through the lean kernel's
  * general-bins mode; RCP_KERNEL_ROWS forces the row-wave kernel (whole rows per wave: AUTO takes
- * it for mean plans with multi-range rows).  All choices give bit-identical results.  heavy_threshold: candidate
+ * it for mean plans with multi-range rows); RCP_KERNEL_BINS the bin-difference kernel (a read adds to
+ * the bins it overlaps, not to positions: AUTO takes it for mean plans of one binned part whose
+ * single-range rows are all cut into whole bins of >= 4 positions, <= 512 bins, e.g. TSS
+ * windows in 200 bins).  All choices give bit-identical results.  heavy_threshold: candidate
  * reads per column chunk above which a skewed row is piled by many workgroups first
  * (-1 = default 4096, 0 = never).  out_ld: see the field. */
-enum { RCP_KERNEL_AUTO = 0, RCP_KERNEL_GENERAL = 1, RCP_KERNEL_LEAN_ANY = 2, RCP_KERNEL_ROWS = 3, RCP_KERNEL_LEAN = 4 };
+enum { RCP_KERNEL_AUTO = 0, RCP_KERNEL_GENERAL = 1, RCP_KERNEL_LEAN_ANY = 2, RCP_KERNEL_ROWS = 3, RCP_KERNEL_LEAN = 4,
+       RCP_KERNEL_BINS = 5 };
 typedef struct {
     int32_t pileup_kernel;
     int32_t heavy_threshold;

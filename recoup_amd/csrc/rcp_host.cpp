@@ -58,6 +58,10 @@ constexpr int kLeanMinRowsBinned = RCP_LEAN_MIN_ROWS_BINNED;
 #define RCP_AUTO_GEN 0  // 1: AUTO also takes the lean kernel's general-bins mode (A/B only)
 #endif
 
+#ifndef RCP_BINS_AUTO
+#define RCP_BINS_AUTO 1  // plans of one binned part with uniform bins of >= 4 positions take the bin-difference kernel
+#endif
+
 #ifndef RCP_ROWS_AUTO
 #define RCP_ROWS_AUTO 1  // plans with multi-range rows take the row-wave pileup kernel
 #endif
@@ -84,6 +88,9 @@ int rcp_lean_max_bins(void);
 int rcp_lean_gen_max_bins(void);
 size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
 size_t rcp_pileup_rows_lds_bytes(void);
+size_t rcp_pileup_bins_lds_bytes(const RcpPlanDev* P);
+int rcp_bins_max_bins(void);
+int rcp_bins_min_width(void);
 int rcp_rows_window_cap(void);
 hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
                               const int8_t* strand, int32_t n_chrom, int32_t strand_filter, int merge, uint64_t* keys,
@@ -984,7 +991,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     if (!rs || !rows || !out) return fail(RCP_EINVAL, "NULL argument");
     const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, 0, 0, {0, 0, 0}};
     if (!opts) opts = &default_opts;
-    if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_LEAN)
+    if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_BINS)
         return fail(RCP_EINVAL, "pileup_kernel = %d", opts->pileup_kernel);
     *out = nullptr;
     const rcp_bins_desc coverage_only{};  // bins == NULL: a calcCoverage-only plan
@@ -1251,6 +1258,36 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         if (rows_ok && (kind == RCP_KERNEL_ROWS || (kind == RCP_KERNEL_AUTO && multi_rows && RCP_ROWS_AUTO)))
             P.lean = 3;
     }
+    // ---- bin-difference kernel (lean == 4): mean plans of one binned part whose rows are
+    // single ranges, every row's slice a whole number of bins of >= rcp_bins_min_width()
+    // positions (no splitVector layout, no interpolation), <= rcp_bins_max_bins() bins.  A row
+    // is one wave's pass over its bins (no column chunks).  AUTO takes it for such plans:
+    // C2 (200 bins of 20 bp) ... ; RCP_KERNEL_BINS forces it where the shape allows
+    {
+        const int kind = opts->pileup_kernel;
+        bool bd = !cov_only && bins->stat == RCP_STAT_MEAN && P.n_parts == 1 && !P.part[0].per_base &&
+                  P.part[0].n_bins > 0 && P.part[0].n_bins <= rcp_bins_max_bins() &&
+                  (kind == RCP_KERNEL_AUTO || kind == RCP_KERNEL_BINS) && RCP_BINS_AUTO;
+        const RcpPart& pt0 = P.part[0];
+        for (int r = 0; bd && r < R; ++r) {
+            const int32_t j0 = B.row_seg[r], j1 = B.row_seg[r + 1];
+            if (B.row_static[r] || j1 == j0) continue;  // NULL rows: zeros
+            if (j1 - j0 > 1 || B.segs[j0].multi || !B.segs[j0].query_ok) {
+                bd = false;
+                break;
+            }
+            int32_t head, L;
+            rcp_part_slice(pt0, B.row_len[r], &head, &L);
+            if (L < pt0.n_bins || L % pt0.n_bins != 0 || L / pt0.n_bins < rcp_bins_min_width()) bd = false;
+        }
+        if (bd && B.interp_row.empty()) {
+            P.lean = 4;
+            P.part[0].chunk_bins = P.part[0].n_bins;
+            P.part[0].n_chunks = 1;
+            P.n_chunks_total = 1;
+            P.stage_cap = P.part[0].n_bins;
+        }
+    }
     // ---- lean plans with few row tiles (one GPU's shard of a region table): the persistent
     // grid (two workgroups per CU) takes (row tile, column chunk) items; with few items per
     // workgroup the last ones leave most workgroups idle, so cut the parts into more column
@@ -1470,8 +1507,9 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         HIP_TRY(plan->rm.alloc(8 * (size_t)R * (size_t)P.n_cols));
         P.rm = plan->rm.as<double>();
     }
-    plan->lds = P.lean == 3 ? rcp_pileup_rows_lds_bytes()
-                            : (P.lean ? rcp_pileup_lean_lds_bytes(&P) : rcp_pileup_lds_bytes(&P, cov_only ? 1 : 0));
+    plan->lds = P.lean == 4 ? rcp_pileup_bins_lds_bytes(&P)
+                : P.lean == 3 ? rcp_pileup_rows_lds_bytes()
+                              : (P.lean ? rcp_pileup_lean_lds_bytes(&P) : rcp_pileup_lds_bytes(&P, cov_only ? 1 : 0));
     // general kernel: 2 rounds (32 rows) per workgroup (C3: 0.88 ms vs 0.91 with 4 rounds, 0.89
     // with 1), 1 when the row table is small, so that the grid still holds two workgroups per
     // CU (C2: 10k rows -> 625 workgroups instead of 157; pileup 0.076 -> 0.063 ms)
@@ -1489,9 +1527,10 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
 #ifdef RCP_GEN_ROUNDS_FIX  // A/B only: force the general kernel's rounds per workgroup
         P.rounds = std::min(rmax, (int)RCP_GEN_ROUNDS_FIX);
 #endif
-        plan->tile_rows = P.lean ? (P.lean_rounds == 2 ? 2 * tile : rcp_tile_rows()) : tile * P.rounds;
+        plan->tile_rows = P.lean == 4 ? tile : (P.lean ? (P.lean_rounds == 2 ? 2 * tile : rcp_tile_rows()) : tile * P.rounds);
     }
     plan->grid = (int64_t)((R + plan->tile_rows - 1) / plan->tile_rows) * P.n_chunks_total;
+    if (P.lean == 4) plan->grid = (plan->grid + 7) / 8 * 8;
     if (plan->lds > 160 * 1024) return fail(RCP_EUNSUPPORTED, "plan needs %zu B of LDS", plan->lds);
     PLAN_MARK("rest");
     HIP_TRY(hipMemset(plan->work.p, 0, plan->work.bytes));

@@ -2718,6 +2718,267 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 }
 
 // =================================================================================
+// bin-difference pileup (P.lean == 4): mean profiles whose rows are single ranges cut into
+// uniform bins (every row's slice L = n bs positions: no splitVector layout, no interpolation)
+// of at least kBDMinWidth positions, at most kBDMaxBins bins.  A read adds to BINS, not to
+// positions: its covered row positions [u, v] (clipped) give bins ku = u / bs and kv = v / bs
+// the partial overlaps bs (ku + 1) - u and v - bs kv + 1 (or v - u + 1 when ku == kv), and the
+// bins strictly between take bs each through a difference array F (+1 at ku + 1, -1 at kv):
+// numerator[k] = D[k] + bs * prefix(F)[k], the exact integer sum the position pileup gives
+// (R/util.R:74-84 with dif = 0, R/profile.R:159-208).  Per row the work is O(n bins) instead
+// of O(L positions) -- C2's 200 bins of 20 bp instead of 4000 positions in four column chunks
+// -- and a whole row is one wave's pass (no column chunks, no per-chunk read ranges).
+// Workgroups of 4 waves own 16-row tiles (one 128-B line of every output column); each wave
+// piles 4 of the rows into its own D / F arrays and stages their numerators; the workgroup
+// then writes the tile column-major.
+// =================================================================================
+constexpr int kBDWaves = 4;
+constexpr int kBDMaxBins = 512;
+constexpr int kBDMinWidth = 4;
+extern "C" int rcp_bins_max_bins(void) { return kBDMaxBins; }
+extern "C" int rcp_bins_min_width(void) { return kBDMinWidth; }
+
+__host__ __device__ __forceinline__ int bd_stage_stride(int n) { return ((n + 3) >> 2 << 2) + 4; }
+__host__ __device__ __forceinline__ int bd_wave_words(int n) { return 2 * (((n + 2) + 63) & ~63); }
+
+extern "C" size_t rcp_pileup_bins_lds_bytes(const RcpPlanDev* P) {
+    const int n = P->part[0].n_bins;
+    return 4 * ((size_t)kTile * bd_stage_stride(n) + (size_t)kBDWaves * bd_wave_words(n) + 2 * kTile);
+}
+
+template <bool UNI>
+__global__ void __launch_bounds__(64 * kBDWaves) __attribute__((amdgpu_waves_per_eu(4)))
+rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restrict__ binsum) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    using RdT = typename std::conditional<UNI, int32_t, int2>::type;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const RcpPart part = P.part[0];
+    const int32_t n = part.n_bins;
+    const int RS = bd_stage_stride(n);
+    const int WW = bd_wave_words(n);
+    uint32_t* stage = reinterpret_cast<uint32_t*>(smem);                 // [16][RS] numerators
+    int32_t* D = reinterpret_cast<int32_t*>(stage + kTile * RS) + wave * WW;  // partial overlaps
+    int32_t* F = D + WW / 2;                                              // full-bin differences
+    int32_t* rbs = reinterpret_cast<int32_t*>(stage + kTile * RS) + kBDWaves * WW;  // [16] bs, 0 NULL, -1 none
+    // tiles of one XCD's workgroups are consecutive (round-robin dispatch over 8 XCDs):
+    // neighbouring regions share reads in that L2
+    const int nt = (P.n_rows + kTile - 1) / kTile;
+    const int per_x = (nt + 7) / 8;
+    const int tile = (blockIdx.x & 7) * per_x + (blockIdx.x >> 3);
+    if (tile >= nt) return;
+    const int row0 = tile * kTile;
+    for (int q = lane; q < WW; q += 64) D[q] = 0;  // D and F
+    auto rd_load = [&](uint32_t idx) -> RdT {
+        if constexpr (UNI) return P.st[idx];
+        else return P.se[idx];
+    };
+    auto rd_pair = [&](RdT v) -> int2 {
+        if constexpr (UNI) return make_int2(v, v + P.st_w);
+        else return v;
+    };
+    // a row's wave-uniform description, from the locate kernel's record
+    struct Row {
+        int32_t flag, heavy, bs, k, gps, gpe, rev, head, L;
+        uint32_t lo[3], hi[3];
+    };
+    auto row_of = [&](int r) -> Row {
+        Row m{};
+        m.flag = -1;
+        if (r >= P.n_rows) return m;
+        RcpRowRec rec;
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(P.rec + r);
+            uint4* dst = reinterpret_cast<uint4*>(&rec);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[q] = src[q];
+        }
+        int32_t v[16];
+        __builtin_memcpy(v, &rec, sizeof v);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = __builtin_amdgcn_readfirstlane(v[q]);
+        RcpRowRec R;
+        __builtin_memcpy(&R, v, sizeof R);
+        if (!(R.flags & RCP_REC_VALID)) {
+            m.flag = 0;  // NULL row -> zeros (profile.R:191-197)
+            return m;
+        }
+        rcp_part_slice(part, R.row_len, &m.head, &m.L);
+        m.bs = m.L / n;
+        if (m.L < n || m.L != m.bs * n || !(R.flags & RCP_REC_FAST)) {
+            // the plan promised uniform bins of single-range rows
+            if (lane == 0) atomicOr(P.status, RCP_STATUS_INTERP);
+            m.flag = 0;
+            return m;
+        }
+        m.flag = 1;
+        m.heavy = R.heavy;
+        m.rev = R.rev;
+        const int32_t len = R.shi - R.slo + 1;
+        const int32_t a = max(m.head, R.off), b = min(m.head + m.L, R.off + len);
+        m.gps = 0;
+        m.gpe = -1;
+        if (a < b) {
+            if (!R.rev) {
+                m.gps = R.slo + (a - R.off);
+                m.gpe = R.slo + (b - 1 - R.off);
+            } else {
+                m.gpe = R.shi - (a - R.off);
+                m.gps = R.shi - (b - 1 - R.off);
+            }
+        }
+        // row position (slice-relative) of genomic g: g + k forward, k - g reversed
+        m.k = R.rev ? R.off + R.shi - m.head : R.off - R.slo - m.head;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            m.lo[s] = R.lo[s];
+            m.hi[s] = a < b ? R.hi[s] : R.lo[s];
+        }
+        return m;
+    };
+    auto n_cand = [&](const Row& m) -> uint32_t {
+        return (m.hi[0] - m.lo[0]) + (m.hi[1] - m.lo[1]) + (m.hi[2] - m.lo[2]);
+    };
+    auto cand_index = [&](const Row& m, uint32_t q) -> uint32_t {
+        if (m.hi[1] == m.lo[1] && m.hi[2] == m.lo[2]) return m.lo[0] + q;
+        const uint32_t c0 = m.hi[0] - m.lo[0], c1 = m.hi[1] - m.lo[1];
+        return q < c0 ? m.lo[0] + q : (q < c0 + c1 ? m.lo[1] + (q - c0) : m.lo[2] + (q - c0 - c1));
+    };
+    auto load_batch = [&](const Row& m, uint32_t nc, uint32_t q0, RdT (&dst)[4]) {
+        if (m.flag == 1 && m.heavy < 0 && q0 < nc) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t q = q0 + lane + 64 * u;
+                dst[u] = rd_load(cand_index(m, q < nc ? q : nc - 1));
+            }
+        }
+    };
+    // bin of slice position x (0 <= x < L): x / bs through a float reciprocal, corrected
+    auto bin_of = [&](int32_t x, int32_t bs, float rb) -> int32_t {
+        int32_t kb = (int32_t)((float)x * rb);
+        kb -= kb * bs > x ? 1 : 0;
+        kb += (kb + 1) * bs <= x ? 1 : 0;
+        return kb;
+    };
+    auto add_read = [&](const Row& m, int2 rd, float rb) {
+        if (rd.y < m.gps || rd.x > m.gpe) return;
+        const int32_t x0 = max(rd.x, m.gps), x1 = min(rd.y, m.gpe);
+        const int32_t u = m.rev ? m.k - x1 : x0 + m.k;
+        const int32_t v = m.rev ? m.k - x0 : x1 + m.k;
+        const int32_t ku = bin_of(u, m.bs, rb), kv = bin_of(v, m.bs, rb);
+        if (ku == kv) {
+            atomicAdd(&D[ku], v - u + 1);
+        } else {
+            atomicAdd(&D[ku], m.bs * (ku + 1) - u);
+            atomicAdd(&D[kv], v - m.bs * kv + 1);
+            if (kv > ku + 1) {
+                atomicAdd(&F[ku + 1], 1);
+                atomicAdd(&F[kv], -1);
+            }
+        }
+    };
+    // my rows of the tile: wave, wave + 4, wave + 8, wave + 12
+    constexpr int kMine = kTile / kBDWaves;
+    RdT bufA[4], bufB[4];
+    Row cur = row_of(row0 + wave);
+    load_batch(cur, n_cand(cur), 0, bufA);
+#pragma unroll
+    for (int j = 0; j < kMine; ++j) {
+        const int i = wave + kBDWaves * j;  // tile row
+        RdT (&c)[4] = (j & 1) ? bufB : bufA;
+        RdT (&nx)[4] = (j & 1) ? bufA : bufB;
+        Row nxt{};
+        nxt.flag = -1;
+        if (j + 1 < kMine) {
+            nxt = row_of(row0 + i + kBDWaves);
+            load_batch(nxt, n_cand(nxt), 0, nx);
+        }
+        const Row m = cur;
+        if (lane == 0) rbs[i] = m.flag == 1 ? m.bs : (m.flag == 0 ? 0 : -1);
+        if (m.flag == 1) {
+            const float rb = 1.0f / (float)m.bs;
+            if (m.heavy >= 0) {
+                // skewed row: its position difference array was piled up by
+                // rcp_heavy_pileup_kernel; depth by a wave scan, summed into D per position
+                const int32_t* g = P.heavy_gdiff + (size_t)m.heavy * P.heavy_stride;
+                int32_t carry = 0;
+                for (int q = lane; q < m.head; q += 64) carry += g[q];
+                carry = wave_sum(carry);
+                for (int32_t b0 = 0; b0 < m.L; b0 += 64) {
+                    const int32_t x = b0 + lane;
+                    const int32_t gv = x < m.L ? g[m.head + x] : 0;
+                    const int32_t incl = (int32_t)wave_inclusive_scan((uint32_t)gv);
+                    const int32_t depth = carry + incl;
+                    carry += __builtin_amdgcn_readlane(incl, 63);
+                    if (x < m.L && depth) atomicAdd(&D[bin_of(x, m.bs, rb)], depth);
+                }
+            } else {
+                const uint32_t nc = n_cand(m);
+                for (uint32_t q0 = 0; q0 < nc; q0 += 256) {
+                    RdT nb[4];
+                    load_batch(m, nc, q0 + 256, nb);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (q0 + lane + 64u * u < nc) add_read(m, rd_pair(c[u]), rb);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) c[u] = nb[u];
+                }
+            }
+            lds_order();
+            // numerators: D[k] + bs * prefix(F)[k]; lane t takes bins [t per, (t + 1) per)
+            const int per = (n + 63) >> 6;
+            const int k0 = lane * per;
+            int32_t fs = 0;
+            for (int q = 0; q < per; ++q) fs += k0 + q < n ? F[k0 + q] : 0;
+            int32_t run = (int32_t)wave_exclusive_scan((uint32_t)fs);
+            uint32_t* srow = stage + i * RS;
+            for (int q = 0; q < per; ++q) {
+                const int k = k0 + q;
+                if (k < n) {
+                    run += F[k];
+                    srow[k] = (uint32_t)(D[k] + m.bs * run);
+                    D[k] = 0;
+                    F[k] = 0;
+                }
+            }
+            lds_order();
+        }
+        cur = nxt;
+    }
+    lds_barrier();
+    // ---- the tile's 16 rows, column-major: thread (row ii, column group cg) stores columns cg,
+    // cg + 16, ...; the 16 lanes of a column write its 128-B line of the tile
+    const int ii = tid & (kTile - 1), cg = tid >> 4;
+    const int r = row0 + ii;
+    if (r >= P.n_rows) return;
+    const int32_t bs = rbs[ii];
+    if (bs < 0) return;
+    const size_t R = (size_t)P.out_ld;
+    const double sc = P.scale;
+    const double dd = (double)max(bs, 1), rdd = 1.0 / dd;
+    const bool pow2 = bs > 0 && (bs & (bs - 1)) == 0;
+    const uint32_t* srow = stage + ii * RS;
+    for (int32_t k = cg; k < n; k += 16) {
+        const size_t o = (size_t)(part.col_off + k) * R + (size_t)r;
+        const uint32_t num = bs > 0 ? srow[k] : 0u;
+        const double x = bs == 0 ? 0.0 : (pow2 ? ((double)num * sc) * rdd : rcp_div_rn((double)num * sc, dd, rdd));
+        out_store(x, out + o);
+        if (binsum) binsum[o] = (int64_t)num;
+    }
+}
+
+static hipError_t launch_pileup_bins(const RcpPlanDev* P, double* out, int64_t* binsum, hipStream_t stream) {
+    const int nt = (P->n_rows + kTile - 1) / kTile;
+    const unsigned grid = (unsigned)(((nt + 7) / 8) * 8);
+    const size_t lds = rcp_pileup_bins_lds_bytes(P);
+    if (P->st) {
+        hipLaunchKernelGGL(rcp_pileup_bins_kernel<true>, dim3(grid), dim3(64 * kBDWaves), lds, stream, *P, out, binsum);
+    } else {
+        hipLaunchKernelGGL(rcp_pileup_bins_kernel<false>, dim3(grid), dim3(64 * kBDWaves), lds, stream, *P, out, binsum);
+    }
+    return hipGetLastError();
+}
+
+// =================================================================================
 // interpolation rows (length(x) < n): spline "fmm", neighborhood, "inear" no-op
 // =================================================================================
 #include "rcp_splitvector.h"
@@ -2972,6 +3233,7 @@ extern "C" hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_
                                         hipStream_t stream) {
     if (P->n_rows == 0) return hipSuccess;
     if (!csr && P->lean == 3 && P->stat == 0) return launch_pileup_rows(P, out, binsum, stream);
+    if (!csr && P->lean == 4 && P->stat == 0) return launch_pileup_bins(P, out, binsum, stream);
     const size_t lds = rcp_pileup_lds_bytes(P, csr);
     if (!csr && (P->lean == 1 || P->lean == 2) && P->stat == 0 && !binsum) return launch_pileup_lean(P, out, stream);
     if (csr) return launch_pileup_t<false, true>(P, out, binsum, lds, stream);

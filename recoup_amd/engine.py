@@ -20,7 +20,7 @@ STRAND = {"+": 0, "-": 1, "*": 2}
 STAT = {"mean": 0, "median": 1}
 INTERP = {"auto": 0, "spline": 1, "linear": 2, "neighborhood": 3}
 RNG = {"Rejection": 0, "Rounding": 1}
-KERNEL = {"auto": 0, "general": 1, "lean_any": 2, "rows": 3, "lean": 4}
+KERNEL = {"auto": 0, "general": 1, "lean_any": 2, "rows": 3, "lean": 4, "bins": 5}
 
 
 def _stream(device, stream):

@@ -59,7 +59,7 @@ struct RcpRowRec {
 #define RCP_REC_VALID 1
 #define RCP_REC_FAST 2
 #define RCP_REC_CRANGE 4  // crange holds this row's per-chunk read ranges
-#define RCP_MAX_CRANGE_CHUNKS 8
+#define RCP_MAX_CRANGE_CHUNKS 16
 
 struct RcpPart {
     // slice [lo, hi) of the row (0-based): lo = (lo_end ? nr : 0) + lo_off, same for hi

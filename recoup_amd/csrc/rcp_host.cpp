@@ -36,6 +36,15 @@
 #define RCP_LEAN_ITEMS_PER_WG 0
 #endif
 constexpr int kLeanItemsPerWg = RCP_LEAN_ITEMS_PER_WG;  // work items per persistent workgroup, at least
+// Per-base plans (C5's TSS windows: reads piled in the window's middle, so the middle column
+// chunks are several times the outer ones' work) on few row tiles -- one GPU's shard -- take at
+// least this many work items per workgroup: narrower chunks let the per-XCD claims balance the
+// heavy middle items against the light outer ones (with ~1.5 items per workgroup the pass lasts
+// as long as the slowest workgroup's heavy items)
+#ifndef RCP_LEAN_ITEMS_PER_WG_BASE
+#define RCP_LEAN_ITEMS_PER_WG_BASE 4
+#endif
+constexpr int kLeanItemsPerWgBase = RCP_LEAN_ITEMS_PER_WG_BASE;
 constexpr int kLeanMinChunkBins = 64;                   // no column chunks narrower than this
 // AUTO keeps binned plans of fewer rows on the general kernel: a lean item is 64 rows, the
 // general kernel's workgroup 32, and with about one item per workgroup the item's read round
@@ -1316,8 +1325,8 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
                 P.n_chunks_total += pt.n_chunks;
             }
         };
-        while (can_split() && (tiles * P.n_chunks_total < kLeanItemsPerWg * grid ||
-                               P.n_chunks_total < opts->min_col_chunks))
+        const int64_t want = (P.lean_rounds == 2 ? kLeanItemsPerWgBase : kLeanItemsPerWg) * grid;
+        while (can_split() && (tiles * P.n_chunks_total < want || P.n_chunks_total < opts->min_col_chunks))
             split();
         P.stage_cap = 1;
         for (int p = 0; p < P.n_parts; ++p) P.stage_cap = std::max(P.stage_cap, P.part[p].chunk_bins);

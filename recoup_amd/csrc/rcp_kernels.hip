@@ -726,13 +726,19 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
             }
         }
     }
+    // bisection down to RCP_LOC_LIN keys, then one pass that loads them all at once and counts
+    // those below the threshold (one round trip instead of log2 RCP_LOC_LIN dependent ones)
+#ifndef RCP_LOC_LIN
+#define RCP_LOC_LIN 16
+#endif
+    constexpr uint32_t kLin = RCP_LOC_LIN;
     while (!(RCP_LOC_ABL & 2)) {
         uint32_t m[K];
         int32_t kv[K];
         bool any = false;
 #pragma unroll
         for (int u = 0; u < K; ++u) {
-            if (lo[u] < hi[u]) {
+            if (lo[u] < hi[u] && hi[u] - lo[u] > kLin) {
                 m[u] = lo[u] + ((hi[u] - lo[u]) >> 1);
                 kv[u] = up[u] ? se[(size_t)m[u] << 1] : P.pmax[m[u]];
                 any = true;
@@ -741,8 +747,31 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
         if (!any) break;
 #pragma unroll
         for (int u = 0; u < K; ++u) {
-            if (lo[u] < hi[u]) {
+            if (lo[u] < hi[u] && hi[u] - lo[u] > kLin) {
                 if ((int64_t)kv[u] < thr[u]) lo[u] = m[u] + 1; else hi[u] = m[u];
+            }
+        }
+    }
+    if (kLin > 0 && !(RCP_LOC_ABL & 2)) {
+        int32_t kv[K][kLin > 0 ? kLin : 1];
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            if (lo[u] < hi[u]) {
+#pragma unroll
+                for (uint32_t i = 0; i < kLin; ++i) {
+                    const uint32_t m = min(lo[u] + i, hi[u] - 1);  // (clamped: inside the arrays)
+                    kv[u][i] = up[u] ? se[(size_t)m << 1] : P.pmax[m];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            if (lo[u] < hi[u]) {
+                const uint32_t n = hi[u] - lo[u];
+                uint32_t c = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < kLin; ++i) c += (i < n && (int64_t)kv[u][i] < thr[u]) ? 1u : 0u;
+                lo[u] += c;
             }
         }
     }
@@ -850,7 +879,7 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
         maxpos[g] = sg.hi;
         const bool qok = ok && sg.query_ok && (sg.streams & 1);
         // the searches, tasks -2 (lower), -1 (upper), 0 .. 2 nc - 1 (chunk edges): lane q takes
-        // tasks -2 + q, -2 + q + 4, ... (up to 5 of 2 + 2 * RCP_MAX_CRANGE_CHUNKS = 18; edges at
+        // tasks -2 + q, -2 + q + 4, ... (up to 9 of 2 + 2 * RCP_MAX_CRANGE_CHUNKS = 34; edges at
         // the row's ends are skipped) and evaluates only its own chunk windows
         int32_t sx[KS] = {};
         int sdst[KS] = {};  // -2 lower, -1 upper, >= 0 xr index (its parity = upper)

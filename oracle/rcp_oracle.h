@@ -19,7 +19,7 @@
  * exists.  The oracle is pinned by (i) R's published RNG known answers
  * (set.seed(42); runif / sample), (ii) exactness properties of the fmm spline, and
  * (iii) SURVEY Appendix B sanity numbers on the reference's own fixture
- * data/recoup_test_data.rda.  See DESIGN.md "Parity pinning".
+ * data/recoup_test_data.rda.  See DESIGN.md §2.
  */
 #ifndef RCP_ORACLE_H
 #define RCP_ORACLE_H

@@ -9,7 +9,7 @@ Step 2 (expected outputs): run the CPU oracle (``oracle/``, a restatement of
 ``R/coverage.R`` + ``R/profile.R`` + ``R/util.R:15-85``) on the C1 configuration of
 ``inst/unitTests/test_recoup.R:4-26`` and write ``c1_expected.npz``.  These expected
 vectors come from the restatement, not from executed R (R is absent here, see
-DESIGN.md "Parity pinning"), so they pin the HIP path to the oracle; the oracle itself is
+DESIGN.md §2), so they pin the HIP path to the oracle; the oracle itself is
 pinned by R's published RNG known answers and the SURVEY Appendix B sanity numbers.
 
 Usage:  python tests/golden/make_fixtures.py [--inputs] [--expected]

@@ -729,7 +729,7 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
     // bisection down to RCP_LOC_LIN keys, then one pass that loads them all at once and counts
     // those below the threshold (one round trip instead of log2 RCP_LOC_LIN dependent ones)
 #ifndef RCP_LOC_LIN
-#define RCP_LOC_LIN 16
+#define RCP_LOC_LIN 0  // 16: a last linear pass over <= 16 keys (slower: profiles/r04/locate_lin_ab.log)
 #endif
     constexpr uint32_t kLin = RCP_LOC_LIN;
     while (!(RCP_LOC_ABL & 2)) {
@@ -790,9 +790,9 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
 #define RCP_LOC_WPE 1
 #endif
 
+template <int KS>  // searches of one lockstep round per lane (8: plans of > 7 column chunks, one round)
 __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres)[2 * RCP_MAX_CRANGE_CHUNKS]) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
-    constexpr int KS = 4;                  // searches of one lockstep round
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = t / LPR;
     const int q = t % LPR;
@@ -1126,10 +1126,11 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
     for (int u = 0; u < 4; ++u) dst[u] = src[u];
 }
 
+template <int KS>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RCP_LOC_WPE))) rcp_locate_kernel(RcpPlanDev P) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
     __shared__ uint32_t xres[kBlock / LPR][2 * RCP_MAX_CRANGE_CHUNKS];  // per row: chunk bounds
-    locate_rows(P, xres);
+    locate_rows<KS>(P, xres);
     // ---- the previous execution's heavy slots (its pileup kernels read them across column
     // chunks, so they are cleared here, before this execution's heavy kernel adds into them).
     // After the rows, each wave reading the count itself: no block-wide wait on that load
@@ -3141,7 +3142,15 @@ hipError_t allow_big_lds(K kernel) {
 extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream) {
     if (P->n_rows == 0) return hipSuccess;
     const int64_t grid = (4 * (int64_t)P->n_rows + kBlock - 1) / kBlock;  // four lanes per row
-    hipLaunchKernelGGL(rcp_locate_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
+    // a single-range row's searches: its two bounds + the interior chunk edges, dealt to the quad;
+    // more than 16 (over 8 column chunks) take lockstep rounds of 8 (one chain, not two)
+#ifndef RCP_LOC_KS8
+#define RCP_LOC_KS8 1
+#endif
+    if (RCP_LOC_KS8 && P->crange && 2 * P->n_chunks_total > 4 * 4)
+        hipLaunchKernelGGL(rcp_locate_kernel<8>, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
+    else
+        hipLaunchKernelGGL(rcp_locate_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
     return hipGetLastError();
 }
 

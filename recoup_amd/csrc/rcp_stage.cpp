@@ -7,12 +7,8 @@
 // devices proceed in parallel (rcp_profile_multi drives one host thread per GPU).
 #include "rcp_stage.h"
 
-#include <sys/mman.h>
-
 #include <algorithm>
 #include <condition_variable>
-#include <cstdint>
-#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -133,19 +129,6 @@ inline void part_range(size_t n, int i, size_t* a, size_t* b) {
     *b = std::min(n, *a + per);
 }
 
-// The caller's destination of a large D2H copy is usually fresh memory (R's allocVector /
-// allocMatrix of a big vector is an untouched mmap): the drain threads then pay one page fault
-// per 4 KB page.  Asking for transparent huge pages on the range's 2 MB-aligned interior (a
-// hint; THP "madvise" mode) makes that one fault per 2 MB.  RCP_NO_THP_ADVISE=1 turns it off.
-void advise_huge(void* p, size_t n) {
-    static const bool off = std::getenv("RCP_NO_THP_ADVISE") != nullptr;
-    constexpr uintptr_t kHuge = uintptr_t(2) << 20;
-    if (off || n < 4 * kHuge) return;
-    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
-    const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + n) & ~(kHuge - 1);
-    if (b > a) (void)madvise(reinterpret_cast<void*>(a), b - a, MADV_HUGEPAGE);
-}
-
 }  // namespace
 
 hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipStream_t stream) {
@@ -199,7 +182,6 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
     }
     const char* s = static_cast<const char*>(src);
     char* d = static_cast<char*>(dst);
-    advise_huge(d, dpitch * (height - 1) + width);
     // device bytes [a, z) of the linear span -> their host rows (padding bytes skipped)
     auto scatter = [&](const char* pin, size_t base, size_t a, size_t z) {
         while (a < z) {

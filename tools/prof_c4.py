@@ -1,5 +1,5 @@
 """Minimal run of one BASELINE config (c4 default; c2, c3, c5) for rocprofv3 counter passes (one plan, a few
-executes).  C3_PART=center keeps one column part of C3."""
+executes).  C3_PART=center keeps one column part of C3; SHARD=k/N one GPU's region shard (not C3)."""
 import os
 import sys
 
@@ -23,6 +23,14 @@ else:
     reg = d["regions"]
     rows = RowTable.from_ranges(reg["chrom"], reg["start"], reg["end"], reg["strand"])
     bins = Bins([("whole", d["n_bins"])]) if d["n_bins"] else Bins([("whole", 0, sum(d["flank"]))])
+if os.environ.get("SHARD"):  # one GPU's shard k/N, as bench.py --sim-shard builds it
+    import bench  # noqa: E402
+    import numpy as np  # noqa: E402
+    k, n = (int(x) for x in os.environ["SHARD"].split("/"))
+    ovl = synthetic.n_overlaps(d["reads"], reg, d["width"], device="cuda:0").astype(np.int64)
+    lo, hi, _ = bench.shard_of(rows, ovl, n, k)
+    rows = bench.subset_rows(rows, lo, hi)
+    rs = ReadSet(*bench.reads_for_rows(d["reads"], rows, len(d["seqlen"])), d["seqlen"], device=0)
 plan = Plan(rs, rows, bins, out_ld="padded")  # as bench.py
 out = plan.empty_output()
 for _ in range(int(os.environ.get("ITERS", "3"))):

@@ -151,6 +151,13 @@ struct RcpPlanDev {
     int32_t lean;               // 1: every row is one plain range with uniform power-of-two bins
                                 //    of one wave chunk -> rcp_pileup_lean_kernel
     int32_t lean_rounds;        // lean kernel: rounds of 16 rows per work item (2; else kRounds)
+    // lean kernel, heaviest items first (per-base plans of few work items, e.g. one GPU's shard):
+    // locate sums each (32-row tile, column chunk) item's candidate reads, files the item code in
+    // item_order under its class floor(log2(reads)) (counts in status[kLptClass + class]), and
+    // the lean kernel claims items from one counter, highest class first.  0: per-XCD order.
+    int32_t lpt;
+    int32_t lpt_cap;            // items per class list (>= the plan's item count)
+    int32_t* item_order;        // [RCP_LPT_CLASSES][lpt_cap]
     // row-wave kernel (lean == 3): its rows' bins go row-major into rm (n_rows x n_cols, whole
     // lines per row); the last wave to finish a 16-row tile writes the tile's rows of every
     // column into the R column-major output as whole 128-B lines (a row-wave store straight
@@ -189,6 +196,8 @@ struct RcpPlanDev {
     uint32_t* status_prev;
 };
 #define RCP_STATUS_WORDS 32
+#define RCP_LPT_CLASSES 15      // item classes by log2 of their candidate reads (status words 17 ..)
+#define RCP_LPT_STATUS 17
 
 __host__ __device__ inline void rcp_part_slice(const RcpPart& p, int32_t nr, int32_t* lo, int32_t* len) {
     *lo = (p.lo_end ? nr : 0) + p.lo_off;

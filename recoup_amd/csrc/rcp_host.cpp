@@ -67,6 +67,10 @@ constexpr int kLeanMinRowsBinned = RCP_LEAN_MIN_ROWS_BINNED;
 #define RCP_AUTO_GEN 0  // 1: AUTO also takes the lean kernel's general-bins mode (A/B only)
 #endif
 
+#ifndef RCP_LEAN_LPT
+#define RCP_LEAN_LPT 1  // per-base lean plans of few items claim the heaviest items first (0: per-XCD order)
+#endif
+
 #ifndef RCP_BINS_AUTO
 #define RCP_BINS_AUTO 1  // plans of one binned part with uniform bins of >= 4 positions take the bin-difference kernel
 #endif
@@ -1414,7 +1418,20 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     const size_t w_rec = al(w_gdiff + (P.heavy_threshold > 0 ? 4 * (size_t)P.heavy_cap * P.heavy_stride : 0));
     const bool keep_crange = P.n_chunks_total > 1 && P.n_chunks_total <= RCP_MAX_CRANGE_CHUNKS;
     const size_t w_crange = al(w_rec + sizeof(RcpRowRec) * Rw);
-    const size_t w_status = al(w_crange + (keep_crange ? sizeof(uint2) * 3 * (size_t)P.n_chunks_total * Rw : 0));
+    // heaviest-first lean items (rcp_device.h lpt): per-base lean plans of few 32-row items,
+    // i.e. one GPU's shard of a per-base table (C5 1/8: TSS windows' middle column chunks hold
+    // several times the outer chunks' reads; in per-XCD order a workgroup that drew two heavy
+    // items sets the pass)
+    const int64_t lpt_items = ((int64_t)R + 31) / 32 * P.n_chunks_total;
+    int lpt_cus = 256;
+    if (hipDeviceGetAttribute(&lpt_cus, hipDeviceAttributeMultiprocessorCount, rs->device) != hipSuccess || lpt_cus <= 0)
+        lpt_cus = 256;
+    // (a full per-base table, e.g. C5's 6256 items, keeps the per-XCD order and its L2 locality)
+    P.lpt = RCP_LEAN_LPT && P.lean == 1 && P.lean_rounds == 2 && keep_crange && R > 0 &&
+            lpt_items <= (int64_t)kLeanItemsPerWgBase * 2 * lpt_cus;
+    P.lpt_cap = P.lpt ? (int32_t)lpt_items : 0;
+    const size_t w_order = al(w_crange + (keep_crange ? sizeof(uint2) * 3 * (size_t)P.n_chunks_total * Rw : 0));
+    const size_t w_status = al(w_order + 4 * (size_t)RCP_LPT_CLASSES * (size_t)P.lpt_cap);
     static_assert(2 * RCP_STATUS_WORDS * 4 <= 256, "two status sets");
     HIP_TRY(plan->work.alloc(w_status + 256));
     PLAN_MARK("work alloc");
@@ -1426,6 +1443,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.heavy_gdiff = reinterpret_cast<int32_t*>(wb + w_gdiff);
     P.rec = reinterpret_cast<RcpRowRec*>(wb + w_rec);
     P.crange = keep_crange ? reinterpret_cast<uint2*>(wb + w_crange) : nullptr;
+    P.item_order = P.lpt ? reinterpret_cast<int32_t*>(wb + w_order) : nullptr;
     // the locate kernel's chunk windows for the rows of the first row's length (all rows of
     // C2 / C4 / C5), when no part of that length has an R-RNG layout: the same arithmetic as
     // the kernel's chunk_window, once per plan instead of once per (row, chunk)

@@ -791,7 +791,8 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
 #endif
 
 template <int KS>  // searches of one lockstep round per lane (8: plans of > 7 column chunks, one round)
-__device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres)[2 * RCP_MAX_CRANGE_CHUNKS]) {
+__device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres)[2 * RCP_MAX_CRANGE_CHUNKS],
+                                            uint32_t (*item_w)[RCP_MAX_CRANGE_CHUNKS]) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = t / LPR;
@@ -1081,6 +1082,7 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
             // merged layout: one stream, so dense (row, chunk) words -- a wave's writes are
             // whole lines (stride 3, as the stranded layout below, measured ~1 us slower on C4)
             if (!(RCP_LOC_ABL & 4)) P.crange[(size_t)r * nc + c] = make_uint2(clo, chi);
+            if (item_w && chi > clo) atomicAdd(&item_w[(threadIdx.x / LPR) >> 5][c], chi - clo);
         }
     } else if (cr && q < 3) {
         // stranded layout: lane q refines its own stream's range chunk by chunk
@@ -1096,6 +1098,7 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
                 chi = clo;
             }
             P.crange[((size_t)r * nc + c) * 3 + q] = make_uint2(clo, chi);
+            if (item_w && chi > clo) atomicAdd(&item_w[(threadIdx.x / LPR) >> 5][c], chi - clo);
         }
     }
     if (!in_row || q != 0) return;
@@ -1130,7 +1133,25 @@ template <int KS>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RCP_LOC_WPE))) rcp_locate_kernel(RcpPlanDev P) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
     __shared__ uint32_t xres[kBlock / LPR][2 * RCP_MAX_CRANGE_CHUNKS];  // per row: chunk bounds
-    locate_rows<KS>(P, xres);
+    // heaviest-first lean items (P.lpt): this block's 64 rows are two 32-row tiles; their
+    // items' candidate reads are summed here and filed by class after the rows
+    __shared__ uint32_t item_w[2][RCP_MAX_CRANGE_CHUNKS];
+    if (P.lpt && threadIdx.x < 2 * RCP_MAX_CRANGE_CHUNKS) item_w[threadIdx.x >> 4][threadIdx.x & 15] = 0u;
+    if (P.lpt) __syncthreads();
+    locate_rows<KS>(P, xres, P.lpt ? item_w : nullptr);
+    if (P.lpt) {
+        __syncthreads();
+        const int nc = P.n_chunks_total;
+        const int t = threadIdx.x;
+        const int tile = blockIdx.x * 2 + t / max(nc, 1);
+        const int n_tiles = (P.n_rows + 31) / 32;
+        if (t < 2 * nc && tile < n_tiles) {
+            const uint32_t w = item_w[t / nc][t % nc];
+            const int cls = w ? min(RCP_LPT_CLASSES - 1, 31 - __clz(w)) : 0;
+            const uint32_t slot = atomicAdd(&P.status[RCP_LPT_STATUS + cls], 1u);
+            if (slot < (uint32_t)P.lpt_cap) P.item_order[cls * P.lpt_cap + slot] = tile * nc + t % nc;
+        }
+    }
     // ---- the previous execution's heavy slots (its pileup kernels read them across column
     // chunks, so they are cleared here, before this execution's heavy kernel adds into them).
     // After the rows, each wave reading the count itself: no block-wide wait on that load
@@ -2411,17 +2432,34 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     auto claim = [&](int buf) {
         uint32_t j = 0;
         int xs = xcd;
-        if (lane == 0) j = atomicAdd(&P.status[8 + xcd], 1u);
-        j = __builtin_amdgcn_readfirstlane(j);
-        for (int k = 1; k < 8 && j >= n_items_of(xs); ++k) {
-            xs = (xcd + k) & 7;
-            if (lane == 0) j = atomicAdd(&P.status[8 + xs], 1u);
-            j = __builtin_amdgcn_readfirstlane(j);
-        }
         int code = -1;
-        if (j < n_items_of(xs)) {
-            const int tl = (int)(j / P.n_chunks_total);
-            code = (tl * 8 + xs) * P.n_chunks_total + (int)(j - (uint32_t)tl * P.n_chunks_total);
+        if (P.lpt) {
+            // heaviest first: one counter over the class lists, highest class first
+            if (lane == 0) j = atomicAdd(&P.status[8], 1u);
+            j = __builtin_amdgcn_readfirstlane(j);
+            for (int c = RCP_LPT_CLASSES - 1; c >= 0; --c) {
+                const uint32_t n = min(__builtin_amdgcn_readfirstlane(P.status[RCP_LPT_STATUS + c]),
+                                       (uint32_t)P.lpt_cap);
+                if (j < n) {
+                    code = __builtin_amdgcn_readfirstlane(P.item_order[c * P.lpt_cap + j]);
+                    break;
+                }
+                j -= n;
+            }
+        } else {
+            if (lane == 0) j = atomicAdd(&P.status[8 + xcd], 1u);
+            j = __builtin_amdgcn_readfirstlane(j);
+            for (int k = 1; k < 8 && j >= n_items_of(xs); ++k) {
+                xs = (xcd + k) & 7;
+                if (lane == 0) j = atomicAdd(&P.status[8 + xs], 1u);
+                j = __builtin_amdgcn_readfirstlane(j);
+            }
+            if (j < n_items_of(xs)) {
+                const int tl = (int)(j / P.n_chunks_total);
+                code = (tl * 8 + xs) * P.n_chunks_total + (int)(j - (uint32_t)tl * P.n_chunks_total);
+            }
+        }
+        if (code >= 0) {
             const LeanItem it = lean_item(P, code);
             if (lane < kIRows)
                 lmeta[buf * kRows + lane] =

@@ -1,11 +1,11 @@
 #!/bin/bash
-# round 4: GPU tests; A/B of new (lockstep rounds of 8 for > 8 chunks) vs ks4 on the shards
+# round 4: GPU tests; A/B of new (heaviest-first lean items, lockstep rounds of 8 for > 8 chunks) vs nolpt / ks4 on the shards
 OUT=gpurun_out/r4h
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/tests.log 2>&1 || { tail -60 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
-for v in new ks4 new ks4; do
+for v in new nolpt ks4 new nolpt; do
   lib=build_var/$v/librecoup_amd.so
   [ $v = new ] && lib=recoup_amd/librecoup_amd.so
   echo "== $v" >> $OUT/ab.log

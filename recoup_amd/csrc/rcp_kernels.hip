@@ -1468,6 +1468,13 @@ __device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart
 #pragma unroll
             for (int q = 0; q < 4; ++q) dst[q] = src[q];
         }
+        // the merged layout's chunk range: its address does not depend on the record, so it is
+        // loaded with it (one round trip, not two); used only when the record says CRANGE
+#ifndef RCP_DECODE_PRE
+#define RCP_DECODE_PRE 1
+#endif
+        uint2 cr_pre = make_uint2(0u, 0u);
+        if (RCP_DECODE_PRE && P.crange && P.merged) cr_pre = P.crange[(size_t)r * P.n_chunks_total + cidx];
         int32_t head, L;
         rcp_part_slice(part, rec.row_len, &head, &L);
         const int32_t n = CSR ? L : part.n_bins;
@@ -1527,7 +1534,7 @@ __device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart
                     if (rec.flags & RCP_REC_CRANGE) {
                         // exact ranges for this chunk from the locate kernel
                         if (P.merged) {  // one stream: dense (row, chunk) words
-                            const uint2 v = P.crange[(size_t)r * P.n_chunks_total + cidx];
+                            const uint2 v = RCP_DECODE_PRE ? cr_pre : P.crange[(size_t)r * P.n_chunks_total + cidx];
                             m.lo[0] = v.x;
                             m.hi[0] = v.y;
                             m.lo[1] = m.hi[1] = m.lo[2] = m.hi[2] = 0;
@@ -2800,7 +2807,11 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 // piles 4 of the rows into its own D / F arrays and stages their numerators; the workgroup
 // then writes the tile column-major.
 // =================================================================================
-constexpr int kBDWaves = 4;
+#ifndef RCP_BD_WAVES
+#define RCP_BD_WAVES 4  // waves per 16-row tile (16 / RCP_BD_WAVES rows each)
+#endif
+constexpr int kBDWaves = RCP_BD_WAVES;
+static_assert(kTile % kBDWaves == 0, "a tile's rows are split evenly over the waves");
 constexpr int kBDMaxBins = 512;
 constexpr int kBDMinWidth = 4;
 extern "C" int rcp_bins_max_bins(void) { return kBDMaxBins; }
@@ -2944,7 +2955,7 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             }
         }
     };
-    // my rows of the tile: wave, wave + 4, wave + 8, wave + 12
+    // my rows of the tile: wave, wave + kBDWaves, ...
     constexpr int kMine = kTile / kBDWaves;
     RdT bufA[4], bufB[4];
     Row cur = row_of(row0 + wave);
@@ -3014,7 +3025,8 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     }
     lds_barrier();
     // ---- the tile's 16 rows, column-major: thread (row ii, column group cg) stores columns cg,
-    // cg + 16, ...; the 16 lanes of a column write its 128-B line of the tile
+    // cg + kCG, ...; the 16 lanes of a column write its 128-B line of the tile
+    constexpr int kCG = 64 * kBDWaves / kTile;
     const int ii = tid & (kTile - 1), cg = tid >> 4;
     const int r = row0 + ii;
     if (r >= P.n_rows) return;
@@ -3025,7 +3037,7 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     const double dd = (double)max(bs, 1), rdd = 1.0 / dd;
     const bool pow2 = bs > 0 && (bs & (bs - 1)) == 0;
     const uint32_t* srow = stage + ii * RS;
-    for (int32_t k = cg; k < n; k += 16) {
+    for (int32_t k = cg; k < n; k += kCG) {
         const size_t o = (size_t)(part.col_off + k) * R + (size_t)r;
         const uint32_t num = bs > 0 ? srow[k] : 0u;
         const double x = bs == 0 ? 0.0 : (pow2 ? ((double)num * sc) * rdd : rcp_div_rn((double)num * sc, dd, rdd));

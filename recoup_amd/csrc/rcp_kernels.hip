@@ -2253,6 +2253,9 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
 #ifndef RCP_LWPE
 #define RCP_LWPE 6
 #endif
+#ifndef RCP_LRING3
+#define RCP_LRING3 0  // 1: two batches of reads in flight ahead of the one being added (lean kernel)
+#endif
 #ifndef RCP_LBATCH_UNI
 #define RCP_LBATCH_UNI 4  // reads per lane per batch of a start-only (uniform-width) lean plan
 #endif
@@ -2596,12 +2599,29 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                             if (q0 + lane + 64u * u < n) lean_add<false>(m, rd_pair(src[u]), diff, sh);
                     }
                 };
-                for (uint32_t q0 = 0; q0 < n; q0 += BQ) {
-                    RdT nx[BL];
-                    load_batch(q0 + BQ, nx);
-                    add_batch(q0, cur);
+                if (RCP_LRING3) {
+                    // three buffers in rotation (no register copies, so each add waits only for
+                    // its own batch): two batches in flight while one is added
+                    RdT b1[BL], b2[BL];
+                    load_batch(BQ, b1);
+                    for (uint32_t q0 = 0; q0 < n; q0 += 3 * BQ) {
+                        load_batch(q0 + 2 * BQ, b2);
+                        add_batch(q0, cur);
+                        if (q0 + BQ >= n) break;
+                        load_batch(q0 + 3 * BQ, cur);
+                        add_batch(q0 + BQ, b1);
+                        if (q0 + 2 * BQ >= n) break;
+                        load_batch(q0 + 4 * BQ, b1);
+                        add_batch(q0 + 2 * BQ, b2);
+                    }
+                } else {
+                    for (uint32_t q0 = 0; q0 < n; q0 += BQ) {
+                        RdT nx[BL];
+                        load_batch(q0 + BQ, nx);
+                        add_batch(q0, cur);
 #pragma unroll
-                    for (int u = 0; u < BL; ++u) cur[u] = nx[u];
+                        for (int u = 0; u < BL; ++u) cur[u] = nx[u];
+                    }
                 }
             }
             lds_order();

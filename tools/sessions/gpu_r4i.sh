@@ -15,6 +15,15 @@ for v in new nopre l1 l2 l4 l8; do
     RCP_LIB_PATH=$lib CFG=$1 timeout -k 10 200 python3 tools/diag_shard_kernels.py $2 auto >> $OUT/ab.log 2>&1 || { tail $OUT/ab.log; exit 1; }
   done
 done
+for v in ring3 ring3b8; do
+  RCP_LIB_PATH=build_var/$v/librecoup_amd.so timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_lean.py > $OUT/lean_$v.log 2>&1 || { tail -30 $OUT/lean_$v.log; exit 1; }
+  tail -1 $OUT/lean_$v.log
+  echo "== $v" >> $OUT/ab.log
+  for spec in "c5 0/8" "c5 0/1" "c4 0/1"; do
+    set -- $spec
+    RCP_LIB_PATH=build_var/$v/librecoup_amd.so CFG=$1 timeout -k 10 200 python3 tools/diag_shard_kernels.py $2 auto >> $OUT/ab.log 2>&1 || { tail $OUT/ab.log; exit 1; }
+  done
+done
 for v in bd8 bd16; do
   RCP_LIB_PATH=build_var/$v/librecoup_amd.so timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_bins.py > $OUT/bins_$v.log 2>&1 || { tail -30 $OUT/bins_$v.log; exit 1; }
   tail -1 $OUT/bins_$v.log

@@ -162,7 +162,10 @@ struct RcpPlanDev {
     // lines per row); the last wave to finish a 16-row tile writes the tile's rows of every
     // column into the R column-major output as whole 128-B lines (a row-wave store straight
     // into the column-major matrix is 8 bytes per 128-B line)
-    double* rm;                 // nullptr: direct column-major stores
+    double* rm;                 // nullptr: direct column-major stores (or rows_lds)
+    // rows_lds > 0: the tiles' bin numerators are staged in LDS instead (rows_lds = the stage's
+    // row stride in words, == 4 mod 64); the flush divides them as the pile would have
+    int32_t rows_lds;
     // coverage (CSR) mode
     const int64_t* csr_off;     // non-null: write per-row depth into csr (calcCoverage)
     int32_t* csr_out;

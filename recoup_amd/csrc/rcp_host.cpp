@@ -78,6 +78,9 @@ constexpr int kLeanMinRowsBinned = RCP_LEAN_MIN_ROWS_BINNED;
 #ifndef RCP_ROWS_AUTO
 #define RCP_ROWS_AUTO 1  // plans with multi-range rows take the row-wave pileup kernel
 #endif
+#ifndef RCP_ROWS_LDS
+#define RCP_ROWS_LDS 1   // row-wave plans stage their tiles in LDS when 16 rows of bins fit
+#endif
 
 extern "C" {
 hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
@@ -100,7 +103,9 @@ void rcp_tile_geometry(int* tile, int* rounds_max);
 int rcp_lean_max_bins(void);
 int rcp_lean_gen_max_bins(void);
 size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
-size_t rcp_pileup_rows_lds_bytes(void);
+size_t rcp_pileup_rows_lds_bytes(const RcpPlanDev* P);
+int rcp_rows_lds_stride(int64_t n_cols);
+int rcp_rows_lds_window_cap(void);
 size_t rcp_pileup_bins_lds_bytes(const RcpPlanDev* P);
 int rcp_bins_max_bins(void);
 int rcp_bins_min_width(void);
@@ -1270,6 +1275,15 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         for (int r = 0; !multi_rows && r < R; ++r) multi_rows = B.row_seg[r + 1] - B.row_seg[r] > 1;
         if (rows_ok && (kind == RCP_KERNEL_ROWS || (kind == RCP_KERNEL_AUTO && multi_rows && RCP_ROWS_AUTO)))
             P.lean = 3;
+        // its tiles' numerators in LDS (no row-major staging round trip through L2 / HBM) when
+        // two slots of 16 rows fit beside the waves' windows
+        P.rows_lds = 0;
+        if (P.lean == 3 && RCP_ROWS_LDS) {
+            bool fit = true;
+            for (int p = 0; p < P.n_parts; ++p)
+                if (!P.part[p].per_base && part_max_bin[p] > rcp_rows_lds_window_cap()) fit = false;
+            if (fit) P.rows_lds = rcp_rows_lds_stride(P.n_cols);
+        }
     }
     // ---- bin-difference kernel (lean == 4): mean plans of one binned part whose rows are
     // single ranges, every row's slice a whole number of bins of >= rcp_bins_min_width()
@@ -1530,12 +1544,12 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.csr_runs = nullptr;
     // row-wave plans stage their bins row-major (whole lines per row) and transpose once
     P.rm = nullptr;
-    if (P.lean == 3 && R > 0 && P.n_cols > 0) {
+    if (P.lean == 3 && P.rows_lds == 0 && R > 0 && P.n_cols > 0) {
         HIP_TRY(plan->rm.alloc(8 * (size_t)R * (size_t)P.n_cols));
         P.rm = plan->rm.as<double>();
     }
     plan->lds = P.lean == 4 ? rcp_pileup_bins_lds_bytes(&P)
-                : P.lean == 3 ? rcp_pileup_rows_lds_bytes()
+                : P.lean == 3 ? rcp_pileup_rows_lds_bytes(&P)
                               : (P.lean ? rcp_pileup_lean_lds_bytes(&P) : rcp_pileup_lds_bytes(&P, cov_only ? 1 : 0));
     // general kernel: 2 rounds (32 rows) per workgroup (C3: 0.88 ms vs 0.91 with 4 rounds, 0.89
     // with 1), 1 when the row table is small, so that the grid still holds two workgroups per

@@ -1923,22 +1923,66 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
 // ---------------------------------------------------------------------------------
 constexpr int kRWaves = 4;                       // waves per workgroup (independent)
 constexpr int kRWSh = 5;                         // 32 positions per lane at most
-constexpr int kRWCap = 64 * (1 << kRWSh) - 1;    // positions per window (+1 sentinel)
-constexpr int kRWWords = 8 + 64 * ((1 << kRWSh) + 4);  // per wave: 8 zero words + padded array
+template <int SH>
+struct RowWin {
+    static constexpr int cap = 64 * (1 << SH) - 1;          // positions per window (+1 sentinel)
+    static constexpr int words = 8 + 64 * ((1 << SH) + 4);  // per wave: 8 zero words + padded array
+};
+constexpr int kRWCap = RowWin<kRWSh>::cap;
+// LDS-staged variant (P.rows_lds): one workgroup of RCP_RWL_WAVES waves per CU whose tiles'
+// bin numerators (uint32, 16 rows x n_cols) sit in RCP_RWL_SLOTS LDS slots
+#ifndef RCP_RWL_WAVES
+#define RCP_RWL_WAVES 8
+#endif
+#ifndef RCP_RWL_SH
+#define RCP_RWL_SH 5
+#endif
+#ifndef RCP_RWL_SLOTS
+#define RCP_RWL_SLOTS 2
+#endif
+constexpr int kRLWaves = RCP_RWL_WAVES, kRLSh = RCP_RWL_SH, kRLSlots = RCP_RWL_SLOTS;
+constexpr size_t kRowsQueueBytes = 64;  // tile queue word + slot table
 
 extern "C" int rcp_rows_window_cap(void) { return kRWCap; }
+extern "C" int rcp_rows_lds_window_cap(void) { return RowWin<kRLSh>::cap; }
+
+static size_t rows_lds_bytes(int lds_stride, int waves, int words, int slots) {
+    return 4 * (size_t)waves * words + kRowsQueueBytes +
+           (size_t)slots * kTile * (4 * (size_t)lds_stride + 8 * RCP_MAX_PARTS);
+}
+
+// Row stride (words) of the LDS stage for n_cols columns, == 4 mod 64 so that the flush's 64
+// lanes (16 rows x 4 columns) hit 64 distinct banks; 0 when the stage does not fit.
+extern "C" int rcp_rows_lds_stride(int64_t n_cols) {
+    if (n_cols <= 0 || n_cols > (1 << 20)) return 0;
+    const int64_t ldw = n_cols <= 4 ? 4 : (n_cols - 4 + 63) / 64 * 64 + 4;
+    return rows_lds_bytes((int)ldw, kRLWaves, RowWin<kRLSh>::words, kRLSlots) <= 160 * 1024 ? (int)ldw : 0;
+}
 
 // Stores of a row's bins: row-major into the staging (P.rm, whole lines per row), or -- with
 // binsum, which keeps the column-major layout -- 8 bytes per 128-B column line; the 16 rows of a
 // line are claimed together by waves of one XCD, so plain stores meet in that L2.
 __device__ __forceinline__ void rows_store(double x, double* p) { *p = x; }
 
-__global__ void __launch_bounds__(64 * kRWaves) __attribute__((amdgpu_waves_per_eu(4)))
+// a bin's mean from its numerator: the same operations in the same order wherever it is made
+// (pile or LDS flush), so the same bits
+__device__ __forceinline__ double rows_mean(uint32_t num, double sc, bool pow2, int32_t w, int32_t bs, double dd,
+                                            double rdd, double dd1, double rdd1) {
+    if (pow2) return ((double)num * sc) * rdd;
+    if (w == bs) return rcp_div_rn((double)num * sc, dd, rdd);
+    return rcp_div_rn((double)num * sc, dd1, rdd1);  // w == bs + 1
+}
+
+// LDS = 1: bins staged in LDS (P.rows_lds, never with binsum); LDS = 0: P.rm staging or, with
+// binsum / no P.rm, direct column-major stores
+template <int LDS, int WAVES, int SH>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(16 / WAVES)))
 rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restrict__ binsum) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int kWinCap = RowWin<SH>::cap, kWords = RowWin<SH>::words;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * kRWWords + 8;
+    int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * kWords + 8;
     if (lane < 8) diff[lane - 8] = 0;  // cum[lp(-1)] == 0
     const int xcd = blockIdx.x & 7;
     const int n_tiles = (P.n_rows + kTile - 1) / kTile;
@@ -1950,15 +1994,21 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     // atomic per tile.  Inside the workgroup the four waves take the tile's rows one at a time
     // from a 64-bit LDS word (tile << 32 | next row); the wave that draws row index 16 fetches
     // the next tile and publishes it, waves drawing past 16 wait for the new tile.
-    unsigned long long* queue = reinterpret_cast<unsigned long long*>(smem + 4 * kRWaves * kRWWords);
+    unsigned long long* queue = reinterpret_cast<unsigned long long*>(smem + 4 * WAVES * kWords);
     constexpr uint32_t kEmpty = 0xFFFFFFFEu, kDone = 0xFFFFFFFFu;
     // tile slots of the flush: tile id, rows finished (kFree: flushed),
     // and the workgroup's tile sequence number (slot = seq % kSlots)
-    constexpr int kSlots = 4;
+    constexpr int kSlots = LDS ? kRLSlots : 4;
+    static_assert(8 + 8 * kSlots + 4 <= (int)kRowsQueueBytes, "slot table");
     constexpr uint32_t kFree = 0xFFFFFFFFu;
     uint32_t* slot_tile = reinterpret_cast<uint32_t*>(queue + 1);
     uint32_t* slot_cnt = slot_tile + kSlots;
     uint32_t* seq = slot_cnt + kSlots;
+    // LDS stage: [slot][row of the tile][ldw] numerators, then [slot][row][part] {bs, lay}
+    // (bs 0: zeros, -1: left to the interpolation kernel)
+    const int ldw = LDS ? P.rows_lds : 0;
+    uint32_t* lstage = reinterpret_cast<uint32_t*>(smem + 4 * WAVES * kWords + kRowsQueueBytes);
+    int2* linfo = reinterpret_cast<int2*>(lstage + (size_t)kSlots * kTile * ldw);
     if (threadIdx.x == 0) *queue = ((unsigned long long)kEmpty << 32) | kTile;
     if (threadIdx.x < kSlots) {
         slot_tile[threadIdx.x] = kDone;
@@ -1966,7 +2016,8 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     }
     if (threadIdx.x == 0) *seq = 0;
     __syncthreads();
-    double* const rm = binsum ? nullptr : P.rm;
+    double* const rm = (binsum || LDS) ? nullptr : P.rm;
+    const bool staged = LDS || rm != nullptr;
     auto fetch_tile = [&]() -> uint32_t {
         for (int k = 0; k < 8; ++k) {
             const int xs = (xcd + k) & 7;
@@ -1993,7 +2044,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             }
             if (idx == (uint32_t)kTile) {
                 const uint32_t t = fetch_tile();
-                if (rm && t != kDone) {
+                if (staged && t != kDone) {
                     // the tile's slot: free once the tile kSlots before it has been flushed (its
                     // last rows are in progress on other waves, which never wait on this one)
                     const uint32_t sl = *(volatile uint32_t*)seq % kSlots;
@@ -2020,6 +2071,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         return rm ? rm + (size_t)r * (size_t)P.n_cols + (size_t)c : out + (size_t)c * R + r;
     };
     auto zero_cols = [&](int r, const RcpPart& part, int32_t n) {
+        if (LDS) return;  // the row's part info says zeros
         for (int32_t k = lane; k < n; k += 64) {
             rows_store(0.0, cell(r, part.col_off + k));
             if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = 0;
@@ -2028,11 +2080,44 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     // the last wave to finish a row of tile T writes the tile's 16 rows of every column from the
     // row-major staging as whole 128-B column lines (release / acquire: the other waves' staging
     // stores are visible to it); lane = (row i, column quarter): 4 columns x 16 rows per store
-    auto flush = [&](uint32_t T) {
+    auto flush = [&](uint32_t T, int sl) {
         const int32_t t16 = (int32_t)T * kTile;
         const int32_t nrow = min(kTile, P.n_rows - t16);
         const int i = lane & 15, cq = lane >> 4;
         const int64_t nc = P.n_cols;
+        if (LDS) {
+            // numerators -> means (the pile's operations), 4 columns x 16 rows per store
+            const uint32_t* srow = lstage + (size_t)(sl * kTile + i) * ldw;
+            const int2* inf = linfo + (sl * kTile + i) * RCP_MAX_PARTS;
+            const double sc = P.scale;
+            for (int p = 0; p < P.n_parts; ++p) {
+                const int32_t n = P.part[p].n_bins, c0p = P.part[p].col_off;
+                const int2 f = i < nrow ? inf[p] : make_int2(-1, -1);
+                const int32_t bs = max(f.x, 1), lay = f.y;
+                const bool pow2 = lay < 0 && (bs & (bs - 1)) == 0;
+                const double dd = (double)bs, rdd = 1.0 / dd;
+                const double dd1 = (double)(bs + 1), rdd1 = 1.0 / dd1;
+                for (int32_t k0 = 0; k0 < n; k0 += 32) {
+                    double v[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int32_t k = k0 + 4 * u + cq;
+                        v[u] = 0.0;
+                        if (f.x > 0 && k < n) {
+                            const int32_t w = lay >= 0 ? bs + P.lay_cnt[lay + k + 1] - P.lay_cnt[lay + k] : bs;
+                            v[u] = rows_mean(srow[c0p + k], sc, pow2, w, bs, dd, rdd, dd1, rdd1);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int32_t k = k0 + 4 * u + cq;
+                        if (f.x >= 0 && k < n)
+                            __builtin_nontemporal_store(v[u], out + (size_t)(c0p + k) * R + (size_t)(t16 + i));
+                    }
+                }
+            }
+            return;
+        }
         const double* src = rm + (size_t)(t16 + i) * (size_t)nc;
         for (int64_t c0 = 0; c0 < nc; c0 += 32) {
             double v[8];
@@ -2048,27 +2133,34 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             }
         }
     };
-    auto row_done = [&](int r) {
+    auto slot_of = [&](int r) {
         const uint32_t T = (uint32_t)(r / kTile);
         int sl = 0;
         for (int k = 1; k < kSlots; ++k)
             if (slot_tile[k] == T) sl = k;
+        return sl;
+    };
+    auto row_done = [&](int r, int sl) {
+        const uint32_t T = (uint32_t)(r / kTile);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         uint32_t old = 0;
         if (lane == 0) old = atomicAdd(&slot_cnt[sl], 1u);
         old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
         if ((int32_t)old + 1 == min(kTile, P.n_rows - (int32_t)T * kTile)) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            flush(T);
+            flush(T, sl);
             lds_order();
             if (lane == 0) atomicExch(&slot_cnt[sl], kFree);
         }
     };
-    auto row_body = [&](int r) {
+    auto row_body = [&](int r, int sl) {
         const uint4 rc = *reinterpret_cast<const uint4*>(P.rec + r);  // flags, row_len, heavy, off
         const int32_t flags = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.x);
         const int32_t nr = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.y);
         const int32_t heavy = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.z);
+        uint32_t* const srow = lstage + (size_t)(sl * kTile + (r & (kTile - 1))) * ldw;
+        int2* const sinfo = linfo + (sl * kTile + (r & (kTile - 1))) * RCP_MAX_PARTS;
+        if (LDS && lane < P.n_parts) sinfo[lane] = make_int2(0, -1);  // zeros unless piled below
         if (!(flags & RCP_REC_VALID)) {  // NULL row -> zeros (profile.R:191-197)
             for (int p = 0; p < P.n_parts; ++p) zero_cols(r, P.part[p], P.part[p].n_bins);
             return;
@@ -2101,7 +2193,10 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             int32_t head, L;
             rcp_part_slice(part, nr, &head, &L);
             const int32_t n = part.n_bins;
-            if (!part.per_base && L < n) continue;  // interpolation row: rcp_interp_kernel
+            if (!part.per_base && L < n) {  // interpolation row: rcp_interp_kernel
+                if (LDS && lane == 0) sinfo[p] = make_int2(-1, -1);
+                continue;
+            }
             if (part.per_base && L != n) {
                 if (lane == 0) atomicOr(P.status, RCP_STATUS_WIDTH);
                 zero_cols(r, part, n);
@@ -2119,7 +2214,8 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     }
                 }
             }
-            const int32_t kw = max(1, kRWCap / (bs + (lay >= 0 ? 1 : 0)));  // bins per window
+            if (LDS && lane == 0) sinfo[p] = make_int2(bs, lay);
+            const int32_t kw = max(1, kWinCap / (bs + (lay >= 0 ? 1 : 0)));  // bins per window
             const bool pow2 = lay < 0 && (bs & (bs - 1)) == 0;
             const double dd = (double)bs, rdd = 1.0 / dd;
             const double dd1 = (double)(bs + 1), rdd1 = 1.0 / dd1;  // an enlarged bin's width
@@ -2189,11 +2285,11 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
                     const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
                     const uint32_t num = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
-                    double x;
-                    if (pow2) x = ((double)num * sc) * rdd;
-                    else if (b - a == bs) x = rcp_div_rn((double)num * sc, dd, rdd);
-                    else x = rcp_div_rn((double)num * sc, dd1, rdd1);  // b - a == bs + 1
-                    rows_store(x, cell(r, part.col_off + k));
+                    if (LDS) {
+                        srow[part.col_off + k] = num;
+                        continue;
+                    }
+                    rows_store(rows_mean(num, sc, pow2, b - a, bs, dd, rdd, dd1, rdd1), cell(r, part.col_off + k));
                     if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = (int64_t)num;
                 }
                 lds_order();
@@ -2201,8 +2297,9 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         }
     };
     for (int r = claim(); r >= 0; r = claim()) {
-        row_body(r);
-        if (rm) row_done(r);
+        const int sl = staged ? slot_of(r) : 0;
+        row_body(r, sl);
+        if (staged) row_done(r, sl);
     }
     // the last workgroup out resets the tile counters for the next launch
     __syncthreads();
@@ -3324,16 +3421,31 @@ static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* bin
                  : launch_pileup_u<MEDIAN, CSR, false>(P, out, binsum, lds, s);
 }
 
-extern "C" size_t rcp_pileup_rows_lds_bytes(void) { return 4 * (size_t)kRWaves * kRWWords + 16 + 48; }
+extern "C" size_t rcp_pileup_rows_lds_bytes(const RcpPlanDev* P) {
+    if (P && P->rows_lds > 0) return rows_lds_bytes(P->rows_lds, kRLWaves, RowWin<kRLSh>::words, kRLSlots);
+    return rows_lds_bytes(0, kRWaves, RowWin<kRWSh>::words, 0);
+}
 
 static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* binsum, hipStream_t s) {
-    // persistent: four workgroups (16 waves) per CU, a multiple of 8 (workgroup b serves XCD
-    // b % 8), never more workgroups than tiles
+    // persistent: a multiple of 8 workgroups (workgroup b serves XCD b % 8), never more
+    // workgroups than tiles; four 4-wave workgroups per CU, or as many LDS-staged ones as fit
     const int cus = std::max(1, P->n_cus);
     const int64_t tiles = ((int64_t)P->n_rows + kTile - 1) / kTile;  // at least a tile per workgroup
+    if (P->rows_lds > 0 && !binsum) {
+        const size_t lds = rcp_pileup_rows_lds_bytes(P);
+        auto k = rcp_pileup_rows_kernel<1, kRLWaves, kRLSh>;
+        const hipError_t e = allow_big_lds(k);
+        if (e != hipSuccess) return e;
+        const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / kRLWaves, (160 * 1024) / lds));
+        const int64_t grid = std::min<int64_t>((per_cu * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
+        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * kRLWaves), lds, s, *P, out, binsum);
+        return hipGetLastError();
+    }
+    RcpPlanDev Q = *P;
+    Q.rows_lds = 0;
     const int64_t grid = std::min<int64_t>(((int64_t)4 * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
-    hipLaunchKernelGGL(rcp_pileup_rows_kernel, dim3((unsigned)grid), dim3(64 * kRWaves), rcp_pileup_rows_lds_bytes(), s,
-                       *P, out, binsum);
+    hipLaunchKernelGGL((rcp_pileup_rows_kernel<0, kRWaves, kRWSh>), dim3((unsigned)grid), dim3(64 * kRWaves),
+                       rcp_pileup_rows_lds_bytes(&Q), s, Q, out, binsum);
     return hipGetLastError();
 }
 

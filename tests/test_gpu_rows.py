@@ -151,3 +151,21 @@ def test_repeated_executions_and_kernel_choice(gpu):
     assert Plan(rs, single, Bins([("whole", 150)])).info["pileup_kernel"] == 0
     assert Plan(rs, single, Bins([("whole", 1000)]), kernel="lean").info["pileup_kernel"] == 1
     assert Plan(rs, rows, bins, kernel="general").info["pileup_kernel"] == 0
+
+
+def test_lds_and_global_staging(gpu):
+    """Tiles staged in LDS (16 rows x n_cols numerators fit two slots: C3's 600 columns) and in
+    the global row-major staging (4100 columns of per-base flanks): the same bits as the general
+    kernel either way, NULL rows and interpolated short genes included."""
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(67)
+    reads = make_reads(rng, 150_000, widths=(50, 600))
+    rows = rna_rows(rng, 203)
+    c3 = Bins([("upstream", 50), ("center", 500), ("downstream", 50)], flank=(2000, 2000), scale=0.61)
+    res, exp, plan = _both(reads, CHROM_LEN, rows, c3, kernel="auto")
+    assert plan.info["lds_bytes"] > 100_000  # LDS stage
+    check(res, exp, rtol=1e-9, atol=1e-12)
+    wide = Bins([("upstream", 0, 2000), ("center", 100), ("downstream", 0, 2000)], flank=(2000, 2000))
+    res, exp, plan = _both(reads, CHROM_LEN, rows, wide, kernel="auto")
+    assert plan.info["lds_bytes"] < 65_536  # row-major staging in HBM
+    check(res, exp, rtol=1e-9, atol=1e-12)

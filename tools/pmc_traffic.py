@@ -18,7 +18,7 @@ import json
 import os
 import sys
 
-KERNELS = ("rcp_pileup_lean_kernel<", "rcp_pileup_kernel<", "rcp_pileup_rows_kernel(")  # whichever the plan launched
+KERNELS = ("rcp_pileup_lean_kernel<", "rcp_pileup_kernel<", "rcp_pileup_rows_kernel<", "rcp_pileup_bins_kernel<")  # whichever the plan launched
 
 
 def per_launch(path, counter):

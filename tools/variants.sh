@@ -8,7 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/build_var
 mode=$1; shift
 if [ "$mode" = build ]; then
-    rm -rf "$OUT"; mkdir -p "$OUT"
+    [ -n "$KEEP" ] || rm -rf "$OUT"; mkdir -p "$OUT"
     for spec in "$@"; do
         name=${spec%%=*}; defs=${spec#*=}
         mkdir -p "$OUT/$name"

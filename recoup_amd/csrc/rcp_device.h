@@ -173,6 +173,14 @@ struct RcpPlanDev {
     // sub-chunk's first position counts only at the row's position 0; rcp_rle_seams_kernel
     // adds the seams between sub-chunks): the run counts of calcCoverage's Rle list
     unsigned long long* csr_runs;
+    // non-null (calcCoverage's Rle list without a dense depth array): each (row, column chunk)
+    // writes its run starts -- the chunk's first position always, then every position whose
+    // depth differs from the one before -- as (depth, row position) to csr_rs at the chunk's
+    // dense offset (csr_off[row] + first position), and (starts, last depth) to
+    // csr_sub[csr_sub_off[row] + column chunk]; rcp_cov_runs_* merge the seams and compact
+    int2* csr_rs;
+    int2* csr_sub;
+    const int64_t* csr_sub_off;
     // skewed depth: rows with more than heavy_threshold candidate reads are piled up
     // first by many workgroups (heavy slices) into a global difference array
     uint32_t* ncand;            // [n_rows] candidate reads (locate output)

@@ -122,6 +122,10 @@ hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, const int32_
 hipError_t rcp_launch_width_range(int64_t n, const uint64_t* keys, const int32_t* vals, int32_t* mm,
                                   hipStream_t stream);
 hipError_t rcp_launch_split_uniform(int64_t n, const int2* se, int32_t* st, int32_t* pmax, hipStream_t stream);
+hipError_t rcp_cov_runs_dev(int32_t n_rows, const int64_t* d_off, const int64_t* d_sub_off, int64_t n_sub,
+                            const int2* d_sub, const int2* d_rs, const uint8_t* d_valid, int32_t chunk, int64_t* d_cnt,
+                            int4* d_info, int64_t* d_base, int64_t* d_run_off, void* temp, size_t* temp_bytes,
+                            int32_t* d_values, int32_t* d_lengths, uint32_t* d_bad, int pass, hipStream_t stream);
 hipError_t rcp_rle_seams_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, const uint8_t* d_valid,
                              int32_t chunk_bins, int32_t chunk_cap, int64_t* d_count, hipStream_t stream);
 hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t* off, const int32_t* pmax, int32_t* out,
@@ -1542,6 +1546,9 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.csr_off = nullptr;
     P.csr_out = nullptr;
     P.csr_runs = nullptr;
+    P.csr_rs = nullptr;
+    P.csr_sub = nullptr;
+    P.csr_sub_off = nullptr;
     // row-wave plans stage their bins row-major (whole lines per row) and transpose once
     P.rm = nullptr;
     if (P.lean == 3 && P.rows_lds == 0 && R > 0 && P.n_cols > 0) {
@@ -1954,12 +1961,49 @@ int calc_coverage_dev(rcp_plan* plan, const int64_t* d_off, int32_t* d_cov, uint
     P.csr_out = d_cov;
     P.valid_out = d_valid;
     P.csr_runs = reinterpret_cast<unsigned long long*>(d_runs);
+    P.csr_rs = nullptr;
     if (d_runs) HIP_TRY(hipMemsetAsync(d_runs, 0, 8 * ((size_t)plan->n_rows + 1), s));
     HIP_TRY(rcp_launch_locate(&P, s));
     HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
     if (d_runs) HIP_TRY(rcp_rle_seams_dev(plan->n_rows, d_off, d_cov, d_valid, pt.chunk_bins, P.chunk_cap, d_runs, s));
     return RCP_OK;
+}
+
+// calcCoverage of every row as run-start lists (no dense depth): per (row, column chunk of
+// *chunk positions) the chunk's run starts at d_rs + d_off[row] + first position and
+// (starts, last depth) at d_sub[d_sub_off[row] + chunk]
+int coverage_starts_dev(rcp_plan* plan, const int64_t* d_off, const int64_t* d_sub_off, int2* d_rs, int2* d_sub,
+                        uint8_t* d_valid, hipStream_t s) {
+    begin_exec(plan);
+    RcpPlanDev P = plan->dev;
+    P.n_parts = 1;
+    RcpPart& pt = P.part[0];
+    pt = RcpPart{};
+    pt.hi_end = 1;
+    pt.per_base = 1;
+    pt.n_bins = std::max<int32_t>(plan->max_row_len, 1);
+    pt.chunk_bins = std::max<int32_t>(std::min(P.chunk_cap, pt.n_bins), 1);
+    pt.n_chunks = (pt.n_bins + pt.chunk_bins - 1) / pt.chunk_bins;
+    P.n_chunks_total = pt.n_chunks;
+    P.crange = nullptr;
+    P.cw_len = -1;
+    P.csr_off = d_off;
+    P.csr_out = nullptr;
+    P.valid_out = d_valid;
+    P.csr_runs = nullptr;
+    P.csr_rs = d_rs;
+    P.csr_sub = d_sub;
+    P.csr_sub_off = d_sub_off;
+    HIP_TRY(rcp_launch_locate(&P, s));
+    HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
+    HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
+    return RCP_OK;
+}
+
+// the column chunk of coverage_starts_dev (one wave sub-chunk each)
+int32_t coverage_chunk(const rcp_plan* plan) {
+    return std::max<int32_t>(std::min(plan->dev.chunk_cap, std::max<int32_t>(plan->max_row_len, 1)), 1);
 }
 
 }  // namespace
@@ -2086,7 +2130,60 @@ extern "C" int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows
     const int64_t n = off[R];
     if (n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "%lld coverage positions", (long long)n);
     hipStream_t s = nullptr;
-    {
+#ifndef RCP_COV_DENSE
+#define RCP_COV_DENSE 0  // 1: round-3 path (dense depth written, counted, re-read by an emit kernel)
+#endif
+    if (!RCP_COV_DENSE) {
+        // the pileup writes each (row, column chunk)'s run starts (depth, position) compacted at
+        // the chunk's dense offset -- no depth array --; a thread per row merges the seams
+        // between chunks, a scan of the kept counts places the runs, and a wave per chunk copies
+        // them out as (value, length)
+        const int32_t chunk = coverage_chunk(plan);
+        std::vector<int64_t> sub_off((size_t)R + 1, 0);
+        for (int32_t r = 0; r < R; ++r) sub_off[r + 1] = sub_off[r] + (plan->row_len[r] + chunk - 1) / chunk;
+        const int64_t S = sub_off[R];
+        PoolBuf d_rs(s), d_off(s), d_sub_off(s), d_sub(s), d_cnt(s), d_info(s), d_base(s), temp(s), bad(s);
+        HIP_TRY(d_rs.alloc(8 * std::max<int64_t>(n, 1)));
+        HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
+        HIP_TRY(d_sub_off.alloc(8 * ((size_t)R + 1)));
+        HIP_TRY(d_sub.alloc(8 * std::max<int64_t>(S, 1)));
+        HIP_TRY(d_cnt.alloc(8 * ((size_t)S + 1)));
+        HIP_TRY(d_info.alloc(16 * std::max<int64_t>(S, 1)));
+        HIP_TRY(d_base.alloc(8 * ((size_t)S + 1)));
+        HIP_TRY(bad.alloc(4));
+        HIP_TRY(res->valid.alloc(std::max<int32_t>(R, 1)));
+        HIP_TRY(res->run_off.alloc(8 * ((size_t)R + 1)));
+        HIP_TRY(hipMemcpyAsync(d_off.p, off.data(), 8 * ((size_t)R + 1), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_sub_off.p, sub_off.data(), 8 * ((size_t)R + 1), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(d_cnt.as<int64_t>() + S, 0, 8, s));
+        HIP_TRY(hipMemsetAsync(bad.p, 0, 4, s));
+        rc = coverage_starts_dev(plan, d_off.as<int64_t>(), d_sub_off.as<int64_t>(), d_rs.as<int2>(), d_sub.as<int2>(),
+                                 res->valid.as<uint8_t>(), s);
+        if (rc) return rc;
+        rc = rcp_plan_status(plan, nullptr);
+        if (rc) return rc;
+        size_t tb = 0;
+        HIP_TRY(rcp_cov_runs_dev(R, nullptr, nullptr, S, nullptr, nullptr, nullptr, chunk, d_cnt.as<int64_t>(), nullptr,
+                                 d_base.as<int64_t>(), nullptr, nullptr, &tb, nullptr, nullptr, nullptr, 0, s));
+        HIP_TRY(temp.alloc(std::max<size_t>(tb, 1)));
+        HIP_TRY(rcp_cov_runs_dev(R, d_off.as<int64_t>(), d_sub_off.as<int64_t>(), S, d_sub.as<int2>(), d_rs.as<int2>(),
+                                 res->valid.as<uint8_t>(), chunk, d_cnt.as<int64_t>(), d_info.as<int4>(),
+                                 d_base.as<int64_t>(), res->run_off.as<int64_t>(), temp.p, &tb, nullptr, nullptr,
+                                 bad.as<uint32_t>(), 1, s));
+        int64_t nr = 0;
+        HIP_TRY(hipMemcpyAsync(&nr, res->run_off.as<int64_t>() + R, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        res->n_runs = nr;
+        HIP_TRY(res->values.alloc(4 * (size_t)std::max<int64_t>(nr, 1)));
+        HIP_TRY(res->lengths.alloc(4 * (size_t)std::max<int64_t>(nr, 1)));
+        HIP_TRY(rcp_cov_runs_dev(R, nullptr, nullptr, S, nullptr, d_rs.as<int2>(), nullptr, chunk, nullptr,
+                                 d_info.as<int4>(), d_base.as<int64_t>(), nullptr, nullptr, nullptr,
+                                 res->values.as<int32_t>(), res->lengths.as<int32_t>(), bad.as<uint32_t>(), 2, s));
+        uint32_t h_bad = 0;
+        HIP_TRY(hipMemcpyAsync(&h_bad, bad.p, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (h_bad) return fail(RCP_EINVAL, "internal: run starts and chunk records disagree");
+    } else {
         // the pileup counts each row's runs as it writes the depth (csr_runs, + the seams
         // between its wave sub-chunks); a scan of the counts places every row's runs
         PoolBuf d_cov(s), d_off(s), d_count(s), temp(s);

@@ -1815,7 +1815,27 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
                 }
                 scan_wave<!(MEDIAN || CSR)>(diff, per);
                 lds_order();
-                if (CSR) {
+                if (CSR && P.csr_rs) {
+                    // run starts of this chunk (its first position always: the seams are
+                    // merged by rcp_cov_runs_plan_kernel), compacted in position order
+                    int2* rs_out = P.csr_rs + P.csr_off[r] + k0 + s0;
+                    const uint64_t below = (1ull << lane) - 1;
+                    uint32_t e = 0;
+                    int32_t carry = 0, lastv = 0;
+                    for (int32_t q0 = 0; q0 < sn; q0 += 64) {
+                        const int32_t q = q0 + lane;
+                        const bool in = q < sn;
+                        const int32_t v = in ? diff[lp(q, sh)] : 0;
+                        const int32_t pv = __builtin_amdgcn_update_dpp(carry, v, 0x138, 0xf, 0xf, false);
+                        const bool f = in && (q == 0 || v != pv);
+                        const uint64_t mk = __ballot(f);
+                        if (f) rs_out[e + (uint32_t)__popcll(mk & below)] = make_int2(v, k0 + s0 + q);
+                        e += (uint32_t)__popcll(mk);
+                        carry = __builtin_amdgcn_readlane(v, 63);
+                        if (q0 + 64 >= sn) lastv = __builtin_amdgcn_readlane(v, sn - 1 - q0);
+                    }
+                    if (lane == 0) P.csr_sub[P.csr_sub_off[r] + cidx + s0 / P.chunk_cap] = make_int2((int32_t)e, lastv);
+                } else if (CSR) {
                     int32_t* orow = P.csr_out + P.csr_off[r];
                     // run starts after this sub-chunk's first position: position q - 1 is the
                     // lane below (wave_shr:1), lane 0's the last lane of the step before
@@ -3644,6 +3664,116 @@ __global__ void __launch_bounds__(64 * kRleWaves) rcp_rle_emit_kernel(int32_t n_
     }
     if (pend >= 0 && pend < end && lane == 0) lengths[pend] = (int32_t)(b - pstart);
     if (lane == 0 && k != end) atomicOr(bad, 1u);  // the counting pass and this one disagree
+}
+
+// Rle runs from the pileup's run-start lists (P.csr_rs / csr_sub, no dense depth array).
+// Plan (a thread per row): a chunk's first start is a run start only at the row's first
+// position or where its depth differs from the previous chunk's last depth; per chunk j the
+// kept starts cnt[j] (scanned into the run offsets), and info[j] = (skipped first entry, row
+// position of the next kept start after the chunk -- the end of its last run --, the chunk's
+// dense offset).  NULL rows keep no runs.
+__global__ void __launch_bounds__(kBlock) rcp_cov_runs_plan_kernel(int32_t n_rows, const int64_t* __restrict__ off,
+                                                                 const int64_t* __restrict__ sub_off,
+                                                                 const int2* __restrict__ sub,
+                                                                 const int2* __restrict__ rs,
+                                                                 const uint8_t* __restrict__ valid, int32_t chunk,
+                                                                 int64_t* __restrict__ cnt, int4* __restrict__ info,
+                                                                 uint32_t* __restrict__ bad) {
+    const int r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= n_rows) return;
+    const int64_t j0 = sub_off[r], j1 = sub_off[r + 1];
+    const int64_t a = off[r];
+    const int32_t L = (int32_t)(off[r + 1] - a);
+    if (!valid[r] || L == 0) {
+        for (int64_t j = j0; j < j1; ++j) cnt[j] = 0;
+        return;
+    }
+    if ((int64_t)(L + chunk - 1) / chunk != j1 - j0) atomicOr(bad, 1u);
+    int32_t prev = 0;
+    for (int64_t j = j0; j < j1; ++j) {
+        const int2 sb = sub[j];
+        const int32_t d0 = (int32_t)(a + (j - j0) * chunk);
+        const int32_t len = min(chunk, L - (int32_t)(j - j0) * chunk);
+        if (sb.x < 1 || sb.x > len) {  // every chunk records its first position
+            atomicOr(bad, 1u);
+            cnt[j] = 0;
+            info[j] = make_int4(0, 0, d0, 0);
+            continue;
+        }
+        const int skip = (j > j0 && rs[d0].x == prev) ? 1 : 0;
+        cnt[j] = sb.x - skip;
+        info[j] = make_int4(skip, 0, d0, 0);
+        prev = sb.y;
+    }
+    int32_t next = L;  // row position of the next kept run start
+    for (int64_t j = j1 - 1; j >= j0; --j) {
+        if (cnt[j] == 0) continue;
+        const int4 in = info[j];
+        info[j] = make_int4(in.x, next, in.z, 0);
+        next = rs[in.z + in.x].y;
+    }
+}
+
+// run offsets of the rows: the scanned chunk counts at each row's first chunk
+__global__ void __launch_bounds__(kBlock) rcp_cov_runs_rowoff_kernel(int32_t n_rows, const int64_t* __restrict__ sub_off,
+                                                                   const int64_t* __restrict__ base,
+                                                                   int64_t* __restrict__ run_off) {
+    const int r = blockIdx.x * kBlock + threadIdx.x;
+    if (r <= n_rows) run_off[r] = base[sub_off[r]];
+}
+
+// Compaction: a wave per chunk copies its kept starts to their final places as (value, length);
+// a run's length reaches the next kept start (the chunk's last run: info.y, possibly in a
+// later chunk)
+__global__ void __launch_bounds__(kBlock) rcp_cov_runs_emit_kernel(int64_t n_sub, const int64_t* __restrict__ base,
+                                                                 const int4* __restrict__ info,
+                                                                 const int2* __restrict__ rs,
+                                                                 int32_t* __restrict__ values,
+                                                                 int32_t* __restrict__ lengths,
+                                                                 uint32_t* __restrict__ bad) {
+    const int64_t j = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (j >= n_sub) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = base[j];
+    const int32_t c = (int32_t)(base[j + 1] - b);
+    if (c <= 0) return;
+    const int4 in = info[j];
+    const int2* src = rs + in.z + in.x;
+    bool ok = true;
+    for (int32_t e = lane; e < c; e += 64) {
+        const int2 x = src[e];
+        const int32_t nx = e + 1 < c ? src[e + 1].y : in.y;
+        values[b + e] = x.x;
+        lengths[b + e] = nx - x.y;
+        ok = ok && nx > x.y;
+    }
+    if (!ok) atomicOr(bad, 1u);
+}
+
+extern "C" hipError_t rcp_cov_runs_dev(int32_t n_rows, const int64_t* d_off, const int64_t* d_sub_off, int64_t n_sub,
+                                       const int2* d_sub, const int2* d_rs, const uint8_t* d_valid, int32_t chunk,
+                                       int64_t* d_cnt, int4* d_info, int64_t* d_base, int64_t* d_run_off, void* temp,
+                                       size_t* temp_bytes, int32_t* d_values, int32_t* d_lengths, uint32_t* d_bad,
+                                       int pass, hipStream_t stream) {
+    // pass 0: temp size of the scan; 1: plan + scan + row offsets (d_cnt[n_sub] must be 0);
+    // 2: emit (values / lengths of d_run_off[n_rows] runs)
+    if (pass == 0) return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, d_cnt, d_base, (int)n_sub + 1, stream);
+    if (pass == 1) {
+        if (n_rows > 0)
+            hipLaunchKernelGGL(rcp_cov_runs_plan_kernel, dim3((unsigned)((n_rows + kBlock - 1) / kBlock)), dim3(kBlock),
+                               0, stream, n_rows, d_off, d_sub_off, d_sub, d_rs, d_valid, chunk, d_cnt, d_info, d_bad);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        e = hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, d_cnt, d_base, (int)n_sub + 1, stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(rcp_cov_runs_rowoff_kernel, dim3((unsigned)((n_rows + 1 + kBlock - 1) / kBlock)), dim3(kBlock),
+                           0, stream, n_rows, d_sub_off, d_base, d_run_off);
+        return hipGetLastError();
+    }
+    if (n_sub > 0)
+        hipLaunchKernelGGL(rcp_cov_runs_emit_kernel, dim3((unsigned)((n_sub + kBlock / 64 - 1) / (kBlock / 64))),
+                           dim3(kBlock), 0, stream, n_sub, d_base, d_info, d_rs, d_values, d_lengths, d_bad);
+    return hipGetLastError();
 }
 
 // The run starts the coverage pileup could not see (rcp_pileup_kernel's csr_runs): the seams

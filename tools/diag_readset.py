@@ -1,6 +1,7 @@
 """Readset creation from host arrays, repeated (variance of the C5-sized H2D + layouts).
 
-    python tools/diag_readset.py [c5|c4] [reps]     (RCP_LIB_PATH: e.g. a -DRCP_PLAN_TIMING=1 build)"""
+    python tools/diag_readset.py [c5|c4] [reps]     (RCP_LIB_PATH: e.g. a -DRCP_PLAN_TIMING=1 build;
+                                                     STRANDED=1: the strand-split layout as well)"""
 import os
 import sys
 import time
@@ -20,9 +21,12 @@ for k in range(reps):
     torch.cuda.synchronize()
     a = time.perf_counter()
     rs = ReadSet(*host, d["seqlen"], device=0)
+    if os.environ.get("STRANDED"):
+        rs.stream_off  # builds the strand-split layout too
     torch.cuda.synchronize()
     b = time.perf_counter()
     del rs
     torch.cuda.synchronize()
     c = time.perf_counter()
-    print(f"rep {k}: create {(b - a) * 1e3:.1f} ms, destroy {(c - b) * 1e3:.1f} ms", flush=True)
+    free = torch.cuda.mem_get_info()[0] / 2**30
+    print(f"rep {k}: create {(b - a) * 1e3:.1f} ms, destroy {(c - b) * 1e3:.1f} ms, free {free:.1f} GB", flush=True)

@@ -2,7 +2,7 @@
 import csv
 import sys
 
-KEYS = ("rle_tile", "rle_interp", "rle_emit", "rle_count", "pileup_kernel<false, true>", "pileup_lean", "locate",
+KEYS = ("rle_tile", "rle_interp", "rle_emit", "rle_count", "cov_runs", "pileup_kernel<false, true", "pileup_lean", "locate",
         "scan_impl<(rocprim::ROCPRIM_400200_NS::detail::lookback_scan_determinism)0, true, true, rocprim::ROCPRIM_400200_NS::default_config, hipcub")
 for path in sys.argv[1:]:
     print(path)

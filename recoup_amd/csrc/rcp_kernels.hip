@@ -790,7 +790,10 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
 #define RCP_LOC_WPE 1
 #endif
 
-template <int KS>  // searches of one lockstep round per lane (8: plans of > 7 column chunks, one round)
+// KS: searches of one lockstep round per lane of a single-range row (2: plans of <= 3 column
+// chunks, 4: <= 7, 8: more, one round); KP: searches per round of the (segment, stream) pair
+// loop (two per pair).  Fewer held dir_k lines = fewer VGPRs = more waves in flight.
+template <int KS, int KP>
 __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres)[2 * RCP_MAX_CRANGE_CHUNKS],
                                             uint32_t (*item_w)[RCP_MAX_CRANGE_CHUNKS]) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
@@ -949,15 +952,25 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
     // (segment, stream) pairs dealt round-robin to the quad; a lane's two pairs of one round
     // (pi, pi + LPR) search their lower and upper bounds in lockstep: one chain of dependent
     // loads for four searches (an exon list of ~10 segments: 2 rounds instead of 6 chains)
-    for (int pb = split1 ? npairs : q; pb < npairs; pb += 2 * LPR) {
-        int32_t sv[4] = {0, 0, 0, 0};
-        int sd[4] = {-2, -1, -2, -1};
-        int64_t sd0[4] = {0, 0, 0, 0};
-        int32_t snb[4] = {1, 1, 1, 1};
-        bool use[2] = {false, false};
+    constexpr int kPairs = KP / 2;  // pairs per lane per round
+    for (int pb = split1 ? npairs : q; pb < npairs; pb += kPairs * LPR) {
+        int32_t sv[KP];
+        int sd[KP];
+        int64_t sd0[KP];
+        int32_t snb[KP];
+        bool use[kPairs];
+#pragma unroll
+        for (int u = 0; u < KP; ++u) {
+            sv[u] = 0;
+            sd[u] = (u & 1) ? -1 : -2;
+            sd0[u] = 0;
+            snb[u] = 1;
+        }
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) use[k] = false;
         int cnt = 0;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kPairs; ++k) {
             const int pi = pb + k * LPR;
             if (pi >= npairs) continue;
             const int j = j0 + pi / ns;
@@ -981,10 +994,10 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
                 cnt = 2 * k + 2;
             }
         }
-        uint32_t res[4];
-        dir_bound_multi<4>(P, sd0, snb, sv, sd, cnt, res);
+        uint32_t res[KP];
+        dir_bound_multi<KP>(P, sd0, snb, sv, sd, cnt, res);
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kPairs; ++k) {
             const int pi = pb + k * LPR;
             if (pi >= npairs) continue;
             const int j = j0 + pi / ns;
@@ -1129,8 +1142,12 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
     for (int u = 0; u < 4; ++u) dst[u] = src[u];
 }
 
-template <int KS>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RCP_LOC_WPE))) rcp_locate_kernel(RcpPlanDev P) {
+#ifndef RCP_LOC_WPE2
+#define RCP_LOC_WPE2 6  // waves per SIMD asked of the KS = 2 variant (<= 80 VGPRs)
+#endif
+template <int KS, int KP>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS == 2 ? RCP_LOC_WPE2 : RCP_LOC_WPE)))
+rcp_locate_kernel(RcpPlanDev P) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
     __shared__ uint32_t xres[kBlock / LPR][2 * RCP_MAX_CRANGE_CHUNKS];  // per row: chunk bounds
     // heaviest-first lean items (P.lpt): this block's 64 rows are two 32-row tiles; their
@@ -1138,7 +1155,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RCP
     __shared__ uint32_t item_w[2][RCP_MAX_CRANGE_CHUNKS];
     if (P.lpt && threadIdx.x < 2 * RCP_MAX_CRANGE_CHUNKS) item_w[threadIdx.x >> 4][threadIdx.x & 15] = 0u;
     if (P.lpt) __syncthreads();
-    locate_rows<KS>(P, xres, P.lpt ? item_w : nullptr);
+    locate_rows<KS, KP>(P, xres, P.lpt ? item_w : nullptr);
     if (P.lpt) {
         __syncthreads();
         const int nc = P.n_chunks_total;
@@ -3334,10 +3351,16 @@ extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream)
 #ifndef RCP_LOC_KS8
 #define RCP_LOC_KS8 1
 #endif
+#ifndef RCP_LOC_KS2
+#define RCP_LOC_KS2 1  // plans of <= 3 column chunks (<= 8 searches a row): 2 per lane
+#endif
+    const int searches = 2 + (P->crange ? 2 * (P->n_chunks_total - 1) : 0);  // a single-range row's
     if (RCP_LOC_KS8 && P->crange && 2 * P->n_chunks_total > 4 * 4)
-        hipLaunchKernelGGL(rcp_locate_kernel<8>, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
+        hipLaunchKernelGGL((rcp_locate_kernel<8, 4>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
+    else if (RCP_LOC_KS2 && searches <= 2 * 4)
+        hipLaunchKernelGGL((rcp_locate_kernel<2, 2>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
     else
-        hipLaunchKernelGGL(rcp_locate_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
+        hipLaunchKernelGGL((rcp_locate_kernel<4, 4>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
     return hipGetLastError();
 }
 

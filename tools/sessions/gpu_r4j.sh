@@ -25,12 +25,14 @@ for v in new covdense; do
 done
 timeout -k 10 900 $T -m gpu tests > $OUT/tests.log 2>&1 || { tail -60 $OUT/tests.log; exit 1; }
 tail -1 $OUT/tests.log
-for v in new nopre l1 l2 l4 l8; do
+STRANDED=1 timeout -k 10 300 python3 tools/diag_readset.py c5 12 > $OUT/readset_c5.log 2>&1 || { tail $OUT/readset_c5.log; exit 1; }
+grep rep $OUT/readset_c5.log
+for v in new ks2off wpe5 nopre l1 l2 l4 l8; do
   lib=build_var/$v/librecoup_amd.so
   [ $v = new ] && lib=recoup_amd/librecoup_amd.so
   echo "== $v" >> $OUT/ab.log
   specs="c2:0/1 c4:0/1"
-  [ $v = new ] || [ $v = nopre ] && specs="c2:0/1 c4:0/1 c4:0/8 c5:0/8"
+  case $v in new|nopre) specs="c2:0/1 c4:0/1 c4:0/8 c5:0/8";; ks2off|wpe5) specs="c2:0/1 c4:0/1 c4:0/8";; esac
   for spec in $specs; do
     RCP_LIB_PATH=$lib CFG=${spec%%:*} timeout -k 10 200 python3 tools/diag_shard_kernels.py ${spec#*:} auto >> $OUT/ab.log 2>&1 || { tail $OUT/ab.log; exit 1; }
   done
@@ -46,5 +48,3 @@ for v in bd8 bd16; do
   RCP_LIB_PATH=build_var/$v/librecoup_amd.so CFG=c2 timeout -k 10 200 python3 tools/diag_shard_kernels.py 0/1 auto >> $OUT/ab.log 2>&1 || { tail $OUT/ab.log; exit 1; }
 done
 grep -E "==|ms/pass" $OUT/ab.log
-STRANDED=1 timeout -k 10 300 python3 tools/diag_readset.py c5 12 > $OUT/readset_c5.log 2>&1 || { tail $OUT/readset_c5.log; exit 1; }
-grep rep $OUT/readset_c5.log

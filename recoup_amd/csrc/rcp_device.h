@@ -156,6 +156,7 @@ struct RcpPlanDev {
     // item_order under its class floor(log2(reads)) (counts in status[kLptClass + class]), and
     // the lean kernel claims items from one counter, highest class first.  0: per-XCD order.
     int32_t lpt;
+    int32_t multi_rows;         // 1: some row is a list of ranges (locate's pair loop does the work)
     int32_t lpt_cap;            // items per class list (>= the plan's item count)
     int32_t* item_order;        // [RCP_LPT_CLASSES][lpt_cap]
     // row-wave kernel (lean == 3): its rows' bins go row-major into rm (n_rows x n_cols, whole

@@ -1050,6 +1050,8 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     for (int r = 0; r < R; ++r) plan->max_row_len = std::max(plan->max_row_len, B.row_len[r]);
 
     RcpPlanDev& P = plan->dev;
+    P.multi_rows = 0;
+    for (int r = 0; r < R && !P.multi_rows; ++r) P.multi_rows = B.row_seg[r + 1] - B.row_seg[r] > 1;
     P.n_parts = bins->n_parts;
     P.stat = bins->stat;
     P.scale = bins->scale;

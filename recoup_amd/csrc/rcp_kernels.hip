@@ -3352,12 +3352,12 @@ extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream)
 #define RCP_LOC_KS8 1
 #endif
 #ifndef RCP_LOC_KS2
-#define RCP_LOC_KS2 1  // plans of <= 3 column chunks (<= 8 searches a row): 2 per lane
+#define RCP_LOC_KS2 1  // single-range plans of <= 3 column chunks (<= 8 searches a row): 2 per lane
 #endif
     const int searches = 2 + (P->crange ? 2 * (P->n_chunks_total - 1) : 0);  // a single-range row's
     if (RCP_LOC_KS8 && P->crange && 2 * P->n_chunks_total > 4 * 4)
         hipLaunchKernelGGL((rcp_locate_kernel<8, 4>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
-    else if (RCP_LOC_KS2 && searches <= 2 * 4)
+    else if (RCP_LOC_KS2 && searches <= 2 * 4 && !P->multi_rows)
         hipLaunchKernelGGL((rcp_locate_kernel<2, 2>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
     else
         hipLaunchKernelGGL((rcp_locate_kernel<4, 4>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);

@@ -47,4 +47,7 @@ for v in bd8 bd16; do
   echo "== $v" >> $OUT/ab.log
   RCP_LIB_PATH=build_var/$v/librecoup_amd.so CFG=c2 timeout -k 10 200 python3 tools/diag_shard_kernels.py 0/1 auto >> $OUT/ab.log 2>&1 || { tail $OUT/ab.log; exit 1; }
 done
+echo "== kernels" >> $OUT/ab.log
+CFG=c5 timeout -k 10 200 python3 tools/diag_shard_kernels.py 0/8 auto general rows >> $OUT/ab.log 2>&1 || { tail $OUT/ab.log; exit 1; }
+CFG=c4 timeout -k 10 200 python3 tools/diag_shard_kernels.py 0/8 auto lean rows >> $OUT/ab.log 2>&1 || { tail $OUT/ab.log; exit 1; }
 grep -E "==|ms/pass" $OUT/ab.log

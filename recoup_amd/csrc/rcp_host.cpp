@@ -278,7 +278,10 @@ hipError_t device_pool(int dev, hipMemPool_t* out) {
     hipMemPool_t pool;
     hipError_t e = hipMemPoolCreate(&pool, &props);
     if (e != hipSuccess) return e;
-    uint64_t thr = uint64_t(64) << 30;  // up to 64 GB kept mapped (C5's build peaks near 40 GB)
+#ifndef RCP_POOL_KEEP_GB
+#define RCP_POOL_KEEP_GB 64  // freed memory kept mapped (C5's build peaks near 40 GB)
+#endif
+    uint64_t thr = uint64_t(RCP_POOL_KEEP_GB) << 30;
     e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
     if (e != hipSuccess) return e;
     g_pools[dev] = pool;

@@ -27,6 +27,8 @@ timeout -k 10 900 $T -m gpu tests > $OUT/tests.log 2>&1 || { tail -60 $OUT/tests
 tail -1 $OUT/tests.log
 STRANDED=1 timeout -k 10 300 python3 tools/diag_readset.py c5 12 > $OUT/readset_c5.log 2>&1 || { tail $OUT/readset_c5.log; exit 1; }
 grep rep $OUT/readset_c5.log
+RCP_LIB_PATH=build_var/pool200/librecoup_amd.so STRANDED=1 timeout -k 10 300 python3 tools/diag_readset.py c5 12 > $OUT/readset_c5_pool200.log 2>&1 || { tail $OUT/readset_c5_pool200.log; exit 1; }
+grep rep $OUT/readset_c5_pool200.log
 for v in new ks2off wpe5 nopre l1 l2 l4 l8; do
   lib=build_var/$v/librecoup_amd.so
   [ $v = new ] && lib=recoup_amd/librecoup_amd.so

@@ -159,13 +159,15 @@ struct RcpPlanDev {
     int32_t multi_rows;         // 1: some row is a list of ranges (locate's pair loop does the work)
     int32_t lpt_cap;            // items per class list (>= the plan's item count)
     int32_t* item_order;        // [RCP_LPT_CLASSES][lpt_cap]
-    // row-wave kernel (lean == 3): its rows' bins go row-major into rm (n_rows x n_cols, whole
-    // lines per row); the last wave to finish a 16-row tile writes the tile's rows of every
-    // column into the R column-major output as whole 128-B lines (a row-wave store straight
-    // into the column-major matrix is 8 bytes per 128-B line)
-    double* rm;                 // nullptr: direct column-major stores (or rows_lds)
-    // rows_lds > 0: the tiles' bin numerators are staged in LDS instead (rows_lds = the stage's
-    // row stride in words, == 4 mod 64); the flush divides them as the pile would have
+    // row-wave kernel (lean == 3): the bin numerators of its rows are staged (uint32, whole
+    // rows) and the last wave to finish a 16-row tile divides them and writes the tile's rows of
+    // every column into the R column-major output as whole 128-B lines (a row-wave store
+    // straight into the column-major matrix is 8 bytes per 128-B line).  The stage is in LDS
+    // when two 16-row slots fit (rows_lds = its row stride in words, == 4 mod 64), else
+    // row-major in HBM: rm32 [n_rows][n_cols] with the rows' part info rinfo [n_rows][8]
+    // ({bin width, layout}; width 0: zeros, -1: left to the interpolation kernel)
+    uint32_t* rm32;
+    int2* rinfo;
     int32_t rows_lds;
     // coverage (CSR) mode
     const int64_t* csr_off;     // non-null: write per-row depth into csr (calcCoverage)

@@ -79,7 +79,9 @@ constexpr int kLeanMinRowsBinned = RCP_LEAN_MIN_ROWS_BINNED;
 #define RCP_ROWS_AUTO 1  // plans with multi-range rows take the row-wave pileup kernel
 #endif
 #ifndef RCP_ROWS_LDS
-#define RCP_ROWS_LDS 1   // row-wave plans stage their tiles in LDS when 16 rows of bins fit
+#define RCP_ROWS_LDS 0   // 1: row-wave plans stage their tiles in LDS when two 16-row slots fit
+                         // (one 8-wave workgroup per CU: C3 0.73 ms vs 0.57 staged in HBM,
+                         // profiles/r04/r4j/c3.log)
 #endif
 
 extern "C" {
@@ -1554,11 +1556,13 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.csr_rs = nullptr;
     P.csr_sub = nullptr;
     P.csr_sub_off = nullptr;
-    // row-wave plans stage their bins row-major (whole lines per row) and transpose once
-    P.rm = nullptr;
+    // row-wave plans whose tile stage does not fit LDS stage their bin numerators row-major
+    P.rm32 = nullptr;
+    P.rinfo = nullptr;
     if (P.lean == 3 && P.rows_lds == 0 && R > 0 && P.n_cols > 0) {
-        HIP_TRY(plan->rm.alloc(8 * (size_t)R * (size_t)P.n_cols));
-        P.rm = plan->rm.as<double>();
+        HIP_TRY(plan->rm.alloc(4 * (size_t)R * (size_t)P.n_cols + 8 * (size_t)R * RCP_MAX_PARTS));
+        P.rinfo = plan->rm.as<int2>();
+        P.rm32 = reinterpret_cast<uint32_t*>(P.rinfo + (size_t)R * RCP_MAX_PARTS);
     }
     plan->lds = P.lean == 4 ? rcp_pileup_bins_lds_bytes(&P)
                 : P.lean == 3 ? rcp_pileup_rows_lds_bytes(&P)
@@ -1962,6 +1966,7 @@ int calc_coverage_dev(rcp_plan* plan, const int64_t* d_off, int32_t* d_cov, uint
     P.n_chunks_total = pt.n_chunks;
     P.crange = nullptr;  // sized for the plan's chunks, not these
     P.cw_len = -1;
+    P.lean = 0;  // the general kernel's CSR mode (locate writes every side output)
     P.csr_off = d_off;
     P.csr_out = d_cov;
     P.valid_out = d_valid;
@@ -1993,6 +1998,7 @@ int coverage_starts_dev(rcp_plan* plan, const int64_t* d_off, const int64_t* d_s
     P.n_chunks_total = pt.n_chunks;
     P.crange = nullptr;
     P.cw_len = -1;
+    P.lean = 0;
     P.csr_off = d_off;
     P.csr_out = nullptr;
     P.valid_out = d_valid;

@@ -941,12 +941,8 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
             if (sl < 0 && q == 0) maxend[g] = P.pmax[hi - 1];
             if (q == 0) ncand = hi - lo;
         }
-#if !(RCP_LOC_ABL & 1)
-        if (q == 0) {
-            P.seg_lo[j0 * 3] = lo;
-            P.seg_hi[j0 * 3] = hi;
-        }
-#endif
+        // (P.seg_lo / seg_hi of the row: written below, once the heavy slot is known -- the
+        // lean and bin-difference kernels read fast rows' ranges from the record)
         if (q != 0) lo = hi = 0;  // the quad combine below reads (lo, hi) from lane 0
     }
     // (segment, stream) pairs dealt round-robin to the quad; a lane's two pairs of one round
@@ -1051,11 +1047,15 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
         }
     }
     int32_t slot = -1;
+    // side outputs a fast row needs only on the heavy path when the pileup is a lean or
+    // bin-difference kernel (they read the record): its (lo, hi) in seg_lo / seg_hi and ncand,
+    // for rcp_heavy_pileup_kernel (4 scattered stores per row fewer: C4 locate -14 us,
+    // profiles/r04/r4j/ab.log l1)
+    const bool rec_only = fast && (P.lean == 1 || P.lean == 2 || P.lean == 4);
     if (in_row && q == 0) {
 #if !(RCP_LOC_ABL & 1)
         P.valid[r] = valid ? 1 : 0;
         if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
-        P.ncand[r] = ncand;
 #endif
         // skewed rows only: many candidates per column chunk (each chunk of a row is one
         // wave's work) AND a deep pileup (> 2 reads per position), so a long row with
@@ -1072,7 +1072,13 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
             }
         }
 #if !(RCP_LOC_ABL & 1)
-        P.heavy_slot[r] = slot;
+        if (!rec_only || slot >= 0) {
+            P.ncand[r] = ncand;
+            if (split1) {
+                P.seg_lo[j0 * 3] = lo0;
+                P.seg_hi[j0 * 3] = hi0;
+            }
+        }
 #endif
     }
     slot = qperm<0x00>(slot);
@@ -1996,9 +2002,9 @@ extern "C" int rcp_rows_lds_stride(int64_t n_cols) {
     return rows_lds_bytes((int)ldw, kRLWaves, RowWin<kRLSh>::words, kRLSlots) <= 160 * 1024 ? (int)ldw : 0;
 }
 
-// Stores of a row's bins: row-major into the staging (P.rm, whole lines per row), or -- with
-// binsum, which keeps the column-major layout -- 8 bytes per 128-B column line; the 16 rows of a
-// line are claimed together by waves of one XCD, so plain stores meet in that L2.
+// Stores of a row's bins without a stage (binsum, which keeps the column-major layout): 8 bytes
+// per 128-B column line; the 16 rows of a line are claimed together by waves of one XCD, so
+// plain stores meet in that L2.
 __device__ __forceinline__ void rows_store(double x, double* p) { *p = x; }
 
 // a bin's mean from its numerator: the same operations in the same order wherever it is made
@@ -2010,9 +2016,10 @@ __device__ __forceinline__ double rows_mean(uint32_t num, double sc, bool pow2, 
     return rcp_div_rn((double)num * sc, dd1, rdd1);  // w == bs + 1
 }
 
-// LDS = 1: bins staged in LDS (P.rows_lds, never with binsum); LDS = 0: P.rm staging or, with
-// binsum / no P.rm, direct column-major stores
-template <int LDS, int WAVES, int SH>
+// MODE 2: bin numerators staged in LDS slots (P.rows_lds); 1: in the row-major HBM stage
+// P.rm32 (row stride n_cols, part info P.rinfo); 0 (binsum): means stored straight into the
+// column-major output.  Staged tiles are flushed by the last wave to finish one of their rows.
+template <int MODE, int WAVES, int SH>
 __global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(16 / WAVES)))
 rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restrict__ binsum) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2035,6 +2042,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     constexpr uint32_t kEmpty = 0xFFFFFFFEu, kDone = 0xFFFFFFFFu;
     // tile slots of the flush: tile id, rows finished (kFree: flushed),
     // and the workgroup's tile sequence number (slot = seq % kSlots)
+    constexpr bool LDS = MODE == 2;
     constexpr int kSlots = LDS ? kRLSlots : 4;
     static_assert(8 + 8 * kSlots + 4 <= (int)kRowsQueueBytes, "slot table");
     constexpr uint32_t kFree = 0xFFFFFFFFu;
@@ -2043,9 +2051,16 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     uint32_t* seq = slot_cnt + kSlots;
     // LDS stage: [slot][row of the tile][ldw] numerators, then [slot][row][part] {bs, lay}
     // (bs 0: zeros, -1: left to the interpolation kernel)
-    const int ldw = LDS ? P.rows_lds : 0;
+    const int ldw = LDS ? P.rows_lds : (MODE == 1 ? (int)P.n_cols : 0);
     uint32_t* lstage = reinterpret_cast<uint32_t*>(smem + 4 * WAVES * kWords + kRowsQueueBytes);
     int2* linfo = reinterpret_cast<int2*>(lstage + (size_t)kSlots * kTile * ldw);
+    // row r's staged numerators and part info
+    auto stage_row = [&](int r, int sl) -> uint32_t* {
+        return LDS ? lstage + (size_t)(sl * kTile + (r & (kTile - 1))) * ldw : P.rm32 + (size_t)r * ldw;
+    };
+    auto stage_info = [&](int r, int sl) -> int2* {
+        return LDS ? linfo + (sl * kTile + (r & (kTile - 1))) * RCP_MAX_PARTS : P.rinfo + (size_t)r * RCP_MAX_PARTS;
+    };
     if (threadIdx.x == 0) *queue = ((unsigned long long)kEmpty << 32) | kTile;
     if (threadIdx.x < kSlots) {
         slot_tile[threadIdx.x] = kDone;
@@ -2053,8 +2068,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     }
     if (threadIdx.x == 0) *seq = 0;
     __syncthreads();
-    double* const rm = (binsum || LDS) ? nullptr : P.rm;
-    const bool staged = LDS || rm != nullptr;
+    constexpr bool staged = MODE != 0;
     auto fetch_tile = [&]() -> uint32_t {
         for (int k = 0; k < 8; ++k) {
             const int xs = (xcd + k) & 7;
@@ -2102,30 +2116,26 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                 __builtin_amdgcn_s_sleep(2);
         }
     };
-    // the matrix cell (row r, column c): row-major staging (P.rm, written into the column-major
-    // output tile by tile: a row's bins are whole lines) or, with binsum, the output itself
-    auto cell = [&](int r, int64_t c) -> double* {
-        return rm ? rm + (size_t)r * (size_t)P.n_cols + (size_t)c : out + (size_t)c * R + r;
-    };
+    // the matrix cell (row r, column c) of the unstaged mode (binsum)
+    auto cell = [&](int r, int64_t c) -> double* { return out + (size_t)c * R + r; };
     auto zero_cols = [&](int r, const RcpPart& part, int32_t n) {
-        if (LDS) return;  // the row's part info says zeros
+        if (staged) return;  // the row's part info says zeros
         for (int32_t k = lane; k < n; k += 64) {
             rows_store(0.0, cell(r, part.col_off + k));
             if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = 0;
         }
     };
     // the last wave to finish a row of tile T writes the tile's 16 rows of every column from the
-    // row-major staging as whole 128-B column lines (release / acquire: the other waves' staging
-    // stores are visible to it); lane = (row i, column quarter): 4 columns x 16 rows per store
+    // stage as whole 128-B column lines (release / acquire: the other waves' staging stores are
+    // visible to it); lane = (row i, column quarter): 4 columns x 16 rows per store
     auto flush = [&](uint32_t T, int sl) {
         const int32_t t16 = (int32_t)T * kTile;
         const int32_t nrow = min(kTile, P.n_rows - t16);
         const int i = lane & 15, cq = lane >> 4;
-        const int64_t nc = P.n_cols;
-        if (LDS) {
+        {
             // numerators -> means (the pile's operations), 4 columns x 16 rows per store
-            const uint32_t* srow = lstage + (size_t)(sl * kTile + i) * ldw;
-            const int2* inf = linfo + (sl * kTile + i) * RCP_MAX_PARTS;
+            const uint32_t* srow = stage_row(t16 + i, sl);
+            const int2* inf = stage_info(t16 + i, sl);
             const double sc = P.scale;
             for (int p = 0; p < P.n_parts; ++p) {
                 const int32_t n = P.part[p].n_bins, c0p = P.part[p].col_off;
@@ -2152,21 +2162,6 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                             __builtin_nontemporal_store(v[u], out + (size_t)(c0p + k) * R + (size_t)(t16 + i));
                     }
                 }
-            }
-            return;
-        }
-        const double* src = rm + (size_t)(t16 + i) * (size_t)nc;
-        for (int64_t c0 = 0; c0 < nc; c0 += 32) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int64_t c = c0 + 4 * u + cq;
-                v[u] = (i < nrow && c < nc) ? src[c] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int64_t c = c0 + 4 * u + cq;
-                if (i < nrow && c < nc) __builtin_nontemporal_store(v[u], out + (size_t)c * R + (size_t)(t16 + i));
             }
         }
     };
@@ -2195,9 +2190,9 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         const int32_t flags = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.x);
         const int32_t nr = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.y);
         const int32_t heavy = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.z);
-        uint32_t* const srow = lstage + (size_t)(sl * kTile + (r & (kTile - 1))) * ldw;
-        int2* const sinfo = linfo + (sl * kTile + (r & (kTile - 1))) * RCP_MAX_PARTS;
-        if (LDS && lane < P.n_parts) sinfo[lane] = make_int2(0, -1);  // zeros unless piled below
+        uint32_t* const srow = stage_row(r, sl);
+        int2* const sinfo = stage_info(r, sl);
+        if (staged && lane < P.n_parts) sinfo[lane] = make_int2(0, -1);  // zeros unless piled below
         if (!(flags & RCP_REC_VALID)) {  // NULL row -> zeros (profile.R:191-197)
             for (int p = 0; p < P.n_parts; ++p) zero_cols(r, P.part[p], P.part[p].n_bins);
             return;
@@ -2231,7 +2226,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             rcp_part_slice(part, nr, &head, &L);
             const int32_t n = part.n_bins;
             if (!part.per_base && L < n) {  // interpolation row: rcp_interp_kernel
-                if (LDS && lane == 0) sinfo[p] = make_int2(-1, -1);
+                if (staged && lane == 0) sinfo[p] = make_int2(-1, -1);
                 continue;
             }
             if (part.per_base && L != n) {
@@ -2251,7 +2246,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     }
                 }
             }
-            if (LDS && lane == 0) sinfo[p] = make_int2(bs, lay);
+            if (staged && lane == 0) sinfo[p] = make_int2(bs, lay);
             const int32_t kw = max(1, kWinCap / (bs + (lay >= 0 ? 1 : 0)));  // bins per window
             const bool pow2 = lay < 0 && (bs & (bs - 1)) == 0;
             const double dd = (double)bs, rdd = 1.0 / dd;
@@ -2322,7 +2317,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
                     const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
                     const uint32_t num = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
-                    if (LDS) {
+                    if (staged) {
                         srow[part.col_off + k] = num;
                         continue;
                     }
@@ -2957,12 +2952,13 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 // (R/util.R:74-84 with dif = 0, R/profile.R:159-208).  Per row the work is O(n bins) instead
 // of O(L positions) -- C2's 200 bins of 20 bp instead of 4000 positions in four column chunks
 // -- and a whole row is one wave's pass (no column chunks, no per-chunk read ranges).
-// Workgroups of 4 waves own 16-row tiles (one 128-B line of every output column); each wave
-// piles 4 of the rows into its own D / F arrays and stages their numerators; the workgroup
-// then writes the tile column-major.
+// Workgroups of RCP_BD_WAVES waves own 16-row tiles (one 128-B line of every output column);
+// each wave piles its rows into its own D / F arrays and stages their numerators; the
+// workgroup then writes the tile column-major.
 // =================================================================================
 #ifndef RCP_BD_WAVES
-#define RCP_BD_WAVES 4  // waves per 16-row tile (16 / RCP_BD_WAVES rows each)
+#define RCP_BD_WAVES 16  // waves per 16-row tile (16 / RCP_BD_WAVES rows each; C2 pileup 4: 30.8,
+                        // 8: 28.7, 16: 28.1 us, profiles/r04/r4j/ab.log)
 #endif
 constexpr int kBDWaves = RCP_BD_WAVES;
 static_assert(kTile % kBDWaves == 0, "a tile's rows are split evenly over the waves");
@@ -3224,7 +3220,7 @@ __device__ void block_window_depth(const RcpPlanDev& P, int r, int32_t w0, int32
     const int per = (wn + 1 + kBlock - 1) / kBlock;
     for (int q = threadIdx.x; q < per * kBlock; q += kBlock) diff[q] = 0;
     __syncthreads();
-    const int32_t slot = P.heavy_slot[r];
+    const int32_t slot = P.rec[r].heavy;
     if (slot >= 0) {
         const int32_t* g = P.heavy_gdiff + (size_t)slot * P.heavy_stride;
         if (threadIdx.x == 0) {
@@ -3357,7 +3353,10 @@ extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream)
     const int searches = 2 + (P->crange ? 2 * (P->n_chunks_total - 1) : 0);  // a single-range row's
     if (RCP_LOC_KS8 && P->crange && 2 * P->n_chunks_total > 4 * 4)
         hipLaunchKernelGGL((rcp_locate_kernel<8, 4>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
-    else if (RCP_LOC_KS2 && searches <= 2 * 4 && !P->multi_rows)
+    // (occupancy pays on big tables -- C4: 100 -> 91 us -- and plans without chunk searches,
+    // C2: 33 -> 30 us; the 25k-row C4 shard runs in one generation anyway and measured 4 us
+    // slower: profiles/r04/r4j/ab.log new vs ks2off)
+    else if (RCP_LOC_KS2 && searches <= 2 * 4 && !P->multi_rows && (!P->crange || P->n_rows >= 50000))
         hipLaunchKernelGGL((rcp_locate_kernel<2, 2>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
     else
         hipLaunchKernelGGL((rcp_locate_kernel<4, 4>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
@@ -3476,7 +3475,7 @@ static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* 
     const int64_t tiles = ((int64_t)P->n_rows + kTile - 1) / kTile;  // at least a tile per workgroup
     if (P->rows_lds > 0 && !binsum) {
         const size_t lds = rcp_pileup_rows_lds_bytes(P);
-        auto k = rcp_pileup_rows_kernel<1, kRLWaves, kRLSh>;
+        auto k = rcp_pileup_rows_kernel<2, kRLWaves, kRLSh>;
         const hipError_t e = allow_big_lds(k);
         if (e != hipSuccess) return e;
         const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / kRLWaves, (160 * 1024) / lds));
@@ -3487,8 +3486,12 @@ static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* 
     RcpPlanDev Q = *P;
     Q.rows_lds = 0;
     const int64_t grid = std::min<int64_t>(((int64_t)4 * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
-    hipLaunchKernelGGL((rcp_pileup_rows_kernel<0, kRWaves, kRWSh>), dim3((unsigned)grid), dim3(64 * kRWaves),
-                       rcp_pileup_rows_lds_bytes(&Q), s, Q, out, binsum);
+    if (binsum || !P->rm32)
+        hipLaunchKernelGGL((rcp_pileup_rows_kernel<0, kRWaves, kRWSh>), dim3((unsigned)grid), dim3(64 * kRWaves),
+                           rcp_pileup_rows_lds_bytes(&Q), s, Q, out, binsum);
+    else
+        hipLaunchKernelGGL((rcp_pileup_rows_kernel<1, kRWaves, kRWSh>), dim3((unsigned)grid), dim3(64 * kRWaves),
+                           rcp_pileup_rows_lds_bytes(&Q), s, Q, out, binsum);
     return hipGetLastError();
 }
 

@@ -168,6 +168,7 @@ struct RcpPlanDev {
     // ({bin width, layout}; width 0: zeros, -1: left to the interpolation kernel)
     uint32_t* rm32;
     int2* rinfo;
+    double* rm64;               // (RCP_ROWS_STAGE 3) the means themselves, [n_rows][n_cols]
     int32_t rows_lds;
     // coverage (CSR) mode
     const int64_t* csr_off;     // non-null: write per-row depth into csr (calcCoverage)

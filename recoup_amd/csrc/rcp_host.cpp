@@ -1557,12 +1557,21 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.csr_sub = nullptr;
     P.csr_sub_off = nullptr;
     // row-wave plans whose tile stage does not fit LDS stage their bin numerators row-major
+#ifndef RCP_ROWS_STAGE
+#define RCP_ROWS_STAGE 1  // 1: uint32 numerators (divided at the flush), 3: the fp64 means
+#endif
     P.rm32 = nullptr;
     P.rinfo = nullptr;
+    P.rm64 = nullptr;
     if (P.lean == 3 && P.rows_lds == 0 && R > 0 && P.n_cols > 0) {
-        HIP_TRY(plan->rm.alloc(4 * (size_t)R * (size_t)P.n_cols + 8 * (size_t)R * RCP_MAX_PARTS));
-        P.rinfo = plan->rm.as<int2>();
-        P.rm32 = reinterpret_cast<uint32_t*>(P.rinfo + (size_t)R * RCP_MAX_PARTS);
+        if (RCP_ROWS_STAGE == 3) {
+            HIP_TRY(plan->rm.alloc(8 * (size_t)R * (size_t)P.n_cols));
+            P.rm64 = plan->rm.as<double>();
+        } else {
+            HIP_TRY(plan->rm.alloc(4 * (size_t)R * (size_t)P.n_cols + 8 * (size_t)R * RCP_MAX_PARTS));
+            P.rinfo = plan->rm.as<int2>();
+            P.rm32 = reinterpret_cast<uint32_t*>(P.rinfo + (size_t)R * RCP_MAX_PARTS);
+        }
     }
     plan->lds = P.lean == 4 ? rcp_pileup_bins_lds_bytes(&P)
                 : P.lean == 3 ? rcp_pileup_rows_lds_bytes(&P)

@@ -1984,6 +1984,9 @@ constexpr int kRWCap = RowWin<kRWSh>::cap;
 #define RCP_RWL_SLOTS 2
 #endif
 constexpr int kRLWaves = RCP_RWL_WAVES, kRLSh = RCP_RWL_SH, kRLSlots = RCP_RWL_SLOTS;
+#ifndef RCP_RWG_WAVES
+#define RCP_RWG_WAVES 4  // waves per workgroup of the HBM-staged variants (16 per CU either way)
+#endif
 constexpr size_t kRowsQueueBytes = 64;  // tile queue word + slot table
 
 extern "C" int rcp_rows_window_cap(void) { return kRWCap; }
@@ -2017,10 +2020,11 @@ __device__ __forceinline__ double rows_mean(uint32_t num, double sc, bool pow2, 
 }
 
 // MODE 2: bin numerators staged in LDS slots (P.rows_lds); 1: in the row-major HBM stage
-// P.rm32 (row stride n_cols, part info P.rinfo); 0 (binsum): means stored straight into the
-// column-major output.  Staged tiles are flushed by the last wave to finish one of their rows.
+// P.rm32 (row stride n_cols, part info P.rinfo); 3: the means themselves (doubles) in the HBM
+// stage P.rm64; 0 (binsum): means stored straight into the column-major output.  Staged tiles
+// are flushed by the last wave to finish one of their rows.
 template <int MODE, int WAVES, int SH>
-__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(16 / WAVES)))
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? (WAVES + 3) / 4 : 4)))
 rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restrict__ binsum) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int kWinCap = RowWin<SH>::cap, kWords = RowWin<SH>::words;
@@ -2051,12 +2055,13 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     uint32_t* seq = slot_cnt + kSlots;
     // LDS stage: [slot][row of the tile][ldw] numerators, then [slot][row][part] {bs, lay}
     // (bs 0: zeros, -1: left to the interpolation kernel)
-    const int ldw = LDS ? P.rows_lds : (MODE == 1 ? (int)P.n_cols : 0);
+    const int ldw = LDS ? P.rows_lds : (MODE == 1 || MODE == 3 ? (int)P.n_cols : 0);
     uint32_t* lstage = reinterpret_cast<uint32_t*>(smem + 4 * WAVES * kWords + kRowsQueueBytes);
     int2* linfo = reinterpret_cast<int2*>(lstage + (size_t)kSlots * kTile * ldw);
     // row r's staged numerators and part info
     auto stage_row = [&](int r, int sl) -> uint32_t* {
-        return LDS ? lstage + (size_t)(sl * kTile + (r & (kTile - 1))) * ldw : P.rm32 + (size_t)r * ldw;
+        return LDS ? lstage + (size_t)(sl * kTile + (r & (kTile - 1))) * ldw
+                   : (MODE == 1 ? P.rm32 + (size_t)r * ldw : nullptr);
     };
     auto stage_info = [&](int r, int sl) -> int2* {
         return LDS ? linfo + (sl * kTile + (r & (kTile - 1))) * RCP_MAX_PARTS : P.rinfo + (size_t)r * RCP_MAX_PARTS;
@@ -2119,6 +2124,10 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     // the matrix cell (row r, column c) of the unstaged mode (binsum)
     auto cell = [&](int r, int64_t c) -> double* { return out + (size_t)c * R + r; };
     auto zero_cols = [&](int r, const RcpPart& part, int32_t n) {
+        if (MODE == 3) {
+            for (int32_t k = lane; k < n; k += 64) P.rm64[(size_t)r * ldw + part.col_off + k] = 0.0;
+            return;
+        }
         if (staged) return;  // the row's part info says zeros
         for (int32_t k = lane; k < n; k += 64) {
             rows_store(0.0, cell(r, part.col_off + k));
@@ -2132,7 +2141,22 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         const int32_t t16 = (int32_t)T * kTile;
         const int32_t nrow = min(kTile, P.n_rows - t16);
         const int i = lane & 15, cq = lane >> 4;
-        {
+        if (MODE == 3) {
+            const double* src = P.rm64 + (size_t)(t16 + i) * (size_t)ldw;
+            for (int32_t c0 = 0; c0 < ldw; c0 += 32) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int32_t c = c0 + 4 * u + cq;
+                    v[u] = (i < nrow && c < ldw) ? src[c] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int32_t c = c0 + 4 * u + cq;
+                    if (i < nrow && c < ldw) __builtin_nontemporal_store(v[u], out + (size_t)c * R + (size_t)(t16 + i));
+                }
+            }
+        } else {
             // numerators -> means (the pile's operations), 4 columns x 16 rows per store
             const uint32_t* srow = stage_row(t16 + i, sl);
             const int2* inf = stage_info(t16 + i, sl);
@@ -2192,7 +2216,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         const int32_t heavy = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.z);
         uint32_t* const srow = stage_row(r, sl);
         int2* const sinfo = stage_info(r, sl);
-        if (staged && lane < P.n_parts) sinfo[lane] = make_int2(0, -1);  // zeros unless piled below
+        if (staged && MODE != 3 && lane < P.n_parts) sinfo[lane] = make_int2(0, -1);  // zeros unless piled below
         if (!(flags & RCP_REC_VALID)) {  // NULL row -> zeros (profile.R:191-197)
             for (int p = 0; p < P.n_parts; ++p) zero_cols(r, P.part[p], P.part[p].n_bins);
             return;
@@ -2226,7 +2250,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             rcp_part_slice(part, nr, &head, &L);
             const int32_t n = part.n_bins;
             if (!part.per_base && L < n) {  // interpolation row: rcp_interp_kernel
-                if (staged && lane == 0) sinfo[p] = make_int2(-1, -1);
+                if (staged && MODE != 3 && lane == 0) sinfo[p] = make_int2(-1, -1);
                 continue;
             }
             if (part.per_base && L != n) {
@@ -2246,7 +2270,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     }
                 }
             }
-            if (staged && lane == 0) sinfo[p] = make_int2(bs, lay);
+            if (staged && MODE != 3 && lane == 0) sinfo[p] = make_int2(bs, lay);
             const int32_t kw = max(1, kWinCap / (bs + (lay >= 0 ? 1 : 0)));  // bins per window
             const bool pow2 = lay < 0 && (bs & (bs - 1)) == 0;
             const double dd = (double)bs, rdd = 1.0 / dd;
@@ -2317,6 +2341,10 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
                     const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
                     const uint32_t num = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
+                    if (MODE == 3) {
+                        P.rm64[(size_t)r * ldw + part.col_off + k] = rows_mean(num, sc, pow2, b - a, bs, dd, rdd, dd1, rdd1);
+                        continue;
+                    }
                     if (staged) {
                         srow[part.col_off + k] = num;
                         continue;
@@ -3485,13 +3513,22 @@ static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* 
     }
     RcpPlanDev Q = *P;
     Q.rows_lds = 0;
-    const int64_t grid = std::min<int64_t>(((int64_t)4 * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
-    if (binsum || !P->rm32)
+    if (binsum || (!P->rm32 && !P->rm64)) {
+        const int64_t grid = std::min<int64_t>(((int64_t)4 * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
         hipLaunchKernelGGL((rcp_pileup_rows_kernel<0, kRWaves, kRWSh>), dim3((unsigned)grid), dim3(64 * kRWaves),
                            rcp_pileup_rows_lds_bytes(&Q), s, Q, out, binsum);
-    else
-        hipLaunchKernelGGL((rcp_pileup_rows_kernel<1, kRWaves, kRWSh>), dim3((unsigned)grid), dim3(64 * kRWaves),
-                           rcp_pileup_rows_lds_bytes(&Q), s, Q, out, binsum);
+        return hipGetLastError();
+    }
+    // HBM stage: 16 waves per CU, as RCP_RWG_WAVES-wave workgroups
+    constexpr int kG = RCP_RWG_WAVES;
+    auto k = P->rm64 ? rcp_pileup_rows_kernel<3, kG, kRWSh> : rcp_pileup_rows_kernel<1, kG, kRWSh>;
+    const size_t lds = rows_lds_bytes(0, kG, RowWin<kRWSh>::words, 0);
+    if (lds > 64 * 1024) {
+        const hipError_t e = allow_big_lds(k);
+        if (e != hipSuccess) return e;
+    }
+    const int64_t grid = std::min<int64_t>(((int64_t)(16 / kG) * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * kG), lds, s, Q, out, binsum);
     return hipGetLastError();
 }
 

@@ -1,0 +1,24 @@
+#!/bin/bash
+# round 4: row-wave HBM stage variants on C3 -- numerators (s1) vs fp64 means (s3), 4- vs
+# 16-wave workgroups; row tests on each; PMC traffic of the two fastest
+OUT=gpurun_out/r4m
+mkdir -p $OUT
+export TMPDIR=/tmp
+T="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
+for v in new s1w16 s3w4 s3w16; do
+  lib=build_var/$v/librecoup_amd.so
+  [ $v = new ] && lib=recoup_amd/librecoup_amd.so
+  RCP_LIB_PATH=$lib timeout -k 10 300 $T -m gpu tests/test_gpu_rows.py > $OUT/rows_$v.log 2>&1 || { tail -40 $OUT/rows_$v.log; exit 1; }
+  echo "$v $(tail -1 $OUT/rows_$v.log)"
+done
+for v in new s1w16 s3w4 s3w16 rowsg new s1w16 s3w4 s3w16 rowsg; do
+  lib=build_var/$v/librecoup_amd.so
+  [ $v = new ] && lib=recoup_amd/librecoup_amd.so
+  echo "== $v" >> $OUT/c3.log
+  RCP_LIB_PATH=$lib CFG=c3 timeout -k 10 200 python3 tools/diag_shard_kernels.py 0/1 auto >> $OUT/c3.log 2>&1 || { tail $OUT/c3.log; exit 1; }
+done
+grep -E "==|ms/pass" $OUT/c3.log
+for v in s1w16 s3w16; do
+  RCP_LIB_PATH=build_var/$v/librecoup_amd.so PASSES=traffic timeout -k 10 600 bash tools/pmc.sh $OUT/pmc_$v c3 || { tail $OUT/pmc_$v/*.log; exit 1; }
+  python3 tools/pmc_traffic.py $OUT/pmc_$v $OUT/traffic_$v.json profiles/fetch_calib.json | grep -E "hbm_bytes|fetch_bytes|write_bytes" || exit 1
+done

@@ -118,6 +118,7 @@ struct RcpPlanDev {
     int32_t n_chunks_total;     // sum over parts (workgroups per row tile)
     const int32_t* lay_index;   // per part: [n_bins] dif -> offset into lay_cnt (-1 = none)
     const int32_t* lay_cnt;     // prefix counts of enlarged bins (n_bins + 1 per layout)
+    const uint32_t* lay_bit;    // the same as bit masks, word lay + j = bins 32 j .. 32 j + 31 (plans only)
     int32_t stat;               // 0 mean, 1 median
     double scale;
     int64_t n_cols;

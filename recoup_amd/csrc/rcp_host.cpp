@@ -865,6 +865,7 @@ struct Builder {
     std::vector<uint8_t> row_static;
     std::vector<RcpSeg> segs;
     std::vector<int32_t> lay_index, lay_cnt;
+    std::vector<std::pair<int32_t, int32_t>> lay_regions;  // (offset in lay_cnt, n bins)
     std::vector<int32_t> interp_row, interp_part, interp_mode, interp_pos, nb_pos;
 };
 
@@ -1145,6 +1146,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
                             const std::vector<int32_t> cnt = rcp::bin_layout_counts(pt.n_bins, dif, rounding);
                             const int32_t o = (int32_t)B.lay_cnt.size();
                             B.lay_cnt.insert(B.lay_cnt.end(), cnt.begin(), cnt.end());
+                            B.lay_regions.emplace_back(o, pt.n_bins);
                             layout_cache[key] = o;
                             slot = o;
                         } else {
@@ -1383,6 +1385,13 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     const size_t o_segs = blob.add(B.segs);
     const size_t o_lay_index = blob.add(B.lay_index);
     const size_t o_lay_cnt = blob.add(B.lay_cnt);
+    // the same layouts as bit masks (word lay + j: bins 32 j .. 32 j + 31 enlarged), indexed
+    // like lay_cnt: one load per 32 bins where the row-wave flush needs the bin widths
+    std::vector<uint32_t> lay_bit(B.lay_cnt.size(), 0u);
+    for (const auto& rg : B.lay_regions)
+        for (int32_t k = 0; k < rg.second; ++k)
+            if (B.lay_cnt[rg.first + k + 1] != B.lay_cnt[rg.first + k]) lay_bit[rg.first + (k >> 5)] |= 1u << (k & 31);
+    const size_t o_lay_bit = blob.add(lay_bit);
     const size_t o_irow = blob.add(B.interp_row);
     const size_t o_ipart = blob.add(B.interp_part);
     const size_t o_imode = blob.add(B.interp_mode);
@@ -1542,6 +1551,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.status_prev = plan->status_sets + RCP_STATUS_WORDS;
     P.lay_index = reinterpret_cast<const int32_t*>(base + o_lay_index);
     P.lay_cnt = reinterpret_cast<const int32_t*>(base + o_lay_cnt);
+    P.lay_bit = reinterpret_cast<const uint32_t*>(base + o_lay_bit);
     P.n_interp = n_interp;
     P.interp_row = reinterpret_cast<const int32_t*>(base + o_irow);
     P.interp_part = reinterpret_cast<const int32_t*>(base + o_ipart);

@@ -1984,8 +1984,13 @@ constexpr int kRWCap = RowWin<kRWSh>::cap;
 #define RCP_RWL_SLOTS 2
 #endif
 constexpr int kRLWaves = RCP_RWL_WAVES, kRLSh = RCP_RWL_SH, kRLSlots = RCP_RWL_SLOTS;
+#ifndef RCP_RWG_SLOTS
+#define RCP_RWG_SLOTS 4  // tiles in flight per workgroup (<= 6)
+#endif
 #ifndef RCP_RWG_WAVES
-#define RCP_RWG_WAVES 4  // waves per workgroup of the HBM-staged variants (16 per CU either way)
+#define RCP_RWG_WAVES 16  // waves per workgroup of the HBM-staged variants (16 per CU either way;
+                          // one 16-wave workgroup per CU keeps fewer tiles in flight: C3 pileup
+                          // 0.573 -> 0.495 ms with fp64 staging, profiles/r04/r4m/c3.log)
 #endif
 constexpr size_t kRowsQueueBytes = 64;  // tile queue word + slot table
 
@@ -2047,7 +2052,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     // tile slots of the flush: tile id, rows finished (kFree: flushed),
     // and the workgroup's tile sequence number (slot = seq % kSlots)
     constexpr bool LDS = MODE == 2;
-    constexpr int kSlots = LDS ? kRLSlots : 4;
+    constexpr int kSlots = LDS ? kRLSlots : RCP_RWG_SLOTS;
     static_assert(8 + 8 * kSlots + 4 <= (int)kRowsQueueBytes, "slot table");
     constexpr uint32_t kFree = 0xFFFFFFFFu;
     uint32_t* slot_tile = reinterpret_cast<uint32_t*>(queue + 1);
@@ -2169,13 +2174,15 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                 const double dd = (double)bs, rdd = 1.0 / dd;
                 const double dd1 = (double)(bs + 1), rdd1 = 1.0 / dd1;
                 for (int32_t k0 = 0; k0 < n; k0 += 32) {
+                    // enlarged bins of the 32 columns (R-RNG layout) as one mask word
+                    const uint32_t bits = (f.x > 0 && lay >= 0) ? P.lay_bit[lay + (k0 >> 5)] : 0u;
                     double v[8];
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         const int32_t k = k0 + 4 * u + cq;
                         v[u] = 0.0;
                         if (f.x > 0 && k < n) {
-                            const int32_t w = lay >= 0 ? bs + P.lay_cnt[lay + k + 1] - P.lay_cnt[lay + k] : bs;
+                            const int32_t w = bs + (int32_t)((bits >> (4 * u + cq)) & 1u);
                             v[u] = rows_mean(srow[c0p + k], sc, pow2, w, bs, dd, rdd, dd1, rdd1);
                         }
                     }

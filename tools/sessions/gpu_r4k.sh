@@ -24,3 +24,5 @@ for r in csv.DictReader(open(sys.argv[1])):
         print(r['Name'][:60], r['Calls'], round(float(r['AverageNs']) / 1000, 2), 'us')
 PY
 done
+STRANDED=1 timeout -k 10 300 python3 tools/diag_readset.py c4 8 > $OUT/readset_c4.log 2>&1 || { tail $OUT/readset_c4.log; exit 1; }
+grep rep $OUT/readset_c4.log

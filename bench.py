@@ -250,6 +250,9 @@ def main():
     # D HIP streams; step k is one complete pass of sample k % D.  Passes are independent, so
     # with D = 2 one sample's locate / heavy launches and its pileup's tail overlap another's
     # pileup.  D = 1 (the default) is one sample, pass after pass.
+    # D = 1 runs `plan` (built alone); D > 1 runs one plan per sample built with
+    # concurrent = dmax (rcp_plan_opts.concurrent: persistent pileup grids leave 1/8 of the
+    # workgroup slots to the other samples' locate / heavy launches)
     plans, outs, valids, rsets = [plan], [out], [valid], [rs]
     streams = [torch.cuda.current_stream()]
     dmax = 4 if args.inflight == "auto" else int(args.inflight)
@@ -259,20 +262,24 @@ def main():
             rk = reads_for_rows(dk["reads"], rows, len(dk["seqlen"])) if s_world > 1 else dk["reads"]
             rsets.append(ReadSet(*rk, dk["seqlen"], device=local))
             del dk, rk
-            p2 = Plan(rsets[-1], rows, bins, out_ld="padded")
-            plans.append(p2)
-            outs.append(p2.empty_output())
             valids.append(torch.empty(max(R, 1), dtype=torch.uint8, device=dev))
+        plans = [Plan(rsets[k], rows, bins, out_ld="padded", concurrent=dmax) for k in range(dmax)]
+        outs = [p.empty_output() for p in plans]
         streams = [torch.cuda.Stream(device=dev) for _ in range(dmax)]
 
     def passes(D, n):
         for k in range(n):
+            if D == 1:
+                plan.execute(out, valid, stream=streams[0])
+                continue
             i = k % D
-            plans[i].execute(outs[i], valids[i], stream=streams[i] if D > 1 else streams[0])
+            plans[i].execute(outs[i], valids[i], stream=streams[i])
 
     # ---- warmup + correctness gate
-    passes(len(plans), max(args.warmup, len(plans)))
-    for p in plans:
+    passes(1, max(args.warmup, 1))
+    if dmax > 1:
+        passes(len(plans), max(args.warmup, len(plans)))
+    for p in plans + [plan]:
         p.status()
     tune = {}
     for d in ([1] + ([2, 3, 4] if args.inflight == "auto" else [])):
@@ -302,7 +309,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
-    for p in plans:
+    for p in plans + [plan]:
         p.status()
     # every sample the timed passes computed, checked bit for bit against an independent plan of
     # its readset on the general pileup kernel (sample 0 is also checked against the oracle below)
@@ -311,7 +318,7 @@ def main():
         ref_plan = Plan(rsets[i], rows, bins, kernel="general", out_ld="padded")
         ref_out = ref_plan.execute()
         ref_plan.status()
-        got = outs[i][:, :R]
+        got = (outs[i] if D > 1 else out)[:, :R]
         inflight_check.append(bool(torch.equal(got.view(torch.int64), ref_out[:, :R].view(torch.int64))))
         del ref_plan, ref_out
 
@@ -404,7 +411,8 @@ def main():
                 "rank0_shard": {"regions": R, "reads": n_reads, "sim_shard": args.sim_shard},
                 "inflight": D,
                 "inflight_note": "samples in flight on separate HIP streams: D distinct samples (independent "
-                                 "read sets, same regions), every step one complete pass of one sample; rank 0's "
+                                 "read sets, same regions), every step one complete pass of one sample (D > 1: "
+                                 "plans built with rcp_plan_opts.concurrent, D = 1: a plan built alone); rank 0's "
                                  "ms per pass by D: " + json.dumps({str(k): round(v, 4) for k, v in tune.items()}),
                 "single_pass_ms": tune[1],
             },

@@ -204,7 +204,13 @@ typedef struct {
                                  * (0 = auto: enough (row tile, chunk) work items for the persistent
                                  * grid -- small row tables, e.g. one GPU's shard, get more chunks so
                                  * the last items do not leave most workgroups idle) */
-    int32_t reserved[3];        /* zero */
+    int32_t concurrent;         /* plans the caller keeps in flight on other streams (0 / 1 = this one
+                                 * alone, e.g. one profileMatrix pass per sample of an input list run
+                                 * on D streams): > 1 makes persistent pileup grids leave 1/8 of the
+                                 * CUs' workgroup slots free, so another sample's locate and heavy
+                                 * launches run beside this pileup (C4, 2 samples in flight:
+                                 * 0.600-0.627 -> 0.580-0.596 ms per pass; alone 0.61 -> 0.67) */
+    int32_t reserved[2];        /* zero */
 } rcp_plan_opts;
 #define RCP_OUT_LD_PADDED (-1)
 RCP_API int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,

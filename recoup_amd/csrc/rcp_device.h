@@ -158,6 +158,7 @@ struct RcpPlanDev {
     // the lean kernel claims items from one counter, highest class first.  0: per-XCD order.
     int32_t lpt;
     int32_t multi_rows;         // 1: some row is a list of ranges (locate's pair loop does the work)
+    int32_t grid_fill;          // eighths of the per-CU workgroup slots persistent pileup grids take
     int32_t lpt_cap;            // items per class list (>= the plan's item count)
     int32_t* item_order;        // [RCP_LPT_CLASSES][lpt_cap]
     // row-wave kernel (lean == 3): the bin numerators of its rows are staged (uint32, whole

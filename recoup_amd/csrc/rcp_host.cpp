@@ -1017,10 +1017,11 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
                                   const rcp_plan_opts* opts, rcp_plan** out) {
     RCP_TRY
     if (!rs || !rows || !out) return fail(RCP_EINVAL, "NULL argument");
-    const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, 0, 0, {0, 0, 0}};
+    const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, 0, 0, 0, {0, 0}};
     if (!opts) opts = &default_opts;
     if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_BINS)
         return fail(RCP_EINVAL, "pileup_kernel = %d", opts->pileup_kernel);
+    if (opts->concurrent < 0) return fail(RCP_EINVAL, "concurrent = %d", opts->concurrent);
     *out = nullptr;
     const rcp_bins_desc coverage_only{};  // bins == NULL: a calcCoverage-only plan
     const bool cov_only = bins == nullptr;
@@ -1058,6 +1059,9 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     RcpPlanDev& P = plan->dev;
     P.multi_rows = 0;
     for (int r = 0; r < R && !P.multi_rows; ++r) P.multi_rows = B.row_seg[r + 1] - B.row_seg[r] > 1;
+    // persistent pileup grids: all workgroup slots alone, 7/8 beside other samples in flight
+    // (rcp_plan_opts.concurrent; profiles/r04/r4p)
+    P.grid_fill = opts->concurrent > 1 ? 7 : 8;
     P.n_parts = bins->n_parts;
     P.stat = bins->stat;
     P.scale = bins->scale;
@@ -1737,7 +1741,7 @@ extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, con
     rcp_plan* plan = nullptr;
     // padded column stride on the device (whole 128-B lines per 16-row column segment); the
     // staged copy drops the padding on the way into R's n_rows x n_cols matrix
-    rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, {0, 0, 0}};
+    rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, 0, {0, 0}};
     int rc = rcp_plan_create_ex(rs, rows, bins, &opts, &plan);
     if (rc) return rc;
     std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
@@ -1835,7 +1839,7 @@ extern "C" int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_sampl
     plans.reserve(n_samples);
     for (int i = 0; i < n_samples; ++i) {
         rcp_plan* plan = nullptr;
-        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, {0, 0, 0}};
+        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, D, {0, 0}};  // D passes in flight
         const int e = rcp_plan_create_ex(readsets[i], rows, bins, &opts, &plan);
         if (e) return e;
         plans.emplace_back(plan, rcp_plan_destroy);
@@ -1926,7 +1930,7 @@ extern "C" int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices
         sub.seg_off = rows->seg_off + r0;
         const rcp_readset* rs = readsets[i];
         rcp_plan* plan = nullptr;
-        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, {0, 0, 0}};
+        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, 0, {0, 0}};
         int e = rcp_plan_create_ex(rs, &sub, bins, &opts, &plan);
         if (e) return e;
         std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);

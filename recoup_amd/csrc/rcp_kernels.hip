@@ -3447,10 +3447,9 @@ static hipError_t launch_pileup_lean_t(const RcpPlanDev* P, double* out, hipStre
     const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
     const int tiles = (P->n_rows + LR * kTile - 1) / (LR * kTile);
     const int64_t items = (int64_t)((tiles + 7) / 8) * 8 * P->n_chunks_total;
-#ifndef RCP_LEAN_FILL
-#define RCP_LEAN_FILL 8  // eighths of the per-CU workgroup slots the persistent grid takes (A/B)
-#endif
-    const int64_t grid = std::min<int64_t>(((int64_t)per_cu * cus * RCP_LEAN_FILL / 8 + 7) / 8 * 8, items);
+    // (P->grid_fill < 8: room for another sample's locate / heavy launches, rcp_plan_opts.concurrent)
+    const int fill = P->grid_fill > 0 && P->grid_fill <= 8 ? P->grid_fill : 8;
+    const int64_t grid = std::min<int64_t>(std::max<int64_t>(((int64_t)per_cu * cus * fill / 8 + 7) / 8 * 8, 8), items);
     hipLaunchKernelGGL((rcp_pileup_lean_kernel<MAXPER, GEN, LR, UNI>), dim3((unsigned)grid), dim3(kLBlock), lds, s, *P,
                        out);
     return hipGetLastError();

@@ -205,6 +205,34 @@ def test_lean_more_column_chunks(gpu, chunks):
     same(more.run(), base.run())
 
 
+def test_lean_concurrent_plans(gpu):
+    """rcp_plan_opts.concurrent: plans built for several samples in flight take 7/8 of the
+    persistent grid's workgroup slots; two such plans on two streams give the bits of plans built
+    alone (binned and per-base), and a negative value is refused."""
+    import torch
+    from recoup_amd._lib import RcpError
+    from recoup_amd.engine import Bins, Plan, ReadSet
+    rng = np.random.default_rng(1234)
+    rs = [ReadSet(*make_reads(rng, 120_000), CHROM_LEN, device=0) for _ in range(2)]
+    rows = single_rows(rng, 700, 2000)
+    for bins in (Bins([("whole", 1000)]), Bins([("whole", 0, 2000)])):
+        alone = [Plan(r, rows, bins, kernel="lean").run() for r in rs]
+        conc = [Plan(r, rows, bins, kernel="lean", concurrent=2) for r in rs]
+        assert all(p.info["pileup_kernel"] == 1 for p in conc)
+        outs = [p.empty_output() for p in conc]
+        streams = [torch.cuda.Stream(device=0) for _ in conc]
+        for _ in range(3):
+            for p, o, st in zip(conc, outs, streams):
+                p.execute(o, stream=st)
+        torch.cuda.synchronize()
+        for p, o, a in zip(conc, outs, alone):
+            p.status()
+            np.testing.assert_array_equal(o.cpu().numpy()[:, :rows.n_rows].view(np.uint64),
+                                          np.ascontiguousarray(a[0]).T.view(np.uint64))
+    with pytest.raises(RcpError):
+        Plan(rs[0], rows, Bins([("whole", 1000)]), concurrent=-1)
+
+
 @pytest.mark.parametrize("stranded,strand_filter", [(False, None), (True, None), (True, "+")])
 @pytest.mark.parametrize("width", [1, 180])
 def test_lean_uniform_width_reads(gpu, stranded, strand_filter, width):

@@ -206,8 +206,9 @@ typedef struct {
                                  * the last items do not leave most workgroups idle) */
     int32_t concurrent;         /* plans the caller keeps in flight on other streams (0 / 1 = this one
                                  * alone, e.g. one profileMatrix pass per sample of an input list run
-                                 * on D streams): > 1 makes persistent pileup grids leave 1/8 of the
-                                 * CUs' workgroup slots free, so another sample's locate and heavy
+                                 * on D streams): > 1 makes the persistent pileup grids (lean,
+                                 * row-wave) leave 1/8 of the CUs' workgroup slots free, so another
+                                 * sample's locate and heavy
                                  * launches run beside this pileup (C4, 2 samples in flight:
                                  * 0.600-0.627 -> 0.580-0.596 ms per pass; alone 0.61 -> 0.67) */
     int32_t reserved[2];        /* zero */

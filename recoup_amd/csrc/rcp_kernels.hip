@@ -3536,7 +3536,9 @@ static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* 
         const hipError_t e = allow_big_lds(k);
         if (e != hipSuccess) return e;
     }
-    const int64_t grid = std::min<int64_t>(((int64_t)(16 / kG) * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
+    const int fill = P->grid_fill > 0 && P->grid_fill <= 8 ? P->grid_fill : 8;  // rcp_plan_opts.concurrent
+    const int64_t grid = std::min<int64_t>(std::max<int64_t>(((int64_t)(16 / kG) * cus * fill / 8 + 7) / 8 * 8, 8),
+                                           (tiles + 7) / 8 * 8);
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * kG), lds, s, Q, out, binsum);
     return hipGetLastError();
 }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4 end: smoke, the measurement set (tools/round_profile.sh: C4 PMC traffic, C4 bench +
 # rocprofv3 kernel summary, C2 / C3 / C5 lines), 1/8-shard rehearsals (C4, C5)
-OUT=gpurun_out/r4k
+OUT=gpurun_out/${R4K_OUT:-r4k}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { tail -30 $OUT/smoke.log; exit 1; }

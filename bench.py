@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--verify-gather", action="store_true",
                     help="N > 1: rank 0 also runs the whole workload alone and checks the gathered matrix bit for bit")
     ap.add_argument("--no-e2e", action="store_true", help="skip the one-off host-to-host timing")
+    ap.add_argument("--kernel", default="auto", help="pileup kernel of the timed plans (A/B; default auto)")
     ap.add_argument("--inflight", default="auto", choices=["auto", "1", "2", "3", "4"],
                     help="samples in flight: D DISTINCT samples (independent read sets over the same region "
                          "table, as profileMatrix loops over a recoup input list) on D HIP streams, step k "
@@ -237,7 +238,7 @@ def main():
     t1 = time.time()
     rs = ReadSet(*reads, data["seqlen"], device=local)
     tp = time.time()
-    plan = Plan(rs, rows, bins, out_ld="padded")  # whole 128-B lines per 16-row column segment
+    plan = Plan(rs, rows, bins, out_ld="padded", kernel=args.kernel)  # whole 128-B lines per 16-row column segment
     plan_s = time.time() - tp
     B = plan.n_cols
     out = plan.empty_output()
@@ -263,7 +264,7 @@ def main():
             rsets.append(ReadSet(*rk, dk["seqlen"], device=local))
             del dk, rk
             valids.append(torch.empty(max(R, 1), dtype=torch.uint8, device=dev))
-        plans = [Plan(rsets[k], rows, bins, out_ld="padded", concurrent=dmax) for k in range(dmax)]
+        plans = [Plan(rsets[k], rows, bins, out_ld="padded", concurrent=dmax, kernel=args.kernel) for k in range(dmax)]
         outs = [p.empty_output() for p in plans]
         streams = [torch.cuda.Stream(device=dev) for _ in range(dmax)]
 

@@ -2022,6 +2022,9 @@ int coverage_starts_dev(rcp_plan* plan, const int64_t* d_off, const int64_t* d_s
     P.crange = nullptr;
     P.cw_len = -1;
     P.lean = 0;
+#ifdef RCP_CSR_ROUNDS  // A/B only: rounds of 16 rows per workgroup of the coverage pileup
+    P.rounds = RCP_CSR_ROUNDS;
+#endif
     P.csr_off = d_off;
     P.csr_out = nullptr;
     P.valid_out = d_valid;

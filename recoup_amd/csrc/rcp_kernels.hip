@@ -2420,9 +2420,6 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
 #ifndef RCP_LRING3
 #define RCP_LRING3 0  // 1: two batches of reads in flight ahead of the one being added (lean kernel)
 #endif
-#ifndef RCP_LAHEAD2
-#define RCP_LAHEAD2 0  // 1: pile waves keep two rows' first reads in flight (A/B)
-#endif
 #ifndef RCP_LBATCH_UNI
 #define RCP_LBATCH_UNI 4  // reads per lane per batch of a start-only (uniform-width) lean plan
 #endif
@@ -2850,37 +2847,12 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         uint32_t g = take();     // this wave's pending row
         bool in_a = true;        // its first reads sit in bufA (else bufB)
         if (code >= 0) fetch(g, bufA);
-#if RCP_LAHEAD2
-        // two rows ahead: the pending rows g, g2 have their first reads in flight (rotation
-        // over three buffers without register copies; at most 16 pending rows in 8 waves, so
-        // they always lie in the next round)
-        RdT bufC[BL];
-        uint32_t g2 = take();
-        int ph = 0;  // g's reads: bufA / bufB / bufC for ph 0 / 1 / 2
-        if (code >= 0) fetch(g2, bufB);
-        (void)in_a;
-#endif
         while (code >= 0) {
             const LeanItem it = lean_item(P, code);
             for (int rd = 0; rd < LR; ++rd) {
                 const uint32_t lim = base + (uint32_t)(T * (rd + 1));
                 while (g < lim) {
                     const uint32_t gn = take();
-#if RCP_LAHEAD2
-                    if (ph == 0) {
-                        fetch(gn - base, bufC);
-                        pile_row(it, (int)(g - base), bufA);
-                    } else if (ph == 1) {
-                        fetch(gn - base, bufA);
-                        pile_row(it, (int)(g - base), bufB);
-                    } else {
-                        fetch(gn - base, bufB);
-                        pile_row(it, (int)(g - base), bufC);
-                    }
-                    ph = ph == 2 ? 0 : ph + 1;
-                    g = g2;
-                    g2 = gn;
-#else
                     if (in_a) {
                         fetch(gn - base, bufB);
                         pile_row(it, (int)(g - base), bufA);
@@ -2890,7 +2862,6 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                     }
                     in_a = !in_a;
                     g = gn;
-#endif
                 }
                 lds_barrier();  // A: the round's stage rows are complete
                 lds_barrier();  // B: the store waves hold them in registers

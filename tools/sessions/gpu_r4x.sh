@@ -15,3 +15,13 @@ for v in new csr1 csr4; do
   echo "== $v"; grep -E "equal" $OUT/rle_$v.txt
   python3 tools/kstat_rle.py $OUT/rle_$v/p_kernel_stats.csv | grep -E "pileup_kernel<false, true|cov_runs"
 done
+# heavy grid scaled by the table's rows (hg32) vs 4096 blocks always (new)
+for v in new hg32 new hg32; do
+  lib=build_var/$v/librecoup_amd.so
+  [ $v = new ] && lib=recoup_amd/librecoup_amd.so
+  echo "== $v" >> $OUT/hg.log
+  for spec in c4:0/8 c5:0/8 c4:0/1; do
+    RCP_LIB_PATH=$lib CFG=${spec%%:*} timeout -k 10 200 python3 tools/diag_shard_kernels.py ${spec#*:} auto >> $OUT/hg.log 2>&1 || { tail $OUT/hg.log; exit 1; }
+  done
+done
+grep -E "==|ms/pass" $OUT/hg.log

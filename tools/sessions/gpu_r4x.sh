@@ -4,6 +4,8 @@ OUT=gpurun_out/r4x
 mkdir -p $OUT
 export TMPDIR=/tmp
 T="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
+timeout -k 10 600 $T -m gpu tests > $OUT/tests.log 2>&1 || { tail -60 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
 for v in csr1 csr4; do
   RCP_LIB_PATH=build_var/$v/librecoup_amd.so timeout -k 10 300 $T -m gpu tests/test_gpu_rle.py > $OUT/rle_$v.log 2>&1 || { tail -30 $OUT/rle_$v.log; exit 1; }
   echo "$v $(tail -1 $OUT/rle_$v.log)"

@@ -171,15 +171,6 @@ constexpr int kHeavyMaxLen = 16383;    // longer rows never take the heavy path
 #define RCP_HEAVY_GRID 4096
 #endif
 constexpr int kHeavyGrid = RCP_HEAVY_GRID;
-#ifndef RCP_HEAVY_GRID_ROWS
-#define RCP_HEAVY_GRID_ROWS 0  // > 0 (A/B): grid = clamp(rows / RCP_HEAVY_GRID_ROWS, 512, RCP_HEAVY_GRID)
-#endif
-// heavy slice workgroups of a plan: idle ones exit at once, but a 4096-block dispatch still
-// costs microseconds on a small table (one GPU's shard)
-int heavy_grid(int64_t rows) {
-    if (RCP_HEAVY_GRID_ROWS <= 0) return kHeavyGrid;
-    return (int)std::min<int64_t>(kHeavyGrid, std::max<int64_t>(512, rows / RCP_HEAVY_GRID_ROWS));
-}
 
 // A wave's difference array: 64 lanes x per positions (per a power of two >= 4), each lane's
 // chunk padded by 4 words (rcp_kernels.hip scan_wave).  Returns the LDS words and the
@@ -1677,7 +1668,7 @@ extern "C" int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_str
     Q.valid_out = d_valid;
     HIP_TRY(rcp_launch_locate(&Q, s));
     Q.heavy_threshold = 0;  // no slices: the heavy launch only zeroes the previous status set
-    HIP_TRY(rcp_launch_heavy(&Q, heavy_grid(Q.n_rows), s));
+    HIP_TRY(rcp_launch_heavy(&Q, kHeavyGrid, s));
     return RCP_OK;
     RCP_CATCH
 }
@@ -1698,7 +1689,7 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
         RcpPlanDev Q = plan->dev;
         Q.valid_out = d_valid;
         HIP_TRY(rcp_launch_locate(&Q, s));
-        HIP_TRY(rcp_launch_heavy(&Q, heavy_grid(Q.n_rows), s));
+        HIP_TRY(rcp_launch_heavy(&Q, kHeavyGrid, s));
     }
     if (stages & RCP_STAGE_PILEUP) HIP_TRY(rcp_launch_pileup(&plan->dev, d_out, d_binsum, 0, s));
     if (stages & RCP_STAGE_INTERP) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
@@ -2006,7 +1997,7 @@ int calc_coverage_dev(rcp_plan* plan, const int64_t* d_off, int32_t* d_cov, uint
     P.csr_rs = nullptr;
     if (d_runs) HIP_TRY(hipMemsetAsync(d_runs, 0, 8 * ((size_t)plan->n_rows + 1), s));
     HIP_TRY(rcp_launch_locate(&P, s));
-    HIP_TRY(rcp_launch_heavy(&P, heavy_grid(P.n_rows), s));
+    HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
     if (d_runs) HIP_TRY(rcp_rle_seams_dev(plan->n_rows, d_off, d_cov, d_valid, pt.chunk_bins, P.chunk_cap, d_runs, s));
     return RCP_OK;
@@ -2031,9 +2022,20 @@ int coverage_starts_dev(rcp_plan* plan, const int64_t* d_off, const int64_t* d_s
     P.crange = nullptr;
     P.cw_len = -1;
     P.lean = 0;
-#ifdef RCP_CSR_ROUNDS  // A/B only: rounds of 16 rows per workgroup of the coverage pileup
-    P.rounds = RCP_CSR_ROUNDS;
+    // four rounds of 16 rows per workgroup (C4 coverage pileup 632 -> 601 us vs two, 635 with
+    // one; profiles/r04/r4x)
+#ifndef RCP_CSR_ROUNDS
+#define RCP_CSR_ROUNDS 4
 #endif
+    {
+        int tile = 16, rmax = 4;
+        rcp_tile_geometry(&tile, &rmax);
+        P.rounds = std::min(rmax, (int)RCP_CSR_ROUNDS);
+        // (fewer rounds when that leaves fewer than two workgroups per CU)
+        while (P.rounds > 1 && (int64_t)((P.n_rows + tile * P.rounds - 1) / (tile * P.rounds)) * P.n_chunks_total <
+                                   2 * (int64_t)std::max(P.n_cus, 1))
+            P.rounds /= 2;
+    }
     P.csr_off = d_off;
     P.csr_out = nullptr;
     P.valid_out = d_valid;
@@ -2042,7 +2044,7 @@ int coverage_starts_dev(rcp_plan* plan, const int64_t* d_off, const int64_t* d_s
     P.csr_sub = d_sub;
     P.csr_sub_off = d_sub_off;
     HIP_TRY(rcp_launch_locate(&P, s));
-    HIP_TRY(rcp_launch_heavy(&P, heavy_grid(P.n_rows), s));
+    HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
     return RCP_OK;
 }

@@ -3500,9 +3500,11 @@ static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* bin
                  : launch_pileup_u<MEDIAN, CSR, false>(P, out, binsum, lds, s);
 }
 
+// dynamic LDS of the row-wave launch: LDS stage, or the HBM-staged kernel's windows
+// (RCP_RWG_WAVES waves; the binsum launch takes the 4-wave unstaged kernel)
 extern "C" size_t rcp_pileup_rows_lds_bytes(const RcpPlanDev* P) {
     if (P && P->rows_lds > 0) return rows_lds_bytes(P->rows_lds, kRLWaves, RowWin<kRLSh>::words, kRLSlots);
-    return rows_lds_bytes(0, kRWaves, RowWin<kRWSh>::words, 0);
+    return rows_lds_bytes(0, RCP_RWG_WAVES, RowWin<kRWSh>::words, 0);
 }
 
 static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* binsum, hipStream_t s) {
@@ -3525,7 +3527,7 @@ static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* 
     if (binsum || (!P->rm32 && !P->rm64)) {
         const int64_t grid = std::min<int64_t>(((int64_t)4 * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
         hipLaunchKernelGGL((rcp_pileup_rows_kernel<0, kRWaves, kRWSh>), dim3((unsigned)grid), dim3(64 * kRWaves),
-                           rcp_pileup_rows_lds_bytes(&Q), s, Q, out, binsum);
+                           rows_lds_bytes(0, kRWaves, RowWin<kRWSh>::words, 0), s, Q, out, binsum);
         return hipGetLastError();
     }
     // HBM stage: 16 waves per CU, as RCP_RWG_WAVES-wave workgroups

@@ -167,5 +167,5 @@ def test_lds_and_global_staging(gpu):
     check(res, exp, rtol=1e-9, atol=1e-12)
     wide = Bins([("upstream", 0, 2000), ("center", 100), ("downstream", 0, 2000)], flank=(2000, 2000))
     res, exp, plan = _both(reads, CHROM_LEN, rows, wide, kernel="auto")
-    assert plan.info["lds_bytes"] < 65_536  # row-major staging in HBM
+    assert plan.info["lds_bytes"] <= 160 * 1024  # (row-major staging in HBM: the waves' windows only)
     check(res, exp, rtol=1e-9, atol=1e-12)

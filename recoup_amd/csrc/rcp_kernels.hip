@@ -2423,8 +2423,12 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
 #ifndef RCP_LBATCH_UNI
 #define RCP_LBATCH_UNI 4  // reads per lane per batch of a start-only (uniform-width) lean plan
 #endif
+#ifndef RCP_LPILE_WAVES
+#define RCP_LPILE_WAVES 8  // pile waves per lean workgroup (<= 16 rows of a round)
+#endif
+constexpr int kLPWaves = RCP_LPILE_WAVES;
 constexpr int kLStoreWaves = RCP_LSTORE_WAVES;
-constexpr int kLBlock = 64 * (kPWaves + kLStoreWaves);
+constexpr int kLBlock = 64 * (kLPWaves + kLStoreWaves);
 constexpr int kLQuads = 64 * kLStoreWaves / kTile;  // column quads per store pass
 constexpr int kLMaxPass = 8;                        // stage_cap <= 4 * kLQuads * kLMaxPass
 static_assert(kRows == 64 && kRounds >= 2, "store wave 0 decodes one row per lane");
@@ -2593,7 +2597,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     const int wave = tid >> 6;
     const int lane = tid & 63;
     const int RS = stage_stride(P.stage_cap);
-    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * P.wave_words;
+    uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kLPWaves * P.wave_words;
     uint32_t* emask = stage + T * RS;  // GEN: [row][16] enlarged-bin bits of the round
     LeanMeta* lmeta = reinterpret_cast<LeanMeta*>(emask + (GEN ? T * 16 : 0));  // [2][kRows]
     int32_t* item = reinterpret_cast<int32_t*>(lmeta + 2 * kRows);  // [2]: item code or -1
@@ -2644,17 +2648,17 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         // wait on its loads (only its stores remain outstanding, and nothing waits on them)
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     };
-    if (wave == kPWaves) claim(0);
+    if (wave == kLPWaves) claim(0);
     if (tid == 0) {
         item[1] = -1;  // (always written by a claim before it is read; defined anyway)
         item[2] = 0;   // the pile waves' row counter (RCP_LEAN_DYN)
     }
     lds_barrier();
 
-    if (wave < kPWaves) {
+    if (wave < kLPWaves) {
         // ================= pile waves
         int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * P.wave_words;
-        [[maybe_unused]] auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
+        [[maybe_unused]] auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kLPWaves + wave; };
         auto rd_load = [&](uint32_t idx) -> RdT {
             if constexpr (UNI) return P.st[idx];
             else return P.se[idx];
@@ -2828,7 +2832,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         // (a static 2 rows per wave waited at barrier A for the round's slowest pair).  A wave
         // holds at most one row ahead: the next round's, or the next item's round 0, whose
         // metadata store wave 0 published rounds ago.
-        static_assert(kPWaves <= kTile, "pending rows of one round fit the next round");
+        static_assert(kLPWaves <= kTile, "pending rows of one round fit the next round");
         uint32_t* ctr = reinterpret_cast<uint32_t*>(item + 2);
         auto take = [&]() -> uint32_t {
             uint32_t v = 0;
@@ -2872,7 +2876,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         }
     } else {
         // ================= store waves: thread (row ii, column quad qd)
-        const int st = tid - 64 * kPWaves;
+        const int st = tid - 64 * kLPWaves;
         const int ii = st & (T - 1);
         const int qd = st / T;
         const size_t R = (size_t)P.out_ld;  // column stride of the output (>= n_rows)
@@ -2888,7 +2892,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 // two rounds per item: the next item is claimed before the first round's barrier A
                 // (pile waves prefetch its first rows during the second round; every wave read
                 // the buffer it overwrites before the previous item's last barrier B)
-                if (LR == 2 && rd == 0 && wave == kPWaves) claim(buf ^ 1);
+                if (LR == 2 && rd == 0 && wave == kLPWaves) claim(buf ^ 1);
                 lds_barrier();  // A
                 const int rb = rd * T + ii;
                 const int r = it.tile * kIRows + rb;
@@ -2959,7 +2963,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 // the next item: claimed and decoded after round 0's stores were issued (its
                 // loads wait for them, with a whole round of pile work to hide that); read
                 // by the pile waves from round 2 on, after this wave has passed barrier A(1)
-                if (LR > 2 && rd == 0 && wave == kPWaves) claim(buf ^ 1);
+                if (LR > 2 && rd == 0 && wave == kLPWaves) claim(buf ^ 1);
             }
             buf ^= 1;
             code = item[buf];
@@ -3469,7 +3473,7 @@ static hipError_t launch_pileup_lean_r(const RcpPlanDev* P, double* out, hipStre
 extern "C" size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P) {
     // [pile waves' difference arrays | stage | (general bins) enlarged-bin bits | row metadata
     //  x 2 | item codes x 2]
-    return 4 * ((size_t)kPWaves * P->wave_words + (size_t)kTile * stage_stride(P->stage_cap) +
+    return 4 * ((size_t)kLPWaves * P->wave_words + (size_t)kTile * stage_stride(P->stage_cap) +
                 (P->lean == 2 ? (size_t)kTile * 16 : 0)) +
            2 * (size_t)kRows * sizeof(LeanMeta) + 16;
 }

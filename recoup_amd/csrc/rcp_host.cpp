@@ -1604,12 +1604,6 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         while (P.rounds > 1 &&
                (int64_t)((R + tile * P.rounds - 1) / (tile * P.rounds)) * P.n_chunks_total < 2 * (int64_t)cus)
             P.rounds /= 2;
-        // small general-kernel tables (fewer than 8 two-round workgroups per CU, e.g. one GPU's
-        // shard of C4): one round, so the chip holds more, shorter-lived workgroups (C4 1/8
-        // shard pileup 0.095 -> 0.090 ms, profiles/r04/r4zb)
-        if (P.lean == 0 && P.rounds == 2 &&
-            (int64_t)((R + 2 * tile - 1) / (2 * tile)) * P.n_chunks_total < 8 * (int64_t)cus)
-            P.rounds = 1;
 #ifdef RCP_GEN_ROUNDS_FIX  // A/B only: force the general kernel's rounds per workgroup
         P.rounds = std::min(rmax, (int)RCP_GEN_ROUNDS_FIX);
 #endif

@@ -164,21 +164,14 @@ struct RcpPlanDev {
     // row-wave kernel (lean == 3): the bin numerators of its rows are staged (uint32, whole
     // rows) and the last wave to finish a 16-row tile divides them and writes the tile's rows of
     // every column into the R column-major output as whole 128-B lines (a row-wave store
-    // straight into the column-major matrix is 8 bytes per 128-B line).  The stage is in LDS
-    // when two 16-row slots fit (rows_lds = its row stride in words, == 4 mod 64), else
+    // straight into the column-major matrix is 8 bytes per 128-B line).  The stage is
     // row-major in HBM: rm32 [n_rows][n_cols] with the rows' part info rinfo [n_rows][8]
     // ({bin width, layout}; width 0: zeros, -1: left to the interpolation kernel)
     uint32_t* rm32;
     int2* rinfo;
-    double* rm64;               // (RCP_ROWS_STAGE 3) the means themselves, [n_rows][n_cols]
-    int32_t rows_lds;
     // coverage (CSR) mode
     const int64_t* csr_off;     // non-null: write per-row depth into csr (calcCoverage)
     int32_t* csr_out;
-    // non-null: each wave adds the Rle run starts inside its sub-chunk to csr_runs[row] (a
-    // sub-chunk's first position counts only at the row's position 0; rcp_rle_seams_kernel
-    // adds the seams between sub-chunks): the run counts of calcCoverage's Rle list
-    unsigned long long* csr_runs;
     // non-null (calcCoverage's Rle list without a dense depth array): each (row, column chunk)
     // writes its run starts -- the chunk's first position always, then every position whose
     // depth differs from the one before -- as (depth, row position) to csr_rs at the chunk's
@@ -199,7 +192,6 @@ struct RcpPlanDev {
     int32_t heavy_stride;       // ints per slot (>= max row length + 1 of eligible rows)
     int32_t heavy_max_len;      // rows longer than this never take the heavy path
     int32_t heavy_slice;        // candidate reads per heavy work item
-    int32_t* heavy_slot;        // [n_rows] slot or -1 (locate output)
     int32_t* heavy_rows;        // [heavy_cap]
     uint32_t* heavy_nslice;     // [heavy_cap] slices of each slot (locate output)
     int32_t* heavy_gdiff;       // [heavy_cap * heavy_stride]; the slots the last execution used

@@ -25,6 +25,7 @@
 
 #include "../../include/recoup_amd.h"
 #include "rcp_device.h"
+#include "rcp_internal.h"
 #include "rcp_rle.h"
 #include "rcp_rng.h"
 #include "rcp_stage.h"
@@ -32,156 +33,27 @@
 // auto split off: on one GPU's 1/8, 1/4, 1/2 shard of C4, 4 and 8 column chunks instead of 2
 // were slower (1/8: pileup 0.109 -> 0.143 / 0.203 ms; profiles/r02c/lean_chunk_split_ab.log) --
 // an item's time is set by its 64 rows' read round trips, not by its width
-#ifndef RCP_LEAN_ITEMS_PER_WG
-#define RCP_LEAN_ITEMS_PER_WG 0
-#endif
-constexpr int kLeanItemsPerWg = RCP_LEAN_ITEMS_PER_WG;  // work items per persistent workgroup, at least
+constexpr int kLeanItemsPerWg = 0;  // work items per persistent workgroup, at least
 // Per-base plans (C5's TSS windows: reads piled in the window's middle, so the middle column
 // chunks are several times the outer ones' work) on few row tiles -- one GPU's shard -- take at
 // least this many work items per workgroup: narrower chunks let the per-XCD claims balance the
 // heavy middle items against the light outer ones (with ~1.5 items per workgroup the pass lasts
 // as long as the slowest workgroup's heavy items)
-#ifndef RCP_LEAN_ITEMS_PER_WG_BASE
-#define RCP_LEAN_ITEMS_PER_WG_BASE 4
-#endif
-constexpr int kLeanItemsPerWgBase = RCP_LEAN_ITEMS_PER_WG_BASE;
+constexpr int kLeanItemsPerWgBase = 4;
 constexpr int kLeanMinChunkBins = 64;                   // no column chunks narrower than this
 // AUTO keeps binned plans of fewer rows on the general kernel: a lean item is 64 rows, the
 // general kernel's workgroup 32, and with about one item per workgroup the item's read round
 // trips set the pass.  C4 shards (1000 bins of 2 bp), ms per pass lean / general: 25 k rows
 // 0.141 / 0.133, 33 k 0.160 / 0.154, 40 k 0.187 / 0.197, 50 k 0.217 / 0.232; per-base C5
 // shards stay lean (12.5 k rows: 0.317 / 0.435).  profiles/r03/pipeline/small_shard_kernels.log
-#ifndef RCP_LEAN_MIN_ROWS_BINNED
-#define RCP_LEAN_MIN_ROWS_BINNED 36000
-#endif
-constexpr int kLeanMinRowsBinned = RCP_LEAN_MIN_ROWS_BINNED;
+constexpr int kLeanMinRowsBinned = 36000;
 // Per-base lean plans (baseCoverageMatrix: every part one column per position) take work items
 // of two 16-row rounds instead of four: ms per pass four / two rounds, C5 0.752 / 0.673, its
 // 1/8 shard 0.272 / 0.253, 1/4 0.319 / 0.290; binned C4 is slower with them (0.553 / 0.563
 // pileup; 1/8 shard 0.107 / 0.115).  profiles/r03/pipeline/lean_rounds_ab.log
-#ifndef RCP_LEAN_ROUNDS2
-#define RCP_LEAN_ROUNDS2 1  // 0: four rounds for every lean plan, 2: two for every lean plan (A/B)
-#endif
 
-#ifndef RCP_AUTO_GEN
-#define RCP_AUTO_GEN 0  // 1: AUTO also takes the lean kernel's general-bins mode (A/B only)
-#endif
 
-#ifndef RCP_LEAN_LPT
-#define RCP_LEAN_LPT 1  // per-base lean plans of few items claim the heaviest items first (0: per-XCD order)
-#endif
-
-#ifndef RCP_BINS_AUTO
-#define RCP_BINS_AUTO 1  // plans of one binned part with uniform bins of >= 4 positions take the bin-difference kernel
-#endif
-
-#ifndef RCP_ROWS_AUTO
-#define RCP_ROWS_AUTO 1  // plans with multi-range rows take the row-wave pileup kernel
-#endif
-#ifndef RCP_ROWS_LDS
-#define RCP_ROWS_LDS 0   // 1: row-wave plans stage their tiles in LDS when two 16-row slots fit
-                         // (one 8-wave workgroup per CU: C3 0.73 ms vs 0.57 staged in HBM,
-                         // profiles/r04/r4j/c3.log)
-#endif
-
-extern "C" {
-hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
-                          int32_t* vout, int64_t n, int begin_bit, int end_bit, hipStream_t stream);
-hipError_t rcp_launch_unsorted(int64_t n, const uint64_t* keys, uint32_t* flag, hipStream_t stream);
-hipError_t rcp_launch_width_end(int64_t n, const int32_t* start, int32_t* width_end, uint32_t* overflow,
-                                hipStream_t stream);
-hipError_t rcp_launch_expand_runs(int64_t n, int32_t n_runs, const int64_t* run_start, const int32_t* run_value,
-                                  int32_t* out, hipStream_t stream);
-hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
-                           hipStream_t stream);
-hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream);
-hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_t stream);
-hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_t* binsum, int csr, hipStream_t stream);
-hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStream_t stream);
-size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr);
-size_t rcp_interp_lds_bytes(const RcpPlanDev* P);
-int rcp_tile_rows(void);
-void rcp_tile_geometry(int* tile, int* rounds_max);
-int rcp_lean_max_bins(void);
-int rcp_lean_gen_max_bins(void);
-size_t rcp_pileup_lean_lds_bytes(const RcpPlanDev* P);
-size_t rcp_pileup_rows_lds_bytes(const RcpPlanDev* P);
-int rcp_rows_lds_stride(int64_t n_cols);
-int rcp_rows_lds_window_cap(void);
-size_t rcp_pileup_bins_lds_bytes(const RcpPlanDev* P);
-int rcp_bins_max_bins(void);
-int rcp_bins_min_width(void);
-int rcp_rows_window_cap(void);
-hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
-                              const int8_t* strand, int32_t n_chrom, int32_t strand_filter, int merge, uint64_t* keys,
-                              int32_t* vals, hipStream_t stream);
-hipError_t rcp_launch_streams(int64_t n, const uint64_t* keys, const int32_t* vals, int64_t* off, int64_t n_off,
-                              int2* se, uint64_t* scan_in, hipStream_t stream);
-hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out, int32_t* pmax, hipStream_t stream);
-hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, int64_t* d_count,
-                              int64_t* d_run_off, void* temp, size_t* temp_bytes, int32_t* d_values,
-                              int32_t* d_lengths, int pass, hipStream_t stream);
-hipError_t rcp_launch_width_range(int64_t n, const uint64_t* keys, const int32_t* vals, int32_t* mm,
-                                  hipStream_t stream);
-hipError_t rcp_launch_split_uniform(int64_t n, const int2* se, int32_t* st, int32_t* pmax, hipStream_t stream);
-hipError_t rcp_cov_runs_dev(int32_t n_rows, const int64_t* d_off, const int64_t* d_sub_off, int64_t n_sub,
-                            const int2* d_sub, const int2* d_rs, const uint8_t* d_valid, int32_t chunk, int64_t* d_cnt,
-                            int4* d_info, int64_t* d_base, int64_t* d_run_off, void* temp, size_t* temp_bytes,
-                            int32_t* d_values, int32_t* d_lengths, uint32_t* d_bad, int pass, hipStream_t stream);
-hipError_t rcp_rle_seams_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, const uint8_t* d_valid,
-                             int32_t chunk_bins, int32_t chunk_cap, int64_t* d_count, hipStream_t stream);
-hipError_t rcp_launch_stream_maxend(int64_t n_streams, const int64_t* off, const int32_t* pmax, int32_t* out,
-                                    hipStream_t stream);
-hipError_t rcp_launch_dir(int64_t n_entries, int64_t n_streams, const int64_t* dir_off, const int64_t* off,
-                          const int32_t* pmax, const int2* se, int shift, int32_t* dir_l, int32_t* dir_u,
-                          hipStream_t stream);
-hipError_t rcp_launch_dirk(int64_t n_entries, const int32_t* dir_lu, const int32_t* pmax, const int2* se,
-                           int32_t* dir_k, hipStream_t stream);
-}
-
-namespace {
-
-constexpr int kChunkMax = 16384;       // positions of an interpolated slice (block LDS array)
-constexpr int kWaveMax = 2047;         // positions per wave sub-chunk (64 x 32 slots incl. the end sentinel)
-#ifndef RCP_STAGE_MAX_BINS
-#define RCP_STAGE_MAX_BINS 512
-#endif
-constexpr int kStageMaxBins = RCP_STAGE_MAX_BINS;  // bins per chunk (LDS stage = bins x 17 words)
-#ifndef RCP_LDS_BUDGET
-#define RCP_LDS_BUDGET (80 * 1024)
-#endif
-constexpr size_t kLdsBudget = RCP_LDS_BUDGET;  // pileup LDS per workgroup (80 KB: two per CU)
-#ifndef RCP_HEAVY_THRESHOLD
-#define RCP_HEAVY_THRESHOLD 4096
-#endif
-constexpr int kHeavyThreshold = RCP_HEAVY_THRESHOLD;  // candidate reads per column chunk above which a row is split across workgroups
-                                        // (8192 before the lean kernel dealt rows dynamically; C4 0.647 -> 0.633 ms)
-#ifndef RCP_DIR_READS
-#define RCP_DIR_READS 8  // mean reads per directory bucket (the locate kernel's search depth)
-#endif
-#ifndef RCP_DIR_INLINE
-#define RCP_DIR_INLINE 1  // build the inline-key directory (one line per locate search)
-#endif
-#ifndef RCP_HEAVY_SLICE
-#define RCP_HEAVY_SLICE 4096
-#endif
-constexpr int kHeavySlice = RCP_HEAVY_SLICE;  // candidate reads per heavy work item
-constexpr int kHeavyMaxLen = 16383;    // longer rows never take the heavy path
-#ifndef RCP_HEAVY_GRID
-#define RCP_HEAVY_GRID 4096
-#endif
-constexpr int kHeavyGrid = RCP_HEAVY_GRID;
-
-// A wave's difference array: 64 lanes x per positions (per a power of two >= 4), each lane's
-// chunk padded by 4 words (rcp_kernels.hip scan_wave).  Returns the LDS words and the
-// position capacity for a chunk of `positions`.
-void wave_geometry(int32_t positions, int32_t* words, int32_t* capacity) {
-    int32_t need = (positions + 1 + 63) / 64;
-    int32_t per = 4;
-    while (per < need) per <<= 1;
-    *words = 64 * (per + 4);
-    *capacity = 64 * per - 1;
-}
+namespace rcpi {
 
 thread_local std::string g_err;
 
@@ -194,65 +66,6 @@ int fail(int code, const char* fmt, ...) {
     g_err = buf;
     return code;
 }
-
-#define HIP_TRY(expr)                                                                        \
-    do {                                                                                     \
-        hipError_t e_ = (expr);                                                              \
-        if (e_ != hipSuccess)                                                                \
-            return fail(e_ == hipErrorOutOfMemory ? RCP_ENOMEM : RCP_EHIP, "%s: %s (%s:%d)", #expr, \
-                        hipGetErrorString(e_), __FILE__, __LINE__);                          \
-    } while (0)
-
-// Nothing may escape into the caller's process (an R session): every C++ exception that a
-// body can raise (std::bad_alloc from table building, std::system_error from threads) becomes
-// an RCP_E* code.
-#define RCP_TRY try {
-#define RCP_CATCH                                                                         \
-    }                                                                                     \
-    catch (const std::bad_alloc&) {                                                       \
-        return fail(RCP_ENOMEM, "host memory exhausted in %s", __func__);                 \
-    }                                                                                     \
-    catch (const std::exception& e_) {                                                    \
-        return fail(RCP_EINVAL, "%s: %s", __func__, e_.what());                          \
-    }                                                                                     \
-    catch (...) {                                                                         \
-        return fail(RCP_EINVAL, "%s: unexpected C++ exception", __func__);               \
-    }
-
-// Device buffer with RAII.
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    DevBuf() = default;
-    DevBuf(const DevBuf&) = delete;
-    DevBuf& operator=(const DevBuf&) = delete;
-    DevBuf& operator=(DevBuf&& o) noexcept {
-        if (this != &o) {
-            reset();
-            p = o.p;
-            bytes = o.bytes;
-            o.p = nullptr;
-            o.bytes = 0;
-        }
-        return *this;
-    }
-    ~DevBuf() { reset(); }
-    void reset() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    hipError_t alloc(size_t n) {
-        reset();
-        bytes = n;
-        if (n == 0) return hipSuccess;
-        return hipMalloc(&p, n);
-    }
-    template <class T>
-    T* as() const {
-        return static_cast<T*>(p);
-    }
-};
 
 // Stream-ordered temporaries from the library's own memory pool on each device (not the
 // process-wide default pool, whose settings other users of hipMallocAsync in the process would
@@ -280,10 +93,7 @@ hipError_t device_pool(int dev, hipMemPool_t* out) {
     hipMemPool_t pool;
     hipError_t e = hipMemPoolCreate(&pool, &props);
     if (e != hipSuccess) return e;
-#ifndef RCP_POOL_KEEP_GB
-#define RCP_POOL_KEEP_GB 64  // freed memory kept mapped (C5's build peaks near 40 GB)
-#endif
-    uint64_t thr = uint64_t(RCP_POOL_KEEP_GB) << 30;
+    uint64_t thr = uint64_t(64) << 30;  // freed memory kept mapped (C5's build peaks near 40 GB)
     e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
     if (e != hipSuccess) return e;
     g_pools[dev] = pool;
@@ -300,45 +110,6 @@ hipError_t pool_alloc(void** p, size_t n, hipStream_t s) {
     return hipMallocFromPoolAsync(p, n, pool, s);
 }
 
-struct PoolBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    hipStream_t s;
-    explicit PoolBuf(hipStream_t st) : s(st) {}
-    PoolBuf(const PoolBuf&) = delete;
-    PoolBuf& operator=(const PoolBuf&) = delete;
-    ~PoolBuf() { reset(); }
-    void reset() {
-        if (p) (void)hipFreeAsync(p, s);
-        p = nullptr;
-        bytes = 0;
-    }
-    hipError_t alloc(size_t n) {
-        reset();
-        bytes = n;
-        if (n == 0) return hipSuccess;
-        return pool_alloc(&p, n, s);
-    }
-    template <class T>
-    T* as() const {
-        return static_cast<T*>(p);
-    }
-};
-
-// Switch to a device for the scope of an API call, restoring the caller's device.
-struct DeviceGuard {
-    int prev = -1;
-    hipError_t err = hipSuccess;
-    explicit DeviceGuard(int dev) {
-        err = hipGetDevice(&prev);
-        if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
 int check_device(int dev) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(RCP_ENODEVICE, "no HIP device visible");
@@ -346,90 +117,40 @@ int check_device(int dev) {
     return RCP_OK;
 }
 
+}  // namespace rcpi
+using namespace rcpi;
+
+namespace {
+
+constexpr int kChunkMax = 16384;       // positions of an interpolated slice (block LDS array)
+constexpr int kWaveMax = 2047;         // positions per wave sub-chunk (64 x 32 slots incl. the end sentinel)
+constexpr int kStageMaxBins = 512;  // bins per chunk (LDS stage = bins x 17 words)
+constexpr size_t kLdsBudget = 80 * 1024;  // pileup LDS per workgroup (80 KB: two per CU)
+constexpr int kHeavyThreshold = 4096;  // candidate reads per column chunk above which a row is split across workgroups
+                                        // (8192 before the lean kernel dealt rows dynamically; C4 0.647 -> 0.633 ms)
+constexpr int kDirReads = 8;  // mean reads per directory bucket (the locate kernel's search depth)
+constexpr int kHeavySlice = 4096;  // candidate reads per heavy work item
+constexpr int kHeavyMaxLen = 16383;    // longer rows never take the heavy path
+constexpr int kHeavyGrid = 4096;
+constexpr int kGeneralMaxChunks = 8;  // column chunks a wide binned part is cut into (general kernel)
+
+// A wave's difference array: 64 lanes x per positions (per a power of two >= 4), each lane's
+// chunk padded by 4 words (rcp_kernels.hip scan_wave).  Returns the LDS words and the
+// position capacity for a chunk of `positions`.
+void wave_geometry(int32_t positions, int32_t* words, int32_t* capacity) {
+    int32_t need = (positions + 1 + 63) / 64;
+    int32_t per = 4;
+    while (per < need) per <<= 1;
+    *words = 64 * (per + 4);
+    *capacity = 64 * per - 1;
+}
+
 }  // namespace
+
 
 // =====================================================================================
 // readset
 // =====================================================================================
-// One sorted layout of the reads: streams (chromosome x strand) of start-sorted (start, end)
-// pairs with their prefix max of end and bucket directory (rcp_device.h).  A readset keeps two:
-// `stranded` (stream c*3 + strand, for findOverlaps with strand compatibility) and `merged`
-// (all strands in stream c*3, streams c*3+1, c*3+2 empty: ignore.strand = TRUE, the default),
-// so the default path searches and streams one range per segment instead of three.
-// A readset's own arrays, from the same pool (a 4 GB hipMalloc of C5's packed reads once took
-// 5.9 s on the box, tools/diag_readset.py with -DRCP_PLAN_TIMING=1), allocated on the build
-// stream and released after one device synchronisation per readset (~rcp_readset) -- what
-// hipFree does implicitly, so a readset destroyed with work still queued on it stays safe --
-// back into the pool.
-struct PoolArr {
-    void* p = nullptr;
-    size_t bytes = 0;
-    PoolArr() = default;
-    PoolArr(const PoolArr&) = delete;
-    PoolArr& operator=(const PoolArr&) = delete;
-    PoolArr(PoolArr&& o) noexcept : p(o.p), bytes(o.bytes) {
-        o.p = nullptr;
-        o.bytes = 0;
-    }
-    PoolArr& operator=(PoolArr&& o) noexcept {
-        if (this != &o) {
-            if (p) (void)hipFreeAsync(p, nullptr);
-            p = o.p;
-            bytes = o.bytes;
-            o.p = nullptr;
-            o.bytes = 0;
-        }
-        return *this;
-    }
-    ~PoolArr() {
-        if (p) (void)hipFreeAsync(p, nullptr);  // after rcp_readset's device synchronisation
-    }
-    hipError_t alloc(size_t n, hipStream_t s) {
-        if (p) return hipErrorInvalidValue;  // allocated once
-        bytes = n;
-        if (n == 0) return hipSuccess;
-        return pool_alloc(&p, n, s);
-    }
-    template <class T>
-    T* as() const {
-        return static_cast<T*>(p);
-    }
-};
-
-struct ReadLayout {
-    std::vector<int64_t> h_stream_off;  // n_chrom*3 + 1
-    std::vector<int64_t> h_dir_off;     // n_chrom*3 + 1
-    PoolArr se, pmax, stream_off;
-    PoolArr dir_l, dir_off;
-    PoolArr dir_k;      // inline-key directory (128 bytes per entry; rcp_device.h)
-    int32_t dir_shift = 12;
-    PoolArr st;         // the starts alone when every read has one width (st_w = end - start)
-    int32_t st_w = 0;
-};
-
-struct rcp_readset {
-    int device = 0;
-    int64_t n = 0;  // reads kept (strand filter applied)
-    int32_t n_chrom = 0;
-    std::vector<int64_t> seqlen;
-    DevBuf d_seqlen;
-    ReadLayout stranded, merged;
-    bool presorted = false;  // the reads came in (chromosome, start) order (no full radix sort)
-    // The stranded layout serves only ignore.strand = FALSE (findOverlaps with strand
-    // compatibility); the default TRUE reads the merged one.  Reads uploaded from the host keep
-    // their device copies here and the stranded layout is built at its first use
-    // (ensure_stranded: a plan with ignore_strand == 0, rcp_readset_info), not by every create.
-    std::mutex mu;
-    bool stranded_ready = false;
-    rcp_reads_desc desc{};  // n, n_chrom, strand_filter of the build
-    DevBuf keep_chrom, keep_start, keep_end, keep_strand;
-    const int32_t *kc = nullptr, *ks = nullptr, *ke = nullptr;
-    const int8_t* kst = nullptr;
-    // one device synchronisation before the members' arrays go back to the pool (what hipFree
-    // does implicitly): work still queued on any stream that reads them has finished
-    ~rcp_readset() { (void)hipDeviceSynchronize(); }
-};
-
 // tools-only phase timing of rcp_plan_create_ex (build with -DRCP_PLAN_TIMING=1)
 #if RCP_PLAN_TIMING
 #include <chrono>
@@ -586,7 +307,7 @@ int build_layout(const rcp_readset* rs, const rcp_reads_desc* d, const int32_t* 
         genome += (double)m;
     }
     const int used = merge ? 1 : 3;  // streams per chromosome that hold reads
-    const double want = kept > 0 ? (double)RCP_DIR_READS * used * genome / (double)kept : 1e9;
+    const double want = kept > 0 ? (double)kDirReads * used * genome / (double)kept : 1e9;
     int shift = 6;
     while (shift < 24 && (double)(int64_t(1) << (shift + 1)) <= want) ++shift;
     L->dir_shift = shift;
@@ -606,11 +327,9 @@ int build_layout(const rcp_readset* rs, const rcp_reads_desc* d, const int32_t* 
     HIP_TRY(rcp_launch_dir(ne, n_streams, L->dir_off.as<int64_t>(), L->stream_off.as<int64_t>(),
                            L->pmax.as<int32_t>(), L->se.as<int2>(), shift, L->dir_l.as<int32_t>(),
                            L->dir_l.as<int32_t>() + 1, s));
-    if (RCP_DIR_INLINE) {
-        HIP_TRY(L->dir_k.alloc(128 * std::max<int64_t>(ne, 1), s));
-        HIP_TRY(rcp_launch_dirk(ne, L->dir_l.as<int32_t>(), L->pmax.as<int32_t>(), L->se.as<int2>(),
-                                L->dir_k.as<int32_t>(), s));
-    }
+    HIP_TRY(L->dir_k.alloc(128 * std::max<int64_t>(ne, 1), s));
+    HIP_TRY(rcp_launch_dirk(ne, L->dir_l.as<int32_t>(), L->pmax.as<int32_t>(), L->se.as<int2>(),
+                            L->dir_k.as<int32_t>(), s));
     HIP_TRY(hipStreamSynchronize(s));
     LAYOUT_MARK("  directory");
     *kept_out = kept;
@@ -829,25 +548,6 @@ extern "C" int rcp_readset_info(const rcp_readset* rs, int64_t* n_reads, int64_t
 // =====================================================================================
 // plan
 // =====================================================================================
-struct rcp_plan {
-    const rcp_readset* rs = nullptr;
-    RcpPlanDev dev{};
-    int32_t n_rows = 0;
-    int64_t n_cols = 0;
-    int64_t n_seg = 0;
-    std::vector<int64_t> row_len;
-    size_t lds = 0;
-    int64_t grid = 0;
-    int32_t tile_rows = 64;  // rows per pileup workgroup (info)
-    DevBuf tables;     // read-only tables
-    DevBuf work;       // seg_lo / seg_hi / valid / status
-    DevBuf scratch;    // interpolation scratch
-    DevBuf rm;         // row-wave kernel: row-major staging of the matrix
-    int32_t max_row_len = 0;
-    int64_t out_ld = 0;
-    uint32_t* status_sets = nullptr;  // 2 x RCP_STATUS_WORDS words in `work`
-    int epoch = 1;                    // parity of the last execution (the first one uses set 0)
-};
 
 namespace {
 
@@ -1179,12 +879,14 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
             int32_t cb = (pt.n_bins + nch - 1) / nch;
             // wide binned chunks would be piled in several wave sub-chunks, each streaming the
             // chunk's reads again: split them into more (up to 8) column chunks instead -- more
-            // workgroups for small row counts, and per-chunk read ranges from locate
+            // workgroups for small row counts, and per-chunk read ranges from locate.  The general
+            // kernel's cap stays at the 8 chunks its A/B measured (lean plans split further, to
+            // RCP_MAX_CRANGE_CHUNKS, below)
             const int32_t pos_max = 1023;
             if (!median && !pt.per_base && part_max_bin[p] > 0 && (int64_t)cb * part_max_bin[p] > pos_max) {
                 const int32_t cb2 = std::max<int32_t>(1, pos_max / part_max_bin[p]);
                 const int32_t nch2 = (pt.n_bins + cb2 - 1) / cb2;
-                if (nch2 <= RCP_MAX_CRANGE_CHUNKS) {
+                if (nch2 <= kGeneralMaxChunks) {
                     nch = nch2;
                     cb = (pt.n_bins + nch - 1) / nch;
                 }
@@ -1275,13 +977,13 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
             if (j1 - j0 > 1) lean = false;
             else if (j1 == j0 + 1 && (B.segs[j0].multi || !B.segs[j0].query_ok)) lean = false;
         }
-        const bool gen = !lean && base && (kind == RCP_KERNEL_LEAN_ANY || (RCP_AUTO_GEN && kind == RCP_KERNEL_AUTO)) &&
+        const bool gen = !lean && base && kind == RCP_KERNEL_LEAN_ANY &&
                          stage_cap <= rcp_lean_gen_max_bins();
         P.lean = lean ? 1 : (gen ? 2 : 0);
         {
             bool per_base = true;
             for (int p = 0; p < P.n_parts; ++p) per_base = per_base && P.part[p].per_base;
-            P.lean_rounds = P.lean && ((RCP_LEAN_ROUNDS2 == 1 && per_base) || RCP_LEAN_ROUNDS2 == 2) ? 2 : 0;
+            P.lean_rounds = P.lean && per_base ? 2 : 0;
         }
         // row-wave kernel (lean == 3): mean bins of any layout, every bin inside one window;
         // AUTO takes it for plans with multi-range rows (coverageRnaRef, genebody + flanks)
@@ -1290,17 +992,8 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
             if (!P.part[p].per_base && part_max_bin[p] > rcp_rows_window_cap()) rows_ok = false;
         bool multi_rows = false;
         for (int r = 0; !multi_rows && r < R; ++r) multi_rows = B.row_seg[r + 1] - B.row_seg[r] > 1;
-        if (rows_ok && (kind == RCP_KERNEL_ROWS || (kind == RCP_KERNEL_AUTO && multi_rows && RCP_ROWS_AUTO)))
+        if (rows_ok && (kind == RCP_KERNEL_ROWS || (kind == RCP_KERNEL_AUTO && multi_rows)))
             P.lean = 3;
-        // its tiles' numerators in LDS (no row-major staging round trip through L2 / HBM) when
-        // two slots of 16 rows fit beside the waves' windows
-        P.rows_lds = 0;
-        if (P.lean == 3 && RCP_ROWS_LDS) {
-            bool fit = true;
-            for (int p = 0; p < P.n_parts; ++p)
-                if (!P.part[p].per_base && part_max_bin[p] > rcp_rows_lds_window_cap()) fit = false;
-            if (fit) P.rows_lds = rcp_rows_lds_stride(P.n_cols);
-        }
     }
     // ---- bin-difference kernel (lean == 4): mean plans of one binned part whose rows are
     // single ranges, every row's slice a whole number of bins of >= rcp_bins_min_width()
@@ -1311,7 +1004,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         const int kind = opts->pileup_kernel;
         bool bd = !cov_only && bins->stat == RCP_STAT_MEAN && P.n_parts == 1 && !P.part[0].per_base &&
                   P.part[0].n_bins > 0 && P.part[0].n_bins <= rcp_bins_max_bins() &&
-                  (kind == RCP_KERNEL_AUTO || kind == RCP_KERNEL_BINS) && RCP_BINS_AUTO;
+                  (kind == RCP_KERNEL_AUTO || kind == RCP_KERNEL_BINS);
         const RcpPart& pt0 = P.part[0];
         for (int r = 0; bd && r < R; ++r) {
             const int32_t j0 = B.row_seg[r], j1 = B.row_seg[r + 1];
@@ -1449,8 +1142,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     const size_t w_hi = al(w_lo + 12 * S);
     const size_t w_valid = al(w_hi + 12 * S);
     const size_t w_ncand = al(w_valid + Rw);
-    const size_t w_hslot = al(w_ncand + 4 * Rw);
-    const size_t w_hrows = al(w_hslot + 4 * Rw);
+    const size_t w_hrows = al(w_ncand + 4 * Rw);
     const size_t w_hoff = al(w_hrows + 4 * (size_t)P.heavy_cap);
     const size_t w_gdiff = al(w_hoff + 4 * ((size_t)P.heavy_cap + 1));
     const size_t w_rec = al(w_gdiff + (P.heavy_threshold > 0 ? 4 * (size_t)P.heavy_cap * P.heavy_stride : 0));
@@ -1465,7 +1157,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     if (hipDeviceGetAttribute(&lpt_cus, hipDeviceAttributeMultiprocessorCount, rs->device) != hipSuccess || lpt_cus <= 0)
         lpt_cus = 256;
     // (a full per-base table, e.g. C5's 6256 items, keeps the per-XCD order and its L2 locality)
-    P.lpt = RCP_LEAN_LPT && P.lean == 1 && P.lean_rounds == 2 && keep_crange && R > 0 &&
+    P.lpt = P.lean == 1 && P.lean_rounds == 2 && keep_crange && R > 0 &&
             lpt_items <= (int64_t)kLeanItemsPerWgBase * 2 * lpt_cus;
     P.lpt_cap = P.lpt ? (int32_t)lpt_items : 0;
     const size_t w_order = al(w_crange + (keep_crange ? sizeof(uint2) * 3 * (size_t)P.n_chunks_total * Rw : 0));
@@ -1475,7 +1167,6 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     PLAN_MARK("work alloc");
     char* wb = plan->work.as<char>();
     P.ncand = reinterpret_cast<uint32_t*>(wb + w_ncand);
-    P.heavy_slot = reinterpret_cast<int32_t*>(wb + w_hslot);
     P.heavy_rows = reinterpret_cast<int32_t*>(wb + w_hrows);
     P.heavy_nslice = reinterpret_cast<uint32_t*>(wb + w_hoff);
     P.heavy_gdiff = reinterpret_cast<int32_t*>(wb + w_gdiff);
@@ -1519,15 +1210,12 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
 
     const ReadLayout& RL = rows->ignore_strand ? rs->merged : rs->stranded;
     P.se = RL.se.as<int2>();
-#ifndef RCP_NO_UNI
-#define RCP_NO_UNI 0  // 1: never stream starts alone (A/B only)
-#endif
     // uniform-width reads: the general kernel and per-base lean plans stream the starts alone;
     // binned lean plans keep the (start, end) pairs -- C4's latency-bound pile measured 4 % slower
     // with starts (pileup 0.578 vs 0.555 ms, same box), C5's dense per-base rows 6 % faster
     // (0.58 vs 0.62), the 1/8 C4 shard's general kernel 4 % (profiles/r03/pipeline/general_starts_ab.log,
     // lean_starts_c4_ab.log)
-    const bool use_st = RL.st.p && !RCP_NO_UNI && (P.lean != 1 || P.lean_rounds == 2);
+    const bool use_st = RL.st.p && (P.lean != 1 || P.lean_rounds == 2);
     P.st = use_st ? RL.st.as<int32_t>() : nullptr;
     P.st_w = RL.st_w;
     P.pmax = RL.pmax.as<int32_t>();
@@ -1566,26 +1254,17 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.interp_scratch = plan->scratch.as<double>();
     P.csr_off = nullptr;
     P.csr_out = nullptr;
-    P.csr_runs = nullptr;
     P.csr_rs = nullptr;
     P.csr_sub = nullptr;
     P.csr_sub_off = nullptr;
     // row-wave plans whose tile stage does not fit LDS stage their bin numerators row-major
-#ifndef RCP_ROWS_STAGE
-#define RCP_ROWS_STAGE 1  // 1: uint32 numerators (divided at the flush), 3: the fp64 means
-#endif
+    // (uint32 numerators, divided at the flush)
     P.rm32 = nullptr;
     P.rinfo = nullptr;
-    P.rm64 = nullptr;
-    if (P.lean == 3 && P.rows_lds == 0 && R > 0 && P.n_cols > 0) {
-        if (RCP_ROWS_STAGE == 3) {
-            HIP_TRY(plan->rm.alloc(8 * (size_t)R * (size_t)P.n_cols));
-            P.rm64 = plan->rm.as<double>();
-        } else {
-            HIP_TRY(plan->rm.alloc(4 * (size_t)R * (size_t)P.n_cols + 8 * (size_t)R * RCP_MAX_PARTS));
-            P.rinfo = plan->rm.as<int2>();
-            P.rm32 = reinterpret_cast<uint32_t*>(P.rinfo + (size_t)R * RCP_MAX_PARTS);
-        }
+    if (P.lean == 3 && R > 0 && P.n_cols > 0) {
+        HIP_TRY(plan->rm.alloc(4 * (size_t)R * (size_t)P.n_cols + 8 * (size_t)R * RCP_MAX_PARTS));
+        P.rinfo = plan->rm.as<int2>();
+        P.rm32 = reinterpret_cast<uint32_t*>(P.rinfo + (size_t)R * RCP_MAX_PARTS);
     }
     plan->lds = P.lean == 4 ? rcp_pileup_bins_lds_bytes(&P)
                 : P.lean == 3 ? rcp_pileup_rows_lds_bytes(&P)
@@ -1604,9 +1283,6 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         while (P.rounds > 1 &&
                (int64_t)((R + tile * P.rounds - 1) / (tile * P.rounds)) * P.n_chunks_total < 2 * (int64_t)cus)
             P.rounds /= 2;
-#ifdef RCP_GEN_ROUNDS_FIX  // A/B only: force the general kernel's rounds per workgroup
-        P.rounds = std::min(rmax, (int)RCP_GEN_ROUNDS_FIX);
-#endif
         plan->tile_rows = P.lean == 4 ? tile : (P.lean ? (P.lean_rounds == 2 ? 2 * tile : rcp_tile_rows()) : tile * P.rounds);
     }
     plan->grid = (int64_t)((R + plan->tile_rows - 1) / plan->tile_rows) * P.n_chunks_total;
@@ -1971,10 +1647,8 @@ extern "C" int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices
 
 namespace {
 
-// calcCoverage of every row into CSR depth (d_off: device [n_rows + 1]); with d_runs (device
-// [n_rows + 1], zeroed here) also each row's Rle run count, 0 for NULL rows
-int calc_coverage_dev(rcp_plan* plan, const int64_t* d_off, int32_t* d_cov, uint8_t* d_valid, int64_t* d_runs,
-                      hipStream_t s) {
+// calcCoverage of every row into CSR depth (d_off: device [n_rows + 1])
+int calc_coverage_dev(rcp_plan* plan, const int64_t* d_off, int32_t* d_cov, uint8_t* d_valid, hipStream_t s) {
     // one per-base part over the whole row, chunked by the plan's chunk capacity
     begin_exec(plan);
     RcpPlanDev P = plan->dev;
@@ -1993,13 +1667,10 @@ int calc_coverage_dev(rcp_plan* plan, const int64_t* d_off, int32_t* d_cov, uint
     P.csr_off = d_off;
     P.csr_out = d_cov;
     P.valid_out = d_valid;
-    P.csr_runs = reinterpret_cast<unsigned long long*>(d_runs);
     P.csr_rs = nullptr;
-    if (d_runs) HIP_TRY(hipMemsetAsync(d_runs, 0, 8 * ((size_t)plan->n_rows + 1), s));
     HIP_TRY(rcp_launch_locate(&P, s));
     HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
-    if (d_runs) HIP_TRY(rcp_rle_seams_dev(plan->n_rows, d_off, d_cov, d_valid, pt.chunk_bins, P.chunk_cap, d_runs, s));
     return RCP_OK;
 }
 
@@ -2024,13 +1695,10 @@ int coverage_starts_dev(rcp_plan* plan, const int64_t* d_off, const int64_t* d_s
     P.lean = 0;
     // four rounds of 16 rows per workgroup (C4 coverage pileup 632 -> 601 us vs two, 635 with
     // one; profiles/r04/r4x)
-#ifndef RCP_CSR_ROUNDS
-#define RCP_CSR_ROUNDS 4
-#endif
     {
         int tile = 16, rmax = 4;
         rcp_tile_geometry(&tile, &rmax);
-        P.rounds = std::min(rmax, (int)RCP_CSR_ROUNDS);
+        P.rounds = std::min(rmax, 4);
         // (fewer rounds when that leaves fewer than two workgroups per CU)
         while (P.rounds > 1 && (int64_t)((P.n_rows + tile * P.rounds - 1) / (tile * P.rounds)) * P.n_chunks_total <
                                    2 * (int64_t)std::max(P.n_cus, 1))
@@ -2039,7 +1707,6 @@ int coverage_starts_dev(rcp_plan* plan, const int64_t* d_off, const int64_t* d_s
     P.csr_off = d_off;
     P.csr_out = nullptr;
     P.valid_out = d_valid;
-    P.csr_runs = nullptr;
     P.csr_rs = d_rs;
     P.csr_sub = d_sub;
     P.csr_sub_off = d_sub_off;
@@ -2070,7 +1737,7 @@ extern "C" int rcp_calc_coverage(rcp_plan* plan, const int64_t* out_off, int32_t
     DevBuf d_off;
     HIP_TRY(d_off.alloc(8 * (plan->n_rows + 1)));
     HIP_TRY(hipMemcpyAsync(d_off.p, out_off, 8 * (plan->n_rows + 1), hipMemcpyHostToDevice, s));
-    const int rc = calc_coverage_dev(plan, d_off.as<int64_t>(), d_cov, d_valid, nullptr, s);
+    const int rc = calc_coverage_dev(plan, d_off.as<int64_t>(), d_cov, d_valid, s);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s));  // d_off is released on return
     return RCP_OK;
@@ -2145,19 +1812,6 @@ extern "C" int rcp_rle_encode(int32_t n_rows, const int64_t* out_off, const int3
 // on the device until rcp_cov_copy moves them straight into the caller's arrays (R's
 // allocVector results): one PCIe transfer, no library-side host copy.
 // =====================================================================================
-struct rcp_cov {
-    int32_t n_rows = 0;
-    int64_t n_runs = 0;
-    int device = 0;
-    PoolBuf run_off{nullptr}, values{nullptr}, lengths{nullptr}, valid{nullptr};
-    ~rcp_cov() {
-        // the buffers go back to the pool after everything queued on the null stream
-        run_off.reset();
-        values.reset();
-        lengths.reset();
-        valid.reset();
-    }
-};
 
 extern "C" int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows, rcp_cov** out) {
     RCP_TRY
@@ -2178,10 +1832,7 @@ extern "C" int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows
     const int64_t n = off[R];
     if (n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "%lld coverage positions", (long long)n);
     hipStream_t s = nullptr;
-#ifndef RCP_COV_DENSE
-#define RCP_COV_DENSE 0  // 1: round-3 path (dense depth written, counted, re-read by an emit kernel)
-#endif
-    if (!RCP_COV_DENSE) {
+    {
         // the pileup writes each (row, column chunk)'s run starts (depth, position) compacted at
         // the chunk's dense offset -- no depth array --; a thread per row merges the seams
         // between chunks, a scan of the kept counts places the runs, and a wave per chunk copies
@@ -2231,40 +1882,6 @@ extern "C" int rcp_coverage_rle(const rcp_readset* rs, const rcp_rows_desc* rows
         HIP_TRY(hipMemcpyAsync(&h_bad, bad.p, 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (h_bad) return fail(RCP_EINVAL, "internal: run starts and chunk records disagree");
-    } else {
-        // the pileup counts each row's runs as it writes the depth (csr_runs, + the seams
-        // between its wave sub-chunks); a scan of the counts places every row's runs
-        PoolBuf d_cov(s), d_off(s), d_count(s), temp(s);
-        HIP_TRY(d_cov.alloc(4 * std::max<int64_t>(n, 1)));
-        HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
-        HIP_TRY(d_count.alloc(8 * ((size_t)R + 1)));
-        HIP_TRY(res->valid.alloc(std::max<int32_t>(R, 1)));
-        HIP_TRY(res->run_off.alloc(8 * ((size_t)R + 1)));
-        HIP_TRY(hipMemcpyAsync(d_off.p, off.data(), 8 * ((size_t)R + 1), hipMemcpyHostToDevice, s));
-        rc = calc_coverage_dev(plan, d_off.as<int64_t>(), d_cov.as<int32_t>(), res->valid.as<uint8_t>(),
-                               d_count.as<int64_t>(), s);
-        if (rc) return rc;
-        rc = rcp_plan_status(plan, nullptr);
-        if (rc) return rc;
-        size_t tb = 0;
-        HIP_TRY(rcp_rle_encode_dev(R, nullptr, nullptr, d_count.as<int64_t>(), res->run_off.as<int64_t>(), nullptr, &tb,
-                                   nullptr, nullptr, 0, s));
-        HIP_TRY(temp.alloc(std::max<size_t>(tb, 1)));
-        HIP_TRY(rcp_rle_encode_dev(R, nullptr, nullptr, d_count.as<int64_t>(), res->run_off.as<int64_t>(), temp.p, &tb,
-                                   nullptr, nullptr, 3, s));
-        int64_t nr = 0;
-        HIP_TRY(hipMemcpyAsync(&nr, res->run_off.as<int64_t>() + R, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        res->n_runs = nr;
-        HIP_TRY(res->values.alloc(4 * (size_t)std::max<int64_t>(nr, 1)));
-        HIP_TRY(res->lengths.alloc(4 * (size_t)std::max<int64_t>(nr, 1)));
-        HIP_TRY(hipMemsetAsync(d_count.p, 0, 4, s));  // the counts are scanned: their words are free
-        HIP_TRY(rcp_rle_encode_dev(R, d_off.as<int64_t>(), d_cov.as<int32_t>(), nullptr, res->run_off.as<int64_t>(),
-                                   d_count.p, nullptr, res->values.as<int32_t>(), res->lengths.as<int32_t>(), 2, s));
-        uint32_t h_bad = 0;
-        HIP_TRY(hipMemcpyAsync(&h_bad, d_count.p, 4, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (h_bad) return fail(RCP_EINVAL, "internal: run counts and emitted runs disagree");
     }
     *out = res.release();
     return RCP_OK;

@@ -195,15 +195,10 @@ __device__ __forceinline__ void ps_prepare(PairStream& ps, int32_t gps, int32_t 
     ps.pa = ps.pl;
 }
 
-// Candidate slot u of a lane in a batch: lane + 64 u, or (RCP_PS_INTERLEAVE) 4 lane + u, so the
-// 64 adds of one instruction are 4 reads apart (fewer same-bank / same-address LDS atomics on
-// start-sorted reads)
-#ifndef RCP_PS_INTERLEAVE
-#define RCP_PS_INTERLEAVE 1  // C3 pass 0.760-0.770 -> 0.753-0.755 ms (interp kernel 0.112 -> 0.106), profiles/r03/pipeline/ps_interleave_ab.log
-#endif
-__device__ __forceinline__ uint32_t ps_slot(int lane, int u) {
-    return RCP_PS_INTERLEAVE ? 4u * (uint32_t)lane + (uint32_t)u : (uint32_t)lane + 64u * (uint32_t)u;
-}
+// Candidate slot u of a lane in a batch: 4 lane + u, so the 64 adds of one instruction are 4
+// reads apart (fewer same-bank / same-address LDS atomics on start-sorted reads than lane + 64 u:
+// C3 pass 0.760-0.770 -> 0.753-0.755 ms, profiles/r03/pipeline/ps_interleave_ab.log)
+__device__ __forceinline__ uint32_t ps_slot(int lane, int u) { return 4u * (uint32_t)lane + (uint32_t)u; }
 
 // Issue the loads of batch [q0, q0 + 256) (q0 < N; lanes past N load the last candidate again).
 __device__ __forceinline__ void ps_load(const RcpPlanDev& P, PairStream& ps, uint32_t q0, int2 (&dst)[4]) {
@@ -592,10 +587,6 @@ __global__ void rcp_dirk_kernel(int64_t n_entries, const int32_t* __restrict__ d
 // =================================================================================
 // locate: per (row, segment, stream) read ranges, the NULL rules, heavy-row slots
 // =================================================================================
-#ifndef RCP_LOC_ABL
-#define RCP_LOC_ABL 0  // timing ablations only (wrong results), bits: 1 no side writes, 2 no bucket searches,
-                       // 4 no crange / record writes, 8 nothing after the row_info load
-#endif
 // Row positions [*p0, *p0 + *np) that column chunk (part, first bin k0) piles up for a
 // valid row of nominal length nr, mirroring the pileup kernel's metadata stage; false when
 // that stage would not pile the chunk (interpolated, wide median, width mismatch, empty).
@@ -657,10 +648,7 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
         // answer is the number of keys below the threshold) or, in a denser bucket, the keys at
         // offsets m_i = (i + 1) n / 15: c keys below the threshold put the answer in
         // (m_{c-1}, m_c] (rcp_dirk_offset), searched below
-#ifndef RCP_DIRK_QUADS
-#define RCP_DIRK_QUADS 4  // 16-byte words of the entry half read per search (keys: 4 q - 2)
-#endif
-        constexpr int kQ = RCP_DIRK_QUADS, kKeys = 4 * kQ - 2;
+        constexpr int kQ = 4, kKeys = 4 * kQ - 2;  // 16-byte words of the entry half read per search
         static_assert(kKeys == kDirKeys, "the search reads the keys rcp_dirk_kernel writes");
         int4 w[K][kQ];
 #pragma unroll
@@ -691,54 +679,16 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
         }
     }
     const int32_t* se = reinterpret_cast<const int32_t*>(P.se);
-    // wide ranges: 8-ary steps, the 7 probes of every unfinished search in flight together
-    // (p_j = lo + j len / 8; c probes below the threshold leave (p_c, p_{c+1}]), then bisection
-#ifndef RCP_LOC_KARY
-#define RCP_LOC_KARY 0  // 1: 8-ary steps (C4 / C5 locate slower: profiles/r04/locate_ab.log)
-#endif
-    while (RCP_LOC_KARY && !(RCP_LOC_ABL & 2)) {
-        constexpr int kP = 7;
-        int32_t kv[K][kP];
-        uint32_t len[K];
-        bool any = false;
-#pragma unroll
-        for (int u = 0; u < K; ++u) {
-            len[u] = hi[u] - lo[u];
-            if (lo[u] < hi[u] && len[u] >= 32u) {
-                any = true;
-#pragma unroll
-                for (int j = 1; j <= kP; ++j) {
-                    const uint32_t m = lo[u] + (uint32_t)(((uint64_t)j * len[u]) >> 3);
-                    kv[u][j - 1] = up[u] ? se[(size_t)m << 1] : P.pmax[m];
-                }
-            }
-        }
-        if (!any) break;
-#pragma unroll
-        for (int u = 0; u < K; ++u) {
-            if (lo[u] < hi[u] && len[u] >= 32u) {
-                int c = 0;
-#pragma unroll
-                for (int j = 0; j < kP; ++j) c += (int64_t)kv[u][j] < thr[u] ? 1 : 0;
-                const uint32_t l0 = lo[u];
-                if (c > 0) lo[u] = l0 + (uint32_t)(((uint64_t)c * len[u]) >> 3) + 1u;
-                if (c < kP) hi[u] = l0 + (uint32_t)(((uint64_t)(c + 1) * len[u]) >> 3);
-            }
-        }
-    }
-    // bisection down to RCP_LOC_LIN keys, then one pass that loads them all at once and counts
-    // those below the threshold (one round trip instead of log2 RCP_LOC_LIN dependent ones)
-#ifndef RCP_LOC_LIN
-#define RCP_LOC_LIN 0  // 16: a last linear pass over <= 16 keys (slower: profiles/r04/locate_lin_ab.log)
-#endif
-    constexpr uint32_t kLin = RCP_LOC_LIN;
-    while (!(RCP_LOC_ABL & 2)) {
+    // bisection to the answer (an 8-ary step -- 7 probes per search in flight -- and a last
+    // linear pass over <= 16 keys both measured slower on C4 / C5: profiles/r04/locate_ab.log,
+    // locate_lin_ab.log)
+    while (true) {
         uint32_t m[K];
         int32_t kv[K];
         bool any = false;
 #pragma unroll
         for (int u = 0; u < K; ++u) {
-            if (lo[u] < hi[u] && hi[u] - lo[u] > kLin) {
+            if (lo[u] < hi[u]) {
                 m[u] = lo[u] + ((hi[u] - lo[u]) >> 1);
                 kv[u] = up[u] ? se[(size_t)m[u] << 1] : P.pmax[m[u]];
                 any = true;
@@ -747,31 +697,8 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
         if (!any) break;
 #pragma unroll
         for (int u = 0; u < K; ++u) {
-            if (lo[u] < hi[u] && hi[u] - lo[u] > kLin) {
+            if (lo[u] < hi[u]) {
                 if ((int64_t)kv[u] < thr[u]) lo[u] = m[u] + 1; else hi[u] = m[u];
-            }
-        }
-    }
-    if (kLin > 0 && !(RCP_LOC_ABL & 2)) {
-        int32_t kv[K][kLin > 0 ? kLin : 1];
-#pragma unroll
-        for (int u = 0; u < K; ++u) {
-            if (lo[u] < hi[u]) {
-#pragma unroll
-                for (uint32_t i = 0; i < kLin; ++i) {
-                    const uint32_t m = min(lo[u] + i, hi[u] - 1);  // (clamped: inside the arrays)
-                    kv[u][i] = up[u] ? se[(size_t)m << 1] : P.pmax[m];
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < K; ++u) {
-            if (lo[u] < hi[u]) {
-                const uint32_t n = hi[u] - lo[u];
-                uint32_t c = 0;
-#pragma unroll
-                for (uint32_t i = 0; i < kLin; ++i) c += (i < n && (int64_t)kv[u][i] < thr[u]) ? 1u : 0u;
-                lo[u] += c;
             }
         }
     }
@@ -786,9 +713,8 @@ __device__ __forceinline__ void dir_bound_multi(const RcpPlanDev& P, const int64
 // counts with DPP.  For a single-range row the lanes also split the per-chunk range searches.
 // Every search is bounded by the bucket directory and independent of the others: the
 // dependent chain per lane is one bucket search, not a sequence of them.
-#ifndef RCP_LOC_WPE
-#define RCP_LOC_WPE 1
-#endif
+constexpr int kLocWpe = 1;   // waves per SIMD asked of the KS = 4 / 8 variants
+constexpr int kLocWpe2 = 6;  // ... of the KS = 2 variant (<= 80 VGPRs)
 
 // KS: searches of one lockstep round per lane of a single-range row (2: plans of <= 3 column
 // chunks, 4: <= 7, 8: more, one round); KP: searches per round of the (segment, stream) pair
@@ -814,10 +740,6 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
 #pragma unroll
             for (int u = 0; u < (int)(sizeof(RcpRowInfo) / 16); ++u) d[u] = make_uint4(0u, 0u, 0u, 0u);
         }
-    }
-    if (RCP_LOC_ABL & 8) {
-        if (in_row && ri.j0 == -12345) P.rec[r].flags = ri.j1;  // keeps the load
-        return;
     }
     const int j0 = ri.j0, j1 = ri.j1;
     const int32_t chrom = in_row ? ri.chrom : -1;
@@ -1050,13 +972,13 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
     // side outputs a fast row needs only on the heavy path when the pileup is a lean or
     // bin-difference kernel (they read the record): its (lo, hi) in seg_lo / seg_hi and ncand,
     // for rcp_heavy_pileup_kernel (4 scattered stores per row fewer: C4 locate -14 us,
-    // profiles/r04/r4j/ab.log l1)
-    const bool rec_only = fast && (P.lean == 1 || P.lean == 2 || P.lean == 4);
+    // profiles/r04/r4j/ab.log l1).  Not when the plan interpolates rows: rcp_interp_kernel piles
+    // an interpolated row from seg_lo / seg_hi (block_window_depth), and a lean plan may hold
+    // such rows (a row shorter than its bins among power-of-two-binned ones)
+    const bool rec_only = fast && P.n_interp == 0 && (P.lean == 1 || P.lean == 2 || P.lean == 4);
     if (in_row && q == 0) {
-#if !(RCP_LOC_ABL & 1)
         P.valid[r] = valid ? 1 : 0;
         if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
-#endif
         // skewed rows only: many candidates per column chunk (each chunk of a row is one
         // wave's work) AND a deep pileup (> 2 reads per position), so a long row with
         // proportionally many reads stays on the workgroup path
@@ -1071,7 +993,6 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
                 P.heavy_nslice[u] = (ncand + (uint32_t)P.heavy_slice - 1) / (uint32_t)P.heavy_slice;
             }
         }
-#if !(RCP_LOC_ABL & 1)
         if (!rec_only || slot >= 0) {
             P.ncand[r] = ncand;
             if (split1) {
@@ -1079,7 +1000,6 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
                 P.seg_hi[j0 * 3] = hi0;
             }
         }
-#endif
     }
     slot = qperm<0x00>(slot);
     const bool cr = P.crange != nullptr && fast && valid && slot < 0;
@@ -1100,7 +1020,7 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
             }
             // merged layout: one stream, so dense (row, chunk) words -- a wave's writes are
             // whole lines (stride 3, as the stranded layout below, measured ~1 us slower on C4)
-            if (!(RCP_LOC_ABL & 4)) P.crange[(size_t)r * nc + c] = make_uint2(clo, chi);
+            P.crange[(size_t)r * nc + c] = make_uint2(clo, chi);
             if (item_w && chi > clo) atomicAdd(&item_w[(threadIdx.x / LPR) >> 5][c], chi - clo);
         }
     } else if (cr && q < 3) {
@@ -1140,19 +1060,12 @@ __device__ __forceinline__ void locate_rows(const RcpPlanDev& P, uint32_t (*xres
     }
     const uint4* src = reinterpret_cast<const uint4*>(&rec);
     uint4* dst = reinterpret_cast<uint4*>(P.rec + r);
-    if (RCP_LOC_ABL & 4) {
-        if (rec.lo[0] == 0x7fffffffu) dst[0] = src[0];  // keeps the computation
-        return;
-    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) dst[u] = src[u];
 }
 
-#ifndef RCP_LOC_WPE2
-#define RCP_LOC_WPE2 6  // waves per SIMD asked of the KS = 2 variant (<= 80 VGPRs)
-#endif
 template <int KS, int KP>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS == 2 ? RCP_LOC_WPE2 : RCP_LOC_WPE)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS == 2 ? kLocWpe2 : kLocWpe)))
 rcp_locate_kernel(RcpPlanDev P) {
     constexpr int LPR = 4;                 // lanes per row (a quad)
     __shared__ uint32_t xres[kBlock / LPR][2 * RCP_MAX_CRANGE_CHUNKS];  // per row: chunk bounds
@@ -1192,10 +1105,7 @@ rcp_locate_kernel(RcpPlanDev P) {
 // =================================================================================
 // heavy rows: slice pileup
 // =================================================================================
-#ifndef RCP_HEAVY_LOADS
-#define RCP_HEAVY_LOADS 16
-#endif
-constexpr int kHeavyLoads = RCP_HEAVY_LOADS;  // = RCP_HEAVY_SLICE / kBlock: one round trip per slice
+constexpr int kHeavyLoads = 16;  // = the heavy slice (4096 reads) / kBlock: one round trip per slice
 
 __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) {
     // dynamic LDS only (a static array on top of the 160 KB dynamic limit fails the launch
@@ -1301,25 +1211,12 @@ __global__ void __launch_bounds__(kBlock) rcp_heavy_pileup_kernel(RcpPlanDev P) 
 // chunk) is resolved once per workgroup by one thread per row (parallel binary searches),
 // and each wave issues the loads of its NEXT row's first 256 candidate reads before
 // working on the current row's LDS, so a row's HBM round trip overlaps the previous row.
-#ifndef RCP_PILE_WAVES
-#define RCP_PILE_WAVES 8
-#endif
-#ifndef RCP_PILE_ROUNDS
-#define RCP_PILE_ROUNDS 4
-#endif
-constexpr int kPWaves = RCP_PILE_WAVES;  // waves per pileup workgroup (they share one stage)
+constexpr int kPWaves = 8;  // waves per pileup workgroup (they share one stage)
 constexpr int kPBlock = 64 * kPWaves;
-constexpr int kRounds = RCP_PILE_ROUNDS;
+constexpr int kRounds = 4;  // at most 4 rounds of kTile rows per workgroup (RcpPlanDev::rounds)
 static_assert(kTile % kPWaves == 0, "a round's rows are split evenly over the waves");
 constexpr int kRowsPerWave = kTile / kPWaves;  // rows a wave piles per round
-#ifndef RCP_PF_AHEAD
-#define RCP_PF_AHEAD 1
-#endif
-constexpr int kAhead = RCP_PF_AHEAD;  // rows whose first reads are prefetched
-#ifndef RCP_STAGE_BUFS
-#define RCP_STAGE_BUFS 1
-#endif
-constexpr int kStageBufs = RCP_STAGE_BUFS;  // 2: double-buffered stage (epilogue overlaps the next round)
+constexpr int kAhead = 1;  // rows whose first reads are prefetched
 constexpr int kRows = kTile * kRounds;  // rows per workgroup
 
 struct RowMeta {  // [kRows] each, in LDS
@@ -1493,11 +1390,8 @@ __device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart
         }
         // the merged layout's chunk range: its address does not depend on the record, so it is
         // loaded with it (one round trip, not two); used only when the record says CRANGE
-#ifndef RCP_DECODE_PRE
-#define RCP_DECODE_PRE 1
-#endif
         uint2 cr_pre = make_uint2(0u, 0u);
-        if (RCP_DECODE_PRE && P.crange && P.merged) cr_pre = P.crange[(size_t)r * P.n_chunks_total + cidx];
+        if (P.crange && P.merged) cr_pre = P.crange[(size_t)r * P.n_chunks_total + cidx];
         int32_t head, L;
         rcp_part_slice(part, rec.row_len, &head, &L);
         const int32_t n = CSR ? L : part.n_bins;
@@ -1557,7 +1451,7 @@ __device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart
                     if (rec.flags & RCP_REC_CRANGE) {
                         // exact ranges for this chunk from the locate kernel
                         if (P.merged) {  // one stream: dense (row, chunk) words
-                            const uint2 v = RCP_DECODE_PRE ? cr_pre : P.crange[(size_t)r * P.n_chunks_total + cidx];
+                            const uint2 v = cr_pre;
                             m.lo[0] = v.x;
                             m.hi[0] = v.y;
                             m.lo[1] = m.hi[1] = m.lo[2] = m.hi[2] = 0;
@@ -1586,14 +1480,8 @@ __device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart
     return m;
 }
 
-#ifndef RCP_GEN_ABL
-#define RCP_GEN_ABL 0  // timing ablations only (wrong results): 1 no output stores, 2 no read loads / adds
-#endif
-#ifndef RCP_GEN_WPE
-#define RCP_GEN_WPE 4
-#endif
 template <bool MEDIAN, bool CSR, bool UNI>
-__global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RCP_GEN_WPE))) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
+__global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4))) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
                                                             int64_t* __restrict__ binsum) {
     // UNI (plan st != null): reads of one width, streamed as their starts alone (the lean kernel's
     // start-only stream): 4-B loads, end = start + st_w formed when a read is added
@@ -1637,7 +1525,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
     const int RS = stage_stride(P.stage_cap);
     int32_t* diff = reinterpret_cast<int32_t*>(smem) + wave * (P.wave_words + 8) + 8;
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * (P.wave_words + 8);
-    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : kStageBufs * T * RS));
+    RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : T * RS));
 
     // ---- per-row metadata, one thread per row, from the locate kernel's 64-byte records
     if (tid < rows_wg) {
@@ -1654,7 +1542,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
     [[maybe_unused]] const int n_steps = kRowsPerWave * rounds;
     auto prefetch = [&](int i, RdT* dst) {
         const RowMeta m = uniform_meta(meta[i]);
-        const uint32_t n = (m.flag == 0 && m.fast && !(RCP_GEN_ABL & 2)) ? fast_candidates(m) : 0;
+        const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
         if (n) {  // wave-uniform
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -1673,7 +1561,6 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
     // and column quads t / 16, t / 16 + 32, ...: one 16-B stage read feeds four stores, and
     // the 16 lanes of a quad column write 16 consecutive rows (128 B) of one column.
     auto flush = [&](int rd) {
-        if (RCP_GEN_ABL & 1) return;
         const int rbase = rd * T;
         const int ii = tid & (T - 1);
         const int r = row0 + rbase + ii;
@@ -1686,7 +1573,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
         const int32_t kq = k0 + 4 * (tid / T);
         const size_t o0 = (size_t)(part.col_off + kq) * R + (size_t)r;
         const size_t ostep = (size_t)kStep * R;
-        const uint32_t* st0 = stage + (rd % kStageBufs) * T * RS + ii * RS + 4 * (tid / T);
+        const uint32_t* st0 = stage + ii * RS + 4 * (tid / T);
         // value of bin k from its stage count: zero row / one divisor / splitVector layout
         const double sc = P.scale;
         const int32_t den = MEDIAN ? 2 : bs;
@@ -1761,7 +1648,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
     // pile row i of the workgroup (round i / T), its first reads in `cur`
     auto pile_row = [&](int i, RdT (&cur)[4]) __attribute__((always_inline)) {
         const RowMeta m = uniform_meta(meta[i]);
-        uint32_t* sbuf = stage + ((i / T) % kStageBufs) * T * RS;  // this round's stage
+        uint32_t* sbuf = stage;  // this round's stage
         if (m.flag == 0) {  // wave-uniform: scalar branch
             const int r = row0 + i;
             const int32_t npos = m.npos;
@@ -1800,7 +1687,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
                     carry = wave_sum(carry);
                     for (int q = lane; q <= sn; q += 64) diff[lp(q, sh)] = g[base + q] + (q == 0 ? carry : 0);
                 } else if (m.fast && whole) {
-                    const uint32_t n = (RCP_GEN_ABL & 2) ? 0u : fast_candidates(m);
+                    const uint32_t n = fast_candidates(m);
                     // batch q0 + 256 is loaded while batch q0 is added
                     for (uint32_t q0 = 0; q0 < n; q0 += 256) {
                         RdT nx[4];
@@ -1860,22 +1747,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
                     if (lane == 0) P.csr_sub[P.csr_sub_off[r] + cidx + s0 / P.chunk_cap] = make_int2((int32_t)e, lastv);
                 } else if (CSR) {
                     int32_t* orow = P.csr_out + P.csr_off[r];
-                    // run starts after this sub-chunk's first position: position q - 1 is the
-                    // lane below (wave_shr:1), lane 0's the last lane of the step before
-                    int32_t runs = 0, carry = 0;
-                    for (int32_t q0 = 0; q0 < sn; q0 += 64) {
-                        const int32_t q = q0 + lane;
-                        const bool in = q < sn;
-                        const int32_t v = in ? diff[lp(q, sh)] : 0;
-                        if (in) orow[k0 + s0 + q] = v;
-                        const int32_t pv = __builtin_amdgcn_update_dpp(carry, v, 0x138, 0xf, 0xf, false);
-                        runs += (in && q > 0 && v != pv) ? 1 : 0;
-                        carry = __builtin_amdgcn_readlane(v, 63);
-                    }
-                    if (P.csr_runs) {  // kernel argument: scalar branch
-                        runs = wave_sum(runs) + (k0 + s0 == 0 ? 1 : 0);
-                        if (lane == 0) atomicAdd(P.csr_runs + r, (unsigned long long)runs);
-                    }
+                    for (int32_t q = lane; q < sn; q += 64) orow[k0 + s0 + q] = diff[lp(q, sh)];
                 } else if (MEDIAN) {
                     for (int32_t k = k0 + lane; k < kend; k += 64) {
                         const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
@@ -1935,18 +1807,10 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RC
             pile_step(rd * kRowsPerWave + s2 + 1, bufB, bufA);
         }
         if (CSR) continue;
-        if (kStageBufs == 2) {
-            // double-buffered stage: round rd - 1 is written while other waves still pile
-            // round rd; one barrier per round; the last round is written after the loop
-            if (rd > 0) flush(rd - 1);
-            lds_barrier();
-        } else {
-            lds_barrier();
-            flush(rd);
-            lds_barrier();
-        }
+        lds_barrier();
+        flush(rd);
+        lds_barrier();
     }
-    if (!CSR && kStageBufs == 2) flush(rounds - 1);
 }
 
 
@@ -1972,43 +1836,20 @@ struct RowWin {
     static constexpr int words = 8 + 64 * ((1 << SH) + 4);  // per wave: 8 zero words + padded array
 };
 constexpr int kRWCap = RowWin<kRWSh>::cap;
-// LDS-staged variant (P.rows_lds): one workgroup of RCP_RWL_WAVES waves per CU whose tiles'
-// bin numerators (uint32, 16 rows x n_cols) sit in RCP_RWL_SLOTS LDS slots
-#ifndef RCP_RWL_WAVES
-#define RCP_RWL_WAVES 8
-#endif
-#ifndef RCP_RWL_SH
-#define RCP_RWL_SH 5
-#endif
-#ifndef RCP_RWL_SLOTS
-#define RCP_RWL_SLOTS 2
-#endif
-constexpr int kRLWaves = RCP_RWL_WAVES, kRLSh = RCP_RWL_SH, kRLSlots = RCP_RWL_SLOTS;
-#ifndef RCP_RWG_SLOTS
-#define RCP_RWG_SLOTS 4  // tiles in flight per workgroup (<= 6)
-#endif
-#ifndef RCP_RWG_WAVES
-#define RCP_RWG_WAVES 16  // waves per workgroup of the HBM-staged variants (16 per CU either way;
-                          // one 16-wave workgroup per CU keeps fewer tiles in flight: C3 pileup
-                          // 0.573 -> 0.495 ms with fp64 staging, profiles/r04/r4m/c3.log)
-#endif
+// The tiles' bin numerators are staged row-major in HBM (uint32, P.rm32) and flushed
+// column-major by the last wave to finish one of a tile's rows.  (Staging them in LDS instead --
+// one 8-wave workgroup per CU, two 16-row slots -- measured slower: C3 0.73 vs 0.57 ms, and the
+// fp64 means instead of numerators 1.21x vs 1.09x of the algorithmic traffic;
+// profiles/r04/r4j/c3.log, r4n/)
+constexpr int kRWGSlots = 4;   // tiles in flight per workgroup (<= 6)
+constexpr int kRWGWaves = 16;  // waves per workgroup of the staged kernel (one 16-wave workgroup
+                               // per CU keeps fewer tiles in flight: C3 pileup 0.573 -> 0.495 ms,
+                               // profiles/r04/r4m/c3.log)
 constexpr size_t kRowsQueueBytes = 64;  // tile queue word + slot table
 
 extern "C" int rcp_rows_window_cap(void) { return kRWCap; }
-extern "C" int rcp_rows_lds_window_cap(void) { return RowWin<kRLSh>::cap; }
 
-static size_t rows_lds_bytes(int lds_stride, int waves, int words, int slots) {
-    return 4 * (size_t)waves * words + kRowsQueueBytes +
-           (size_t)slots * kTile * (4 * (size_t)lds_stride + 8 * RCP_MAX_PARTS);
-}
-
-// Row stride (words) of the LDS stage for n_cols columns, == 4 mod 64 so that the flush's 64
-// lanes (16 rows x 4 columns) hit 64 distinct banks; 0 when the stage does not fit.
-extern "C" int rcp_rows_lds_stride(int64_t n_cols) {
-    if (n_cols <= 0 || n_cols > (1 << 20)) return 0;
-    const int64_t ldw = n_cols <= 4 ? 4 : (n_cols - 4 + 63) / 64 * 64 + 4;
-    return rows_lds_bytes((int)ldw, kRLWaves, RowWin<kRLSh>::words, kRLSlots) <= 160 * 1024 ? (int)ldw : 0;
-}
+static size_t rows_lds_bytes(int waves, int words) { return 4 * (size_t)waves * words + kRowsQueueBytes; }
 
 // Stores of a row's bins without a stage (binsum, which keeps the column-major layout): 8 bytes
 // per 128-B column line; the 16 rows of a line are claimed together by waves of one XCD, so
@@ -2024,12 +1865,11 @@ __device__ __forceinline__ double rows_mean(uint32_t num, double sc, bool pow2, 
     return rcp_div_rn((double)num * sc, dd1, rdd1);  // w == bs + 1
 }
 
-// MODE 2: bin numerators staged in LDS slots (P.rows_lds); 1: in the row-major HBM stage
-// P.rm32 (row stride n_cols, part info P.rinfo); 3: the means themselves (doubles) in the HBM
-// stage P.rm64; 0 (binsum): means stored straight into the column-major output.  Staged tiles
-// are flushed by the last wave to finish one of their rows.
+// MODE 1: bin numerators staged in the row-major HBM stage P.rm32 (row stride n_cols, part
+// info P.rinfo), tiles flushed by the last wave to finish one of their rows; 0 (binsum): means
+// stored straight into the column-major output.
 template <int MODE, int WAVES, int SH>
-__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? (WAVES + 3) / 4 : 4)))
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4)))
 rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restrict__ binsum) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int kWinCap = RowWin<SH>::cap, kWords = RowWin<SH>::words;
@@ -2051,26 +1891,17 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     constexpr uint32_t kEmpty = 0xFFFFFFFEu, kDone = 0xFFFFFFFFu;
     // tile slots of the flush: tile id, rows finished (kFree: flushed),
     // and the workgroup's tile sequence number (slot = seq % kSlots)
-    constexpr bool LDS = MODE == 2;
-    constexpr int kSlots = LDS ? kRLSlots : RCP_RWG_SLOTS;
+    constexpr int kSlots = kRWGSlots;
     static_assert(8 + 8 * kSlots + 4 <= (int)kRowsQueueBytes, "slot table");
     constexpr uint32_t kFree = 0xFFFFFFFFu;
     uint32_t* slot_tile = reinterpret_cast<uint32_t*>(queue + 1);
     uint32_t* slot_cnt = slot_tile + kSlots;
     uint32_t* seq = slot_cnt + kSlots;
-    // LDS stage: [slot][row of the tile][ldw] numerators, then [slot][row][part] {bs, lay}
-    // (bs 0: zeros, -1: left to the interpolation kernel)
-    const int ldw = LDS ? P.rows_lds : (MODE == 1 || MODE == 3 ? (int)P.n_cols : 0);
-    uint32_t* lstage = reinterpret_cast<uint32_t*>(smem + 4 * WAVES * kWords + kRowsQueueBytes);
-    int2* linfo = reinterpret_cast<int2*>(lstage + (size_t)kSlots * kTile * ldw);
-    // row r's staged numerators and part info
-    auto stage_row = [&](int r, int sl) -> uint32_t* {
-        return LDS ? lstage + (size_t)(sl * kTile + (r & (kTile - 1))) * ldw
-                   : (MODE == 1 ? P.rm32 + (size_t)r * ldw : nullptr);
-    };
-    auto stage_info = [&](int r, int sl) -> int2* {
-        return LDS ? linfo + (sl * kTile + (r & (kTile - 1))) * RCP_MAX_PARTS : P.rinfo + (size_t)r * RCP_MAX_PARTS;
-    };
+    // row r's staged numerators [n_cols] and part info [part] {bs, lay} (bs 0: zeros, -1: left
+    // to the interpolation kernel)
+    const int ldw = MODE == 1 ? (int)P.n_cols : 0;
+    auto stage_row = [&](int r, int) -> uint32_t* { return MODE == 1 ? P.rm32 + (size_t)r * ldw : nullptr; };
+    auto stage_info = [&](int r, int) -> int2* { return P.rinfo + (size_t)r * RCP_MAX_PARTS; };
     if (threadIdx.x == 0) *queue = ((unsigned long long)kEmpty << 32) | kTile;
     if (threadIdx.x < kSlots) {
         slot_tile[threadIdx.x] = kDone;
@@ -2129,10 +1960,6 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     // the matrix cell (row r, column c) of the unstaged mode (binsum)
     auto cell = [&](int r, int64_t c) -> double* { return out + (size_t)c * R + r; };
     auto zero_cols = [&](int r, const RcpPart& part, int32_t n) {
-        if (MODE == 3) {
-            for (int32_t k = lane; k < n; k += 64) P.rm64[(size_t)r * ldw + part.col_off + k] = 0.0;
-            return;
-        }
         if (staged) return;  // the row's part info says zeros
         for (int32_t k = lane; k < n; k += 64) {
             rows_store(0.0, cell(r, part.col_off + k));
@@ -2146,22 +1973,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         const int32_t t16 = (int32_t)T * kTile;
         const int32_t nrow = min(kTile, P.n_rows - t16);
         const int i = lane & 15, cq = lane >> 4;
-        if (MODE == 3) {
-            const double* src = P.rm64 + (size_t)(t16 + i) * (size_t)ldw;
-            for (int32_t c0 = 0; c0 < ldw; c0 += 32) {
-                double v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int32_t c = c0 + 4 * u + cq;
-                    v[u] = (i < nrow && c < ldw) ? src[c] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int32_t c = c0 + 4 * u + cq;
-                    if (i < nrow && c < ldw) __builtin_nontemporal_store(v[u], out + (size_t)c * R + (size_t)(t16 + i));
-                }
-            }
-        } else {
+        {
             // numerators -> means (the pile's operations), 4 columns x 16 rows per store
             const uint32_t* srow = stage_row(t16 + i, sl);
             const int2* inf = stage_info(t16 + i, sl);
@@ -2223,7 +2035,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         const int32_t heavy = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.z);
         uint32_t* const srow = stage_row(r, sl);
         int2* const sinfo = stage_info(r, sl);
-        if (staged && MODE != 3 && lane < P.n_parts) sinfo[lane] = make_int2(0, -1);  // zeros unless piled below
+        if (staged && lane < P.n_parts) sinfo[lane] = make_int2(0, -1);  // zeros unless piled below
         if (!(flags & RCP_REC_VALID)) {  // NULL row -> zeros (profile.R:191-197)
             for (int p = 0; p < P.n_parts; ++p) zero_cols(r, P.part[p], P.part[p].n_bins);
             return;
@@ -2257,7 +2069,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             rcp_part_slice(part, nr, &head, &L);
             const int32_t n = part.n_bins;
             if (!part.per_base && L < n) {  // interpolation row: rcp_interp_kernel
-                if (staged && MODE != 3 && lane == 0) sinfo[p] = make_int2(-1, -1);
+                if (staged && lane == 0) sinfo[p] = make_int2(-1, -1);
                 continue;
             }
             if (part.per_base && L != n) {
@@ -2277,7 +2089,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     }
                 }
             }
-            if (staged && MODE != 3 && lane == 0) sinfo[p] = make_int2(bs, lay);
+            if (staged && lane == 0) sinfo[p] = make_int2(bs, lay);
             const int32_t kw = max(1, kWinCap / (bs + (lay >= 0 ? 1 : 0)));  // bins per window
             const bool pow2 = lay < 0 && (bs & (bs - 1)) == 0;
             const double dd = (double)bs, rdd = 1.0 / dd;
@@ -2348,10 +2160,6 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
                     const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
                     const uint32_t num = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
-                    if (MODE == 3) {
-                        P.rm64[(size_t)r * ldw + part.col_off + k] = rows_mean(num, sc, pow2, b - a, bs, dd, rdd, dd1, rdd1);
-                        continue;
-                    }
                     if (staged) {
                         srow[part.col_off + k] = num;
                         continue;
@@ -2403,31 +2211,12 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
 // k + 1 and decodes its 64 row records into the second metadata buffer, and the pile waves
 // prefetch its first reads during item k's last row: no workgroup start-up latency.
 // ---------------------------------------------------------------------------------
-#ifndef RCP_LSTORE_WAVES
-#define RCP_LSTORE_WAVES 4
-#endif
-// 1: three batches of reads in flight per row instead of two (measured neutral on C4 / C5 /
-// C3, tools/ab_variants.sh: kept as a build option, off by default)
-#ifndef RCP_LUNI_RUNS
-#define RCP_LUNI_RUNS 1  // start-only dense rows: one run detection for both atomics (0: per key)
-#endif
-#ifndef RCP_LEAN_ABL
-#define RCP_LEAN_ABL 0  // timing ablations only (wrong results): 1 no LDS adds (loads kept), 2 no output stores
-#endif
-#ifndef RCP_LWPE
-#define RCP_LWPE 6
-#endif
-#ifndef RCP_LRING3
-#define RCP_LRING3 0  // 1: two batches of reads in flight ahead of the one being added (lean kernel)
-#endif
-#ifndef RCP_LBATCH_UNI
-#define RCP_LBATCH_UNI 4  // reads per lane per batch of a start-only (uniform-width) lean plan
-#endif
-#ifndef RCP_LPILE_WAVES
-#define RCP_LPILE_WAVES 8  // pile waves per lean workgroup (<= 16 rows of a round)
-#endif
-constexpr int kLPWaves = RCP_LPILE_WAVES;
-constexpr int kLStoreWaves = RCP_LSTORE_WAVES;
+// Not adopted (same-box A/B): 2 or 6 store waves, 10 pile waves, a third batch
+// of reads in flight per row (neutral), 8-read batches for start-only streams.
+constexpr int kLPWaves = 8;       // pile waves per lean workgroup (<= 16 rows of a round)
+constexpr int kLStoreWaves = 4;
+constexpr int kLWpe = 6;          // waves per SIMD asked of the lean kernel
+constexpr int kLBatchUni = 4;     // reads per lane per batch of a start-only (uniform-width) lean plan
 constexpr int kLBlock = 64 * (kLPWaves + kLStoreWaves);
 constexpr int kLQuads = 64 * kLStoreWaves / kTile;  // column quads per store pass
 constexpr int kLMaxPass = 8;                        // stage_cap <= 4 * kLQuads * kLMaxPass
@@ -2574,11 +2363,8 @@ __device__ __forceinline__ LeanItem lean_item(const RcpPlanDev& P, int code) {
 // cumulative scan (bin-edge differences, as the general kernel) plus a per-row bitmask of the
 // enlarged bins, and store waves divide by the bin width.
 constexpr int kLMaxPassGen = 4;  // general-bins mode: <= 4 * kLQuads * 4 = 256 bins per chunk
-#ifndef RCP_LWPE_GEN
-#define RCP_LWPE_GEN RCP_LWPE
-#endif
 template <int MAXPER, bool GEN, int LR, bool UNI>
-__global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(GEN ? RCP_LWPE_GEN : RCP_LWPE)))
+__global__ void __launch_bounds__(kLBlock) __attribute__((amdgpu_waves_per_eu(kLWpe)))
 rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int T = kTile;
@@ -2590,8 +2376,8 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
     // is formed when the read is added, so the prefetched loads stay in flight until then
     static_assert(!(UNI && GEN), "uniform-width reads: single-range mode only");
     using RdT = typename std::conditional<UNI, int32_t, int2>::type;
-    // reads per lane per batch: start-only streams (4 B per read) keep RCP_LBATCH_UNI in flight
-    constexpr int BL = UNI ? RCP_LBATCH_UNI : 4;
+    // reads per lane per batch
+    constexpr int BL = UNI ? kLBatchUni : 4;
     constexpr uint32_t BQ = 64u * BL;  // reads per batch
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -2711,8 +2497,8 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                 pileup_row_wave(P, it.tile * kIRows + i, m.P0, npos, diff, sh);
             } else {
                 const uint32_t n = lean_candidates(m);
-                // batches of 256 reads, three in flight: `cur` (prefetched with the previous
-                // row), b1, b2; the loop is unrolled over the ring so no buffer is copied
+                // batches of 64 BL reads, two in flight: `cur` (prefetched with the previous row)
+                // and the next
                 auto load_batch = [&](uint32_t q0, RdT (&dst)[BL]) {
                     if (q0 < n) {
 #pragma unroll
@@ -2722,18 +2508,11 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                         }
                     }
                 };
-#ifndef RCP_LDENSE
-#define RCP_LDENSE 1
-#endif
-                const bool dense = RCP_LDENSE && n >= (uint32_t)npos;  // wave-uniform
+                // dense rows (more reads than positions): run-merged adds
+                const bool dense = n >= (uint32_t)npos;  // wave-uniform
                 auto add_batch = [&](uint32_t q0, const RdT (&src)[BL]) {
-                    if (RCP_LEAN_ABL & 1) {  // timing ablation: loads kept, no adds
-#pragma unroll
-                        for (int u = 0; u < BL; ++u) asm volatile("" ::"v"(src[u]));
-                        return;
-                    }
                     if constexpr (UNI) {
-                        if (dense && RCP_LUNI_RUNS) {
+                        if (dense) {  // start-only: one run detection for both atomics
                             const int32_t w = P.st_w;
                             const int32_t lo_w = m.rev ? m.k - m.gpe : m.gps + m.k;
                             const int32_t hi_w = m.rev ? m.k - m.gps : m.gpe + m.k;
@@ -2767,29 +2546,12 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
                             if (q0 + lane + 64u * u < n) lean_add<false>(m, rd_pair(src[u]), diff, sh);
                     }
                 };
-                if (RCP_LRING3) {
-                    // three buffers in rotation (no register copies, so each add waits only for
-                    // its own batch): two batches in flight while one is added
-                    RdT b1[BL], b2[BL];
-                    load_batch(BQ, b1);
-                    for (uint32_t q0 = 0; q0 < n; q0 += 3 * BQ) {
-                        load_batch(q0 + 2 * BQ, b2);
-                        add_batch(q0, cur);
-                        if (q0 + BQ >= n) break;
-                        load_batch(q0 + 3 * BQ, cur);
-                        add_batch(q0 + BQ, b1);
-                        if (q0 + 2 * BQ >= n) break;
-                        load_batch(q0 + 4 * BQ, b1);
-                        add_batch(q0 + 2 * BQ, b2);
-                    }
-                } else {
-                    for (uint32_t q0 = 0; q0 < n; q0 += BQ) {
-                        RdT nx[BL];
-                        load_batch(q0 + BQ, nx);
-                        add_batch(q0, cur);
+                for (uint32_t q0 = 0; q0 < n; q0 += BQ) {
+                    RdT nx[BL];
+                    load_batch(q0 + BQ, nx);
+                    add_batch(q0, cur);
 #pragma unroll
-                        for (int u = 0; u < BL; ++u) cur[u] = nx[u];
-                    }
+                    for (int u = 0; u < BL; ++u) cur[u] = nx[u];
                 }
             }
             lds_order();
@@ -2920,7 +2682,7 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 #pragma unroll
                 for (int j = 0; j < kPass; ++j)
                     if (j < npass) asm volatile("" : "+v"(v[j].x), "+v"(v[j].y), "+v"(v[j].z), "+v"(v[j].w));
-                if (live && !(RCP_LEAN_ABL & 2)) {
+                if (live) {
                     // power-of-two bin width: multiplying by its reciprocal is exact; a NULL row
                     // (flag 1) scales its (unwritten) stage words by 0.0 -> zeros
                     const double rdd = 1.0 / (double)(1 << ((w0 >> 4) & 31));
@@ -2991,15 +2753,12 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 // (R/util.R:74-84 with dif = 0, R/profile.R:159-208).  Per row the work is O(n bins) instead
 // of O(L positions) -- C2's 200 bins of 20 bp instead of 4000 positions in four column chunks
 // -- and a whole row is one wave's pass (no column chunks, no per-chunk read ranges).
-// Workgroups of RCP_BD_WAVES waves own 16-row tiles (one 128-B line of every output column);
+// Workgroups of kBDWaves waves own 16-row tiles (one 128-B line of every output column);
 // each wave piles its rows into its own D / F arrays and stages their numerators; the
 // workgroup then writes the tile column-major.
 // =================================================================================
-#ifndef RCP_BD_WAVES
-#define RCP_BD_WAVES 16  // waves per 16-row tile (16 / RCP_BD_WAVES rows each; C2 pileup 4: 30.8,
-                        // 8: 28.7, 16: 28.1 us, profiles/r04/r4j/ab.log)
-#endif
-constexpr int kBDWaves = RCP_BD_WAVES;
+constexpr int kBDWaves = 16;  // waves per 16-row tile (16 / kBDWaves rows each; C2 pileup 4: 30.8,
+                              // 8: 28.7, 16: 28.1 us, profiles/r04/r4j/ab.log)
 static_assert(kTile % kBDWaves == 0, "a tile's rows are split evenly over the waves");
 constexpr int kBDMaxBins = 512;
 constexpr int kBDMinWidth = 4;
@@ -3273,7 +3032,7 @@ __device__ void block_window_depth(const RcpPlanDev& P, int r, int32_t w0, int32
         // the row's (segment, stream) pairs as one stream of candidate batches, dealt to the
         // block's waves (pileup_row walked the pairs one after the other: one round trip each,
         // a dozen per interpolated C3 gene)
-        if (!(RCP_INTERP_ABL & 2)) pileup_row_wave(P, r, w0, wn, diff, 30, (int)(threadIdx.x >> 6), kWaves);
+        pileup_row_wave(P, r, w0, wn, diff, 30, (int)(threadIdx.x >> 6), kWaves);
     }
     __syncthreads();
     scan_block_depth(diff, per, scratch);
@@ -3383,19 +3142,14 @@ extern "C" hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream)
     const int64_t grid = (4 * (int64_t)P->n_rows + kBlock - 1) / kBlock;  // four lanes per row
     // a single-range row's searches: its two bounds + the interior chunk edges, dealt to the quad;
     // more than 16 (over 8 column chunks) take lockstep rounds of 8 (one chain, not two)
-#ifndef RCP_LOC_KS8
-#define RCP_LOC_KS8 1
-#endif
-#ifndef RCP_LOC_KS2
-#define RCP_LOC_KS2 1  // single-range plans of <= 3 column chunks (<= 8 searches a row): 2 per lane
-#endif
+    // single-range plans of <= 3 column chunks (<= 8 searches a row): 2 per lane
     const int searches = 2 + (P->crange ? 2 * (P->n_chunks_total - 1) : 0);  // a single-range row's
-    if (RCP_LOC_KS8 && P->crange && 2 * P->n_chunks_total > 4 * 4)
+    if (P->crange && 2 * P->n_chunks_total > 4 * 4)
         hipLaunchKernelGGL((rcp_locate_kernel<8, 4>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
     // (occupancy pays on big tables -- C4: 100 -> 91 us -- and plans without chunk searches,
     // C2: 33 -> 30 us; the 25k-row C4 shard runs in one generation anyway and measured 4 us
     // slower: profiles/r04/r4j/ab.log new vs ks2off)
-    else if (RCP_LOC_KS2 && searches <= 2 * 4 && !P->multi_rows && (!P->crange || P->n_rows >= 50000))
+    else if (searches <= 2 * 4 && !P->multi_rows && (!P->crange || P->n_rows >= 50000))
         hipLaunchKernelGGL((rcp_locate_kernel<2, 2>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
     else
         hipLaunchKernelGGL((rcp_locate_kernel<4, 4>), dim3((unsigned)grid), dim3(kBlock), 0, stream, *P);
@@ -3419,7 +3173,7 @@ extern "C" hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_
 }
 
 extern "C" size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr) {
-    const size_t stage_words = csr ? 0 : (size_t)kStageBufs * kTile * stage_stride(P->stage_cap);
+    const size_t stage_words = csr ? 0 : (size_t)kTile * stage_stride(P->stage_cap);
     return 4 * ((size_t)kPWaves * (P->wave_words + 8) + stage_words + (size_t)kRows * kMetaWords + 8);
 }
 
@@ -3504,40 +3258,27 @@ static hipError_t launch_pileup_t(const RcpPlanDev* P, double* out, int64_t* bin
                  : launch_pileup_u<MEDIAN, CSR, false>(P, out, binsum, lds, s);
 }
 
-// dynamic LDS of the row-wave launch: LDS stage, or the HBM-staged kernel's windows
-// (RCP_RWG_WAVES waves; the binsum launch takes the 4-wave unstaged kernel)
-extern "C" size_t rcp_pileup_rows_lds_bytes(const RcpPlanDev* P) {
-    if (P && P->rows_lds > 0) return rows_lds_bytes(P->rows_lds, kRLWaves, RowWin<kRLSh>::words, kRLSlots);
-    return rows_lds_bytes(0, RCP_RWG_WAVES, RowWin<kRWSh>::words, 0);
-}
+// dynamic LDS of the row-wave launch: the staged kernel's windows (kRWGWaves waves; the
+// binsum launch takes the 4-wave unstaged kernel)
+extern "C" size_t rcp_pileup_rows_lds_bytes(const RcpPlanDev*) { return rows_lds_bytes(kRWGWaves, RowWin<kRWSh>::words); }
 
 static hipError_t launch_pileup_rows(const RcpPlanDev* P, double* out, int64_t* binsum, hipStream_t s) {
     // persistent: a multiple of 8 workgroups (workgroup b serves XCD b % 8), never more
-    // workgroups than tiles; four 4-wave workgroups per CU, or as many LDS-staged ones as fit
+    // workgroups than tiles
     const int cus = std::max(1, P->n_cus);
     const int64_t tiles = ((int64_t)P->n_rows + kTile - 1) / kTile;  // at least a tile per workgroup
-    if (P->rows_lds > 0 && !binsum) {
-        const size_t lds = rcp_pileup_rows_lds_bytes(P);
-        auto k = rcp_pileup_rows_kernel<2, kRLWaves, kRLSh>;
-        const hipError_t e = allow_big_lds(k);
-        if (e != hipSuccess) return e;
-        const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(32 / kRLWaves, (160 * 1024) / lds));
-        const int64_t grid = std::min<int64_t>((per_cu * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
-        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * kRLWaves), lds, s, *P, out, binsum);
-        return hipGetLastError();
-    }
-    RcpPlanDev Q = *P;
-    Q.rows_lds = 0;
-    if (binsum || (!P->rm32 && !P->rm64)) {
+    const RcpPlanDev& Q = *P;
+    if (binsum || !P->rm32) {
+        // four 4-wave workgroups per CU, means stored straight into the output
         const int64_t grid = std::min<int64_t>(((int64_t)4 * cus + 7) / 8 * 8, (tiles + 7) / 8 * 8);
         hipLaunchKernelGGL((rcp_pileup_rows_kernel<0, kRWaves, kRWSh>), dim3((unsigned)grid), dim3(64 * kRWaves),
-                           rows_lds_bytes(0, kRWaves, RowWin<kRWSh>::words, 0), s, Q, out, binsum);
+                           rows_lds_bytes(kRWaves, RowWin<kRWSh>::words), s, Q, out, binsum);
         return hipGetLastError();
     }
-    // HBM stage: 16 waves per CU, as RCP_RWG_WAVES-wave workgroups
-    constexpr int kG = RCP_RWG_WAVES;
-    auto k = P->rm64 ? rcp_pileup_rows_kernel<3, kG, kRWSh> : rcp_pileup_rows_kernel<1, kG, kRWSh>;
-    const size_t lds = rows_lds_bytes(0, kG, RowWin<kRWSh>::words, 0);
+    // HBM stage: 16 waves per CU, as kRWGWaves-wave workgroups
+    constexpr int kG = kRWGWaves;
+    auto k = rcp_pileup_rows_kernel<1, kG, kRWSh>;
+    const size_t lds = rows_lds_bytes(kG, RowWin<kRWSh>::words);
     if (lds > 64 * 1024) {
         const hipError_t e = allow_big_lds(k);
         if (e != hipSuccess) return e;
@@ -3856,46 +3597,13 @@ extern "C" hipError_t rcp_cov_runs_dev(int32_t n_rows, const int64_t* d_off, con
     return hipGetLastError();
 }
 
-// The run starts the coverage pileup could not see (rcp_pileup_kernel's csr_runs): the seams
-// between the wave sub-chunks of chunk_cap positions inside the column chunks of chunk_bins
-// positions, a thread per row (most rows have one or two seams); NULL rows (valid 0) keep no
-// runs.
-__global__ void __launch_bounds__(kBlock) rcp_rle_seams_kernel(int32_t n_rows, const int64_t* __restrict__ off,
-                                                             const int32_t* __restrict__ cov,
-                                                             const uint8_t* __restrict__ valid, int32_t chunk_bins,
-                                                             int32_t chunk_cap, unsigned long long* __restrict__ count) {
-    const int r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= n_rows || !valid[r]) return;
-    const int64_t a = off[r];
-    const int64_t L = off[r + 1] - a;
-    unsigned long long c = 0;
-    for (int64_t k0 = 0; k0 < L; k0 += chunk_bins)
-        for (int64_t p = k0 == 0 ? chunk_cap : k0; p < k0 + chunk_bins && p < L; p += chunk_cap)
-            c += cov[a + p] != cov[a + p - 1] ? 1 : 0;
-    if (c) count[r] += c;  // the pileup's atomics have completed (earlier launch)
-}
-
-extern "C" hipError_t rcp_rle_seams_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov,
-                                        const uint8_t* d_valid, int32_t chunk_bins, int32_t chunk_cap,
-                                        int64_t* d_count, hipStream_t stream) {
-    if (n_rows <= 0) return hipSuccess;
-    if (chunk_bins <= 0 || chunk_cap <= 0) return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)((n_rows + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(rcp_rle_seams_kernel, dim3(grid), dim3(kBlock), 0, stream, n_rows, d_off, d_cov, d_valid,
-                       chunk_bins, chunk_cap, reinterpret_cast<unsigned long long*>(d_count));
-    return hipGetLastError();
-}
-
 extern "C" hipError_t rcp_rle_encode_dev(int32_t n_rows, const int64_t* d_off, const int32_t* d_cov, int64_t* d_count,
                                          int64_t* d_run_off, void* temp, size_t* temp_bytes, int32_t* d_values,
                                          int32_t* d_lengths, int pass, hipStream_t stream) {
     // pass 0: temp size of the scan; 1: count + scan (d_run_off[n_rows] = total); 2: emit
-    // (temp: a zeroed uint32 flag, set when a row's runs differ from its count); 3: scan of
-    // counts made elsewhere (d_count[n_rows] must be 0)
+    // (temp: a zeroed uint32 flag, set when a row's runs differ from its count)
     if (pass == 0)
         return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, d_count, d_run_off, (int)n_rows + 1, stream);
-    if (pass == 3)
-        return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, d_count, d_run_off, (int)n_rows + 1, stream);
     const unsigned grid = (unsigned)((n_rows + kRleWaves - 1) / kRleWaves);
     if (pass == 1) {
         hipError_t e = hipMemsetAsync(d_count + n_rows, 0, 8, stream);

@@ -121,9 +121,7 @@ __global__ void __launch_bounds__(kRleBlock) rcp_rle_interp_kernel(RcpRleDev P) 
     interp_finish(t.mode - RCP_RLE_INTERP, L, n, x, t.nbpos >= 0 ? P.nb_pos + t.nbpos : nullptr, P.spl_tb, o, ld);
 }
 
-#ifndef RCP_RLE_WPE
-#define RCP_RLE_WPE 8  // 8 waves per SIMD: two 16-wave workgroups per CU (<= 64 VGPRs)
-#endif
+constexpr int kRleWpe = 8;  // 8 waves per SIMD: two 16-wave workgroups per CU (<= 64 VGPRs)
 constexpr int kTRows = 16;                 // rows per tile: one 128-B line of every column; one wave per row
 constexpr int kTBlock = 64 * kTRows;
 constexpr int kTCols = 128;                // columns per chunk (2 per lane)
@@ -263,7 +261,7 @@ __device__ __forceinline__ void batch_starts(const RunBatch<VT>& b, uint32_t gbl
 // picks it per part when every row of the part qualifies).  LEN: starts from the lengths
 // (load_batch).
 template <bool DBL, int KIND, bool LEN>
-__global__ void __launch_bounds__(kTBlock) __attribute__((amdgpu_waves_per_eu(RCP_RLE_WPE)))
+__global__ void __launch_bounds__(kTBlock) __attribute__((amdgpu_waves_per_eu(kRleWpe)))
 rcp_rle_tile_kernel(RcpRleDev P, int p) {
     constexpr bool MEDIAN = KIND == 1, DENSE = !DBL && KIND == 2;
     using VT = typename std::conditional<DBL, double, int32_t>::type;

@@ -46,10 +46,7 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
         tp[i] = tb[2 * i + 1];
     }
     __syncthreads();
-#ifndef RCP_INTERP_ABL
-#define RCP_INTERP_ABL 0  // timing ablations only (wrong results): 1 no elimination chains, 2 no reads
-#endif
-    if (t == 0 && !(RCP_INTERP_ABL & 1)) {
+    if (t == 0) {
         double c1 = 0.0, cn = 0.0;
         if (n > 3) {
             c1 = c[2] / 2.0 - c[1] / 2.0;

@@ -1,6 +1,6 @@
 /* Checks rcp_div_rn (recoup_amd/csrc/rcp_divrn.h) against IEEE division: exhaustively for
  * numerators 0 .. 2^NBITS - 1 and widths 1 .. DMAX, then on random (numerator < 2^32,
- * width < 2^20, scale factor) triples.  Test infrastructure (tests/test_host.py). */
+ * width < 2^20, scale factor: none, uniform (0, 1) or min(lib) / lib) triples.  Test infrastructure (tests/test_host.py). */
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -29,7 +29,12 @@ int main(int argc, char** argv) {
     for (long i = 0; i < nrand; ++i) {
         const double n = (double)(uint32_t)xr();
         const double dd = (double)(1 + (xr() & 0xFFFFF));
-        const double sc = (i & 1) ? 1.0 : (double)(xr() >> 11) / 9007199254740992.0;
+        double sc = 1.0;
+        if (i % 3 == 1) sc = (double)(xr() >> 11) / 9007199254740992.0;
+        if (i % 3 == 2) {  /* calcLinearFactors: min(lib) / lib of library sizes up to 2^31 */
+            const double lib = (double)(1 + (xr() & 0x7FFFFFFF)), mn = (double)(1 + (uint64_t)(lib * ((double)(xr() >> 11) / 9007199254740992.0)));
+            sc = mn / lib;
+        }
         const double a = n * sc;
         if (rcp_div_rn(a, dd, 1.0 / dd) != a / dd) ++bad;
     }

@@ -285,3 +285,25 @@ def test_dense_bucket_bounds(gpu, kernel):
     for bins in (Bins([("whole", 1024)]), Bins([("whole", 256)])):
         res = Plan(rs, rows, bins, kernel=kernel, heavy_threshold=0).run()
         check(res, oracle_rows.profile(cov, bins))
+
+
+@pytest.mark.parametrize("mode", ["lean", "lean_any"])
+def test_lean_with_interpolated_single_rows(gpu, mode):
+    """Single-range rows shorter than their bins among power-of-two-binned ones: the plan stays
+    on the lean kernel and the short rows go through the interpolation kernel, which piles them
+    from the locate kernel's per-segment ranges -- locate must write them for such plans (a
+    regression: fast rows of lean plans once skipped them and profiled as zeros)."""
+    from recoup_amd.engine import Bins
+    rng = np.random.default_rng(4242)
+    reads = make_reads(rng, 100_000)
+    rows = single_rows(rng, 300, 2000)
+    short = rng.choice(np.arange(2, 300), 40, replace=False)
+    rows.end[short[:20]] = rows.start[short[:20]] + 499   # spline: (1000 - 500) / 1000 >= 0.2
+    rows.end[short[20:]] = rows.start[short[20:]] + 899   # neighborhood: 0.1 < 0.2
+    for bins in (Bins([("whole", 1000)]), Bins([("whole", 1000)], interp="spline")):
+        lean, gen, kind, exp = plans(reads, CHROM_LEN, rows, bins, lean_mode=mode)
+        assert kind == 1
+        assert lean[1][short].all()
+        assert (lean[0][short].sum(axis=1) > 0).all()
+        check(lean, exp, rtol=1e-9, atol=1e-12)
+        same(lean, gen)

@@ -153,11 +153,10 @@ def test_repeated_executions_and_kernel_choice(gpu):
     assert Plan(rs, rows, bins, kernel="general").info["pileup_kernel"] == 0
 
 
-def test_lds_and_global_staging(gpu):
-    """Tiles staged as bin numerators -- in the HBM row-major stage (default), or in LDS when the
-    library is built with RCP_ROWS_LDS=1 and two 16-row slots fit (C3's 600 columns) -- and a wide
-    plan (4100 columns of per-base flanks, never in LDS): the same bits as the general kernel,
-    NULL rows and interpolated short genes included."""
+def test_row_major_staging(gpu):
+    """Tiles staged as bin numerators in the HBM row-major stage -- C3's 600 columns and a wide
+    plan (4100 columns of per-base flanks): the same bits as the general kernel, NULL rows and
+    interpolated short genes included."""
     from recoup_amd.engine import Bins
     rng = np.random.default_rng(67)
     reads = make_reads(rng, 150_000, widths=(50, 600))

@@ -256,18 +256,52 @@ RCP_API int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, const 
 
 /* Several GPUs in one call: the reference parallelises the per-region
  * work over host cores with cmclapply (R/util.R:364-382, used by R/coverage.R:147-154 and
- * R/profile.R:84-96); here the rows are cut into n_devices contiguous blocks (balanced by a
- * per-row weight: output + genomic width) and one host thread per GPU builds the plan for its
- * block, executes it and copies its rows of every column straight into the caller's R
- * column-major n_rows x n_cols matrix -- no collective, no host reassembly.
- * rcp_readset_create_multi makes one readset of the same reads on each listed device (in
- * parallel, one thread per device); readsets[i] lives on its own device and may be reused
- * across calls, as R keeps input$ranges.  row_split (may be NULL) receives the n_devices + 1
- * block boundaries.  The result is bit-identical to rcp_profile on one device. */
+ * R/profile.R:84-96); here the rows are cut into n_devices contiguous blocks and one host thread
+ * per GPU builds the plan for its block, executes it and copies its rows of every column straight
+ * into the caller's R column-major n_rows x n_cols matrix -- no collective, no host reassembly.
+ *
+ * Two ways to hold the reads:
+ *  - rcp_shards_create (below): the reads split for ONE row table -- each GPU holds only the reads
+ *    its block's regions can overlap.  What recoup()'s own path uses (r/R/rcp.R).
+ *  - rcp_readset_create_multi: REPLICAS -- one readset of all the reads on each listed device (in
+ *    parallel, one thread per device), reusable with any row table (rcp_profile_multi), as R keeps
+ *    input$ranges.  n_devices x the upload and the device memory of one readset.
+ * rcp_profile_multi balances its blocks by each row's candidate reads (counted on readsets[0]'s
+ * GPU) plus its length / 8, in the caller's row order; row_split (may be NULL) receives the
+ * n_devices + 1 block boundaries.  The result is bit-identical to rcp_profile on one device. */
 RCP_API int rcp_readset_create_multi(const rcp_reads_desc* desc, const int32_t* device_ids, int32_t n_devices,
                                      rcp_readset** out);
 RCP_API int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices, const rcp_rows_desc* rows,
                               const rcp_bins_desc* bins, double* out, uint8_t* row_valid, int32_t* row_split);
+
+/* One sample's reads split over several GPUs for ONE row table (what cmclapply over the regions
+ * of calcCoverage, R/coverage.R:147-154, and over the rows of binCoverageMatrix, R/profile.R:198-199,
+ * parallelise).  The rows are cut into n_devices contiguous blocks (the caller's order) of
+ * near-equal weight -- each row's candidate reads, counted on the GPUs, plus its length / 8 -- and
+ * device i keeps ONLY the reads block i's rows can overlap:
+ *   the reads are uploaded in n_devices slices, one per GPU (all PCIe links at once; device input:
+ *   one slice on its device); each GPU sorts its slice and counts every row range's candidates;
+ *   each GPU gathers, for every block, its slice's reads inside the block's candidate ranges and
+ *   copies them device to device (xGMI, hipMemcpyPeer) to the block's GPU, which builds the
+ *   block's readset (the layout rows->ignore_strand searches).
+ * A read that several blocks' regions overlap goes to each of them.  The row table is copied;
+ * bins come per call.  device_ids may repeat a device.  Every result is bit-identical to the
+ * same call on one device (a region sees exactly the reads findOverlaps hits). */
+typedef struct rcp_shards rcp_shards;
+typedef struct rcp_cov rcp_cov;  /* (calcCoverage results: see rcp_coverage_rle) */
+RCP_API int rcp_shards_create(const rcp_reads_desc* reads, const rcp_rows_desc* rows, const int32_t* device_ids,
+                              int32_t n_devices, rcp_shards** out);
+/* n_rows, n_devices; row_split [n_devices + 1]: the row blocks; n_reads [n_devices]: the reads each
+ * device holds (any may be NULL) */
+RCP_API int rcp_shards_info(const rcp_shards* sh, int32_t* n_rows, int32_t* n_devices, int32_t* row_split,
+                            int64_t* n_reads);
+/* profileMatrix of the row table (as rcp_profile: out = host R column-major n_rows x n_cols,
+ * row_valid may be NULL): one plan per device, each writing its rows of the caller's matrix */
+RCP_API int rcp_shards_profile(rcp_shards* sh, const rcp_bins_desc* bins, double* out, uint8_t* row_valid);
+/* calcCoverage of the row table as run-length encoded lists (as rcp_coverage_rle): one handle
+ * over the devices' blocks; rcp_cov_info / rcp_cov_copy / rcp_cov_free as for one device */
+RCP_API int rcp_shards_coverage(rcp_shards* sh, rcp_cov** out);
+RCP_API int rcp_shards_destroy(rcp_shards* sh);
 
 /* Several samples over one region table -- profileMatrix's loop over the samples of a recoup
  * input list (R/profile.R:13-98, `for (n in names(input))`) -- in one call: one plan per sample
@@ -303,6 +337,12 @@ typedef struct {
 } rcp_rle_desc;
 RCP_API int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out,
                             uint8_t* row_valid);
+/* rcp_profile_rle over several GPUs: the rows cut into n_devices contiguous blocks balanced by
+ * their runs (+ a constant per row: the output), each block's runs uploaded to its GPU and its
+ * rows of every column copied into `out` (binCoverageMatrix's per-row cmclapply,
+ * R/profile.R:198-199).  Bit-identical to rcp_profile_rle. */
+RCP_API int rcp_profile_rle_multi(const rcp_rle_desc* cov, const rcp_bins_desc* bins, const int32_t* device_ids,
+                                  int32_t n_devices, double* out, uint8_t* row_valid);
 
 /* calcCoverage: per-row integer depth vectors (CSR).  out_off is the host prefix sum of
  * rcp_plan_row_lengths(); d_cov (device int32 [out_off[n_rows]]) receives each valid row's

@@ -9,9 +9,12 @@
 # load() of a recoup object works as before.
 #
 # Devices: options(recoup.devices = c(0L, 1L, ...)) lists the GPUs (default 0).  With several
-# GPUs the fused profile path splits the regions over them (one host thread per GPU inside
-# the library), as cmclapply (R/util.R:364-382) splits them over cores.  The shim is not
-# fork-safe: these functions run in the R main process, never inside cmclapply workers.
+# GPUs every step splits the regions over them, as cmclapply (R/util.R:364-382) splits them over
+# cores (R/coverage.R:147-154, R/profile.R:198-199): a sample's reads are uploaded in one slice per
+# GPU and redistributed so that each GPU holds only the reads its block of regions can overlap
+# (rcp_shards), its coverage and profile computed there (one host thread per GPU inside the
+# library); a stored $coverage list is profiled with its rows split the same way.  The shim is
+# not fork-safe: these functions run in the R main process, never inside cmclapply workers.
 
 .rcpDevices <- function() as.integer(getOption("recoup.devices", 0L))
 
@@ -69,11 +72,21 @@
 # A sample's reads on the GPU: an "rcpReadSet" (the library's readset as an external pointer,
 # freed by .rcpFree or by the garbage collector, plus the seqlevels its chromosome codes index).
 # Built once per sample by coverageBaseRef / coverageAreaRef / coverageRnaRef below, so one
-# sample's reads cross PCIe once per recoup() call whatever the number of masks.
-.rcpReadSet <- function(input, strand = NULL, devices = .rcpDevices(), levels = NULL) {
+# sample's reads cross PCIe once per recoup() call whatever the number of masks.  rowsOf: a
+# function of the seqlevels giving the one row table the readset serves; with several devices
+# the reads are then split over them for those rows (rcp_R_shards, `rows` kept in the object),
+# else (no rowsOf) every device gets all of them (rcp_R_readsets, replicas).
+.rcpReadSet <- function(input, strand = NULL, devices = .rcpDevices(), levels = NULL, rowsOf = NULL) {
     ra <- .rcpReadArgs(input, levels)
     sf <- if (is.null(strand)) -1L else .rcpStrandCode(strand)
     args <- c(ra$args, list(sf))
+    if (length(devices) > 1 && !is.null(rowsOf)) {
+        rows <- rowsOf(ra$levels)
+        ptr <- do.call(.Call, c(list("rcp_R_shards"), args, .rcpRowArgs(rows), list(devices),
+            list(PACKAGE = "recoup")))
+        return(structure(list(ptr = ptr, levels = ra$levels, strand = strand, rows = rows),
+            class = "rcpReadSet"))
+    }
     ptr <- if (length(devices) > 1)
         do.call(.Call, c(list("rcp_R_readsets"), args, list(devices), list(PACKAGE = "recoup"))) else
         do.call(.Call, c(list("rcp_R_readset"), args, list(devices[1]), list(PACKAGE = "recoup")))
@@ -84,20 +97,25 @@
 
 # release the device arrays now instead of at the next garbage collection
 .rcpFree <- function(rs) {
-    if (.rcpIsReadSet(rs))
-        for (p in if (is.list(rs$ptr)) rs$ptr else list(rs$ptr))
+    if (.rcpIsReadSet(rs)) {
+        if (!is.null(rs$rows))
+            .Call("rcp_R_shards_free", rs$ptr, PACKAGE = "recoup")
+        else for (p in if (is.list(rs$ptr)) rs$ptr else list(rs$ptr))
             .Call("rcp_R_free", p, PACKAGE = "recoup")
+    }
     invisible(NULL)
 }
 
 # what calcCoverage reads for a sample of a recoup input list (R/coverage.R:32-39,53-62,94-97):
 # its reads (strand filter, findOverlaps' ignore.strand), or its BAM file -- whose branch skips
-# the strand filter (:141) and never reads ignore.strand (coverageFromBam, :228-295)
-.rcpSampleReadSet <- function(x, strandedParams) {
+# the strand filter (:141) and never reads ignore.strand (coverageFromBam, :228-295).
+# rowsOf(levels, ignore.strand): the sample's row table (several devices: the reads split for it)
+.rcpSampleReadSet <- function(x, strandedParams, rowsOf = NULL) {
+    ign <- if (!is.null(x$ranges)) strandedParams$ignoreStrand else TRUE
+    ro <- if (is.null(rowsOf)) NULL else function(lv) rowsOf(lv, ign)
     if (!is.null(x$ranges))
-        return(list(rs = .rcpReadSet(x$ranges, strandedParams$strand),
-            ignore.strand = strandedParams$ignoreStrand))
-    list(rs = .rcpReadSet(.rcpReadBam(x$file), NULL), ignore.strand = TRUE)
+        return(list(rs = .rcpReadSet(x$ranges, strandedParams$strand, rowsOf = ro), ignore.strand = ign))
+    list(rs = .rcpReadSet(.rcpReadBam(x$file), NULL, rowsOf = ro), ignore.strand = TRUE)
 }
 
 # One row per mask element: a GRanges element is one segment; a GRangesList element (the exon
@@ -124,10 +142,12 @@
 
 # rcp_R_coverage over a readset and a row table -> calcCoverage's named list of Rle
 # (R/coverage.R:171-173; NULL where findOverlaps finds no read, the chromosome is absent or a
-# subscript fails), run-length encoded on the GPU and rebuilt here without expanding it
+# subscript fails), run-length encoded on the GPU and rebuilt here without expanding it.  A
+# readset split over several devices serves its own row table (rs$rows), every device at once
 .rcpCoverage <- function(rs, rows, names) {
-    ptr <- if (is.list(rs$ptr)) rs$ptr[[1]] else rs$ptr
-    res <- do.call(.Call, c(list("rcp_R_coverage", ptr), .rcpRowArgs(rows), list(PACKAGE = "recoup")))
+    res <- if (!is.null(rs$rows)) .Call("rcp_R_shards_coverage", rs$ptr, PACKAGE = "recoup") else
+        do.call(.Call, c(list("rcp_R_coverage", if (is.list(rs$ptr)) rs$ptr[[1]] else rs$ptr),
+            .rcpRowArgs(rows), list(PACKAGE = "recoup")))
     cov <- lapply(seq_along(res$valid), function(r) {
         if (!res$valid[r])
             return(NULL)
@@ -160,8 +180,9 @@ calcCoverage <- function(input, mask, strand = NULL, ignore.strand = TRUE, rc = 
         # coverageFromBam (R/coverage.R:228-295): every mapped alignment overlapping the region
         # ("keep" spans); calcCoverage skips the strand filter for a BAM (:141) and
         # coverageFromBam never reads ignore.strand
-        rs <- .rcpReadSet(.rcpReadBam(input), NULL, .rcpDevices()[1])
         ignore.strand <- TRUE
+        rs <- .rcpReadSet(.rcpReadBam(input), NULL,
+            rowsOf = function(lv) .rcpRows(mask, lv, ignore.strand))
     } else {
         # a GRanges, or a list of them; the reference's strand filter (:141-144) is the
         # readset's.  On a list the reference's input[strand(input) == strand] has no strand()
@@ -169,11 +190,11 @@ calcCoverage <- function(input, mask, strand = NULL, ignore.strand = TRUE, rc = 
         # so one here too
         if (!is.null(strand) && !is.list(strand) && !is(input, "GRanges"))
             .rcpStrandOfListError()
-        rs <- .rcpReadSet(input, strand, .rcpDevices()[1])
+        rs <- .rcpReadSet(input, strand, rowsOf = function(lv) .rcpRows(mask, lv, ignore.strand))
     }
     if (own)
         on.exit(.rcpFree(rs))
-    .rcpCoverage(rs, .rcpRows(mask, rs$levels, ignore.strand), names(mask))
+    .rcpCoverage(rs, if (is.null(rs$rows)) .rcpRows(mask, rs$levels, ignore.strand) else rs$rows, names(mask))
 }
 
 # calcCoverage's strand filter applied to a plain list (splitBySeqname's result): strand() has
@@ -195,9 +216,10 @@ calcCoverage <- function(input, mask, strand = NULL, ignore.strand = TRUE, rc = 
         if (split && !is.null(input[[n]]$ranges) && !is.null(strandedParams$strand)
             && !is.list(strandedParams$strand))
             .rcpStrandOfListError()
-        s <- .rcpSampleReadSet(input[[n]], strandedParams)
-        input[[n]]$coverage <- .rcpCoverage(s$rs, .rcpRows(mainRanges, s$rs$levels, s$ignore.strand),
-            names(mainRanges))
+        s <- .rcpSampleReadSet(input[[n]], strandedParams,
+            function(lv, ign) .rcpRows(mainRanges, lv, ign))
+        rows <- if (is.null(s$rs$rows)) .rcpRows(mainRanges, s$rs$levels, s$ignore.strand) else s$rs$rows
+        input[[n]]$coverage <- .rcpCoverage(s$rs, rows, names(mainRanges))
         .rcpFree(s$rs)
     }
     return(input)
@@ -257,8 +279,9 @@ coverageRnaRef <- function(input, genomeRanges, helperRanges, flank,
         if (!is.null(input[[n]]$ranges) && !is.null(strandedParams$strand)
             && !is.list(strandedParams$strand))
             .rcpStrandOfListError()
-        s <- .rcpSampleReadSet(input[[n]], strandedParams)
-        rows <- .rcpRnaRows(leftRanges, genomeRanges, rightRanges, s$rs$levels, s$ignore.strand)
+        rowsOf <- function(lv, ign) .rcpRnaRows(leftRanges, genomeRanges, rightRanges, lv, ign)
+        s <- .rcpSampleReadSet(input[[n]], strandedParams, rowsOf)
+        rows <- if (is.null(s$rs$rows)) rowsOf(s$rs$levels, s$ignore.strand) else s$rs$rows
         input[[n]]$coverage <- .rcpCoverage(s$rs, rows, names(genomeRanges))
         .rcpFree(s$rs)
     }
@@ -280,7 +303,8 @@ coverageRnaRef <- function(input, genomeRanges, helperRanges, flank,
         lengths = as.integer(unlist(rl, use.names = FALSE)), isNull = isNull)
 }
 
-# parts: where codes 0 whole, 1 center, 2 upstream, 3 downstream; nBins 0 = per base.
+# parts: where codes 0 whole, 1 center, 2 upstream, 3 downstream; nBins 0 = per base.  Several
+# devices: the rows split over them (binCoverageMatrix's cmclapply over rows, R/profile.R:198-199).
 # rowNames: the rownames the reference's matrix carries (NULL: none).  The shim sets the
 # matrix's dimnames as the reference's rbind / cbind leave them (r/src/recoup_amd_shim.c,
 # set_dimnames): rownames = rowNames, colnames "<bin>.<stat>" for binned parts, "" for per-base
@@ -291,7 +315,7 @@ coverageRnaRef <- function(input, genomeRanges, helperRanges, flank,
     res <- .Call("rcp_R_profile_rle", a$runOff, a$values, a$lengths, a$isNull,
         as.integer(where), as.integer(if (is.null(flank)) c(0, 0) else flank),
         as.integer(nBins), as.integer(perBase), .rcpStat(stat), .rcpInterp(interpolation),
-        .rcpRngKind(), 1.0, .rcpDevices()[1], rowNames, PACKAGE = "recoup")
+        .rcpRngKind(), 1.0, .rcpDevices(), rowNames, PACKAGE = "recoup")
     res$profile
 }
 
@@ -379,7 +403,8 @@ profileMatrix <- function(input, flank, binParams, rc = NULL) {
 # profileMatrix straight from the reads, for a caller that does not keep $coverage: the mask's
 # rows over every sample's reads.  One GPU: all samples in ONE library call, passes kept two
 # deep on separate HIP streams (one sample's locate and pileup tail overlap another's pileup);
-# several GPUs (options(recoup.devices)): each sample's rows split over them.
+# several GPUs (options(recoup.devices)): each sample's rows split over them, each GPU holding
+# only the reads of its rows (rcp_R_shards).
 profileMatrixFromReads <- function(input, mask, flank, binParams, ignore.strand = TRUE) {
     len <- width(mask)
     equal <- all(len == len[1])
@@ -397,8 +422,8 @@ profileMatrixFromReads <- function(input, mask, flank, binParams, ignore.strand 
     rows <- .rcpRows(mask, lv, ignore.strand)
     if (length(devs) > 1) {
         for (i in todo) {
-            rs <- .rcpReadSet(input[[i]]$ranges, NULL, devs, lv)
-            res <- do.call(.Call, c(list("rcp_R_profile_multi", rs$ptr), .rcpRowArgs(rows), binArgs,
+            rs <- .rcpReadSet(input[[i]]$ranges, NULL, devs, lv, rowsOf = function(l) rows)
+            res <- do.call(.Call, c(list("rcp_R_shards_profile", rs$ptr), binArgs,
                 list(names(mask), PACKAGE = "recoup")))
             .rcpFree(rs)
             input[[i]]$profile <- res$profile

@@ -4,15 +4,17 @@
  *
  *   R function (reference file:line)                      .Call entry point here
  *   splitBySeqname + strand filter (R/util.R:1-13,           rcp_R_readset / rcp_R_readsets
- *       R/coverage.R:141-144)
- *   calcCoverage / coverageFromRanges (R/coverage.R:126-226) rcp_R_coverage -> list of Rle pieces
+ *       R/coverage.R:141-144)                                    (replicas) / rcp_R_shards (several
+ *                                                                GPUs, the reads split for one mask)
+ *   calcCoverage / coverageFromRanges (R/coverage.R:126-226) rcp_R_coverage / rcp_R_shards_coverage
+ *                                                                -> list of Rle pieces
  *   binCoverageMatrix / baseCoverageMatrix / splitVector     rcp_R_profile_rle (the stored $coverage,
  *       (R/profile.R:100-212, R/util.R:15-85)                    a list of Rle, as R keeps it)
  *   profileMatrix straight from the reads (fused, one call   rcp_R_profile / rcp_R_profile_multi /
- *       per sample, or all samples at once; R/profile.R:1-98)   rcp_R_profile_samples
+ *       per sample, or all samples at once; R/profile.R:1-98)   rcp_R_profile_samples / rcp_R_shards_profile
  *   readBam (R/ranges.R:111-146)                             rcp_R_read_bam
  *   preprocessRanges downsample / sampleto (R/ranges.R:32-62) rcp_R_sample_sorted
- *   (release a readset's device arrays now)                  rcp_R_free
+ *   (release a readset's / shard set's device arrays now)    rcp_R_free / rcp_R_shards_free
  *
  * Errors: every library call returns an RCP_E* code and is checked only AFTER it returned, so
  * Rf_error never longjmps through the library's C++ frames.  Memory R hands in is read in
@@ -36,6 +38,14 @@ static void readset_finalizer(SEXP p) {
     rcp_readset* rs = (rcp_readset*)R_ExternalPtrAddr(p);
     if (rs) {
         rcp_readset_destroy(rs);
+        R_ClearExternalPtr(p);
+    }
+}
+
+static void shards_finalizer(SEXP p) {
+    rcp_shards* sh = (rcp_shards*)R_ExternalPtrAddr(p);
+    if (sh) {
+        rcp_shards_destroy(sh);
         R_ClearExternalPtr(p);
     }
 }
@@ -191,6 +201,30 @@ static rcp_rows_desc rows_of(SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP
     rd.group_is_list = il;
     rd.ignore_strand = asLogical(ignoreStrand);
     return rd;
+}
+
+/* .Call("rcp_R_shards", <reads: 6 args as rcp_R_readset>, <rows: 8 args>, devices) -> the reads
+ * split over several GPUs for ONE row table (rcp_shards_create): each GPU keeps only the reads
+ * its block of the rows can overlap -- what cmclapply over the regions parallelises
+ * (R/coverage.R:147-154, R/profile.R:198-199) */
+SEXP rcp_R_shards(SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP seqlen, SEXP sfilter, SEXP segOff,
+                  SEXP rchrom, SEXP rstart, SEXP rend, SEXP rstrand, SEXP group, SEXP isList, SEXP ignoreStrand,
+                  SEXP devs) {
+    rcp_reads_desc d = reads_of(chrom, start, end, strand, seqlen, sfilter);
+    rcp_rows_desc rd = rows_of(segOff, rchrom, rstart, rend, rstrand, group, isList, ignoreStrand);
+    SEXP p = PROTECT(new_guard(shards_finalizer));
+    rcp_shards* sh = NULL;
+    int rc = rcp_shards_create(&d, &rd, INTEGER(devs), LENGTH(devs), &sh);
+    R_SetExternalPtrAddr(p, sh);
+    check(rc);
+    UNPROTECT(1);
+    return p;
+}
+
+/* .Call("rcp_R_shards_free", shards) releases a shard set's device arrays now */
+SEXP rcp_R_shards_free(SEXP p) {
+    shards_finalizer(p);
+    return R_NilValue;
 }
 
 /* bins: where (RCP_WHERE_* per part), flank (2 ints), nBins (per part, 0 = per base),
@@ -349,8 +383,31 @@ SEXP rcp_R_profile_multi(SEXP rsl, SEXP segOff, SEXP chrom, SEXP start, SEXP end
     return res;
 }
 
+/* .Call("rcp_R_shards_profile", shards, <bins: 8 args>, rowNames) -> list(profile, valid): the
+ * shard set's row table profiled on every GPU at once, each writing its rows of the matrix */
+SEXP rcp_R_shards_profile(SEXP shp, SEXP where, SEXP flank, SEXP nBins, SEXP pbw, SEXP stat, SEXP interp, SEXP rng,
+                          SEXP scale, SEXP rowNames) {
+    rcp_shards* sh = (rcp_shards*)R_ExternalPtrAddr(shp);
+    int ncol = 0;
+    rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
+    int32_t nrow = 0;
+    check(rcp_shards_info(sh, &nrow, NULL, NULL, NULL));
+    SEXP out = PROTECT(allocMatrix(REALSXP, nrow, ncol));
+    uint8_t* valid = (uint8_t*)R_alloc(nrow ? nrow : 1, 1);
+    int rc = rcp_shards_profile(sh, &bd, REAL(out), valid);
+    if (rc != RCP_OK) {
+        UNPROTECT(1);
+        check(rc);
+    }
+    set_dimnames(out, rowNames, &bd, nrow, ncol);
+    SEXP res = profile_result(out, valid, nrow);
+    UNPROTECT(1);
+    return res;
+}
+
 /* .Call("rcp_R_profile_rle", runOff (numeric, n_rows + 1), values (integer or double),
- *       lengths (integer), isNull (logical), <bins: 8 args>, device, rowNames)
+ *       lengths (integer), isNull (logical), <bins: 8 args>, devices, rowNames): devices of
+ *       length > 1 split the rows over several GPUs (rcp_profile_rle_multi)
  * binCoverageMatrix / baseCoverageMatrix of the stored coverage list (list of Rle flattened
  * by .rcpRleArrays); -> list(profile, valid) */
 SEXP rcp_R_profile_rle(SEXP runOff, SEXP values, SEXP lengths, SEXP isNull, SEXP where, SEXP flank, SEXP nBins,
@@ -372,7 +429,8 @@ SEXP rcp_R_profile_rle(SEXP runOff, SEXP values, SEXP lengths, SEXP isNull, SEXP
     rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
     SEXP out = PROTECT(allocMatrix(REALSXP, nrow, ncol));
     uint8_t* valid = (uint8_t*)R_alloc(nrow ? nrow : 1, 1);
-    int rc = rcp_profile_rle(&cd, &bd, asInteger(dev), REAL(out), valid);
+    int rc = LENGTH(dev) > 1 ? rcp_profile_rle_multi(&cd, &bd, INTEGER(dev), LENGTH(dev), REAL(out), valid)
+                             : rcp_profile_rle(&cd, &bd, asInteger(dev), REAL(out), valid);
     if (rc != RCP_OK) {
         UNPROTECT(1);
         check(rc);
@@ -388,14 +446,8 @@ SEXP rcp_R_profile_rle(SEXP runOff, SEXP values, SEXP lengths, SEXP isNull, SEXP
  * -> list(runOff = numeric n_rows + 1, values = integer, lengths = integer, valid = logical):
  * the pieces of calcCoverage's named list of Rle (R/coverage.R:171-173), from which the R side
  * builds S4Vectors::Rle(values, lengths) per valid row without expanding it */
-SEXP rcp_R_coverage(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
-                    SEXP isList, SEXP ignoreStrand) {
-    rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
-    SEXP guard = PROTECT(new_guard(cov_finalizer));
-    rcp_cov* cov = NULL;
-    int rc = rcp_coverage_rle((const rcp_readset*)R_ExternalPtrAddr(rsp), &rd, &cov);
-    R_SetExternalPtrAddr(guard, cov);
-    check(rc);
+/* The Rle pieces of a coverage handle held by `guard` (released here once copied) */
+static SEXP coverage_result(SEXP guard, rcp_cov* cov) {
     int32_t nrow = 0;
     int64_t nruns = 0;
     check(rcp_cov_info(cov, &nrow, &nruns));
@@ -405,7 +457,7 @@ SEXP rcp_R_coverage(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEX
     SEXP ok = PROTECT(allocVector(LGLSXP, nrow));
     int64_t* o64 = (int64_t*)R_alloc(nrow + 1, sizeof(int64_t));
     uint8_t* v8 = (uint8_t*)R_alloc(nrow > 0 ? nrow : 1, 1);
-    rc = rcp_cov_copy(cov, o64, INTEGER(val), INTEGER(len), v8);
+    int rc = rcp_cov_copy(cov, o64, INTEGER(val), INTEGER(len), v8);
     cov_finalizer(guard); /* the runs are in R's vectors now */
     check(rc);
     for (int r = 0; r <= nrow; ++r) REAL(off)[r] = (double)o64[r];
@@ -421,7 +473,33 @@ SEXP rcp_R_coverage(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEX
     SET_STRING_ELT(nm, 2, mkChar("lengths"));
     SET_STRING_ELT(nm, 3, mkChar("valid"));
     setAttrib(res, R_NamesSymbol, nm);
-    UNPROTECT(7);
+    UNPROTECT(6);
+    return res;
+}
+
+SEXP rcp_R_coverage(SEXP rsp, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
+                    SEXP isList, SEXP ignoreStrand) {
+    rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
+    SEXP guard = PROTECT(new_guard(cov_finalizer));
+    rcp_cov* cov = NULL;
+    int rc = rcp_coverage_rle((const rcp_readset*)R_ExternalPtrAddr(rsp), &rd, &cov);
+    R_SetExternalPtrAddr(guard, cov);
+    check(rc);
+    SEXP res = coverage_result(guard, cov);
+    UNPROTECT(1);
+    return res;
+}
+
+/* .Call("rcp_R_shards_coverage", shards) -> as rcp_R_coverage, for the shard set's row table:
+ * every GPU's block of rows at once (calcCoverage's cmclapply over regions, R/coverage.R:147-154) */
+SEXP rcp_R_shards_coverage(SEXP shp) {
+    SEXP guard = PROTECT(new_guard(cov_finalizer));
+    rcp_cov* cov = NULL;
+    int rc = rcp_shards_coverage((rcp_shards*)R_ExternalPtrAddr(shp), &cov);
+    R_SetExternalPtrAddr(guard, cov);
+    check(rc);
+    SEXP res = coverage_result(guard, cov);
+    UNPROTECT(1);
     return res;
 }
 
@@ -502,6 +580,10 @@ static const R_CallMethodDef call_methods[] = {
     {"rcp_R_read_bam", (DL_FUNC)&rcp_R_read_bam, 4},
     {"rcp_R_sample_sorted", (DL_FUNC)&rcp_R_sample_sorted, 4},
     {"rcp_R_free", (DL_FUNC)&rcp_R_free, 1},
+    {"rcp_R_shards", (DL_FUNC)&rcp_R_shards, 15},
+    {"rcp_R_shards_profile", (DL_FUNC)&rcp_R_shards_profile, 10},
+    {"rcp_R_shards_coverage", (DL_FUNC)&rcp_R_shards_coverage, 1},
+    {"rcp_R_shards_free", (DL_FUNC)&rcp_R_shards_free, 1},
     {NULL, NULL, 0}};
 
 void R_init_recoup(DllInfo* dll) {

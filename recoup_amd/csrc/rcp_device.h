@@ -152,6 +152,8 @@ struct RcpPlanDev {
     int32_t lean;               // 1: every row is one plain range with uniform power-of-two bins
                                 //    of one wave chunk -> rcp_pileup_lean_kernel
     int32_t lean_rounds;        // lean kernel: rounds of 16 rows per work item (2; else kRounds)
+    int32_t fold;               // 1: the pileup kernel searches its rows' read ranges itself and applies
+                                //    the NULL rules (no locate / heavy launches; bin-difference plans)
     // lean kernel, heaviest items first (per-base plans of few work items, e.g. one GPU's shard):
     // locate sums each (32-row tile, column chunk) item's candidate reads, files the item code in
     // item_order under its class floor(log2(reads)) (counts in status[kLptClass + class]), and

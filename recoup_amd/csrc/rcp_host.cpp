@@ -192,9 +192,11 @@ namespace {
 // 8-bit pass instead of five: the start order inside each stream is already there).
 // Builds one layout of the reads into *L (a fresh ReadLayout: PoolArr allocates once) and
 // returns the number of reads it kept in *kept.  Reads rs's seqlengths only.
+// directory = false: the search index only (streams, pmax), no bucket directory -- a readset a
+// shard build only searches once (rcp_shards_create).
 int build_layout(const rcp_readset* rs, const rcp_reads_desc* d, const int32_t* pc, const int32_t* ps,
                  const int32_t* pe, const int8_t* pst, int merge, ReadLayout* L, hipStream_t s, bool* presorted,
-                 int64_t* kept_out) {
+                 int64_t* kept_out, bool directory = true) {
     const int64_t n = d->n;
     const int64_t n_streams = (int64_t)d->n_chrom * 3;  // + 1 sentinel stream (dropped reads)
 #if RCP_PLAN_TIMING
@@ -288,6 +290,12 @@ int build_layout(const rcp_readset* rs, const rcp_reads_desc* d, const int32_t* 
     LAYOUT_MARK("  frees");
     L->h_stream_off.resize(n_streams + 2);
     HIP_TRY(hipMemcpyAsync(L->h_stream_off.data(), L->stream_off.p, 8 * (n_streams + 2), hipMemcpyDeviceToHost, s));
+    if (!directory) {
+        HIP_TRY(hipStreamSynchronize(s));
+        *kept_out = L->h_stream_off[n_streams];
+        L->h_stream_off.resize(n_streams + 1);
+        return RCP_OK;
+    }
     // ---- bucket directory: ~32 reads of a stream per bucket on average
     PoolBuf maxend(s);
     HIP_TRY(maxend.alloc(4 * std::max<int64_t>(n_streams, 1)));
@@ -346,6 +354,7 @@ int ensure_stranded(const rcp_readset* crs) {
     rcp_readset* rs = const_cast<rcp_readset*>(crs);
     std::lock_guard<std::mutex> lock(rs->mu);
     if (rs->stranded_ready) return RCP_OK;
+    if (!rs->kc && !rs->ks) return fail(RCP_EINVAL, "this readset holds no strand-split layout (a shard built for ignore.strand = TRUE)");
     DeviceGuard g(rs->device);
     HIP_TRY(g.err);
     bool presorted = rs->presorted;
@@ -370,9 +379,11 @@ int ensure_stranded(const rcp_readset* crs) {
 
 }  // namespace
 
-extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp_readset** out) {
-    RCP_TRY
+namespace rcpi {
+
+int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_readset** out) {
     if (!d || !out) return fail(RCP_EINVAL, "NULL argument");
+    if (!(layouts & (kLayMerged | kLayStranded))) return fail(RCP_EINVAL, "internal: no layout requested");
     *out = nullptr;
     int rc = check_device(d->device);
     if (rc) return rc;
@@ -407,7 +418,6 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     if (d->strand_filter < -1 || d->strand_filter > 2) return fail(RCP_EINVAL, "strand_filter = %d", d->strand_filter);
     DeviceGuard g(d->device);
     HIP_TRY(g.err);
-    hipStream_t s = static_cast<hipStream_t>(hip_stream);
     auto rs = std::make_unique<rcp_readset>();
     rs->device = d->device;
     rs->n_chrom = d->n_chrom;
@@ -473,19 +483,27 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     PLAN_MARK("reads H2D");
     bool presorted = false;
     int64_t kept = 0;
-    rc = build_layout(rs.get(), d, pc, ps, pe, pst, 1, &rs->merged, s, &presorted, &kept);
-    if (rc) return rc;
-    rs->n = kept;
-    PLAN_MARK("merged layout");
+    const bool dir = !(layouts & kLayIndexOnly);
+    if (layouts & kLayMerged) {
+        rc = build_layout(rs.get(), d, pc, ps, pe, pst, 1, &rs->merged, s, &presorted, &kept, dir);
+        if (rc) return rc;
+        rs->n = kept;
+        rs->has_merged = true;
+        PLAN_MARK("merged layout");
+    }
     rs->presorted = presorted;
     rs->desc = *d;
-    if (d->on_device) {
-        // the caller's device arrays are not ours to keep: the stranded layout now
-        rc = build_layout(rs.get(), d, pc, ps, pe, pst, 0, &rs->stranded, s, &presorted, &kept);
+    if (layouts & kLayStranded) {
+        int64_t kept2 = 0;
+        rc = build_layout(rs.get(), d, pc, ps, pe, pst, 0, &rs->stranded, s, &presorted, &kept2, dir);
         if (rc) return rc;
+        if ((layouts & kLayMerged) && kept2 != kept)
+            return fail(RCP_EINVAL, "internal: stranded layout kept %lld reads, merged %lld", (long long)kept2,
+                        (long long)kept);
+        rs->n = kept2;
         rs->stranded_ready = true;
         PLAN_MARK("stranded layout");
-    } else {
+    } else if (!d->on_device && (layouts & kLayKeep)) {
         // keep the uploaded copies for a later stranded layout (ensure_stranded)
         rs->keep_chrom = std::move(in_chrom);
         rs->keep_start = std::move(in_start);
@@ -501,6 +519,17 @@ extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp
     HIP_TRY(hipStreamSynchronize(s));
     *out = rs.release();
     return RCP_OK;
+}
+
+}  // namespace rcpi
+
+extern "C" int rcp_readset_create(const rcp_reads_desc* d, void* hip_stream, rcp_readset** out) {
+    RCP_TRY
+    if (!d) return fail(RCP_EINVAL, "NULL argument");
+    // device arrays are the caller's (not ours to keep): both layouts now; host arrays: the
+    // merged layout, the uploaded copies kept for the stranded one at its first use
+    const int layouts = d->on_device ? (kLayMerged | kLayStranded) : (kLayMerged | kLayKeep);
+    return readset_build(d, static_cast<hipStream_t>(hip_stream), layouts, out);
     RCP_CATCH
 }
 
@@ -743,6 +772,8 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     if (!rows->ignore_strand) {  // findOverlaps with strand compatibility: the stranded layout
         const int rc0 = ensure_stranded(rs);
         if (rc0) return rc0;
+    } else if (!rs->has_merged) {
+        return fail(RCP_EINVAL, "this readset holds no strand-merged layout (a shard built for ignore.strand = FALSE)");
     }
     auto plan = std::make_unique<rcp_plan>();
     plan->rs = rs;
@@ -1023,6 +1054,9 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
             P.part[0].n_chunks = 1;
             P.n_chunks_total = 1;
             P.stage_cap = P.part[0].n_bins;
+            // the kernel searches its rows' read ranges itself (the locate and heavy launches
+            // were as long as the pileup on C2) unless the caller asked for the heavy path
+            P.fold = opts->heavy_threshold <= 0 ? 1 : 0;
         }
     }
     // ---- lean plans with few row tiles (one GPU's shard of a region table): the persistent
@@ -1071,7 +1105,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.heavy_stride = ((eligible_len + 1) + 63) & ~63;
     P.heavy_slice = kHeavySlice;
     P.heavy_cap = (int32_t)std::min<int64_t>(std::max(R, 1), std::min<int64_t>(4096, (256ll << 20) / (4ll * P.heavy_stride)));
-    if (heavy_thr <= 0 || R == 0) P.heavy_threshold = 0;
+    if (heavy_thr <= 0 || R == 0 || P.fold) P.heavy_threshold = 0;
 
     // ---- upload tables (one arena)
     Arena blob;
@@ -1360,14 +1394,20 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     if (stages & RCP_STAGE_LOCATE) {
         // locate (also clears the previous execution's heavy slots and status words, and writes
-        // the caller's validity vector), heavy slices
+        // the caller's validity vector), heavy slices; a folded plan's pileup kernel does both
         begin_exec(plan);
-        RcpPlanDev Q = plan->dev;
-        Q.valid_out = d_valid;
-        HIP_TRY(rcp_launch_locate(&Q, s));
-        HIP_TRY(rcp_launch_heavy(&Q, kHeavyGrid, s));
+        if (!plan->dev.fold) {
+            RcpPlanDev Q = plan->dev;
+            Q.valid_out = d_valid;
+            HIP_TRY(rcp_launch_locate(&Q, s));
+            HIP_TRY(rcp_launch_heavy(&Q, kHeavyGrid, s));
+        }
     }
-    if (stages & RCP_STAGE_PILEUP) HIP_TRY(rcp_launch_pileup(&plan->dev, d_out, d_binsum, 0, s));
+    if (stages & RCP_STAGE_PILEUP) {
+        RcpPlanDev Q = plan->dev;
+        if (Q.fold) Q.valid_out = d_valid;
+        HIP_TRY(rcp_launch_pileup(&Q, d_out, d_binsum, 0, s));
+    }
     if (stages & RCP_STAGE_INTERP) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
     return RCP_OK;
     RCP_CATCH
@@ -1440,34 +1480,6 @@ extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, con
     RCP_CATCH
 }
 
-namespace {
-
-// Run fn(i) for i in [0, n) on one host thread each (one per GPU), collecting the first failure's
-// code and message into the calling thread's rcp_last_error().
-template <class F>
-int run_per_device(int n, F fn) {
-    std::vector<int> rc(n, RCP_OK);
-    std::vector<std::string> msg(n);
-    std::vector<std::thread> th;
-    th.reserve(n);
-    for (int i = 0; i < n; ++i)
-        th.emplace_back([&, i] {
-            try {
-                rc[i] = fn(i);
-            } catch (const std::bad_alloc&) {
-                rc[i] = fail(RCP_ENOMEM, "host memory exhausted (device thread %d)", i);
-            } catch (...) {
-                rc[i] = fail(RCP_EINVAL, "unexpected C++ exception (device thread %d)", i);
-            }
-            if (rc[i]) msg[i] = g_err;  // g_err is thread-local
-        });
-    for (auto& t : th) t.join();
-    for (int i = 0; i < n; ++i)
-        if (rc[i]) return fail(rc[i], "device %d: %s", i, msg[i].c_str());
-    return RCP_OK;
-}
-
-}  // namespace
 
 extern "C" int rcp_readset_create_multi(const rcp_reads_desc* desc, const int32_t* device_ids, int32_t n_devices,
                                         rcp_readset** out) {
@@ -1570,6 +1582,56 @@ extern "C" int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_sampl
     RCP_CATCH
 }
 
+namespace rcpi {
+
+int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bins_desc* bins, double* out,
+                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols) {
+    rcp_plan* plan = nullptr;
+    rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, 0, {0, 0}};
+    int e = rcp_plan_create_ex(rs, sub, bins, &opts, &plan);
+    if (e) return e;
+    std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
+    DeviceGuard g(rs->device);
+    HIP_TRY(g.err);
+    if (n_cols) *n_cols = plan->n_cols;
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(s, hipStreamDestroy);
+    const size_t cells = (size_t)plan->out_ld * (size_t)plan->n_cols;
+    DevBuf d_out, d_valid;
+    HIP_TRY(d_out.alloc(8 * std::max<size_t>(cells, 1)));
+    HIP_TRY(d_valid.alloc(std::max<int32_t>(plan->n_rows, 1)));
+    e = rcp_plan_execute(plan, d_out.as<double>(), d_valid.as<uint8_t>(), nullptr, s);
+    if (e) return e;
+    e = rcp_plan_status(plan, s);
+    if (e) return e;
+    // this block's rows of every column of the caller's R matrix
+    if (out && plan->n_cols && plan->n_rows)
+        HIP_TRY(rcp::stage_d2h_2d(out + r0, 8 * (size_t)n_rows_total, d_out.p, 8 * (size_t)plan->out_ld,
+                                  8 * (size_t)plan->n_rows, (size_t)plan->n_cols, rs->device, s));
+    if (row_valid && plan->n_rows) {
+        HIP_TRY(hipMemcpyAsync(row_valid + r0, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return RCP_OK;
+}
+
+// Contiguous row blocks [split[i], split[i + 1]) of near-equal total weight (cum: prefix sums
+// of the per-row weights, n_rows + 1 entries)
+std::vector<int32_t> balanced_split(const std::vector<double>& cum, int32_t n_blocks) {
+    const int32_t R = (int32_t)cum.size() - 1;
+    std::vector<int32_t> split(n_blocks + 1, 0);
+    split[n_blocks] = R;
+    for (int i = 1; i < n_blocks; ++i) {
+        const double target = cum[R] * i / n_blocks;
+        split[i] = (int32_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+        split[i] = std::min(std::max(split[i], split[i - 1]), R);
+    }
+    return split;
+}
+
+}  // namespace rcpi
+
 extern "C" int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices, const rcp_rows_desc* rows,
                                  const rcp_bins_desc* bins, double* out, uint8_t* row_valid, int32_t* row_split) {
     RCP_TRY
@@ -1579,22 +1641,27 @@ extern "C" int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices
         if (!readsets[i]) return fail(RCP_EINVAL, "readsets[%d] is NULL", i);
     const int32_t R = rows->n_rows;
     if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
-    if (R > 0 && !rows->seg_off) return fail(RCP_EINVAL, "NULL seg_off");
-    // contiguous row blocks balanced by a per-row weight: the row's output (the same for every
-    // row) plus its genomic width (the reads it can touch grow with it)
-    std::vector<double> cum(R + 1, 0.0);
-    for (int32_t r = 0; r < R; ++r) {
-        double w = 0;
-        for (int64_t j = rows->seg_off[r]; j < rows->seg_off[r + 1]; ++j)
-            w += std::max<double>(0.0, (double)rows->seg_end[j] - rows->seg_start[j] + 1);
-        cum[r + 1] = cum[r] + 2048.0 + w;
-    }
+    if (R > 0 && (!rows->seg_off || !rows->seg_chrom || !rows->seg_start || !rows->seg_end || !rows->seg_strand))
+        return fail(RCP_EINVAL, "NULL row array");
+    // contiguous row blocks balanced by each row's candidate reads, counted on the first device
+    // (the reads a row's pileup streams), plus its length / 8 and a constant (its output and
+    // per-row work): a count, not the genomic width, so hot peaks weigh what they cost
     std::vector<int32_t> split(n_devices + 1, 0);
     split[n_devices] = R;
-    for (int i = 1; i < n_devices; ++i) {
-        const double target = cum[R] * i / n_devices;
-        split[i] = (int32_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
-        split[i] = std::min(std::max(split[i], split[i - 1]), R);
+    if (n_devices > 1 && R > 0) {
+        std::vector<uint2> b;
+        const int e = seg_bounds(readsets[0], rows, &b);
+        if (e) return e;
+        std::vector<double> cum(R + 1, 0.0);
+        for (int32_t r = 0; r < R; ++r) {
+            double w = 16.0;
+            for (int64_t j = rows->seg_off[r]; j < rows->seg_off[r + 1]; ++j) {
+                for (int k = 0; k < 3; ++k) w += (double)(b[3 * j + k].y - b[3 * j + k].x);
+                w += std::max<double>(0.0, (double)rows->seg_end[j] - rows->seg_start[j] + 1) / 8.0;
+            }
+            cum[r + 1] = cum[r] + w;
+        }
+        split = balanced_split(cum, n_devices);
     }
     if (row_split) std::copy(split.begin(), split.end(), row_split);
     std::vector<int64_t> n_cols(n_devices, -1);
@@ -1604,35 +1671,7 @@ extern "C" int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices
         rcp_rows_desc sub = *rows;  // seg_off indexes the shared segment arrays directly
         sub.n_rows = r1 - r0;
         sub.seg_off = rows->seg_off + r0;
-        const rcp_readset* rs = readsets[i];
-        rcp_plan* plan = nullptr;
-        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, 0, {0, 0}};
-        int e = rcp_plan_create_ex(rs, &sub, bins, &opts, &plan);
-        if (e) return e;
-        std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
-        DeviceGuard g(rs->device);
-        HIP_TRY(g.err);
-        n_cols[i] = plan->n_cols;
-        hipStream_t s = nullptr;
-        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(s, hipStreamDestroy);
-        const size_t cells = (size_t)plan->out_ld * (size_t)plan->n_cols;
-        DevBuf d_out, d_valid;
-        HIP_TRY(d_out.alloc(8 * std::max<size_t>(cells, 1)));
-        HIP_TRY(d_valid.alloc(std::max<int32_t>(plan->n_rows, 1)));
-        e = rcp_plan_execute(plan, d_out.as<double>(), d_valid.as<uint8_t>(), nullptr, s);
-        if (e) return e;
-        e = rcp_plan_status(plan, s);
-        if (e) return e;
-        // this device's block of rows of every column of the caller's R matrix
-        if (out && plan->n_cols)
-            HIP_TRY(rcp::stage_d2h_2d(out + r0, 8 * (size_t)R, d_out.p, 8 * (size_t)plan->out_ld,
-                                      8 * (size_t)plan->n_rows, (size_t)plan->n_cols, rs->device, s));
-        if (row_valid) {
-            HIP_TRY(hipMemcpyAsync(row_valid + r0, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipStreamSynchronize(s));
-        }
-        return (int)RCP_OK;
+        return profile_block(readsets[i], &sub, bins, out, R, r0, row_valid, &n_cols[i]);
     });
     if (rc) return rc;
     int64_t nc = -1;
@@ -1664,6 +1703,7 @@ int calc_coverage_dev(rcp_plan* plan, const int64_t* d_off, int32_t* d_cov, uint
     P.crange = nullptr;  // sized for the plan's chunks, not these
     P.cw_len = -1;
     P.lean = 0;  // the general kernel's CSR mode (locate writes every side output)
+    P.fold = 0;
     P.csr_off = d_off;
     P.csr_out = d_cov;
     P.valid_out = d_valid;
@@ -1693,6 +1733,7 @@ int coverage_starts_dev(rcp_plan* plan, const int64_t* d_off, const int64_t* d_s
     P.crange = nullptr;
     P.cw_len = -1;
     P.lean = 0;
+    P.fold = 0;
     // four rounds of 16 rows per workgroup (C4 coverage pileup 632 -> 601 us vs two, 635 with
     // one; profiles/r04/r4x)
     {
@@ -1901,6 +1942,7 @@ extern "C" int rcp_cov_copy(const rcp_cov* c, int64_t* run_off, int32_t* values,
                             uint8_t* valid) {
     RCP_TRY
     if (!c) return fail(RCP_EINVAL, "NULL coverage");
+    if (!c->parts.empty()) return cov_copy_parts(c, run_off, values, lengths, valid);
     DeviceGuard g(c->device);
     HIP_TRY(g.err);
     // pinned double-buffered staging (rcp_stage.h) straight into the caller's arrays
@@ -1914,6 +1956,11 @@ extern "C" int rcp_cov_copy(const rcp_cov* c, int64_t* run_off, int32_t* values,
 
 extern "C" int rcp_cov_free(rcp_cov* c) {
     if (c) {
+        for (auto& p : c->parts) {  // each part's buffers go back to its own device's pool
+            if (!p) continue;
+            DeviceGuard g(p->device);
+            p.reset();
+        }
         DeviceGuard g(c->device);
         delete c;
     }
@@ -1938,9 +1985,8 @@ bool part_slice_spec(int where, int32_t f1, int32_t f2, RcpPart* pt) {
 
 }  // namespace
 
-extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out,
-                               uint8_t* row_valid) {
-    RCP_TRY
+int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out,
+                           int64_t out_ld, uint8_t* row_valid) {
     if (!cov || !bins) return fail(RCP_EINVAL, "NULL argument");
     const int32_t R = cov->n_rows;
     if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
@@ -2178,11 +2224,59 @@ extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bin
     P.scratch = d_scratch.as<double>();
     HIP_TRY(rcp_rle_profile_launch(&P, dbl ? 1 : 0, P.interp_lds ? lds : 0, s));
     if (out && R && col)
-        HIP_TRY(rcp::stage_d2h_2d(out, 8 * (size_t)R, d_out.p, 8 * (size_t)ld, 8 * (size_t)R, (size_t)col, device, s));
+        HIP_TRY(rcp::stage_d2h_2d(out, 8 * (size_t)out_ld, d_out.p, 8 * (size_t)ld, 8 * (size_t)R, (size_t)col, device, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (row_valid)
         for (int32_t r = 0; r < R; ++r) row_valid[r] = (cov->is_null && cov->is_null[r]) ? 0 : 1;
     return RCP_OK;
+}
+
+extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out,
+                               uint8_t* row_valid) {
+    RCP_TRY
+    if (!cov) return fail(RCP_EINVAL, "NULL argument");
+    return profile_rle_impl(cov, bins, device, out, cov->n_rows, row_valid);
+    RCP_CATCH
+}
+
+extern "C" int rcp_profile_rle_multi(const rcp_rle_desc* cov, const rcp_bins_desc* bins, const int32_t* device_ids,
+                                     int32_t n_devices, double* out, uint8_t* row_valid) {
+    RCP_TRY
+    if (!cov || !bins || !device_ids) return fail(RCP_EINVAL, "NULL argument");
+    if (n_devices < 1 || n_devices > 64) return fail(RCP_EINVAL, "n_devices = %d", n_devices);
+    for (int i = 0; i < n_devices; ++i) {
+        const int rc = check_device(device_ids[i]);
+        if (rc) return rc;
+    }
+    const int32_t R = cov->n_rows;
+    if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
+    if (R > 0 && !cov->run_off) return fail(RCP_EINVAL, "NULL run_off");
+    if (R > 0 && cov->run_off[0] != 0) return fail(RCP_EINVAL, "run_off[0] != 0");
+    for (int32_t r = 0; r < R; ++r)
+        if (cov->run_off[r + 1] < cov->run_off[r]) return fail(RCP_EINVAL, "run_off decreases at row %d", r);
+    if (n_devices == 1) return profile_rle_impl(cov, bins, device_ids[0], out, R, row_valid);
+    // contiguous row blocks balanced by the runs each row streams (12 bytes each up, read once)
+    // plus its output columns (the same for every row: a constant per row)
+    std::vector<double> cum((size_t)R + 1, 0.0);
+    for (int32_t r = 0; r < R; ++r) cum[r + 1] = cum[r] + 64.0 + (double)(cov->run_off[r + 1] - cov->run_off[r]);
+    const std::vector<int32_t> split = balanced_split(cum, n_devices);
+    return run_per_device(n_devices, [&](int i) {
+        const int32_t r0 = split[i], r1 = split[i + 1];
+        if (r1 <= r0) return (int)RCP_OK;
+        // the block as an Rle list of its own: run offsets from 0, arrays from its first run
+        const int64_t base = cov->run_off[r0];
+        std::vector<int64_t> off((size_t)(r1 - r0) + 1);
+        for (int32_t r = r0; r <= r1; ++r) off[r - r0] = cov->run_off[r] - base;
+        rcp_rle_desc sub = *cov;
+        sub.n_rows = r1 - r0;
+        sub.run_off = off.data();
+        sub.lengths = cov->lengths ? cov->lengths + base : nullptr;
+        sub.ivalues = cov->ivalues ? cov->ivalues + base : nullptr;
+        sub.dvalues = cov->dvalues ? cov->dvalues + base : nullptr;
+        sub.is_null = cov->is_null ? cov->is_null + r0 : nullptr;
+        return profile_rle_impl(&sub, bins, device_ids[i], out ? out + r0 : nullptr, R,
+                                row_valid ? row_valid + r0 : nullptr);
+    });
     RCP_CATCH
 }
 

@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdint>
 #include <exception>
@@ -11,6 +12,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/recoup_amd.h"
@@ -177,6 +179,58 @@ struct DeviceGuard {
 // RCP_OK, or RCP_ENODEVICE / RCP_EINVAL when `dev` is not a visible device
 int check_device(int dev);
 
+// Run fn(i) for i in [0, n) on one host thread each (one per GPU), collecting the first failure's
+// code and message into the calling thread's rcp_last_error().
+template <class F>
+int run_per_device(int n, F fn) {
+    std::vector<int> rc(n, RCP_OK);
+    std::vector<std::string> msg(n);
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (int i = 0; i < n; ++i)
+        th.emplace_back([&, i] {
+            try {
+                rc[i] = fn(i);
+            } catch (const std::bad_alloc&) {
+                rc[i] = fail(RCP_ENOMEM, "host memory exhausted (device thread %d)", i);
+            } catch (...) {
+                rc[i] = fail(RCP_EINVAL, "unexpected C++ exception (device thread %d)", i);
+            }
+            if (rc[i]) msg[i] = g_err;  // g_err is thread-local
+        });
+    for (auto& t : th) t.join();
+    for (int i = 0; i < n; ++i)
+        if (rc[i]) return fail(rc[i], "device %d: %s", i, msg[i].c_str());
+    return RCP_OK;
+}
+
+// Block [r0, r0 + sub->n_rows) of an n_rows_total-row profile on readset rs: plan, execute, and
+// copy its rows of every column into the caller's R column-major matrix `out` (may be NULL) and
+// row_valid + r0 (may be NULL); *n_cols receives the plan's column count (rcp_host.cpp)
+int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bins_desc* bins, double* out,
+                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols);
+
+// rcp_profile_rle into rows [0, n_rows) of a matrix with column stride out_ld (rcp_host.cpp)
+int profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out, int64_t out_ld,
+                     uint8_t* row_valid);
+
+// Contiguous row blocks of near-equal weight from the prefix sums of the row weights (rcp_host.cpp)
+std::vector<int32_t> balanced_split(const std::vector<double>& cum, int32_t n_blocks);
+
+// Candidate reads [lo, hi) of every (range, stream slot) of `rows` in the layout of rs the rows
+// search (merged for ignore_strand, else strand-split): host [3 * n_seg] (rcp_shard.cpp)
+int seg_bounds(const rcp_readset* rs, const rcp_rows_desc* rows, std::vector<uint2>* out);
+
+// rcp_cov_copy of a coverage made of per-device parts (rcp_shard.cpp)
+int cov_copy_parts(const rcp_cov* c, int64_t* run_off, int32_t* values, int32_t* lengths, uint8_t* valid);
+
+// A readset with the layouts asked for (rcp_host.cpp): kLayMerged (ignore.strand = TRUE),
+// kLayStranded (FALSE); kLayKeep: host input keeps its uploaded copies for a stranded layout
+// built at first use; kLayIndexOnly: streams and prefix max only, no bucket directory (a
+// readset searched once, never planned on)
+enum { kLayMerged = 1, kLayStranded = 2, kLayKeep = 4, kLayIndexOnly = 8 };
+int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_readset** out);
+
 }  // namespace rcpi
 
 // One sorted layout of the reads: streams (chromosome x strand) of start-sorted (start, end)
@@ -246,6 +300,7 @@ struct rcp_readset {
     rcpi::DevBuf d_seqlen;
     rcpi::ReadLayout stranded, merged;
     bool presorted = false;  // the reads came in (chromosome, start) order (no full radix sort)
+    bool has_merged = false; // the merged layout was built (every readset but a strand-split shard's)
     // The stranded layout serves only ignore.strand = FALSE (findOverlaps with strand
     // compatibility); the default TRUE reads the merged one.  Reads uploaded from the host keep
     // their device copies here and the stranded layout is built at its first use

@@ -2794,6 +2794,9 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     const int tile = (blockIdx.x & 7) * per_x + (blockIdx.x >> 3);
     if (tile >= nt) return;
     const int row0 = tile * kTile;
+    // a folded plan launches no heavy kernel: zero the status set the next execution uses here
+    // (nothing in this execution reads it)
+    if (P.fold && blockIdx.x == 0 && tid < RCP_STATUS_WORDS) P.status_prev[tid] = 0u;
     for (int q = lane; q < WW; q += 64) D[q] = 0;  // D and F
     auto rd_load = [&](uint32_t idx) -> RdT {
         if constexpr (UNI) return P.st[idx];
@@ -2808,23 +2811,93 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         int32_t flag, heavy, bs, k, gps, gpe, rev, head, L;
         uint32_t lo[3], hi[3];
     };
+    // P.fold: the locate kernel's work for row r done here -- the single range's candidate reads
+    // per strand stream (lanes 2s / 2s + 1: lower / upper bound of stream s, bucket directory +
+    // bisection as rcp_locate_kernel) and the NULL rules (no hit; the range past seqlength, or
+    // past the hits' last end when seqlength is NA: R/coverage.R:189-225); writes the row's
+    // validity and returns the record rcp_locate_kernel would have left
+    auto locate_row = [&](int r) -> RcpRowRec {
+        RcpRowInfo ri;
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(P.row_info + r);
+            uint4 w[sizeof(RcpRowInfo) / 16];
+#pragma unroll
+            for (int q = 0; q < (int)(sizeof(RcpRowInfo) / 16); ++q) w[q] = src[q];
+            int32_t v[sizeof(RcpRowInfo) / 4];
+            __builtin_memcpy(v, w, sizeof v);
+#pragma unroll
+            for (int q = 0; q < (int)(sizeof(RcpRowInfo) / 4); ++q) v[q] = __builtin_amdgcn_readfirstlane(v[q]);
+            __builtin_memcpy(&ri, v, sizeof ri);
+        }
+        RcpRowRec R{};
+        R.row_len = ri.row_len;
+        R.heavy = -1;
+        const RcpSeg sg = ri.seg0;
+        const bool ok = !ri.stat && ri.chrom >= 0 && ri.chrom < P.n_chrom && ri.j1 == ri.j0 + 1 && sg.query_ok;
+        bool valid = false;
+        if (ok) {  // wave-uniform
+            const int ns = P.merged ? 1 : 3;
+            uint32_t res = 0;
+            if (lane < 2 * ns && ((sg.streams >> (lane >> 1)) & 1)) {
+                const int st = lane >> 1;
+                int64_t d0[1] = {ri.d0};
+                int32_t nb[1] = {ri.nb};
+                if (!P.merged) {
+                    d0[0] = P.dir_off[ri.chrom * 3 + st];
+                    nb[0] = (int32_t)(P.dir_off[ri.chrom * 3 + st + 1] - d0[0]) - 1;
+                }
+                const int32_t v[1] = {(lane & 1) ? sg.hi : sg.lo};
+                const int dst[1] = {(lane & 1) ? -1 : -2};
+                uint32_t out1[1];
+                dir_bound_multi<1>(P, d0, nb, v, dst, 1, out1);
+                res = out1[0];
+            }
+            bool hit = false;
+            int32_t maxend = INT32_MIN;
+#pragma unroll
+            for (int st = 0; st < 3; ++st) {
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)res, 2 * st);
+                const uint32_t hi = max(lo, (uint32_t)__builtin_amdgcn_readlane((int)res, 2 * st + 1));
+                R.lo[st] = R.hi[st] = 0;
+                if (st < ns && ((sg.streams >> st) & 1) && lo < hi) {
+                    R.lo[st] = lo;
+                    R.hi[st] = hi;
+                    hit = true;
+                    if (ri.seqlen < 0) maxend = max(maxend, P.pmax[hi - 1]);  // only NA seqlengths need it
+                }
+            }
+            valid = hit && (ri.seqlen >= 0 ? (int64_t)sg.hi <= ri.seqlen : sg.hi <= maxend);
+        }
+        if (lane == 0) {
+            P.valid[r] = valid ? 1 : 0;
+            if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
+        }
+        R.flags = valid ? (RCP_REC_VALID | RCP_REC_FAST) : 0;
+        R.off = sg.off;
+        R.slo = sg.lo;
+        R.shi = sg.hi;
+        R.rev = sg.rev;
+        return R;
+    };
     auto row_of = [&](int r) -> Row {
         Row m{};
         m.flag = -1;
         if (r >= P.n_rows) return m;
-        RcpRowRec rec;
-        {
+        RcpRowRec R;
+        if (P.fold) {
+            R = locate_row(r);
+        } else {
+            RcpRowRec rec;
             const uint4* src = reinterpret_cast<const uint4*>(P.rec + r);
             uint4* dst = reinterpret_cast<uint4*>(&rec);
 #pragma unroll
             for (int q = 0; q < 4; ++q) dst[q] = src[q];
-        }
-        int32_t v[16];
-        __builtin_memcpy(v, &rec, sizeof v);
+            int32_t v[16];
+            __builtin_memcpy(v, &rec, sizeof v);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = __builtin_amdgcn_readfirstlane(v[q]);
-        RcpRowRec R;
-        __builtin_memcpy(&R, v, sizeof R);
+            for (int q = 0; q < 16; ++q) v[q] = __builtin_amdgcn_readfirstlane(v[q]);
+            __builtin_memcpy(&R, v, sizeof R);
+        }
         if (!(R.flags & RCP_REC_VALID)) {
             m.flag = 0;  // NULL row -> zeros (profile.R:191-197)
             return m;
@@ -2870,11 +2943,14 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         const uint32_t c0 = m.hi[0] - m.lo[0], c1 = m.hi[1] - m.lo[1];
         return q < c0 ? m.lo[0] + q : (q < c0 + c1 ? m.lo[1] + (q - c0) : m.lo[2] + (q - c0 - c1));
     };
+    // candidate slot u of a lane in a batch: 4 lane + u (ps_slot), so the 64 adds of one
+    // instruction are 4 reads apart: start-sorted reads of one lane group spread over 4x the bins,
+    // fewer same-address LDS atomics (a 180-bp read spans 9 bins of 20 bp)
     auto load_batch = [&](const Row& m, uint32_t nc, uint32_t q0, RdT (&dst)[4]) {
         if (m.flag == 1 && m.heavy < 0 && q0 < nc) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const uint32_t q = q0 + lane + 64 * u;
+                const uint32_t q = q0 + ps_slot(lane, u);
                 dst[u] = rd_load(cand_index(m, q < nc ? q : nc - 1));
             }
         }
@@ -2945,23 +3021,22 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     load_batch(m, nc, q0 + 256, nb);
 #pragma unroll
                     for (int u = 0; u < 4; ++u)
-                        if (q0 + lane + 64u * u < nc) add_read(m, rd_pair(c[u]), rb);
+                        if (q0 + ps_slot(lane, u) < nc) add_read(m, rd_pair(c[u]), rb);
 #pragma unroll
                     for (int u = 0; u < 4; ++u) c[u] = nb[u];
                 }
             }
             lds_order();
-            // numerators: D[k] + bs * prefix(F)[k]; lane t takes bins [t per, (t + 1) per)
-            const int per = (n + 63) >> 6;
-            const int k0 = lane * per;
-            int32_t fs = 0;
-            for (int q = 0; q < per; ++q) fs += k0 + q < n ? F[k0 + q] : 0;
-            int32_t run = (int32_t)wave_exclusive_scan((uint32_t)fs);
+            // numerators: D[k] + bs * prefix(F)[k], 64 bins per step (lane t: bin 64 j + t; one
+            // wave scan per step): consecutive lanes, consecutive words -- no bank conflicts
             uint32_t* srow = stage + i * RS;
-            for (int q = 0; q < per; ++q) {
-                const int k = k0 + q;
+            int32_t carry = 0;
+            for (int32_t k0 = 0; k0 < n; k0 += 64) {
+                const int k = k0 + lane;
+                const int32_t f = k < n ? F[k] : 0;
+                const int32_t run = carry + (int32_t)wave_inclusive_scan((uint32_t)f);
+                carry = __builtin_amdgcn_readlane(run, 63);
                 if (k < n) {
-                    run += F[k];
                     srow[k] = (uint32_t)(D[k] + m.bs * run);
                     D[k] = 0;
                     F[k] = 0;

@@ -1,10 +1,12 @@
 // rcp_stage.cpp -- pinned double-buffered staging of pageable host memory (rcp_stage.h).
 //
-// Per device: two 64 MB pinned buffers, one HIP event each, and a small pool of host threads
-// that memcpy between the caller's memory and the pinned buffer.  D2H: chunk k is DMA'd into
-// buffer k % 2 while the threads drain chunk k - 1; H2D: the threads fill chunk k while the DMA
-// engine uploads chunk k - 1.  A per-device mutex serialises users of one device's buffers;
-// devices proceed in parallel (rcp_profile_multi drives one host thread per GPU).
+// Per device and direction: two 64 MB pinned buffers, one HIP event each, and a small pool of
+// host threads that memcpy between the caller's memory and the pinned buffer.  D2H: chunk k is
+// DMA'd into buffer k % 2 while the threads drain chunk k - 1; H2D: the threads fill chunk k
+// while the DMA engine uploads chunk k - 1.  A mutex per (device, direction) serialises users of
+// one set of buffers; the two directions of a device proceed in parallel (PCIe is full duplex:
+// one sample's upload beside another's download, rcp_profile_samples_reads), and so do devices
+// (rcp_profile_multi drives one host thread per GPU).
 #include "rcp_stage.h"
 
 #include <algorithm>
@@ -101,9 +103,9 @@ struct Stager {
 
 // Process lifetime: the pinned buffers are returned to the OS at exit (freeing them from a
 // static destructor could run after the HIP runtime is gone).
-Stager* stager(int device) {
-    static Stager* s = new Stager[kMaxDevices];
-    return device >= 0 && device < kMaxDevices ? &s[device] : nullptr;
+Stager* stager(int device, int dir) {  // dir 0: host -> device, 1: device -> host
+    static Stager* s = new Stager[2 * kMaxDevices];
+    return device >= 0 && device < kMaxDevices ? &s[2 * device + dir] : nullptr;
 }
 
 bool ready(Stager* s) {  // under s->mu, on the device
@@ -133,7 +135,7 @@ inline void part_range(size_t n, int i, size_t* a, size_t* b) {
 
 hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipStream_t stream) {
     if (bytes == 0) return hipSuccess;
-    Stager* st = stager(device);
+    Stager* st = stager(device, 0);
     if (bytes < kDirect || !st) {
         hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream);
         return e == hipSuccess ? hipStreamSynchronize(stream) : e;
@@ -170,7 +172,7 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
     if (width == 0 || height == 0) return hipSuccess;
     // the device bytes moved: rows with their padding, except after the last row
     const size_t bytes = spitch * (height - 1) + width;
-    Stager* st = stager(device);
+    Stager* st = stager(device, 1);
     if (bytes < kDirect || !st) {
         hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost, stream);
         return e == hipSuccess ? hipStreamSynchronize(stream) : e;

@@ -391,6 +391,69 @@ def profile_multi(readsets, rows, bins):
     return out.T, valid.astype(bool), split
 
 
+class Shards:
+    """rcp_shards_create: one sample's host reads split over ``devices`` for ONE row table -- the
+    rows cut into one contiguous block per device (balanced by counted candidate reads), each
+    device holding only the reads its block's rows can overlap (uploaded in one slice per GPU,
+    redistributed device to device).  ``devices`` may repeat a device."""
+
+    def __init__(self, chrom, start, end, strand, seqlengths, rows, devices, strand_filter=None):
+        lib = _lib.lib()
+        if _lib.device_count() == 0:
+            raise _lib.RcpError(-6, "no GPU visible: recoup_amd runs only on the GPU")
+        self.seqlengths = np.ascontiguousarray(seqlengths, dtype=np.int64)
+        runs = _chrom_runs(chrom)
+        wruns = _chrom_runs(end)
+        keep = [None if runs else np.ascontiguousarray(chrom, dtype=np.int32),
+                np.ascontiguousarray(start, dtype=np.int32),
+                None if wruns else np.ascontiguousarray(end, dtype=np.int32),
+                np.ascontiguousarray(strand, dtype=np.int8)]
+        sf = -1 if strand_filter is None else STRAND.get(strand_filter, strand_filter)
+        d = _reads_desc(int(keep[1].shape[0]), keep, runs, self.seqlengths, 0, 0, int(sf), wruns)
+        self.devices = np.ascontiguousarray(devices, dtype=np.int32)
+        self.rows = rows
+        rd = rows.desc()
+        h = ctypes.c_void_p()
+        check(lib.rcp_shards_create(ctypes.byref(d), ctypes.byref(rd), cptr(self.devices, _lib._i32p),
+                                    len(self.devices), ctypes.byref(h)))
+        self.h = h
+
+    def info(self):
+        """(row block boundaries [n_devices + 1], reads held per device [n_devices])."""
+        n = len(self.devices)
+        split = np.zeros(n + 1, np.int32)
+        reads = np.zeros(n, np.int64)
+        check(_lib.lib().rcp_shards_info(self.h, None, None, cptr(split, _lib._i32p), cptr(reads, _lib._i64p)))
+        return split, reads
+
+    def profile(self, bins):
+        """rcp_shards_profile -> (matrix (n_rows, n_cols) float64 view of R's column-major
+        matrix, validity bool)."""
+        R = self.rows.n_rows
+        out = np.zeros((bins.n_cols, R), np.float64)
+        valid = np.zeros(max(R, 1), np.uint8)
+        bd = bins.desc()
+        check(_lib.lib().rcp_shards_profile(self.h, ctypes.byref(bd), cptr(out, _lib._dp), cptr(valid, _lib._u8p)))
+        return out.T, valid[:R].astype(bool)
+
+    def coverage_rle(self):
+        """rcp_shards_coverage + rcp_cov_copy: (run_off, values, lengths, valid) as coverage_rle_host."""
+        h = ctypes.c_void_p()
+        check(_lib.lib().rcp_shards_coverage(self.h, ctypes.byref(h)))
+        return _cov_copy(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib().rcp_shards_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def profile_samples(readsets, rows, bins, inflight=0):
     """rcp_profile_samples: one region table over several samples' readsets (one GPU), passes
     kept ``inflight`` deep on separate HIP streams (0 = the library's default, 2), each matrix
@@ -468,9 +531,14 @@ def profile_rle_arrays(run_off, lengths, values, nulls, bins, device=0, out=None
         raise ValueError("out must be an F-ordered float64 array of n_rows x n_cols")
     valid = np.zeros(max(R, 1), np.uint8)
     bd = bins.desc()
-    with torch.cuda.device(int(device)):
-        check(_lib.lib().rcp_profile_rle(ctypes.byref(d), ctypes.byref(bd), int(device), cptr(out, _lib._dp),
-                                         cptr(valid, _lib._u8p)))
+    if np.ndim(device) == 0:
+        with torch.cuda.device(int(device)):
+            check(_lib.lib().rcp_profile_rle(ctypes.byref(d), ctypes.byref(bd), int(device), cptr(out, _lib._dp),
+                                             cptr(valid, _lib._u8p)))
+    else:  # several GPUs: rcp_profile_rle_multi
+        devs = np.ascontiguousarray(device, dtype=np.int32)
+        check(_lib.lib().rcp_profile_rle_multi(ctypes.byref(d), ctypes.byref(bd), cptr(devs, _lib._i32p), len(devs),
+                                               cptr(out, _lib._dp), cptr(valid, _lib._u8p)))
     return out, valid[:R].astype(bool)
 
 
@@ -486,6 +554,16 @@ def coverage_rle_host(readset, rows, timing=None):
     with torch.cuda.device(readset.device):
         check(L.rcp_coverage_rle(readset.h, ctypes.byref(rd), ctypes.byref(h)))
     t1 = time.perf_counter()
+    res = _cov_copy(h)
+    if timing is not None:
+        timing["coverage_ms"] = round((t1 - t0) * 1e3, 2)
+        timing["copy_ms"] = round((time.perf_counter() - t1) * 1e3, 2)
+    return res
+
+
+def _cov_copy(h):
+    """rcp_cov_info + rcp_cov_copy + rcp_cov_free of a coverage handle."""
+    L = _lib.lib()
     try:
         nr, nruns = ctypes.c_int32(), ctypes.c_int64()
         check(L.rcp_cov_info(h, ctypes.byref(nr), ctypes.byref(nruns)))
@@ -497,7 +575,4 @@ def coverage_rle_host(readset, rows, timing=None):
                              cptr(valid, _lib._u8p)))
     finally:
         L.rcp_cov_free(h)
-    if timing is not None:
-        timing["coverage_ms"] = round((t1 - t0) * 1e3, 2)
-        timing["copy_ms"] = round((time.perf_counter() - t1) * 1e3, 2)
     return run_off, values[:nruns.value], lengths[:nruns.value], valid[:nr.value]

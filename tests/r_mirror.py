@@ -11,7 +11,7 @@ import numpy as np
 
 from recoup_amd.granges import GRanges, GRangesList, getFlankingRanges, getRegionalRanges
 
-MIRRORED = [".rcpReadArgs", ".rcpReadSet", ".rcpFree", ".rcpSampleReadSet", ".rcpRows", ".rcpRowArgs",
+MIRRORED = [".rcpDevices", ".rcpReadArgs", ".rcpReadSet", ".rcpFree", ".rcpSampleReadSet", ".rcpRows", ".rcpRowArgs",
             ".rcpCoverage", "calcCoverage", ".rcpCoverageRef", ".rcpRnaRows", "coverageRnaRef", ".rcpRleArrays",
             ".rcpProfileRle", ".rcpStrandOfListError", "binCoverageMatrix", "baseCoverageMatrix", ".rcpParts", "profileMatrix",
             "profileMatrixFromReads"]
@@ -103,20 +103,34 @@ def rcp_read_args(inp, levels=None):
     return lv, [chrom, st, ends, sd, seqlen]
 
 
-class ReadSet:
-    """The R "rcpReadSet": list(ptr, levels, strand)."""
+# options(recoup.devices): set by the tests (getOption's value)
+DEVICES = (0,)
 
-    def __init__(self, ptr, levels, strand):
-        self.ptr, self.levels, self.strand = ptr, levels, strand
+
+def rcp_devices():
+    """.rcpDevices()."""
+    return tuple(DEVICES)
+
+
+class ReadSet:
+    """The R "rcpReadSet": list(ptr, levels, strand[, rows])."""
+
+    def __init__(self, ptr, levels, strand, rows=None):
+        self.ptr, self.levels, self.strand, self.rows = ptr, levels, strand, rows
 
 
 STRAND = {"+": 0, "-": 1, "*": 2}
 
 
-def rcp_read_set(sh, inp, strand=None, devices=(0,), levels=None):
-    """.rcpReadSet(input, strand, devices, levels)."""
+def rcp_read_set(sh, inp, strand=None, devices=None, levels=None, rows_of=None):
+    """.rcpReadSet(input, strand, devices, levels, rowsOf)."""
+    devices = rcp_devices() if devices is None else tuple(devices)
     lv, args = rcp_read_args(inp, levels)
     sf = -1 if strand is None else STRAND[strand]
+    if len(devices) > 1 and rows_of is not None:
+        rows = rows_of(lv)
+        ptr = sh.call("rcp_R_shards", *args, np.int32(sf), *rcp_row_args(rows), np.asarray(devices, np.int32))
+        return ReadSet(ptr, lv, strand, rows)
     if len(devices) > 1:
         ptr = sh.call("rcp_R_readsets", *args, np.int32(sf), np.asarray(devices, np.int32), raw=False)
     else:
@@ -126,6 +140,9 @@ def rcp_read_set(sh, inp, strand=None, devices=(0,), levels=None):
 
 def rcp_free(sh, rs):
     """.rcpFree(rs)."""
+    if rs.rows is not None:
+        sh.call("rcp_R_shards_free", rs.ptr)
+        return
     for p in (rs.ptr if isinstance(rs.ptr, list) else [rs.ptr]):
         sh.call("rcp_R_free", p)
 
@@ -152,8 +169,11 @@ def rcp_row_args(rows):
 
 def rcp_coverage(sh, rs, rows, names=None):
     """.rcpCoverage(rs, rows, names): named list of (values, lengths) runs or None."""
-    ptr = rs.ptr[0] if isinstance(rs.ptr, list) else rs.ptr
-    res = sh.call("rcp_R_coverage", ptr, *rcp_row_args(rows))
+    if rs.rows is not None:
+        res = sh.call("rcp_R_shards_coverage", rs.ptr)
+    else:
+        ptr = rs.ptr[0] if isinstance(rs.ptr, list) else rs.ptr
+        res = sh.call("rcp_R_coverage", ptr, *rcp_row_args(rows))
     cov = []
     for r in range(len(res["valid"])):
         if not res["valid"][r]:
@@ -177,9 +197,10 @@ def calc_coverage(sh, inp, mask, strand=None, ignore_strand=True):
     """calcCoverage(input, mask, strand, ignore.strand) for a GRanges or a split list."""
     if strand is not None and not isinstance(inp, GRanges):
         rcp_strand_of_list_error()
-    rs = rcp_read_set(sh, inp, strand)
+    rs = rcp_read_set(sh, inp, strand, rows_of=lambda lv: rcp_rows(mask, lv, ignore_strand))
     try:
-        return rcp_coverage(sh, rs, rcp_rows(mask, rs.levels, ignore_strand), mask.names)
+        return rcp_coverage(sh, rs, rs.rows if rs.rows is not None else rcp_rows(mask, rs.levels, ignore_strand),
+                            mask.names)
     finally:
         rcp_free(sh, rs)
 
@@ -190,9 +211,10 @@ def coverage_ref(sh, input, genomeRanges, region, flank, strandedParams, split=F
     for x in input:
         if split and x.get("ranges") is not None and strandedParams.get("strand") is not None:
             rcp_strand_of_list_error()
-        rs = rcp_read_set(sh, x["ranges"], strandedParams.get("strand"))
-        x["coverage"] = rcp_coverage(sh, rs, rcp_rows(main, rs.levels, strandedParams.get("ignoreStrand", True)),
-                                     main.names)
+        ign = strandedParams.get("ignoreStrand", True)  # .rcpSampleReadSet
+        rs = rcp_read_set(sh, x["ranges"], strandedParams.get("strand"), rows_of=lambda lv: rcp_rows(main, lv, ign))
+        rows = rs.rows if rs.rows is not None else rcp_rows(main, rs.levels, ign)
+        x["coverage"] = rcp_coverage(sh, rs, rows, main.names)
         rcp_free(sh, rs)
     return input
 
@@ -232,8 +254,12 @@ def coverage_rna_ref(sh, input, genomeRanges, helperRanges, flank, strandedParam
     for x in input:
         if x.get("ranges") is not None and sp.get("strand") is not None:
             rcp_strand_of_list_error()
-        rs = rcp_read_set(sh, x["ranges"], sp.get("strand"))
-        rows = rcp_rna_rows(left, genomeRanges, right, rs.levels, sp.get("ignoreStrand", True))
+        ign = sp.get("ignoreStrand", True)
+
+        def rows_of(lv):
+            return rcp_rna_rows(left, genomeRanges, right, lv, ign)
+        rs = rcp_read_set(sh, x["ranges"], sp.get("strand"), rows_of=rows_of)
+        rows = rs.rows if rs.rows is not None else rows_of(rs.levels)
         x["coverage"] = rcp_coverage(sh, rs, rows, genomeRanges.names)
         rcp_free(sh, rs)
     return input
@@ -255,14 +281,15 @@ INTERP = {"auto": 0, "spline": 1, "linear": 2, "neighborhood": 3}
 
 
 def rcp_profile_rle(sh, cvrg, where, flank, n_bins, per_base, stat="mean", interpolation="auto", rng_kind=0,
-                    device=0, row_names=None):
+                    row_names=None):
     """.rcpProfileRle(cvrg, where, flank, nBins, perBase, stat, interpolation, rowNames): the
     matrix (an rmini RArray carrying the dimnames the shim set)."""
     a = rcp_rle_arrays(cvrg)
     res = sh.call("rcp_R_profile_rle", a["runOff"], a["values"], a["lengths"], a["isNull"],
                   np.asarray(where, np.int32), np.asarray((0, 0) if flank is None else flank, np.int32),
                   np.asarray(n_bins, np.int32), np.asarray(per_base, np.int32), np.int32(STAT[stat]),
-                  np.int32(INTERP[interpolation]), np.int32(rng_kind), 1.0, np.int32(device), _rchar(row_names))
+                  np.int32(INTERP[interpolation]), np.int32(rng_kind), 1.0, np.asarray(rcp_devices(), np.int32),
+                  _rchar(row_names))
     return res["profile"]
 
 
@@ -413,7 +440,7 @@ def ref_forced_heatmap(sh, input, region, flank, binParams, customIsBase=False):
         bin_coverage_matrix(sh, x["coverage"], fbs[0], stat, interp, flank, "upstream")
         raise NameError("object 'forcedBinSize' not found")
     return out
-def profile_matrix_from_reads(sh, input, mask, flank, binParams, ignore_strand=True, devices=(0,)):
+def profile_matrix_from_reads(sh, input, mask, flank, binParams, ignore_strand=True):
     """profileMatrixFromReads(input, mask, flank, binParams, ignore.strand)."""
     ln = mask.width
     equal = bool(np.all(ln == ln[0]))
@@ -426,10 +453,11 @@ def profile_matrix_from_reads(sh, input, mask, flank, binParams, ignore_strand=T
     todo = [i for i, x in enumerate(input) if x.get("profile") is None]
     lv = list(dict.fromkeys(l for i in todo for l in input[i]["ranges"].seqlevels))
     rows = rcp_rows(mask, lv, ignore_strand)
+    devices = rcp_devices()
     if len(devices) > 1:
         for i in todo:
-            rs = rcp_read_set(sh, input[i]["ranges"], None, devices, lv)
-            res = sh.call("rcp_R_profile_multi", rs.ptr, *rcp_row_args(rows), *bin_args, names)
+            rs = rcp_read_set(sh, input[i]["ranges"], None, devices, lv, rows_of=lambda _lv: rows)
+            res = sh.call("rcp_R_shards_profile", rs.ptr, *bin_args, names)
             rcp_free(sh, rs)
             input[i]["profile"] = res["profile"]
         return input

@@ -201,18 +201,75 @@ def test_rna_recoup_path(sh, c1):
         _assert_same_matrix(x["profile"], ref[k]["profile"], "rna: rcp.R profileMatrix vs R/profile.R's")
 
 
+class _devices:
+    """options(recoup.devices = devs) for the duration of a block."""
+
+    def __init__(self, devs):
+        self.devs = tuple(devs)
+
+    def __enter__(self):
+        self.prev, rm.DEVICES = rm.DEVICES, self.devs
+
+    def __exit__(self, *exc):
+        rm.DEVICES = self.prev
+
+
 def test_profile_from_reads(sh, c1):
     """profileMatrixFromReads: every sample in one rcp_R_profile_samples call, and the rows
-    split over two device slots (rcp_R_readsets + rcp_R_profile_multi) bit-equal to it."""
+    split over two device slots (rcp_R_shards + rcp_R_shards_profile) bit-equal to it."""
     from recoup_amd.granges import getRegionalRanges
     mask = getRegionalRanges(c1["genes"], "tss", (2000, 2000))
     bp = dict(flankBinSize=0, regionBinSize=200)
     one = rm.profile_matrix_from_reads(sh, _inputs(c1), mask, (2000, 2000), bp)
-    two = rm.profile_matrix_from_reads(sh, _inputs(c1), mask, (2000, 2000), bp, devices=(0, 0))
+    with _devices((0, 0)):
+        two = rm.profile_matrix_from_reads(sh, _inputs(c1), mask, (2000, 2000), bp)
     for k in range(2):
         np.testing.assert_allclose(one[k]["profile"], c1["gold"][f"tss_heat_s{k}"], rtol=MEAN_RTOL, atol=0)
         _assert_dimnames(one[k]["profile"], o.profile_dimnames(list(mask.names), (2000, 2000), bp, True), "reads")
         _assert_same_matrix(two[k]["profile"], one[k]["profile"], "two device slots vs one")
+    assert sh.live_handles() == 0
+
+
+def _same_coverage(a, b):
+    assert a.names == b.names and len(a) == len(b)
+    for x, y in zip(a, b):
+        assert (x is None) == (y is None)
+        if x is not None:
+            np.testing.assert_array_equal(x[0], y[0])
+            np.testing.assert_array_equal(x[1], y[1])
+
+
+@pytest.mark.parametrize("devs", [(0, 0), (0, 0, 0)])
+def test_recoup_path_on_several_devices(sh, c1, devs):
+    """recoup()'s own path with options(recoup.devices = devs): coverageRef (TSS, genebody) and
+    coverageRnaRef -> $coverage -> profileMatrix, every step split over the devices (the reads of
+    each sample split for its row table, rcp_R_shards; the stored coverage list's rows split,
+    rcp_profile_rle_multi) -- bit-equal, coverage and profiles with their dimnames, to one device."""
+    genes, exons = c1["genes"], c1["exons"]
+    sp = {"strand": None, "ignoreStrand": True}
+    runs = [("tss", dict(flankBinSize=0, regionBinSize=0)),
+            ("genebody", dict(flankBinSize=50, regionBinSize=150, sumStat="mean", interpolation="auto")),
+            ("rna", dict(flankBinSize=50, regionBinSize=150, interpolation="auto"))]
+    for region, bp in runs:
+        def path():
+            if region == "rna":
+                inp = rm.coverage_rna_ref(sh, _inputs(c1), exons, genes, (2000, 2000))
+            else:
+                inp = rm.coverage_ref(sh, _inputs(c1), genes, region, (2000, 2000), sp)
+            return rm.profile_matrix(sh, inp, (2000, 2000), bp)
+        one = path()
+        with _devices(devs):
+            many = path()
+        for a, b in zip(many, one):
+            _same_coverage(a["coverage"], b["coverage"])
+            _assert_same_matrix(a["profile"], b["profile"], f"{region}: {len(devs)} devices vs one")
+    # calcCoverage straight from a GRanges and from splitBySeqname's list
+    from recoup_amd.granges import getRegionalRanges
+    mask = getRegionalRanges(genes, "tss", (2000, 2000))
+    for inp in (c1["reads"][0], rm.split_by_seqname(c1["reads"][1])):
+        one = rm.calc_coverage(sh, inp, mask)
+        with _devices(devs):
+            _same_coverage(rm.calc_coverage(sh, inp, mask), one)
     assert sh.live_handles() == 0
 
 

@@ -367,6 +367,10 @@ def main():
     if args.config == "c3":  # + 4 R (B + 1): the per-row bin tables of non-uniform (R-RNG) layouts
         bytes_pileup += 4 * R * (B + 1)
     achieved = bytes_pileup / (kt[1] * 1e-3) / 1e9
+    # the same with the bytes the kernel actually streams per read: 4 for reads of one width whose
+    # starts alone the kernel loads (C2, C5; C4's binned lean kernel loads the pairs)
+    rb = int(plan.info.get("read_bytes", 8))
+    bytes_streamed = bytes_pileup - (8 - rb) * ovl
     kernel = PILEUP_KERNELS[plan.info["pileup_kernel"]]
     traffic = load_traffic(args.traffic or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json"), args,
                            kernel, R, n_reads, world)
@@ -421,6 +425,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                          "kernel": kernel,
                          "algorithmic_bytes_per_launch": bytes_pileup,
+                         "read_bytes": rb,
+                         "frac_streamed_bytes": bytes_streamed / (kt[1] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                         "streamed_bytes_note": "frac with the bytes per read the kernel loads (read_bytes) instead of "
+                                                "SURVEY 8(d)'s 8: the start-only stream of reads of one width",
                          "kernel_ms": kt[1],
                          "step_frac": bytes_pileup / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if world == 1 else None},
             "cpu_baseline": cpu,
@@ -518,15 +526,61 @@ def end_to_end(reads, seqlen, rows, bins, local, units, reps=3, rle=True):
         res[name] = {"ms": med[0], "region_bins_per_s": units / (med[0] * 1e-3),
                      "phases_ms": {"readset_create": med[1], "profile_one_shot": med[2]},
                      "first_call_ms": calls[0][0], "calls_ms": [round(c[0], 2) for c in calls]}
-    e2e = dict(res["sorted_runs"])
+    e2e = one_call(forms["sorted_runs"], seqlen, rows, bins, local, units, out, reps)
+    e2e["two_calls"] = res["sorted_runs"]
     e2e["any_order"] = res["any_order"]
+    e2e["samples_pipelined"] = samples_pipelined(forms["sorted_runs"], seqlen, rows, bins, local, units, out, reps)
     if rle:
         e2e["rle_path"] = rle_path(forms["sorted_runs"], seqlen, rows, bins, local, units, out, reps)
     e2e["width_runs"] = n_wruns
-    e2e["note"] = ("C ABI: rcp_readset_create from host arrays + rcp_profile into a host matrix; PCIe both ways; "
-                   "reads coordinate-sorted with seqnames runs (a sorted BAM) and width runs when few "
-                   "(width_runs: their count; null = per-read ends); any_order: unsorted, one code and one end per read")
+    e2e["note"] = ("host reads -> host matrix through the C ABI, PCIe both ways. ms: one rcp_profile_reads call "
+                   "(profileMatrixFromReads), reads coordinate-sorted with seqnames runs (a sorted BAM) and width "
+                   "runs when few (width_runs: their count; null = per-read ends), streamed in row blocks; "
+                   "two_calls: rcp_readset_create then rcp_profile (phases_ms); any_order: the two calls on "
+                   "unsorted reads, one code and one end per read")
     return e2e
+
+
+def one_call(host, seqlen, rows, bins, local, units, fused, reps):
+    """The headline e2e: profileMatrix straight from one sample's host reads in one C ABI call,
+    as r/R/rcp.R's profileMatrixFromReads makes it (rcp_profile_reads): coordinate-sorted reads
+    stream through the GPU in row blocks -- block b's slice of the reads goes up while block b - 1's
+    rows of the matrix come down.  `fused`: the matrix of the two-call sequence (readset_create +
+    rcp_profile), which this must equal bit for bit."""
+    from recoup_amd.engine import profile_reads
+    out = np.zeros((bins.n_cols, rows.n_rows))
+    calls = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = profile_reads([host], seqlen, rows, bins, local, [out])
+        calls.append((time.perf_counter() - t0) * 1e3)
+    med = sorted(calls)[len(calls) // 2]
+    return {"ms": med, "region_bins_per_s": units / (med * 1e-3), "first_call_ms": calls[0],
+            "calls_ms": [round(c, 2) for c in calls],
+            "equal_two_calls": bool(np.array_equal(res[0][0].T.view(np.int64), fused.view(np.int64)))}
+
+
+def samples_pipelined(host, seqlen, rows, bins, local, units, fused, reps, n_samples=3):
+    """profileMatrix straight from the reads of an input list of samples (r/R/rcp.R
+    profileMatrixFromReads -> rcp_profile_reads): sample k + 1's reads go up while sample k's
+    matrix comes down (both PCIe directions; the sequential e2e above uses one at a time).  The
+    samples reuse one sample's host arrays (the timing does not depend on their values); `ms` is
+    per sample, the median of `reps` calls of n_samples samples each."""
+    from recoup_amd.engine import profile_reads
+    outs = [np.zeros((bins.n_cols, rows.n_rows)) for _ in range(n_samples)]
+    calls = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = profile_reads([host] * n_samples, seqlen, rows, bins, local, outs)
+        calls.append((time.perf_counter() - t0) * 1e3 / n_samples)
+    med = sorted(calls)[len(calls) // 2]
+    return {"ms": med, "region_bins_per_s": units / (med * 1e-3), "samples": n_samples,
+            "calls_ms_per_sample": [round(c, 2) for c in calls],
+            "equal_one_shot": bool(all(np.array_equal(m.T.view(np.int64), fused.view(np.int64)) for m, _ in res)),
+            "note": "rcp_profile_reads: readset upload + build of sample k+1 beside the pass and matrix download "
+                    "of sample k (both PCIe directions); per-sample time"}
 
 
 def rle_path(host, seqlen, rows, bins, local, units, fused, reps):

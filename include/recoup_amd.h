@@ -167,7 +167,8 @@ typedef struct {
     int32_t chunk_positions;
     int32_t pileup_kernel;   /* 0: general pileup kernel; 1: lean kernel (pile + store waves);
                               * 2: lean kernel, general bins; 3: row-wave kernel; 4: bin-difference kernel */
-    int32_t reserved;
+    int32_t read_bytes;      /* bytes per candidate read the pileup kernel streams: 4 (the starts alone,
+                              * reads of one width) or 8 ((start, end) pairs) */
     int64_t out_ld;          /* column stride of d_out / d_binsum (rcp_plan_opts.out_ld resolved):
                               * both must hold out_ld * (n_cols - 1) + n_rows elements */
 } rcp_plan_info;
@@ -314,6 +315,16 @@ RCP_API int rcp_shards_destroy(rcp_shards* sh);
 RCP_API int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_samples, const rcp_rows_desc* rows,
                                 const rcp_bins_desc* bins, int32_t inflight, double* const* outs,
                                 uint8_t* const* row_valid);
+
+/* profileMatrix straight from the reads of several samples over one region table, reads on the
+ * host (R's vectors): samples[k] describes sample k's reads (all for one device, host arrays),
+ * outs[k] its R column-major n_rows x n_cols matrix (row_valid may be NULL or hold per-sample
+ * pointers).  Sample k + 1's readset is uploaded and built while sample k's pass runs and its
+ * matrix is copied down -- both PCIe directions at once (the one-shot rcp_readset_create +
+ * rcp_profile of each sample in turn uses one direction at a time); at most two samples' reads
+ * are on the device.  Bit-identical to rcp_profile per sample. */
+RCP_API int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_samples, const rcp_rows_desc* rows,
+                              const rcp_bins_desc* bins, double* const* outs, uint8_t* const* row_valid);
 
 /* Profiles of a coverage list the caller holds as run-length encoded vectors -- the reference's
  * own `$coverage` object, a named list of S4Vectors::Rle (R/coverage.R:171-173) -- as

@@ -401,8 +401,8 @@ profileMatrix <- function(input, flank, binParams, rc = NULL) {
 }
 
 # profileMatrix straight from the reads, for a caller that does not keep $coverage: the mask's
-# rows over every sample's reads.  One GPU: all samples in ONE library call, passes kept two
-# deep on separate HIP streams (one sample's locate and pileup tail overlap another's pileup);
+# rows over every sample's reads.  One GPU: all samples in ONE library call (rcp_R_profile_reads),
+# one sample's upload beside the previous sample's pass and matrix download;
 # several GPUs (options(recoup.devices)): each sample's rows split over them, each GPU holding
 # only the reads of its rows (rcp_R_shards).
 profileMatrixFromReads <- function(input, mask, flank, binParams, ignore.strand = TRUE) {
@@ -430,10 +430,11 @@ profileMatrixFromReads <- function(input, mask, flank, binParams, ignore.strand 
         }
         return(input)
     }
-    rsl <- lapply(input[todo], function(x) .rcpReadSet(x$ranges, NULL, devs[1], lv))
-    on.exit(lapply(rsl, .rcpFree))
-    res <- do.call(.Call, c(list("rcp_R_profile_samples", lapply(rsl, `[[`, "ptr")), .rcpRowArgs(rows),
-        binArgs, list(2L, names(mask), PACKAGE = "recoup")))
+    # one GPU: every sample's reads handed over in one call, sample k + 1 uploaded while sample
+    # k's matrix comes down (both PCIe directions at once)
+    readArgs <- lapply(input[todo], function(x) c(.rcpReadArgs(x$ranges, lv)$args, list(-1L)))
+    res <- do.call(.Call, c(list("rcp_R_profile_reads", readArgs, devs[1]), .rcpRowArgs(rows),
+        binArgs, list(names(mask), PACKAGE = "recoup")))
     for (k in seq_along(todo))
         input[[todo[k]]]$profile <- res[[k]]$profile
     return(input)

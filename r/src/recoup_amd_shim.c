@@ -11,7 +11,8 @@
  *   binCoverageMatrix / baseCoverageMatrix / splitVector     rcp_R_profile_rle (the stored $coverage,
  *       (R/profile.R:100-212, R/util.R:15-85)                    a list of Rle, as R keeps it)
  *   profileMatrix straight from the reads (fused, one call   rcp_R_profile / rcp_R_profile_multi /
- *       per sample, or all samples at once; R/profile.R:1-98)   rcp_R_profile_samples / rcp_R_shards_profile
+ *       per sample, or all samples at once; R/profile.R:1-98)   rcp_R_profile_samples / rcp_R_shards_profile /
+ *                                                                rcp_R_profile_reads (reads on the host)
  *   readBam (R/ranges.R:111-146)                             rcp_R_read_bam
  *   preprocessRanges downsample / sampleto (R/ranges.R:32-62) rcp_R_sample_sorted
  *   (release a readset's / shard set's device arrays now)    rcp_R_free / rcp_R_shards_free
@@ -359,6 +360,44 @@ SEXP rcp_R_profile_samples(SEXP rsl, SEXP segOff, SEXP chrom, SEXP start, SEXP e
     return res;
 }
 
+/* .Call("rcp_R_profile_reads", list of samples' read args (each list(<reads: 6 args as
+ * rcp_R_readset>)), device, <rows: 8 args>, <bins: 8 args>, rowNames) -> list (per sample) of
+ * list(profile, valid): profileMatrix straight from the reads of an input list on one GPU, sample
+ * k + 1's reads uploaded while sample k's matrix comes down (rcp_profile_reads) */
+SEXP rcp_R_profile_reads(SEXP readsList, SEXP dev, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand,
+                         SEXP group, SEXP isList, SEXP ignoreStrand, SEXP where, SEXP flank, SEXP nBins, SEXP pbw,
+                         SEXP stat, SEXP interp, SEXP rng, SEXP scale, SEXP rowNames) {
+    rcp_rows_desc rd = rows_of(segOff, chrom, start, end, strand, group, isList, ignoreStrand);
+    int ncol = 0;
+    rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
+    int ns = LENGTH(readsList);
+    rcp_reads_desc* rds = (rcp_reads_desc*)R_alloc(ns > 0 ? ns : 1, sizeof(rcp_reads_desc));
+    double** outs = (double**)R_alloc(ns > 0 ? ns : 1, sizeof(double*));
+    uint8_t** valid = (uint8_t**)R_alloc(ns > 0 ? ns : 1, sizeof(uint8_t*));
+    SEXP mats = PROTECT(allocVector(VECSXP, ns));
+    for (int i = 0; i < ns; ++i) {
+        SEXP a = VECTOR_ELT(readsList, i);
+        rds[i] = reads_of(VECTOR_ELT(a, 0), VECTOR_ELT(a, 1), VECTOR_ELT(a, 2), VECTOR_ELT(a, 3), VECTOR_ELT(a, 4),
+                          VECTOR_ELT(a, 5));
+        rds[i].device = asInteger(dev);
+        SET_VECTOR_ELT(mats, i, allocMatrix(REALSXP, rd.n_rows, ncol));
+        outs[i] = REAL(VECTOR_ELT(mats, i));
+        valid[i] = (uint8_t*)R_alloc(rd.n_rows ? rd.n_rows : 1, 1);
+    }
+    int rc = rcp_profile_reads(rds, ns, &rd, &bd, outs, valid);
+    if (rc != RCP_OK) {
+        UNPROTECT(1);
+        check(rc);
+    }
+    SEXP res = PROTECT(allocVector(VECSXP, ns));
+    for (int i = 0; i < ns; ++i) {
+        set_dimnames(VECTOR_ELT(mats, i), rowNames, &bd, rd.n_rows, ncol);
+        SET_VECTOR_ELT(res, i, profile_result(VECTOR_ELT(mats, i), valid[i], rd.n_rows));
+    }
+    UNPROTECT(2);
+    return res;
+}
+
 /* .Call("rcp_R_profile_multi", list of readsets (one per GPU, rcp_R_readsets), <rows>, <bins>, rowNames):
  * row blocks on every GPU at once (the reference's cmclapply over regions) */
 SEXP rcp_R_profile_multi(SEXP rsl, SEXP segOff, SEXP chrom, SEXP start, SEXP end, SEXP strand, SEXP group,
@@ -575,6 +614,7 @@ static const R_CallMethodDef call_methods[] = {
     {"rcp_R_profile", (DL_FUNC)&rcp_R_profile, 18},
     {"rcp_R_profile_multi", (DL_FUNC)&rcp_R_profile_multi, 18},
     {"rcp_R_profile_samples", (DL_FUNC)&rcp_R_profile_samples, 19},
+    {"rcp_R_profile_reads", (DL_FUNC)&rcp_R_profile_reads, 19},
     {"rcp_R_profile_rle", (DL_FUNC)&rcp_R_profile_rle, 14},
     {"rcp_R_coverage", (DL_FUNC)&rcp_R_coverage, 9},
     {"rcp_R_read_bam", (DL_FUNC)&rcp_R_read_bam, 4},

@@ -64,7 +64,7 @@ class BinsDesc(ctypes.Structure):
 class PlanInfo(ctypes.Structure):
     _fields_ = [("n_cols", ctypes.c_int64), ("n_segments", ctypes.c_int64), ("n_interp_rows", ctypes.c_int64),
                 ("lds_bytes", ctypes.c_int64), ("grid", ctypes.c_int64), ("tile_rows", ctypes.c_int32),
-                ("chunk_positions", ctypes.c_int32), ("pileup_kernel", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("chunk_positions", ctypes.c_int32), ("pileup_kernel", ctypes.c_int32), ("read_bytes", ctypes.c_int32),
                 ("out_ld", ctypes.c_int64)]
 
 
@@ -112,6 +112,8 @@ SIGNATURES = [
     ("rcp_shards_destroy", ctypes.c_int, [_vp]),
     ("rcp_profile_rle_multi", ctypes.c_int, [ctypes.POINTER(RleDesc), ctypes.POINTER(BinsDesc), _i32p, ctypes.c_int32,
                                              _dp, _u8p]),
+    ("rcp_profile_reads", ctypes.c_int, [ctypes.POINTER(ReadsDesc), ctypes.c_int32, ctypes.POINTER(RowsDesc),
+                                         ctypes.POINTER(BinsDesc), ctypes.POINTER(_dp), ctypes.POINTER(_u8p)]),
     ("rcp_profile_samples", ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int32, ctypes.POINTER(RowsDesc),
                                            ctypes.POINTER(BinsDesc), ctypes.c_int32, ctypes.POINTER(_dp),
                                            ctypes.POINTER(_u8p)]),

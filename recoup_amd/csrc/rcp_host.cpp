@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <deque>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdint>
@@ -479,6 +481,16 @@ int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_reads
         HIP_TRY(hipStreamSynchronize(s));  // rstart is released on return
         if (h_over) return fail(RCP_EUNSUPPORTED, "a read's start + width - 1 exceeds 2^31 - 1");
         pe = in_end.as<int32_t>();
+    }
+    if ((layouts & kLayCheckOrder) && n > 1) {
+        PoolBuf flag(s);
+        HIP_TRY(flag.alloc(4));
+        HIP_TRY(hipMemsetAsync(flag.p, 0, 4, s));
+        HIP_TRY(rcp_launch_order(n, pc, ps, flag.as<uint32_t>(), s));
+        uint32_t h_flag = 0;
+        HIP_TRY(hipMemcpyAsync(&h_flag, flag.p, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (h_flag) return kNotInOrder;
     }
     PLAN_MARK("reads H2D");
     bool presorted = false;
@@ -1353,7 +1365,7 @@ extern "C" int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info) {
     info->tile_rows = plan->tile_rows;
     info->chunk_positions = plan->dev.chunk_cap;
     info->pileup_kernel = plan->dev.lean;
-    info->reserved = 0;
+    info->read_bytes = plan->dev.st ? 4 : 8;
     info->out_ld = plan->out_ld;
     return RCP_OK;
     RCP_CATCH
@@ -1403,12 +1415,28 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
             HIP_TRY(rcp_launch_heavy(&Q, kHeavyGrid, s));
         }
     }
+    // rows with fewer positions than bins (splines of short genes: serial chains) write only their
+    // own cells, and read only locate's outputs: they run on a side stream beside the pileup
+    // (C3: 0.1 ms of interpolation behind a 0.5 ms pileup) and join the caller's stream after it
+    const bool fork = (stages & RCP_STAGE_PILEUP) && (stages & RCP_STAGE_INTERP) && plan->dev.n_interp > 0;
+    if (fork) {
+        if (!plan->side) {
+            HIP_TRY(hipStreamCreateWithFlags(&plan->side, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&plan->ev_fork, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&plan->ev_join, hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(plan->ev_fork, s));
+        HIP_TRY(hipStreamWaitEvent(plan->side, plan->ev_fork, 0));
+        HIP_TRY(rcp_launch_interp(&plan->dev, d_out, plan->side));
+        HIP_TRY(hipEventRecord(plan->ev_join, plan->side));
+    }
     if (stages & RCP_STAGE_PILEUP) {
         RcpPlanDev Q = plan->dev;
         if (Q.fold) Q.valid_out = d_valid;
         HIP_TRY(rcp_launch_pileup(&Q, d_out, d_binsum, 0, s));
     }
-    if (stages & RCP_STAGE_INTERP) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
+    if (fork) HIP_TRY(hipStreamWaitEvent(s, plan->ev_join, 0));
+    else if (stages & RCP_STAGE_INTERP) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
     return RCP_OK;
     RCP_CATCH
 }
@@ -1506,6 +1534,276 @@ extern "C" int rcp_readset_create_multi(const rcp_reads_desc* desc, const int32_
     RCP_CATCH
 }
 
+namespace {
+
+// One sample's reads cut for one row table (rcp_profile_reads): row block b = rows
+// [rows[b], rows[b + 1]) needs only the reads [a[b], z[b]) of the caller's arrays.
+struct StreamCut {
+    std::vector<int32_t> rows;
+    std::vector<int64_t> a, z;
+};
+
+// The cut of a sample whose host reads are coordinate-sorted -- chromosome runs, each code in
+// one run, starts ascending inside a run (what a sorted BAM gives: R/ranges.R:111-132 keeps file
+// order) -- and come with width runs (the widest read bounds how far before a range its reads
+// start).  Row blocks of equal row count (equal matrix bytes to copy down); each block's reads
+// are found by bisection of the host starts per chromosome, and the slices together cover every
+// read, so that the device check of each slice (kLayCheckOrder) plus the host check of the pair
+// in front of every slice end prove the order the bisections assumed.  false: the sample goes
+// as one piece (per-read chromosome or end vectors, few reads or rows, or slices that would
+// overlap much -- rows in another chromosome order than the reads).
+bool stream_cut(const rcp_reads_desc& d, const rcp_rows_desc* rows, StreamCut* cut) {
+    const int64_t n = d.n;
+    const int32_t R = rows->n_rows;
+    if (d.on_device || d.chrom || d.end || !d.start || n < (int64_t(1) << 22) || R < 2048) return false;
+    if (d.n_chrom_runs <= 0 || !d.chrom_run_value || !d.chrom_run_length || d.n_width_runs <= 0 ||
+        !d.width_run_value || !d.width_run_length || d.n_chrom <= 0)
+        return false;
+    int32_t maxw = 0;
+    for (int32_t k = 0; k < d.n_width_runs; ++k) {
+        if (d.width_run_value[k] < 0) return false;  // (the build reports it)
+        maxw = std::max(maxw, d.width_run_value[k]);
+    }
+    // chromosome code -> its run [cs, ce)
+    std::vector<int64_t> cs(d.n_chrom, -1), ce(d.n_chrom, -1), run_at;
+    run_at.reserve(d.n_chrom_runs + 1);
+    int64_t pos = 0;
+    for (int32_t k = 0; k < d.n_chrom_runs; ++k) {
+        const int32_t c = d.chrom_run_value[k];
+        if (d.chrom_run_length[k] <= 0) return false;
+        if (c >= 0 && c < d.n_chrom) {
+            if (cs[c] >= 0) return false;  // a chromosome in two runs: not grouped
+            cs[c] = pos;
+            ce[c] = pos + d.chrom_run_length[k];
+        }
+        run_at.push_back(pos);
+        pos += d.chrom_run_length[k];
+    }
+    if (pos != n) return false;
+    const int nb = (int)std::min<int64_t>(8, std::max<int64_t>(2, n >> 22));  // >= 4 M reads a block
+    cut->rows.resize(nb + 1);
+    for (int b = 0; b <= nb; ++b) cut->rows[b] = (int32_t)((int64_t)R * b / nb);
+    std::vector<int64_t> L(nb, n), H(nb, 0), smin(d.n_chrom), emax(d.n_chrom);
+    std::vector<char> touched(d.n_chrom, 0);
+    std::vector<int32_t> list;
+    const int32_t* st = d.start;
+    for (int b = 0; b < nb; ++b) {
+        list.clear();
+        for (int64_t j = rows->seg_off[cut->rows[b]]; j < rows->seg_off[cut->rows[b + 1]]; ++j) {
+            const int32_t c = rows->seg_chrom[j];
+            if (c < 0 || c >= d.n_chrom || cs[c] < 0) continue;
+            const int64_t s0 = std::max<int64_t>(rows->seg_start[j], 1), e0 = rows->seg_end[j];
+            if (e0 < s0) continue;
+            const int64_t lo = s0 - maxw + 1;  // a read overlapping [s0, e0] starts in [lo, e0]
+            if (!touched[c]) {
+                touched[c] = 1;
+                list.push_back(c);
+                smin[c] = lo;
+                emax[c] = e0;
+            } else {
+                smin[c] = std::min(smin[c], lo);
+                emax[c] = std::max(emax[c], e0);
+            }
+        }
+        for (int32_t c : list) {
+            touched[c] = 0;
+            const int64_t l = std::lower_bound(st + cs[c], st + ce[c], smin[c],
+                                               [](int32_t v, int64_t x) { return (int64_t)v < x; }) - st;
+            const int64_t h = std::upper_bound(st + cs[c], st + ce[c], emax[c],
+                                               [](int64_t x, int32_t v) { return x < (int64_t)v; }) - st;
+            if (h > l) {
+                L[b] = std::min(L[b], l);
+                H[b] = std::max(H[b], h);
+            }
+        }
+    }
+    // slices: [a_b, z_b) holds block b's reads; together they cover [0, n)
+    cut->a.assign(nb, 0);
+    cut->z.assign(nb, 0);
+    int64_t Z = 0, total = 0;
+    for (int b = 0; b < nb; ++b) {
+        cut->a[b] = b == 0 ? 0 : std::min(L[b], Z);
+        cut->z[b] = b == nb - 1 ? n : std::max(H[b], cut->a[b]);
+        Z = std::max(Z, cut->z[b]);
+        total += cut->z[b] - cut->a[b];
+    }
+    if (total > n + n / 4) return false;
+    // the pair of reads in front of each slice end (the device checks the pairs inside a slice)
+    for (int b = 0; b < nb; ++b) {
+        const int64_t i = cut->z[b];
+        if (i <= 0 || i >= n) continue;
+        const bool same_run = !std::binary_search(run_at.begin(), run_at.end(), i);
+        if (same_run && st[i - 1] > st[i]) return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_samples, const rcp_rows_desc* rows,
+                                 const rcp_bins_desc* bins, double* const* outs, uint8_t* const* row_valid) {
+    RCP_TRY
+    if (!samples || !rows || !bins) return fail(RCP_EINVAL, "NULL argument");
+    if (n_samples < 0) return fail(RCP_EINVAL, "n_samples = %d", n_samples);
+    if (n_samples == 0) return RCP_OK;
+    const int dev = samples[0].device;
+    for (int i = 0; i < n_samples; ++i)
+        if (samples[i].device != dev)
+            return fail(RCP_EINVAL, "samples[%d] is for device %d, samples[0] for %d (one device per call)", i,
+                        samples[i].device, dev);
+    int rc = check_device(dev);
+    if (rc) return rc;
+    const int32_t R = rows->n_rows;
+    if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
+    if (R > 0 && (!rows->seg_off || !rows->seg_chrom || !rows->seg_start || !rows->seg_end || !rows->seg_strand))
+        return fail(RCP_EINVAL, "NULL row array");
+    // the one layout the row table searches, built from the uploaded copies right away
+    const int layout = rows->ignore_strand ? kLayMerged : kLayStranded;
+    // Work items: a sample of sorted reads is cut into row blocks, each with the slice of the
+    // reads it needs (stream_cut); any other sample is one item.  One uploader thread builds the
+    // items' readsets in order (H2D through the upload staging buffers, sort, index); two profiler
+    // threads take them in order, each planning + running its block's pass and copying the block's
+    // rows of the matrix down (the download staging buffers): while one copies down, the other
+    // plans and runs, and the uploader sends the next slice up -- both PCIe directions busy.  At
+    // most three readsets exist at once.  A sample whose slices prove unsorted on the device is
+    // redone as one item after its blocks in flight have finished.
+    struct Item {
+        int sample;
+        int32_t r0, r1;
+        bool redo;
+        rcp_readset* rs;
+    };
+    std::deque<Item> items;
+    size_t next = 0;
+    int alive = 0;
+    bool uploaded = false, abort = false;
+    std::vector<char> poisoned(n_samples, 0);
+    std::vector<int> active(n_samples, 0);
+    std::mutex mu;
+    std::condition_variable cv;
+    const bool tr = rcp::trace_on();
+    const double t0 = tr ? rcp::trace_ms() : 0.0;
+    const int r2 = run_per_device(3, [&](int role) -> int {
+        DeviceGuard g(dev);
+        HIP_TRY(g.err);
+        hipStream_t s = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(s, hipStreamDestroy);
+        if (role == 0) {  // uploader
+            auto build = [&](const rcp_reads_desc& d, int lay, rcp_readset** out) -> int {
+                {
+                    std::unique_lock<std::mutex> lock(mu);
+                    cv.wait(lock, [&] { return abort || alive < 3; });
+                    if (abort) return -1000;
+                    ++alive;
+                }
+                const int e = readset_build(&d, s, lay, out);
+                if (e) {
+                    std::lock_guard<std::mutex> lock(mu);
+                    --alive;
+                }
+                return e;
+            };
+            auto publish = [&](const Item& it) {
+                {
+                    std::lock_guard<std::mutex> lock(mu);
+                    items.push_back(it);
+                }
+                cv.notify_all();
+            };
+            auto failed = [&](int e) {
+                {
+                    std::lock_guard<std::mutex> lock(mu);
+                    abort = true;
+                }
+                cv.notify_all();
+                return e == -1000 ? (int)RCP_OK : e;
+            };
+            for (int k = 0; k < n_samples; ++k) {
+                StreamCut cut;
+                bool redo = false;
+                if (stream_cut(samples[k], rows, &cut)) {
+                    for (size_t b = 0; b + 1 < cut.rows.size(); ++b) {
+                        ReadSlice sl;
+                        slice_reads(&samples[k], cut.a[b], cut.z[b], &sl);
+                        rcp_readset* r = nullptr;
+                        const double tb = tr ? rcp::trace_ms() : 0.0;
+                        const int e = build(sl.d, layout | kLayCheckOrder, &r);
+                        if (tr)
+                            fprintf(stderr, "[reads] sample %d block %zu: %lld reads up + built %.2f ms (at %.2f)\n", k, b,
+                                    (long long)sl.d.n, rcp::trace_ms() - tb, tb - t0);
+                        if (e == kNotInOrder) {
+                            redo = true;
+                            std::lock_guard<std::mutex> lock(mu);
+                            poisoned[k] = 1;
+                            break;
+                        }
+                        if (e) return failed(e);
+                        publish(Item{k, cut.rows[b], cut.rows[b + 1], false, r});
+                    }
+                } else {
+                    redo = true;
+                }
+                if (redo) {
+                    rcp_readset* r = nullptr;
+                    const int e = build(samples[k], layout, &r);
+                    if (e) return failed(e);
+                    publish(Item{k, 0, R, poisoned[k] != 0, r});
+                }
+            }
+            {
+                std::lock_guard<std::mutex> lock(mu);
+                uploaded = true;
+            }
+            cv.notify_all();
+            return (int)RCP_OK;
+        }
+        for (;;) {  // profilers
+            Item it{};
+            {
+                std::unique_lock<std::mutex> lock(mu);
+                cv.wait(lock, [&] { return abort || next < items.size() || uploaded; });
+                if (abort || next >= items.size()) return (int)RCP_OK;
+                it = items[next++];
+                if (poisoned[it.sample] && !it.redo) {  // a block of a sample being redone whole
+                    lock.unlock();
+                    rcp_readset_destroy(it.rs);
+                    lock.lock();
+                    --alive;
+                    cv.notify_all();
+                    continue;
+                }
+                if (it.redo) cv.wait(lock, [&] { return abort || active[it.sample] == 0; });
+                ++active[it.sample];
+            }
+            const double tb = tr ? rcp::trace_ms() : 0.0;
+            rcp_rows_desc sub = *rows;
+            sub.n_rows = it.r1 - it.r0;
+            sub.seg_off = rows->seg_off + it.r0;
+            int64_t nc = 0;
+            int e = abort ? (int)RCP_OK
+                          : profile_block(it.rs, &sub, bins, outs ? outs[it.sample] : nullptr, R, it.r0,
+                                          row_valid ? row_valid[it.sample] : nullptr, &nc, s);
+            if (tr)
+                fprintf(stderr, "[reads] sample %d rows [%d, %d): profile + down %.2f ms (at %.2f)\n", it.sample, it.r0,
+                        it.r1, rcp::trace_ms() - tb, tb - t0);
+            rcp_readset_destroy(it.rs);  // (a device synchronisation: outside the lock)
+            {
+                std::lock_guard<std::mutex> lock(mu);
+                --alive;
+                --active[it.sample];
+                if (e) abort = true;
+            }
+            cv.notify_all();
+            if (e) return e;
+        }
+    });
+    // (left behind by a failure: items not taken)
+    for (size_t i = next; i < items.size(); ++i) rcp_readset_destroy(items[i].rs);
+    return r2;
+    RCP_CATCH
+}
+
 extern "C" int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_samples, const rcp_rows_desc* rows,
                                    const rcp_bins_desc* bins, int32_t inflight, double* const* outs,
                                    uint8_t* const* row_valid) {
@@ -1585,7 +1883,7 @@ extern "C" int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_sampl
 namespace rcpi {
 
 int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bins_desc* bins, double* out,
-                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols) {
+                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream) {
     rcp_plan* plan = nullptr;
     rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, 0, {0, 0}};
     int e = rcp_plan_create_ex(rs, sub, bins, &opts, &plan);
@@ -1594,11 +1892,14 @@ int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bin
     DeviceGuard g(rs->device);
     HIP_TRY(g.err);
     if (n_cols) *n_cols = plan->n_cols;
-    hipStream_t s = nullptr;
-    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(s, hipStreamDestroy);
+    hipStream_t s = stream;
+    if (!stream) HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(
+        stream ? nullptr : s, hipStreamDestroy);
+    // stream-ordered from the pool: no hipMalloc / hipFree (a device-wide synchronisation that would
+    // wait for other threads' uploads) per block
     const size_t cells = (size_t)plan->out_ld * (size_t)plan->n_cols;
-    DevBuf d_out, d_valid;
+    PoolBuf d_out(s), d_valid(s);
     HIP_TRY(d_out.alloc(8 * std::max<size_t>(cells, 1)));
     HIP_TRY(d_valid.alloc(std::max<int32_t>(plan->n_rows, 1)));
     e = rcp_plan_execute(plan, d_out.as<double>(), d_valid.as<uint8_t>(), nullptr, s);
@@ -1986,7 +2287,7 @@ bool part_slice_spec(int where, int32_t f1, int32_t f2, RcpPart* pt) {
 }  // namespace
 
 int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out,
-                           int64_t out_ld, uint8_t* row_valid) {
+                           int64_t out_ld, uint8_t* row_valid, hipStream_t s) {
     if (!cov || !bins) return fail(RCP_EINVAL, "NULL argument");
     const int32_t R = cov->n_rows;
     if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
@@ -2040,10 +2341,9 @@ int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, i
     if (rc) return rc;
     DeviceGuard g(device);
     HIP_TRY(g.err);
-    hipStream_t s = nullptr;
     // ---- runs to the device: lengths (+ a 0 pad for the scan), values, row offsets;
     // the scan of the lengths gives every run's start (rcp_rle.h gstart)
-    DevBuf d_len, d_val, d_off, d_gstart, temp;
+    PoolBuf d_len(s), d_val(s), d_off(s), d_gstart(s), temp(s);
     HIP_TRY(d_len.alloc(4 * ((size_t)n_runs + 1)));
     HIP_TRY(d_val.alloc((dbl ? 8 : 4) * std::max<size_t>((size_t)n_runs, 1)));
     HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
@@ -2197,7 +2497,7 @@ int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, i
     const size_t o_lay = put(blob, lay_cnt);
     const size_t o_nb = put(blob, nb_pos);
     const size_t o_spl = put(blob, spl_tb);
-    DevBuf d_tab, d_scratch, d_out;
+    PoolBuf d_tab(s), d_scratch(s), d_out(s);
     HIP_TRY(d_tab.alloc(blob.size()));
     HIP_TRY(rcp::stage_h2d(d_tab.p, blob.data(), blob.size(), device, s));
     if (n_scratch && !P.interp_lds) HIP_TRY(d_scratch.alloc(8 * (size_t)stride * n_scratch));
@@ -2231,11 +2531,69 @@ int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, i
     return RCP_OK;
 }
 
+namespace {
+
+// rcp_profile_rle of rows [0, cov->n_rows) on one device, into a matrix of column stride out_ld:
+// big lists in row blocks through two host threads with a stream each, so that one block's runs
+// go up while another's rows of the matrix come down (PCIe is full duplex; the staging buffers
+// are per direction, rcp_stage.cpp): C4's 0.8 GB of runs up and 1.6 GB of matrix down overlap
+int profile_rle_device(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out, int64_t out_ld,
+                       uint8_t* row_valid) {
+    const int32_t R = cov->n_rows;
+    const int64_t n_runs = R > 0 ? cov->run_off[R] : 0;
+    int nb = 1;  // row blocks
+    if (n_runs >= (int64_t(1) << 23) && R >= 4096) nb = 8;
+    else if (n_runs >= (int64_t(1) << 21) && R >= 1024) nb = 4;
+    // (one block, or no such device: the single call validates the lists before any device work)
+    if (nb == 1 || check_device(device) != RCP_OK)
+        return profile_rle_impl(cov, bins, device, out, out_ld, row_valid, nullptr);
+    std::vector<double> cum((size_t)R + 1, 0.0);
+    for (int32_t r = 0; r < R; ++r) cum[r + 1] = cum[r] + 64.0 + (double)(cov->run_off[r + 1] - cov->run_off[r]);
+    const std::vector<int32_t> split = balanced_split(cum, nb);
+    return run_per_device(2, [&](int t) {
+        DeviceGuard gt(device);
+        HIP_TRY(gt.err);
+        hipStream_t s = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(s, hipStreamDestroy);
+        for (int b = t; b < nb; b += 2) {
+            const int32_t r0 = split[b], r1 = split[b + 1];
+            if (r1 <= r0) continue;
+            // the block as an Rle list of its own: run offsets from 0, arrays from its first run
+            const int64_t base = cov->run_off[r0];
+            std::vector<int64_t> off((size_t)(r1 - r0) + 1);
+            for (int32_t r = r0; r <= r1; ++r) off[r - r0] = cov->run_off[r] - base;
+            rcp_rle_desc sub = *cov;
+            sub.n_rows = r1 - r0;
+            sub.run_off = off.data();
+            sub.lengths = cov->lengths ? cov->lengths + base : nullptr;
+            sub.ivalues = cov->ivalues ? cov->ivalues + base : nullptr;
+            sub.dvalues = cov->dvalues ? cov->dvalues + base : nullptr;
+            sub.is_null = cov->is_null ? cov->is_null + r0 : nullptr;
+            const double tb = rcp::trace_on() ? rcp::trace_ms() : 0.0;
+            const int e = profile_rle_impl(&sub, bins, device, out ? out + r0 : nullptr, out_ld,
+                                           row_valid ? row_valid + r0 : nullptr, s);
+            if (rcp::trace_on())
+                fprintf(stderr, "[rle] block %d rows [%d, %d): %.2f ms (from %.2f)\n", b, r0, r1, rcp::trace_ms() - tb, tb);
+            if (e) return e;
+        }
+        return (int)RCP_OK;
+    });
+}
+
+}  // namespace
+
 extern "C" int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out,
                                uint8_t* row_valid) {
     RCP_TRY
-    if (!cov) return fail(RCP_EINVAL, "NULL argument");
-    return profile_rle_impl(cov, bins, device, out, cov->n_rows, row_valid);
+    if (!cov || !bins) return fail(RCP_EINVAL, "NULL argument");
+    const int32_t R = cov->n_rows;
+    if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
+    if (R > 0 && !cov->run_off) return fail(RCP_EINVAL, "NULL run_off");
+    if (R > 0 && cov->run_off[0] != 0) return fail(RCP_EINVAL, "run_off[0] != 0");
+    for (int32_t r = 0; r < R; ++r)
+        if (cov->run_off[r + 1] < cov->run_off[r]) return fail(RCP_EINVAL, "run_off decreases at row %d", r);
+    return profile_rle_device(cov, bins, device, out, R, row_valid);
     RCP_CATCH
 }
 
@@ -2254,7 +2612,7 @@ extern "C" int rcp_profile_rle_multi(const rcp_rle_desc* cov, const rcp_bins_des
     if (R > 0 && cov->run_off[0] != 0) return fail(RCP_EINVAL, "run_off[0] != 0");
     for (int32_t r = 0; r < R; ++r)
         if (cov->run_off[r + 1] < cov->run_off[r]) return fail(RCP_EINVAL, "run_off decreases at row %d", r);
-    if (n_devices == 1) return profile_rle_impl(cov, bins, device_ids[0], out, R, row_valid);
+    if (n_devices == 1) return profile_rle_device(cov, bins, device_ids[0], out, R, row_valid);
     // contiguous row blocks balanced by the runs each row streams (12 bytes each up, read once)
     // plus its output columns (the same for every row: a constant per row)
     std::vector<double> cum((size_t)R + 1, 0.0);
@@ -2274,8 +2632,8 @@ extern "C" int rcp_profile_rle_multi(const rcp_rle_desc* cov, const rcp_bins_des
         sub.ivalues = cov->ivalues ? cov->ivalues + base : nullptr;
         sub.dvalues = cov->dvalues ? cov->dvalues + base : nullptr;
         sub.is_null = cov->is_null ? cov->is_null + r0 : nullptr;
-        return profile_rle_impl(&sub, bins, device_ids[i], out ? out + r0 : nullptr, R,
-                                row_valid ? row_valid + r0 : nullptr);
+        return profile_rle_device(&sub, bins, device_ids[i], out ? out + r0 : nullptr, R,
+                                  row_valid ? row_valid + r0 : nullptr);
     });
     RCP_CATCH
 }

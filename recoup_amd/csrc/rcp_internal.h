@@ -24,6 +24,7 @@ hipError_t rcp_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* kin, u
 hipError_t rcp_launch_unsorted(int64_t n, const uint64_t* keys, uint32_t* flag, hipStream_t stream);
 hipError_t rcp_launch_width_end(int64_t n, const int32_t* start, int32_t* width_end, uint32_t* overflow,
                                 hipStream_t stream);
+hipError_t rcp_launch_order(int64_t n, const int32_t* chrom, const int32_t* start, uint32_t* flag, hipStream_t stream);
 hipError_t rcp_launch_expand_runs(int64_t n, int32_t n_runs, const int64_t* run_start, const int32_t* run_value,
                                   int32_t* out, hipStream_t stream);
 hipError_t rcp_segmax_scan(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
@@ -206,13 +207,15 @@ int run_per_device(int n, F fn) {
 
 // Block [r0, r0 + sub->n_rows) of an n_rows_total-row profile on readset rs: plan, execute, and
 // copy its rows of every column into the caller's R column-major matrix `out` (may be NULL) and
-// row_valid + r0 (may be NULL); *n_cols receives the plan's column count (rcp_host.cpp)
+// row_valid + r0 (may be NULL); *n_cols receives the plan's column count.  On `stream` (NULL: a
+// stream of its own); returns with the copies done (rcp_host.cpp)
 int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bins_desc* bins, double* out,
-                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols);
+                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream = nullptr);
 
-// rcp_profile_rle into rows [0, n_rows) of a matrix with column stride out_ld (rcp_host.cpp)
+// rcp_profile_rle into rows [0, n_rows) of a matrix with column stride out_ld, on stream s
+// (rcp_host.cpp)
 int profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out, int64_t out_ld,
-                     uint8_t* row_valid);
+                     uint8_t* row_valid, hipStream_t s);
 
 // Contiguous row blocks of near-equal weight from the prefix sums of the row weights (rcp_host.cpp)
 std::vector<int32_t> balanced_split(const std::vector<double>& cum, int32_t n_blocks);
@@ -221,6 +224,15 @@ std::vector<int32_t> balanced_split(const std::vector<double>& cum, int32_t n_bl
 // search (merged for ignore_strand, else strand-split): host [3 * n_seg] (rcp_shard.cpp)
 int seg_bounds(const rcp_readset* rs, const rcp_rows_desc* rows, std::vector<uint2>* out);
 
+// Reads [a, b) of a sample as a descriptor of their own (run lists cut to the slice, owned here)
+// (rcp_shard.cpp)
+struct ReadSlice {
+    rcp_reads_desc d{};
+    std::vector<int32_t> cv, wv;
+    std::vector<int64_t> cl, wl;
+};
+void slice_reads(const rcp_reads_desc* src, int64_t a, int64_t b, ReadSlice* out);
+
 // rcp_cov_copy of a coverage made of per-device parts (rcp_shard.cpp)
 int cov_copy_parts(const rcp_cov* c, int64_t* run_off, int32_t* values, int32_t* lengths, uint8_t* valid);
 
@@ -228,7 +240,10 @@ int cov_copy_parts(const rcp_cov* c, int64_t* run_off, int32_t* values, int32_t*
 // kLayStranded (FALSE); kLayKeep: host input keeps its uploaded copies for a stranded layout
 // built at first use; kLayIndexOnly: streams and prefix max only, no bucket directory (a
 // readset searched once, never planned on)
-enum { kLayMerged = 1, kLayStranded = 2, kLayKeep = 4, kLayIndexOnly = 8 };
+// kLayCheckOrder: host input with chromosome runs must be coordinate-sorted (starts ascending
+// inside each chromosome's reads): kNotInOrder (> 0, no error message) when it is not
+enum { kLayMerged = 1, kLayStranded = 2, kLayKeep = 4, kLayIndexOnly = 8, kLayCheckOrder = 16 };
+constexpr int kNotInOrder = 1;
 int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_readset** out);
 
 }  // namespace rcpi
@@ -336,6 +351,15 @@ struct rcp_plan {
     int64_t out_ld = 0;
     uint32_t* status_sets = nullptr;  // 2 x RCP_STATUS_WORDS words in `work`
     int epoch = 1;                    // parity of the last execution (the first one uses set 0)
+    // the interpolation rows run on a side stream beside the pileup (fork / join on the caller's
+    // stream; made at the first execution that interpolates)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    ~rcp_plan() {  // (on the plan's device: rcp_plan_destroy)
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (side) (void)hipStreamDestroy(side);
+    }
 };
 
 // a calcCoverage result held on the device (rcp_host.cpp); a coverage of several devices' row

@@ -503,6 +503,15 @@ __global__ void rcp_width_end_kernel(int64_t n, const int32_t* __restrict__ star
     width_end[i] = (int32_t)e;
 }
 
+// flag = 1 when a read starts before the one in front of it on the same chromosome (the slices
+// of a streamed sample must hold coordinate-sorted reads, rcp_profile_reads)
+__global__ void rcp_order_kernel(int64_t n, const int32_t* __restrict__ chrom, const int32_t* __restrict__ start,
+                                 uint32_t* __restrict__ flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i + 1 >= n) return;
+    if (chrom[i] == chrom[i + 1] && start[i] > start[i + 1]) *flag = 1u;
+}
+
 // chromosome code of read i from the seqnames runs (run_start: prefix sums, n_runs + 1 entries)
 __global__ void rcp_expand_runs_kernel(int64_t n, int32_t n_runs, const int64_t* __restrict__ run_start,
                                        const int32_t* __restrict__ run_value, int32_t* __restrict__ out) {
@@ -3426,6 +3435,14 @@ extern "C" hipError_t rcp_launch_width_end(int64_t n, const int32_t* start, int3
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(rcp_width_end_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, n,
                        start, width_end, overflow);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rcp_launch_order(int64_t n, const int32_t* chrom, const int32_t* start, uint32_t* flag,
+                                       hipStream_t stream) {
+    if (n < 2) return hipSuccess;
+    hipLaunchKernelGGL(rcp_order_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, n,
+                       chrom, start, flag);
     return hipGetLastError();
 }
 

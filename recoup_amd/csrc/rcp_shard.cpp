@@ -150,6 +150,35 @@ void slice_runs(const int32_t* val, const int64_t* len, int32_t n_runs, int64_t 
     }
 }
 
+}  // namespace
+
+void rcpi::slice_reads(const rcp_reads_desc* src, int64_t a, int64_t b, ReadSlice* out) {
+    rcp_reads_desc& d = out->d;
+    d = *src;
+    d.n = b - a;
+    // (per-read arrays: host or device pointers; the runs are host arrays in both modes)
+    if (src->chrom) {
+        d.chrom = src->chrom + a;
+    } else if (d.n > 0) {
+        slice_runs(src->chrom_run_value, src->chrom_run_length, src->n_chrom_runs, a, b, &out->cv, &out->cl);
+        d.n_chrom_runs = (int32_t)out->cv.size();
+        d.chrom_run_value = out->cv.data();
+        d.chrom_run_length = out->cl.data();
+    }
+    if (src->end) {
+        d.end = src->end + a;
+    } else if (d.n > 0) {
+        slice_runs(src->width_run_value, src->width_run_length, src->n_width_runs, a, b, &out->wv, &out->wl);
+        d.n_width_runs = (int32_t)out->wv.size();
+        d.width_run_value = out->wv.data();
+        d.width_run_length = out->wl.data();
+    }
+    if (d.start) d.start = src->start + a;
+    if (d.strand) d.strand = src->strand + a;
+}
+
+namespace {
+
 // Enable direct device-to-device copies between every pair of the listed GPUs (xGMI), once per
 // pair; where that is refused the copies below still run (staged by the runtime).
 void enable_peers(const std::vector<int32_t>& devices) {
@@ -245,30 +274,10 @@ extern "C" int rcp_shards_create(const rcp_reads_desc* reads, const rcp_rows_des
     const int64_t n = reads->n;
     int rc = run_per_device(K, [&](int i) {
         const int64_t a = n * i / K, b = n * (i + 1) / K;
-        rcp_reads_desc d = *reads;
-        d.device = slice_dev[i];
-        d.n = b - a;
-        std::vector<int32_t> cv, wv;
-        std::vector<int64_t> cl, wl;
-        if (reads->chrom) {
-            d.chrom = reads->chrom + a;
-        } else if (d.n > 0) {
-            slice_runs(reads->chrom_run_value, reads->chrom_run_length, reads->n_chrom_runs, a, b, &cv, &cl);
-            d.n_chrom_runs = (int32_t)cv.size();
-            d.chrom_run_value = cv.data();
-            d.chrom_run_length = cl.data();
-        }
-        if (reads->end) {
-            d.end = reads->end + a;
-        } else if (d.n > 0) {
-            slice_runs(reads->width_run_value, reads->width_run_length, reads->n_width_runs, a, b, &wv, &wl);
-            d.n_width_runs = (int32_t)wv.size();
-            d.width_run_value = wv.data();
-            d.width_run_length = wl.data();
-        }
-        if (d.start) d.start = reads->start + a;
-        if (d.strand) d.strand = reads->strand + a;
-        return readset_build(&d, nullptr, layout | kLayIndexOnly, &slice[i]);
+        ReadSlice sl;
+        slice_reads(reads, a, b, &sl);
+        sl.d.device = slice_dev[i];
+        return readset_build(&sl.d, nullptr, layout | kLayIndexOnly, &slice[i]);
     });
     if (rc) return rc;
     // ---- B: candidate reads of every (range, stream) in every slice

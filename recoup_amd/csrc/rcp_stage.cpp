@@ -9,8 +9,15 @@
 // (rcp_profile_multi drives one host thread per GPU).
 #include "rcp_stage.h"
 
+#include <emmintrin.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -124,6 +131,65 @@ bool ready(Stager* s) {  // under s->mu, on the device
     return true;
 }
 
+// RCP_TRACE=1 in the environment: one stderr line per staged copy (direction, bytes, time waiting
+// for the direction's buffers, copy time) -- diagnostics of the PCIe pipelines, off by default
+bool trace() { return std::getenv("RCP_TRACE") != nullptr; }  // (read per call: tests set it around one call)
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// The direction's buffers: a copy below kShared does not wait for them when another thread holds
+// them (the lock comes back unowned) but goes through HIP's own staging -- a plan's table upload
+// need not queue behind the next sample's multi-GB read upload
+constexpr size_t kShared = size_t(16) << 20;
+std::unique_lock<std::mutex> take(Stager* st, size_t bytes) {
+    if (bytes < kShared) {
+        std::unique_lock<std::mutex> g(st->mu, std::try_to_lock);
+        return g;
+    }
+    return std::unique_lock<std::mutex>(st->mu);
+}
+
+// memcpy with non-temporal 16-B stores: the destination lines are not read first (no
+// read-for-ownership) and do not evict the other direction's working set -- the host memory
+// traffic of a staged copy is the DMA's plus one read and one write per byte
+void copy_nt(char* dst, const char* src, size_t n) {
+    if (n < 256) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+    std::memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    for (; i + 16 <= n; i += 16)
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i)));
+    std::memcpy(dst + i, src + i, n - i);
+    _mm_sfence();
+}
+
+// A large destination the caller has just allocated (R's vectors of a coverage list) is
+// first-touched by the drain threads: transparent huge pages make that one fault per 2 MB
+void advise_huge(void* p, size_t n) {
+    static const size_t page = (size_t)sysconf(_SC_PAGESIZE);
+    const uintptr_t huge = uintptr_t(2) << 20;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + huge - 1) & ~(huge - 1);
+    const uintptr_t z = (reinterpret_cast<uintptr_t>(p) + n) & ~(huge - 1);
+    if (z > a && page <= huge) madvise(reinterpret_cast<void*>(a), z - a, MADV_HUGEPAGE);  // advisory: result ignored
+}
+
 // Split [0, n) into kThreads near-equal 4 KB-aligned parts.
 inline void part_range(size_t n, int i, size_t* a, size_t* b) {
     const size_t per = ((n + kThreads - 1) / kThreads + 4095) & ~size_t(4095);
@@ -133,17 +199,22 @@ inline void part_range(size_t n, int i, size_t* a, size_t* b) {
 
 }  // namespace
 
+bool trace_on() { return trace(); }
+double trace_ms() { return now_ms(); }
+
 hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipStream_t stream) {
     if (bytes == 0) return hipSuccess;
     Stager* st = stager(device, 0);
-    if (bytes < kDirect || !st) {
+    const double t0 = trace() ? now_ms() : 0.0;
+    std::unique_lock<std::mutex> g;
+    if (bytes >= kDirect && st) g = take(st, bytes);
+    const double t1 = trace() ? now_ms() : 0.0;
+    if (!g.owns_lock() || !ready(st)) {
         hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream);
-        return e == hipSuccess ? hipStreamSynchronize(stream) : e;
-    }
-    std::lock_guard<std::mutex> g(st->mu);
-    if (!ready(st)) {
-        hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream);
-        return e == hipSuccess ? hipStreamSynchronize(stream) : e;
+        e = e == hipSuccess ? hipStreamSynchronize(stream) : e;
+        if (trace() && bytes >= kDirect)
+            fprintf(stderr, "[stage] h2d %zu B direct %.2f ms\n", bytes, now_ms() - t1);
+        return e;
     }
     const char* s = static_cast<const char*>(src);
     char* d = static_cast<char*>(dst);
@@ -158,12 +229,13 @@ hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipSt
         st->pool->run(kThreads, [&](int i) {
             size_t a, z;
             part_range(len, i, &a, &z);
-            if (z > a) std::memcpy(pin + a, s + a0 + a, z - a);
+            if (z > a) copy_nt(pin + a, s + a0 + a, z - a);
         });
         e = hipMemcpyAsync(d + a0, pin, len, hipMemcpyHostToDevice, stream);
         if (e == hipSuccess) e = hipEventRecord(st->ev[b], stream);
     }
     const hipError_t e2 = hipStreamSynchronize(stream);  // buffers free for the next user
+    if (trace()) fprintf(stderr, "[stage] h2d %zu B wait %.2f ms copy %.2f ms\n", bytes, t1 - t0, now_ms() - t1);
     return e != hipSuccess ? e : e2;
 }
 
@@ -173,17 +245,20 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
     // the device bytes moved: rows with their padding, except after the last row
     const size_t bytes = spitch * (height - 1) + width;
     Stager* st = stager(device, 1);
-    if (bytes < kDirect || !st) {
+    const double t0 = trace() ? now_ms() : 0.0;
+    std::unique_lock<std::mutex> g;
+    if (bytes >= kDirect && st) g = take(st, bytes);
+    const double t1 = trace() ? now_ms() : 0.0;
+    if (!g.owns_lock() || !ready(st)) {
         hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost, stream);
-        return e == hipSuccess ? hipStreamSynchronize(stream) : e;
-    }
-    std::lock_guard<std::mutex> g(st->mu);
-    if (!ready(st)) {
-        hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost, stream);
-        return e == hipSuccess ? hipStreamSynchronize(stream) : e;
+        e = e == hipSuccess ? hipStreamSynchronize(stream) : e;
+        if (trace() && bytes >= kDirect)
+            fprintf(stderr, "[stage] d2h %zu B direct %.2f ms\n", bytes, now_ms() - t1);
+        return e;
     }
     const char* s = static_cast<const char*>(src);
     char* d = static_cast<char*>(dst);
+    if (bytes >= kShared) advise_huge(d, dpitch * (height - 1) + width);
     // device bytes [a, z) of the linear span -> their host rows (padding bytes skipped)
     auto scatter = [&](const char* pin, size_t base, size_t a, size_t z) {
         while (a < z) {
@@ -193,7 +268,7 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
                 continue;
             }
             const size_t n = std::min(z - a, width - off);
-            std::memcpy(d + row * dpitch + off, pin + (a - base), n);
+            copy_nt(d + row * dpitch + off, pin + (a - base), n);
             a += n;
         }
     };
@@ -221,6 +296,7 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
         }
     }
     const hipError_t e2 = hipStreamSynchronize(stream);
+    if (trace()) fprintf(stderr, "[stage] d2h %zu B wait %.2f ms copy %.2f ms\n", bytes, t1 - t0, now_ms() - t1);
     return e != hipSuccess ? e : e2;
 }
 

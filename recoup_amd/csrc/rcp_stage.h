@@ -24,6 +24,10 @@ hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipSt
 hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
                         int device, hipStream_t stream);
 
+// RCP_TRACE set in the environment: stderr lines per staged copy / pipeline step (diagnostics)
+bool trace_on();
+double trace_ms();  // a steady clock in ms
+
 inline hipError_t stage_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t stream) {
     return stage_d2h_2d(dst, bytes, src, bytes, bytes, 1, device, stream);
 }

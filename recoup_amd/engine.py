@@ -454,6 +454,33 @@ class Shards:
             pass
 
 
+def profile_reads(samples, seqlengths, rows, bins, device=0, outs=None, strand_filter=None):
+    """rcp_profile_reads: several samples' host reads (each a tuple chrom, start, end, strand as
+    ReadSet takes them) over one region table; coordinate-sorted samples given as runs stream
+    through the GPU in row blocks, and sample k + 1 is uploaded while sample k is profiled and
+    copied down.  ``outs``: optional caller-owned (n_cols, n_rows) float64 arrays.
+    Returns [(matrix (n_rows, n_cols), validity bool)]."""
+    seql = np.ascontiguousarray(seqlengths, dtype=np.int64)
+    sf = -1 if strand_filter is None else STRAND.get(strand_filter, strand_filter)
+    descs = []
+    for chrom, start, end, strand in samples:
+        runs, wruns = _chrom_runs(chrom), _chrom_runs(end)
+        keep = [None if runs else np.ascontiguousarray(chrom, dtype=np.int32), np.ascontiguousarray(start, dtype=np.int32),
+                None if wruns else np.ascontiguousarray(end, dtype=np.int32), np.ascontiguousarray(strand, dtype=np.int8)]
+        descs.append(_reads_desc(int(keep[1].shape[0]), keep, runs, seql, int(device), 0, int(sf), wruns))
+    n = len(descs)
+    arr = (_lib.ReadsDesc * n)(*descs)
+    if outs is None:
+        outs = [np.zeros((bins.n_cols, rows.n_rows), np.float64) for _ in range(n)]
+    valids = [np.zeros(max(rows.n_rows, 1), np.uint8) for _ in range(n)]
+    po = (_lib._dp * n)(*[cptr(o, _lib._dp) for o in outs])
+    pv = (_lib._u8p * n)(*[cptr(v, _lib._u8p) for v in valids])
+    rd, bd = rows.desc(), bins.desc()
+    with torch.cuda.device(int(device)):
+        check(_lib.lib().rcp_profile_reads(arr, n, ctypes.byref(rd), ctypes.byref(bd), po, pv))
+    return [(o.T, v[:rows.n_rows].astype(bool)) for o, v in zip(outs, valids)]
+
+
 def profile_samples(readsets, rows, bins, inflight=0):
     """rcp_profile_samples: one region table over several samples' readsets (one GPU), passes
     kept ``inflight`` deep on separate HIP streams (0 = the library's default, 2), each matrix

@@ -461,13 +461,8 @@ def profile_matrix_from_reads(sh, input, mask, flank, binParams, ignore_strand=T
             rcp_free(sh, rs)
             input[i]["profile"] = res["profile"]
         return input
-    rsl = [rcp_read_set(sh, input[i]["ranges"], None, devices[:1], lv) for i in todo]
-    try:
-        res = sh.call("rcp_R_profile_samples", [rs.ptr for rs in rsl], *rcp_row_args(rows), *bin_args, np.int32(2),
-                      names)
-    finally:
-        for rs in rsl:
-            rcp_free(sh, rs)
+    read_args = [rcp_read_args(input[i]["ranges"], lv)[1] + [np.int32(-1)] for i in todo]
+    res = sh.call("rcp_R_profile_reads", read_args, np.int32(devices[0]), *rcp_row_args(rows), *bin_args, names)
     for k, i in enumerate(todo):
         input[i]["profile"] = res[k]["profile"]
     return input

@@ -249,3 +249,160 @@ def test_release_pool_then_rebuild(c1):
     assert rc == 0
     assert np.array_equal(before.view(np.int64), after.view(np.int64)) and np.array_equal(vb, va)
     assert L.rcp_release_pool(-1) != 0  # a device that does not exist
+
+
+@pytest.mark.parametrize("n_samples,nb,stranded", [(3, 1000, False), (4, 0, False), (2, 150, True), (1, 40, False)])
+def test_profile_reads_pipelined(gpu, n_samples, nb, stranded):
+    """rcp_profile_reads (sample k + 1 uploaded while sample k is profiled and copied down) gives
+    every sample the bits of its own readset + one-shot profile; reads as runs or per-read ends."""
+    from recoup_amd.engine import ReadSet, RowTable, profile_host, profile_reads
+    from tests.test_gpu_random import CHROM_LEN, make_reads, single_rows
+    rng = np.random.default_rng(140 + n_samples)
+    r0 = single_rows(rng, 500, 2000, edge=nb > 0)
+    rows = RowTable(r0.seg_off, r0.chrom, r0.start, r0.end, r0.strand, ignore_strand=not stranded)
+    bins = Bins([("whole", nb)]) if nb else Bins([("whole", 0, 2000)])
+    samples = [make_reads(rng, 50_000 + 7_000 * i, star_frac=0.1, widths=(100, 100) if i % 2 else (20, 400))
+               for i in range(n_samples)]
+    got = profile_reads(samples, CHROM_LEN, rows, bins)
+    for reads, (mat, valid) in zip(samples, got):
+        out = np.zeros((bins.n_cols, rows.n_rows))
+        v1 = np.zeros(rows.n_rows, np.uint8)
+        profile_host(ReadSet(*reads, CHROM_LEN, device=0), rows, bins, out, v1)
+        np.testing.assert_array_equal(valid, v1.astype(bool))
+        assert np.array_equal(mat.view(np.uint64), np.ascontiguousarray(out.T).view(np.uint64))
+
+
+def test_profile_rle_row_blocks(gpu):
+    """A long Rle list is profiled in row blocks through two streams (runs of one block up while
+    another block's rows come down): the same bits as per-row oracle means and as a short list."""
+    from recoup_amd.engine import profile_rle_arrays
+    rng = np.random.default_rng(99)
+    R = 6000  # 2.5 M runs: four row blocks
+    lens = rng.integers(1, 4, size=(R, 620)).astype(np.int32)
+    L = lens.sum(axis=1)
+    keep = L >= 1000
+    lens, L = lens[keep], L[keep]
+    R = len(L)
+    # trim every row to 1000 positions: drop runs past it and shorten the last one
+    runs, vals, off = [], [], [0]
+    for r in range(R):
+        c = np.cumsum(lens[r])
+        k = int(np.searchsorted(c, 1000))
+        x = lens[r][:k + 1].copy()
+        x[-1] -= c[k] - 1000
+        runs.append(x)
+        vals.append(rng.integers(0, 50, k + 1).astype(np.int32))
+        off.append(off[-1] + k + 1)
+    lengths, values = np.concatenate(runs), np.concatenate(vals)
+    run_off = np.array(off, np.int64)
+    nulls = (rng.random(R) < 0.05).astype(np.uint8)
+    bins = Bins([("whole", 100)])
+    mat, valid = profile_rle_arrays(run_off, lengths, values, nulls, bins)
+    assert run_off[-1] > (1 << 21)
+    dense = [np.repeat(v, ln) for v, ln in zip(vals, runs)]
+    want = np.array([np.zeros(100) if nulls[r] else dense[r].reshape(100, 10).mean(axis=1) for r in range(R)])
+    np.testing.assert_array_equal(valid, nulls == 0)
+    np.testing.assert_allclose(mat, want, rtol=1e-12, atol=0)
+    few = profile_rle_arrays(run_off[:101].copy(), lengths[:run_off[100]], values[:run_off[100]], nulls[:100], bins)
+    assert np.array_equal(few[0].view(np.uint64), np.ascontiguousarray(mat[:100]).view(np.uint64))
+
+
+def sorted_sample(rng, n, order=(2, 0, 1), width=100):
+    """n reads in (chromosome, start) order with the chromosomes in `order` (a BAM sorted by a
+    header whose order is not the seqlevel codes'): the per-read form and the runs form R's
+    seqnames(x) / width(x) Rle give (chromosome runs, one width run)."""
+    from tests.test_gpu_random import make_reads
+    chrom, start, end, strand = make_reads(rng, n, widths=(width, width), star_frac=0.1)
+    rank = np.argsort(np.array(order))
+    o = np.lexsort((start, rank[chrom]))
+    chrom, start, end, strand = chrom[o], start[o], end[o], strand[o]
+    cut = np.flatnonzero(np.diff(chrom)) + 1
+    cv = chrom[np.r_[0, cut]].astype(np.int32)
+    cl = np.diff(np.r_[0, cut, n]).astype(np.int64)
+    runs = ((cv, cl), start, (np.array([width], np.int32), np.array([n], np.int64)), strand)
+    return (chrom, start, end, strand), runs
+
+
+def sorted_rows(rng, R, order=(2, 0, 1), ignore_strand=True):
+    from recoup_amd.engine import RowTable
+    from tests.test_gpu_random import single_rows
+    r0 = single_rows(rng, R, 2000)
+    rank = np.argsort(np.array(order))
+    o = np.lexsort((r0.start, rank[r0.chrom]))
+    return RowTable(r0.seg_off, r0.chrom[o], r0.start[o], r0.end[o], r0.strand[o], ignore_strand=ignore_strand)
+
+
+def one_shot(reads, rows, bins, strand_filter=None):
+    from recoup_amd.engine import ReadSet, profile_host
+    from tests.test_gpu_random import CHROM_LEN
+    out = np.zeros((bins.n_cols, rows.n_rows))
+    v1 = np.zeros(rows.n_rows, np.uint8)
+    profile_host(ReadSet(*reads, CHROM_LEN, device=0, strand_filter=strand_filter), rows, bins, out, v1)
+    return np.ascontiguousarray(out.T), v1.astype(bool)
+
+
+def traced(capfd, fn):
+    import os
+    os.environ["RCP_TRACE"] = "1"
+    try:
+        res = fn()
+    finally:
+        del os.environ["RCP_TRACE"]
+    return res, [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[reads]")]
+
+
+@pytest.mark.parametrize("ignore_strand,strand_filter", [(True, None), (False, None), (False, "-")])
+def test_profile_reads_streamed(gpu, capfd, ignore_strand, strand_filter):
+    """A coordinate-sorted sample given as runs streams through the GPU in row blocks (each block
+    uploads only the slice of reads its rows need while the previous block's rows of the matrix
+    come down): the bits of the one-shot readset + profile, on merged and strand-split layouts and
+    with a strand filter."""
+    from recoup_amd.engine import Bins, profile_reads
+    from tests.test_gpu_random import CHROM_LEN
+    rng = np.random.default_rng(7 + ignore_strand)
+    reads, runs = sorted_sample(rng, 13_000_000)
+    rows = sorted_rows(rng, 4000, ignore_strand=ignore_strand)
+    bins = Bins([("whole", 100)])
+    want = one_shot(reads, rows, bins, strand_filter)
+    got, lines = traced(capfd, lambda: profile_reads([runs], CHROM_LEN, rows, bins, strand_filter=strand_filter))
+    assert sum("block" in ln for ln in lines) == 3, lines  # 13 M reads: three blocks
+    np.testing.assert_array_equal(got[0][1], want[1])
+    assert np.array_equal(got[0][0].view(np.uint64), want[0].view(np.uint64))
+
+
+def test_profile_reads_stream_fallbacks(gpu, capfd):
+    """Samples that cannot stream go through whole, with the same bits: a pair of reads out of
+    order inside a slice (found on the device after the first slice went up: the sample is redone
+    whole), rows in another order than the reads (slices would overlap), a chromosome split over
+    two runs.  One call holds all four samples; the first streams."""
+    from recoup_amd.engine import Bins, profile_reads
+    from tests.test_gpu_random import CHROM_LEN
+    rng = np.random.default_rng(21)
+    reads, runs = sorted_sample(rng, 4_600_000)
+    rows = sorted_rows(rng, 3000)
+    bins = Bins([("whole", 0, 2000)])
+    n = len(reads[1])
+    i = n // 5  # inside the first slice, one chromosome
+    assert reads[1][i] < reads[1][i + 1] and reads[0][i] == reads[0][i + 1]
+    bad_start = reads[1].copy()
+    bad_start[[i, i + 1]] = bad_start[[i + 1, i]]
+    bad = (runs[0], bad_start, runs[2], runs[3])
+    bad_reads = (reads[0], bad_start, bad_start + 99, reads[3])
+    cv, cl = runs[0]
+    split = ((np.r_[cv[:1], cv]).astype(np.int32), np.r_[cl[:1] // 2, cl[:1] - cl[:1] // 2, cl[1:]].astype(np.int64))
+    two_runs = (split, runs[1], runs[2], runs[3])
+    got, lines = traced(capfd, lambda: profile_reads([runs, bad, two_runs], CHROM_LEN, rows, bins))
+    assert sum("sample 0 block" in ln for ln in lines) == 2, lines
+    assert any("sample 1 rows [0, 3000)" in ln for ln in lines), lines
+    assert any("sample 2 rows [0, 3000)" in ln for ln in lines), lines
+    for (mat, valid), r in zip(got, (reads, bad_reads, reads)):
+        m1, v1 = one_shot(r, rows, bins)
+        np.testing.assert_array_equal(valid, v1)
+        assert np.array_equal(mat.view(np.uint64), m1.view(np.uint64))
+    from recoup_amd.engine import RowTable
+    perm = rng.permutation(rows.n_rows)
+    shuffled = RowTable(rows.seg_off, rows.chrom[perm], rows.start[perm], rows.end[perm], rows.strand[perm])
+    got, lines = traced(capfd, lambda: profile_reads([runs], CHROM_LEN, shuffled, bins))
+    assert not any("block" in ln for ln in lines), lines
+    m1, v1 = one_shot(reads, shuffled, bins)
+    assert np.array_equal(got[0][0].view(np.uint64), m1.view(np.uint64))

@@ -215,7 +215,7 @@ class _devices:
 
 
 def test_profile_from_reads(sh, c1):
-    """profileMatrixFromReads: every sample in one rcp_R_profile_samples call, and the rows
+    """profileMatrixFromReads: every sample in one rcp_R_profile_reads call, and the rows
     split over two device slots (rcp_R_shards + rcp_R_shards_profile) bit-equal to it."""
     from recoup_amd.granges import getRegionalRanges
     mask = getRegionalRanges(c1["genes"], "tss", (2000, 2000))

@@ -103,8 +103,11 @@ typedef struct {
  * the per-(chrom, strand) stream offsets plus the prefix-max-of-end search index. */
 RCP_API int rcp_readset_create(const rcp_reads_desc* desc, void* hip_stream, rcp_readset** out);
 RCP_API int rcp_readset_destroy(rcp_readset* rs);
-/* The library's device memory pool (readset arrays, build and encode temporaries) keeps up to
- * 64 GB of freed memory mapped for the next build; this returns what no live object uses. */
+/* The library's device memory (readset and plan arrays, build and encode temporaries) comes from
+ * a caching allocator: freed blocks are kept, keyed by size class, for the next build of that
+ * size (no hipMalloc / hipFree -- each a device-wide synchronisation, and now and then a
+ * multi-second stall on the box -- once warm).  This returns every cached block to the runtime;
+ * blocks are also released when a device allocation fails. */
 RCP_API int rcp_release_pool(int device);
 /* n_reads kept, and stream offsets (host array of n_chrom*3+1, may be NULL) of the strand-split
  * layout.  A readset made from host arrays builds that layout at its first use -- here when
@@ -319,10 +322,14 @@ RCP_API int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_samples,
 /* profileMatrix straight from the reads of several samples over one region table, reads on the
  * host (R's vectors): samples[k] describes sample k's reads (all for one device, host arrays),
  * outs[k] its R column-major n_rows x n_cols matrix (row_valid may be NULL or hold per-sample
- * pointers).  Sample k + 1's readset is uploaded and built while sample k's pass runs and its
- * matrix is copied down -- both PCIe directions at once (the one-shot rcp_readset_create +
- * rcp_profile of each sample in turn uses one direction at a time); at most two samples' reads
- * are on the device.  Bit-identical to rcp_profile per sample. */
+ * pointers).  A sample of >= 4 M coordinate-sorted reads given as chromosome runs (each
+ * chromosome one run) and width runs -- a sorted BAM's GAlignments -- over >= 2048 rows streams
+ * through the GPU in row blocks: block b's slice of the reads (found by bisection of the host
+ * starts; the slices' order is checked on the device and a sample that proves unsorted is redone
+ * whole) goes up while block b - 1's rows of the matrix come down; any other sample goes up whole
+ * while the previous one's matrix comes down.  Both PCIe directions at once (the one-shot
+ * rcp_readset_create + rcp_profile uses one direction at a time); at most three readsets are on
+ * the device.  Bit-identical to rcp_profile per sample. */
 RCP_API int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_samples, const rcp_rows_desc* rows,
                               const rcp_bins_desc* bins, double* const* outs, uint8_t* const* row_valid);
 

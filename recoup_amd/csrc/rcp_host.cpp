@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <condition_variable>
 #include <deque>
 #include <cstdarg>
@@ -69,47 +70,139 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
-// Stream-ordered temporaries from the library's own memory pool on each device (not the
-// process-wide default pool, whose settings other users of hipMallocAsync in the process would
-// inherit), which keeps up to 64 GB of freed memory mapped: the multi-GB sort and scan buffers
-// of a readset build cost a hipMalloc / hipFree pair each, and on the box those took 0.3-6 s
+// The library's device memory: a caching allocator per device.  A readset build's multi-GB sort,
+// scan and index buffers cost a hipMalloc / hipFree pair each, and on the box those took 0.3-6 s
 // now and then (C5, 500 M reads: a 0.19 s build became 1.4 s and 7.4 s, tools/diag_readset.py);
-// from the pool the same memory is handed out again.  Allocated and freed on the stream that
-// uses it, so the reuse is ordered after the last kernel touching it.  rcp_release_pool()
-// returns the cached memory (e.g. to torch's caching allocator in the same process).
-std::mutex g_pool_mu;
-std::map<int, hipMemPool_t> g_pools;
+// a hipMemPool did the same once its size crossed some runtime heuristic (a 1.1 s destroy per
+// rep, then a 6 s create: profiles/r05/readset_c5_pool.log).  Here a freed block goes into a free
+// list keyed by its size class (8 classes per power of two, so same-sized builds -- repeated
+// samples, a streamed sample's row blocks -- get the same blocks back) with an event recorded on
+// the stream that freed it; the next allocation of that class on any stream waits for the event
+// (stream-ordered, no host synchronisation) and takes the block.  hipMalloc runs only when no
+// block of the class is free; device memory goes back to the runtime at rcp_release_pool() or
+// when a hipMalloc fails (then every cached block is released and the allocation retried).
+namespace {
 
-hipError_t device_pool(int dev, hipMemPool_t* out) {
-    std::lock_guard<std::mutex> lock(g_pool_mu);
-    auto it = g_pools.find(dev);
-    if (it != g_pools.end()) {
-        *out = it->second;
-        return hipSuccess;
-    }
-    hipMemPoolProps props{};
-    props.allocType = hipMemAllocationTypePinned;
-    props.handleTypes = hipMemHandleTypeNone;
-    props.location.type = hipMemLocationTypeDevice;
-    props.location.id = dev;
-    hipMemPool_t pool;
-    hipError_t e = hipMemPoolCreate(&pool, &props);
-    if (e != hipSuccess) return e;
-    uint64_t thr = uint64_t(64) << 30;  // freed memory kept mapped (C5's build peaks near 40 GB)
-    e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-    if (e != hipSuccess) return e;
-    g_pools[dev] = pool;
-    *out = pool;
-    return hipSuccess;
+struct Cached {
+    void* p;
+    hipEvent_t ev;
+};
+
+struct DevCache {
+    std::multimap<size_t, Cached> free;  // size class -> block
+    std::vector<hipEvent_t> spare;       // recycled events (made on this device)
+};
+
+// one lock over every device's lists (allocations are few: a handful per build or plan)
+std::mutex g_cache_mu;
+std::map<void*, std::pair<int, size_t>> g_live;  // block -> (device, size class)
+
+DevCache& dev_cache(int dev) {
+    static DevCache* c = new DevCache[64];  // process lifetime (freed by the OS at exit)
+    return c[dev & 63];
 }
 
+size_t size_class(size_t n) {
+    if (n <= 4096) return 4096;
+    const int lg = 63 - __builtin_clzll(n - 1);  // 2^lg < n <= 2^(lg + 1)
+    const size_t step = (size_t(1) << lg) / 8;
+    return (n + step - 1) / step * step;
+}
+
+// return every cached block of the device to the runtime (after its last user's work)
+void release_cached(int dev) {
+    DevCache& c = dev_cache(dev);
+    std::multimap<size_t, Cached> blocks;
+    std::vector<hipEvent_t> spare;
+    {
+        std::lock_guard<std::mutex> lock(g_cache_mu);
+        blocks.swap(c.free);
+        spare.swap(c.spare);
+    }
+    DeviceGuard g(dev);
+    for (auto& kv : blocks) {
+        if (kv.second.ev) (void)hipEventSynchronize(kv.second.ev);
+        (void)hipFree(kv.second.p);
+        if (kv.second.ev) (void)hipEventDestroy(kv.second.ev);
+    }
+    for (hipEvent_t e : spare) (void)hipEventDestroy(e);
+}
+
+}  // namespace
+
 hipError_t pool_alloc(void** p, size_t n, hipStream_t s) {
+    *p = nullptr;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    hipMemPool_t pool;
-    if ((e = device_pool(dev, &pool)) != hipSuccess) return e;
-    return hipMallocFromPoolAsync(p, n, pool, s);
+    DevCache& c = dev_cache(dev);
+    const size_t cls = size_class(n);
+    Cached blk{nullptr, nullptr};
+    {
+        std::lock_guard<std::mutex> lock(g_cache_mu);
+        auto it = c.free.find(cls);
+        if (it != c.free.end()) {
+            blk = it->second;
+            c.free.erase(it);
+        }
+    }
+    if (blk.p) {
+        // after the previous user's last work on the block (no event: it was idle when freed)
+        e = blk.ev ? hipStreamWaitEvent(s, blk.ev, 0) : hipSuccess;
+        std::lock_guard<std::mutex> lock(g_cache_mu);
+        if (e != hipSuccess) {
+            c.free.emplace(cls, blk);
+            return e;
+        }
+        if (blk.ev) c.spare.push_back(blk.ev);
+        g_live[blk.p] = {dev, cls};
+        *p = blk.p;
+        return hipSuccess;
+    }
+    e = hipMalloc(p, cls);
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        release_cached(dev);
+        e = hipMalloc(p, cls);
+    }
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return e;
+    }
+    std::lock_guard<std::mutex> lock(g_cache_mu);
+    g_live[*p] = {dev, cls};
+    return hipSuccess;
+}
+
+void pool_free(void* p, hipStream_t s) {
+    if (!p) return;
+    int dev = 0;
+    size_t cls = 0;
+    hipEvent_t ev = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_cache_mu);
+        auto it = g_live.find(p);
+        if (it == g_live.end()) return;  // (not ours)
+        dev = it->second.first;
+        cls = it->second.second;
+        g_live.erase(it);
+        DevCache& c = dev_cache(dev);
+        if (!c.spare.empty()) {
+            ev = c.spare.back();
+            c.spare.pop_back();
+        }
+    }
+    DevCache& c = dev_cache(dev);
+    DeviceGuard g(dev);  // (s is a stream of the block's device, or the null stream)
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+    if (!ev || hipEventRecord(ev, s) != hipSuccess) {
+        // no event: the block goes back only after everything queued on the device so far
+        (void)hipDeviceSynchronize();
+        if (ev) (void)hipEventDestroy(ev);
+        ev = nullptr;
+    }
+    std::lock_guard<std::mutex> lock(g_cache_mu);
+    c.free.emplace(cls, Cached{p, ev});
 }
 
 int check_device(int dev) {
@@ -153,23 +246,19 @@ void wave_geometry(int32_t positions, int32_t* words, int32_t* capacity) {
 // =====================================================================================
 // readset
 // =====================================================================================
-// tools-only phase timing of rcp_plan_create_ex (build with -DRCP_PLAN_TIMING=1)
-#if RCP_PLAN_TIMING
-#include <chrono>
+// phase timing of readset builds and plan creation: stderr lines under RCP_TRACE (rcp_stage.h)
 struct PlanTimer {
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), t = t0;
+    bool on = rcp::trace_on();
+    double t = on ? rcp::trace_ms() : 0.0;
     void mark(const char* what) {
-        const auto n = std::chrono::steady_clock::now();
-        fprintf(stderr, "[plan] %-14s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        if (!on) return;
+        const double n = rcp::trace_ms();
+        fprintf(stderr, "[plan] %-14s %8.3f ms\n", what, n - t);
         t = n;
     }
 };
 #define PLAN_MARK(what) ptimer.mark(what)
-#define LAYOUT_MARK(what) (void)hipStreamSynchronize(s), ltimer.mark(what)
-#else
-#define PLAN_MARK(what) ((void)0)
-#define LAYOUT_MARK(what) ((void)0)
-#endif
+#define LAYOUT_MARK(what) ((void)(ltimer.on && hipStreamSynchronize(s) == hipSuccess), ltimer.mark(what))
 
 int rcp_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
 
@@ -201,9 +290,7 @@ int build_layout(const rcp_readset* rs, const rcp_reads_desc* d, const int32_t* 
                  int64_t* kept_out, bool directory = true) {
     const int64_t n = d->n;
     const int64_t n_streams = (int64_t)d->n_chrom * 3;  // + 1 sentinel stream (dropped reads)
-#if RCP_PLAN_TIMING
     PlanTimer ltimer;
-#endif
     PoolBuf keys(s), keys2(s), vals(s), vals2(s), scan_in(s), scan_out(s), temp(s);
     HIP_TRY(keys.alloc(8 * std::max<int64_t>(n, 1)));
     HIP_TRY(keys2.alloc(8 * std::max<int64_t>(n, 1)));
@@ -427,12 +514,10 @@ int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_reads
     if (d->seqlen)
         for (int c = 0; c < d->n_chrom; ++c) rs->seqlen[c] = d->seqlen[c] < 0 ? -1 : d->seqlen[c];
     const int64_t n = d->n;
-#if RCP_PLAN_TIMING
     PlanTimer ptimer;
-#endif
 
     // inputs on device
-    DevBuf in_chrom, in_start, in_end, in_strand, runs, wruns;
+    PoolBuf in_chrom(s), in_start(s), in_end(s), in_strand(s), runs(s), wruns(s);
     const int32_t *pc = d->chrom, *ps = d->start, *pe = d->end;
     const int8_t* pst = d->strand;
     if (!d->chrom && n > 0) {
@@ -517,16 +602,16 @@ int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_reads
         PLAN_MARK("stranded layout");
     } else if (!d->on_device && (layouts & kLayKeep)) {
         // keep the uploaded copies for a later stranded layout (ensure_stranded)
-        rs->keep_chrom = std::move(in_chrom);
-        rs->keep_start = std::move(in_start);
-        rs->keep_end = std::move(in_end);
-        rs->keep_strand = std::move(in_strand);
+        rs->keep_chrom.adopt(in_chrom);
+        rs->keep_start.adopt(in_start);
+        rs->keep_end.adopt(in_end);
+        rs->keep_strand.adopt(in_strand);
         rs->kc = pc;
         rs->ks = ps;
         rs->ke = pe;
         rs->kst = pst;
     }
-    HIP_TRY(rs->d_seqlen.alloc(8 * d->n_chrom));
+    HIP_TRY(rs->d_seqlen.alloc(8 * d->n_chrom, s));
     HIP_TRY(hipMemcpyAsync(rs->d_seqlen.p, rs->seqlen.data(), 8 * d->n_chrom, hipMemcpyHostToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));
     *out = rs.release();
@@ -560,15 +645,7 @@ extern "C" int rcp_release_pool(int device) {
     if (rc) return rc;
     DeviceGuard g(device);
     HIP_TRY(g.err);
-    hipMemPool_t pool;
-    {
-        std::lock_guard<std::mutex> lock(g_pool_mu);
-        auto it = g_pools.find(device);
-        if (it == g_pools.end()) return RCP_OK;
-        pool = it->second;
-    }
-    HIP_TRY(hipDeviceSynchronize());  // frees still queued on streams land first
-    HIP_TRY(hipMemPoolTrimTo(pool, 0));
+    release_cached(device);
     return RCP_OK;
     RCP_CATCH
 }
@@ -594,6 +671,19 @@ namespace {
 
 // A new execution: alternate the status sets (RcpPlanDev::status / status_prev); the locate
 // kernel clears the previous execution's heavy slots and zeroes its set.
+// after an execution's launches on s: the plan's arrays stay allocated until this point (rcp_plan)
+int end_exec(rcp_plan* plan, hipStream_t s) {
+    if (plan->n_streams == 0) {
+        plan->last = s;
+        plan->n_streams = 1;
+    } else if (plan->last != s) {
+        plan->n_streams = 2;
+    }
+    if (!plan->ev_done) HIP_TRY(hipEventCreateWithFlags(&plan->ev_done, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(plan->ev_done, s));
+    return RCP_OK;
+}
+
 void begin_exec(rcp_plan* plan) {
     plan->epoch ^= 1;
     plan->dev.status = plan->status_sets + RCP_STATUS_WORDS * plan->epoch;
@@ -778,9 +868,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     DeviceGuard g(rs->device);
     HIP_TRY(g.err);
 
-#if RCP_PLAN_TIMING
     PlanTimer ptimer;
-#endif
     if (!rows->ignore_strand) {  // findOverlaps with strand compatibility: the stranded layout
         const int rc0 = ensure_stranded(rs);
         if (rc0) return rc0;
@@ -1176,7 +1264,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     }
     const size_t o_spl = blob.add(spl_tb);
     PLAN_MARK("tables (host)");
-    HIP_TRY(plan->tables.alloc(blob.total));
+    HIP_TRY(plan->tables.alloc(blob.total, nullptr));
     HIP_TRY(blob.upload(plan->tables.p, rs->device, nullptr));
     PLAN_MARK("tables upload");
     char* base = plan->tables.as<char>();
@@ -1209,7 +1297,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     const size_t w_order = al(w_crange + (keep_crange ? sizeof(uint2) * 3 * (size_t)P.n_chunks_total * Rw : 0));
     const size_t w_status = al(w_order + 4 * (size_t)RCP_LPT_CLASSES * (size_t)P.lpt_cap);
     static_assert(2 * RCP_STATUS_WORDS * 4 <= 256, "two status sets");
-    HIP_TRY(plan->work.alloc(w_status + 256));
+    HIP_TRY(plan->work.alloc(w_status + 256, nullptr));
     PLAN_MARK("work alloc");
     char* wb = plan->work.as<char>();
     P.ncand = reinterpret_cast<uint32_t*>(wb + w_ncand);
@@ -1252,7 +1340,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     const int32_t n_interp = (int32_t)B.interp_row.size();
     // x (L+1) | b, c, d (3 (L+1)) for the spline, or the neighborhood fill's n pre-fill values
     P.interp_stride = (max_interp_len + 1) + std::max(max_interp_bins, 3 * (max_interp_len + 1)) + 8;
-    if (n_interp) HIP_TRY(plan->scratch.alloc(8 * (size_t)n_interp * P.interp_stride));
+    if (n_interp) HIP_TRY(plan->scratch.alloc(8 * (size_t)n_interp * P.interp_stride, nullptr));
 
     const ReadLayout& RL = rows->ignore_strand ? rs->merged : rs->stranded;
     P.se = RL.se.as<int2>();
@@ -1308,7 +1396,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.rm32 = nullptr;
     P.rinfo = nullptr;
     if (P.lean == 3 && R > 0 && P.n_cols > 0) {
-        HIP_TRY(plan->rm.alloc(4 * (size_t)R * (size_t)P.n_cols + 8 * (size_t)R * RCP_MAX_PARTS));
+        HIP_TRY(plan->rm.alloc(4 * (size_t)R * (size_t)P.n_cols + 8 * (size_t)R * RCP_MAX_PARTS, nullptr));
         P.rinfo = plan->rm.as<int2>();
         P.rm32 = reinterpret_cast<uint32_t*>(P.rinfo + (size_t)R * RCP_MAX_PARTS);
     }
@@ -1335,11 +1423,11 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     if (P.lean == 4) plan->grid = (plan->grid + 7) / 8 * 8;
     if (plan->lds > 160 * 1024) return fail(RCP_EUNSUPPORTED, "plan needs %zu B of LDS", plan->lds);
     PLAN_MARK("rest");
-    HIP_TRY(hipMemset(plan->work.p, 0, plan->work.bytes));
-#if RCP_PLAN_TIMING
-    HIP_TRY(hipDeviceSynchronize());
+    // cleared before the plan is returned: its executions run on the caller's (non-blocking)
+    // streams, which do not wait for the null stream
+    HIP_TRY(hipMemsetAsync(plan->work.p, 0, plan->work.bytes, nullptr));
+    HIP_TRY(hipStreamSynchronize(nullptr));
     PLAN_MARK("memset");
-#endif
     *out = plan.release();
     return RCP_OK;
     RCP_CATCH
@@ -1391,7 +1479,7 @@ extern "C" int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_str
     HIP_TRY(rcp_launch_locate(&Q, s));
     Q.heavy_threshold = 0;  // no slices: the heavy launch only zeroes the previous status set
     HIP_TRY(rcp_launch_heavy(&Q, kHeavyGrid, s));
-    return RCP_OK;
+    return end_exec(plan, s);
     RCP_CATCH
 }
 
@@ -1437,7 +1525,7 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
     }
     if (fork) HIP_TRY(hipStreamWaitEvent(s, plan->ev_join, 0));
     else if (stages & RCP_STAGE_INTERP) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
-    return RCP_OK;
+    return end_exec(plan, s);
     RCP_CATCH
 }
 
@@ -1581,8 +1669,21 @@ bool stream_cut(const rcp_reads_desc& d, const rcp_rows_desc* rows, StreamCut* c
     }
     if (pos != n) return false;
     const int nb = (int)std::min<int64_t>(8, std::max<int64_t>(2, n >> 22));  // >= 4 M reads a block
-    cut->rows.resize(nb + 1);
-    for (int b = 0; b <= nb; ++b) cut->rows[b] = (int32_t)((int64_t)R * b / nb);
+    // the first blocks smaller (a quarter, three quarters of the others): the first rows of the
+    // matrix start down sooner, and the download -- the longer direction -- runs longer
+    std::vector<double> w(nb, 1.0);
+    if (nb >= 4) {
+        w[0] = 0.25;
+        w[1] = 0.75;
+    }
+    double wsum = 0.0;
+    for (double x : w) wsum += x;
+    cut->rows.assign(nb + 1, 0);
+    double acc = 0.0;
+    for (int b = 0; b < nb; ++b) {
+        acc += w[b];
+        cut->rows[b + 1] = b + 1 == nb ? R : (int32_t)std::min<double>(R, std::floor(R * acc / wsum));
+    }
     std::vector<int64_t> L(nb, n), H(nb, 0), smin(d.n_chrom), emax(d.n_chrom);
     std::vector<char> touched(d.n_chrom, 0);
     std::vector<int32_t> list;
@@ -1660,50 +1761,108 @@ extern "C" int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_sample
     // the one layout the row table searches, built from the uploaded copies right away
     const int layout = rows->ignore_strand ? kLayMerged : kLayStranded;
     // Work items: a sample of sorted reads is cut into row blocks, each with the slice of the
-    // reads it needs (stream_cut); any other sample is one item.  One uploader thread builds the
-    // items' readsets in order (H2D through the upload staging buffers, sort, index); two profiler
-    // threads take them in order, each planning + running its block's pass and copying the block's
-    // rows of the matrix down (the download staging buffers): while one copies down, the other
-    // plans and runs, and the uploader sends the next slice up -- both PCIe directions busy.  At
-    // most three readsets exist at once.  A sample whose slices prove unsorted on the device is
-    // redone as one item after its blocks in flight have finished.
+    // reads it needs (stream_cut); any other sample is one item.  Four host threads:
+    //   uploader  -- copies each block's slice of starts and strands up (the upload staging
+    //                buffers) into device buffers, at most two slices ahead of the builder;
+    //   builder   -- builds each block's readset from its device slice (order check, sort, index);
+    //                a whole item's readset straight from the host arrays;
+    //   profilers -- two, taking the built items in order: plan, pass, and the block's rows of
+    //                the matrix copied down (the download staging buffers) -- while one copies
+    //                down, the other plans and runs.
+    // Both PCIe directions stay busy, and at most three readsets exist at once.  A sample whose
+    // slices prove unsorted on the device is redone as one item after its blocks in flight.
+    struct Staged {
+        int sample;
+        int32_t r0, r1;
+        bool whole;
+        ReadSlice sl;
+        void* d_start;
+        void* d_strand;
+    };
     struct Item {
         int sample;
         int32_t r0, r1;
         bool redo;
         rcp_readset* rs;
     };
+    std::deque<Staged> staged;
+    int n_staged = 0;  // slices up, not yet taken by the builder
     std::deque<Item> items;
     size_t next = 0;
     int alive = 0;
-    bool uploaded = false, abort = false;
+    bool up_done = false, built_done = false, abort = false;
     std::vector<char> poisoned(n_samples, 0);
     std::vector<int> active(n_samples, 0);
     std::mutex mu;
     std::condition_variable cv;
     const bool tr = rcp::trace_on();
     const double t0 = tr ? rcp::trace_ms() : 0.0;
-    const int r2 = run_per_device(3, [&](int role) -> int {
+    auto set_abort = [&] {
+        {
+            std::lock_guard<std::mutex> lock(mu);
+            abort = true;
+        }
+        cv.notify_all();
+    };
+    const int r2 = run_per_device(4, [&](int role) -> int {
         DeviceGuard g(dev);
         HIP_TRY(g.err);
         hipStream_t s = nullptr;
         HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(s, hipStreamDestroy);
         if (role == 0) {  // uploader
-            auto build = [&](const rcp_reads_desc& d, int lay, rcp_readset** out) -> int {
+            auto push = [&](Staged&& x) {
                 {
-                    std::unique_lock<std::mutex> lock(mu);
-                    cv.wait(lock, [&] { return abort || alive < 3; });
-                    if (abort) return -1000;
-                    ++alive;
-                }
-                const int e = readset_build(&d, s, lay, out);
-                if (e) {
                     std::lock_guard<std::mutex> lock(mu);
-                    --alive;
+                    if (!x.whole) ++n_staged;
+                    staged.push_back(std::move(x));
                 }
-                return e;
+                cv.notify_all();
             };
+            for (int k = 0; k < n_samples; ++k) {
+                StreamCut cut;
+                if (!stream_cut(samples[k], rows, &cut)) {
+                    push(Staged{k, 0, R, true, {}, nullptr, nullptr});
+                    continue;
+                }
+                for (size_t b = 0; b + 1 < cut.rows.size(); ++b) {
+                    {
+                        std::unique_lock<std::mutex> lock(mu);
+                        cv.wait(lock, [&] { return abort || n_staged < 2 || poisoned[k]; });
+                        if (abort) return (int)RCP_OK;
+                        if (poisoned[k]) break;
+                    }
+                    Staged x{k, cut.rows[b], cut.rows[b + 1], false, {}, nullptr, nullptr};
+                    slice_reads(&samples[k], cut.a[b], cut.z[b], &x.sl);
+                    const int64_t n = x.sl.d.n;
+                    const double tb = tr ? rcp::trace_ms() : 0.0;
+                    hipError_t e = hipSuccess;
+                    if (n > 0) {
+                        e = pool_alloc(&x.d_start, 4 * (size_t)n, s);
+                        if (e == hipSuccess) e = pool_alloc(&x.d_strand, (size_t)n, s);
+                        if (e == hipSuccess) e = rcp::stage_h2d(x.d_start, x.sl.d.start, 4 * (size_t)n, dev, s);
+                        if (e == hipSuccess) e = rcp::stage_h2d(x.d_strand, x.sl.d.strand, (size_t)n, dev, s);
+                    }
+                    if (tr)
+                        fprintf(stderr, "[reads] sample %d block %zu: %lld reads up %.2f ms (at %.2f)\n", k, b,
+                                (long long)n, rcp::trace_ms() - tb, tb - t0);
+                    if (e != hipSuccess) {
+                        pool_free(x.d_start, s);
+                        pool_free(x.d_strand, s);
+                        set_abort();
+                        HIP_TRY(e);
+                    }
+                    push(std::move(x));
+                }
+            }
+            {
+                std::lock_guard<std::mutex> lock(mu);
+                up_done = true;
+            }
+            cv.notify_all();
+            return (int)RCP_OK;
+        }
+        if (role == 1) {  // builder
             auto publish = [&](const Item& it) {
                 {
                     std::lock_guard<std::mutex> lock(mu);
@@ -1711,49 +1870,94 @@ extern "C" int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_sample
                 }
                 cv.notify_all();
             };
-            auto failed = [&](int e) {
+            auto take_slot = [&]() {
+                std::unique_lock<std::mutex> lock(mu);
+                cv.wait(lock, [&] { return abort || alive < 3; });
+                if (abort) return false;
+                ++alive;
+                return true;
+            };
+            auto drop_slot = [&] {
+                std::lock_guard<std::mutex> lock(mu);
+                --alive;
+            };
+            for (;;) {
+                Staged x;
                 {
-                    std::lock_guard<std::mutex> lock(mu);
-                    abort = true;
+                    std::unique_lock<std::mutex> lock(mu);
+                    cv.wait(lock, [&] { return abort || !staged.empty() || up_done; });
+                    if (abort) return (int)RCP_OK;
+                    if (staged.empty()) {
+                        built_done = true;
+                        break;
+                    }
+                    x = std::move(staged.front());
+                    staged.pop_front();
+                    if (!x.whole) --n_staged;
                 }
                 cv.notify_all();
-                return e == -1000 ? (int)RCP_OK : e;
-            };
-            for (int k = 0; k < n_samples; ++k) {
-                StreamCut cut;
-                bool redo = false;
-                if (stream_cut(samples[k], rows, &cut)) {
-                    for (size_t b = 0; b + 1 < cut.rows.size(); ++b) {
-                        ReadSlice sl;
-                        slice_reads(&samples[k], cut.a[b], cut.z[b], &sl);
-                        rcp_readset* r = nullptr;
-                        const double tb = tr ? rcp::trace_ms() : 0.0;
-                        const int e = build(sl.d, layout | kLayCheckOrder, &r);
-                        if (tr)
-                            fprintf(stderr, "[reads] sample %d block %zu: %lld reads up + built %.2f ms (at %.2f)\n", k, b,
-                                    (long long)sl.d.n, rcp::trace_ms() - tb, tb - t0);
-                        if (e == kNotInOrder) {
-                            redo = true;
+                const int k = x.sample;
+                bool whole = x.whole;
+                if (!whole) {
+                    bool skip;
+                    {
+                        std::lock_guard<std::mutex> lock(mu);
+                        skip = poisoned[k] != 0;
+                    }
+                    if (skip) {  // a slice of a sample being redone whole
+                        pool_free(x.d_start, s);
+                        pool_free(x.d_strand, s);
+                        continue;
+                    }
+                    if (!take_slot()) {
+                        pool_free(x.d_start, s);
+                        pool_free(x.d_strand, s);
+                        return (int)RCP_OK;
+                    }
+                    rcp_reads_desc d = x.sl.d;
+                    d.on_device = 1;
+                    d.start = static_cast<const int32_t*>(x.d_start);
+                    d.strand = static_cast<const int8_t*>(x.d_strand);
+                    rcp_readset* r = nullptr;
+                    const double tb = tr ? rcp::trace_ms() : 0.0;
+                    const int e = readset_build(&d, s, layout | kLayCheckOrder, &r);
+                    pool_free(x.d_start, s);
+                    pool_free(x.d_strand, s);
+                    if (tr)
+                        fprintf(stderr, "[reads] sample %d rows [%d, %d): built %.2f ms (at %.2f)\n", k, x.r0, x.r1,
+                                rcp::trace_ms() - tb, tb - t0);
+                    if (e == kNotInOrder) {
+                        drop_slot();
+                        {
                             std::lock_guard<std::mutex> lock(mu);
                             poisoned[k] = 1;
-                            break;
                         }
-                        if (e) return failed(e);
-                        publish(Item{k, cut.rows[b], cut.rows[b + 1], false, r});
+                        cv.notify_all();
+                        whole = true;
+                    } else if (e) {
+                        drop_slot();
+                        set_abort();
+                        return e;
+                    } else {
+                        publish(Item{k, x.r0, x.r1, false, r});
                     }
-                } else {
-                    redo = true;
                 }
-                if (redo) {
+                if (whole) {
+                    if (!take_slot()) return (int)RCP_OK;
                     rcp_readset* r = nullptr;
-                    const int e = build(samples[k], layout, &r);
-                    if (e) return failed(e);
-                    publish(Item{k, 0, R, poisoned[k] != 0, r});
+                    const int e = readset_build(&samples[k], s, layout, &r);
+                    if (e) {
+                        drop_slot();
+                        set_abort();
+                        return e;
+                    }
+                    bool redo;
+                    {
+                        std::lock_guard<std::mutex> lock(mu);
+                        redo = poisoned[k] != 0;
+                    }
+                    publish(Item{k, 0, R, redo, r});
                 }
-            }
-            {
-                std::lock_guard<std::mutex> lock(mu);
-                uploaded = true;
             }
             cv.notify_all();
             return (int)RCP_OK;
@@ -1762,7 +1966,7 @@ extern "C" int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_sample
             Item it{};
             {
                 std::unique_lock<std::mutex> lock(mu);
-                cv.wait(lock, [&] { return abort || next < items.size() || uploaded; });
+                cv.wait(lock, [&] { return abort || next < items.size() || built_done; });
                 if (abort || next >= items.size()) return (int)RCP_OK;
                 it = items[next++];
                 if (poisoned[it.sample] && !it.redo) {  // a block of a sample being redone whole
@@ -1798,6 +2002,10 @@ extern "C" int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_sample
             if (e) return e;
         }
     });
+    for (Staged& x : staged) {  // (left behind by a failure: slices not built)
+        pool_free(x.d_start, nullptr);
+        pool_free(x.d_strand, nullptr);
+    }
     // (left behind by a failure: items not taken)
     for (size_t i = next; i < items.size(); ++i) rcp_readset_destroy(items[i].rs);
     return r2;
@@ -1884,6 +2092,8 @@ namespace rcpi {
 
 int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bins_desc* bins, double* out,
                   int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream) {
+    const bool tr = rcp::trace_on();
+    const double t0 = tr ? rcp::trace_ms() : 0.0;
     rcp_plan* plan = nullptr;
     rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, 0, {0, 0}};
     int e = rcp_plan_create_ex(rs, sub, bins, &opts, &plan);
@@ -1892,6 +2102,7 @@ int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bin
     DeviceGuard g(rs->device);
     HIP_TRY(g.err);
     if (n_cols) *n_cols = plan->n_cols;
+    const double t1 = tr ? rcp::trace_ms() : 0.0;
     hipStream_t s = stream;
     if (!stream) HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(
@@ -1906,10 +2117,14 @@ int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bin
     if (e) return e;
     e = rcp_plan_status(plan, s);
     if (e) return e;
+    const double t2 = tr ? rcp::trace_ms() : 0.0;
     // this block's rows of every column of the caller's R matrix
     if (out && plan->n_cols && plan->n_rows)
         HIP_TRY(rcp::stage_d2h_2d(out + r0, 8 * (size_t)n_rows_total, d_out.p, 8 * (size_t)plan->out_ld,
                                   8 * (size_t)plan->n_rows, (size_t)plan->n_cols, rs->device, s));
+    if (tr)
+        fprintf(stderr, "[block] rows [%d, %d): plan %.2f ms, pass %.2f ms, down %.2f ms\n", r0, r0 + plan->n_rows,
+                t1 - t0, t2 - t1, rcp::trace_ms() - t2);
     if (row_valid && plan->n_rows) {
         HIP_TRY(hipMemcpyAsync(row_valid + r0, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -2012,7 +2227,7 @@ int calc_coverage_dev(rcp_plan* plan, const int64_t* d_off, int32_t* d_cov, uint
     HIP_TRY(rcp_launch_locate(&P, s));
     HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
-    return RCP_OK;
+    return end_exec(plan, s);
 }
 
 // calcCoverage of every row as run-start lists (no dense depth): per (row, column chunk of
@@ -2055,7 +2270,7 @@ int coverage_starts_dev(rcp_plan* plan, const int64_t* d_off, const int64_t* d_s
     HIP_TRY(rcp_launch_locate(&P, s));
     HIP_TRY(rcp_launch_heavy(&P, kHeavyGrid, s));
     HIP_TRY(rcp_launch_pileup(&P, nullptr, nullptr, 1, s));
-    return RCP_OK;
+    return end_exec(plan, s);
 }
 
 // the column chunk of coverage_starts_dev (one wave sub-chunk each)
@@ -2286,8 +2501,25 @@ bool part_slice_spec(int where, int32_t f1, int32_t f2, RcpPart* pt) {
 
 }  // namespace
 
-int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out,
-                           int64_t out_ld, uint8_t* row_valid, hipStream_t s) {
+namespace {
+
+// One rcp_profile_rle call (or one row block of it) split in two: rle_prepare -- host checks and
+// tasks, the runs and tables up, the run-start scan -- on one stream, and rle_finish -- the profile
+// kernel and the matrix down -- on another, so that a pipeline can prepare block b + 1 while block
+// b's rows come down (profile_rle_device).  The buffers are the preparing stream's; rle_prepare
+// returns with its stream idle.
+struct RleJob {
+    explicit RleJob(hipStream_t s) : d_len(s), d_val(s), d_off(s), d_gstart(s), temp(s), d_tab(s), d_scratch(s), d_out(s) {}
+    PoolBuf d_len, d_val, d_off, d_gstart, temp, d_tab, d_scratch, d_out;
+    RcpRleDev P{};
+    size_t lds = 0;
+    bool dbl = false;
+    int32_t R = 0;
+    int64_t col = 0, ld = 0;
+    const uint8_t* is_null = nullptr;
+};
+
+int rle_prepare(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, hipStream_t s, RleJob* job) {
     if (!cov || !bins) return fail(RCP_EINVAL, "NULL argument");
     const int32_t R = cov->n_rows;
     if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
@@ -2343,7 +2575,8 @@ int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, i
     HIP_TRY(g.err);
     // ---- runs to the device: lengths (+ a 0 pad for the scan), values, row offsets;
     // the scan of the lengths gives every run's start (rcp_rle.h gstart)
-    PoolBuf d_len(s), d_val(s), d_off(s), d_gstart(s), temp(s);
+    PoolBuf &d_len = job->d_len, &d_val = job->d_val, &d_off = job->d_off, &d_gstart = job->d_gstart,
+            &temp = job->temp;
     HIP_TRY(d_len.alloc(4 * ((size_t)n_runs + 1)));
     HIP_TRY(d_val.alloc((dbl ? 8 : 4) * std::max<size_t>((size_t)n_runs, 1)));
     HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
@@ -2356,7 +2589,7 @@ int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, i
     if (R > 0) HIP_TRY(rcp::stage_h2d(d_off.p, cov->run_off, 8 * ((size_t)R + 1), device, s));
     // ---- tasks: one per (row, part), with the read path's splitVector decisions
     const bool rounding = bins->rng_kind == RCP_RNG_ROUNDING;
-    RcpRleDev P{};
+    RcpRleDev& P = job->P;
     std::vector<RcpRleTask> tasks;
     tasks.reserve((size_t)R * bins->n_parts);
     std::vector<int32_t> lay_cnt, nb_pos;
@@ -2497,7 +2730,7 @@ int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, i
     const size_t o_lay = put(blob, lay_cnt);
     const size_t o_nb = put(blob, nb_pos);
     const size_t o_spl = put(blob, spl_tb);
-    PoolBuf d_tab(s), d_scratch(s), d_out(s);
+    PoolBuf &d_tab = job->d_tab, &d_scratch = job->d_scratch, &d_out = job->d_out;
     HIP_TRY(d_tab.alloc(blob.size()));
     HIP_TRY(rcp::stage_h2d(d_tab.p, blob.data(), blob.size(), device, s));
     if (n_scratch && !P.interp_lds) HIP_TRY(d_scratch.alloc(8 * (size_t)stride * n_scratch));
@@ -2522,21 +2755,48 @@ int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, i
     P.stat = bins->stat;
     P.scale = bins->scale;
     P.scratch = d_scratch.as<double>();
-    HIP_TRY(rcp_rle_profile_launch(&P, dbl ? 1 : 0, P.interp_lds ? lds : 0, s));
-    if (out && R && col)
-        HIP_TRY(rcp::stage_d2h_2d(out, 8 * (size_t)out_ld, d_out.p, 8 * (size_t)ld, 8 * (size_t)R, (size_t)col, device, s));
+    job->lds = P.interp_lds ? lds : 0;
+    job->dbl = dbl;
+    job->R = R;
+    job->col = col;
+    job->ld = ld;
+    job->is_null = cov->is_null;
+    HIP_TRY(hipStreamSynchronize(s));
+    return RCP_OK;
+}
+
+int rle_finish(RleJob* job, int device, double* out, int64_t out_ld, uint8_t* row_valid, hipStream_t s) {
+    DeviceGuard g(device);
+    HIP_TRY(g.err);
+    HIP_TRY(rcp_rle_profile_launch(&job->P, job->dbl ? 1 : 0, job->lds, s));
+    if (out && job->R && job->col)
+        HIP_TRY(rcp::stage_d2h_2d(out, 8 * (size_t)out_ld, job->d_out.p, 8 * (size_t)job->ld, 8 * (size_t)job->R,
+                                  (size_t)job->col, device, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (row_valid)
-        for (int32_t r = 0; r < R; ++r) row_valid[r] = (cov->is_null && cov->is_null[r]) ? 0 : 1;
+        for (int32_t r = 0; r < job->R; ++r) row_valid[r] = (job->is_null && job->is_null[r]) ? 0 : 1;
     return RCP_OK;
+}
+
+}  // namespace
+
+int rcpi::profile_rle_impl(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out,
+                           int64_t out_ld, uint8_t* row_valid, hipStream_t s) {
+    RleJob job(s);
+    const int rc = rle_prepare(cov, bins, device, s, &job);
+    if (rc) return rc;
+    return rle_finish(&job, device, out, out_ld, row_valid, s);
 }
 
 namespace {
 
 // rcp_profile_rle of rows [0, cov->n_rows) on one device, into a matrix of column stride out_ld:
-// big lists in row blocks through two host threads with a stream each, so that one block's runs
-// go up while another's rows of the matrix come down (PCIe is full duplex; the staging buffers
-// are per direction, rcp_stage.cpp): C4's 0.8 GB of runs up and 1.6 GB of matrix down overlap
+// a big list goes in row blocks through three host threads -- one prepares each block (host
+// checks and tasks, its runs up through the upload staging buffers), two finish them in turn
+// (profile kernel, the block's rows of the matrix down through the download staging buffers) --
+// so that block b + 1's runs go up while block b's rows come down (PCIe is full duplex; the
+// staging buffers are per direction, rcp_stage.cpp): C4's 0.8 GB of runs up and 1.6 GB of
+// matrix down overlap.  At most three blocks are on the device.
 int profile_rle_device(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, double* out, int64_t out_ld,
                        uint8_t* row_valid) {
     const int32_t R = cov->n_rows;
@@ -2550,35 +2810,106 @@ int profile_rle_device(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int d
     std::vector<double> cum((size_t)R + 1, 0.0);
     for (int32_t r = 0; r < R; ++r) cum[r + 1] = cum[r] + 64.0 + (double)(cov->run_off[r + 1] - cov->run_off[r]);
     const std::vector<int32_t> split = balanced_split(cum, nb);
-    return run_per_device(2, [&](int t) {
+    struct Block {
+        int b;
+        std::unique_ptr<RleJob> job;
+    };
+    std::deque<Block> ready;
+    int in_flight = 0;  // prepared, not yet finished
+    bool prepared_all = false, abort = false;
+    std::mutex mu;
+    std::condition_variable cv;
+    const bool tr = rcp::trace_on();
+    const double t0 = tr ? rcp::trace_ms() : 0.0;
+    // the preparer's stream outlives every job (their buffers are freed on it)
+    DeviceGuard g(device);
+    HIP_TRY(g.err);
+    hipStream_t sp = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&sp, hipStreamNonBlocking));
+    std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> spguard(sp, hipStreamDestroy);
+    const int rc = run_per_device(3, [&](int role) -> int {
         DeviceGuard gt(device);
         HIP_TRY(gt.err);
-        hipStream_t s = nullptr;
-        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(s, hipStreamDestroy);
-        for (int b = t; b < nb; b += 2) {
-            const int32_t r0 = split[b], r1 = split[b + 1];
-            if (r1 <= r0) continue;
-            // the block as an Rle list of its own: run offsets from 0, arrays from its first run
-            const int64_t base = cov->run_off[r0];
-            std::vector<int64_t> off((size_t)(r1 - r0) + 1);
-            for (int32_t r = r0; r <= r1; ++r) off[r - r0] = cov->run_off[r] - base;
-            rcp_rle_desc sub = *cov;
-            sub.n_rows = r1 - r0;
-            sub.run_off = off.data();
-            sub.lengths = cov->lengths ? cov->lengths + base : nullptr;
-            sub.ivalues = cov->ivalues ? cov->ivalues + base : nullptr;
-            sub.dvalues = cov->dvalues ? cov->dvalues + base : nullptr;
-            sub.is_null = cov->is_null ? cov->is_null + r0 : nullptr;
-            const double tb = rcp::trace_on() ? rcp::trace_ms() : 0.0;
-            const int e = profile_rle_impl(&sub, bins, device, out ? out + r0 : nullptr, out_ld,
-                                           row_valid ? row_valid + r0 : nullptr, s);
-            if (rcp::trace_on())
-                fprintf(stderr, "[rle] block %d rows [%d, %d): %.2f ms (from %.2f)\n", b, r0, r1, rcp::trace_ms() - tb, tb);
+        hipStream_t s = sp;
+        std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(nullptr,
+                                                                                                     hipStreamDestroy);
+        if (role != 0) {
+            HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            sguard.reset(s);
+        }
+        if (role == 0) {  // preparer
+            for (int b = 0; b < nb; ++b) {
+                const int32_t r0 = split[b], r1 = split[b + 1];
+                if (r1 <= r0) continue;
+                {
+                    std::unique_lock<std::mutex> lock(mu);
+                    cv.wait(lock, [&] { return abort || in_flight < 3; });
+                    if (abort) return (int)RCP_OK;
+                    ++in_flight;
+                }
+                // the block as an Rle list of its own: run offsets from 0, arrays from its first run
+                const int64_t base = cov->run_off[r0];
+                std::vector<int64_t> off((size_t)(r1 - r0) + 1);
+                for (int32_t r = r0; r <= r1; ++r) off[r - r0] = cov->run_off[r] - base;
+                rcp_rle_desc sub = *cov;
+                sub.n_rows = r1 - r0;
+                sub.run_off = off.data();
+                sub.lengths = cov->lengths ? cov->lengths + base : nullptr;
+                sub.ivalues = cov->ivalues ? cov->ivalues + base : nullptr;
+                sub.dvalues = cov->dvalues ? cov->dvalues + base : nullptr;
+                sub.is_null = cov->is_null ? cov->is_null + r0 : nullptr;
+                const double tb = tr ? rcp::trace_ms() : 0.0;
+                auto job = std::make_unique<RleJob>(s);
+                const int e = rle_prepare(&sub, bins, device, s, job.get());
+                if (tr)
+                    fprintf(stderr, "[rle] block %d rows [%d, %d): prepared %.2f ms (at %.2f)\n", b, r0, r1,
+                            rcp::trace_ms() - tb, tb - t0);
+                {
+                    std::lock_guard<std::mutex> lock(mu);
+                    if (e) {
+                        abort = true;
+                    } else {
+                        ready.push_back(Block{b, std::move(job)});
+                    }
+                }
+                cv.notify_all();
+                if (e) return e;
+            }
+            {
+                std::lock_guard<std::mutex> lock(mu);
+                prepared_all = true;
+            }
+            cv.notify_all();
+            return (int)RCP_OK;
+        }
+        for (;;) {  // finishers
+            Block blk;
+            {
+                std::unique_lock<std::mutex> lock(mu);
+                cv.wait(lock, [&] { return abort || !ready.empty() || prepared_all; });
+                if (abort || ready.empty()) return (int)RCP_OK;
+                blk = std::move(ready.front());
+                ready.pop_front();
+            }
+            const int32_t r0 = split[blk.b];
+            const double tb = tr ? rcp::trace_ms() : 0.0;
+            const int e = rle_finish(blk.job.get(), device, out ? out + r0 : nullptr, out_ld,
+                                     row_valid ? row_valid + r0 : nullptr, s);
+            if (tr)
+                fprintf(stderr, "[rle] block %d: profiled + down %.2f ms (at %.2f)\n", blk.b, rcp::trace_ms() - tb,
+                        tb - t0);
+            blk.job.reset();  // (its buffers back to the cache: this stream is idle)
+            {
+                std::lock_guard<std::mutex> lock(mu);
+                --in_flight;
+                if (e) abort = true;
+            }
+            cv.notify_all();
             if (e) return e;
         }
-        return (int)RCP_OK;
     });
+    ready.clear();  // (left by a failure: freed while the preparer's stream exists)
+    return rc;
 }
 
 }  // namespace

@@ -135,8 +135,10 @@ struct DevBuf {
     }
 };
 
-// Stream-ordered temporaries from the library's own device memory pool (rcp_host.cpp)
+// Stream-ordered device memory from the library's caching allocator (rcp_host.cpp): pool_alloc's
+// block is usable in stream order on s; pool_free hands it back after the work queued on s so far
 hipError_t pool_alloc(void** p, size_t n, hipStream_t s);
+void pool_free(void* p, hipStream_t s);
 
 struct PoolBuf {
     void* p = nullptr;
@@ -147,7 +149,7 @@ struct PoolBuf {
     PoolBuf& operator=(const PoolBuf&) = delete;
     ~PoolBuf() { reset(); }
     void reset() {
-        if (p) (void)hipFreeAsync(p, s);
+        pool_free(p, s);
         p = nullptr;
         bytes = 0;
     }
@@ -156,6 +158,12 @@ struct PoolBuf {
         bytes = n;
         if (n == 0) return hipSuccess;
         return pool_alloc(&p, n, s);
+    }
+    void* release() {  // ownership to the caller
+        void* q = p;
+        p = nullptr;
+        bytes = 0;
+        return q;
     }
     template <class T>
     T* as() const {
@@ -253,11 +261,11 @@ int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_reads
 // `stranded` (stream c*3 + strand, for findOverlaps with strand compatibility) and `merged`
 // (all strands in stream c*3, streams c*3+1, c*3+2 empty: ignore.strand = TRUE, the default),
 // so the default path searches and streams one range per segment instead of three.
-// A readset's own arrays, from the same pool (a 4 GB hipMalloc of C5's packed reads once took
-// 5.9 s on the box, tools/diag_readset.py with -DRCP_PLAN_TIMING=1), allocated on the build
-// stream and released after one device synchronisation per readset (~rcp_readset) -- what
-// hipFree does implicitly, so a readset destroyed with work still queued on it stays safe --
-// back into the pool.
+// A readset's (and a plan's) own arrays, from the same caching allocator (a 4 GB hipMalloc of
+// C5's packed reads once took 5.9 s on the box, tools/diag_readset.py), allocated on the build
+// stream and handed back after the owner's last work has finished (~rcp_readset: one device
+// synchronisation -- what hipFree does implicitly, so a readset destroyed with work still queued
+// on it stays safe; ~rcp_plan: its completion event).
 namespace rcpi {
 struct PoolArr {
     void* p = nullptr;
@@ -271,7 +279,7 @@ struct PoolArr {
     }
     PoolArr& operator=(PoolArr&& o) noexcept {
         if (this != &o) {
-            if (p) (void)hipFreeAsync(p, nullptr);
+            pool_free(p, nullptr);
             p = o.p;
             bytes = o.bytes;
             o.p = nullptr;
@@ -280,13 +288,23 @@ struct PoolArr {
         return *this;
     }
     ~PoolArr() {
-        if (p) (void)hipFreeAsync(p, nullptr);  // after rcp_readset's device synchronisation
+        pool_free(p, nullptr);  // after rcp_readset's device synchronisation
     }
     hipError_t alloc(size_t n, hipStream_t s) {
         if (p) return hipErrorInvalidValue;  // allocated once
         bytes = n;
         if (n == 0) return hipSuccess;
         return pool_alloc(&p, n, s);
+    }
+    void reset() {
+        pool_free(p, nullptr);
+        p = nullptr;
+        bytes = 0;
+    }
+    void adopt(PoolBuf& b) {  // a build temporary kept (freed as this array is)
+        reset();
+        bytes = b.bytes;
+        p = b.release();
     }
     template <class T>
     T* as() const {
@@ -312,7 +330,7 @@ struct rcp_readset {
     int64_t n = 0;  // reads kept (strand filter applied)
     int32_t n_chrom = 0;
     std::vector<int64_t> seqlen;
-    rcpi::DevBuf d_seqlen;
+    rcpi::PoolArr d_seqlen;
     rcpi::ReadLayout stranded, merged;
     bool presorted = false;  // the reads came in (chromosome, start) order (no full radix sort)
     bool has_merged = false; // the merged layout was built (every readset but a strand-split shard's)
@@ -323,7 +341,7 @@ struct rcp_readset {
     std::mutex mu;
     bool stranded_ready = false;
     rcp_reads_desc desc{};  // n, n_chrom, strand_filter of the build
-    rcpi::DevBuf keep_chrom, keep_start, keep_end, keep_strand;
+    rcpi::PoolArr keep_chrom, keep_start, keep_end, keep_strand;
     const int32_t *kc = nullptr, *ks = nullptr, *ke = nullptr;
     const int8_t* kst = nullptr;
     // one device synchronisation before the members' arrays go back to the pool (what hipFree
@@ -343,10 +361,13 @@ struct rcp_plan {
     size_t lds = 0;
     int64_t grid = 0;
     int32_t tile_rows = 64;  // rows per pileup workgroup (info)
-    rcpi::DevBuf tables;     // read-only tables
-    rcpi::DevBuf work;       // seg_lo / seg_hi / valid / status
-    rcpi::DevBuf scratch;    // interpolation scratch
-    rcpi::DevBuf rm;         // row-wave kernel: row-major staging of the matrix
+    // device arrays from the pool, released when the plan's last execution has finished (ev_done,
+    // or a device synchronisation when it ran on several streams): no hipMalloc / hipFree -- a
+    // device-wide synchronisation -- per plan, which would stall the other threads of a pipeline
+    rcpi::PoolArr tables;    // read-only tables
+    rcpi::PoolArr work;      // seg_lo / seg_hi / valid / status
+    rcpi::PoolArr scratch;   // interpolation scratch
+    rcpi::PoolArr rm;        // row-wave kernel: row-major staging of the matrix
     int32_t max_row_len = 0;
     int64_t out_ld = 0;
     uint32_t* status_sets = nullptr;  // 2 x RCP_STATUS_WORDS words in `work`
@@ -355,7 +376,13 @@ struct rcp_plan {
     // stream; made at the first execution that interpolates)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_done = nullptr;  // recorded after every execution (rcp_host.cpp end_exec)
+    hipStream_t last = nullptr;    // the executions' stream, when n_streams == 1
+    int n_streams = 0;             // 0, 1, 2 = several
     ~rcp_plan() {  // (on the plan's device: rcp_plan_destroy)
+        if (n_streams > 1) (void)hipDeviceSynchronize();
+        else if (ev_done) (void)hipEventSynchronize(ev_done);
+        if (ev_done) (void)hipEventDestroy(ev_done);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
         if (side) (void)hipStreamDestroy(side);

@@ -343,7 +343,10 @@ extern "C" int rcp_shards_create(const rcp_reads_desc* reads, const rcp_rows_des
         const size_t m = (size_t)std::max<int64_t>(n_blk[b], 1);
         HIP_TRY(rcv[b].alloc(13 * m));
         // ignore.strand = TRUE never reads the strand: every read '*'
-        if (merged) HIP_TRY(hipMemset(rcv[b].as<char>() + 12 * m, RCP_STRAND_ANY, m));
+        if (merged) {
+            HIP_TRY(hipMemsetAsync(rcv[b].as<char>() + 12 * m, RCP_STRAND_ANY, m, nullptr));
+            HIP_TRY(hipStreamSynchronize(nullptr));  // (the gathers run on non-blocking streams)
+        }
         return (int)RCP_OK;
     });
     if (rc) return rc;

@@ -10,8 +10,6 @@
 #include "rcp_stage.h"
 
 #include <emmintrin.h>
-#include <sys/mman.h>
-#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -30,7 +28,11 @@ namespace {
 
 constexpr size_t kChunk = size_t(64) << 20;  // 64 MB: 51-54 GB/s vs 41 GB/s at 16 MB (pcie.log)
 constexpr size_t kDirect = size_t(4) << 20;  // below this, a plain hipMemcpy
-constexpr int kThreads = 4;                  // 4 memcpy threads saturate one x16 link
+// memcpy threads per direction: 4 saturate one direction of an x16 link alone (pcie.log), but
+// with both directions busy the host memory traffic (3 bytes per byte moved) needs 8 each to keep
+// 86 GB/s in flight vs 55 with 4 (profiles/r05/pcie_duplex.log).  The download -- a profile's
+// matrix, 1.6x a C4 sample's reads -- is the longer direction of a streamed sample: it gets more.
+constexpr int kThreadsDir[2] = {8, 8};
 constexpr int kMaxDevices = 64;
 
 // A fixed pool: run(parts, fn) executes fn(0 .. parts - 1) on the workers and the caller.
@@ -104,7 +106,11 @@ struct Stager {
     std::mutex mu;
     bool init = false, ok = false;
     char* pin[2] = {nullptr, nullptr};
+    // blocking-sync events: a thread waiting for a DMA sleeps instead of spinning -- the box gives
+    // a process 16 cores of CPU time (cgroup quota), and spinning waiters next to the memcpy
+    // threads ran it out (10-ms stalls of every thread until the next quota period)
     hipEvent_t ev[2] = {nullptr, nullptr};
+    hipEvent_t done = nullptr;
     std::unique_ptr<Pool> pool;
 };
 
@@ -115,15 +121,17 @@ Stager* stager(int device, int dir) {  // dir 0: host -> device, 1: device -> ho
     return device >= 0 && device < kMaxDevices ? &s[2 * device + dir] : nullptr;
 }
 
-bool ready(Stager* s) {  // under s->mu, on the device
+bool ready(Stager* s, int dir) {  // under s->mu, on the device
     if (s->init) return s->ok;
     s->init = true;
     for (int b = 0; b < 2; ++b) {
         if (hipHostMalloc(reinterpret_cast<void**>(&s->pin[b]), kChunk, hipHostMallocDefault) != hipSuccess) return false;
-        if (hipEventCreateWithFlags(&s->ev[b], hipEventDisableTiming) != hipSuccess) return false;
+        if (hipEventCreateWithFlags(&s->ev[b], hipEventDisableTiming | hipEventBlockingSync) != hipSuccess)
+            return false;
     }
+    if (hipEventCreateWithFlags(&s->done, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) return false;
     try {
-        s->pool.reset(new Pool(kThreads - 1));
+        s->pool.reset(new Pool(kThreadsDir[dir] - 1));
     } catch (const std::exception&) {
         return false;
     }
@@ -180,19 +188,20 @@ void copy_nt(char* dst, const char* src, size_t n) {
     _mm_sfence();
 }
 
-// A large destination the caller has just allocated (R's vectors of a coverage list) is
-// first-touched by the drain threads: transparent huge pages make that one fault per 2 MB
-void advise_huge(void* p, size_t n) {
-    static const size_t page = (size_t)sysconf(_SC_PAGESIZE);
-    const uintptr_t huge = uintptr_t(2) << 20;
-    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + huge - 1) & ~(huge - 1);
-    const uintptr_t z = (reinterpret_cast<uintptr_t>(p) + n) & ~(huge - 1);
-    if (z > a && page <= huge) madvise(reinterpret_cast<void*>(a), z - a, MADV_HUGEPAGE);  // advisory: result ignored
+// Chunk size of one staged copy: up to the 64 MB buffers, but a copy of less than 256 MB in four
+// chunks at least (4 MB minimum), so that the host memcpy of one chunk runs beside the DMA of
+// another -- a 50 MB copy in one chunk does them one after the other (24 GB/s)
+size_t chunk_of(size_t bytes) {
+    const size_t quarter = ((bytes / 4) + (size_t(1) << 20) - 1) & ~((size_t(1) << 20) - 1);
+    return std::min(kChunk, std::max(size_t(4) << 20, quarter));
 }
 
-// Split [0, n) into kThreads near-equal 4 KB-aligned parts.
+// A chunk is cut into kParts 4 KB-aligned parts taken by the threads as they come free: a
+// thread descheduled for a while (the box's cores are shared with the pipeline's own threads)
+// holds up 2 MB, not a whole thread's share of the chunk.
+constexpr int kParts = 32;
 inline void part_range(size_t n, int i, size_t* a, size_t* b) {
-    const size_t per = ((n + kThreads - 1) / kThreads + 4095) & ~size_t(4095);
+    const size_t per = ((n + kParts - 1) / kParts + 4095) & ~size_t(4095);
     *a = std::min(n, per * (size_t)i);
     *b = std::min(n, *a + per);
 }
@@ -209,7 +218,7 @@ hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipSt
     std::unique_lock<std::mutex> g;
     if (bytes >= kDirect && st) g = take(st, bytes);
     const double t1 = trace() ? now_ms() : 0.0;
-    if (!g.owns_lock() || !ready(st)) {
+    if (!g.owns_lock() || !ready(st, 0)) {
         hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream);
         e = e == hipSuccess ? hipStreamSynchronize(stream) : e;
         if (trace() && bytes >= kDirect)
@@ -218,15 +227,16 @@ hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipSt
     }
     const char* s = static_cast<const char*>(src);
     char* d = static_cast<char*>(dst);
-    const size_t nch = (bytes + kChunk - 1) / kChunk;
+    const size_t ch = chunk_of(bytes);
+    const size_t nch = (bytes + ch - 1) / ch;
     hipError_t e = hipSuccess;
     for (size_t k = 0; k < nch && e == hipSuccess; ++k) {
         const int b = (int)(k & 1);
-        const size_t a0 = k * kChunk, len = std::min(kChunk, bytes - a0);
+        const size_t a0 = k * ch, len = std::min(ch, bytes - a0);
         if (k >= 2) e = hipEventSynchronize(st->ev[b]);  // the DMA out of this buffer is done
         if (e != hipSuccess) break;
         char* pin = st->pin[b];
-        st->pool->run(kThreads, [&](int i) {
+        st->pool->run(kParts, [&](int i) {
             size_t a, z;
             part_range(len, i, &a, &z);
             if (z > a) copy_nt(pin + a, s + a0 + a, z - a);
@@ -234,7 +244,8 @@ hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipSt
         e = hipMemcpyAsync(d + a0, pin, len, hipMemcpyHostToDevice, stream);
         if (e == hipSuccess) e = hipEventRecord(st->ev[b], stream);
     }
-    const hipError_t e2 = hipStreamSynchronize(stream);  // buffers free for the next user
+    hipError_t e2 = hipEventRecord(st->done, stream);  // buffers free for the next user
+    if (e2 == hipSuccess) e2 = hipEventSynchronize(st->done);
     if (trace()) fprintf(stderr, "[stage] h2d %zu B wait %.2f ms copy %.2f ms\n", bytes, t1 - t0, now_ms() - t1);
     return e != hipSuccess ? e : e2;
 }
@@ -249,7 +260,7 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
     std::unique_lock<std::mutex> g;
     if (bytes >= kDirect && st) g = take(st, bytes);
     const double t1 = trace() ? now_ms() : 0.0;
-    if (!g.owns_lock() || !ready(st)) {
+    if (!g.owns_lock() || !ready(st, 1)) {
         hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost, stream);
         e = e == hipSuccess ? hipStreamSynchronize(stream) : e;
         if (trace() && bytes >= kDirect)
@@ -258,7 +269,6 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
     }
     const char* s = static_cast<const char*>(src);
     char* d = static_cast<char*>(dst);
-    if (bytes >= kShared) advise_huge(d, dpitch * (height - 1) + width);
     // device bytes [a, z) of the linear span -> their host rows (padding bytes skipped)
     auto scatter = [&](const char* pin, size_t base, size_t a, size_t z) {
         while (a < z) {
@@ -272,30 +282,32 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
             a += n;
         }
     };
-    const size_t nch = (bytes + kChunk - 1) / kChunk;
+    const size_t ch = chunk_of(bytes);
+    const size_t nch = (bytes + ch - 1) / ch;
     hipError_t e = hipSuccess;
     for (size_t k = 0; k <= nch && e == hipSuccess; ++k) {
         if (k < nch) {  // DMA chunk k into buffer k % 2 (drained below one iteration ago)
             const int b = (int)(k & 1);
-            const size_t a0 = k * kChunk, len = std::min(kChunk, bytes - a0);
+            const size_t a0 = k * ch, len = std::min(ch, bytes - a0);
             e = hipMemcpyAsync(st->pin[b], s + a0, len, hipMemcpyDeviceToHost, stream);
             if (e == hipSuccess) e = hipEventRecord(st->ev[b], stream);
         }
         if (k > 0 && e == hipSuccess) {  // drain chunk k - 1 while chunk k is in flight
             const size_t j = k - 1;
             const int b = (int)(j & 1);
-            const size_t a0 = j * kChunk, len = std::min(kChunk, bytes - a0);
+            const size_t a0 = j * ch, len = std::min(ch, bytes - a0);
             e = hipEventSynchronize(st->ev[b]);
             if (e != hipSuccess) break;
             const char* pin = st->pin[b];
-            st->pool->run(kThreads, [&](int i) {
+            st->pool->run(kParts, [&](int i) {
                 size_t a, z;
                 part_range(len, i, &a, &z);
                 if (z > a) scatter(pin, a0, a0 + a, a0 + z);
             });
         }
     }
-    const hipError_t e2 = hipStreamSynchronize(stream);
+    hipError_t e2 = hipEventRecord(st->done, stream);
+    if (e2 == hipSuccess) e2 = hipEventSynchronize(st->done);
     if (trace()) fprintf(stderr, "[stage] d2h %zu B wait %.2f ms copy %.2f ms\n", bytes, t1 - t0, now_ms() - t1);
     return e != hipSuccess ? e : e2;
 }

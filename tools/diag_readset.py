@@ -1,6 +1,6 @@
 """Readset creation from host arrays, repeated (variance of the C5-sized H2D + layouts).
 
-    python tools/diag_readset.py [c5|c4] [reps]     (RCP_LIB_PATH: e.g. a -DRCP_PLAN_TIMING=1 build;
+    python tools/diag_readset.py [c5|c4] [reps]     (RCP_TRACE=1: per-phase lines of each build;
                                                      STRANDED=1: the strand-split layout as well)"""
 import os
 import sys

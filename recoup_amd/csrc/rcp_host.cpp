@@ -1403,6 +1403,11 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     plan->lds = P.lean == 4 ? rcp_pileup_bins_lds_bytes(&P)
                 : P.lean == 3 ? rcp_pileup_rows_lds_bytes(&P)
                               : (P.lean ? rcp_pileup_lean_lds_bytes(&P) : rcp_pileup_lds_bytes(&P, cov_only ? 1 : 0));
+    // the row-wave kernel's persistent grid holds one workgroup per CU for the whole pass: the
+    // interpolation rows (a side stream, forked after locate) fit beside it only in the LDS it
+    // leaves -- their spline arrays then go to global scratch (C3: 148 KB + 4 KB, vs 20 KB that
+    // waited for the pileup to end)
+    P.interp_lds_budget = P.lean == 3 ? (int32_t)std::max<int64_t>(0, 160 * 1024 - (int64_t)plan->lds) : 0;
     // general kernel: 2 rounds (32 rows) per workgroup (C3: 0.88 ms vs 0.91 with 4 rounds, 0.89
     // with 1), 1 when the row table is small, so that the grid still holds two workgroups per
     // CU (C2: 10k rows -> 625 workgroups instead of 157; pileup 0.076 -> 0.063 ms)
@@ -2519,7 +2524,10 @@ struct RleJob {
     const uint8_t* is_null = nullptr;
 };
 
-int rle_prepare(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, hipStream_t s, RleJob* job) {
+// dev_rows: the row lengths and the run-length checks on the device (a row block of a big list:
+// no host pass over its runs); row_base numbers the rows of the messages
+int rle_prepare(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, hipStream_t s, RleJob* job,
+                bool dev_rows = false, int32_t row_base = 0) {
     if (!cov || !bins) return fail(RCP_EINVAL, "NULL argument");
     const int32_t R = cov->n_rows;
     if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
@@ -2539,7 +2547,7 @@ int rle_prepare(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, 
     // Rle lengths are positive and every row fits int32 positions; row lengths (the slices of
     // the parts).  One pass over the runs, rows split over host threads (C4: 100 M runs).
     std::vector<int32_t> row_len(std::max(R, 1), 0);
-    {
+    if (!dev_rows) {
         const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
                                                                      n_runs / (1 << 20) + 1}));
         std::vector<int32_t> bad(nt, -1), big(nt, -1);
@@ -2587,6 +2595,20 @@ int rle_prepare(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, 
     }
     HIP_TRY(hipMemsetAsync(d_len.as<int32_t>() + n_runs, 0, 4, s));
     if (R > 0) HIP_TRY(rcp::stage_h2d(d_off.p, cov->run_off, 8 * ((size_t)R + 1), device, s));
+    if (dev_rows && R > 0) {
+        PoolBuf d_rl(s), d_bad(s);
+        HIP_TRY(d_rl.alloc(4 * (size_t)R));
+        HIP_TRY(d_bad.alloc(8));
+        HIP_TRY(hipMemsetAsync(d_bad.p, 0x7f, 8, s));  // 0x7f7f7f7f: no such row
+        HIP_TRY(rcp_rle_rowlen(R, d_off.as<int64_t>(), d_len.as<int32_t>(), d_rl.as<int32_t>(), d_bad.as<int32_t>(), s));
+        int32_t h_bad[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(row_len.data(), d_rl.p, 4 * (size_t)R, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(h_bad, d_bad.p, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (h_bad[0] != 0x7f7f7f7f) return fail(RCP_EINVAL, "row %d: an Rle run length <= 0", row_base + h_bad[0]);
+        if (h_bad[1] != 0x7f7f7f7f)
+            return fail(RCP_EUNSUPPORTED, "row %d: 2^31 or more positions", row_base + h_bad[1]);
+    }
     // ---- tasks: one per (row, part), with the read path's splitVector decisions
     const bool rounding = bins->rng_kind == RCP_RNG_ROUNDING;
     RcpRleDev& P = job->P;
@@ -2815,37 +2837,60 @@ int profile_rle_device(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int d
         std::unique_ptr<RleJob> job;
     };
     std::deque<Block> ready;
-    int in_flight = 0;  // prepared, not yet finished
-    bool prepared_all = false, abort = false;
+    int in_flight = 0;  // being prepared or prepared, not yet finished
+    int next_b = 0, preparers_left = 2;
+    bool abort = false;
     std::mutex mu;
     std::condition_variable cv;
     const bool tr = rcp::trace_on();
     const double t0 = tr ? rcp::trace_ms() : 0.0;
-    // the preparer's stream outlives every job (their buffers are freed on it)
+    // the preparers' streams outlive every job (their buffers are freed on them)
     DeviceGuard g(device);
     HIP_TRY(g.err);
-    hipStream_t sp = nullptr;
-    HIP_TRY(hipStreamCreateWithFlags(&sp, hipStreamNonBlocking));
-    std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> spguard(sp, hipStreamDestroy);
-    const int rc = run_per_device(3, [&](int role) -> int {
+    hipStream_t sp[2] = {nullptr, nullptr};
+    struct Streams {
+        hipStream_t* v;
+        ~Streams() {
+            for (int i = 0; i < 2; ++i)
+                if (v[i]) (void)hipStreamDestroy(v[i]);
+        }
+    } spguard{sp};
+    for (int i = 0; i < 2; ++i) HIP_TRY(hipStreamCreateWithFlags(&sp[i], hipStreamNonBlocking));
+    // two preparers (the host checks and tasks of one block beside the other's uploads) and two
+    // finishers (one block's kernel and plan beside the other's download); at most four blocks
+    const int rc = run_per_device(4, [&](int role) -> int {
         DeviceGuard gt(device);
         HIP_TRY(gt.err);
-        hipStream_t s = sp;
+        hipStream_t s = role < 2 ? sp[role] : nullptr;
         std::unique_ptr<std::remove_pointer<hipStream_t>::type, hipError_t (*)(hipStream_t)> sguard(nullptr,
                                                                                                      hipStreamDestroy);
-        if (role != 0) {
+        if (role >= 2) {
             HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             sguard.reset(s);
         }
-        if (role == 0) {  // preparer
-            for (int b = 0; b < nb; ++b) {
-                const int32_t r0 = split[b], r1 = split[b + 1];
-                if (r1 <= r0) continue;
+        if (role < 2) {  // preparers
+            auto done = [&] {
+                {
+                    std::lock_guard<std::mutex> lock(mu);
+                    --preparers_left;
+                }
+                cv.notify_all();
+            };
+            for (;;) {
+                int b;
                 {
                     std::unique_lock<std::mutex> lock(mu);
-                    cv.wait(lock, [&] { return abort || in_flight < 3; });
+                    cv.wait(lock, [&] { return abort || in_flight < 4 || next_b >= nb; });
                     if (abort) return (int)RCP_OK;
+                    if (next_b >= nb) break;
+                    b = next_b++;
                     ++in_flight;
+                }
+                const int32_t r0 = split[b], r1 = split[b + 1];
+                if (r1 <= r0) {
+                    std::lock_guard<std::mutex> lock(mu);
+                    --in_flight;
+                    continue;
                 }
                 // the block as an Rle list of its own: run offsets from 0, arrays from its first run
                 const int64_t base = cov->run_off[r0];
@@ -2860,7 +2905,7 @@ int profile_rle_device(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int d
                 sub.is_null = cov->is_null ? cov->is_null + r0 : nullptr;
                 const double tb = tr ? rcp::trace_ms() : 0.0;
                 auto job = std::make_unique<RleJob>(s);
-                const int e = rle_prepare(&sub, bins, device, s, job.get());
+                const int e = rle_prepare(&sub, bins, device, s, job.get(), true, r0);
                 if (tr)
                     fprintf(stderr, "[rle] block %d rows [%d, %d): prepared %.2f ms (at %.2f)\n", b, r0, r1,
                             rcp::trace_ms() - tb, tb - t0);
@@ -2873,20 +2918,19 @@ int profile_rle_device(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int d
                     }
                 }
                 cv.notify_all();
-                if (e) return e;
+                if (e) {
+                    done();
+                    return e;
+                }
             }
-            {
-                std::lock_guard<std::mutex> lock(mu);
-                prepared_all = true;
-            }
-            cv.notify_all();
+            done();
             return (int)RCP_OK;
         }
         for (;;) {  // finishers
             Block blk;
             {
                 std::unique_lock<std::mutex> lock(mu);
-                cv.wait(lock, [&] { return abort || !ready.empty() || prepared_all; });
+                cv.wait(lock, [&] { return abort || !ready.empty() || preparers_left == 0; });
                 if (abort || ready.empty()) return (int)RCP_OK;
                 blk = std::move(ready.front());
                 ready.pop_front();

@@ -3126,6 +3126,10 @@ __device__ void block_window_depth(const RcpPlanDev& P, int r, int32_t w0, int32
 // Rows the pileup kernel leaves out: interpolation (length(x) < n bins, modes 1-3) and
 // median bins wider than a wave chunk (mode 4, bins taken in groups that fit the window).
 __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double* __restrict__ out) {
+    // these blocks run beside the persistent pileup workgroups (a side stream forked after
+    // locate) and are latency-bound (the spline's serial chains): their waves issue first on a
+    // shared SIMD, so the pass does not wait for them after the memory-bound pileup has ended
+    __builtin_amdgcn_s_setprio(2);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* diff = reinterpret_cast<int32_t*>(smem);
     const int diff_words = (P.interp_cap + 8 + 1023) & ~1023;
@@ -3393,8 +3397,10 @@ static size_t interp_int_bytes(const RcpPlanDev* P) {
 
 static bool interp_in_lds(const RcpPlanDev* P) {
     // (the spline's arrays in global scratch instead, which lets every row's block be resident
-    // at once, measured slower on C3: 0.128 vs 0.123 ms, profiles/r02h/c3_transpose_interp_ab.log)
-    return interp_int_bytes(P) + 8 * (size_t)P->interp_stride + 16 <= 160 * 1024;
+    // at once, measured slower alone on C3: 0.128 vs 0.123 ms, profiles/r02h/c3_transpose_interp_ab.log;
+    // beside the row-wave pileup the smaller block is what fits, interp_lds_budget)
+    const size_t budget = P->interp_lds_budget > 0 ? (size_t)P->interp_lds_budget : 160 * 1024;
+    return interp_int_bytes(P) + 8 * (size_t)P->interp_stride + 16 <= budget;
 }
 
 extern "C" size_t rcp_interp_lds_bytes(const RcpPlanDev* P) {

@@ -465,7 +465,44 @@ rcp_rle_tile_kernel(RcpRleDev P, int p) {
     }
 }
 
+// Row lengths of an Rle list and its checks (rcp_profile_rle's host pass, on the device for a
+// big list): one wave per row sums its run lengths (int64) and takes their minimum; row_len[r] =
+// min(sum, INT32_MAX); bad[0] / bad[1] = the first row with a length <= 0 / with 2^31 or more
+// positions (atomicMin over rows; the caller presets them to INT32_MAX)
+__global__ void __launch_bounds__(256) rcp_rle_rowlen_kernel(int32_t R, const int64_t* __restrict__ run_off,
+                                                             const int32_t* __restrict__ lengths,
+                                                             int32_t* __restrict__ row_len, int32_t* bad) {
+    const int lane = threadIdx.x & 63;
+    const int32_t r = (int32_t)((blockIdx.x * 256 + threadIdx.x) >> 6);
+    if (r >= R) return;
+    int64_t acc = 0;
+    int32_t mn = INT32_MAX;
+    for (int64_t j = run_off[r] + lane; j < run_off[r + 1]; j += 64) {
+        const int32_t v = lengths[j];
+        acc += v;
+        mn = min(mn, v);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        acc += __shfl_xor(acc, o);
+        mn = min(mn, __shfl_xor(mn, o));
+    }
+    if (lane == 0) {
+        row_len[r] = (int32_t)min(acc, (int64_t)INT32_MAX);
+        if (mn <= 0) atomicMin(&bad[0], r);
+        if (acc >= (int64_t(1) << 31)) atomicMin(&bad[1], r);
+    }
+}
+
 }  // namespace
+
+extern "C" hipError_t rcp_rle_rowlen(int32_t R, const int64_t* run_off, const int32_t* lengths, int32_t* row_len,
+                                     int32_t* bad, hipStream_t stream) {
+    if (R <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rcp_rle_rowlen_kernel, dim3((unsigned)(((int64_t)R * 64 + 255) / 256)), dim3(256), 0, stream, R,
+                       run_off, lengths, row_len, bad);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t rcp_rle_scan(const int32_t* lengths, int64_t n_runs, int64_t* gstart, void* temp,
                                    size_t* temp_bytes, hipStream_t stream) {

@@ -77,25 +77,37 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
             c[i] = cp;
         }
         const double bn = -1.0 - tt[n - 1];  // b[n-1] = -1 - t_{n-1}
-        // back substitution: c[i] = (c[i] - c[i+1]) / b[i]
+        // back substitution: c[i] = (c[i] - c[i+1]) / b[i].  The pivot's reciprocal is in the
+        // table already -- t_{i+1} = RN(1 / b_i), the host's IEEE division -- so each quotient is
+        // q = RN(x y), then corrected once: RN(q + RN(x - q b) y) with the remainder exact by
+        // FMA is the correctly rounded x / b (Markstein), i.e. the division's bits, in three
+        // dependent operations instead of the division's ten; zeros (signed) and extreme
+        // exponents, where the theorem's assumptions fail, take the division itself
+        auto quot = [](double x, double b, double y) -> double {
+            const double ax = __builtin_fabs(x);
+            if (!(ax >= 0x1p-960 && ax <= 0x1p+960)) return x / b;
+            const double q = x * y;
+            return __builtin_fma(__builtin_fma(-q, b, x), y, q);
+        };
         double cnext = cp / bn;
         c[n - 1] = cnext;
         i = n - 2;
         for (; i >= 7; i -= 8) {
-            double cv[8], bv[8];
+            double cv[8], bv[8], yv[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 cv[u] = c[i - u];
                 bv[u] = tp[i - u];
+                yv[u] = tt[i - u + 1];
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                cnext = (cv[u] - cnext) / bv[u];
+                cnext = quot(cv[u] - cnext, bv[u], yv[u]);
                 c[i - u] = cnext;
             }
         }
         for (; i >= 0; --i) {
-            cnext = (c[i] - cnext) / tp[i];
+            cnext = quot(c[i] - cnext, tp[i], tt[i + 1]);
             c[i] = cnext;
         }
         b[n - 1] = (y[n - 1] - y[n - 2]) + (c[n - 2] + 2.0 * c[n - 1]);

@@ -305,6 +305,13 @@ def test_profile_rle_row_blocks(gpu):
     np.testing.assert_allclose(mat, want, rtol=1e-12, atol=0)
     few = profile_rle_arrays(run_off[:101].copy(), lengths[:run_off[100]], values[:run_off[100]], nulls[:100], bins)
     assert np.array_equal(few[0].view(np.uint64), np.ascontiguousarray(mat[:100]).view(np.uint64))
+    # a bad run length in a late block: the blocks check their runs on the device, same message
+    from recoup_amd._lib import RcpError
+    bad = lengths.copy()
+    r_bad = R - 7
+    bad[run_off[r_bad] + 1] = 0
+    with pytest.raises(RcpError, match=f"row {r_bad}: an Rle run length <= 0"):
+        profile_rle_arrays(run_off, bad, values, nulls, bins)
 
 
 def sorted_sample(rng, n, order=(2, 0, 1), width=100):

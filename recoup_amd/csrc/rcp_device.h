@@ -139,6 +139,8 @@ struct RcpPlanDev {
     int32_t interp_lds;         // byte offset of the row's doubles in LDS, -1 = global scratch (launcher)
     int32_t interp_lds_budget;  // LDS bytes an interpolation block may take so that it runs beside the
                                 // persistent pileup workgroups (the rest of a CU's 160 KB); 0 = all
+    int32_t interp_stage;       // per execution: the row-wave kernel (HBM stage) piles the interpolated
+                                // parts into rm32 and rcp_interp_kernel, launched after it, reads them
     // geometry
     int32_t chunk_cap;          // max positions per chunk (one wave's difference array)
     int32_t wave_words;         // LDS words per wave difference array (multiple of 256)

@@ -1509,9 +1509,13 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
         }
     }
     // rows with fewer positions than bins (splines of short genes: serial chains) write only their
-    // own cells, and read only locate's outputs: they run on a side stream beside the pileup
-    // (C3: 0.1 ms of interpolation behind a 0.5 ms pileup) and join the caller's stream after it
-    const bool fork = (stages & RCP_STAGE_PILEUP) && (stages & RCP_STAGE_INTERP) && plan->dev.n_interp > 0;
+    // own cells.  Row-wave plans with the HBM stage pile them in the pileup kernel (interp_stage:
+    // the interpolation kernel, after it, reads their depth from the stage -- no second pileup of
+    // the row); other plans' interpolation reads only locate's outputs and runs on a side stream
+    // beside the pileup, joining the caller's stream after it
+    plan->dev.interp_stage = (plan->dev.lean == 3 && plan->dev.rm32 && !d_binsum) ? 1 : 0;
+    const bool fork = (stages & RCP_STAGE_PILEUP) && (stages & RCP_STAGE_INTERP) && plan->dev.n_interp > 0 &&
+                      !plan->dev.interp_stage;
     if (fork) {
         if (!plan->side) {
             HIP_TRY(hipStreamCreateWithFlags(&plan->side, hipStreamNonBlocking));

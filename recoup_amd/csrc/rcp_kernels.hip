@@ -2076,18 +2076,24 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             const RcpPart part = P.part[p];
             int32_t head, L;
             rcp_part_slice(part, nr, &head, &L);
-            const int32_t n = part.n_bins;
-            if (!part.per_base && L < n) {  // interpolation row: rcp_interp_kernel
+            const int32_t n_bins = part.n_bins;
+            // interpolation row (fewer positions than bins): rcp_interp_kernel writes its columns.
+            // With the HBM stage (P.interp_stage) this wave piles its L positions as L one-position
+            // bins into the first L stage words of the part, and the interpolation kernel, run
+            // after this one, takes the depth from there instead of piling the row again.
+            const bool itp = !part.per_base && L < n_bins;
+            if (itp) {
                 if (staged && lane == 0) sinfo[p] = make_int2(-1, -1);
-                continue;
+                if (!staged || !P.interp_stage) continue;
             }
+            const int32_t n = itp ? L : n_bins;  // the bins of this pass
             if (part.per_base && L != n) {
                 if (lane == 0) atomicOr(P.status, RCP_STATUS_WIDTH);
                 zero_cols(r, part, n);
                 continue;
             }
             int32_t bs = 1, lay = -1;
-            if (!part.per_base) {
+            if (!part.per_base && !itp) {
                 bs = L / n;
                 const int32_t dif = L - bs * n;
                 if (dif) {
@@ -2098,7 +2104,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     }
                 }
             }
-            if (staged && lane == 0) sinfo[p] = make_int2(bs, lay);
+            if (staged && lane == 0 && !itp) sinfo[p] = make_int2(bs, lay);
             const int32_t kw = max(1, kWinCap / (bs + (lay >= 0 ? 1 : 0)));  // bins per window
             const bool pow2 = lay < 0 && (bs & (bs - 1)) == 0;
             const double dd = (double)bs, rdd = 1.0 / dd;
@@ -3190,11 +3196,17 @@ __global__ void __launch_bounds__(kBlock) rcp_interp_kernel(RcpPlanDev P, double
         if (threadIdx.x == 0) atomicOr(P.status, RCP_STATUS_INTERP);
         return;
     }
-    block_window_depth(P, r, head, L, diff, scratch);
     // the spline / fill works on LDS copies (global scratch only for huge rows)
     double* x = P.interp_lds >= 0 ? reinterpret_cast<double*>(smem + P.interp_lds)
                                   : P.interp_scratch + (size_t)e * P.interp_stride;
-    for (int i = threadIdx.x; i < L; i += kBlock) x[i] = (double)diff[i] * P.scale;
+    if (P.interp_stage) {
+        // piled by the row-wave kernel into the row's stage words (rcp_pileup_rows_kernel)
+        const uint32_t* src = P.rm32 + (size_t)r * (size_t)P.n_cols + part.col_off;
+        for (int i = threadIdx.x; i < L; i += kBlock) x[i] = (double)src[i] * P.scale;
+    } else {
+        block_window_depth(P, r, head, L, diff, scratch);
+        for (int i = threadIdx.x; i < L; i += kBlock) x[i] = (double)diff[i] * P.scale;
+    }
     __syncthreads();
     interp_finish(mode, L, n, x, mode == 3 ? P.nb_pos + P.interp_pos[e] : nullptr, P.spl_tb,
                   out + (size_t)part.col_off * R + r, R);
@@ -3399,7 +3411,7 @@ static bool interp_in_lds(const RcpPlanDev* P) {
     // (the spline's arrays in global scratch instead, which lets every row's block be resident
     // at once, measured slower alone on C3: 0.128 vs 0.123 ms, profiles/r02h/c3_transpose_interp_ab.log;
     // beside the row-wave pileup the smaller block is what fits, interp_lds_budget)
-    const size_t budget = P->interp_lds_budget > 0 ? (size_t)P->interp_lds_budget : 160 * 1024;
+    const size_t budget = (P->interp_lds_budget > 0 && !P->interp_stage) ? (size_t)P->interp_lds_budget : 160 * 1024;
     return interp_int_bytes(P) + 8 * (size_t)P->interp_stride + 16 <= budget;
 }
 

@@ -215,7 +215,11 @@ typedef struct {
                                  * sample's locate and heavy
                                  * launches run beside this pileup (C4, 2 samples in flight:
                                  * 0.600-0.627 -> 0.580-0.596 ms per pass; alone 0.61 -> 0.67) */
-    int32_t reserved[2];        /* zero */
+    int32_t row_split;          /* small tables: 0 = auto -- a general-kernel plan of 4096..65536 rows with
+                                 * AUTO kernel choice runs as 3 row blocks, each its own plan on its own
+                                 * HIP stream forked from the caller's (one table's locate beside another
+                                 * block's pileup: the C4 1/8 shard's pass), 1 = one block */
+    int32_t reserved[1];        /* zero */
 } rcp_plan_opts;
 #define RCP_OUT_LD_PADDED (-1)
 RCP_API int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,
@@ -328,7 +332,7 @@ RCP_API int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_samples,
  * starts; the slices' order is checked on the device and a sample that proves unsorted is redone
  * whole) goes up while block b - 1's rows of the matrix come down; any other sample goes up whole
  * while the previous one's matrix comes down.  Both PCIe directions at once (the one-shot
- * rcp_readset_create + rcp_profile uses one direction at a time); at most three readsets are on
+ * rcp_readset_create + rcp_profile uses one direction at a time); at most four readsets are on
  * the device.  Bit-identical to rcp_profile per sample. */
 RCP_API int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_samples, const rcp_rows_desc* rows,
                               const rcp_bins_desc* bins, double* const* outs, uint8_t* const* row_valid);

@@ -15,10 +15,18 @@ namespace {
 // b_i and multipliers t_i = 1 / b_{i-1} do not depend on y: the host tabulates them once
 // per plan (P.spl_tb, same operations in the same order), so the forward elimination is
 // the dependent chain c_i = c_i - t_i c_{i-1} alone (one multiply, one subtract per step)
-// and the back substitution divides by tabulated pivots; both chains run on thread 0 with
-// the next 8 table / LDS values loaded ahead.  Data-parallel loops run over the block.
+// and the back substitution divides by tabulated pivots; both chains run in
+// the first wave's registers (below).  Data-parallel loops run over the block.
 // Same operations in the same order per element as R: bit-equal.
 // Call from all threads of the block; y, b, c, d in LDS (or global), 0-based.
+// lane j's double to every lane (j wave-uniform): two v_readlane, no LDS permute
+__device__ __forceinline__ double lane_bcast(double v, int j) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), j);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 __device__ void fmm_spline_block(int n, const double* y, double* b, double* __restrict__ c, double* d,
                                  const double* __restrict__ tb) {
     const int t = threadIdx.x;
@@ -46,36 +54,63 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
         tp[i] = tb[2 * i + 1];
     }
     __syncthreads();
-    if (t == 0) {
-        double c1 = 0.0, cn = 0.0;
+    // The two chains run in the first wave's REGISTERS: lane l holds elements 4 l .. 4 l + 3 of a
+    // 256-element segment (c, the multipliers, the pivots and their reciprocals), and the lanes
+    // take their turns in order, the running value passed on by v_readlane -- each step is its
+    // dependent arithmetic alone, not an LDS round trip (thread 0 walking LDS spent ~80 cycles a
+    // step: tools/spline_timing.hip).  Same operations in the same order: the same bits.
+    if (t < 64) {
+        constexpr int V = 4, SEG = 64 * V;  // elements per lane, per segment
+        const int lane = t;
+        double c1 = 0.0, cn = 0.0;  // (every lane: the same operations)
         if (n > 3) {
             c1 = c[2] / 2.0 - c[1] / 2.0;
             cn = c[n - 2] / 2.0 - c[n - 3] / 2.0;
             c1 = c1 / 3.0;  // * d[1] * d[1] (= 1) / 3
             cn = -cn / 3.0;
         }
-        c[0] = c1;
-        c[n - 1] = cn;
-        // forward elimination: t = d[i-1] / b[i-1]; b[i] -= t d[i-1]; c[i] -= t c[i-1]
+        // forward elimination: t = d[i-1] / b[i-1]; b[i] -= t d[i-1]; c[i] -= t c[i-1], i = 1 .. n-1.
+        // The padding past n - 1 enters as zeros, so the lanes' V steps run unconditionally (the
+        // padding is never stored, and c[n - 1] is read back below); element 0 (lane 0 of the
+        // first segment) is kept as c1 by the one conditional turn
         double cp = c1;
-        int i = 1;
-        for (; i + 8 <= n; i += 8) {
-            double cv[8], tv[8];
+        for (int s0 = 0; s0 < n; s0 += SEG) {
+            double cv[V], tv[V];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                cv[u] = c[i + u];
-                tv[u] = tt[i + u];
+            for (int u = 0; u < V; ++u) {
+                const int i = s0 + V * lane + u;
+                cv[u] = i == 0 ? c1 : (i == n - 1 ? cn : (i < n ? c[i] : 0.0));
+                tv[u] = (i >= 1 && i < n) ? tt[i] : 0.0;
+            }
+            const int last = min(63, (n - 1 - s0) / V);
+            for (int j = 0; j <= last; ++j) {
+                if (lane == j) {
+                    if (s0 == 0 && j == 0) {
+#pragma unroll
+                        for (int u = 1; u < V; ++u) {
+                            cp = cv[u] - tv[u] * cp;
+                            cv[u] = cp;
+                        }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < V; ++u) {
+                            cp = cv[u] - tv[u] * cp;
+                            cv[u] = cp;
+                        }
+                    }
+                }
+                cp = lane_bcast(cp, j);
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                cp = cv[u] - tv[u] * cp;
-                c[i + u] = cp;
+            for (int u = 0; u < V; ++u) {
+                const int i = s0 + V * lane + u;
+                if (i < n) c[i] = cv[u];
             }
         }
-        for (; i < n; ++i) {
-            cp = c[i] - tt[i] * cp;
-            c[i] = cp;
-        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        cp = c[n - 1];  // (the padding steps ran past it)
         const double bn = -1.0 - tt[n - 1];  // b[n-1] = -1 - t_{n-1}
         // back substitution: c[i] = (c[i] - c[i+1]) / b[i].  The pivot's reciprocal is in the
         // table already -- t_{i+1} = RN(1 / b_i), the host's IEEE division -- so each quotient is
@@ -83,34 +118,88 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
         // FMA is the correctly rounded x / b (Markstein), i.e. the division's bits, in three
         // dependent operations instead of the division's ten; zeros (signed) and extreme
         // exponents, where the theorem's assumptions fail, take the division itself
-        auto quot = [](double x, double b, double y) -> double {
+        // (the range test is off the dependent path: a segment any of whose steps left it is run
+        // again with the division itself -- never on coverage data)
+        // (+0 too: RN(+0 y) corrected is the division's signed zero for either sign of b; -0, which
+        // coverage data never makes, and tiny or huge x take the division)
+        auto in_range = [](double x) -> bool {
             const double ax = __builtin_fabs(x);
-            if (!(ax >= 0x1p-960 && ax <= 0x1p+960)) return x / b;
-            const double q = x * y;
-            return __builtin_fma(__builtin_fma(-q, b, x), y, q);
+            return (ax >= 0x1p-960 && ax <= 0x1p+960) || __builtin_bit_cast(uint64_t, x) == 0;
         };
-        double cnext = cp / bn;
-        c[n - 1] = cnext;
-        i = n - 2;
-        for (; i >= 7; i -= 8) {
-            double cv[8], bv[8], yv[8];
+        double cnext = cp / bn;  // c[n-1]
+        const int jn = ((n - 1) % SEG) / V;  // the lane holding element n - 1 in the last segment
+        for (int s0 = ((n - 1) / SEG) * SEG; s0 >= 0; s0 -= SEG) {
+            double cv[V], bv[V], yv[V];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                cv[u] = c[i - u];
-                bv[u] = tp[i - u];
-                yv[u] = tt[i - u + 1];
+            for (int u = 0; u < V; ++u) {
+                const int i = s0 + V * lane + u;
+                cv[u] = i < n ? c[i] : 0.0;
+                bv[u] = i < n ? tp[i] : 1.0;
+                yv[u] = i + 1 < n ? tt[i + 1] : 1.0;
+            }
+            const bool top = s0 + SEG >= n;  // the segment holding element n - 1
+            const double centry = cnext;
+            for (int exact = 0; exact < 2; ++exact) {
+                bool off = false;
+                double w[V];
+#pragma unroll
+                for (int u = 0; u < V; ++u) w[u] = cv[u];
+                cnext = centry;
+                for (int j = top ? jn : 63; j >= 0; --j) {
+                    if (lane == j) {
+                        if (top && j == jn) {  // element n - 1 and the padding above it
+#pragma unroll
+                            for (int u = V - 1; u >= 0; --u) {
+                                const int i = s0 + V * j + u;
+                                if (i == n - 1) {
+                                    w[u] = cnext;
+                                } else if (i < n - 1) {
+                                    const double x = w[u] - cnext;
+                                    if (exact) {
+                                        cnext = x / bv[u];
+                                    } else {
+                                        off |= !in_range(x);
+                                        const double q = x * yv[u];
+                                        cnext = __builtin_fma(__builtin_fma(-q, bv[u], x), yv[u], q);
+                                    }
+                                    w[u] = cnext;
+                                }
+                            }
+                        } else if (exact) {
+#pragma unroll
+                            for (int u = V - 1; u >= 0; --u) {
+                                cnext = (w[u] - cnext) / bv[u];
+                                w[u] = cnext;
+                            }
+                        } else {
+#pragma unroll
+                            for (int u = V - 1; u >= 0; --u) {
+                                const double x = w[u] - cnext;
+                                off |= !in_range(x);
+                                const double q = x * yv[u];
+                                cnext = __builtin_fma(__builtin_fma(-q, bv[u], x), yv[u], q);
+                                w[u] = cnext;
+                            }
+                        }
+                    }
+                    cnext = lane_bcast(cnext, j);
+                }
+                if (!__builtin_amdgcn_ballot_w64(off)) {  // (exact: off stays false)
+#pragma unroll
+                    for (int u = 0; u < V; ++u) cv[u] = w[u];
+                    break;
+                }
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                cnext = quot(cv[u] - cnext, bv[u], yv[u]);
-                c[i - u] = cnext;
+            for (int u = 0; u < V; ++u) {
+                const int i = s0 + V * lane + u;
+                if (i < n) c[i] = cv[u];
             }
         }
-        for (; i >= 0; --i) {
-            cnext = quot(c[i] - cnext, tp[i], tt[i + 1]);
-            c[i] = cnext;
-        }
-        b[n - 1] = (y[n - 1] - y[n - 2]) + (c[n - 2] + 2.0 * c[n - 1]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0) b[n - 1] = (y[n - 1] - y[n - 2]) + (c[n - 2] + 2.0 * c[n - 1]);
     }
     __syncthreads();
     // coefficients: b[i] = (y[i+1] - y[i]) - (c[i+1] + 2 c[i]); d[i] = c[i+1] - c[i]; c[i] *= 3

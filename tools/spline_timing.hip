@@ -36,6 +36,20 @@ __global__ void __launch_bounds__(256) spline_rows(int L, int n, const double* t
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// cycles per step of a dependent FP64 chain in one lane (mul + sub, no contraction), for scale
+#pragma clang fp contract(off)
+__global__ void chain_latency(double a, double b, int steps, double* out, long long* cyc) {
+    double x = (double)threadIdx.x;
+    const long long t0 = clock64();
+    for (int i = 0; i < steps; ++i) x = b - a * x;
+    const long long t1 = clock64();
+    if (threadIdx.x == 0) {
+        out[0] = x;
+        cyc[0] = t1 - t0;
+    }
+}
+#pragma clang fp contract(on)
+
 int main(int argc, char** argv) {
     const int B = argc > 1 ? atoi(argv[1]) : 1555;
     const int L = argc > 2 ? atoi(argv[2]) : 300;
@@ -77,6 +91,15 @@ int main(int argc, char** argv) {
             std::printf("%s B=%d L=%d n=%d: kernel %.1f us, cycles per block mean %lld max %lld\n",
                         phase ? "spline + eval" : "fmm chains  ", B, L, n, ms * 1e3, sum / B, mx);
         }
+    }
+    {
+        const int steps = 10000;
+        hipLaunchKernelGGL(chain_latency, dim3(1), dim3(64), 0, 0, 0.25, 1.5, steps, d_out, d_cyc);
+        CK(hipDeviceSynchronize());
+        hipLaunchKernelGGL(chain_latency, dim3(1), dim3(64), 0, 0, 0.25, 1.5, steps, d_out, d_cyc);
+        long long c = 0;
+        CK(hipMemcpy(&c, d_cyc, 8, hipMemcpyDeviceToHost));
+        std::printf("dependent fp64 mul + sub: %.1f cycles per step\n", (double)c / steps);
     }
     return 0;
 }

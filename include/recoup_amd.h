@@ -215,11 +215,7 @@ typedef struct {
                                  * sample's locate and heavy
                                  * launches run beside this pileup (C4, 2 samples in flight:
                                  * 0.600-0.627 -> 0.580-0.596 ms per pass; alone 0.61 -> 0.67) */
-    int32_t row_split;          /* small tables: 0 = auto -- a general-kernel plan of 4096..65536 rows with
-                                 * AUTO kernel choice runs as 3 row blocks, each its own plan on its own
-                                 * HIP stream forked from the caller's (one table's locate beside another
-                                 * block's pileup: the C4 1/8 shard's pass), 1 = one block */
-    int32_t reserved[1];        /* zero */
+    int32_t reserved[2];        /* zero */
 } rcp_plan_opts;
 #define RCP_OUT_LD_PADDED (-1)
 RCP_API int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* rows, const rcp_bins_desc* bins,

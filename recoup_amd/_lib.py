@@ -76,7 +76,7 @@ class RleDesc(ctypes.Structure):
 class PlanOpts(ctypes.Structure):
     _fields_ = [("pileup_kernel", ctypes.c_int32), ("heavy_threshold", ctypes.c_int32),
                 ("out_ld", ctypes.c_int64), ("min_col_chunks", ctypes.c_int32), ("concurrent", ctypes.c_int32),
-                ("row_split", ctypes.c_int32), ("reserved", ctypes.c_int32 * 1)]
+                ("reserved", ctypes.c_int32 * 2)]
 
 
 # every symbol include/recoup_amd.h declares: (name, restype, argtypes)

@@ -227,10 +227,7 @@ constexpr int kDirReads = 8;  // mean reads per directory bucket (the locate ker
 constexpr int kHeavySlice = 4096;  // candidate reads per heavy work item
 constexpr int kHeavyMaxLen = 16383;    // longer rows never take the heavy path
 constexpr int kHeavyGrid = 4096;
-constexpr int kGeneralMaxChunks = 8;
-// small general-kernel tables run as row blocks (rcp_plan_opts.row_split)
-constexpr int kSplitBlocks = 3;
-constexpr int32_t kSplitMinRows = 4096, kSplitMaxRows = 65536;  // column chunks a wide binned part is cut into (general kernel)
+constexpr int kGeneralMaxChunks = 8;  // column chunks a wide binned part is cut into (general kernel)
 
 // A wave's difference array: 64 lanes x per positions (per a power of two >= 4), each lane's
 // chunk padded by 4 words (rcp_kernels.hip scan_wave).  Returns the LDS words and the
@@ -851,7 +848,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
                                   const rcp_plan_opts* opts, rcp_plan** out) {
     RCP_TRY
     if (!rs || !rows || !out) return fail(RCP_EINVAL, "NULL argument");
-    const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, 0, 0, 0, 0, {0}};
+    const rcp_plan_opts default_opts{RCP_KERNEL_AUTO, -1, 0, 0, 0, {0, 0}};
     if (!opts) opts = &default_opts;
     if (opts->pileup_kernel < RCP_KERNEL_AUTO || opts->pileup_kernel > RCP_KERNEL_BINS)
         return fail(RCP_EINVAL, "pileup_kernel = %d", opts->pileup_kernel);
@@ -1436,33 +1433,6 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     HIP_TRY(hipMemsetAsync(plan->work.p, 0, plan->work.bytes, nullptr));
     HIP_TRY(hipStreamSynchronize(nullptr));
     PLAN_MARK("memset");
-    // ---- a small general-kernel table as row blocks on their own streams (rcp_plan_opts.row_split):
-    // one table's pass is then a few independent grids -- one block's locate (a latency-bound chain
-    // of probes) beside another's pileup -- instead of locate, then a pileup grid of one or two
-    // workgroup generations.  Same bits: rows are independent.
-    if (!cov_only && P.lean == 0 && !P.fold && opts->row_split == 0 && opts->pileup_kernel == RCP_KERNEL_AUTO &&
-        opts->concurrent <= 1 && R >= kSplitMinRows && R <= kSplitMaxRows) {
-        rcp_plan_opts so = *opts;
-        so.pileup_kernel = RCP_KERNEL_GENERAL;  // (what AUTO chose for the table)
-        so.out_ld = plan->out_ld;               // the blocks write rows of the table's matrix
-        so.concurrent = kSplitBlocks;
-        so.row_split = 1;
-        for (int k = 0; k < kSplitBlocks; ++k) {
-            // blocks of whole 16-row tiles (each block's column segments start on 128-B lines)
-            const int32_t r0 = (int32_t)((int64_t)R * k / kSplitBlocks) & ~15;
-            const int32_t r1 = k + 1 == kSplitBlocks ? R : ((int32_t)((int64_t)R * (k + 1) / kSplitBlocks) & ~15);
-            rcp_rows_desc sub = *rows;
-            sub.n_rows = r1 - r0;
-            sub.seg_off = rows->seg_off + r0;
-            rcp_plan* sp = nullptr;
-            const int e = rcp_plan_create_ex(rs, &sub, bins, &so, &sp);
-            if (e) return e;  // (the parts made so far go with `plan`)
-            plan->parts.push_back(sp);
-            plan->part_row0.push_back(r0);
-        }
-        // (the table's own arrays stay: calcCoverage of this plan, rcp_calc_coverage, runs on them)
-        PLAN_MARK("row blocks");
-    }
     *out = plan.release();
     return RCP_OK;
     RCP_CATCH
@@ -1502,47 +1472,12 @@ extern "C" int rcp_plan_row_lengths(const rcp_plan* plan, int64_t* out_len) {
     RCP_CATCH
 }
 
-namespace {
-
-// fn(part, stream) for every row block of a split plan, each on its own stream forked from s and
-// joined back into it
-template <class F>
-int for_parts(rcp_plan* plan, hipStream_t s, F fn) {
-    const size_t K = plan->parts.size();
-    if (plan->part_streams.empty()) {
-        HIP_TRY(hipEventCreateWithFlags(&plan->ev_split, hipEventDisableTiming));
-        for (size_t k = 0; k < K; ++k) {
-            hipStream_t x = nullptr;
-            HIP_TRY(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
-            plan->part_streams.push_back(x);
-            hipEvent_t e = nullptr;
-            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            plan->part_joins.push_back(e);
-        }
-    }
-    HIP_TRY(hipEventRecord(plan->ev_split, s));
-    for (size_t k = 0; k < K; ++k) {
-        HIP_TRY(hipStreamWaitEvent(plan->part_streams[k], plan->ev_split, 0));
-        const int e = fn(plan->parts[k], plan->part_row0[k], plan->part_streams[k]);
-        if (e) return e;
-        HIP_TRY(hipEventRecord(plan->part_joins[k], plan->part_streams[k]));
-    }
-    for (size_t k = 0; k < K; ++k) HIP_TRY(hipStreamWaitEvent(s, plan->part_joins[k], 0));
-    return RCP_OK;
-}
-
-}  // namespace
-
 extern "C" int rcp_plan_validity(rcp_plan* plan, uint8_t* d_valid, void* hip_stream) {
     RCP_TRY
     if (!plan) return fail(RCP_EINVAL, "NULL plan");
     DeviceGuard g(plan->rs->device);
     HIP_TRY(g.err);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    if (!plan->parts.empty())
-        return for_parts(plan, s, [&](rcp_plan* q, int32_t r0, hipStream_t x) {
-            return rcp_plan_validity(q, d_valid ? d_valid + r0 : nullptr, x);
-        });
     begin_exec(plan);
     RcpPlanDev Q = plan->dev;
     Q.valid_out = d_valid;
@@ -1562,11 +1497,6 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
     DeviceGuard g(plan->rs->device);
     HIP_TRY(g.err);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    if (!plan->parts.empty())
-        return for_parts(plan, s, [&](rcp_plan* q, int32_t r0, hipStream_t x) {
-            return rcp_plan_execute_stages(q, d_out ? d_out + r0 : nullptr, d_valid ? d_valid + r0 : nullptr,
-                                           d_binsum ? d_binsum + r0 : nullptr, x, stages);
-        });
     if (stages & RCP_STAGE_LOCATE) {
         // locate (also clears the previous execution's heavy slots and status words, and writes
         // the caller's validity vector), heavy slices; a folded plan's pileup kernel does both
@@ -1621,10 +1551,6 @@ extern "C" int rcp_plan_status(rcp_plan* plan, void* hip_stream) {
     DeviceGuard g(plan->rs->device);
     HIP_TRY(g.err);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    for (rcp_plan* q : plan->parts) {  // (then the table's own: a coverage pass runs on it)
-        const int e = rcp_plan_status(q, hip_stream);
-        if (e) return e;
-    }
     uint32_t st = 0;
     HIP_TRY(hipMemcpyAsync(&st, plan->dev.status, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -1642,17 +1568,6 @@ extern "C" int rcp_plan_heavy_rows(rcp_plan* plan, void* hip_stream, int32_t* n_
     DeviceGuard g(plan->rs->device);
     HIP_TRY(g.err);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    if (!plan->parts.empty()) {
-        int32_t sum = 0;
-        for (rcp_plan* q : plan->parts) {
-            int32_t m = 0;
-            const int e = rcp_plan_heavy_rows(q, hip_stream, &m);
-            if (e) return e;
-            sum += m;
-        }
-        *n_rows = sum;
-        return RCP_OK;
-    }
     uint32_t n = 0;
     HIP_TRY(hipMemcpyAsync(&n, plan->dev.status + 1, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -1667,7 +1582,7 @@ extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, con
     rcp_plan* plan = nullptr;
     // padded column stride on the device (whole 128-B lines per 16-row column segment); the
     // staged copy drops the padding on the way into R's n_rows x n_cols matrix
-    rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, 0, 0, {0}};
+    rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, 0, {0, 0}};
     int rc = rcp_plan_create_ex(rs, rows, bins, &opts, &plan);
     if (rc) return rc;
     std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);
@@ -2082,8 +1997,7 @@ extern "C" int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_sample
             int64_t nc = 0;
             int e = abort ? (int)RCP_OK
                           : profile_block(it.rs, &sub, bins, outs ? outs[it.sample] : nullptr, R, it.r0,
-                                          row_valid ? row_valid[it.sample] : nullptr, &nc, s,
-                                          it.redo || it.r1 - it.r0 == R ? 0 : 1);  // (blocks: one plan each)
+                                          row_valid ? row_valid[it.sample] : nullptr, &nc, s);
             if (tr)
                 fprintf(stderr, "[reads] sample %d rows [%d, %d): profile + down %.2f ms (at %.2f)\n", it.sample, it.r0,
                         it.r1, rcp::trace_ms() - tb, tb - t0);
@@ -2129,7 +2043,7 @@ extern "C" int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_sampl
     plans.reserve(n_samples);
     for (int i = 0; i < n_samples; ++i) {
         rcp_plan* plan = nullptr;
-        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, D, 0, {0}};  // D passes in flight
+        rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, D, {0, 0}};  // D passes in flight
         const int e = rcp_plan_create_ex(readsets[i], rows, bins, &opts, &plan);
         if (e) return e;
         plans.emplace_back(plan, rcp_plan_destroy);
@@ -2187,12 +2101,11 @@ extern "C" int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_sampl
 namespace rcpi {
 
 int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bins_desc* bins, double* out,
-                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream,
-                  int row_split) {
+                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream) {
     const bool tr = rcp::trace_on();
     const double t0 = tr ? rcp::trace_ms() : 0.0;
     rcp_plan* plan = nullptr;
-    rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, 0, row_split, {0}};
+    rcp_plan_opts opts{RCP_KERNEL_AUTO, -1, RCP_OUT_LD_PADDED, 0, 0, {0, 0}};
     int e = rcp_plan_create_ex(rs, sub, bins, &opts, &plan);
     if (e) return e;
     std::unique_ptr<rcp_plan, int (*)(rcp_plan*)> guard(plan, rcp_plan_destroy);

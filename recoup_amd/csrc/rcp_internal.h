@@ -216,10 +216,9 @@ int run_per_device(int n, F fn) {
 // Block [r0, r0 + sub->n_rows) of an n_rows_total-row profile on readset rs: plan, execute, and
 // copy its rows of every column into the caller's R column-major matrix `out` (may be NULL) and
 // row_valid + r0 (may be NULL); *n_cols receives the plan's column count.  On `stream` (NULL: a
-// stream of its own); row_split as rcp_plan_opts'; returns with the copies done (rcp_host.cpp)
+// stream of its own); returns with the copies done (rcp_host.cpp)
 int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bins_desc* bins, double* out,
-                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream = nullptr,
-                  int row_split = 0);
+                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream = nullptr);
 
 // rcp_profile_rle into rows [0, n_rows) of a matrix with column stride out_ld, on stream s
 // (rcp_host.cpp)
@@ -380,18 +379,7 @@ struct rcp_plan {
     hipEvent_t ev_done = nullptr;  // recorded after every execution (rcp_host.cpp end_exec)
     hipStream_t last = nullptr;    // the executions' stream, when n_streams == 1
     int n_streams = 0;             // 0, 1, 2 = several
-    // a small table run as row blocks (rcp_plan_opts.row_split): each block its own plan, executed
-    // on its own stream forked from the caller's (this plan's own arrays serve calcCoverage)
-    std::vector<rcp_plan*> parts;
-    std::vector<int32_t> part_row0;
-    std::vector<hipStream_t> part_streams;
-    std::vector<hipEvent_t> part_joins;
-    hipEvent_t ev_split = nullptr;
     ~rcp_plan() {  // (on the plan's device: rcp_plan_destroy)
-        for (rcp_plan* q : parts) delete q;  // (each waits for its own last execution)
-        for (hipEvent_t e : part_joins) (void)hipEventDestroy(e);
-        for (hipStream_t x : part_streams) (void)hipStreamDestroy(x);
-        if (ev_split) (void)hipEventDestroy(ev_split);
         if (n_streams > 1) (void)hipDeviceSynchronize();
         else if (ev_done) (void)hipEventSynchronize(ev_done);
         if (ev_done) (void)hipEventDestroy(ev_done);

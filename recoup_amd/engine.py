@@ -224,7 +224,7 @@ class Plan:
     """One fused coverage -> profile pass of ``rows`` over ``readset`` with ``bins``."""
 
     def __init__(self, readset, rows, bins, kernel="auto", heavy_threshold=-1, out_ld=0, min_col_chunks=0,
-                 concurrent=0, row_split=0):
+                 concurrent=0):
         """``kernel``: "auto" | "general" | "lean" | "lean_any" | "rows" (rcp_plan_opts.pileup_kernel; every choice
         gives bit-identical results); ``heavy_threshold``: -1 default, 0 off; ``out_ld``: the
         output's column stride, 0 = n_rows, "padded" = the next multiple of 16 (whole 128-B
@@ -238,7 +238,7 @@ class Plan:
         bd = ctypes.byref(bins.desc()) if bins is not None else None
         ld = -1 if out_ld == "padded" else int(out_ld)
         opts = _lib.PlanOpts(KERNEL[kernel] if isinstance(kernel, str) else int(kernel), int(heavy_threshold), ld,
-                             int(min_col_chunks), int(concurrent), int(row_split))
+                             int(min_col_chunks), int(concurrent))
         h = ctypes.c_void_p()
         with torch.cuda.device(readset.device):
             check(_lib.lib().rcp_plan_create_ex(readset.h, ctypes.byref(rd), bd, ctypes.byref(opts),

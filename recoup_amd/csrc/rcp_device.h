@@ -140,7 +140,10 @@ struct RcpPlanDev {
     int32_t interp_lds_budget;  // LDS bytes an interpolation block may take so that it runs beside the
                                 // persistent pileup workgroups (the rest of a CU's 160 KB); 0 = all
     int32_t interp_stage;       // per execution: the row-wave kernel (HBM stage) piles the interpolated
-                                // parts into rm32 and rcp_interp_kernel, launched after it, reads them
+                                // parts and interpolates them itself (interp_of) -- or, without that
+                                // table, stages them in rm32 for rcp_interp_kernel launched after it
+    const int32_t* interp_of;   // row-wave plans: [n_rows][n_parts] interpolation entry or -1
+    const int32_t* tile_perm;   // row-wave plans with interp_of: the order 16-row tiles are claimed in
     // geometry
     int32_t chunk_cap;          // max positions per chunk (one wave's difference array)
     int32_t wave_words;         // LDS words per wave difference array (multiple of 256)

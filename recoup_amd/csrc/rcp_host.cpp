@@ -1022,6 +1022,11 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
                     cb = (pt.n_bins + nch - 1) / nch;
                 }
             }
+            // opts->min_col_chunks (one-part plans): at least that many column chunks
+            if (!median && P.n_parts == 1 && opts->min_col_chunks > nch) {
+                nch = std::min<int32_t>(std::min(opts->min_col_chunks, RCP_MAX_CRANGE_CHUNKS), pt.n_bins);
+                cb = (pt.n_bins + nch - 1) / nch;
+            }
             if (median) cb = std::min<int32_t>(cb, std::max<int32_t>(1, kWaveMax / part_max_bin[p]));
             pt.chunk_bins = cb;
             pt.n_chunks = (pt.n_bins + cb - 1) / cb;
@@ -1123,8 +1128,13 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
             if (!P.part[p].per_base && part_max_bin[p] > rcp_rows_window_cap()) rows_ok = false;
         bool multi_rows = false;
         for (int r = 0; !multi_rows && r < R; ++r) multi_rows = B.row_seg[r + 1] - B.row_seg[r] > 1;
-        if (rows_ok && (kind == RCP_KERNEL_ROWS || (kind == RCP_KERNEL_AUTO && multi_rows)))
+        if (rows_ok && (kind == RCP_KERNEL_ROWS || (kind == RCP_KERNEL_AUTO && multi_rows))) {
             P.lean = 3;
+            // each wave searches its rows' (segment, stream) ranges itself (no locate launch, no
+            // 64-B record round trip; a skewed row stays with the wave that claimed it) unless
+            // the caller asked for the heavy path
+            P.fold = opts->heavy_threshold <= 0 ? 1 : 0;
+        }
     }
     // ---- bin-difference kernel (lean == 4): mean plans of one binned part whose rows are
     // single ranges, every row's slice a whole number of bins of >= rcp_bins_min_width()
@@ -1227,6 +1237,26 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     const size_t o_ipart = blob.add(B.interp_part);
     const size_t o_imode = blob.add(B.interp_mode);
     const size_t o_ipos = blob.add(B.interp_pos);
+    // row-wave plans interpolate the rows they pile (rcp_pileup_rows_kernel): entry of (row, part)
+    std::vector<int32_t> interp_of;
+    if (P.lean == 3 && !B.interp_row.empty()) {
+        interp_of.assign((size_t)R * P.n_parts, -1);
+        for (size_t e = 0; e < B.interp_row.size(); ++e)
+            interp_of[(size_t)B.interp_row[e] * P.n_parts + B.interp_part[e]] = (int32_t)e;
+    }
+    const size_t o_iof = blob.add(interp_of);
+    // ... and claim the 16-row tiles holding such rows first, most first: the spline's serial
+    // chains then run beside the other waves' pileup, not in the grid's tail
+    std::vector<int32_t> tile_perm;
+    if (!interp_of.empty()) {
+        const int32_t n_tiles = (R + 15) / 16;
+        std::vector<int32_t> cnt(n_tiles, 0);
+        for (int32_t r : B.interp_row) ++cnt[r / 16];
+        tile_perm.resize(n_tiles);
+        for (int32_t t = 0; t < n_tiles; ++t) tile_perm[t] = t;
+        std::stable_sort(tile_perm.begin(), tile_perm.end(), [&](int32_t a, int32_t b) { return cnt[a] > cnt[b]; });
+    }
+    const size_t o_tperm = blob.add(tile_perm);
     const size_t o_nb = blob.add(B.nb_pos);
     // locate's per-row input (RcpRowInfo)
     std::vector<RcpRowInfo> row_info((size_t)std::max(R, 1));
@@ -1383,6 +1413,8 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     P.interp_part = reinterpret_cast<const int32_t*>(base + o_ipart);
     P.interp_mode = reinterpret_cast<const int32_t*>(base + o_imode);
     P.interp_pos = reinterpret_cast<const int32_t*>(base + o_ipos);
+    P.interp_of = interp_of.empty() ? nullptr : reinterpret_cast<const int32_t*>(base + o_iof);
+    P.tile_perm = tile_perm.empty() ? nullptr : reinterpret_cast<const int32_t*>(base + o_tperm);
     P.nb_pos = reinterpret_cast<const int32_t*>(base + o_nb);
     P.spl_tb = reinterpret_cast<const double*>(base + o_spl);
     P.interp_scratch = plan->scratch.as<double>();
@@ -1515,7 +1547,7 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
     // beside the pileup, joining the caller's stream after it
     plan->dev.interp_stage = (plan->dev.lean == 3 && plan->dev.rm32 && !d_binsum) ? 1 : 0;
     const bool fork = (stages & RCP_STAGE_PILEUP) && (stages & RCP_STAGE_INTERP) && plan->dev.n_interp > 0 &&
-                      !plan->dev.interp_stage;
+                      !plan->dev.interp_stage && !plan->dev.fold;  // (folded: the pileup kernel locates)
     if (fork) {
         if (!plan->side) {
             HIP_TRY(hipStreamCreateWithFlags(&plan->side, hipStreamNonBlocking));
@@ -1532,8 +1564,11 @@ extern "C" int rcp_plan_execute_stages(rcp_plan* plan, double* d_out, uint8_t* d
         if (Q.fold) Q.valid_out = d_valid;
         HIP_TRY(rcp_launch_pileup(&Q, d_out, d_binsum, 0, s));
     }
+    // (row-wave plans with the HBM stage interpolate in the pileup kernel: the wave that piled
+    // the row runs its spline)
+    const bool fused = plan->dev.interp_stage && plan->dev.interp_of;
     if (fork) HIP_TRY(hipStreamWaitEvent(s, plan->ev_join, 0));
-    else if (stages & RCP_STAGE_INTERP) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
+    else if ((stages & RCP_STAGE_INTERP) && !fused) HIP_TRY(rcp_launch_interp(&plan->dev, d_out, s));
     return end_exec(plan, s);
     RCP_CATCH
 }

@@ -1824,6 +1824,8 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
 
 
 
+#include "rcp_splitvector.h"  // splitVector interpolation (also rcp_interp_kernel below)
+
 // ---------------------------------------------------------------------------------
 // Row-wave pileup kernel (mean bins; P.lean == 3): every wave owns whole rows.  For plans
 // whose rows are lists of ranges (coverageRnaRef's c(flank, exons, flank), genebody rows with
@@ -1917,6 +1919,9 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         slot_cnt[threadIdx.x] = kFree;
     }
     if (threadIdx.x == 0) *seq = 0;
+    // a folded plan launches no locate / heavy kernel: zero the status set the next execution
+    // uses here (nothing in this execution reads it)
+    if (P.fold && blockIdx.x == 0 && threadIdx.x < RCP_STATUS_WORDS) P.status_prev[threadIdx.x] = 0u;
     __syncthreads();
     constexpr bool staged = MODE != 0;
     auto fetch_tile = [&]() -> uint32_t {
@@ -1927,7 +1932,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             uint32_t j = 0;
             if (lane == 0) j = atomicAdd(&P.status[8 + xs], 1u);
             j = __builtin_amdgcn_readfirstlane(j);
-            if (j < nt) return j * 8 + xs;
+            if (j < nt) return P.tile_perm && P.interp_stage ? (uint32_t)P.tile_perm[j * 8 + xs] : j * 8 + xs;
         }
         return kDone;
     };
@@ -2038,40 +2043,157 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         }
     };
     auto row_body = [&](int r, int sl) {
-        const uint4 rc = *reinterpret_cast<const uint4*>(P.rec + r);  // flags, row_len, heavy, off
-        const int32_t flags = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.x);
-        const int32_t nr = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.y);
-        const int32_t heavy = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.z);
-        uint32_t* const srow = stage_row(r, sl);
-        int2* const sinfo = stage_info(r, sl);
-        if (staged && lane < P.n_parts) sinfo[lane] = make_int2(0, -1);  // zeros unless piled below
-        if (!(flags & RCP_REC_VALID)) {  // NULL row -> zeros (profile.R:191-197)
-            for (int p = 0; p < P.n_parts; ++p) zero_cols(r, P.part[p], P.part[p].n_bins);
-            return;
-        }
-
-        const int j0 = P.row_info[r].j0, j1 = P.row_info[r].j1;
-        const int64_t d0 = P.row_info[r].d0;
-        const int32_t dnb = P.row_info[r].nb;
+        const RcpRowInfo& ri = P.row_info[r];
+        const int j0 = ri.j0, j1 = ri.j1;
+        const int64_t d0 = ri.d0;
+        const int32_t dnb = ri.nb;
         const int n_all = (j1 - j0) * ns;
-        // lane t: pair t of the row (pairs 64.. are reloaded per window)
-        auto load_pair = [&](int t, RcpSeg& sg, uint32_t& lo, uint32_t& hi, int& st) {
+        int32_t flags = 0, nr = 0, heavy = -1;
+        uint32_t itp_parts = 0;  // parts this wave interpolates after the row (interp_rows)
+        if (P.fold) {
+            nr = ri.row_len;
+        } else {
+            const uint4 rc = *reinterpret_cast<const uint4*>(P.rec + r);  // flags, row_len, heavy, off
+            flags = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.x);
+            nr = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.y);
+            heavy = (int32_t)__builtin_amdgcn_readfirstlane((int)rc.z);
+        }
+        // P.fold: rcp_locate_kernel's searches for this row, here (bucket directory + bisection,
+        // dir_bound_multi).  Pairs t0 .. t0 + 63: in round k lane l searches bound l >> 5 (lower,
+        // upper) of pair t0 + 32 k + (l & 31) -- one search's directory line per lane, not two --
+        // and lane t then gathers pair t0 + t's two bounds; a second round only for > 32 pairs.
+        // Call with the whole wave.
+        const int32_t chrom = ri.chrom;
+        const bool rok = P.fold && !ri.stat && chrom >= 0 && chrom < P.n_chrom && j1 > j0;
+        auto fold_bounds = [&](int t0, uint32_t& lo, uint32_t& hi) {
+            uint32_t res[2] = {0u, 0u};
+            const int half = lane >> 5;
+            for (int k = 0; k < 2 && t0 + 32 * k < n_all; ++k) {  // (wave-uniform)
+                const int q = t0 + 32 * k + (lane & 31);
+                int64_t dd[1] = {d0};
+                int32_t nb1[1] = {dnb};
+                int32_t v[1] = {0};
+                const int dst[1] = {half ? -1 : -2};
+                int cnt = 0;
+                if (rok && q < n_all) {
+                    const int st = q % ns;
+                    const RcpSeg sg = P.segs[j0 + q / ns];
+                    if (sg.query_ok && ((sg.streams >> st) & 1)) {
+                        cnt = 1;
+                        v[0] = half ? sg.hi : sg.lo;
+                        if (!P.merged) {
+                            dd[0] = P.dir_off[chrom * 3 + st];
+                            nb1[0] = (int32_t)(P.dir_off[chrom * 3 + st + 1] - dd[0]) - 1;
+                        }
+                    }
+                }
+                uint32_t w[1];
+                dir_bound_multi<1>(P, dd, nb1, v, dst, cnt, w);
+                res[k] = w[0];
+            }
+            const int src = lane & 31;
+            const uint32_t l0 = (uint32_t)__shfl((int)res[0], src), h0 = (uint32_t)__shfl((int)res[0], src + 32);
+            const uint32_t l1 = (uint32_t)__shfl((int)res[1], src), h1 = (uint32_t)__shfl((int)res[1], src + 32);
+            lo = lane < 32 ? l0 : l1;
+            hi = max(lo, lane < 32 ? h0 : h1);
+        };
+        // lane t: pair t0 + t of the row (pairs 64.. are reloaded per window); the whole wave
+        auto load_pair = [&](int t0, RcpSeg& sg, uint32_t& lo, uint32_t& hi, int& st) {
+            const int t = t0 + lane;
             sg = RcpSeg{};
             lo = hi = 0;
             st = 0;
+            uint32_t flo = 0, fhi = 0;
+            if (P.fold) fold_bounds(t0, flo, fhi);
             if (t < n_all) {
                 const int j = j0 + t / ns;
                 st = t % ns;
                 sg = P.segs[j];
-                lo = P.seg_lo[j * 3 + st];
-                hi = P.seg_hi[j * 3 + st];
-                if (!sg.query_ok || !((sg.streams >> st) & 1)) hi = lo;
+                const bool use = sg.query_ok && ((sg.streams >> st) & 1);
+                if (P.fold) {
+                    lo = flo;
+                    hi = fhi;
+                } else {
+                    lo = P.seg_lo[j * 3 + st];
+                    hi = P.seg_hi[j * 3 + st];
+                }
+                if (!use) hi = lo;
             }
         };
         RcpSeg sg0;
         uint32_t plo0, phi0;
         int pst0;
-        load_pair(lane, sg0, plo0, phi0, pst0);
+        load_pair(0, sg0, plo0, phi0, pst0);
+        if (P.fold) {
+            // the NULL rules (R/coverage.R:189-225, as rcp_locate_kernel): every group of the row
+            // needs a hit, and its last position inside seqlength -- or, when that is NA, inside
+            // the group's hits' last end
+            const int64_t seqlen = ri.seqlen;
+            bool valid = rok;
+            const bool wide = P.n_interp > 0 && !P.interp_stage;  // rcp_interp_kernel piles from seg_lo / seg_hi
+            uint32_t present = 0, hit = 0, past = 0;
+            int32_t maxpos[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
+            int32_t maxend[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
+            for (int t0 = 0; rok && t0 < n_all; t0 += 64) {
+                RcpSeg sg = sg0;
+                uint32_t lo = plo0, hi = phi0;
+                int st = pst0;
+                if (t0 > 0) load_pair(t0, sg, lo, hi, st);
+                if (t0 + lane < n_all) {
+                    const int g = sg.group & 3;
+                    present |= 1u << g;
+                    if (lo < hi) hit |= 1u << g;
+                    if (seqlen >= 0) {
+                        if ((int64_t)sg.hi > seqlen) past |= 1u << g;
+                    } else {
+                        const int32_t me = lo < hi ? P.pmax[hi - 1] : INT32_MIN;
+#pragma unroll
+                        for (int gg = 0; gg < 4; ++gg) {  // (registers: no dynamically indexed array)
+                            if (gg == g) {
+                                maxpos[gg] = max(maxpos[gg], sg.hi);
+                                maxend[gg] = max(maxend[gg], me);
+                            }
+                        }
+                    }
+                    if (wide) {
+                        const int j = j0 + (t0 + lane) / ns;
+                        P.seg_lo[j * 3 + st] = lo;
+                        P.seg_hi[j * 3 + st] = hi;
+                    }
+                }
+            }
+            if (rok) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    if (!__ballot((present >> g) & 1)) continue;
+                    bool ok_g = __ballot((hit >> g) & 1) != 0;
+                    if (seqlen >= 0) {
+                        ok_g = ok_g && !__ballot((past >> g) & 1);
+                    } else {
+                        int32_t mp = maxpos[g], me = maxend[g];
+                        for (int o = 32; o > 0; o >>= 1) {
+                            mp = max(mp, __shfl_xor(mp, o));
+                            me = max(me, __shfl_xor(me, o));
+                        }
+                        ok_g = ok_g && mp <= me;
+                    }
+                    valid = valid && ok_g;
+                }
+            }
+            if (lane == 0) {
+                P.valid[r] = valid ? 1 : 0;
+                if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
+            }
+            flags = valid ? RCP_REC_VALID : 0;
+        }
+        uint32_t* const srow = stage_row(r, sl);
+        int2* const sinfo = stage_info(r, sl);
+        if (staged && lane < P.n_parts) sinfo[lane] = make_int2(0, -1);  // zeros unless piled below
+        if (!(flags & RCP_REC_VALID)) {  // NULL row -> zeros (profile.R:191-197)
+            for (int p = 0; p < P.n_parts; ++p) zero_cols(r, P.part[p], P.part[p].n_bins);
+            return itp_parts;
+        }
+
         for (int p = 0; p < P.n_parts; ++p) {
             const RcpPart part = P.part[p];
             int32_t head, L;
@@ -2087,6 +2209,11 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                 if (!staged || !P.interp_stage) continue;
             }
             const int32_t n = itp ? L : n_bins;  // the bins of this pass
+            // ... and with P.interp_of this wave interpolates the row itself (below): the depth goes
+            // to the entry's scratch doubles, the spline's serial chains run here, beside the other
+            // waves' pileup, instead of in a kernel after it
+            const int e_itp = itp && P.interp_of ? P.interp_of[(size_t)r * P.n_parts + p] : -1;
+            double* const xs = e_itp >= 0 ? P.interp_scratch + (size_t)e_itp * P.interp_stride : nullptr;
             if (part.per_base && L != n) {
                 if (lane == 0) atomicOr(P.status, RCP_STATUS_WIDTH);
                 zero_cols(r, part, n);
@@ -2134,7 +2261,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                         RcpSeg sg = sg0;
                         uint32_t lo = plo0, hi = phi0;
                         int st = pst0;
-                        if (t0 > 0) load_pair(t0 + lane, sg, lo, hi, st);
+                        if (t0 > 0) load_pair(t0, sg, lo, hi, st);
                         // this pair's piece of the window
                         const int32_t len = sg.hi - sg.lo + 1;
                         const int32_t a = max(W0, sg.off), b = min(W1, sg.off + len);
@@ -2175,6 +2302,10 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
                     const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
                     const uint32_t num = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
+                    if (xs) {
+                        xs[k] = (double)num * sc;  // (rcp_interp_kernel's x[i])
+                        continue;
+                    }
                     if (staged) {
                         srow[part.col_off + k] = num;
                         continue;
@@ -2184,12 +2315,30 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                 }
                 lds_order();
             }
+            if (xs) itp_parts |= 1u << p;
+        }
+        return itp_parts;
+    };
+    // splitVector of row r's piled slices (itp_parts: the parts with an interpolation entry) into
+    // their columns, as rcp_interp_kernel would: run after the row, where little else is live
+    auto interp_rows = [&](int r, uint32_t itp_parts) {
+        for (int p = 0; p < P.n_parts; ++p) {
+            if (!((itp_parts >> p) & 1)) continue;
+            const int e = P.interp_of[(size_t)r * P.n_parts + p];
+            const RcpPart part = P.part[p];
+            int32_t head, L;
+            rcp_part_slice(part, P.row_info[r].row_len, &head, &L);
+            const int mode = P.interp_mode[e];
+            interp_finish_wave(mode, L, part.n_bins, P.interp_scratch + (size_t)e * P.interp_stride,
+                               mode == 3 ? P.nb_pos + P.interp_pos[e] : nullptr, P.spl_tb,
+                               out + (size_t)part.col_off * R + r, R);
         }
     };
     for (int r = claim(); r >= 0; r = claim()) {
         const int sl = staged ? slot_of(r) : 0;
-        row_body(r, sl);
+        const uint32_t itp_parts = row_body(r, sl);
         if (staged) row_done(r, sl);
+        if (itp_parts) interp_rows(r, itp_parts);
     }
     // the last workgroup out resets the tile counters for the next launch
     __syncthreads();
@@ -3098,8 +3247,8 @@ static hipError_t launch_pileup_bins(const RcpPlanDev* P, double* out, int64_t* 
 
 // =================================================================================
 // interpolation rows (length(x) < n): spline "fmm", neighborhood, "inear" no-op
+// (rcp_splitvector.h, included above the row-wave kernel, which runs them too)
 // =================================================================================
-#include "rcp_splitvector.h"
 
 // Block-level window: depth of row r over row positions [w0, w0 + wn) into diff[0 .. wn)
 // (reads piled by all 256 threads, or copied from a heavy row's global difference array).
@@ -3108,7 +3257,7 @@ __device__ void block_window_depth(const RcpPlanDev& P, int r, int32_t w0, int32
     const int per = (wn + 1 + kBlock - 1) / kBlock;
     for (int q = threadIdx.x; q < per * kBlock; q += kBlock) diff[q] = 0;
     __syncthreads();
-    const int32_t slot = P.rec[r].heavy;
+    const int32_t slot = P.heavy_threshold > 0 ? P.rec[r].heavy : -1;  // (folded plans: no record)
     if (slot >= 0) {
         const int32_t* g = P.heavy_gdiff + (size_t)slot * P.heavy_stride;
         if (threadIdx.x == 0) {

@@ -18,7 +18,31 @@ namespace {
 // and the back substitution divides by tabulated pivots; both chains run in
 // the first wave's registers (below).  Data-parallel loops run over the block.
 // Same operations in the same order per element as R: bit-equal.
-// Call from all threads of the block; y, b, c, d in LDS (or global), 0-based.
+// Call from all threads of the team; y, b, c, d in LDS (or global), 0-based.
+//
+// A team runs one row: the whole block (rcp_interp_kernel, rcp_rle.hip) or a single wave (the
+// row-wave pileup kernel interpolates the rows it piles, its arrays in global scratch).
+struct BlockTeam {
+    __device__ int id() const { return (int)threadIdx.x; }
+    __device__ int size() const { return (int)blockDim.x; }
+    __device__ void sync() const { __syncthreads(); }
+};
+struct WaveTeam {
+    __device__ int id() const { return (int)(threadIdx.x & 63); }
+    __device__ int size() const { return 64; }
+    __device__ void sync() const {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+};
+// the first wave's stores visible to its own later loads (LDS or global arrays)
+__device__ __forceinline__ void lead_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // lane j's double to every lane (j wave-uniform): two v_readlane, no LDS permute
 __device__ __forceinline__ double lane_bcast(double v, int j) {
     const uint64_t u = __builtin_bit_cast(uint64_t, v);
@@ -27,9 +51,10 @@ __device__ __forceinline__ double lane_bcast(double v, int j) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-__device__ void fmm_spline_block(int n, const double* y, double* b, double* __restrict__ c, double* d,
-                                 const double* __restrict__ tb) {
-    const int t = threadIdx.x;
+template <class Team>
+__device__ void fmm_spline_team(const Team& tm, int n, const double* y, double* b, double* __restrict__ c, double* d,
+                                const double* __restrict__ tb) {
+    const int t = tm.id(), nt = tm.size();
     if (n < 3) {
         if (t == 0) {
             if (n == 2) {
@@ -39,21 +64,21 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
             }
             for (int i = 0; i < n; ++i) c[i] = d[i] = 0.0;
         }
-        __syncthreads();
+        tm.sync();
         return;
     }
     // 1-based i = 2 .. n-1 (0-based i - 1): c[i] = (y[i+1] - y[i]) - (y[i] - y[i-1])
-    for (int i = 1 + t; i < n - 1; i += blockDim.x) c[i] = (y[i + 1] - y[i]) - (y[i] - y[i - 1]);
+    for (int i = 1 + t; i < n - 1; i += nt) c[i] = (y[i + 1] - y[i]) - (y[i] - y[i - 1]);
     // the tabulated multipliers t_i and pivots b_i staged next to the data (b and d are free
     // until the coefficients below): thread 0's chains read them at LDS latency, not the
     // global table's (one round trip per 8 steps: 0.116 ms of C3's interpolation kernel)
     double* tt = b;
     double* tp = d;
-    for (int i = t; i < n; i += blockDim.x) {
+    for (int i = t; i < n; i += nt) {
         tt[i] = tb[2 * i];
         tp[i] = tb[2 * i + 1];
     }
-    __syncthreads();
+    tm.sync();
     // The two chains run in the first wave's REGISTERS: lane l holds elements 4 l .. 4 l + 3 of a
     // 256-element segment (c, the multipliers, the pivots and their reciprocals), and the lanes
     // take their turns in order, the running value passed on by v_readlane -- each step is its
@@ -107,9 +132,7 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
                 if (i < n) c[i] = cv[u];
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        lead_wave_sync();
         cp = c[n - 1];  // (the padding steps ran past it)
         const double bn = -1.0 - tt[n - 1];  // b[n-1] = -1 - t_{n-1}
         // back substitution: c[i] = (c[i] - c[i+1]) / b[i].  The pivot's reciprocal is in the
@@ -196,22 +219,25 @@ __device__ void fmm_spline_block(int n, const double* y, double* b, double* __re
                 if (i < n) c[i] = cv[u];
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        lead_wave_sync();
         if (lane == 0) b[n - 1] = (y[n - 1] - y[n - 2]) + (c[n - 2] + 2.0 * c[n - 1]);
     }
-    __syncthreads();
+    tm.sync();
     // coefficients: b[i] = (y[i+1] - y[i]) - (c[i+1] + 2 c[i]); d[i] = c[i+1] - c[i]; c[i] *= 3
-    for (int i = t; i < n - 1; i += blockDim.x) {
+    for (int i = t; i < n - 1; i += nt) {
         const double ci = c[i], cn1 = c[i + 1];
         b[i] = (y[i + 1] - y[i]) - (cn1 + 2.0 * ci);
         d[i] = cn1 - ci;
     }
-    __syncthreads();
-    for (int i = t; i < n; i += blockDim.x) c[i] = 3.0 * c[i];
+    tm.sync();
+    for (int i = t; i < n; i += nt) c[i] = 3.0 * c[i];
     if (t == 0) d[n - 1] = d[n - 2];
-    __syncthreads();
+    tm.sync();
+}
+
+__device__ void fmm_spline_block(int n, const double* y, double* b, double* __restrict__ c, double* d,
+                                 const double* __restrict__ tb) {
+    fmm_spline_team(BlockTeam{}, n, y, b, c, d, tb);
 }
 
 __device__ double seq_point(int L, int n, int i) {
@@ -263,21 +289,23 @@ __device__ double spline_eval_at(const double* y, const double* b, const double*
 // each) for the spline, or the n pre-fill values of the neighborhood fill; every output point is
 // computed and stored by its own thread (no staging of the n outputs: the block's scratch stays
 // small enough for every interpolated row's block to be resident at once).  Call with every
-// thread of the block.
-__device__ void interp_finish(int mode, int L, int n, double* x, const int32_t* nb_pos, const double* spl_tb,
-                              double* out, size_t ld) {
+// thread of the team.
+template <class Team>
+__device__ void interp_finish_team(const Team& tm, int mode, int L, int n, double* x, const int32_t* nb_pos,
+                                   const double* spl_tb, double* out, size_t ld) {
+    const int t0 = tm.id(), nt = tm.size();
     double* b = x + L + 1;
     if (mode == 1) {  // spline(x, n = n)$y, then x[x < 0] <- 0
         double* c = b + L + 1;
         double* d = c + L + 1;
-        fmm_spline_block(L, x, b, c, d, spl_tb);
+        fmm_spline_team(tm, L, x, b, c, d, spl_tb);
         auto put = [&](int k, int iv) {
             const double v = L == 1 ? x[0] : spline_eval_at(x, b, c, d, iv, seq_point(L, n, k));
             out[(size_t)k * ld] = v < 0 ? 0.0 : v;
         };
         if (L < n) {  // always, for rows of this kernel; the sequential walk stays as the rule
-            for (int k = threadIdx.x; k < n; k += (int)blockDim.x) put(k, spline_interval_at(L, n, k));
-        } else if (threadIdx.x == 0) {
+            for (int k = t0; k < n; k += nt) put(k, spline_interval_at(L, n, k));
+        } else if (t0 == 0) {
             int i = 0;  // spline_eval's walk, point by point
             for (int k = 0; k < n; ++k) {
                 const double u = seq_point(L, n, k);
@@ -288,17 +316,17 @@ __device__ void interp_finish(int mode, int L, int n, double* x, const int32_t* 
     } else if (mode == 3) {  // neighborhood fill (util.R:53-69), from the pre-fill vector
         const int32_t* pos = nb_pos;
         double* pre = b;
-        for (int i = threadIdx.x; i < n; i += (int)blockDim.x) pre[i] = __builtin_nan("");
-        __syncthreads();
-        if (threadIdx.x == 0) {
+        for (int i = t0; i < n; i += nt) pre[i] = __builtin_nan("");
+        tm.sync();
+        if (t0 == 0) {
             pre[0] = x[0];
             pre[1] = x[1];
             pre[n - 2] = x[L - 2];
             pre[n - 1] = x[L - 1];
         }
-        for (int i = threadIdx.x; i < L - 4; i += (int)blockDim.x) pre[pos[i] - 1] = x[2 + i];
-        __syncthreads();
-        for (int z = threadIdx.x; z < n; z += (int)blockDim.x) {
+        for (int i = t0; i < L - 4; i += nt) pre[pos[i] - 1] = x[2 + i];
+        tm.sync();
+        for (int z = t0; z < n; z += nt) {
             double v;
             if (!isnan(pre[z])) {
                 v = pre[z];
@@ -316,8 +344,22 @@ __device__ void interp_finish(int mode, int L, int n, double* x, const int32_t* 
             out[(size_t)z * ld] = v;
         }
     } else {  // "linear": the switch arm is spelled "inear" -> x unchanged; rbind recycles
-        for (int i = threadIdx.x; i < n; i += (int)blockDim.x) out[(size_t)i * ld] = x[i % L];
+        for (int i = t0; i < n; i += nt) out[(size_t)i * ld] = x[i % L];
     }
+}
+
+__device__ void interp_finish(int mode, int L, int n, double* x, const int32_t* nb_pos, const double* spl_tb,
+                              double* out, size_t ld) {
+    interp_finish_team(BlockTeam{}, mode, L, n, x, nb_pos, spl_tb, out, ld);
+}
+
+// one wave's interpolation of a row (the row-wave pileup kernel): a call, so that the spline's
+// registers are not added to the pileup loop's
+__device__ __attribute__((noinline)) void interp_finish_wave(int mode, int L, int n, double* x, const int32_t* nb_pos,
+                                                             const double* spl_tb, double* out, size_t ld) {
+    const WaveTeam tm;
+    tm.sync();
+    interp_finish_team(tm, mode, L, n, x, nb_pos, spl_tb, out, ld);
 }
 
 }  // namespace

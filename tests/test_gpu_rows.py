@@ -168,3 +168,31 @@ def test_row_major_staging(gpu):
     res, exp, plan = _both(reads, CHROM_LEN, rows, wide, kernel="auto")
     assert plan.info["lds_bytes"] <= 160 * 1024  # (row-major staging in HBM: the waves' windows only)
     check(res, exp, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("stranded", [False, True])
+def test_folded_locate(gpu, stranded):
+    """Row-wave plans search their rows' read ranges in the pileup kernel (plan dev.fold: no
+    locate launch) unless the caller asks for the heavy path: NA seqlengths (the group's hits'
+    last end decides, R/coverage.R:217-222), NULL rows, interpolated genes both from the HBM stage
+    and -- with binsum -- piled again by the interpolation kernel from the ranges the pileup wrote,
+    and one plan executed with and without binsum in turn; the same bits as the located plan
+    (heavy_threshold 16) and the general kernel."""
+    from recoup_amd.engine import Bins, Plan, ReadSet
+    rng = np.random.default_rng(71 + stranded)
+    reads = make_reads(rng, 120_000, widths=(50, 600), star_frac=0.1)
+    rows = rna_rows(rng, 150, ignore_strand=not stranded)
+    bins = Bins([("upstream", 50), ("center", 300), ("downstream", 50)], flank=(2000, 2000))
+    for seqlen in (CHROM_LEN, np.array([-1, CHROM_LEN[1], -1], np.int64)):
+        res, exp, plan = _both(reads, seqlen, rows, bins, kernel="auto")
+        check(res, exp, rtol=1e-9, atol=1e-12)
+        assert plan.heavy_rows() == 0
+        located = Plan(ReadSet(*reads, seqlen, device=0), rows, bins, heavy_threshold=16)
+        ref = located.run(binsum=True)
+        for binsum in (True, False, True):
+            got = plan.run(binsum=binsum)
+            np.testing.assert_array_equal(got[1], ref[1])
+            assert np.array_equal(np.ascontiguousarray(got[0]).view(np.uint64),
+                                  np.ascontiguousarray(ref[0]).view(np.uint64))
+            if binsum:
+                np.testing.assert_array_equal(got[2], ref[2])

@@ -1,6 +1,6 @@
 """One GPU's shard k/N of the C4 (or $CFG) workload (as bench.py --sim-shard builds it) on each pileup
 kernel: ms per pass (D = 1, execute after execute), the stage times, and bit-equality with the
-default plan.   python tools/diag_shard_kernels.py [K/N] [kernels...]"""
+default plan.   python tools/diag_shard_kernels.py [K/N] [kernels...]   (kernel:C = min_col_chunks C)"""
 import os
 import sys
 import time
@@ -24,7 +24,8 @@ reads = bench.reads_for_rows(data["reads"], rows, len(data["seqlen"])) if n > 1 
 rs = ReadSet(*reads, data["seqlen"], device=0)
 ref = None
 for kern in kernels:
-    plan = Plan(rs, rows, bins, kernel=kern, out_ld="padded")
+    name, _, mcc = kern.partition(":")
+    plan = Plan(rs, rows, bins, kernel=name, out_ld="padded", min_col_chunks=int(mcc or 0))
     out = plan.empty_output()
     for _ in range(5):
         plan.execute(out)

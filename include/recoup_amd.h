@@ -194,7 +194,9 @@ RCP_API int rcp_plan_create(const rcp_readset* rs, const rcp_rows_desc* rows, co
  * single-range rows are all cut into whole bins of >= 4 positions, <= 512 bins, e.g. TSS
  * windows in 200 bins).  All choices give bit-identical results.  heavy_threshold: candidate
  * reads per column chunk above which a skewed row is piled by many workgroups first
- * (-1 = default 4096, 0 = never).  out_ld: see the field. */
+ * (-1 = default 4096, 0 = never; row-wave and bin-difference plans without an explicit
+ * threshold search their rows' read ranges in the pileup kernel itself and have no heavy path).
+ * out_ld: see the field. */
 enum { RCP_KERNEL_AUTO = 0, RCP_KERNEL_GENERAL = 1, RCP_KERNEL_LEAN_ANY = 2, RCP_KERNEL_ROWS = 3, RCP_KERNEL_LEAN = 4,
        RCP_KERNEL_BINS = 5 };
 typedef struct {
@@ -204,10 +206,12 @@ typedef struct {
                                  * 0 = n_rows (plain R column-major); >= n_rows otherwise.  A multiple
                                  * of 16 keeps every 16-row column segment on whole 128-B lines
                                  * (RCP_OUT_LD_PADDED picks the next multiple of 16) */
-    int32_t min_col_chunks;     /* lean plans: cut each part into at least this many column chunks
-                                 * (0 = auto: enough (row tile, chunk) work items for the persistent
-                                 * grid -- small row tables, e.g. one GPU's shard, get more chunks so
-                                 * the last items do not leave most workgroups idle) */
+    int32_t min_col_chunks;     /* lean plans and one-part general plans: cut each part into at least
+                                 * this many column chunks (<= 16; 0 = auto: lean plans take enough
+                                 * (row tile, chunk) work items for the persistent grid -- small row
+                                 * tables, e.g. one GPU's shard, get more chunks so the last items do
+                                 * not leave most workgroups idle; general plans keep <= 1023
+                                 * positions a chunk -- more measured slower on the C4 shard) */
     int32_t concurrent;         /* plans the caller keeps in flight on other streams (0 / 1 = this one
                                  * alone, e.g. one profileMatrix pass per sample of an input list run
                                  * on D streams): > 1 makes the persistent pileup grids (lean,

@@ -120,12 +120,27 @@ void release_cached(int dev) {
         spare.swap(c.spare);
     }
     DeviceGuard g(dev);
+    // (best effort: a failing call here is reported under RCP_TRACE and cleared from the thread's
+    // last-error slot, where the next kernel launch's hipGetLastError would find it)
+    hipError_t first = hipSuccess;
+    const char* what = "";
+    auto note = [&](hipError_t e, const char* w) {
+        if (e != hipSuccess && first == hipSuccess) {
+            first = e;
+            what = w;
+        }
+    };
     for (auto& kv : blocks) {
-        if (kv.second.ev) (void)hipEventSynchronize(kv.second.ev);
-        (void)hipFree(kv.second.p);
-        if (kv.second.ev) (void)hipEventDestroy(kv.second.ev);
+        if (kv.second.ev) note(hipEventSynchronize(kv.second.ev), "hipEventSynchronize");
+        note(hipFree(kv.second.p), "hipFree");
+        if (kv.second.ev) note(hipEventDestroy(kv.second.ev), "hipEventDestroy");
     }
-    for (hipEvent_t e : spare) (void)hipEventDestroy(e);
+    for (hipEvent_t e : spare) note(hipEventDestroy(e), "hipEventDestroy (spare)");
+    if (first != hipSuccess) {
+        if (rcp::trace_on())
+            fprintf(stderr, "[pool] release of %zu blocks: %s: %s\n", blocks.size(), what, hipGetErrorString(first));
+        (void)hipGetLastError();
+    }
 }
 
 }  // namespace
@@ -1632,9 +1647,10 @@ extern "C" int rcp_profile(const rcp_readset* rs, const rcp_rows_desc* rows, con
     rc = rcp_plan_status(plan, nullptr);
     if (rc) return rc;
     // into R's allocMatrix memory (pageable): pinned double-buffered staging (rcp_stage.h)
-    if (out && plan->n_rows && plan->n_cols)
-        HIP_TRY(rcp::stage_d2h_2d(out, 8 * (size_t)plan->n_rows, d_out.p, 8 * (size_t)plan->out_ld,
-                                  8 * (size_t)plan->n_rows, (size_t)plan->n_cols, rs->device, nullptr));
+    if (out && plan->n_rows && plan->n_cols) {
+        rc = download_matrix(plan, d_out.as<double>(), out, (size_t)plan->n_rows, nullptr);
+        if (rc) return rc;
+    }
     if (row_valid && plan->n_rows) HIP_TRY(hipMemcpy(row_valid, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost));
     return RCP_OK;
     RCP_CATCH
@@ -2107,9 +2123,10 @@ extern "C" int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_sampl
         rcp_plan* plan = plans[j].get();
         int e = rcp_plan_status(plan, st[k]);
         if (e) return e;
-        if (outs && outs[j] && plan->n_rows && plan->n_cols)
-            HIP_TRY(rcp::stage_d2h_2d(outs[j], 8 * (size_t)plan->n_rows, d_out[k].p, 8 * (size_t)plan->out_ld,
-                                      8 * (size_t)plan->n_rows, (size_t)plan->n_cols, dev, st[k]));
+        if (outs && outs[j] && plan->n_rows && plan->n_cols) {
+            e = download_matrix(plan, d_out[k].as<double>(), outs[j], (size_t)plan->n_rows, st[k]);
+            if (e) return e;
+        }
         if (row_valid && row_valid[j] && plan->n_rows) {
             HIP_TRY(hipMemcpyAsync(row_valid[j], d_valid[k].p, plan->n_rows, hipMemcpyDeviceToHost, st[k]));
             HIP_TRY(hipStreamSynchronize(st[k]));
@@ -2134,6 +2151,79 @@ extern "C" int rcp_profile_samples(rcp_readset* const* readsets, int32_t n_sampl
 }
 
 namespace rcpi {
+
+// A plan's matrix (d_out, column stride plan->out_ld, on stream s) into the host's column-major
+// double matrix (column stride host_ld): as uint32 bin numerators, 4 bytes a cell over PCIe, when
+// every mean is one (rcp_pack_kernel: one-part plans without interpolated rows or R-RNG layouts,
+// positive scale), the host making each double with the device's operations -- else as the
+// doubles.  (C4's 1.6 GB matrix: 0.8 GB down, and 2.4 instead of 3.2 GB of host memory traffic
+// -- DMA in, pinned read, destination write -- which is what bounds a streamed call.)
+int download_packed(const double* d_out, size_t ld, size_t R, size_t C, double scale, double* host, size_t host_ld,
+                    int device, hipStream_t s,
+                    const std::function<hipError_t(uint32_t* q, uint32_t* div, uint32_t* bad_row)>& pack) {
+    PoolBuf q(s), aux(s);
+    HIP_TRY(q.alloc(4 * ld * C));
+    HIP_TRY(aux.alloc(8 * R));
+    uint32_t* d_div = aux.as<uint32_t>();
+    uint32_t* d_bad = d_div + R;
+    HIP_TRY(hipMemsetAsync(d_bad, 0, 4 * R, s));
+    HIP_TRY(pack(q.as<uint32_t>(), d_div, d_bad));
+    std::vector<uint32_t> h(2 * R);
+    HIP_TRY(hipMemcpyAsync(h.data(), d_div, 8 * R, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<int32_t> bad;
+    for (size_t r = 0; r < R; ++r)
+        if (h[R + r]) bad.push_back((int32_t)r);
+    // many rows the numerators cannot carry (interpolated genes, R-RNG layouts): all doubles
+    if (bad.size() > R / 8) {
+        if (rcp::trace_on()) fprintf(stderr, "[pack] doubles: %zu of %zu rows not numerators\n", bad.size(), R);
+        HIP_TRY(rcp::stage_d2h_2d(host, 8 * host_ld, d_out, 8 * ld, 8 * R, C, device, s));
+        return RCP_OK;
+    }
+    HIP_TRY(rcp::stage_d2h_expand(host, host_ld, q.as<uint32_t>(), ld, R, C, h.data(), scale, device, s));
+    if (!bad.empty()) {  // those rows' doubles, gathered on the device, over the expanded cells
+        const size_t nb = bad.size();
+        PoolBuf d_rows(s), d_vals(s);
+        HIP_TRY(d_rows.alloc(4 * nb));
+        HIP_TRY(d_vals.alloc(8 * nb * C));
+        HIP_TRY(hipMemcpyAsync(d_rows.p, bad.data(), 4 * nb, hipMemcpyHostToDevice, s));
+        HIP_TRY(rcp_launch_gather_rows(d_out, (int64_t)ld, d_rows.as<int32_t>(), (int32_t)nb, (int64_t)C,
+                                       d_vals.as<double>(), s));
+        std::vector<double> vals(nb * C);
+        HIP_TRY(hipMemcpyAsync(vals.data(), d_vals.p, 8 * nb * C, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        for (size_t c = 0; c < C; ++c)
+            for (size_t i = 0; i < nb; ++i) host[c * host_ld + (size_t)bad[i]] = vals[c * nb + i];
+        if (rcp::trace_on()) fprintf(stderr, "[pack] %zu rows as doubles\n", nb);
+    }
+    return RCP_OK;
+}
+
+// A plan's matrix (d_out, column stride plan->out_ld, on stream s) into the host's column-major
+// double matrix (column stride host_ld): as uint32 bin numerators, 4 bytes a cell over PCIe
+// (rcp_pack_kernel: one-part plans of mean bins, positive scale), the host making each double with
+// the device's operations; rows the numerators cannot carry (interpolated, R-RNG layouts) come down
+// apart as doubles.  Plans of several parts, or many such rows: the doubles.  (C4's 1.6 GB matrix: 0.8 GB down, and
+// 2.4 instead of 3.2 GB of host memory traffic -- DMA in, pinned read, destination write --
+// which is what bounds a streamed call.)
+int download_matrix(rcp_plan* plan, const double* d_out, double* host, size_t host_ld, hipStream_t s) {
+    const RcpPlanDev& P = plan->dev;
+    const int dev = plan->rs->device;
+    const size_t R = (size_t)plan->n_rows, C = (size_t)plan->n_cols, ld = (size_t)plan->out_ld;
+    if (!host || R == 0 || C == 0) return RCP_OK;
+    const bool pack = P.n_parts == 1 && P.n_interp <= plan->n_rows / 8 && P.stat == 0 && P.scale > 0.0 && std::isfinite(P.scale) &&
+                      C <= 65535u * 8u && 8 * R * C >= (size_t(4) << 20) && P.csr_off == nullptr;
+    if (!pack) {
+        if (rcp::trace_on() && 8 * R * C >= (size_t(4) << 20))
+            fprintf(stderr, "[pack] doubles: plan of %d parts, %d interpolated rows\n", P.n_parts, P.n_interp);
+        HIP_TRY(rcp::stage_d2h_2d(host, 8 * host_ld, d_out, 8 * ld, 8 * R, C, dev, s));
+        return RCP_OK;
+    }
+    return download_packed(d_out, ld, R, C, P.scale, host, host_ld, dev, s,
+                           [&](uint32_t* q, uint32_t* div, uint32_t* bad) {
+                               return rcp_launch_pack(&P, d_out, q, div, bad, s);
+                           });
+}
 
 int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bins_desc* bins, double* out,
                   int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream) {
@@ -2164,9 +2254,10 @@ int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bin
     if (e) return e;
     const double t2 = tr ? rcp::trace_ms() : 0.0;
     // this block's rows of every column of the caller's R matrix
-    if (out && plan->n_cols && plan->n_rows)
-        HIP_TRY(rcp::stage_d2h_2d(out + r0, 8 * (size_t)n_rows_total, d_out.p, 8 * (size_t)plan->out_ld,
-                                  8 * (size_t)plan->n_rows, (size_t)plan->n_cols, rs->device, s));
+    if (out && plan->n_cols && plan->n_rows) {
+        e = download_matrix(plan, d_out.as<double>(), out + r0, (size_t)n_rows_total, s);
+        if (e) return e;
+    }
     if (tr)
         fprintf(stderr, "[block] rows [%d, %d): plan %.2f ms, pass %.2f ms, down %.2f ms\n", r0, r0 + plan->n_rows,
                 t1 - t0, t2 - t1, rcp::trace_ms() - t2);
@@ -2831,9 +2922,19 @@ int rle_finish(RleJob* job, int device, double* out, int64_t out_ld, uint8_t* ro
     DeviceGuard g(device);
     HIP_TRY(g.err);
     HIP_TRY(rcp_rle_profile_launch(&job->P, job->dbl ? 1 : 0, job->lds, s));
-    if (out && job->R && job->col)
-        HIP_TRY(rcp::stage_d2h_2d(out, 8 * (size_t)out_ld, job->d_out.p, 8 * (size_t)job->ld, 8 * (size_t)job->R,
-                                  (size_t)job->col, device, s));
+    const size_t R = (size_t)job->R, C = (size_t)job->col;
+    const RcpRleDev& P = job->P;
+    // integer Rle, one part of mean bins: the matrix as numerators (download_matrix)
+    if (out && R && C && !job->dbl && P.n_parts == 1 && P.stat == 0 && (size_t)P.n_itasks <= R / 8 && P.scale > 0.0 &&
+        std::isfinite(P.scale) && C <= 65535u * 8u && 8 * R * C >= (size_t(4) << 20)) {
+        const int e = download_packed(job->d_out.as<double>(), (size_t)job->ld, R, C, P.scale, out, (size_t)out_ld,
+                                      device, s, [&](uint32_t* q, uint32_t* div, uint32_t* bad) {
+                                          return rcp_rle_pack(&P, (int64_t)C, q, div, bad, s);
+                                      });
+        if (e) return e;
+    } else if (out && R && C) {
+        HIP_TRY(rcp::stage_d2h_2d(out, 8 * (size_t)out_ld, job->d_out.p, 8 * (size_t)job->ld, 8 * R, C, device, s));
+    }
     HIP_TRY(hipStreamSynchronize(s));
     if (row_valid)
         for (int32_t r = 0; r < job->R; ++r) row_valid[r] = (job->is_null && job->is_null[r]) ? 0 : 1;

@@ -13,6 +13,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <functional>
 #include <vector>
 
 #include "../../include/recoup_amd.h"
@@ -33,6 +34,10 @@ hipError_t rcp_launch_locate(const RcpPlanDev* P, hipStream_t stream);
 hipError_t rcp_launch_heavy(const RcpPlanDev* P, int grid, hipStream_t stream);
 hipError_t rcp_launch_pileup(const RcpPlanDev* P, double* out, int64_t* binsum, int csr, hipStream_t stream);
 hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStream_t stream);
+hipError_t rcp_launch_pack(const RcpPlanDev* P, const double* out, uint32_t* q_out, uint32_t* div, uint32_t* bad_row,
+                           hipStream_t stream);
+hipError_t rcp_launch_gather_rows(const double* out, int64_t ld, const int32_t* rows, int32_t n, int64_t n_cols,
+                                  double* dst, hipStream_t stream);
 size_t rcp_pileup_lds_bytes(const RcpPlanDev* P, int csr);
 size_t rcp_interp_lds_bytes(const RcpPlanDev* P);
 int rcp_tile_rows(void);
@@ -213,6 +218,15 @@ int run_per_device(int n, F fn) {
     return RCP_OK;
 }
 
+// A plan's matrix on the device (column stride plan->out_ld) into a host column-major double
+// matrix of column stride host_ld, as bin numerators when the plan allows (rcp_host.cpp)
+int download_matrix(rcp_plan* plan, const double* d_out, double* host, size_t host_ld, hipStream_t s);
+// the numerator download of an R x C column-major device matrix d_out (stride ld): pack(q, div,
+// bad_row) fills the numerators, per-row widths and per-row failure marks (zeroed first); rows
+// marked come down as doubles apart, or everything does when they are many
+int download_packed(const double* d_out, size_t ld, size_t R, size_t C, double scale, double* host, size_t host_ld,
+                    int device, hipStream_t s,
+                    const std::function<hipError_t(uint32_t* q, uint32_t* div, uint32_t* bad_row)>& pack);
 // Block [r0, r0 + sub->n_rows) of an n_rows_total-row profile on readset rs: plan, execute, and
 // copy its rows of every column into the caller's R column-major matrix `out` (may be NULL) and
 // row_valid + r0 (may be NULL); *n_cols receives the plan's column count.  On `stream` (NULL: a

@@ -3580,6 +3580,88 @@ extern "C" hipError_t rcp_launch_interp(const RcpPlanDev* P, double* out, hipStr
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------
+// Numerator download (rcp_profile_reads and the other host-matrix paths): a one-part plan's means
+// are (q * scale) / bs of a uint32 bin numerator q and the row's bin width bs -- with bs a power
+// of two, (q * scale) * (1 / bs) -- so the host can make every double of the matrix from q and bs
+// with the same IEEE operations, and PCIe carries 4 bytes a cell instead of 8.  This kernel
+// recovers q from each mean and checks that the forward operation gives back the mean's bits;
+// rows whose means are not such quotients (interpolated rows, R-RNG layouts: bins of two widths)
+// are marked in bad[r] and the caller fetches their doubles apart (rcp_gather_rows_kernel), or
+// all doubles when there are many.  div[r] = bs, 0 for a NULL row (its means are +0.0).
+constexpr int kPackCols = 8;  // columns per thread
+__global__ void __launch_bounds__(kBlock) rcp_pack_kernel(RcpPlanDev P, const double* __restrict__ out,
+                                                          uint32_t* __restrict__ q_out, uint32_t* __restrict__ div,
+                                                          uint32_t* __restrict__ bad_row) {
+    const int r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= P.n_rows) return;
+    const RcpPart& part = P.part[0];
+    const int32_t n = part.n_bins;
+    uint32_t bs = 0;
+    bool bad = false;
+    if (P.valid[r]) {
+        int32_t head, L;
+        rcp_part_slice(part, P.row_len[r], &head, &L);
+        if (part.per_base) {
+            bs = 1;
+            bad = L != n;
+        } else {
+            bad = L < n || L % n != 0;
+            bs = bad ? 0u : (uint32_t)(L / n);
+        }
+    }
+    if (blockIdx.y == 0) div[r] = bs;
+    const double sc = P.scale;
+    const double dd = (double)max(bs, 1u), rdd = 1.0 / dd;
+    const bool pow2 = (bs & (bs - 1)) == 0;
+    const size_t ld = (size_t)P.out_ld;
+    const int64_t k0 = (int64_t)blockIdx.y * kPackCols;
+    uint32_t why = bad ? 4u : 0u;  // (bits: 1 a mean that is no quotient, 2 a NULL row's nonzero, 4 row shape)
+    for (int64_t k = k0; k < min<int64_t>(k0 + kPackCols, P.n_cols); ++k) {
+        const double v = out[k * ld + r];
+        uint32_t q = 0;
+        if (bs) {
+            const double x = rint(v * dd / sc);
+            q = (x >= 0.0 && x <= 4294967295.0) ? (uint32_t)x : 0u;
+            const double back = pow2 ? ((double)q * sc) * rdd : rcp_div_rn((double)q * sc, dd, rdd);
+            if (__double_as_longlong(back) != __double_as_longlong(v)) why |= 1u;
+        } else if (__double_as_longlong(v) != 0) {
+            why |= 2u;  // a NULL row's +0.0
+        }
+        q_out[k * ld + r] = q;
+    }
+    if (why) atomicOr(bad_row + r, why);
+}
+
+// rows[i]'s doubles (column-major, stride ld) into dst[c * n + i]: the rows the numerator download
+// could not carry
+__global__ void __launch_bounds__(kBlock) rcp_gather_rows_kernel(const double* __restrict__ out, int64_t ld,
+                                                                 const int32_t* __restrict__ rows, int32_t n,
+                                                                 int64_t n_cols, double* __restrict__ dst) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (int64_t)n * n_cols) return;
+    const int64_t c = t / n;
+    const int32_t i = (int32_t)(t - c * n);
+    dst[t] = out[c * ld + rows[i]];
+}
+
+extern "C" hipError_t rcp_launch_gather_rows(const double* out, int64_t ld, const int32_t* rows, int32_t n,
+                                             int64_t n_cols, double* dst, hipStream_t stream) {
+    const int64_t cells = (int64_t)n * n_cols;
+    if (cells == 0) return hipSuccess;
+    hipLaunchKernelGGL(rcp_gather_rows_kernel, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                       out, ld, rows, n, n_cols, dst);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rcp_launch_pack(const RcpPlanDev* P, const double* out, uint32_t* q_out, uint32_t* div,
+                                      uint32_t* bad_row, hipStream_t stream) {
+    if (P->n_rows == 0 || P->n_cols == 0) return hipSuccess;
+    const dim3 grid((unsigned)((P->n_rows + kBlock - 1) / kBlock), (unsigned)((P->n_cols + kPackCols - 1) / kPackCols));
+    hipLaunchKernelGGL(rcp_pack_kernel, grid, dim3(kBlock), 0, stream, *P, out, q_out, div, bad_row);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t rcp_launch_readset(int64_t n, const int32_t* chrom, const int32_t* start, const int32_t* end,
                                          const int8_t* strand, int32_t n_chrom, int32_t strand_filter, int merge,
                                          uint64_t* keys, int32_t* vals, hipStream_t stream) {

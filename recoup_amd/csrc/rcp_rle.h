@@ -56,6 +56,9 @@ extern "C" {
 hipError_t rcp_rle_scan(const int32_t* lengths, int64_t n_runs, int64_t* gstart, void* temp, size_t* temp_bytes,
                         hipStream_t stream);
 hipError_t rcp_rle_profile_launch(const RcpRleDev* P, int dbl, size_t lds, hipStream_t stream);
+// the profile's means as uint32 numerators + per-row bin widths (flag set: not expressible)
+hipError_t rcp_rle_pack(const RcpRleDev* P, int64_t n_cols, uint32_t* q_out, uint32_t* div, uint32_t* flag,
+                        hipStream_t stream);
 // row lengths and run-length checks of an Rle list (bad[2]: first row with a length <= 0 / with
 // 2^31 or more positions, preset to INT32_MAX)
 hipError_t rcp_rle_rowlen(int32_t R, const int64_t* run_off, const int32_t* lengths, int32_t* row_len, int32_t* bad,

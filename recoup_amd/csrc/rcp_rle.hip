@@ -516,6 +516,50 @@ static void launch_tiles(const RcpRleDev* P, int p, int64_t grid, hipStream_t st
     hipLaunchKernelGGL((rcp_rle_tile_kernel<DBL, KIND, LEN>), dim3((unsigned)grid), dim3(kTBlock), 0, stream, *P, p);
 }
 
+// The numerator download of an integer Rle profile (rcp_pack_kernel's, rcp_kernels.hip): one
+// part, mean bins; div[r] = the row's uniform bin width (1 per base, 0 NULL); rows of R-RNG
+// layouts or interpolated ones are marked in flag[r] (their doubles are fetched apart)
+constexpr int kPackCols = 8;
+__global__ void __launch_bounds__(kRleBlock) rcp_rle_pack_kernel(RcpRleDev P, int64_t n_cols, uint32_t* __restrict__ q_out,
+                                                               uint32_t* __restrict__ div, uint32_t* __restrict__ flag) {
+    const int r = blockIdx.x * kRleBlock + threadIdx.x;
+    if (r >= P.n_rows) return;
+    const RcpRleTask t = P.tasks[r];
+    uint32_t bs = 0;
+    bool bad = false;
+    if (t.mode == RCP_RLE_BASE) bs = 1;
+    else if (t.mode == RCP_RLE_BINNED && t.lay < 0 && t.bs > 0) bs = (uint32_t)t.bs;
+    else if (t.mode != RCP_RLE_ZERO) bad = true;
+    if (blockIdx.y == 0) div[r] = bs;
+    const double sc = P.scale;
+    const double dd = (double)max(bs, 1u), rdd = 1.0 / dd;
+    const bool pow2 = (bs & (bs - 1)) == 0;
+    const size_t ld = (size_t)P.ld;
+    const int64_t k0 = (int64_t)blockIdx.y * kPackCols;
+    for (int64_t k = k0; k < min<int64_t>(k0 + kPackCols, n_cols); ++k) {
+        const double v = P.out[k * ld + r];
+        uint32_t q = 0;
+        if (bs) {
+            const double x = rint(v * dd / sc);
+            q = (x >= 0.0 && x <= 4294967295.0) ? (uint32_t)x : 0u;
+            const double back = pow2 ? ((double)q * sc) * rdd : ((double)q * sc) / dd;
+            bad = bad || __double_as_longlong(back) != __double_as_longlong(v);
+        } else {
+            bad = bad || __double_as_longlong(v) != 0;
+        }
+        q_out[k * ld + r] = q;
+    }
+    if (bad) atomicOr(flag + r, 1u);  // (per row: bad_row, as rcp_pack_kernel)
+}
+
+extern "C" hipError_t rcp_rle_pack(const RcpRleDev* P, int64_t n_cols, uint32_t* q_out, uint32_t* div, uint32_t* flag,
+                                   hipStream_t stream) {
+    if (P->n_rows == 0 || n_cols == 0) return hipSuccess;
+    const dim3 grid((unsigned)((P->n_rows + kRleBlock - 1) / kRleBlock), (unsigned)((n_cols + kPackCols - 1) / kPackCols));
+    hipLaunchKernelGGL(rcp_rle_pack_kernel, grid, dim3(kRleBlock), 0, stream, *P, n_cols, q_out, div, flag);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t rcp_rle_profile_launch(const RcpRleDev* P, int dbl, size_t lds, hipStream_t stream) {
     // tiles of every part first (they also zero-fill the interpolated rows' columns), then the
     // interpolation tasks on the same stream

@@ -206,6 +206,32 @@ inline void part_range(size_t n, int i, size_t* a, size_t* b) {
     *b = std::min(n, *a + per);
 }
 
+// dst[i] = q[i] * scale / div of row i (rows r .. r + n - 1 of a column; rcp_pack_kernel): the
+// device's operations -- ((double)q * scale) * (1 / div) for a power of two, the correctly
+// rounded quotient otherwise, +0.0 for a NULL row (div 0) -- with non-temporal stores
+void expand_nt(double* dst, const uint32_t* q, const double* rd, const double* dv, bool all_pow2, double sc,
+               size_t n) {
+    auto one = [&](size_t i) -> double {
+        const double x = (double)q[i] * sc;
+        return dv[i] != 0.0 ? x / dv[i] : x * rd[i];
+    };
+    size_t i = 0;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) && n) {
+        dst[0] = one(0);
+        i = 1;
+    }
+    if (all_pow2) {
+        for (; i + 2 <= n; i += 2) {
+            const __m128d x = _mm_set_pd((double)q[i + 1] * sc, (double)q[i] * sc);
+            _mm_stream_pd(dst + i, _mm_mul_pd(x, _mm_loadu_pd(rd + i)));
+        }
+    } else {
+        for (; i + 2 <= n; i += 2) _mm_stream_pd(dst + i, _mm_set_pd(one(i + 1), one(i)));
+    }
+    for (; i < n; ++i) dst[i] = one(i);
+    _mm_sfence();
+}
+
 }  // namespace
 
 bool trace_on() { return trace(); }
@@ -309,6 +335,73 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
     hipError_t e2 = hipEventRecord(st->done, stream);
     if (e2 == hipSuccess) e2 = hipEventSynchronize(st->done);
     if (trace()) fprintf(stderr, "[stage] d2h %zu B wait %.2f ms copy %.2f ms\n", bytes, t1 - t0, now_ms() - t1);
+    return e != hipSuccess ? e : e2;
+}
+
+hipError_t stage_d2h_expand(double* dst, size_t dld, const uint32_t* src, size_t sld, size_t rows, size_t cols,
+                            const uint32_t* div, double scale, int device, hipStream_t stream) {
+    if (rows == 0 || cols == 0) return hipSuccess;
+    // per row: the reciprocal of a power-of-two width (0 for a NULL row) or the width to divide by
+    std::vector<double> rd(rows), dv(rows);
+    bool all_pow2 = true;
+    for (size_t i = 0; i < rows; ++i) {
+        const uint32_t d = div[i];
+        const bool p2 = (d & (d - 1)) == 0;
+        rd[i] = p2 && d ? 1.0 / (double)d : 0.0;
+        dv[i] = p2 ? 0.0 : (double)d;
+        all_pow2 = all_pow2 && p2;
+    }
+    const size_t bytes = 4 * (sld * (cols - 1) + rows);  // device bytes moved (column padding inside)
+    Stager* st = stager(device, 1);
+    const double t0 = trace() ? now_ms() : 0.0;
+    std::unique_lock<std::mutex> g;
+    if (st) g = take(st, std::max(bytes, kShared));  // (always the buffers: the expansion needs them)
+    const double t1 = trace() ? now_ms() : 0.0;
+    if (!g.owns_lock() || !ready(st, 1)) return hipErrorOutOfMemory;
+    // device words [a, z) of the linear span -> their host cells (padding skipped)
+    auto scatter = [&](const uint32_t* pin, size_t base, size_t a, size_t z) {
+        while (a < z) {
+            const size_t col = a / sld, off = a % sld;
+            if (off >= rows) {
+                a = (col + 1) * sld;
+                continue;
+            }
+            const size_t n = std::min(z - a, rows - off);
+            expand_nt(dst + col * dld + off, pin + (a - base), rd.data() + off, dv.data() + off, all_pow2, scale, n);
+            a += n;
+        }
+    };
+    const size_t words = bytes / 4;
+    const size_t ch = chunk_of(bytes) / 4 / 1024 * 1024;  // words per chunk
+    const size_t nch = (words + ch - 1) / ch;
+    const char* s = reinterpret_cast<const char*>(src);
+    hipError_t e = hipSuccess;
+    for (size_t k = 0; k <= nch && e == hipSuccess; ++k) {
+        if (k < nch) {
+            const int b = (int)(k & 1);
+            const size_t a0 = k * ch, len = std::min(ch, words - a0);
+            e = hipMemcpyAsync(st->pin[b], s + 4 * a0, 4 * len, hipMemcpyDeviceToHost, stream);
+            if (e == hipSuccess) e = hipEventRecord(st->ev[b], stream);
+        }
+        if (k > 0 && e == hipSuccess) {
+            const size_t j = k - 1;
+            const int b = (int)(j & 1);
+            const size_t a0 = j * ch, len = std::min(ch, words - a0);
+            e = hipEventSynchronize(st->ev[b]);
+            if (e != hipSuccess) break;
+            const uint32_t* pin = reinterpret_cast<const uint32_t*>(st->pin[b]);
+            st->pool->run(kParts, [&](int i) {
+                const size_t per = (len + kParts - 1) / kParts;
+                const size_t a = std::min(len, per * (size_t)i), z = std::min(len, a + per);
+                if (z > a) scatter(pin, a0, a0 + a, a0 + z);
+            });
+        }
+    }
+    hipError_t e2 = hipEventRecord(st->done, stream);
+    if (e2 == hipSuccess) e2 = hipEventSynchronize(st->done);
+    if (trace())
+        fprintf(stderr, "[stage] d2h-expand %zu B (%zu cells) wait %.2f ms copy %.2f ms\n", bytes, rows * cols, t1 - t0,
+                now_ms() - t1);
     return e != hipSuccess ? e : e2;
 }
 

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <cstdint>
 
 namespace rcp {
 
@@ -27,6 +28,12 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
 // RCP_TRACE set in the environment: stderr lines per staged copy / pipeline step (diagnostics)
 bool trace_on();
 double trace_ms();  // a steady clock in ms
+
+// A column-major matrix of bin numerators (rows x cols words, column stride sld) into the host's
+// double matrix (column stride dld): cell (i, c) = q * scale / div[i] as the device makes a mean
+// (rcp_pack_kernel), through the same pinned buffers, expanded by the copy threads.  Waits.
+hipError_t stage_d2h_expand(double* dst, size_t dld, const uint32_t* src, size_t sld, size_t rows, size_t cols,
+                            const uint32_t* div, double scale, int device, hipStream_t stream);
 
 inline hipError_t stage_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t stream) {
     return stage_d2h_2d(dst, bytes, src, bytes, bytes, 1, device, stream);

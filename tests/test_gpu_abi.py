@@ -414,3 +414,57 @@ def test_profile_reads_stream_fallbacks(gpu, capfd):
     assert not any("block" in ln for ln in lines), lines
     m1, v1 = one_shot(reads, shuffled, bins)
     assert np.array_equal(got[0][0].view(np.uint64), m1.view(np.uint64))
+
+
+@pytest.mark.parametrize("n_bins,scale,expand", [(1000, 1.0, True), (1000, 0.37, True), (400, 2.5, True),
+                                                 (300, 1.0, False), (5000, 1.0, False)])
+def test_matrix_download_as_numerators(gpu, capfd, n_bins, scale, expand):
+    """Host matrices travel as uint32 bin numerators when every mean is one (rcp_pack_kernel:
+    one-part plans, uniform bins -- power-of-two widths multiply by the reciprocal, others divide --
+    NULL rows, a linear scale), the host making each double with the device's operations; R-RNG
+    layouts (300 bins of 4000 positions) and interpolated rows (5000 bins) fall back to the doubles.
+    Either way bit-equal to the device matrix."""
+    from recoup_amd.engine import ReadSet
+    from tests.test_gpu_random import CHROM_LEN, make_reads, single_rows
+    rng = np.random.default_rng(n_bins)
+    reads = make_reads(rng, 300_000)
+    rows = single_rows(rng, 6_000, 4000, edge=True)
+    bins = Bins([("whole", n_bins)], scale=scale)
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    ref, rv = Plan(rs, rows, bins).run()
+    assert not rv.all()  # NULL rows among them
+    os.environ["RCP_TRACE"] = "1"
+    try:
+        rc, out, valid = _profile(rs, rows, bins)
+    finally:
+        del os.environ["RCP_TRACE"]
+    lines = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith(("[stage] d2h", "[pack]"))]
+    assert rc == 0
+    assert any("d2h-expand" in ln for ln in lines) == expand, lines
+    assert np.array_equal(out.view(np.uint64), np.asfortranarray(ref).view(np.uint64))
+    np.testing.assert_array_equal(valid.astype(bool), rv)
+
+
+@pytest.mark.parametrize("n_bins,scale,expand", [(1000, 1.0, True), (800, 0.61, True), (300, 1.0, False)])
+def test_rle_matrix_download_as_numerators(gpu, capfd, n_bins, scale, expand):
+    """recoup()'s Rle path (calcCoverage's list -> rcp_profile_rle): an integer Rle list's profile
+    comes down as numerators too (rcp_rle_pack_kernel), R-RNG layouts as doubles; the same bits
+    as the fused read profile."""
+    from recoup_amd.engine import ReadSet, coverage_rle_host, profile_rle_arrays
+    from tests.test_gpu_random import CHROM_LEN, make_reads, single_rows
+    rng = np.random.default_rng(7 + n_bins)
+    reads = make_reads(rng, 300_000)
+    rows = single_rows(rng, 6_000, 4000, edge=True)
+    bins = Bins([("whole", n_bins)], scale=scale)
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    ref, rv = Plan(rs, rows, bins).run()
+    run_off, values, lengths, valid = coverage_rle_host(rs, rows)
+    out = np.full((rows.n_rows, bins.n_cols), np.nan, order="F")
+    os.environ["RCP_TRACE"] = "1"
+    try:
+        profile_rle_arrays(run_off, lengths, values, (valid == 0).astype(np.uint8), bins, 0, out)
+    finally:
+        del os.environ["RCP_TRACE"]
+    lines = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith(("[stage] d2h", "[pack]"))]
+    assert any("d2h-expand" in ln for ln in lines) == expand, lines
+    assert np.array_equal(out.view(np.uint64), np.asfortranarray(ref).view(np.uint64))

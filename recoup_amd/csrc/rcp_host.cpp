@@ -553,11 +553,12 @@ int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_reads
         HIP_TRY(in_start.alloc(4 * n));
         if (d->end) HIP_TRY(in_end.alloc(4 * n));
         HIP_TRY(in_strand.alloc(n));
-        // caller-owned pageable arrays (R vectors): pinned double-buffered staging (rcp_stage.h)
-        if (d->chrom) HIP_TRY(rcp::stage_h2d(in_chrom.p, d->chrom, 4 * n, d->device, s));
-        HIP_TRY(rcp::stage_h2d(in_start.p, d->start, 4 * n, d->device, s));
-        if (d->end) HIP_TRY(rcp::stage_h2d(in_end.p, d->end, 4 * n, d->device, s));
-        HIP_TRY(rcp::stage_h2d(in_strand.p, d->strand, n, d->device, s));
+        // caller-owned pageable arrays (R vectors): pinned double-buffered staging (rcp_stage.h),
+        // coordinates as 16-bit offsets within blocks and strands four to a byte where they fit
+        if (d->chrom) HIP_TRY(rcp::stage_h2d_i32(in_chrom.as<int32_t>(), d->chrom, (size_t)n, d->device, s));
+        HIP_TRY(rcp::stage_h2d_i32(in_start.as<int32_t>(), d->start, (size_t)n, d->device, s));
+        if (d->end) HIP_TRY(rcp::stage_h2d_i32(in_end.as<int32_t>(), d->end, (size_t)n, d->device, s));
+        HIP_TRY(rcp::stage_h2d_strand(in_strand.as<int8_t>(), d->strand, (size_t)n, d->device, s));
         pc = in_chrom.as<int32_t>();
         ps = in_start.as<int32_t>();
         if (d->end) pe = in_end.as<int32_t>();
@@ -1901,8 +1902,10 @@ extern "C" int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_sample
                     if (n > 0) {
                         e = pool_alloc(&x.d_start, 4 * (size_t)n, s);
                         if (e == hipSuccess) e = pool_alloc(&x.d_strand, (size_t)n, s);
-                        if (e == hipSuccess) e = rcp::stage_h2d(x.d_start, x.sl.d.start, 4 * (size_t)n, dev, s);
-                        if (e == hipSuccess) e = rcp::stage_h2d(x.d_strand, x.sl.d.strand, (size_t)n, dev, s);
+                        if (e == hipSuccess)
+                            e = rcp::stage_h2d_i32(static_cast<int32_t*>(x.d_start), x.sl.d.start, (size_t)n, dev, s);
+                        if (e == hipSuccess)
+                            e = rcp::stage_h2d_strand(static_cast<int8_t*>(x.d_strand), x.sl.d.strand, (size_t)n, dev, s);
                     }
                     if (tr)
                         fprintf(stderr, "[reads] sample %d block %zu: %lld reads up %.2f ms (at %.2f)\n", k, b,

@@ -4023,3 +4023,53 @@ extern "C" hipError_t rcp_launch_unpack_pmax(int64_t n, const uint64_t* scan_out
     hipLaunchKernelGGL(rcp_unpack_pmax_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, n, scan_out, pmax);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------
+// Packed uploads (rcp_stage.cpp stage_h2d_i32 / stage_h2d_strand): the host sends a chunk of
+// int32 values as [base int32 x nb][slot int32 x nb][16-bit offsets x n][raw blocks], blocks of
+// kPackBlock values -- value = base + offset, or, for a block whose span does not fit 16 bits,
+// raw[slot] -- and strand codes four to a byte (3: a code outside 0..2, which drops the read).
+// ---------------------------------------------------------------------------------
+constexpr int kPackBlock = 1024;
+__global__ void __launch_bounds__(kBlock) rcp_unpack_i32_kernel(const char* __restrict__ src, int64_t n, int64_t nb,
+                                                                int32_t* __restrict__ dst) {
+    const int64_t b = blockIdx.x;
+    const int32_t base = reinterpret_cast<const int32_t*>(src)[b];
+    const int32_t slot = reinterpret_cast<const int32_t*>(src)[nb + b];
+    const uint16_t* off = reinterpret_cast<const uint16_t*>(src + 8 * nb) + b * kPackBlock;
+    const int32_t* raw = reinterpret_cast<const int32_t*>(src + 8 * nb + 2 * ((n + 1) & ~int64_t(1)));
+    const int64_t i0 = b * kPackBlock;
+    for (int j = threadIdx.x; j < kPackBlock && i0 + j < n; j += kBlock)
+        dst[i0 + j] = slot < 0 ? (int32_t)((uint32_t)base + off[j]) : raw[(int64_t)slot * kPackBlock + j];
+}
+
+__global__ void __launch_bounds__(kBlock) rcp_unpack_strand_kernel(const uint8_t* __restrict__ src, int64_t n,
+                                                                   int8_t* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (4 * i >= n) return;
+    const uint32_t w = src[i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        if (4 * i + u >= n) break;
+        const int c = (int)((w >> (2 * u)) & 3u);
+        dst[4 * i + u] = (int8_t)(c == 3 ? -1 : c);
+    }
+}
+
+extern "C" int rcp_pack_block(void) { return kPackBlock; }
+
+extern "C" hipError_t rcp_launch_unpack_i32(const void* src, int64_t n, int32_t* dst, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const int64_t nb = (n + kPackBlock - 1) / kPackBlock;
+    hipLaunchKernelGGL(rcp_unpack_i32_kernel, dim3((unsigned)nb), dim3(kBlock), 0, stream,
+                       static_cast<const char*>(src), n, nb, dst);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rcp_launch_unpack_strand(const void* src, int64_t n, int8_t* dst, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const int64_t words = (n + 3) / 4;
+    hipLaunchKernelGGL(rcp_unpack_strand_kernel, dim3((unsigned)((words + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       stream, static_cast<const uint8_t*>(src), n, dst);
+    return hipGetLastError();
+}

@@ -235,7 +235,7 @@ __device__ void fmm_spline_team(const Team& tm, int n, const double* y, double* 
     tm.sync();
 }
 
-__device__ void fmm_spline_block(int n, const double* y, double* b, double* __restrict__ c, double* d,
+[[maybe_unused]] __device__ void fmm_spline_block(int n, const double* y, double* b, double* __restrict__ c, double* d,
                                  const double* __restrict__ tb) {
     fmm_spline_team(BlockTeam{}, n, y, b, c, d, tb);
 }
@@ -355,7 +355,7 @@ __device__ void interp_finish(int mode, int L, int n, double* x, const int32_t* 
 
 // one wave's interpolation of a row (the row-wave pileup kernel): a call, so that the spline's
 // registers are not added to the pileup loop's
-__device__ __attribute__((noinline)) void interp_finish_wave(int mode, int L, int n, double* x, const int32_t* nb_pos,
+[[maybe_unused]] __device__ __attribute__((noinline)) void interp_finish_wave(int mode, int L, int n, double* x, const int32_t* nb_pos,
                                                              const double* spl_tb, double* out, size_t ld) {
     const WaveTeam tm;
     tm.sync();

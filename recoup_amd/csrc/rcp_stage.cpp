@@ -12,6 +12,7 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -22,6 +23,12 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+
+extern "C" {
+int rcp_pack_block(void);
+hipError_t rcp_launch_unpack_i32(const void* src, int64_t n, int32_t* dst, hipStream_t stream);
+hipError_t rcp_launch_unpack_strand(const void* src, int64_t n, int8_t* dst, hipStream_t stream);
+}
 
 namespace rcp {
 namespace {
@@ -112,6 +119,7 @@ struct Stager {
     hipEvent_t ev[2] = {nullptr, nullptr};
     hipEvent_t done = nullptr;
     std::unique_ptr<Pool> pool;
+    char* dev[2] = {nullptr, nullptr};  // H2D: device landing buffers of packed chunks (decoded into place)
 };
 
 // Process lifetime: the pinned buffers are returned to the OS at exit (freeing them from a
@@ -232,6 +240,16 @@ void expand_nt(double* dst, const uint32_t* q, const double* rd, const double* d
     _mm_sfence();
 }
 
+// H2D landing buffers on the device (packed uploads), made on first use
+bool ready_dev(Stager* s) {
+    for (int b = 0; b < 2; ++b)
+        if (!s->dev[b] && hipMalloc(reinterpret_cast<void**>(&s->dev[b]), kChunk) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+    return true;
+}
+
 }  // namespace
 
 bool trace_on() { return trace(); }
@@ -274,6 +292,177 @@ hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipSt
     if (e2 == hipSuccess) e2 = hipEventSynchronize(st->done);
     if (trace()) fprintf(stderr, "[stage] h2d %zu B wait %.2f ms copy %.2f ms\n", bytes, t1 - t0, now_ms() - t1);
     return e != hipSuccess ? e : e2;
+}
+
+// ---- packed uploads: PCIe and host memory carry what the values need, the device restores them
+// (rcp_kernels.hip rcp_unpack_*).  A chunk of m int32 values goes as [base x nb][slot x nb]
+// [16-bit offsets x m (even)][raw blocks]: a block of B values spanning < 2^16 (coordinate-sorted
+// starts: nearly every block) is its minimum + offsets, another one raw; a chunk with more raw
+// blocks than its buffer holds goes plain.  Strand codes go four to a byte.
+namespace {
+constexpr size_t kPackMin = size_t(1) << 20;  // values; below this the plain copy
+
+hipError_t h2d_packed(Stager* st, size_t n, size_t per_chunk, hipStream_t stream, const char* what,
+                      const std::function<size_t(char* pin, size_t a0, size_t m, bool* plain)>& encode,
+                      const std::function<hipError_t(const char* dev, char* dst_plain_chunk, size_t a0, size_t m,
+                                                     size_t bytes, bool plain, hipStream_t s)>& land) {
+    const double t1 = trace() ? now_ms() : 0.0;
+    size_t raw_chunks = 0, sent = 0;
+    const size_t nch = (n + per_chunk - 1) / per_chunk;
+    hipError_t e = hipSuccess;
+    for (size_t k = 0; k < nch && e == hipSuccess; ++k) {
+        const int b = (int)(k & 1);
+        const size_t a0 = k * per_chunk, m = std::min(per_chunk, n - a0);
+        if (k >= 2) e = hipEventSynchronize(st->ev[b]);  // buffer b's DMA (and the decode after it) queued before
+        if (e != hipSuccess) break;
+        bool plain = false;
+        const size_t bytes = encode(st->pin[b], a0, m, &plain);
+        raw_chunks += plain ? 1 : 0;
+        sent += bytes;
+        e = land(st->dev[b], st->pin[b], a0, m, bytes, plain, stream);
+        if (e == hipSuccess) e = hipEventRecord(st->ev[b], stream);
+    }
+    hipError_t e2 = hipEventRecord(st->done, stream);
+    if (e2 == hipSuccess) e2 = hipEventSynchronize(st->done);
+    if (trace())
+        fprintf(stderr, "[stage] h2d-packed %s %zu values as %zu B (%zu of %zu chunks plain) %.2f ms\n", what, n, sent,
+                raw_chunks, nch, now_ms() - t1);
+    return e != hipSuccess ? e : e2;
+}
+}  // namespace
+
+hipError_t stage_h2d_i32(int32_t* dst, const int32_t* src, size_t n, int device, hipStream_t stream) {
+    Stager* st = stager(device, 0);
+    if (n < kPackMin || !st) return stage_h2d(dst, src, 4 * n, device, stream);
+    std::unique_lock<std::mutex> g(st->mu);
+    if (!ready(st, 0) || !ready_dev(st)) {
+        g.unlock();
+        return stage_h2d(dst, src, 4 * n, device, stream);
+    }
+    const size_t B = (size_t)rcp_pack_block();
+    const size_t per_chunk = kChunk / 4;  // values: a plain chunk fills the buffer
+    auto encode = [&](char* pin, size_t a0, size_t m, bool* plain) -> size_t {
+        const size_t nb = (m + B - 1) / B;
+        int32_t* base = reinterpret_cast<int32_t*>(pin);
+        int32_t* slot = base + nb;
+        uint16_t* off = reinterpret_cast<uint16_t*>(pin + 8 * nb);
+        char* raw = pin + 8 * nb + 2 * ((m + 1) & ~size_t(1));
+        const size_t cap = (kChunk - (size_t)(raw - pin)) / (4 * B);
+        std::atomic<size_t> n_raw{0};
+        std::atomic<bool> over{false};
+        const int32_t* s = src + a0;
+        st->pool->run(kParts, [&](int i) {
+            alignas(16) uint16_t tmp[1024 + 8];
+            const size_t b0 = nb * (size_t)i / kParts, b1 = nb * (size_t)(i + 1) / kParts;
+            for (size_t b = b0; b < b1 && !over.load(std::memory_order_relaxed); ++b) {
+                const size_t j0 = b * B, len = std::min(B, m - j0);
+                const int32_t* v = s + j0;
+                // one pass with the first value as the base (sorted blocks), else the minimum
+                int32_t lo = v[0];
+                uint32_t bad = 0;
+                for (size_t j = 0; j < len; ++j) {
+                    const uint32_t o = (uint32_t)v[j] - (uint32_t)lo;
+                    bad |= o;
+                    tmp[j] = (uint16_t)o;
+                }
+                bool fits = (bad >> 16) == 0;
+                if (!fits) {
+                    int32_t hi = v[0];
+                    for (size_t j = 1; j < len; ++j) {
+                        lo = std::min(lo, v[j]);
+                        hi = std::max(hi, v[j]);
+                    }
+                    fits = (int64_t)hi - (int64_t)lo <= 65535;
+                    if (fits)
+                        for (size_t j = 0; j < len; ++j) tmp[j] = (uint16_t)((uint32_t)v[j] - (uint32_t)lo);
+                }
+                if (fits) {
+                    base[b] = lo;
+                    slot[b] = -1;
+                    copy_nt(reinterpret_cast<char*>(off + j0), reinterpret_cast<const char*>(tmp), 2 * len);
+                } else {
+                    const size_t q = n_raw.fetch_add(1, std::memory_order_relaxed);
+                    if (q >= cap) {
+                        over.store(true, std::memory_order_relaxed);
+                        break;
+                    }
+                    base[b] = 0;
+                    slot[b] = (int32_t)q;
+                    copy_nt(raw + 4 * B * q, reinterpret_cast<const char*>(v), 4 * len);
+                }
+            }
+        });
+        if (over.load()) {  // too many raw blocks: the chunk as it is
+            *plain = true;
+            st->pool->run(kParts, [&](int i) {
+                size_t a, z;
+                part_range(4 * m, i, &a, &z);
+                if (z > a) copy_nt(pin + a, reinterpret_cast<const char*>(s) + a, z - a);
+            });
+            return 4 * m;
+        }
+        return (size_t)(raw - pin) + 4 * B * std::min(n_raw.load(), cap);
+    };
+    auto land = [&](const char* dev, char* pin, size_t a0, size_t m, size_t bytes, bool plain, hipStream_t s) {
+        if (plain) return hipMemcpyAsync(dst + a0, pin, 4 * m, hipMemcpyHostToDevice, s);
+        hipError_t e = hipMemcpyAsync(const_cast<char*>(dev), pin, bytes, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = rcp_launch_unpack_i32(dev, (int64_t)m, dst + a0, s);
+        return e;
+    };
+    return h2d_packed(st, n, per_chunk, stream, "i32", encode, land);
+}
+
+hipError_t stage_h2d_strand(int8_t* dst, const int8_t* src, size_t n, int device, hipStream_t stream) {
+    Stager* st = stager(device, 0);
+    if (n < kPackMin || !st) return stage_h2d(dst, src, n, device, stream);
+    std::unique_lock<std::mutex> g(st->mu);
+    if (!ready(st, 0) || !ready_dev(st)) {
+        g.unlock();
+        return stage_h2d(dst, src, n, device, stream);
+    }
+    const size_t per_chunk = size_t(32) << 20;  // codes (8 MB packed): chunks pipeline encoding and DMA
+    // eight codes -> 16 bits: per byte, 3 for a code outside 0..2 (bytes >= 3: bit 7 set, or
+    // bits 0..6 + 125 carrying into bit 7), else the code; then the 2-bit fields gathered
+    auto pack8 = [](uint64_t w) -> uint32_t {
+        constexpr uint64_t k7F = 0x7F7F7F7F7F7F7F7Full, k80 = 0x8080808080808080ull, k03 = 0x0303030303030303ull;
+        const uint64_t inv = ((w & k7F) + 0x7D7D7D7D7D7D7D7Dull | w) & k80;  // bit 7 of each byte: invalid
+        uint64_t x = (w & k03) | ((inv >> 7) * 3);
+        x = (x | (x >> 6)) & 0x000F000F000F000Full;
+        x = (x | (x >> 12)) & 0x000000FF000000FFull;
+        x = (x | (x >> 24)) & 0xFFFFull;
+        return (uint32_t)x;
+    };
+    auto encode = [&](char* pin, size_t a0, size_t m, bool*) -> size_t {
+        const int8_t* s = src + a0;
+        const size_t words = (m + 3) / 4;  // packed bytes
+        const size_t groups = m / 8;       // whole groups of eight codes
+        st->pool->run(kParts, [&](int i) {
+            alignas(16) uint16_t tmp[2048];
+            const size_t g0 = groups * (size_t)i / kParts, g1 = groups * (size_t)(i + 1) / kParts;
+            for (size_t g = g0; g < g1; g += 2048) {
+                const size_t cnt = std::min<size_t>(2048, g1 - g);
+                for (size_t q = 0; q < cnt; ++q) {
+                    uint64_t w;
+                    std::memcpy(&w, s + 8 * (g + q), 8);
+                    tmp[q] = (uint16_t)pack8(w);
+                }
+                copy_nt(pin + 2 * g, reinterpret_cast<const char*>(tmp), 2 * cnt);
+            }
+        });
+        if (m % 8) {  // the last codes
+            uint64_t w = 0;
+            std::memcpy(&w, s + 8 * groups, m % 8);
+            const uint32_t x = pack8(w);
+            for (size_t q = 2 * groups; q < words; ++q) pin[q] = (char)(x >> (8 * (q - 2 * groups)));
+        }
+        return words;
+    };
+    auto land = [&](const char* dev, char* pin, size_t a0, size_t m, size_t bytes, bool, hipStream_t s) {
+        hipError_t e = hipMemcpyAsync(const_cast<char*>(dev), pin, bytes, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = rcp_launch_unpack_strand(dev, (int64_t)m, dst + a0, s);
+        return e;
+    };
+    return h2d_packed(st, n, per_chunk, stream, "strand", encode, land);
 }
 
 hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,

@@ -29,6 +29,12 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
 bool trace_on();
 double trace_ms();  // a steady clock in ms
 
+// int32 values (read starts) up as 16-bit offsets from per-block minima where the block's span
+// allows, strand codes four to a byte (codes outside 0..2 arrive as -1): decoded on the device
+// into dst.  Below 2^20 values, or without the device landing buffers: the plain staged copy.
+hipError_t stage_h2d_i32(int32_t* dst, const int32_t* src, size_t n, int device, hipStream_t stream);
+hipError_t stage_h2d_strand(int8_t* dst, const int8_t* src, size_t n, int device, hipStream_t stream);
+
 // A column-major matrix of bin numerators (rows x cols words, column stride sld) into the host's
 // double matrix (column stride dld): cell (i, c) = q * scale / div[i] as the device makes a mean
 // (rcp_pack_kernel), through the same pinned buffers, expanded by the copy threads.  Waits.

@@ -468,3 +468,51 @@ def test_rle_matrix_download_as_numerators(gpu, capfd, n_bins, scale, expand):
     lines = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith(("[stage] d2h", "[pack]"))]
     assert any("d2h-expand" in ln for ln in lines) == expand, lines
     assert np.array_equal(out.view(np.uint64), np.asfortranarray(ref).view(np.uint64))
+
+
+@pytest.mark.parametrize("sorted_reads", [True, False])
+def test_packed_read_uploads(gpu, capfd, sorted_reads):
+    """Host read arrays go up packed (rcp_stage.h stage_h2d_i32 / stage_h2d_strand): chromosomes,
+    starts and ends as 16-bit offsets from per-1024-read block minima -- blocks spanning 2^16 or
+    more (gaps, chromosome changes) raw, chunks with too many such blocks plain (the unsorted
+    sample) -- and strand codes four to a byte, codes outside 0..2 still dropping their reads.
+    The readset equals one built from the same arrays already on the device: streams, kept reads
+    and a profile, bit for bit."""
+    from recoup_amd.engine import ReadSet
+    from tests.test_gpu_random import CHROM_LEN, single_rows
+    rng = np.random.default_rng(3 + sorted_reads)
+    n = 3_000_000
+    codes = np.array([0, 1, 2, 0, 1, 2, -1, 7], np.int8)
+    chrom = np.sort(rng.integers(0, 3, n)).astype(np.int32)
+    start = np.empty(n, np.int32)
+    for c in range(3):
+        m = chrom == c
+        k = int(m.sum())
+        # clustered starts with a few long gaps (raw blocks)
+        gaps = rng.geometric(0.05, k).astype(np.int64)
+        gaps[rng.random(k) < 2e-4] += 200_000
+        start[m] = (1 + np.cumsum(gaps) % (CHROM_LEN[c] - 1000)).astype(np.int32)
+    if sorted_reads:
+        order = np.lexsort((start, chrom))
+        chrom, start = chrom[order], start[order]
+    else:
+        rng.shuffle(start)
+    end = start + rng.integers(0, 300, n).astype(np.int32)
+    strand = codes[rng.integers(0, len(codes), n)]
+    os.environ["RCP_TRACE"] = "1"
+    try:
+        host = ReadSet(chrom, start, end, strand, CHROM_LEN, device=0)
+    finally:
+        del os.environ["RCP_TRACE"]
+    lines = [ln for ln in capfd.readouterr().err.splitlines() if "h2d-packed" in ln]
+    assert len(lines) == 4, lines  # chrom, start, end, strand
+    if not sorted_reads:
+        assert any("i32" in ln and " 0 of " not in ln for ln in lines), lines  # plain chunks
+    dev = ReadSet(*(torch.from_numpy(a).cuda() for a in (chrom, start, end, strand)), CHROM_LEN, device=0)
+    assert host.n == dev.n == int(((strand >= 0) & (strand <= 2)).sum())
+    np.testing.assert_array_equal(host.stream_off, dev.stream_off)
+    rows = single_rows(rng, 2_000, 3000)
+    bins = Bins([("whole", 300)])
+    a, b = Plan(host, rows, bins).run(), Plan(dev, rows, bins).run()
+    assert np.array_equal(np.ascontiguousarray(a[0]).view(np.uint64), np.ascontiguousarray(b[0]).view(np.uint64))
+    np.testing.assert_array_equal(a[1], b[1])

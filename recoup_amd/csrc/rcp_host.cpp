@@ -2602,8 +2602,11 @@ extern "C" int rcp_cov_copy(const rcp_cov* c, int64_t* run_off, int32_t* values,
     HIP_TRY(g.err);
     // pinned double-buffered staging (rcp_stage.h) straight into the caller's arrays
     if (run_off) HIP_TRY(rcp::stage_d2h(run_off, c->run_off.p, 8 * ((size_t)c->n_rows + 1), c->device, nullptr));
-    if (values && c->n_runs) HIP_TRY(rcp::stage_d2h(values, c->values.p, 4 * (size_t)c->n_runs, c->device, nullptr));
-    if (lengths && c->n_runs) HIP_TRY(rcp::stage_d2h(lengths, c->lengths.p, 4 * (size_t)c->n_runs, c->device, nullptr));
+    // (depths and run lengths: 16-bit offsets within blocks where they fit, rcp_stage.h)
+    if (values && c->n_runs)
+        HIP_TRY(rcp::stage_d2h_i32(values, c->values.as<int32_t>(), (size_t)c->n_runs, c->device, nullptr));
+    if (lengths && c->n_runs)
+        HIP_TRY(rcp::stage_d2h_i32(lengths, c->lengths.as<int32_t>(), (size_t)c->n_runs, c->device, nullptr));
     if (valid && c->n_rows) HIP_TRY(rcp::stage_d2h(valid, c->valid.p, (size_t)c->n_rows, c->device, nullptr));
     return RCP_OK;
     RCP_CATCH
@@ -2722,10 +2725,10 @@ int rle_prepare(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, 
     HIP_TRY(d_len.alloc(4 * ((size_t)n_runs + 1)));
     HIP_TRY(d_val.alloc((dbl ? 8 : 4) * std::max<size_t>((size_t)n_runs, 1)));
     HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
-    if (n_runs) {
-        HIP_TRY(rcp::stage_h2d(d_len.p, cov->lengths, 4 * (size_t)n_runs, device, s));
-        HIP_TRY(rcp::stage_h2d(d_val.p, dbl ? (const void*)cov->dvalues : (const void*)cov->ivalues,
-                               (dbl ? 8 : 4) * (size_t)n_runs, device, s));
+    if (n_runs) {  // (integer runs: 16-bit offsets within blocks where they fit, rcp_stage.h)
+        HIP_TRY(rcp::stage_h2d_i32(d_len.as<int32_t>(), cov->lengths, (size_t)n_runs, device, s));
+        if (dbl) HIP_TRY(rcp::stage_h2d(d_val.p, cov->dvalues, 8 * (size_t)n_runs, device, s));
+        else HIP_TRY(rcp::stage_h2d_i32(d_val.as<int32_t>(), cov->ivalues, (size_t)n_runs, device, s));
     }
     HIP_TRY(hipMemsetAsync(d_len.as<int32_t>() + n_runs, 0, 4, s));
     if (R > 0) HIP_TRY(rcp::stage_h2d(d_off.p, cov->run_off, 8 * ((size_t)R + 1), device, s));

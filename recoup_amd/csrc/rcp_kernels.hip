@@ -4073,3 +4073,59 @@ extern "C" hipError_t rcp_launch_unpack_strand(const void* src, int64_t n, int8_
                        stream, static_cast<const uint8_t*>(src), n, dst);
     return hipGetLastError();
 }
+
+// The packed download of an int32 array (rcp_stage.cpp stage_d2h_i32): blocks of kPackBlock values
+// as their minimum + 16-bit offsets ([base x nb][flag x nb][offsets x n]); flag 1: the block's
+// values span 2^16 or more and the host copies it from the source itself
+__global__ void __launch_bounds__(kBlock) rcp_pack_i32_kernel(const int32_t* __restrict__ src, int64_t n, int64_t nb,
+                                                              char* __restrict__ dst) {
+    static_assert(kPackBlock == 4 * kBlock, "four values per thread");
+    __shared__ int32_t s_lo[kBlock / 64], s_hi[kBlock / 64];
+    const int64_t b = blockIdx.x;
+    const int64_t i0 = b * kPackBlock;
+    const int len = (int)min<int64_t>(kPackBlock, n - i0);
+    int32_t v[4];
+    int32_t lo = INT32_MAX, hi = INT32_MIN;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int j = threadIdx.x + kBlock * u;
+        v[u] = j < len ? src[i0 + j] : 0;
+        if (j < len) {
+            lo = min(lo, v[u]);
+            hi = max(hi, v[u]);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_lo[threadIdx.x >> 6] = lo;
+        s_hi[threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        lo = min(lo, s_lo[w]);
+        hi = max(hi, s_hi[w]);
+    }
+    const bool fits = (int64_t)hi - (int64_t)lo <= 65535;
+    uint16_t* off = reinterpret_cast<uint16_t*>(dst + 8 * nb) + i0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int j = threadIdx.x + kBlock * u;
+        if (j < len) off[j] = (uint16_t)((uint32_t)v[u] - (uint32_t)lo);
+    }
+    if (threadIdx.x == 0) {
+        reinterpret_cast<int32_t*>(dst)[b] = lo;
+        reinterpret_cast<int32_t*>(dst)[nb + b] = fits ? 0 : 1;
+    }
+}
+
+extern "C" hipError_t rcp_launch_pack_i32(const int32_t* src, int64_t n, void* dst, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const int64_t nb = (n + kPackBlock - 1) / kPackBlock;
+    hipLaunchKernelGGL(rcp_pack_i32_kernel, dim3((unsigned)nb), dim3(kBlock), 0, stream, src, n, nb,
+                       static_cast<char*>(dst));
+    return hipGetLastError();
+}

@@ -28,6 +28,7 @@ extern "C" {
 int rcp_pack_block(void);
 hipError_t rcp_launch_unpack_i32(const void* src, int64_t n, int32_t* dst, hipStream_t stream);
 hipError_t rcp_launch_unpack_strand(const void* src, int64_t n, int8_t* dst, hipStream_t stream);
+hipError_t rcp_launch_pack_i32(const int32_t* src, int64_t n, void* dst, hipStream_t stream);
 }
 
 namespace rcp {
@@ -119,7 +120,8 @@ struct Stager {
     hipEvent_t ev[2] = {nullptr, nullptr};
     hipEvent_t done = nullptr;
     std::unique_ptr<Pool> pool;
-    char* dev[2] = {nullptr, nullptr};  // H2D: device landing buffers of packed chunks (decoded into place)
+    char* dev[2] = {nullptr, nullptr};  // device buffers of packed chunks: H2D landing (decoded into place),
+                                        // D2H packing (rcp_pack_i32_kernel)
 };
 
 // Process lifetime: the pinned buffers are returned to the OS at exit (freeing them from a
@@ -463,6 +465,74 @@ hipError_t stage_h2d_strand(int8_t* dst, const int8_t* src, size_t n, int device
         return e;
     };
     return h2d_packed(st, n, per_chunk, stream, "strand", encode, land);
+}
+
+hipError_t stage_d2h_i32(int32_t* dst, const int32_t* src, size_t n, int device, hipStream_t stream) {
+    Stager* st = stager(device, 1);
+    if (n < kPackMin || !st) return stage_d2h(dst, src, 4 * n, device, stream);
+    std::unique_lock<std::mutex> g(st->mu);
+    if (!ready(st, 1) || !ready_dev(st)) {
+        g.unlock();
+        return stage_d2h(dst, src, 4 * n, device, stream);
+    }
+    const double t1 = trace() ? now_ms() : 0.0;
+    const size_t B = (size_t)rcp_pack_block();
+    const size_t per_chunk = size_t(16) << 20;  // values: 8 x nb + 2 x per_chunk bytes < the buffers
+    const size_t nch = (n + per_chunk - 1) / per_chunk;
+    size_t n_raw = 0;
+    hipError_t e = hipSuccess;
+    // chunk k: packed on the device into dev[k % 2], DMA'd into pin[k % 2]; expanded by the threads
+    // one iteration later, while chunk k + 1 is packed and in flight
+    auto bytes_of = [&](size_t m) { return 8 * ((m + B - 1) / B) + 2 * m; };
+    for (size_t k = 0; k <= nch && e == hipSuccess; ++k) {
+        if (k < nch) {
+            const int b = (int)(k & 1);
+            const size_t a0 = k * per_chunk, m = std::min(per_chunk, n - a0);
+            e = rcp_launch_pack_i32(src + a0, (int64_t)m, st->dev[b], stream);
+            if (e == hipSuccess) e = hipMemcpyAsync(st->pin[b], st->dev[b], bytes_of(m), hipMemcpyDeviceToHost, stream);
+            if (e == hipSuccess) e = hipEventRecord(st->ev[b], stream);
+        }
+        if (k > 0 && e == hipSuccess) {
+            const size_t j = k - 1;
+            const int b = (int)(j & 1);
+            const size_t a0 = j * per_chunk, m = std::min(per_chunk, n - a0), nb = (m + B - 1) / B;
+            e = hipEventSynchronize(st->ev[b]);
+            if (e != hipSuccess) break;
+            const char* pin = st->pin[b];
+            const int32_t* base = reinterpret_cast<const int32_t*>(pin);
+            const int32_t* flag = base + nb;
+            const uint16_t* off = reinterpret_cast<const uint16_t*>(pin + 8 * nb);
+            st->pool->run(kParts, [&](int i) {
+                alignas(16) int32_t tmp[1024];
+                for (size_t bl = nb * (size_t)i / kParts; bl < nb * (size_t)(i + 1) / kParts; ++bl) {
+                    if (flag[bl]) continue;  // (copied from the device below)
+                    const size_t j0 = bl * B, len = std::min(B, m - j0);
+                    const uint32_t bs = (uint32_t)base[bl];
+                    for (size_t q = 0; q < len; ++q) tmp[q] = (int32_t)(bs + off[j0 + q]);
+                    copy_nt(reinterpret_cast<char*>(dst + a0 + j0), reinterpret_cast<const char*>(tmp), 4 * len);
+                }
+            });
+            // blocks whose values span 2^16 or more: straight from the device array (a chunk with
+            // many of them as a whole: one copy)
+            size_t raw_here = 0;
+            for (size_t bl = 0; bl < nb; ++bl) raw_here += flag[bl] ? 1 : 0;
+            n_raw += raw_here;
+            if (raw_here > nb / 32) {
+                e = hipMemcpy(dst + a0, src + a0, 4 * m, hipMemcpyDeviceToHost);
+            } else {
+                for (size_t bl = 0; bl < nb && e == hipSuccess; ++bl) {
+                    if (!flag[bl]) continue;
+                    const size_t j0 = bl * B, len = std::min(B, m - j0);
+                    e = hipMemcpy(dst + a0 + j0, src + a0 + j0, 4 * len, hipMemcpyDeviceToHost);
+                }
+            }
+        }
+    }
+    hipError_t e2 = hipEventRecord(st->done, stream);
+    if (e2 == hipSuccess) e2 = hipEventSynchronize(st->done);
+    if (trace())
+        fprintf(stderr, "[stage] d2h-packed i32 %zu values, %zu raw blocks, %.2f ms\n", n, n_raw, now_ms() - t1);
+    return e != hipSuccess ? e : e2;
 }
 
 hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,

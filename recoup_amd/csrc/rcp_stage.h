@@ -34,6 +34,9 @@ double trace_ms();  // a steady clock in ms
 // into dst.  Below 2^20 values, or without the device landing buffers: the plain staged copy.
 hipError_t stage_h2d_i32(int32_t* dst, const int32_t* src, size_t n, int device, hipStream_t stream);
 hipError_t stage_h2d_strand(int8_t* dst, const int8_t* src, size_t n, int device, hipStream_t stream);
+// ... and down (Rle runs): blocks packed on the device as their first value + 16-bit offsets,
+// expanded by the copy threads; blocks that do not fit are copied as they are
+hipError_t stage_d2h_i32(int32_t* dst, const int32_t* src, size_t n, int device, hipStream_t stream);
 
 // A column-major matrix of bin numerators (rows x cols words, column stride sld) into the host's
 // double matrix (column stride dld): cell (i, c) = q * scale / div[i] as the device makes a mean

@@ -516,3 +516,38 @@ def test_packed_read_uploads(gpu, capfd, sorted_reads):
     a, b = Plan(host, rows, bins).run(), Plan(dev, rows, bins).run()
     assert np.array_equal(np.ascontiguousarray(a[0]).view(np.uint64), np.ascontiguousarray(b[0]).view(np.uint64))
     np.testing.assert_array_equal(a[1], b[1])
+
+
+def test_packed_run_downloads(gpu, capfd):
+    """calcCoverage's Rle list comes down packed (rcp_stage.h stage_d2h_i32: per-1024 blocks of
+    depths and run lengths as a base + 16-bit offsets, blocks that do not fit -- a zero run of
+    2^16 or more positions -- copied as they are): the runs equal the device encoder's, row for
+    row."""
+    from recoup_amd.engine import ReadSet, RowTable, coverage_rle_host
+    from tests.test_gpu_random import CHROM_LEN, make_reads
+    rng = np.random.default_rng(5)
+    c, st, en, sd = make_reads(rng, 1_500_000, widths=(20, 60), chroms=2)
+    # one read on chromosome 3: its 80-kb row is that read and one long zero run
+    c, st, en, sd = (np.append(c, 2).astype(np.int32), np.append(st, 1000).astype(np.int32),
+                     np.append(en, 1049).astype(np.int32), np.append(sd, 0).astype(np.int8))
+    rs = ReadSet(c, st, en, sd, CHROM_LEN, device=0)
+    R = 3_000
+    rc = rng.integers(0, 2, R)
+    rstart = np.array([rng.integers(1, CHROM_LEN[k] - 2000) for k in rc], np.int64)
+    rows = RowTable.from_ranges(np.append(rc, 2).astype(np.int32), np.append(rstart, 1000),
+                                np.append(rstart + 1999, 80_999), np.zeros(R + 1, np.int8))
+    os.environ["RCP_TRACE"] = "1"
+    try:
+        run_off, values, lengths, valid = coverage_rle_host(rs, rows)
+    finally:
+        del os.environ["RCP_TRACE"]
+    lines = [ln for ln in capfd.readouterr().err.splitlines() if "d2h-packed" in ln]
+    assert run_off[-1] >= (1 << 20) and len(lines) == 2, (run_off[-1], lines)
+    assert any(" 0 raw blocks" not in ln for ln in lines), lines  # the long zero run
+    ref = Plan(rs, rows, None).coverage(rle=True)
+    for r, e in enumerate(ref):
+        assert bool(valid[r]) == (e is not None)
+        if e is not None:
+            np.testing.assert_array_equal(values[run_off[r]:run_off[r + 1]], e[0])
+            np.testing.assert_array_equal(lengths[run_off[r]:run_off[r + 1]], e[1])
+    assert lengths[run_off[R + 1] - 1] == 80_000 - 50  # (the last row: read, then zeros)

@@ -242,14 +242,22 @@ void expand_nt(double* dst, const uint32_t* q, const double* rd, const double* d
     _mm_sfence();
 }
 
-// H2D landing buffers on the device (packed uploads), made on first use
-bool ready_dev(Stager* s) {
-    for (int b = 0; b < 2; ++b)
+// device buffers of packed transfers, made on first use on the stager's device
+bool ready_dev(Stager* s, int device) {
+    if (s->dev[0] && s->dev[1]) return true;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || (cur != device && hipSetDevice(device) != hipSuccess)) {
+        (void)hipGetLastError();
+        return false;
+    }
+    bool ok = true;
+    for (int b = 0; b < 2 && ok; ++b)
         if (!s->dev[b] && hipMalloc(reinterpret_cast<void**>(&s->dev[b]), kChunk) != hipSuccess) {
             (void)hipGetLastError();
-            return false;
+            ok = false;
         }
-    return true;
+    if (cur != device) (void)hipSetDevice(cur);
+    return ok;
 }
 
 }  // namespace
@@ -337,7 +345,7 @@ hipError_t stage_h2d_i32(int32_t* dst, const int32_t* src, size_t n, int device,
     Stager* st = stager(device, 0);
     if (n < kPackMin || !st) return stage_h2d(dst, src, 4 * n, device, stream);
     std::unique_lock<std::mutex> g(st->mu);
-    if (!ready(st, 0) || !ready_dev(st)) {
+    if (!ready(st, 0) || !ready_dev(st, device)) {
         g.unlock();
         return stage_h2d(dst, src, 4 * n, device, stream);
     }
@@ -418,7 +426,7 @@ hipError_t stage_h2d_strand(int8_t* dst, const int8_t* src, size_t n, int device
     Stager* st = stager(device, 0);
     if (n < kPackMin || !st) return stage_h2d(dst, src, n, device, stream);
     std::unique_lock<std::mutex> g(st->mu);
-    if (!ready(st, 0) || !ready_dev(st)) {
+    if (!ready(st, 0) || !ready_dev(st, device)) {
         g.unlock();
         return stage_h2d(dst, src, n, device, stream);
     }
@@ -471,7 +479,7 @@ hipError_t stage_d2h_i32(int32_t* dst, const int32_t* src, size_t n, int device,
     Stager* st = stager(device, 1);
     if (n < kPackMin || !st) return stage_d2h(dst, src, 4 * n, device, stream);
     std::unique_lock<std::mutex> g(st->mu);
-    if (!ready(st, 1) || !ready_dev(st)) {
+    if (!ready(st, 1) || !ready_dev(st, device)) {
         g.unlock();
         return stage_d2h(dst, src, 4 * n, device, stream);
     }

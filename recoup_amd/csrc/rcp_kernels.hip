@@ -1081,7 +1081,8 @@ rcp_locate_kernel(RcpPlanDev P) {
     // heaviest-first lean items (P.lpt): this block's 64 rows are two 32-row tiles; their
     // items' candidate reads are summed here and filed by class after the rows
     __shared__ uint32_t item_w[2][RCP_MAX_CRANGE_CHUNKS];
-    if (P.lpt && threadIdx.x < 2 * RCP_MAX_CRANGE_CHUNKS) item_w[threadIdx.x >> 4][threadIdx.x & 15] = 0u;
+    if (P.lpt && threadIdx.x < 2 * RCP_MAX_CRANGE_CHUNKS)
+        item_w[threadIdx.x / RCP_MAX_CRANGE_CHUNKS][threadIdx.x % RCP_MAX_CRANGE_CHUNKS] = 0u;
     if (P.lpt) __syncthreads();
     locate_rows<KS, KP>(P, xres, P.lpt ? item_w : nullptr);
     if (P.lpt) {

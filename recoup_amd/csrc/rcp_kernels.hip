@@ -3595,7 +3595,12 @@ __global__ void __launch_bounds__(kBlock) rcp_pack_kernel(RcpPlanDev P, const do
                                                           uint32_t* __restrict__ q_out, uint32_t* __restrict__ div,
                                                           uint32_t* __restrict__ bad_row) {
     const int r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= P.n_rows) return;
+    if (r >= P.out_ld) return;
+    if (r >= P.n_rows) {  // column padding: zeros (the download packs whole column runs)
+        for (int64_t k = (int64_t)blockIdx.y * kPackCols; k < min<int64_t>((int64_t)(blockIdx.y + 1) * kPackCols, P.n_cols); ++k)
+            q_out[k * P.out_ld + r] = 0u;
+        return;
+    }
     const RcpPart& part = P.part[0];
     const int32_t n = part.n_bins;
     uint32_t bs = 0;
@@ -3658,7 +3663,7 @@ extern "C" hipError_t rcp_launch_gather_rows(const double* out, int64_t ld, cons
 extern "C" hipError_t rcp_launch_pack(const RcpPlanDev* P, const double* out, uint32_t* q_out, uint32_t* div,
                                       uint32_t* bad_row, hipStream_t stream) {
     if (P->n_rows == 0 || P->n_cols == 0) return hipSuccess;
-    const dim3 grid((unsigned)((P->n_rows + kBlock - 1) / kBlock), (unsigned)((P->n_cols + kPackCols - 1) / kPackCols));
+    const dim3 grid((unsigned)((P->out_ld + kBlock - 1) / kBlock), (unsigned)((P->n_cols + kPackCols - 1) / kPackCols));
     hipLaunchKernelGGL(rcp_pack_kernel, grid, dim3(kBlock), 0, stream, *P, out, q_out, div, bad_row);
     return hipGetLastError();
 }

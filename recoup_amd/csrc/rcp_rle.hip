@@ -523,7 +523,12 @@ constexpr int kPackCols = 8;
 __global__ void __launch_bounds__(kRleBlock) rcp_rle_pack_kernel(RcpRleDev P, int64_t n_cols, uint32_t* __restrict__ q_out,
                                                                uint32_t* __restrict__ div, uint32_t* __restrict__ flag) {
     const int r = blockIdx.x * kRleBlock + threadIdx.x;
-    if (r >= P.n_rows) return;
+    if (r >= P.ld) return;
+    if (r >= P.n_rows) {  // column padding: zeros
+        for (int64_t k = (int64_t)blockIdx.y * kPackCols; k < min<int64_t>((int64_t)(blockIdx.y + 1) * kPackCols, n_cols); ++k)
+            q_out[k * P.ld + r] = 0u;
+        return;
+    }
     const RcpRleTask t = P.tasks[r];
     uint32_t bs = 0;
     bool bad = false;
@@ -555,7 +560,7 @@ __global__ void __launch_bounds__(kRleBlock) rcp_rle_pack_kernel(RcpRleDev P, in
 extern "C" hipError_t rcp_rle_pack(const RcpRleDev* P, int64_t n_cols, uint32_t* q_out, uint32_t* div, uint32_t* flag,
                                    hipStream_t stream) {
     if (P->n_rows == 0 || n_cols == 0) return hipSuccess;
-    const dim3 grid((unsigned)((P->n_rows + kRleBlock - 1) / kRleBlock), (unsigned)((n_cols + kPackCols - 1) / kPackCols));
+    const dim3 grid((unsigned)((P->ld + kRleBlock - 1) / kRleBlock), (unsigned)((n_cols + kPackCols - 1) / kPackCols));
     hipLaunchKernelGGL(rcp_rle_pack_kernel, grid, dim3(kRleBlock), 0, stream, *P, n_cols, q_out, div, flag);
     return hipGetLastError();
 }

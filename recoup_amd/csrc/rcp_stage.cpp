@@ -639,36 +639,89 @@ hipError_t stage_d2h_expand(double* dst, size_t dld, const uint32_t* src, size_t
         }
     };
     const size_t words = bytes / 4;
-    const size_t ch = chunk_of(bytes) / 4 / 1024 * 1024;  // words per chunk
-    const size_t nch = (words + ch - 1) / ch;
-    const char* s = reinterpret_cast<const char*>(src);
     hipError_t e = hipSuccess;
-    for (size_t k = 0; k <= nch && e == hipSuccess; ++k) {
-        if (k < nch) {
-            const int b = (int)(k & 1);
-            const size_t a0 = k * ch, len = std::min(ch, words - a0);
-            e = hipMemcpyAsync(st->pin[b], s + 4 * a0, 4 * len, hipMemcpyDeviceToHost, stream);
-            if (e == hipSuccess) e = hipEventRecord(st->ev[b], stream);
+    size_t n_raw = 0;
+    if (ready_dev(st, device)) {
+        // the numerators themselves travel packed: blocks of B words as their minimum + 16-bit
+        // offsets (rcp_pack_i32_kernel; C4's are bin sums of a few hundred), a block that does not
+        // fit fetched as it is -- 2 bytes a cell over PCIe
+        const size_t B = (size_t)rcp_pack_block();
+        const size_t per_chunk = size_t(16) << 20;
+        const size_t nch = (words + per_chunk - 1) / per_chunk;
+        auto bytes_of = [&](size_t m) { return 8 * ((m + B - 1) / B) + 2 * m; };
+        std::atomic<size_t> raw_count{0};
+        for (size_t k = 0; k <= nch && e == hipSuccess; ++k) {
+            if (k < nch) {
+                const int b = (int)(k & 1);
+                const size_t a0 = k * per_chunk, m = std::min(per_chunk, words - a0);
+                e = rcp_launch_pack_i32(reinterpret_cast<const int32_t*>(src) + a0, (int64_t)m, st->dev[b], stream);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(st->pin[b], st->dev[b], bytes_of(m), hipMemcpyDeviceToHost, stream);
+                if (e == hipSuccess) e = hipEventRecord(st->ev[b], stream);
+            }
+            if (k > 0 && e == hipSuccess) {
+                const size_t j = k - 1;
+                const int b = (int)(j & 1);
+                const size_t a0 = j * per_chunk, m = std::min(per_chunk, words - a0), nb = (m + B - 1) / B;
+                e = hipEventSynchronize(st->ev[b]);
+                if (e != hipSuccess) break;
+                const char* pin = st->pin[b];
+                const int32_t* base = reinterpret_cast<const int32_t*>(pin);
+                const int32_t* flag = base + nb;
+                const uint16_t* off = reinterpret_cast<const uint16_t*>(pin + 8 * nb);
+                std::atomic<int> err{0};
+                st->pool->run(kParts, [&](int i) {
+                    uint32_t tmp[1024];
+                    for (size_t bl = nb * (size_t)i / kParts; bl < nb * (size_t)(i + 1) / kParts; ++bl) {
+                        const size_t j0 = bl * B, len = std::min(B, m - j0);
+                        if (flag[bl]) {  // (values spanning 2^16 or more: the block as it is)
+                            raw_count.fetch_add(1, std::memory_order_relaxed);
+                            if (hipMemcpy(tmp, src + a0 + j0, 4 * len, hipMemcpyDeviceToHost) != hipSuccess) {
+                                err.store(1);
+                                return;
+                            }
+                        } else {
+                            const uint32_t bs = (uint32_t)base[bl];
+                            for (size_t q = 0; q < len; ++q) tmp[q] = bs + off[j0 + q];
+                        }
+                        scatter(tmp, a0 + j0, a0 + j0, a0 + j0 + len);
+                    }
+                });
+                if (err.load()) e = hipErrorUnknown;
+            }
         }
-        if (k > 0 && e == hipSuccess) {
-            const size_t j = k - 1;
-            const int b = (int)(j & 1);
-            const size_t a0 = j * ch, len = std::min(ch, words - a0);
-            e = hipEventSynchronize(st->ev[b]);
-            if (e != hipSuccess) break;
-            const uint32_t* pin = reinterpret_cast<const uint32_t*>(st->pin[b]);
-            st->pool->run(kParts, [&](int i) {
-                const size_t per = (len + kParts - 1) / kParts;
-                const size_t a = std::min(len, per * (size_t)i), z = std::min(len, a + per);
-                if (z > a) scatter(pin, a0, a0 + a, a0 + z);
-            });
+        n_raw = raw_count.load();
+    } else {
+        const size_t ch = chunk_of(bytes) / 4 / 1024 * 1024;  // words per chunk
+        const size_t nch = (words + ch - 1) / ch;
+        const char* s = reinterpret_cast<const char*>(src);
+        for (size_t k = 0; k <= nch && e == hipSuccess; ++k) {
+            if (k < nch) {
+                const int b = (int)(k & 1);
+                const size_t a0 = k * ch, len = std::min(ch, words - a0);
+                e = hipMemcpyAsync(st->pin[b], s + 4 * a0, 4 * len, hipMemcpyDeviceToHost, stream);
+                if (e == hipSuccess) e = hipEventRecord(st->ev[b], stream);
+            }
+            if (k > 0 && e == hipSuccess) {
+                const size_t j = k - 1;
+                const int b = (int)(j & 1);
+                const size_t a0 = j * ch, len = std::min(ch, words - a0);
+                e = hipEventSynchronize(st->ev[b]);
+                if (e != hipSuccess) break;
+                const uint32_t* pin = reinterpret_cast<const uint32_t*>(st->pin[b]);
+                st->pool->run(kParts, [&](int i) {
+                    const size_t per = (len + kParts - 1) / kParts;
+                    const size_t a = std::min(len, per * (size_t)i), z = std::min(len, a + per);
+                    if (z > a) scatter(pin, a0, a0 + a, a0 + z);
+                });
+            }
         }
     }
     hipError_t e2 = hipEventRecord(st->done, stream);
     if (e2 == hipSuccess) e2 = hipEventSynchronize(st->done);
     if (trace())
-        fprintf(stderr, "[stage] d2h-expand %zu B (%zu cells) wait %.2f ms copy %.2f ms\n", bytes, rows * cols, t1 - t0,
-                now_ms() - t1);
+        fprintf(stderr, "[stage] d2h-expand %zu B (%zu cells, %zu raw blocks) wait %.2f ms copy %.2f ms\n", bytes,
+                rows * cols, n_raw, t1 - t0, now_ms() - t1);
     return e != hipSuccess ? e : e2;
 }
 

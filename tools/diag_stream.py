@@ -56,7 +56,14 @@ def stats(name, xs):
     print(f"{name}: median {xs[len(xs) // 2]:.2f} ms, min {xs[0]:.2f}, all {[round(x, 1) for x in xs]}", flush=True)
 
 
-one, three, rle, rle_ph = [], [], [], []
+one, three, rle, rle_ph, fresh = [], [], [], [], []
+for k in range(max(3, reps // 2)):  # into a matrix never touched before, as R's allocMatrix gives it
+    f = np.empty((bins.n_cols, rows.n_rows))
+    a = time.perf_counter()
+    profile_reads([host], seqlen, rows, bins, 0, [f])
+    fresh.append((time.perf_counter() - a) * 1e3)
+    check(f"fresh[{k}]", f)
+    del f
 for k in range(reps):
     torch.cuda.synchronize()
     a = time.perf_counter()
@@ -86,6 +93,7 @@ for k in range(max(3, reps // 2)):
     rle.append((e - a) * 1e3)
     rle_ph.append(((b - a) * 1e3, (c - b) * 1e3, (e - c) * 1e3))
 stats("one sample, one call", one)
+stats("one sample, one call, fresh matrix", fresh)
 stats("three samples, per sample", three)
 stats("rle path", rle)
 print("rle phases (readset, coverage_rle, profile_rle):", [tuple(round(x, 1) for x in p) for p in rle_ph])

@@ -14,7 +14,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
             "-fvisibility=hidden"]
 SOURCES = ["rcp_kernels.hip", "rcp_rle.hip", "rcp_shard.hip", "rcp_host.cpp", "rcp_shard.cpp", "rcp_stage.cpp", "rcp_bam.cpp"]
-DEPS = ["rcp_internal.h", "rcp_device.h", "rcp_divrn.h", "rcp_rng.h", "rcp_stage.h", "rcp_splitvector.h", "rcp_rle.h", os.path.join("..", "..", "include", "recoup_amd.h")]
+DEPS = ["rcp_internal.h", "rcp_device.h", "rcp_divrn.h", "rcp_rng.h", "rcp_stage.h", "rcp_pack.h", "rcp_splitvector.h", "rcp_rle.h", os.path.join("..", "..", "include", "recoup_amd.h")]
 
 
 def _newer(target, sources):

@@ -9,6 +9,8 @@
 // (rcp_profile_multi drives one host thread per GPU).
 #include "rcp_stage.h"
 
+#include "rcp_pack.h"
+
 #include <emmintrin.h>
 
 #include <algorithm>
@@ -367,26 +369,8 @@ hipError_t stage_h2d_i32(int32_t* dst, const int32_t* src, size_t n, int device,
             for (size_t b = b0; b < b1 && !over.load(std::memory_order_relaxed); ++b) {
                 const size_t j0 = b * B, len = std::min(B, m - j0);
                 const int32_t* v = s + j0;
-                // one pass with the first value as the base (sorted blocks), else the minimum
-                int32_t lo = v[0];
-                uint32_t bad = 0;
-                for (size_t j = 0; j < len; ++j) {
-                    const uint32_t o = (uint32_t)v[j] - (uint32_t)lo;
-                    bad |= o;
-                    tmp[j] = (uint16_t)o;
-                }
-                bool fits = (bad >> 16) == 0;
-                if (!fits) {
-                    int32_t hi = v[0];
-                    for (size_t j = 1; j < len; ++j) {
-                        lo = std::min(lo, v[j]);
-                        hi = std::max(hi, v[j]);
-                    }
-                    fits = (int64_t)hi - (int64_t)lo <= 65535;
-                    if (fits)
-                        for (size_t j = 0; j < len; ++j) tmp[j] = (uint16_t)((uint32_t)v[j] - (uint32_t)lo);
-                }
-                if (fits) {
+                int32_t lo = 0;
+                if (rcp_pack_block16(v, (int)len, tmp, &lo)) {
                     base[b] = lo;
                     slot[b] = -1;
                     copy_nt(reinterpret_cast<char*>(off + j0), reinterpret_cast<const char*>(tmp), 2 * len);
@@ -431,17 +415,7 @@ hipError_t stage_h2d_strand(int8_t* dst, const int8_t* src, size_t n, int device
         return stage_h2d(dst, src, n, device, stream);
     }
     const size_t per_chunk = size_t(32) << 20;  // codes (8 MB packed): chunks pipeline encoding and DMA
-    // eight codes -> 16 bits: per byte, 3 for a code outside 0..2 (bytes >= 3: bit 7 set, or
-    // bits 0..6 + 125 carrying into bit 7), else the code; then the 2-bit fields gathered
-    auto pack8 = [](uint64_t w) -> uint32_t {
-        constexpr uint64_t k7F = 0x7F7F7F7F7F7F7F7Full, k80 = 0x8080808080808080ull, k03 = 0x0303030303030303ull;
-        const uint64_t inv = ((w & k7F) + 0x7D7D7D7D7D7D7D7Dull | w) & k80;  // bit 7 of each byte: invalid
-        uint64_t x = (w & k03) | ((inv >> 7) * 3);
-        x = (x | (x >> 6)) & 0x000F000F000F000Full;
-        x = (x | (x >> 12)) & 0x000000FF000000FFull;
-        x = (x | (x >> 24)) & 0xFFFFull;
-        return (uint32_t)x;
-    };
+    auto pack8 = [](uint64_t w) { return rcp_pack_strand8(w); };  // (rcp_pack.h)
     auto encode = [&](char* pin, size_t a0, size_t m, bool*) -> size_t {
         const int8_t* s = src + a0;
         const size_t words = (m + 3) / 4;  // packed bytes

@@ -201,3 +201,17 @@ def test_reciprocal_division_is_correctly_rounded(tmp_path):
                            exe, os.path.join(root, "tests", "native", "div_rn_check.c"), "-lm"])
     r = subprocess.run([exe, "18", "600", "2000000"], capture_output=True, text=True)
     assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout + r.stderr
+
+
+def test_packed_transfer_encoders(tmp_path):
+    """The host encoders of the packed transfers (recoup_amd/csrc/rcp_pack.h, rcp_stage.cpp): strand
+    codes four to a byte (every byte value in every position; codes outside 0..2 -> 3) and blocks of
+    int32 as a base + 16-bit offsets (decoded back exactly; refused exactly when the span is 2^16 or
+    more)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "pack_check")
+    subprocess.check_call(["gcc", "-O2", "-I", os.path.join(root, "recoup_amd", "csrc"), "-o", exe,
+                           os.path.join(root, "tests", "native", "pack_check.c")])
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout + r.stderr

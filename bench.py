@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+`--gpus N > 1` without a torch.distributed environment (WORLD_SIZE unset) starts the N ranks
+itself: torch.distributed.run as a CHILD process (this process never touches a GPU; it exits
+with the launcher's status), after checking that N devices are visible (RCP_SHARE_GPU=1: a
+rehearsal of N ranks on fewer GPUs, over gloo).  Under a launcher, --gpus must equal WORLD_SIZE.
+
 A step is one pass of the hot path -- calcCoverage + profileMatrix fused: locate,
 heavy-slice, pileup-bin and interpolation kernels -- over one synthetic workload (default
 C4: 200k ChIP peak summits +-1 kb, 1000 bins, 200M reads) with the reads, region tables and
@@ -42,7 +47,8 @@ PILEUP_KERNELS = {0: "rcp_pileup_kernel", 1: "rcp_pileup_lean_kernel", 2: "rcp_p
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks, one per GPU); default WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=["c4", "c2", "c3", "c5"])
@@ -203,17 +209,79 @@ def load_traffic(path, args, kernel, R, n_reads, world):
     return None
 
 
+class Refused(SystemExit):
+    """A bench configuration that cannot run as asked (exit status 2, message on stderr)."""
+
+    def __init__(self, msg):
+        log(f"bench.py: {msg}")
+        super().__init__(2)
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_plan(args, env, n_visible, argv, port=None):
+    """How this invocation runs: (world, None) to run here as one rank of `world`, or (N, cmd)
+    to start N ranks as a child torch.distributed.run.  `n_visible` = torch.cuda.device_count()
+    (on this image that count does not initialise the GPU, so the launcher process never does).
+    Refuses (exit status 2) when N GPUs are asked for and fewer are visible -- unless
+    RCP_SHARE_GPU=1 (several ranks per device: a rehearsal) -- or when --gpus disagrees with the
+    launcher's WORLD_SIZE."""
+    share = env.get("RCP_SHARE_GPU") == "1"
+    if env.get("WORLD_SIZE") is not None:
+        world = int(env["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            raise Refused(f"--gpus {args.gpus} but the launcher started WORLD_SIZE = {world} ranks")
+        if not share and n_visible < world:
+            raise Refused(f"{world} ranks but {n_visible} visible GPU(s) (RCP_SHARE_GPU=1 to share them)")
+        return world, None
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise Refused(f"--gpus {n}")
+    if not share and n_visible < n:
+        raise Refused(f"--gpus {n} but {n_visible} visible GPU(s) (RCP_SHARE_GPU=1 to share them)")
+    if n == 1:
+        return 1, None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port or free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    return n, cmd
+
+
+def devices_used(world, n_visible, share):
+    """Distinct GPUs the ranks run on (rank r on device r % n_visible when they share)."""
+    if not share:
+        return world
+    return len({r % max(n_visible, 1) for r in range(world)})
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    n_visible = torch.cuda.device_count()
+    share = os.environ.get("RCP_SHARE_GPU") == "1"
+    world, cmd = launch_plan(args, os.environ, n_visible, sys.argv[1:])
+    if cmd is not None:
+        # N ranks as children; this process has not touched the GPU (no exec after GPU init)
+        log("bench.py: starting", " ".join(cmd))
+        env = dict(os.environ)
+        if share:
+            env.setdefault("RCP_DIST_BACKEND", "gloo")
+        sys.exit(__import__("subprocess").call(cmd, env=env))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
-    # rehearsal of the N > 1 path on fewer GPUs: RCP_DIST_BACKEND=gloo RCP_SHARE_GPU=1 puts
-    # several ranks on one device and the barrier / max-reduction / gather on the host
-    backend = os.environ.get("RCP_DIST_BACKEND", "nccl")
-    if os.environ.get("RCP_SHARE_GPU") == "1":
-        local = local % torch.cuda.device_count()
+    # rehearsal of the N > 1 path on fewer GPUs: RCP_SHARE_GPU=1 puts several ranks on one device
+    # and (RCP_DIST_BACKEND=gloo, its default then: RCCL needs one rank per GPU) the barrier /
+    # max-reduction / gather on the host
+    backend = os.environ.get("RCP_DIST_BACKEND", "gloo" if share else "nccl")
+    if share:
+        local = local % max(n_visible, 1)
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
@@ -243,6 +311,11 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] data {args.config}: shard rows [{lo}, {hi}) of {R_total}, {n_reads} of {n_reads_total} "
         f"reads in {time.time() - t0:.1f}s")
+    shards = [{"rank": rank, "device": local, "rows": [lo, hi], "reads": n_reads}]
+    if dist:  # every rank's shard, for the line rank 0 prints
+        got = [None] * world
+        tdist.all_gather_object(got, shards[0])
+        shards = got
 
     t1 = time.time()
     rs = ReadSet(*reads, data["seqlen"], device=local)
@@ -427,6 +500,8 @@ def main():
             "value": value,
             "unit": "region-bins/s",
             "n_gpus": world,
+            "devices_used": devices_used(world, n_visible, share),
+            "shared_gpu": share,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": step_ms,
@@ -441,6 +516,7 @@ def main():
                 "parallelism": f"region-sharded x{world}: one contiguous region shard per GPU, balanced by "
                                f"overlapping reads; no data-path collective",
                 "rank0_shard": {"regions": R, "reads": n_reads, "sim_shard": args.sim_shard},
+                "shards": shards,
                 "inflight": D,
                 "inflight_note": "samples in flight on separate HIP streams: D distinct samples (independent "
                                  "read sets, same regions), every step one complete pass of one sample (D > 1: "

@@ -173,6 +173,10 @@ calcCoverage <- function(input, mask, strand = NULL, ignore.strand = TRUE, rc = 
     if (!own) {
         if (!identical(strand, input$strand))
             stop("the readset was prepared with another strand filter")
+        # a readset split over several devices holds the reads of ITS row table only
+        if (!is.null(input$rows) &&
+            !identical(input$rows, .rcpRows(mask, input$levels, ignore.strand)))
+            stop("the readset was split over the devices for another mask")
         rs <- input
     } else if (is.character(input)) {
         if (length(grep("\\.bam$", input, ignore.case = TRUE, perl = TRUE)) == 0)

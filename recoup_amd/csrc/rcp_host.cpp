@@ -485,12 +485,9 @@ int ensure_stranded(const rcp_readset* crs) {
 
 namespace rcpi {
 
-int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_readset** out) {
-    if (!d || !out) return fail(RCP_EINVAL, "NULL argument");
-    if (!(layouts & (kLayMerged | kLayStranded))) return fail(RCP_EINVAL, "internal: no layout requested");
-    *out = nullptr;
-    int rc = check_device(d->device);
-    if (rc) return rc;
+// The read descriptor's shape (sizes, NULL arrays, runs that cover the reads), before any copy:
+// what readset_build and every entry point taking host read arrays check first
+int validate_reads(const rcp_reads_desc* d) {
     if (d->n < 0 || d->n >= (int64_t(1) << 31)) return fail(RCP_EUNSUPPORTED, "read count %lld outside [0, 2^31)", (long long)d->n);
     if (d->n_chrom <= 0 || d->n_chrom > (1 << 20)) return fail(RCP_EINVAL, "n_chrom = %d", d->n_chrom);
     if (d->n > 0 && (!d->start || !d->strand)) return fail(RCP_EINVAL, "NULL read array");
@@ -520,6 +517,29 @@ int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_reads
                                      (long long)d->n);
     }
     if (d->strand_filter < -1 || d->strand_filter > 2) return fail(RCP_EINVAL, "strand_filter = %d", d->strand_filter);
+    return RCP_OK;
+}
+
+// A row table's shape: non-NULL arrays, seg_off from 0 and never decreasing
+int validate_rows(const rcp_rows_desc* rows) {
+    const int32_t R = rows->n_rows;
+    if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
+    if (R > 0 && (!rows->seg_off || !rows->seg_chrom || !rows->seg_start || !rows->seg_end || !rows->seg_strand))
+        return fail(RCP_EINVAL, "NULL row array");
+    if (R > 0 && rows->seg_off[0] != 0) return fail(RCP_EINVAL, "seg_off[0] != 0");
+    for (int32_t r = 0; r < R; ++r)
+        if (rows->seg_off[r + 1] < rows->seg_off[r]) return fail(RCP_EINVAL, "seg_off not monotone at row %d", r);
+    return RCP_OK;
+}
+
+int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_readset** out) {
+    if (!d || !out) return fail(RCP_EINVAL, "NULL argument");
+    if (!(layouts & (kLayMerged | kLayStranded))) return fail(RCP_EINVAL, "internal: no layout requested");
+    *out = nullptr;
+    int rc = check_device(d->device);
+    if (rc) return rc;
+    rc = validate_reads(d);
+    if (rc) return rc;
     DeviceGuard g(d->device);
     HIP_TRY(g.err);
     auto rs = std::make_unique<rcp_readset>();
@@ -1815,10 +1835,16 @@ extern "C" int rcp_profile_reads(const rcp_reads_desc* samples, int32_t n_sample
                         samples[i].device, dev);
     int rc = check_device(dev);
     if (rc) return rc;
+    // every descriptor checked before anything is cut or copied (stream_cut indexes the row table,
+    // the packed uploads read the strand arrays)
+    rc = validate_rows(rows);
+    if (rc) return rc;
+    for (int i = 0; i < n_samples; ++i)
+        if ((rc = validate_reads(&samples[i]))) {
+            const std::string msg = rcp_last_error();
+            return fail(rc, "samples[%d]: %s", i, msg.c_str());
+        }
     const int32_t R = rows->n_rows;
-    if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
-    if (R > 0 && (!rows->seg_off || !rows->seg_chrom || !rows->seg_start || !rows->seg_end || !rows->seg_strand))
-        return fail(RCP_EINVAL, "NULL row array");
     // the one layout the row table searches, built from the uploaded copies right away
     const int layout = rows->ignore_strand ? kLayMerged : kLayStranded;
     // Work items: a sample of sorted reads is cut into row blocks, each with the slice of the
@@ -2183,7 +2209,12 @@ int download_packed(const double* d_out, size_t ld, size_t R, size_t C, double s
         HIP_TRY(rcp::stage_d2h_2d(host, 8 * host_ld, d_out, 8 * ld, 8 * R, C, device, s));
         return RCP_OK;
     }
-    HIP_TRY(rcp::stage_d2h_expand(host, host_ld, q.as<uint32_t>(), ld, R, C, h.data(), scale, device, s));
+    bool no_buffers = false;
+    HIP_TRY(rcp::stage_d2h_expand(host, host_ld, q.as<uint32_t>(), ld, R, C, h.data(), scale, device, s, &no_buffers));
+    if (no_buffers) {  // no pinned buffers for this device: the doubles, as a direct copy
+        HIP_TRY(rcp::stage_d2h_2d(host, 8 * host_ld, d_out, 8 * ld, 8 * R, C, device, s));
+        return RCP_OK;
+    }
     if (!bad.empty()) {  // those rows' doubles, gathered on the device, over the expanded cells
         const size_t nb = bad.size();
         PoolBuf d_rows(s), d_vals(s);
@@ -2924,7 +2955,7 @@ int rle_prepare(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, 
     return RCP_OK;
 }
 
-int rle_finish(RleJob* job, int device, double* out, int64_t out_ld, uint8_t* row_valid, hipStream_t s) {
+int rle_finish_run(RleJob* job, int device, double* out, int64_t out_ld, uint8_t* row_valid, hipStream_t s) {
     DeviceGuard g(device);
     HIP_TRY(g.err);
     HIP_TRY(rcp_rle_profile_launch(&job->P, job->dbl ? 1 : 0, job->lds, s));
@@ -2945,6 +2976,19 @@ int rle_finish(RleJob* job, int device, double* out, int64_t out_ld, uint8_t* ro
     if (row_valid)
         for (int32_t r = 0; r < job->R; ++r) row_valid[r] = (job->is_null && job->is_null[r]) ? 0 : 1;
     return RCP_OK;
+}
+
+// The profile of a prepared job and its rows down; on every exit the stream has drained, so the
+// caller may hand the job's pool buffers back (they are recorded idle on the preparer's stream,
+// while the kernel ran on `s`)
+int rle_finish(RleJob* job, int device, double* out, int64_t out_ld, uint8_t* row_valid, hipStream_t s) {
+    const int rc = rle_finish_run(job, device, out, out_ld, row_valid, s);
+    if (rc != RCP_OK) {
+        DeviceGuard g(device);
+        (void)hipStreamSynchronize(s);
+        (void)hipGetLastError();
+    }
+    return rc;
 }
 
 }  // namespace

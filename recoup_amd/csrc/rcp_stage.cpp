@@ -499,15 +499,18 @@ hipError_t stage_d2h_i32(int32_t* dst, const int32_t* src, size_t n, int device,
             size_t raw_here = 0;
             for (size_t bl = 0; bl < nb; ++bl) raw_here += flag[bl] ? 1 : 0;
             n_raw += raw_here;
+            // (on the caller's stream, one synchronisation: the next chunk's pack and DMA, already
+            // queued, finish first)
             if (raw_here > nb / 32) {
-                e = hipMemcpy(dst + a0, src + a0, 4 * m, hipMemcpyDeviceToHost);
+                e = hipMemcpyAsync(dst + a0, src + a0, 4 * m, hipMemcpyDeviceToHost, stream);
             } else {
                 for (size_t bl = 0; bl < nb && e == hipSuccess; ++bl) {
                     if (!flag[bl]) continue;
                     const size_t j0 = bl * B, len = std::min(B, m - j0);
-                    e = hipMemcpy(dst + a0 + j0, src + a0 + j0, 4 * len, hipMemcpyDeviceToHost);
+                    e = hipMemcpyAsync(dst + a0 + j0, src + a0 + j0, 4 * len, hipMemcpyDeviceToHost, stream);
                 }
             }
+            if (raw_here && e == hipSuccess) e = hipStreamSynchronize(stream);
         }
     }
     hipError_t e2 = hipEventRecord(st->done, stream);
@@ -580,7 +583,8 @@ hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch
 }
 
 hipError_t stage_d2h_expand(double* dst, size_t dld, const uint32_t* src, size_t sld, size_t rows, size_t cols,
-                            const uint32_t* div, double scale, int device, hipStream_t stream) {
+                            const uint32_t* div, double scale, int device, hipStream_t stream, bool* unavailable) {
+    if (unavailable) *unavailable = false;
     if (rows == 0 || cols == 0) return hipSuccess;
     // per row: the reciprocal of a power-of-two width (0 for a NULL row) or the width to divide by
     std::vector<double> rd(rows), dv(rows);
@@ -598,7 +602,12 @@ hipError_t stage_d2h_expand(double* dst, size_t dld, const uint32_t* src, size_t
     std::unique_lock<std::mutex> g;
     if (st) g = take(st, std::max(bytes, kShared));  // (always the buffers: the expansion needs them)
     const double t1 = trace() ? now_ms() : 0.0;
-    if (!g.owns_lock() || !ready(st, 1)) return hipErrorOutOfMemory;
+    if (!g.owns_lock() || !ready(st, 1)) {
+        // no pinned buffers on this device (an ordinal past the stagers, or hipHostMalloc refused):
+        // the caller downloads the doubles instead
+        if (unavailable) *unavailable = true;
+        return unavailable ? hipSuccess : hipErrorOutOfMemory;
+    }
     // device words [a, z) of the linear span -> their host cells (padding skipped)
     auto scatter = [&](const uint32_t* pin, size_t base, size_t a, size_t z) {
         while (a < z) {
@@ -623,7 +632,8 @@ hipError_t stage_d2h_expand(double* dst, size_t dld, const uint32_t* src, size_t
         const size_t per_chunk = size_t(16) << 20;
         const size_t nch = (words + per_chunk - 1) / per_chunk;
         auto bytes_of = [&](size_t m) { return 8 * ((m + B - 1) / B) + 2 * m; };
-        std::atomic<size_t> raw_count{0};
+        std::vector<uint32_t> raw;  // raw blocks of the chunk being drained (host copy)
+        std::vector<size_t> raw_blocks;
         for (size_t k = 0; k <= nch && e == hipSuccess; ++k) {
             if (k < nch) {
                 const int b = (int)(k & 1);
@@ -643,28 +653,43 @@ hipError_t stage_d2h_expand(double* dst, size_t dld, const uint32_t* src, size_t
                 const int32_t* base = reinterpret_cast<const int32_t*>(pin);
                 const int32_t* flag = base + nb;
                 const uint16_t* off = reinterpret_cast<const uint16_t*>(pin + 8 * nb);
-                std::atomic<int> err{0};
+                // blocks whose values span 2^16 or more come as they are, fetched by THIS thread (on
+                // the caller's device and stream; the pool's threads make no HIP calls): a chunk with
+                // many of them in one copy, else block by block, all before one synchronisation
+                raw_blocks.clear();
+                for (size_t bl = 0; bl < nb; ++bl)
+                    if (flag[bl]) raw_blocks.push_back(bl);
+                n_raw += raw_blocks.size();
+                if (!raw_blocks.empty()) {
+                    if (raw.size() < m) raw.resize(m);
+                    if (raw_blocks.size() > nb / 32) {
+                        e = hipMemcpyAsync(raw.data(), src + a0, 4 * m, hipMemcpyDeviceToHost, stream);
+                    } else {
+                        for (size_t bl : raw_blocks) {
+                            const size_t j0 = bl * B, len = std::min(B, m - j0);
+                            e = hipMemcpyAsync(raw.data() + j0, src + a0 + j0, 4 * len, hipMemcpyDeviceToHost, stream);
+                            if (e != hipSuccess) break;
+                        }
+                    }
+                    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+                    if (e != hipSuccess) break;
+                }
+                const uint32_t* rawp = raw.data();
                 st->pool->run(kParts, [&](int i) {
                     uint32_t tmp[1024];
                     for (size_t bl = nb * (size_t)i / kParts; bl < nb * (size_t)(i + 1) / kParts; ++bl) {
                         const size_t j0 = bl * B, len = std::min(B, m - j0);
-                        if (flag[bl]) {  // (values spanning 2^16 or more: the block as it is)
-                            raw_count.fetch_add(1, std::memory_order_relaxed);
-                            if (hipMemcpy(tmp, src + a0 + j0, 4 * len, hipMemcpyDeviceToHost) != hipSuccess) {
-                                err.store(1);
-                                return;
-                            }
-                        } else {
-                            const uint32_t bs = (uint32_t)base[bl];
-                            for (size_t q = 0; q < len; ++q) tmp[q] = bs + off[j0 + q];
+                        if (flag[bl]) {
+                            scatter(rawp + j0, a0 + j0, a0 + j0, a0 + j0 + len);
+                            continue;
                         }
+                        const uint32_t bs = (uint32_t)base[bl];
+                        for (size_t q = 0; q < len; ++q) tmp[q] = bs + off[j0 + q];
                         scatter(tmp, a0 + j0, a0 + j0, a0 + j0 + len);
                     }
                 });
-                if (err.load()) e = hipErrorUnknown;
             }
         }
-        n_raw = raw_count.load();
     } else {
         const size_t ch = chunk_of(bytes) / 4 / 1024 * 1024;  // words per chunk
         const size_t nch = (words + ch - 1) / ch;

@@ -41,8 +41,10 @@ hipError_t stage_d2h_i32(int32_t* dst, const int32_t* src, size_t n, int device,
 // A column-major matrix of bin numerators (rows x cols words, column stride sld) into the host's
 // double matrix (column stride dld): cell (i, c) = q * scale / div[i] as the device makes a mean
 // (rcp_pack_kernel), through the same pinned buffers, expanded by the copy threads.  Waits.
+// When the device has no pinned buffers (no stager for its ordinal, hipHostMalloc refused), sets
+// *unavailable and returns hipSuccess without copying: the caller downloads the doubles instead.
 hipError_t stage_d2h_expand(double* dst, size_t dld, const uint32_t* src, size_t sld, size_t rows, size_t cols,
-                            const uint32_t* div, double scale, int device, hipStream_t stream);
+                            const uint32_t* div, double scale, int device, hipStream_t stream, bool* unavailable);
 
 inline hipError_t stage_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t stream) {
     return stage_d2h_2d(dst, bytes, src, bytes, bytes, 1, device, stream);

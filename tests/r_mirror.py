@@ -193,16 +193,31 @@ def rcp_strand_of_list_error():
     raise RStop("unable to find an inherited method for function 'strand' for signature '\"list\"'")
 
 
+def _rows_identical(a, b):
+    """identical() of two .rcpRows lists."""
+    return a.keys() == b.keys() and all(np.array_equal(np.asarray(a[k]), np.asarray(b[k])) for k in a)
+
+
 def calc_coverage(sh, inp, mask, strand=None, ignore_strand=True):
-    """calcCoverage(input, mask, strand, ignore.strand) for a GRanges or a split list."""
-    if strand is not None and not isinstance(inp, GRanges):
-        rcp_strand_of_list_error()
-    rs = rcp_read_set(sh, inp, strand, rows_of=lambda lv: rcp_rows(mask, lv, ignore_strand))
+    """calcCoverage(input, mask, strand, ignore.strand) for a GRanges, a split list or a readset
+    the caller prepared (.rcpReadSet)."""
+    own = not isinstance(inp, ReadSet)
+    if not own:
+        if strand != inp.strand:
+            raise RStop("the readset was prepared with another strand filter")
+        if inp.rows is not None and not _rows_identical(inp.rows, rcp_rows(mask, inp.levels, ignore_strand)):
+            raise RStop("the readset was split over the devices for another mask")
+        rs = inp
+    else:
+        if strand is not None and not isinstance(inp, GRanges):
+            rcp_strand_of_list_error()
+        rs = rcp_read_set(sh, inp, strand, rows_of=lambda lv: rcp_rows(mask, lv, ignore_strand))
     try:
         return rcp_coverage(sh, rs, rs.rows if rs.rows is not None else rcp_rows(mask, rs.levels, ignore_strand),
                             mask.names)
     finally:
-        rcp_free(sh, rs)
+        if own:
+            rcp_free(sh, rs)
 
 
 def coverage_ref(sh, input, genomeRanges, region, flank, strandedParams, split=False):

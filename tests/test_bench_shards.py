@@ -77,3 +77,40 @@ def test_shards_balance_by_overlaps():
             lo, hi, _ = bench.shard_of(rows, ovl, world, rank)
             loads.append(w[lo:hi].sum())
         assert max(loads) <= w.sum() / world + w.max() + 1e-9
+
+
+class _Args:
+    def __init__(self, gpus):
+        self.gpus = gpus
+
+
+def test_gpus_flag_reaches_the_world_size():
+    """`bench.py --gpus N` without a launcher starts N ranks as a child torch.distributed.run
+    (the driver may run it either way); under a launcher --gpus must match WORLD_SIZE."""
+    argv = ["--gpus", "8", "--steps", "5"]
+    world, cmd = bench.launch_plan(_Args(8), {}, 8, argv, port=29555)
+    assert world == 8 and cmd is not None
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=8" in cmd and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-len(argv):] == argv and cmd[-len(argv) - 1].endswith("bench.py")
+    # one GPU: run here; no flag under a launcher: the launcher's world
+    assert bench.launch_plan(_Args(None), {}, 1, []) == (1, None)
+    assert bench.launch_plan(_Args(None), {"WORLD_SIZE": "4"}, 8, []) == (4, None)
+    assert bench.launch_plan(_Args(4), {"WORLD_SIZE": "4"}, 8, []) == (4, None)
+    # a rehearsal: two ranks sharing one GPU
+    world, cmd = bench.launch_plan(_Args(2), {"RCP_SHARE_GPU": "1"}, 1, ["--gpus", "2"])
+    assert world == 2 and "--nproc-per-node=2" in cmd
+    assert bench.devices_used(2, 1, True) == 1 and bench.devices_used(8, 8, False) == 8
+
+
+@pytest.mark.parametrize("args,env,visible", [
+    (8, {}, 1),                      # fewer GPUs than asked for
+    (2, {}, 0),
+    (1, {}, 0),                      # no GPU at all
+    (4, {"WORLD_SIZE": "2"}, 8),     # --gpus disagrees with the launcher
+    (None, {"WORLD_SIZE": "8"}, 2),  # the launcher started more ranks than GPUs
+])
+def test_gpus_flag_refuses_what_cannot_run(args, env, visible):
+    with pytest.raises(SystemExit) as e:
+        bench.launch_plan(_Args(args), env, visible, [])
+    assert e.value.code == 2

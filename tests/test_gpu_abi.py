@@ -445,6 +445,44 @@ def test_matrix_download_as_numerators(gpu, capfd, n_bins, scale, expand):
     np.testing.assert_array_equal(valid.astype(bool), rv)
 
 
+@pytest.mark.parametrize("hot_rows", [2, 400], ids=["few_raw_blocks", "many_raw_blocks"])
+def test_matrix_download_deep_numerators(gpu, capfd, hot_rows):
+    """Bin numerators of 2^16 and more (a deep pile under 40-bp bins) do not fit a block's 16-bit
+    offsets: those blocks come down as they are -- block by block when few, the whole chunk when
+    many -- fetched by the calling thread on its stream, expanded by the copy threads.  Bit-equal
+    to the device matrix either way."""
+    from recoup_amd.engine import ReadSet
+    from tests.test_gpu_random import CHROM_LEN, make_reads, single_rows
+    rng = np.random.default_rng(90 + hot_rows)
+    base = make_reads(rng, 300_000)
+    k = 9000  # ~3600 deep around chr0:200000 -> bin sums ~1.4e5
+    hs = (200_000 + rng.integers(-200, 200, k)).astype(np.int32)
+    reads = (np.r_[base[0], np.zeros(k, np.int32)], np.r_[base[1], hs], np.r_[base[2], hs + 179],
+             np.r_[base[3], rng.integers(0, 2, k).astype(np.int8)])
+    rows = single_rows(rng, 12_000, 4000)
+    chrom, start, end, strand = rows.chrom.copy(), rows.start.copy(), rows.end.copy(), rows.strand.copy()
+    at = np.arange(100, 100 + hot_rows) if hot_rows < 10 else np.arange(0, 12_000, 12_000 // hot_rows)[:hot_rows]
+    chrom[at] = 0
+    start[at] = 200_000 - 2000 + rng.integers(-300, 300, len(at))
+    end[at] = start[at] + 3999
+    rows = RowTable.from_ranges(chrom, start, end, strand)
+    bins = Bins([("whole", 100)])
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    ref, rv = Plan(rs, rows, bins).run()
+    assert ref.max() * 40 >= 2 ** 16
+    os.environ["RCP_TRACE"] = "1"
+    try:
+        rc, out, valid = _profile(rs, rows, bins)
+    finally:
+        del os.environ["RCP_TRACE"]
+    lines = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[stage] d2h-expand")]
+    assert rc == 0 and len(lines) == 1, lines
+    n_raw = int(lines[0].split(" raw blocks")[0].rsplit(" ", 1)[1])
+    assert n_raw > 0, lines
+    assert np.array_equal(out.view(np.uint64), np.asfortranarray(ref).view(np.uint64))
+    np.testing.assert_array_equal(valid.astype(bool), rv)
+
+
 @pytest.mark.parametrize("n_bins,scale,expand", [(1000, 1.0, True), (800, 0.61, True), (300, 1.0, False)])
 def test_rle_matrix_download_as_numerators(gpu, capfd, n_bins, scale, expand):
     """recoup()'s Rle path (calcCoverage's list -> rcp_profile_rle): an integer Rle list's profile

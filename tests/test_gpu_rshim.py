@@ -270,6 +270,17 @@ def test_recoup_path_on_several_devices(sh, c1, devs):
         one = rm.calc_coverage(sh, inp, mask)
         with _devices(devs):
             _same_coverage(rm.calc_coverage(sh, inp, mask), one)
+    # a readset the caller prepared for this mask serves it; for another mask calcCoverage stops
+    # instead of returning the prepared mask's coverage under the other mask's names
+    with _devices(devs):
+        rs = rm.rcp_read_set(sh, c1["reads"][0], rows_of=lambda lv: rm.rcp_rows(mask, lv))
+        try:
+            _same_coverage(rm.calc_coverage(sh, rs, mask), rm.calc_coverage(sh, c1["reads"][0], mask))
+            other = getRegionalRanges(genes, "tss", (1000, 1000))
+            with pytest.raises(rm.RStop, match="another mask"):
+                rm.calc_coverage(sh, rs, other)
+        finally:
+            rm.rcp_free(sh, rs)
     assert sh.live_handles() == 0
 
 

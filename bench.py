@@ -287,8 +287,16 @@ def main():
         torch.cuda.set_device(local)
         if backend == "nccl":
             tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        else:
-            tdist.init_process_group(backend)
+        else:  # (gloo prints its connection lines on stdout: sent to stderr, the JSON line stays alone)
+            sys.stdout.flush()
+            fd = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                tdist.init_process_group(backend)
+                tdist.barrier()
+            finally:
+                os.dup2(fd, 1)
+                os.close(fd)
     dev = f"cuda:{local}"
     torch.cuda.set_device(local)
 

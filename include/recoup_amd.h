@@ -284,7 +284,8 @@ RCP_API int rcp_profile_multi(rcp_readset* const* readsets, int32_t n_devices, c
 
 /* One sample's reads split over several GPUs for ONE row table (what cmclapply over the regions
  * of calcCoverage, R/coverage.R:147-154, and over the rows of binCoverageMatrix, R/profile.R:198-199,
- * parallelise).  The rows are cut into n_devices contiguous blocks (the caller's order) of
+ * parallelise).  The rows, taken in (chromosome, start) order whatever the caller's order (rows on
+ * an absent chromosome last), are cut into n_devices contiguous blocks of that order of
  * near-equal weight -- each row's candidate reads, counted on the GPUs, plus its length / 8 -- and
  * device i keeps ONLY the reads block i's rows can overlap:
  *   the reads are uploaded in n_devices slices, one per GPU (all PCIe links at once; device input:
@@ -299,10 +300,14 @@ typedef struct rcp_shards rcp_shards;
 typedef struct rcp_cov rcp_cov;  /* (calcCoverage results: see rcp_coverage_rle) */
 RCP_API int rcp_shards_create(const rcp_reads_desc* reads, const rcp_rows_desc* rows, const int32_t* device_ids,
                               int32_t n_devices, rcp_shards** out);
-/* n_rows, n_devices; row_split [n_devices + 1]: the row blocks; n_reads [n_devices]: the reads each
- * device holds (any may be NULL) */
+/* n_rows, n_devices; row_split [n_devices + 1]: the row blocks, as positions of the order
+ * rcp_shards_rows gives; n_reads [n_devices]: the reads each device holds (any may be NULL) */
 RCP_API int rcp_shards_info(const rcp_shards* sh, int32_t* n_rows, int32_t* n_devices, int32_t* row_split,
                             int64_t* n_reads);
+/* order [n_rows]: the caller's row at each position of the blocks' (chromosome, start) order --
+ * block b holds rows order[row_split[b]] .. order[row_split[b + 1] - 1].  Results (profiles,
+ * coverage lists) are always in the caller's row order. */
+RCP_API int rcp_shards_rows(const rcp_shards* sh, int32_t* order);
 /* profileMatrix of the row table (as rcp_profile: out = host R column-major n_rows x n_cols,
  * row_valid may be NULL): one plan per device, each writing its rows of the caller's matrix */
 RCP_API int rcp_shards_profile(rcp_shards* sh, const rcp_bins_desc* bins, double* out, uint8_t* row_valid);

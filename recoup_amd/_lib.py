@@ -107,6 +107,7 @@ SIGNATURES = [
     ("rcp_shards_create", ctypes.c_int, [ctypes.POINTER(ReadsDesc), ctypes.POINTER(RowsDesc), _i32p, ctypes.c_int32,
                                          ctypes.POINTER(_vp)]),
     ("rcp_shards_info", ctypes.c_int, [_vp, _i32p, _i32p, _i32p, _i64p]),
+    ("rcp_shards_rows", ctypes.c_int, [_vp, _i32p]),
     ("rcp_shards_profile", ctypes.c_int, [_vp, ctypes.POINTER(BinsDesc), _dp, _u8p]),
     ("rcp_shards_coverage", ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     ("rcp_shards_destroy", ctypes.c_int, [_vp]),

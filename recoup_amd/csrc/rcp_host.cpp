@@ -2189,7 +2189,16 @@ namespace rcpi {
 // -- DMA in, pinned read, destination write -- which is what bounds a streamed call.)
 int download_packed(const double* d_out, size_t ld, size_t R, size_t C, double scale, double* host, size_t host_ld,
                     int device, hipStream_t s,
-                    const std::function<hipError_t(uint32_t* q, uint32_t* div, uint32_t* bad_row)>& pack) {
+                    const std::function<hipError_t(uint32_t* q, uint32_t* div, uint32_t* bad_row)>& pack,
+                    const std::vector<RowRun>* runs) {
+    const std::vector<RowRun> all{RowRun{0, 0, R}};
+    if (!runs) runs = &all;
+    // the doubles of every run, straight into their host rows
+    auto doubles = [&]() -> int {
+        for (const RowRun& u : *runs)
+            HIP_TRY(rcp::stage_d2h_2d(host + u.dst, 8 * host_ld, d_out + u.src, 8 * ld, 8 * u.len, C, device, s));
+        return (int)RCP_OK;
+    };
     PoolBuf q(s), aux(s);
     HIP_TRY(q.alloc(4 * ld * C));
     HIP_TRY(aux.alloc(8 * R));
@@ -2206,14 +2215,19 @@ int download_packed(const double* d_out, size_t ld, size_t R, size_t C, double s
     // many rows the numerators cannot carry (interpolated genes, R-RNG layouts): all doubles
     if (bad.size() > R / 8) {
         if (rcp::trace_on()) fprintf(stderr, "[pack] doubles: %zu of %zu rows not numerators\n", bad.size(), R);
-        HIP_TRY(rcp::stage_d2h_2d(host, 8 * host_ld, d_out, 8 * ld, 8 * R, C, device, s));
-        return RCP_OK;
+        return doubles();
     }
-    bool no_buffers = false;
-    HIP_TRY(rcp::stage_d2h_expand(host, host_ld, q.as<uint32_t>(), ld, R, C, h.data(), scale, device, s, &no_buffers));
-    if (no_buffers) {  // no pinned buffers for this device: the doubles, as a direct copy
-        HIP_TRY(rcp::stage_d2h_2d(host, 8 * host_ld, d_out, 8 * ld, 8 * R, C, device, s));
-        return RCP_OK;
+    std::vector<size_t> dst_of;  // host row of each device row (the marked rows' doubles below)
+    if (runs != &all && !bad.empty()) {
+        dst_of.assign(R, 0);
+        for (const RowRun& u : *runs)
+            for (size_t i = 0; i < u.len; ++i) dst_of[u.src + i] = u.dst + i;
+    }
+    for (const RowRun& u : *runs) {
+        bool no_buffers = false;
+        HIP_TRY(rcp::stage_d2h_expand(host + u.dst, host_ld, q.as<uint32_t>() + u.src, ld, u.len, C, h.data() + u.src,
+                                      scale, device, s, &no_buffers));
+        if (no_buffers) return doubles();  // no pinned buffers for this device: the doubles, as a direct copy
     }
     if (!bad.empty()) {  // those rows' doubles, gathered on the device, over the expanded cells
         const size_t nb = bad.size();
@@ -2227,7 +2241,8 @@ int download_packed(const double* d_out, size_t ld, size_t R, size_t C, double s
         HIP_TRY(hipMemcpyAsync(vals.data(), d_vals.p, 8 * nb * C, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         for (size_t c = 0; c < C; ++c)
-            for (size_t i = 0; i < nb; ++i) host[c * host_ld + (size_t)bad[i]] = vals[c * nb + i];
+            for (size_t i = 0; i < nb; ++i)
+                host[c * host_ld + (dst_of.empty() ? (size_t)bad[i] : dst_of[(size_t)bad[i]])] = vals[c * nb + i];
         if (rcp::trace_on()) fprintf(stderr, "[pack] %zu rows as doubles\n", nb);
     }
     return RCP_OK;
@@ -2240,7 +2255,8 @@ int download_packed(const double* d_out, size_t ld, size_t R, size_t C, double s
 // apart as doubles.  Plans of several parts, or many such rows: the doubles.  (C4's 1.6 GB matrix: 0.8 GB down, and
 // 2.4 instead of 3.2 GB of host memory traffic -- DMA in, pinned read, destination write --
 // which is what bounds a streamed call.)
-int download_matrix(rcp_plan* plan, const double* d_out, double* host, size_t host_ld, hipStream_t s) {
+int download_matrix(rcp_plan* plan, const double* d_out, double* host, size_t host_ld, hipStream_t s,
+                    const std::vector<RowRun>* runs) {
     const RcpPlanDev& P = plan->dev;
     const int dev = plan->rs->device;
     const size_t R = (size_t)plan->n_rows, C = (size_t)plan->n_cols, ld = (size_t)plan->out_ld;
@@ -2250,17 +2266,24 @@ int download_matrix(rcp_plan* plan, const double* d_out, double* host, size_t ho
     if (!pack) {
         if (rcp::trace_on() && 8 * R * C >= (size_t(4) << 20))
             fprintf(stderr, "[pack] doubles: plan of %d parts, %d interpolated rows\n", P.n_parts, P.n_interp);
-        HIP_TRY(rcp::stage_d2h_2d(host, 8 * host_ld, d_out, 8 * ld, 8 * R, C, dev, s));
+        if (!runs) {
+            HIP_TRY(rcp::stage_d2h_2d(host, 8 * host_ld, d_out, 8 * ld, 8 * R, C, dev, s));
+        } else {
+            for (const RowRun& u : *runs)
+                HIP_TRY(rcp::stage_d2h_2d(host + u.dst, 8 * host_ld, d_out + u.src, 8 * ld, 8 * u.len, C, dev, s));
+        }
         return RCP_OK;
     }
     return download_packed(d_out, ld, R, C, P.scale, host, host_ld, dev, s,
                            [&](uint32_t* q, uint32_t* div, uint32_t* bad) {
                                return rcp_launch_pack(&P, d_out, q, div, bad, s);
-                           });
+                           },
+                           runs);
 }
 
 int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bins_desc* bins, double* out,
-                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream) {
+                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream,
+                  const int32_t* dst_rows) {
     const bool tr = rcp::trace_on();
     const double t0 = tr ? rcp::trace_ms() : 0.0;
     rcp_plan* plan = nullptr;
@@ -2287,17 +2310,48 @@ int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bin
     e = rcp_plan_status(plan, s);
     if (e) return e;
     const double t2 = tr ? rcp::trace_ms() : 0.0;
-    // this block's rows of every column of the caller's R matrix
-    if (out && plan->n_cols && plan->n_rows) {
-        e = download_matrix(plan, d_out.as<double>(), out + r0, (size_t)n_rows_total, s);
-        if (e) return e;
+    const size_t n = (size_t)plan->n_rows, C = (size_t)plan->n_cols;
+    // the block's rows as runs of consecutive caller rows (one run: rows r0 .. in order)
+    std::vector<RowRun> runs;
+    if (!dst_rows) {
+        runs.push_back(RowRun{0, (size_t)r0, n});
+    } else {
+        for (size_t i = 0; i < n; ++i) {
+            if (!runs.empty() && (size_t)dst_rows[i] == runs.back().dst + runs.back().len) ++runs.back().len;
+            else runs.push_back(RowRun{i, (size_t)dst_rows[i], 1});
+        }
+    }
+    // this block's rows of every column of the caller's R matrix: run by run when the runs are few
+    // and long, else (rows of a table in no particular order) through a host matrix of the block
+    // whose rows the threads scatter
+    const bool scatter = runs.size() > std::max<size_t>(16, n / 256);
+    if (out && C && n) {
+        if (!scatter) {
+            e = download_matrix(plan, d_out.as<double>(), out, (size_t)n_rows_total, s, &runs);
+            if (e) return e;
+        } else {
+            std::vector<double> tmp(n * C);
+            e = download_matrix(plan, d_out.as<double>(), tmp.data(), n, s);
+            if (e) return e;
+            const int nt = (int)std::min<size_t>(8, std::max<size_t>(1, C / 64));
+            std::vector<std::thread> th;
+            for (int t = 0; t < nt; ++t)
+                th.emplace_back([&, t] {
+                    for (size_t c = C * t / nt; c < C * (t + 1) / nt; ++c)
+                        for (const RowRun& u : runs)
+                            std::memcpy(out + c * (size_t)n_rows_total + u.dst, tmp.data() + c * n + u.src, 8 * u.len);
+                });
+            for (auto& x : th) x.join();
+        }
     }
     if (tr)
-        fprintf(stderr, "[block] rows [%d, %d): plan %.2f ms, pass %.2f ms, down %.2f ms\n", r0, r0 + plan->n_rows,
-                t1 - t0, t2 - t1, rcp::trace_ms() - t2);
-    if (row_valid && plan->n_rows) {
-        HIP_TRY(hipMemcpyAsync(row_valid + r0, d_valid.p, plan->n_rows, hipMemcpyDeviceToHost, s));
+        fprintf(stderr, "[block] rows [%d, %d) in %zu runs: plan %.2f ms, pass %.2f ms, down %.2f ms\n", r0,
+                r0 + plan->n_rows, runs.size(), t1 - t0, t2 - t1, rcp::trace_ms() - t2);
+    if (row_valid && n) {
+        std::vector<uint8_t> v(n);
+        HIP_TRY(hipMemcpyAsync(v.data(), d_valid.p, n, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        for (const RowRun& u : runs) std::memcpy(row_valid + u.dst, v.data() + u.src, u.len);
     }
     return RCP_OK;
 }

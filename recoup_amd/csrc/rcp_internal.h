@@ -218,21 +218,30 @@ int run_per_device(int n, F fn) {
     return RCP_OK;
 }
 
+// Device rows [src, src + len) of a matrix go to host rows [dst, dst + len)
+struct RowRun {
+    size_t src, dst, len;
+};
 // A plan's matrix on the device (column stride plan->out_ld) into a host column-major double
-// matrix of column stride host_ld, as bin numerators when the plan allows (rcp_host.cpp)
-int download_matrix(rcp_plan* plan, const double* d_out, double* host, size_t host_ld, hipStream_t s);
+// matrix of column stride host_ld, as bin numerators when the plan allows (rcp_host.cpp); runs
+// (NULL: row i to host row i) place the device rows
+int download_matrix(rcp_plan* plan, const double* d_out, double* host, size_t host_ld, hipStream_t s,
+                    const std::vector<RowRun>* runs = nullptr);
 // the numerator download of an R x C column-major device matrix d_out (stride ld): pack(q, div,
 // bad_row) fills the numerators, per-row widths and per-row failure marks (zeroed first); rows
 // marked come down as doubles apart, or everything does when they are many
 int download_packed(const double* d_out, size_t ld, size_t R, size_t C, double scale, double* host, size_t host_ld,
                     int device, hipStream_t s,
-                    const std::function<hipError_t(uint32_t* q, uint32_t* div, uint32_t* bad_row)>& pack);
+                    const std::function<hipError_t(uint32_t* q, uint32_t* div, uint32_t* bad_row)>& pack,
+                    const std::vector<RowRun>* runs = nullptr);
 // Block [r0, r0 + sub->n_rows) of an n_rows_total-row profile on readset rs: plan, execute, and
 // copy its rows of every column into the caller's R column-major matrix `out` (may be NULL) and
-// row_valid + r0 (may be NULL); *n_cols receives the plan's column count.  On `stream` (NULL: a
-// stream of its own); returns with the copies done (rcp_host.cpp)
+// row_valid + r0 (may be NULL); *n_cols receives the plan's column count.  dst_rows (may be NULL):
+// the caller's row of each block row instead of r0 + i.  On `stream` (NULL: a stream of its own);
+// returns with the copies done (rcp_host.cpp)
 int profile_block(const rcp_readset* rs, const rcp_rows_desc* sub, const rcp_bins_desc* bins, double* out,
-                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream = nullptr);
+                  int64_t n_rows_total, int32_t r0, uint8_t* row_valid, int64_t* n_cols, hipStream_t stream = nullptr,
+                  const int32_t* dst_rows = nullptr);
 
 // rcp_profile_rle into rows [0, n_rows) of a matrix with column stride out_ld, on stream s
 // (rcp_host.cpp)
@@ -412,6 +421,7 @@ struct rcp_cov {
     rcpi::PoolBuf run_off{nullptr}, values{nullptr}, lengths{nullptr}, valid{nullptr};
     std::vector<std::unique_ptr<rcp_cov>> parts;
     std::vector<int32_t> split;
+    std::vector<int32_t> order;  // the parts' rows in the caller's numbering (empty: in order)
     ~rcp_cov() {
         // the buffers go back to the pool after everything queued on the null stream
         run_off.reset();

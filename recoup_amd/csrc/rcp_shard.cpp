@@ -41,7 +41,9 @@ using namespace rcpi;
 struct rcp_shards {
     std::vector<int32_t> devices;
     std::vector<rcp_readset*> rs;  // one per device (the block's reads)
-    std::vector<int32_t> split;    // row blocks [split[b], split[b + 1])
+    std::vector<int32_t> split;    // row blocks [split[b], split[b + 1]) of the table in (chrom, start) order
+    std::vector<int32_t> order;    // the caller's row at each position of that order (empty: the caller's
+                                   // table is in that order already)
     // the row table (a copy: the caller's arrays may go away)
     int32_t n_rows = 0;
     std::vector<int64_t> seg_off;
@@ -108,10 +110,46 @@ int seg_bounds(const rcp_readset* rs, const rcp_rows_desc* rows, std::vector<uin
 }
 
 int cov_copy_parts(const rcp_cov* c, int64_t* run_off, int32_t* values, int32_t* lengths, uint8_t* valid) {
+    const int np = (int)c->parts.size();
+    if (!c->order.empty()) {
+        // the parts hold rows in (chrom, start) order: each part's runs come into host arrays of its
+        // own, then every row's runs go to the caller's row (offsets from the caller-order counts)
+        std::vector<std::vector<int64_t>> off(np);
+        std::vector<std::vector<uint8_t>> val(np);
+        int rc = run_per_device(np, [&](int b) {
+            const rcp_cov* p = c->parts[b].get();
+            off[b].assign((size_t)p->n_rows + 1, 0);
+            val[b].assign((size_t)std::max(p->n_rows, 1), 0);
+            return rcp_cov_copy(p, off[b].data(), nullptr, nullptr, val[b].data());
+        });
+        if (rc) return rc;
+        std::vector<int64_t> at((size_t)c->n_rows + 1, 0);  // caller-order run offsets
+        for (int b = 0; b < np; ++b)
+            for (int32_t i = 0; i < c->parts[b]->n_rows; ++i) {
+                const int32_t r = c->order[(size_t)c->split[b] + i];
+                at[(size_t)r + 1] = off[b][i + 1] - off[b][i];
+                if (valid) valid[r] = val[b][i];
+            }
+        for (int32_t r = 0; r < c->n_rows; ++r) at[(size_t)r + 1] += at[r];
+        if (run_off) std::copy(at.begin(), at.end(), run_off);
+        if (!values && !lengths) return RCP_OK;
+        return run_per_device(np, [&](int b) {
+            const rcp_cov* p = c->parts[b].get();
+            std::vector<int32_t> v((size_t)std::max<int64_t>(p->n_runs, 1)), l(v.size());
+            int e = rcp_cov_copy(p, nullptr, values ? v.data() : nullptr, lengths ? l.data() : nullptr, nullptr);
+            if (e) return e;
+            for (int32_t i = 0; i < p->n_rows; ++i) {
+                const int64_t a = off[b][i], k = off[b][i + 1] - a;
+                const size_t to = (size_t)at[c->order[(size_t)c->split[b] + i]];
+                if (values) std::memcpy(values + to, v.data() + a, 4 * (size_t)k);
+                if (lengths) std::memcpy(lengths + to, l.data() + a, 4 * (size_t)k);
+            }
+            return (int)RCP_OK;
+        });
+    }
     // each part's runs land at its place in the caller's arrays (the parts' rows and runs are
     // consecutive blocks of the whole list), one host thread per part; its run offsets are
     // shifted by the runs of the parts before it
-    const int np = (int)c->parts.size();
     std::vector<int64_t> base(np + 1, 0);
     for (int b = 0; b < np; ++b) base[b + 1] = base[b] + c->parts[b]->n_runs;
     const int rc = run_per_device(np, [&](int b) {
@@ -225,19 +263,44 @@ extern "C" int rcp_shards_create(const rcp_reads_desc* reads, const rcp_rows_des
         return fail(RCP_EUNSUPPORTED, "read count %lld outside [0, 2^31)", (long long)reads->n);
     auto sh = std::make_unique<rcp_shards>();
     sh->devices.assign(device_ids, device_ids + n_devices);
-    // ---- the row table, copied
+    // ---- the row table, copied in (chromosome, start) order: the blocks are contiguous in that
+    // order, so a block's regions are neighbours on the genome and its reads few, whatever order
+    // the caller's table is in (an annotation need not be position-sorted)
     const int64_t n_seg = R > 0 ? rows->seg_off[R] : 0;
     sh->n_rows = R;
-    sh->seg_off.assign(rows->seg_off, rows->seg_off + R + 1);
-    if (R == 0) sh->seg_off.assign(1, 0);
-    sh->chrom.assign(rows->seg_chrom, rows->seg_chrom + n_seg);
-    sh->start.assign(rows->seg_start, rows->seg_start + n_seg);
-    sh->end.assign(rows->seg_end, rows->seg_end + n_seg);
-    sh->strand.assign(rows->seg_strand, rows->seg_strand + n_seg);
-    if (rows->seg_group) {
-        sh->group.assign(rows->seg_group, rows->seg_group + n_seg);
-        sh->has_group = true;
+    std::vector<int32_t> ord((size_t)R);
+    for (int32_t r = 0; r < R; ++r) ord[r] = r;
+    if (n_devices > 1) {  // (one device: one block, the caller's order)
+        // key: the row's first segment's chromosome (an absent one -- NA, outside the readset's
+        // codes -- last) and its segments' lowest start
+        std::vector<std::pair<int64_t, int64_t>> key((size_t)R);
+        for (int32_t r = 0; r < R; ++r) {
+            int64_t c = INT64_MAX, lo = INT64_MAX;
+            if (rows->seg_off[r + 1] > rows->seg_off[r]) {
+                const int32_t c0 = rows->seg_chrom[rows->seg_off[r]];
+                c = (c0 >= 0 && c0 < reads->n_chrom) ? c0 : INT64_MAX;
+                for (int64_t j = rows->seg_off[r]; j < rows->seg_off[r + 1]; ++j) lo = std::min<int64_t>(lo, rows->seg_start[j]);
+            }
+            key[r] = {c, lo};
+        }
+        std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
     }
+    bool identity = true;
+    for (int32_t r = 0; r < R && identity; ++r) identity = ord[r] == r;
+    if (!identity) sh->order = ord;
+    sh->seg_off.assign(1, 0);
+    sh->chrom.reserve(n_seg);
+    for (int32_t i = 0; i < R; ++i) {
+        const int32_t r = ord[i];
+        const int64_t a = rows->seg_off[r], z = rows->seg_off[r + 1];
+        sh->chrom.insert(sh->chrom.end(), rows->seg_chrom + a, rows->seg_chrom + z);
+        sh->start.insert(sh->start.end(), rows->seg_start + a, rows->seg_start + z);
+        sh->end.insert(sh->end.end(), rows->seg_end + a, rows->seg_end + z);
+        sh->strand.insert(sh->strand.end(), rows->seg_strand + a, rows->seg_strand + z);
+        if (rows->seg_group) sh->group.insert(sh->group.end(), rows->seg_group + a, rows->seg_group + z);
+        sh->seg_off.push_back(sh->seg_off.back() + (z - a));
+    }
+    if (rows->seg_group) sh->has_group = true;
     if (rows->group_is_list) {
         std::memcpy(sh->is_list, rows->group_is_list, 4);
         sh->has_list = true;
@@ -451,6 +514,14 @@ extern "C" int rcp_shards_info(const rcp_shards* sh, int32_t* n_rows, int32_t* n
     RCP_CATCH
 }
 
+extern "C" int rcp_shards_rows(const rcp_shards* sh, int32_t* order) {
+    RCP_TRY
+    if (!sh || !order) return fail(RCP_EINVAL, "NULL argument");
+    for (int32_t i = 0; i < sh->n_rows; ++i) order[i] = sh->order.empty() ? i : sh->order[i];
+    return RCP_OK;
+    RCP_CATCH
+}
+
 extern "C" int rcp_shards_profile(rcp_shards* sh, const rcp_bins_desc* bins, double* out, uint8_t* row_valid) {
     RCP_TRY
     if (!sh || !bins) return fail(RCP_EINVAL, "NULL argument");
@@ -459,7 +530,8 @@ extern "C" int rcp_shards_profile(rcp_shards* sh, const rcp_bins_desc* bins, dou
     const int rc = run_per_device(N, [&](int b) {
         const rcp_rows_desc sub = sh->block(b);
         if (sub.n_rows == 0) return (int)RCP_OK;
-        return profile_block(sh->rs[b], &sub, bins, out, sh->n_rows, sh->split[b], row_valid, &n_cols[b]);
+        return profile_block(sh->rs[b], &sub, bins, out, sh->n_rows, sh->split[b], row_valid, &n_cols[b], nullptr,
+                             sh->order.empty() ? nullptr : sh->order.data() + sh->split[b]);
     });
     if (rc) return rc;
     int64_t nc = -1;
@@ -481,6 +553,7 @@ extern "C" int rcp_shards_coverage(rcp_shards* sh, rcp_cov** out) {
     res->n_rows = sh->n_rows;
     res->device = sh->devices[0];
     res->split = sh->split;
+    res->order = sh->order;
     std::vector<rcp_cov*> parts(N, nullptr);
     const int rc = run_per_device(N, [&](int b) {
         const rcp_rows_desc sub = sh->block(b);

@@ -419,12 +419,20 @@ class Shards:
         self.h = h
 
     def info(self):
-        """(row block boundaries [n_devices + 1], reads held per device [n_devices])."""
+        """(row block boundaries [n_devices + 1] as positions of order(), reads held per device
+        [n_devices])."""
         n = len(self.devices)
         split = np.zeros(n + 1, np.int32)
         reads = np.zeros(n, np.int64)
         check(_lib.lib().rcp_shards_info(self.h, None, None, cptr(split, _lib._i32p), cptr(reads, _lib._i64p)))
         return split, reads
+
+    def order(self):
+        """rcp_shards_rows: the table's row at each position of the blocks' (chromosome, start)
+        order."""
+        out = np.zeros(self.rows.n_rows, np.int32)
+        check(_lib.lib().rcp_shards_rows(self.h, cptr(out, _lib._i32p)))
+        return out
 
     def profile(self, bins):
         """rcp_shards_profile -> (matrix (n_rows, n_cols) float64 view of R's column-major

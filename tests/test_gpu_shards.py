@@ -34,6 +34,31 @@ def overlapping(reads, rows, r0, r1, strand_filter=None):
     return np.flatnonzero(hit)
 
 
+def block_order(rows, order):
+    """The table with its rows in the shards' order (rcp_shards_rows): block b is rows
+    split[b] .. split[b + 1] - 1 of it."""
+    from recoup_amd.engine import RowTable
+    order = np.asarray(order)
+    idx = np.concatenate([np.arange(rows.seg_off[r], rows.seg_off[r + 1]) for r in order]) if len(order) else \
+        np.zeros(0, np.int64)
+    seg_off = np.concatenate([[0], np.cumsum(np.diff(rows.seg_off)[order])]).astype(np.int64)
+    return RowTable(seg_off, rows.chrom[idx], rows.start[idx], rows.end[idx], rows.strand[idx],
+                    seg_group=None if rows.seg_group is None else rows.seg_group[idx],
+                    group_is_list=rows.group_is_list, ignore_strand=rows.ignore_strand)
+
+
+def check_order(sh, rows):
+    """The shards' row order is a permutation of the table in (chromosome, start) order (the
+    chromosome of a row's first range, its lowest start)."""
+    order = sh.order()
+    assert np.array_equal(np.sort(order), np.arange(rows.n_rows))
+    first = rows.seg_off[:-1]
+    lo = np.minimum.reduceat(rows.start, first) if len(rows.start) else np.zeros(0)
+    key = np.stack([rows.chrom[first][order], lo[order]], 1)
+    assert all(tuple(key[i]) <= tuple(key[i + 1]) for i in range(len(key) - 1))
+    return block_order(rows, order)
+
+
 def same_bits(a, b):
     assert a.shape == b.shape
     assert np.array_equal(np.ascontiguousarray(a).view(np.uint64), np.ascontiguousarray(b).view(np.uint64))
@@ -49,25 +74,33 @@ def one_device(reads, rows, bins, strand_filter=None, seqlen=CHROM_LEN):
 
 
 @pytest.mark.parametrize("n_dev", [2, 3])
-@pytest.mark.parametrize("shuffle", [False, True])
-def test_shards_single_range_rows(gpu, n_dev, shuffle):
+@pytest.mark.parametrize("table", ["sorted", "chrom_blocks", "shuffled"])
+def test_shards_single_range_rows(gpu, n_dev, table):
     """TSS-like windows (binned and per-base profiles, coverage Rle lists): bit-equal to one
-    device; each device holds exactly the reads its block's windows overlap, sorted or shuffled
-    row order alike."""
+    device; each device holds exactly the reads its block's windows overlap.  The blocks are cut
+    in (chromosome, start) order whatever the table's order -- position-sorted, chromosomes in
+    another order (a few runs of rows per block: copied run by run), shuffled (rows scattered on
+    the host) -- so the devices hold the same reads as for the sorted table."""
     from recoup_amd.engine import Bins, RowTable, Shards
-    rng = np.random.default_rng(50 + n_dev + 10 * shuffle)
+    rng = np.random.default_rng(50 + n_dev)
     reads = make_reads(rng, 120_000, widths=(150, 150))
     r0 = single_rows(rng, 500, 2000, edge=True)
     r0.start[1], r0.end[1] = 1, 2000  # (a start at 0 shortens its row: not a per-base row of 2000)
-    order = rng.permutation(500) if shuffle else np.lexsort((r0.start, r0.chrom))
+    by_pos = np.lexsort((r0.start, r0.chrom))
+    order = {"sorted": by_pos, "chrom_blocks": np.lexsort((r0.start, -r0.chrom)),
+             "shuffled": rng.permutation(500)}[table]
     rows = RowTable.from_ranges(r0.chrom[order], r0.start[order], r0.end[order], r0.strand[order])
     sh = Shards(*reads, CHROM_LEN, rows, [0] * n_dev)
     split, held = sh.info()
     assert split[0] == 0 and split[-1] == rows.n_rows and np.all(np.diff(split) > 0)
+    brows = check_order(sh, rows)
     for b in range(n_dev):
-        assert held[b] == len(overlapping(reads, rows, split[b], split[b + 1]))
-    if not shuffle:  # (500 windows of 2 kb cover most of this 740-kb genome: shuffled blocks each see most reads)
-        assert held.sum() < 0.8 * n_dev * len(reads[1])  # not replicas
+        assert held[b] == len(overlapping(reads, brows, split[b], split[b + 1]))
+    assert held.sum() < 0.8 * n_dev * len(reads[1])  # not replicas
+    if table != "sorted":
+        s_rows = RowTable.from_ranges(r0.chrom[by_pos], r0.start[by_pos], r0.end[by_pos], r0.strand[by_pos])
+        _, held_sorted = Shards(*reads, CHROM_LEN, s_rows, [0] * n_dev).info()
+        assert held.sum() <= 1.1 * held_sorted.sum()
     for bins in (Bins([("whole", 1000)]), Bins([("whole", 0, 2000)]), Bins([("whole", 150)])):
         (m1, v1), _ = one_device(reads, rows, bins)
         m, v = sh.profile(bins)
@@ -89,8 +122,9 @@ def test_shards_rna_rows(gpu, stranded, strand_filter):
     rows = rna_rows(rng, 240, ignore_strand=not stranded)
     sh = Shards(*reads, CHROM_LEN, rows, [0, 0, 0], strand_filter=strand_filter)
     split, held = sh.info()
+    brows = check_order(sh, rows)
     for b in range(3):
-        assert held[b] == len(overlapping(reads, rows, split[b], split[b + 1], strand_filter))
+        assert held[b] == len(overlapping(reads, brows, split[b], split[b + 1], strand_filter))
     bins = Bins([("upstream", 50), ("center", 500), ("downstream", 50)], flank=(2000, 2000), scale=0.73)
     (m1, v1), cov1 = one_device(reads, rows, bins, strand_filter)
     m, v = sh.profile(bins)
@@ -119,8 +153,9 @@ def test_shards_general_widths_heavy_rows_and_na_seqlengths(gpu):
     na = np.array([-1, -1, -1], np.int64)
     sh = Shards(*reads, na, rows, [0, 0])
     split, held = sh.info()
+    brows = check_order(sh, rows)
     for b in range(2):
-        assert held[b] >= len(overlapping(reads, rows, split[b], split[b + 1]))
+        assert held[b] >= len(overlapping(reads, brows, split[b], split[b + 1]))
     for bins in (Bins([("whole", 1000)]), Bins([("whole", 200)], stat="median")):
         (m1, v1), cov1 = one_device(reads, rows, bins, seqlen=na)
         m, v = sh.profile(bins)
@@ -203,3 +238,29 @@ def test_profile_multi_replicas_balanced_by_counts(gpu):
     profile_host(ReadSet(*reads, CHROM_LEN, device=0), rows, bins, out, v1)
     same_bits(mat, out.T)
     np.testing.assert_array_equal(valid, v1.astype(bool))
+
+
+def test_shards_on_distinct_devices(gpu):
+    """Two DIFFERENT GPUs (peer access enabled between them, the reads redistributed by
+    hipMemcpyPeerAsync over xGMI, each block's readset and plan on its own device): bit-equal to
+    one device.  A one-GPU box cannot run it: skipped by hardware, not passed."""
+    from recoup_amd import _lib
+    from recoup_amd.engine import Bins, Shards
+    if _lib.device_count() < 2:
+        pytest.skip("skipped by hardware: one GPU visible (needs 2 for device-to-device copies)")
+    rng = np.random.default_rng(202)
+    reads = make_reads(rng, 150_000, widths=(150, 150))
+    rows = single_rows(rng, 600, 2000)
+    for devs in ([0, 1], [1, 0]):
+        sh = Shards(*reads, CHROM_LEN, rows, devs)
+        split, held = sh.info()
+        brows = check_order(sh, rows)
+        for b in range(2):
+            assert held[b] == len(overlapping(reads, brows, split[b], split[b + 1]))
+        for bins in (Bins([("whole", 1000)]), Bins([("whole", 0, 2000)])):
+            (m1, v1), cov1 = one_device(reads, rows, bins)
+            m, v = sh.profile(bins)
+            np.testing.assert_array_equal(v, v1)
+            same_bits(m, m1)
+        for a, b in zip(sh.coverage_rle(), cov1):
+            np.testing.assert_array_equal(a, b)

@@ -27,7 +27,7 @@ if has write; then
 fi
 if has share2; then
   RCP_SHARE_GPU=1 timeout -k 10 600 python3 bench.py --gpus 2 --verify-gather --no-cpu --no-e2e > "$OUT/share2_c4.json" 2> "$OUT/share2_c4.err" || { tail -30 "$OUT/share2_c4.err"; exit 1; }
-  python3 -c "import json; d=json.load(open('$OUT/share2_c4.json')); print('share2', d['n_gpus'], d['devices_used'], d['value'], d['ms_per_step'], d['config']['shards'], d['gather'])"
+  python3 -c "import json; d=json.loads([l for l in open('$OUT/share2_c4.json') if l.startswith('{')][-1]); print('share2', d['n_gpus'], d['devices_used'], d['value'], d['ms_per_step'], d['config']['shards'], d['gather'])"
 fi
 if has c4; then
   timeout -k 10 600 python3 bench.py > "$OUT/c4_bench.json" 2> "$OUT/c4_bench.err" || { tail -30 "$OUT/c4_bench.err"; exit 1; }

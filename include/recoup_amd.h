@@ -174,6 +174,11 @@ typedef struct {
                               * reads of one width) or 8 ((start, end) pairs) */
     int64_t out_ld;          /* column stride of d_out / d_binsum (rcp_plan_opts.out_ld resolved):
                               * both must hold out_ld * (n_cols - 1) + n_rows elements */
+    int32_t fold;            /* 1: the pileup kernel searches its rows' read ranges itself (no locate or
+                              * heavy-slice launch; skewed rows piled by whole workgroups): bin-difference
+                              * and row-wave plans, and general-kernel plans of <= 65536 single-range rows
+                              * in the merged layout, unless a heavy_threshold > 0 was asked for */
+    int32_t reserved;
 } rcp_plan_info;
 
 /* Host work: orientation of segments, R-RNG bin layouts (set.seed(42); sample(1:n, dif)),

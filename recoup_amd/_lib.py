@@ -65,7 +65,7 @@ class PlanInfo(ctypes.Structure):
     _fields_ = [("n_cols", ctypes.c_int64), ("n_segments", ctypes.c_int64), ("n_interp_rows", ctypes.c_int64),
                 ("lds_bytes", ctypes.c_int64), ("grid", ctypes.c_int64), ("tile_rows", ctypes.c_int32),
                 ("chunk_positions", ctypes.c_int32), ("pileup_kernel", ctypes.c_int32), ("read_bytes", ctypes.c_int32),
-                ("out_ld", ctypes.c_int64)]
+                ("out_ld", ctypes.c_int64), ("fold", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class RleDesc(ctypes.Structure):

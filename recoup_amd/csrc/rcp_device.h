@@ -161,6 +161,8 @@ struct RcpPlanDev {
     int32_t lean_rounds;        // lean kernel: rounds of 16 rows per work item (2; else kRounds)
     int32_t fold;               // 1: the pileup kernel searches its rows' read ranges itself and applies
                                 //    the NULL rules (no locate / heavy launches; bin-difference plans)
+    int32_t coop_min;           // fold plans (general kernel): a fused-bins chunk of a row with more
+                                //    candidate reads than this is piled by the whole workgroup
     // lean kernel, heaviest items first (per-base plans of few work items, e.g. one GPU's shard):
     // locate sums each (32-row tile, column chunk) item's candidate reads, files the item code in
     // item_order under its class floor(log2(reads)) (counts in status[kLptClass + class]), and

@@ -242,6 +242,13 @@ constexpr int kDirReads = 8;  // mean reads per directory bucket (the locate ker
 constexpr int kHeavySlice = 4096;  // candidate reads per heavy work item
 constexpr int kHeavyMaxLen = 16383;    // longer rows never take the heavy path
 constexpr int kHeavyGrid = 4096;
+// general-kernel plans of at most this many rows search their rows' read ranges in the pileup
+// kernel (P.fold): one GPU's share of a region table, where the locate launch and its record round
+// trip are a third of the pass
+constexpr int kFoldMaxRows = 65536;
+// ... and pile a fused-bins chunk of a row with more candidate reads than this with the whole
+// workgroup (8 waves, 16 reads per lane in flight) instead of one wave
+constexpr int kCoopMin = 8192;
 constexpr int kGeneralMaxChunks = 8;  // column chunks a wide binned part is cut into (general kernel)
 
 // A wave's difference array: 64 lanes x per positions (per a power of two >= 4), each lane's
@@ -1205,6 +1212,29 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
             P.fold = opts->heavy_threshold <= 0 ? 1 : 0;
         }
     }
+    // ---- general-kernel plans of small tables of single ranges in the merged layout (one GPU's
+    // shard of a peak table: C4 1/8 spent locate 25 + heavy 8 us ahead of a 93-us pileup): the
+    // pileup kernel searches each row's and chunk's read ranges itself (fold_row) and piles a
+    // skewed row with the whole workgroup instead of heavy slices -- unless the caller asked for
+    // the heavy path.  Every chunk must be one wave pass (no sub-chunks: those read locate's
+    // segment ranges) and no row interpolated (rcp_interp_kernel reads them too)
+    if (P.lean == 0 && !cov_only && rows->ignore_strand && opts->heavy_threshold <= 0 && B.interp_row.empty() &&
+        R > 0 && R <= kFoldMaxRows) {
+        bool f = true;
+        for (int p = 0; f && p < P.n_parts; ++p) {
+            const RcpPart& pt = P.part[p];
+            const int64_t w = pt.per_base ? 1 : part_max_bin[p];
+            if ((int64_t)pt.chunk_bins * w > P.chunk_cap) f = false;
+        }
+        for (int r = 0; f && r < R; ++r) {
+            const int32_t j0 = B.row_seg[r], j1 = B.row_seg[r + 1];
+            if (B.row_static[r] || j1 == j0) continue;  // NULL rows
+            if (j1 - j0 > 1 || B.segs[j0].multi || !B.segs[j0].query_ok) f = false;
+        }
+        P.fold = f ? 1 : 0;
+    }
+    // (RCP_COOP_MIN: diagnostics A/B of the cooperative rows' threshold)
+    P.coop_min = std::getenv("RCP_COOP_MIN") ? std::max(0, std::atoi(std::getenv("RCP_COOP_MIN"))) : kCoopMin;
     // ---- lean plans with few row tiles (one GPU's shard of a region table): the persistent
     // grid (two workgroups per CU) takes (row tile, column chunk) items; with few items per
     // workgroup the last ones leave most workgroups idle, so cut the parts into more column
@@ -1528,6 +1558,8 @@ extern "C" int rcp_plan_info_get(const rcp_plan* plan, rcp_plan_info* info) {
     info->pileup_kernel = plan->dev.lean;
     info->read_bytes = plan->dev.st ? 4 : 8;
     info->out_ld = plan->out_ld;
+    info->fold = plan->dev.fold;
+    info->reserved = 0;
     return RCP_OK;
     RCP_CATCH
 }

@@ -1490,6 +1490,188 @@ __device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart
     return m;
 }
 
+// A bound search (dir_bound_multi: lower_bound(pmax >= v) or, up, upper_bound(start > v),
+// inside v's bucket of the directory at entry d0, nb buckets) by a group of G consecutive lanes
+// of one wave (G divides 64, group-aligned): after the bucket's directory line, each step probes G
+// points at once and keeps the (G + 1)-th of the interval holding the answer -- log_{G+1} of the
+// bucket's reads in dependent loads instead of log_2 (a hot peak's bucket holds thousands of
+// reads: 10 bisection steps -> 4 or 5).  Returns the same index as the bisection, in every lane
+// of the group.
+template <int G>
+__device__ __forceinline__ uint32_t dir_bound_group(const RcpPlanDev& P, int64_t d0, int32_t nb, int32_t v, bool up,
+                                                    bool active) {
+    const int lane = threadIdx.x & 63;
+    const int j = lane % G;
+    const int gbase = lane - j;
+    const int64_t thr = (int64_t)v + (up ? 1 : 0);
+    uint32_t lo = 0, hi = 0;
+    if (active) {
+        const int32_t b = min(max(v, 0) >> P.dir_shift, nb - 1);
+        if (P.dir_k) {
+            constexpr int kQ = 4, kKeys = 4 * kQ - 2;
+            const int4* src = reinterpret_cast<const int4*>(P.dir_k + 32 * (d0 + b) + (up ? 16 : 0));
+            int4 w[kQ];
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) w[q] = src[q];
+            const int32_t* x = reinterpret_cast<const int32_t*>(w);
+            const int32_t n = x[1] - x[0];
+            uint32_t c = 0;
+#pragma unroll
+            for (int i = 0; i < kKeys; ++i) c += (i < n && (int64_t)x[2 + i] < thr) ? 1u : 0u;
+            if (n <= kKeys) {
+                lo = (uint32_t)x[0] + c;
+                hi = c < (uint32_t)kKeys ? lo : (uint32_t)x[1];
+            } else {
+                lo = (uint32_t)x[0] + (c ? (uint32_t)rcp_dirk_offset(n, (int)c - 1) + 1u : 0u);
+                hi = c < (uint32_t)kKeys ? (uint32_t)x[0] + (uint32_t)rcp_dirk_offset(n, (int)c) : (uint32_t)x[1];
+            }
+        } else {
+            const int32_t* dir = up ? P.dir_u : P.dir_l;
+            lo = (uint32_t)dir[2 * (d0 + b)];
+            hi = (uint32_t)dir[2 * (d0 + b + 1)];
+        }
+    }
+    const int32_t* se = reinterpret_cast<const int32_t*>(P.se);
+    const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
+    while (true) {
+        const bool go = active && lo < hi;  // (uniform in the group)
+        if (!__ballot(go)) break;
+        const uint64_t width = hi - lo;
+        const uint32_t m = lo + (uint32_t)(((uint64_t)(j + 1) * width) / (G + 1));
+        bool pred = false;
+        if (go) pred = (int64_t)(up ? se[(size_t)m << 1] : P.pmax[m]) < thr;
+        // the probes below the threshold are a prefix (sorted keys): the answer is past the c-th
+        const uint32_t c = (uint32_t)__popcll(__ballot(pred) & gmask);
+        if (go) {
+            const uint32_t nlo = c ? lo + (uint32_t)(((uint64_t)c * width) / (G + 1)) + 1u : lo;
+            const uint32_t nhi = c < (uint32_t)G ? lo + (uint32_t)(((uint64_t)(c + 1) * width) / (G + 1)) : hi;
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    return lo;
+}
+
+// Fold plans (P.fold, general kernel; rcp_host.cpp sets it for small single-range tables in the
+// merged layout): the locate kernel's work for row r and this workgroup's column chunk, done by
+// the 4 G lanes of the row (G = 512 / (4 x the workgroup's rows): the whole workgroup) -- search s
+// of the row by lanes 4 s' .. : (0, 1) the row's lower / upper bound, for the row hit and the NULL
+// rules (R/coverage.R:189-225), (2, 3) the chunk piece's, i.e. its candidate reads (the locate
+// kernel's crange), each a G-lane search (dir_bound_group).  No locate launch and no 64-B record
+// round trip.  Every lane returns the row's metadata; the row's first lane in chunk 0 writes its
+// validity.  A fused-bins row with more than coop_min candidate reads in the chunk is marked
+// heavy = -2: the whole workgroup piles it (coop_row).
+template <bool MEDIAN, int G>
+__device__ __forceinline__ RowMeta fold_row(const RcpPlanDev& P, const RcpPart& part, int32_t k0, int cidx, int r) {
+    const int lane = threadIdx.x & 63;
+    const int rbase = lane & ~(4 * G - 1);  // the row's first lane
+    const int q = (lane - rbase) / G;       // its search
+    RowMeta m;
+    m.flag = 2; m.bs = 0; m.lay = -1; m.P0 = 0; m.npos = 0; m.kend = k0; m.heavy = -1; m.fast = 0;
+    m.off = m.slo = m.shi = m.rev = m.gps = m.gpe = 0;
+    for (int s = 0; s < 3; ++s) m.lo[s] = m.hi[s] = 0;
+    const bool in = r < P.n_rows;
+    RcpRowInfo ri;
+    {
+        uint4* d = reinterpret_cast<uint4*>(&ri);
+        const uint4* src = reinterpret_cast<const uint4*>(P.row_info + (in ? r : 0));
+#pragma unroll
+        for (int u = 0; u < (int)(sizeof(RcpRowInfo) / 16); ++u) d[u] = in ? src[u] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    const RcpSeg sg = ri.seg0;
+    const bool ok = in && !ri.stat && ri.chrom >= 0 && ri.chrom < P.n_chrom && ri.j1 == ri.j0 + 1 && sg.query_ok &&
+                    (sg.streams & 1);
+    // the chunk's slice of the row (decode_row)
+    int32_t head = 0, L = 0;
+    rcp_part_slice(part, ri.row_len, &head, &L);
+    const int32_t n = part.n_bins;
+    m.kend = min(k0 + part.chunk_bins, n);
+    bool pile = false;
+    if (in && k0 < n && !(!part.per_base && L < n)) {
+        if (part.per_base && L != n) {
+            m.flag = 1;  // (a width mismatch: raised below when the row is valid)
+        } else {
+            pile = true;
+            if (part.per_base) {
+                m.bs = 1;
+            } else {
+                m.bs = L / n;
+                const int32_t dif = L - m.bs * n;
+                if (dif) {
+                    m.lay = P.lay_index[part.lay_base + dif];
+                    if (m.lay < 0) m.lay = -1;
+                }
+            }
+            const int32_t e0 = bin_edge(m.bs, m.lay, P.lay_cnt, k0);
+            const int32_t e1 = bin_edge(m.bs, m.lay, P.lay_cnt, m.kend);
+            m.P0 = head + e0;
+            m.npos = e1 - e0;
+        }
+    }
+    // the chunk's genomic piece of the range
+    const int32_t len = sg.hi - sg.lo + 1;
+    const int32_t a = max(m.P0, sg.off), b = min(m.P0 + m.npos, sg.off + len);
+    const bool piece = pile && a < b;
+    int32_t gps = 0, gpe = 0;
+    if (piece) {
+        if (!sg.rev) {
+            gps = sg.lo + (a - sg.off);
+            gpe = sg.lo + (b - 1 - sg.off);
+        } else {
+            gpe = sg.hi - (a - sg.off);
+            gps = sg.hi - (b - 1 - sg.off);
+        }
+    }
+    // the row's four searches, G lanes each
+    const int32_t v = q == 0 ? sg.lo : (q == 1 ? sg.hi : (q == 2 ? gps : gpe));
+    const uint32_t res = dir_bound_group<G>(P, ri.d0, ri.nb, v, (q & 1) != 0, ok && (q < 2 || piece));
+    const uint32_t rlo = (uint32_t)__shfl((int)res, rbase);
+    const uint32_t rhi = max(rlo, (uint32_t)__shfl((int)res, rbase + G));
+    const uint32_t plo = (uint32_t)__shfl((int)res, rbase + 2 * G);
+    const uint32_t phi = (uint32_t)__shfl((int)res, rbase + 3 * G);
+    bool valid = ok && rlo < rhi;
+    // Rle[i2k] past the Rle -> NULL: seqlength, or the hits' last end when NA (locate_rows)
+    if (valid) valid = ri.seqlen >= 0 ? (int64_t)sg.hi <= ri.seqlen : sg.hi <= P.pmax[rhi - 1];
+    const bool first = lane == rbase;
+    if (in && first && cidx == 0) {
+        P.valid[r] = valid ? 1 : 0;
+        if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
+    }
+    if (!in) return m;
+    if (!valid) {
+        m.flag = 1;  // NULL row -> zeros (profile.R:191-197)
+        return m;
+    }
+    if (!pile) {
+        if (m.flag == 1 && first) atomicOr(P.status, RCP_STATUS_WIDTH);  // per-base width mismatch
+        return m;
+    }
+    if (m.lay < 0 && !part.per_base && L - m.bs * n != 0) {
+        if (first) atomicOr(P.status, RCP_STATUS_INTERP);
+    }
+    m.flag = 0;
+    if (MEDIAN && m.bs + (m.lay >= 0 ? 1 : 0) > P.chunk_cap) {
+        m.flag = 2;
+        return m;
+    }
+    if (m.npos <= P.chunk_cap) {
+        m.fast = 1;
+        m.off = sg.off; m.slo = sg.lo; m.shi = sg.hi; m.rev = sg.rev;
+        if (piece) {
+            m.gps = gps;
+            m.gpe = gpe;
+            const uint32_t clo = max(rlo, plo);
+            m.lo[0] = clo;
+            m.hi[0] = max(clo, min(rhi, phi));
+            const int need = (m.npos + 1 + 63) >> 6;
+            const int per = need <= 4 ? 4 : 1 << (32 - __clz(need - 1));
+            const bool fused = !MEDIAN && m.lay < 0 && (m.bs & (m.bs - 1)) == 0 && m.bs <= per && per <= 16;
+            if (fused && m.hi[0] - m.lo[0] > (uint32_t)P.coop_min) m.heavy = -2;
+        }
+    }
+    return m;
+}
+
 template <bool MEDIAN, bool CSR, bool UNI>
 __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4))) rcp_pileup_kernel(RcpPlanDev P, double* __restrict__ out,
                                                             int64_t* __restrict__ binsum) {
@@ -1537,13 +1719,32 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem) + kPWaves * (P.wave_words + 8);
     RowMeta* meta = reinterpret_cast<RowMeta*>(stage + (CSR ? 0 : T * RS));
 
-    // ---- per-row metadata, one thread per row, from the locate kernel's 64-byte records
-    if (tid < rows_wg) {
+    // ---- per-row metadata, one thread per row, from the locate kernel's 64-byte records -- or,
+    // in a fold plan, a quad of lanes per row searching its read ranges (fold_row)
+    if (!CSR && P.fold) {
+        // the whole workgroup: 512 / rows_wg lanes per row, a quarter of them per search
+        auto fold = [&](auto gc) {
+            constexpr int G = decltype(gc)::value;
+            const int i = tid / (4 * G);
+            const RowMeta m = fold_row<MEDIAN, G>(P, part, k0, cidx, row0 + i);
+            if (tid % (4 * G) == 0) meta[i] = m;
+        };
+        static_assert(kPBlock == 512, "fold lanes per row: 512 / rows");
+        if (rows_wg == 64) fold(std::integral_constant<int, 2>());
+        else if (rows_wg == 32) fold(std::integral_constant<int, 4>());
+        else fold(std::integral_constant<int, 8>());
+        // no heavy launch: the status set the next execution uses is zeroed here (nothing in this
+        // execution reads it)
+        if (blockIdx.x == 0 && tid < RCP_STATUS_WORDS) P.status_prev[tid] = 0u;
+    } else if (tid < rows_wg) {
         meta[tid] = decode_row<MEDIAN, CSR>(P, part, k0, cidx, row0 + tid);
     }
     uint32_t* ctr = reinterpret_cast<uint32_t*>(meta + kRows);  // row counter (RCP_GEN_DYN), in the tail words
     if (tid == 0) *ctr = 0u;
     lds_barrier();
+    // fold plans: the rows the whole workgroup piles (heavy = -2), one bit per workgroup row
+    uint64_t coop_bits = 0;
+    if (!CSR && !MEDIAN && P.fold) coop_bits = __ballot(lane < rows_wg && meta[lane].heavy == -2);
 
     // ---- rows of this wave (static dealing): round rd, sub s -> row rd*T + s*kPWaves + wave
     [[maybe_unused]] auto row_of = [&](int step) { return (step / kRowsPerWave) * T + (step % kRowsPerWave) * kPWaves + wave; };
@@ -1552,7 +1753,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     [[maybe_unused]] const int n_steps = kRowsPerWave * rounds;
     auto prefetch = [&](int i, RdT* dst) {
         const RowMeta m = uniform_meta(meta[i]);
-        const uint32_t n = (m.flag == 0 && m.fast) ? fast_candidates(m) : 0;
+        const uint32_t n = (m.flag == 0 && m.fast && m.heavy != -2) ? fast_candidates(m) : 0;
         if (n) {  // wave-uniform
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -1659,7 +1860,7 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
     auto pile_row = [&](int i, RdT (&cur)[4]) __attribute__((always_inline)) {
         const RowMeta m = uniform_meta(meta[i]);
         uint32_t* sbuf = stage;  // this round's stage
-        if (m.flag == 0) {  // wave-uniform: scalar branch
+        if (m.flag == 0 && m.heavy != -2) {  // wave-uniform: scalar branch (-2: piled by coop_row)
             const int r = row0 + i;
             const int32_t npos = m.npos;
             const int32_t bs = m.bs, lay = m.lay, kend = m.kend;
@@ -1806,12 +2007,77 @@ __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(4)
             }
         }
     };
+    // rows of round rd piled by the whole workgroup (coop_row, below)
+    auto round_coop = [&](int rd) { return (uint32_t)(coop_bits >> (rd * T)) & ((1u << T) - 1u); };
     auto pile_step = [&](int step, RdT (&cur)[4], RdT (&nxt)[4]) __attribute__((always_inline)) {
-        if (step + 1 < n_steps) prefetch(row_of(step + 1), nxt);
+        // (a round that starts with cooperative rows prefetches its first row after them: no read
+        // buffer is held across that phase)
+        const int ns = step + 1;
+        if (ns < n_steps && !(ns % kRowsPerWave == 0 && round_coop(ns / kRowsPerWave))) prefetch(row_of(ns), nxt);
         pile_row(row_of(step), cur);
     };
-    prefetch(row_of(0), bufA);
+    // a skewed row of a fold plan (no heavy slices): every wave piles batches w, w + 8, ... of its
+    // reads into the difference array of wave `owner`, which then stages its bin sums (fused
+    // pass) -- 8 waves on the row instead of one
+    auto coop_row = [&](int i, int owner) __attribute__((always_inline)) {
+        const RowMeta m = uniform_meta(meta[i]);
+        const int need = (m.npos + 1 + 63) >> 6;
+        const int sh = need <= 4 ? 2 : 32 - __clz(need - 1);
+        int32_t* od = reinterpret_cast<int32_t*>(smem) + owner * (P.wave_words + 8) + 8;
+        if (wave == owner) {
+            if (!(clean && clean_sh == sh)) {
+                int4* d4 = reinterpret_cast<int4*>(od);
+                for (int q = lane - 2; q < ((1 << sh) + 4) * 16; q += 64) d4[q] = make_int4(0, 0, 0, 0);
+            }
+            clean = false;
+        }
+        lds_barrier();
+        // every lane keeps KC reads in flight (a wave's 64 KC consecutive reads per round trip, the
+        // workgroup's 8 waves on interleaved batches: the heavy-slice kernel's memory parallelism);
+        // a skewed row's reads pile onto few positions, so equal positions of neighbouring lanes
+        // are one LDS add per run (run_add)
+        constexpr int KC = UNI ? 16 : 8;
+        const uint32_t n = fast_candidates(m);
+        const int32_t kf = m.off - m.slo - m.P0, kr = m.off + m.shi - m.P0;
+        for (uint32_t wb = 64u * KC * (uint32_t)wave; wb < n; wb += 64u * KC * kPWaves) {
+            RdT rdv[KC];
+#pragma unroll
+            for (int u = 0; u < KC; ++u) {
+                const uint32_t q = wb + 64u * u + lane;
+                rdv[u] = rd_load(fast_index(m, q < n ? q : n - 1));
+            }
+#pragma unroll
+            for (int u = 0; u < KC; ++u) {
+                const int2 x = rd_pair(rdv[u]);
+                const bool act = wb + 64u * u + lane < n && !(x.y < m.gps || x.x > m.gpe);
+                const int32_t x0 = max(x.x, m.gps), x1 = min(x.y, m.gpe);
+                const int32_t a0 = m.rev ? kr - x1 : x0 + kf;
+                const int32_t b0 = m.rev ? kr - x0 + 1 : x1 + kf + 1;
+                run_add(od, lp(a0, sh), act, 1);
+                run_add(od, lp(b0, sh), act, -1);
+            }
+        }
+        lds_barrier();
+        if (wave == owner) {
+            uint32_t* srow = stage + (i & (T - 1)) * RS;
+            const int lbs = 31 - __clz(m.bs);
+            if (sh == 2) scan_bins_fast<4>(od, lbs, srow, m.kend - k0);
+            else if (sh == 3) scan_bins_fast<8>(od, lbs, srow, m.kend - k0);
+            else scan_bins_fast<16>(od, lbs, srow, m.kend - k0);
+            lds_order();
+            clean = true;  // (the fused pass leaves the array zeroed)
+            clean_sh = sh;
+        }
+    };
+    if (!round_coop(0)) prefetch(row_of(0), bufA);
     for (int rd = 0; rd < rounds; ++rd) {
+        if (!CSR && !MEDIAN) {
+            uint32_t cm = round_coop(rd);  // (wave-uniform)
+            if (cm) {
+                for (int c = 0; cm; ++c, cm &= cm - 1) coop_row(rd * T + __builtin_ctz(cm), c & (kPWaves - 1));
+                prefetch(row_of(rd * kRowsPerWave), bufA);
+            }
+        }
         for (int s2 = 0; s2 < kRowsPerWave; s2 += 2) {
             pile_step(rd * kRowsPerWave + s2, bufA, bufB);
             pile_step(rd * kRowsPerWave + s2 + 1, bufB, bufA);

@@ -411,3 +411,44 @@ def test_coordinates_near_int32_max(gpu, ignore_strand):
             check(res, exp)
             if seqlen[0] > 0:
                 assert res[1][8] and not res[1][9]
+
+
+@pytest.mark.parametrize("uniform", [True, False], ids=["one_width", "many_widths"])
+def test_fold_plans_and_cooperative_rows(gpu, uniform):
+    """Small single-range tables in the merged layout run the general kernel FOLDED: each
+    workgroup searches its rows' and chunk's read ranges itself (no locate launch), and a row
+    whose chunk holds more than 8192 candidate reads is piled by the whole workgroup (no heavy
+    slices).  C4's shape (2-bp bins in two column chunks), per-base and 20-bp bins; rows on both
+    strands over a 60k-read pile; NA seqlengths; repeated executions.  Bit-equal to the oracle
+    and to the same plan on the locate + heavy-slice path."""
+    from recoup_amd.engine import Bins, Plan, ReadSet, RowTable
+    rng = np.random.default_rng(77 + uniform)
+    base = make_reads(rng, 150_000, widths=(150, 150) if uniform else (40, 400))
+    k = 60_000
+    hs = (200_000 + rng.integers(0, 1500, k)).astype(np.int32)
+    hw = np.full(k, 150) if uniform else rng.integers(40, 400, k)
+    reads = (np.r_[base[0], np.zeros(k, np.int32)], np.r_[base[1], hs], np.r_[base[2], (hs + hw - 1).astype(np.int32)],
+             np.r_[base[3], rng.integers(0, 3, k).astype(np.int8)])
+    r0 = single_rows(rng, 300, 2000, edge=True)
+    r0.start[1], r0.end[1] = 1, 2000  # (a start at 0 shortens its row: not a per-base row of 2000)
+    hot = (199_000 + rng.integers(-800, 1200, 8)).astype(np.int64)
+    rows = RowTable.from_ranges(np.r_[r0.chrom, np.zeros(8, np.int32)], np.r_[r0.start, hot],
+                                np.r_[r0.end, hot + 1999], np.r_[r0.strand, np.array([0, 1, 2, 1, 0, 1, 2, 1], np.int8)])
+    for seqlen in (CHROM_LEN, np.full(3, -1, np.int64)):
+        rs = ReadSet(*reads, seqlen, device=0)
+        ix = oracle_rows.index_for(reads, seqlen)
+        cov = oracle_rows.row_coverage(ix, rows)
+        for bins in (Bins([("whole", 1000)]), Bins([("whole", 0, 2000)]), Bins([("whole", 100)])):
+            fold = Plan(rs, rows, bins, kernel="general")
+            assert fold.info["fold"] == 1 and fold.info["pileup_kernel"] == 0, fold.info
+            slices = Plan(rs, rows, bins, kernel="general", heavy_threshold=4096)
+            assert slices.info["fold"] == 0
+            exp = oracle_rows.profile(cov, bins)
+            ref = slices.run()
+            assert slices.heavy_rows() > 0  # (the pile is skewed enough for the slice path)
+            for _ in range(3):  # (status words alternate between executions)
+                got = fold.run()
+                check(got, exp)
+                np.testing.assert_array_equal(got[1], ref[1])
+                assert np.array_equal(got[0].view(np.uint64), ref[0].view(np.uint64))
+            np.testing.assert_array_equal(fold.validity(), exp[1])

@@ -1,6 +1,6 @@
 """One GPU's shard k/N of the C4 (or $CFG) workload (as bench.py --sim-shard builds it) on each pileup
 kernel: ms per pass (D = 1, execute after execute), the stage times, and bit-equality with the
-default plan.   python tools/diag_shard_kernels.py [K/N] [kernels...]   (kernel:C = min_col_chunks C)"""
+default plan.   python tools/diag_shard_kernels.py [K/N] [kernels...]   (kernel:C:H = min_col_chunks C, heavy_threshold H)"""
 import os
 import sys
 import time
@@ -24,8 +24,10 @@ reads = bench.reads_for_rows(data["reads"], rows, len(data["seqlen"])) if n > 1 
 rs = ReadSet(*reads, data["seqlen"], device=0)
 ref = None
 for kern in kernels:
-    name, _, mcc = kern.partition(":")
-    plan = Plan(rs, rows, bins, kernel=name, out_ld="padded", min_col_chunks=int(mcc or 0))
+    name, _, rest = kern.partition(":")
+    mcc, _, heavy = rest.partition(":")
+    plan = Plan(rs, rows, bins, kernel=name, out_ld="padded", min_col_chunks=int(mcc or 0),
+                heavy_threshold=int(heavy or -1))
     out = plan.empty_output()
     for _ in range(5):
         plan.execute(out)
@@ -52,5 +54,5 @@ for kern in kernels:
     same = None if ref is None else bool(torch.equal(m.view(torch.int64), ref.view(torch.int64)))
     if ref is None:
         ref = m
-    print(f"{args.config} {spec} {kern:8s} kernel {plan.info['pileup_kernel']} grid {plan.info['grid']} ms/pass {ms:.4f} "
+    print(f"{args.config} {spec} {kern:8s} kernel {plan.info['pileup_kernel']} fold {plan.info['fold']} grid {plan.info['grid']} ms/pass {ms:.4f} "
           f"locate {st[0]:.4f} pileup {st[1]:.4f} same_as_first {same}", flush=True)

@@ -706,20 +706,27 @@ def rle_path(host, seqlen, rows, bins, local, units, fused, reps):
     Phases per call: readset_create, coverage_rle (incl. the D2H of the runs), profile_rle
     (H2D of the runs, the profile kernel, D2H of the matrix).  The matrix is checked bit-equal
     to the fused pass's (``fused``, the host matrix end_to_end just filled)."""
-    from recoup_amd.engine import ReadSet, coverage_rle_host, profile_rle_arrays
+    from recoup_amd.engine import ReadSet, coverage_rle_kept, profile_rle_arrays
     out = np.zeros((rows.n_rows, bins.n_cols), order="F")
+    up = np.zeros((rows.n_rows, bins.n_cols), order="F")
     calls = []
     n_runs = None
+    upload_ms = []
     for _ in range(reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         rs = ReadSet(*host, seqlen, device=local)
         t1 = time.perf_counter()
-        run_off, values, lengths, valid = coverage_rle_host(rs, rows)
+        kept = coverage_rle_kept(rs, rows)
+        run_off, values, lengths, valid = kept.copy()  # the list of Rle R builds
         t2 = time.perf_counter()
-        profile_rle_arrays(run_off, lengths, values, (valid == 0).astype(np.uint8), bins, local, out)
+        kept.profile(bins, out)  # profileMatrix of that unchanged list: its runs on the device
         t3 = time.perf_counter()
+        # the same list after it changed (an element replaced, save / load): its runs uploaded
+        profile_rle_arrays(run_off, lengths, values, (valid == 0).astype(np.uint8), bins, local, up)
+        upload_ms.append((time.perf_counter() - t3) * 1e3)
         del rs
+        kept.close()
         n_runs = int(run_off[-1])
         # the host runs (0.8 GB on C4) are released between calls, outside the timed phases: R
         # frees a finished call's vectors at its garbage collection, not inside the next call
@@ -731,9 +738,13 @@ def rle_path(host, seqlen, rows, bins, local, units, fused, reps):
             "phases_ms": {"readset_create": med[1], "coverage_rle": med[2], "profile_rle": med[3]},
             "calls_ms": [round(c[0], 2) for c in calls], "n_runs": n_runs,
             "run_bytes": 8 * n_runs, "equal_fused": bool(np.array_equal(out.T.view(np.int64), fused.view(np.int64))),
-            "note": "recoup()'s default R path: rcp_coverage_rle (GPU pileup + RLE, runs to the host) then "
-                    "rcp_profile_rle of the host runs (H2D, profile kernel, D2H); equal_fused: bit-equal to "
-                    "the fused rcp_profile matrix"}
+            "profile_rle_upload_ms": sorted(upload_ms)[len(upload_ms) // 2],
+            "equal_upload": bool(np.array_equal(up.view(np.int64), out.view(np.int64))),
+            "note": "recoup()'s default R path: rcp_coverage_rle (GPU pileup + RLE, runs to the host: the list of "
+                    "Rle) then profileMatrix of that unchanged list from its runs still on the device "
+                    "(rcp_profile_cov; r/R/rcp.R keeps them beside the list); profile_rle_upload_ms: the same "
+                    "profile of the host runs uploaded again (rcp_profile_rle: a list that changed, or was "
+                    "loaded); equal_fused: bit-equal to the fused rcp_profile matrix"}
 
 
 def cpu_baseline(args, data, rows, bins, plan, B):

@@ -376,6 +376,15 @@ RCP_API int rcp_profile_rle(const rcp_rle_desc* cov, const rcp_bins_desc* bins, 
 RCP_API int rcp_profile_rle_multi(const rcp_rle_desc* cov, const rcp_bins_desc* bins, const int32_t* device_ids,
                                   int32_t n_devices, double* out, uint8_t* row_valid);
 
+/* rcp_profile_rle of a calcCoverage result still held on the device (rcp_coverage_rle /
+ * rcp_shards_coverage): the profile of exactly the runs rcp_cov_copy gives, without them crossing
+ * PCIe again -- recoup() profiles the list coverageRef just returned (R/recoup.R:551-597, and the
+ * forced heatmap binning :659-714); the R wrappers use it while the list's Rle vectors are the ones
+ * copied out (r/R/rcp.R).  bins, out (host R column-major n_rows x n_cols) and row_valid as for
+ * rcp_profile_rle; NULL rows are the invalid ones.  Bit-identical to rcp_profile_rle of the copied
+ * runs. */
+RCP_API int rcp_profile_cov(const rcp_cov* cov, const rcp_bins_desc* bins, double* out, uint8_t* row_valid);
+
 /* calcCoverage: per-row integer depth vectors (CSR).  out_off is the host prefix sum of
  * rcp_plan_row_lengths(); d_cov (device int32 [out_off[n_rows]]) receives each valid row's
  * depth at its offset; d_valid (device) the NULL mask.  Rows are in the row's own

@@ -143,7 +143,13 @@
 # rcp_R_coverage over a readset and a row table -> calcCoverage's named list of Rle
 # (R/coverage.R:171-173; NULL where findOverlaps finds no read, the chromosome is absent or a
 # subscript fails), run-length encoded on the GPU and rebuilt here without expanding it.  A
-# readset split over several devices serves its own row table (rs$rows), every device at once
+# readset split over several devices serves its own row table (rs$rows), every device at once.
+# The runs also stay on the GPU(s): attr(, "rcpRuns") holds their handle and the addresses of
+# the Rle vectors built here, and profileMatrix profiles them there while the list still holds
+# those vectors (.rcpProfileRle) -- recoup() profiles the list coverageRef just returned
+# (R/recoup.R:551-597, the forced heatmap pass :659-714), so its 12 bytes a run do not cross PCIe
+# again.  options(recoup.deviceRuns = FALSE) releases them at once; otherwise the garbage
+# collector does, with the list
 .rcpCoverage <- function(rs, rows, names) {
     res <- if (!is.null(rs$rows)) .Call("rcp_R_shards_coverage", rs$ptr, PACKAGE = "recoup") else
         do.call(.Call, c(list("rcp_R_coverage", if (is.list(rs$ptr)) rs$ptr[[1]] else rs$ptr),
@@ -155,6 +161,11 @@
         Rle(res$values[i], res$lengths[i])
     })
     names(cov) <- names
+    if (isTRUE(getOption("recoup.deviceRuns", TRUE)))
+        attr(cov, "rcpRuns") <- list(handle = res$handle,
+            addr = .Call("rcp_R_rle_addresses", cov, PACKAGE = "recoup"))
+    else
+        .Call("rcp_R_cov_free", res$handle, PACKAGE = "recoup")
     cov
 }
 
@@ -313,13 +324,22 @@ coverageRnaRef <- function(input, genomeRanges, helperRanges, flank,
 # matrix's dimnames as the reference's rbind / cbind leave them (r/src/recoup_amd_shim.c,
 # set_dimnames): rownames = rowNames, colnames "<bin>.<stat>" for binned parts, "" for per-base
 # parts, none when no part is binned
+# parts, where the list is still the one .rcpCoverage built: profiled from its runs on the GPU(s)
+# (rcp_R_profile_cov; any element replaced -- R keeps the attribute -- or the handle released, as
+# load() leaves it: the list's own vectors are uploaded instead)
 .rcpProfileRle <- function(cvrg, where, flank, nBins, perBase, stat = "mean",
     interpolation = "auto", rowNames = NULL) {
-    a <- .rcpRleArrays(cvrg)
-    res <- .Call("rcp_R_profile_rle", a$runOff, a$values, a$lengths, a$isNull,
-        as.integer(where), as.integer(if (is.null(flank)) c(0, 0) else flank),
+    binArgs <- list(as.integer(where), as.integer(if (is.null(flank)) c(0, 0) else flank),
         as.integer(nBins), as.integer(perBase), .rcpStat(stat), .rcpInterp(interpolation),
-        .rcpRngKind(), 1.0, .rcpDevices(), rowNames, PACKAGE = "recoup")
+        .rcpRngKind(), 1.0)
+    h <- attr(cvrg, "rcpRuns")
+    if (!is.null(h) && .Call("rcp_R_cov_alive", h$handle, PACKAGE = "recoup") &&
+        identical(.Call("rcp_R_rle_addresses", cvrg, PACKAGE = "recoup"), h$addr))
+        return(do.call(.Call, c(list("rcp_R_profile_cov", h$handle), binArgs,
+            list(rowNames, PACKAGE = "recoup")))$profile)
+    a <- .rcpRleArrays(cvrg)
+    res <- do.call(.Call, c(list("rcp_R_profile_rle", a$runOff, a$values, a$lengths, a$isNull),
+        binArgs, list(.rcpDevices(), rowNames, PACKAGE = "recoup")))
     res$profile
 }
 

@@ -9,7 +9,10 @@
  *   calcCoverage / coverageFromRanges (R/coverage.R:126-226) rcp_R_coverage / rcp_R_shards_coverage
  *                                                                -> list of Rle pieces
  *   binCoverageMatrix / baseCoverageMatrix / splitVector     rcp_R_profile_rle (the stored $coverage,
- *       (R/profile.R:100-212, R/util.R:15-85)                    a list of Rle, as R keeps it)
+ *       (R/profile.R:100-212, R/util.R:15-85)                    a list of Rle, as R keeps it) /
+ *                                                                rcp_R_profile_cov (its runs still on
+ *                                                                the device: rcp_R_rle_addresses,
+ *                                                                rcp_R_cov_alive, rcp_R_cov_free)
  *   profileMatrix straight from the reads (fused, one call   rcp_R_profile / rcp_R_profile_multi /
  *       per sample, or all samples at once; R/profile.R:1-98)   rcp_R_profile_samples / rcp_R_shards_profile /
  *                                                                rcp_R_profile_reads (reads on the host)
@@ -482,10 +485,13 @@ SEXP rcp_R_profile_rle(SEXP runOff, SEXP values, SEXP lengths, SEXP isNull, SEXP
 
 /* ------------------------------------------------------------------ coverage */
 /* .Call("rcp_R_coverage", readset, <rows: 8 args>)
- * -> list(runOff = numeric n_rows + 1, values = integer, lengths = integer, valid = logical):
- * the pieces of calcCoverage's named list of Rle (R/coverage.R:171-173), from which the R side
- * builds S4Vectors::Rle(values, lengths) per valid row without expanding it */
-/* The Rle pieces of a coverage handle held by `guard` (released here once copied) */
+ * -> list(runOff = numeric n_rows + 1, values = integer, lengths = integer, valid = logical,
+ *         handle = external pointer): the pieces of calcCoverage's named list of Rle
+ * (R/coverage.R:171-173), from which the R side builds S4Vectors::Rle(values, lengths) per valid
+ * row without expanding it, and the handle that keeps the same runs on the device (released by
+ * rcp_R_cov_free or the garbage collector): while the list is unchanged, profileMatrix profiles
+ * them there (rcp_R_profile_cov) instead of uploading its Rle vectors again */
+/* The Rle pieces of a coverage handle held by `guard` (kept: the result's `handle`) */
 static SEXP coverage_result(SEXP guard, rcp_cov* cov) {
     int32_t nrow = 0;
     int64_t nruns = 0;
@@ -497,22 +503,85 @@ static SEXP coverage_result(SEXP guard, rcp_cov* cov) {
     int64_t* o64 = (int64_t*)R_alloc(nrow + 1, sizeof(int64_t));
     uint8_t* v8 = (uint8_t*)R_alloc(nrow > 0 ? nrow : 1, 1);
     int rc = rcp_cov_copy(cov, o64, INTEGER(val), INTEGER(len), v8);
-    cov_finalizer(guard); /* the runs are in R's vectors now */
+    if (rc != RCP_OK) cov_finalizer(guard); /* (nothing to keep) */
     check(rc);
     for (int r = 0; r <= nrow; ++r) REAL(off)[r] = (double)o64[r];
     for (int r = 0; r < nrow; ++r) LOGICAL(ok)[r] = v8[r];
-    SEXP res = PROTECT(allocVector(VECSXP, 4));
+    SEXP res = PROTECT(allocVector(VECSXP, 5));
     SET_VECTOR_ELT(res, 0, off);
     SET_VECTOR_ELT(res, 1, val);
     SET_VECTOR_ELT(res, 2, len);
     SET_VECTOR_ELT(res, 3, ok);
-    SEXP nm = PROTECT(allocVector(STRSXP, 4));
+    SET_VECTOR_ELT(res, 4, guard);
+    SEXP nm = PROTECT(allocVector(STRSXP, 5));
     SET_STRING_ELT(nm, 0, mkChar("runOff"));
     SET_STRING_ELT(nm, 1, mkChar("values"));
     SET_STRING_ELT(nm, 2, mkChar("lengths"));
     SET_STRING_ELT(nm, 3, mkChar("valid"));
+    SET_STRING_ELT(nm, 4, mkChar("handle"));
     setAttrib(res, R_NamesSymbol, nm);
     UNPROTECT(6);
+    return res;
+}
+
+/* .Call("rcp_R_rle_addresses", list) -> numeric 2 n: for element i, the addresses of its
+ * "values" and "lengths" slot vectors when it is an S4 object with both (an S4Vectors::Rle), else
+ * 0, 0.  R replaces a modified vector (copy on modify) and builds a new Rle for any operation on
+ * one (runValue<-, arithmetic, a linear rescale), so equal addresses mean the list still holds
+ * the runs it was built from -- read in C: runValue() per element would be an S4 dispatch each */
+SEXP rcp_R_rle_addresses(SEXP list) {
+    R_xlen_t n = TYPEOF(list) == VECSXP ? XLENGTH(list) : 0;
+    SEXP out = PROTECT(allocVector(REALSXP, 2 * n));
+    SEXP vs = PROTECT(install("values")), ls = PROTECT(install("lengths"));
+    for (R_xlen_t i = 0; i < n; ++i) {
+        SEXP x = VECTOR_ELT(list, i);
+        double a = 0.0, b = 0.0;
+        if (IS_S4_OBJECT(x) && R_has_slot(x, vs) && R_has_slot(x, ls)) {
+            a = (double)(uintptr_t)R_do_slot(x, vs);
+            b = (double)(uintptr_t)R_do_slot(x, ls);
+        }
+        REAL(out)[2 * i] = a;
+        REAL(out)[2 * i + 1] = b;
+    }
+    UNPROTECT(3);
+    return out;
+}
+
+/* .Call("rcp_R_cov_alive", handle) -> TRUE while the handle holds its device runs (FALSE once
+ * freed, or after save() / load(): R restores an external pointer as NULL) */
+SEXP rcp_R_cov_alive(SEXP p) {
+    SEXP out = PROTECT(allocVector(LGLSXP, 1));
+    LOGICAL(out)[0] = TYPEOF(p) == EXTPTRSXP && R_ExternalPtrAddr(p) != NULL;
+    UNPROTECT(1);
+    return out;
+}
+
+/* .Call("rcp_R_cov_free", handle): release the device runs now */
+SEXP rcp_R_cov_free(SEXP p) {
+    cov_finalizer(p);
+    return R_NilValue;
+}
+
+/* .Call("rcp_R_profile_cov", handle, <bins: 8 args>, rowNames) -> list(profile, valid):
+ * rcp_R_profile_rle of the runs the handle keeps on the device(s) (rcp_profile_cov) */
+SEXP rcp_R_profile_cov(SEXP p, SEXP where, SEXP flank, SEXP nBins, SEXP pbw, SEXP stat, SEXP interp, SEXP rng,
+                       SEXP scale, SEXP rowNames) {
+    rcp_cov* cov = (rcp_cov*)R_ExternalPtrAddr(p);
+    if (!cov) Rf_error("recoup_amd: the coverage handle was released");
+    int32_t nrow = 0;
+    check(rcp_cov_info(cov, &nrow, NULL));
+    int ncol = 0;
+    rcp_bins_desc bd = bins_of(where, flank, nBins, pbw, stat, interp, rng, scale, &ncol);
+    SEXP out = PROTECT(allocMatrix(REALSXP, nrow, ncol));
+    uint8_t* valid = (uint8_t*)R_alloc(nrow ? nrow : 1, 1);
+    int rc = rcp_profile_cov(cov, &bd, REAL(out), valid);
+    if (rc != RCP_OK) {
+        UNPROTECT(1);
+        check(rc);
+    }
+    set_dimnames(out, rowNames, &bd, nrow, ncol);
+    SEXP res = profile_result(out, valid, nrow);
+    UNPROTECT(1);
     return res;
 }
 
@@ -624,6 +693,10 @@ static const R_CallMethodDef call_methods[] = {
     {"rcp_R_shards_profile", (DL_FUNC)&rcp_R_shards_profile, 10},
     {"rcp_R_shards_coverage", (DL_FUNC)&rcp_R_shards_coverage, 1},
     {"rcp_R_shards_free", (DL_FUNC)&rcp_R_shards_free, 1},
+    {"rcp_R_rle_addresses", (DL_FUNC)&rcp_R_rle_addresses, 1},
+    {"rcp_R_cov_alive", (DL_FUNC)&rcp_R_cov_alive, 1},
+    {"rcp_R_cov_free", (DL_FUNC)&rcp_R_cov_free, 1},
+    {"rcp_R_profile_cov", (DL_FUNC)&rcp_R_profile_cov, 10},
     {NULL, NULL, 0}};
 
 void R_init_recoup(DllInfo* dll) {

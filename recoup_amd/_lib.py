@@ -125,6 +125,7 @@ SIGNATURES = [
     ("rcp_cov_info", ctypes.c_int, [_vp, _i32p, _i64p]),
     ("rcp_cov_copy", ctypes.c_int, [_vp, _i64p, _i32p, _i32p, _u8p]),
     ("rcp_cov_free", ctypes.c_int, [_vp]),
+    ("rcp_profile_cov", ctypes.c_int, [_vp, ctypes.POINTER(BinsDesc), _dp, _u8p]),
     ("rcp_bam_read", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                     ctypes.POINTER(_vp)]),
     ("rcp_bam_info", ctypes.c_int, [_vp, _i64p, _i32p, _i64p]),

@@ -2776,28 +2776,50 @@ struct RleJob {
     int32_t R = 0;
     int64_t col = 0, ld = 0;
     const uint8_t* is_null = nullptr;
+    std::vector<uint8_t> null_own;  // a device-resident list's NULL rows (rle_prepare with `res`)
 };
 
 // dev_rows: the row lengths and the run-length checks on the device (a row block of a big list:
 // no host pass over its runs); row_base numbers the rows of the messages
-int rle_prepare(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, hipStream_t s, RleJob* job,
-                bool dev_rows = false, int32_t row_base = 0) {
+// res (cov NULL): the list is a calcCoverage result still on the device (rcp_profile_cov) -- its
+// runs are copied device to device, its NULL rows read from its validity; nothing crosses PCIe
+int rle_prepare(const rcp_rle_desc* cov_in, const rcp_bins_desc* bins, int device, hipStream_t s, RleJob* job,
+                bool dev_rows = false, int32_t row_base = 0, const rcp_cov* res = nullptr) {
+    rcp_rle_desc rdesc{};
+    const rcp_rle_desc* cov = cov_in;
+    if (res) {
+        if (res->device != device) return fail(RCP_EINVAL, "internal: coverage on device %d, not %d", res->device, device);
+        rdesc.n_rows = res->n_rows;
+        cov = &rdesc;
+        dev_rows = true;
+    }
     if (!cov || !bins) return fail(RCP_EINVAL, "NULL argument");
     const int32_t R = cov->n_rows;
     if (R < 0) return fail(RCP_EINVAL, "n_rows < 0");
-    if (R > 0 && !cov->run_off) return fail(RCP_EINVAL, "NULL run_off");
+    if (R > 0 && !cov->run_off && !res) return fail(RCP_EINVAL, "NULL run_off");
     if (bins->n_parts < 1 || bins->n_parts > RCP_MAX_PARTS) return fail(RCP_EINVAL, "n_parts = %d", bins->n_parts);
     if (bins->stat != RCP_STAT_MEAN && bins->stat != RCP_STAT_MEDIAN) return fail(RCP_EINVAL, "stat = %d", bins->stat);
     if (bins->interp < 0 || bins->interp > 3) return fail(RCP_EINVAL, "interp = %d", bins->interp);
     if (bins->flank[0] < 0 || bins->flank[1] < 0) return fail(RCP_EINVAL, "negative flank");
     const bool dbl = cov->dvalues != nullptr;
-    const int64_t n_runs = R > 0 ? cov->run_off[R] : 0;
-    if (R > 0 && cov->run_off[0] != 0) return fail(RCP_EINVAL, "run_off[0] != 0");
-    for (int32_t r = 0; r < R; ++r)
-        if (cov->run_off[r + 1] < cov->run_off[r]) return fail(RCP_EINVAL, "run_off decreases at row %d", r);
-    if (n_runs > 0 && (!cov->lengths || (!cov->ivalues && !cov->dvalues)))
-        return fail(RCP_EINVAL, "NULL lengths / values");
-    if (cov->ivalues && cov->dvalues) return fail(RCP_EINVAL, "both integer and numeric values given");
+    const int64_t n_runs = res ? res->n_runs : (R > 0 ? cov->run_off[R] : 0);
+    if (!res) {
+        if (R > 0 && cov->run_off[0] != 0) return fail(RCP_EINVAL, "run_off[0] != 0");
+        for (int32_t r = 0; r < R; ++r)
+            if (cov->run_off[r + 1] < cov->run_off[r]) return fail(RCP_EINVAL, "run_off decreases at row %d", r);
+        if (n_runs > 0 && (!cov->lengths || (!cov->ivalues && !cov->dvalues)))
+            return fail(RCP_EINVAL, "NULL lengths / values");
+        if (cov->ivalues && cov->dvalues) return fail(RCP_EINVAL, "both integer and numeric values given");
+    } else if (R > 0) {
+        // the list's NULL elements: its invalid rows (calcCoverage's NULL, R/coverage.R:217-225)
+        DeviceGuard gd(device);
+        HIP_TRY(gd.err);
+        job->null_own.resize((size_t)R);
+        HIP_TRY(hipMemcpyAsync(job->null_own.data(), res->valid.p, (size_t)R, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        for (uint8_t& v : job->null_own) v = v ? 0 : 1;
+        rdesc.is_null = job->null_own.data();
+    }
     // Rle lengths are positive and every row fits int32 positions; row lengths (the slices of
     // the parts).  One pass over the runs, rows split over host threads (C4: 100 M runs).
     std::vector<int32_t> row_len(std::max(R, 1), 0);
@@ -2842,13 +2864,19 @@ int rle_prepare(const rcp_rle_desc* cov, const rcp_bins_desc* bins, int device, 
     HIP_TRY(d_len.alloc(4 * ((size_t)n_runs + 1)));
     HIP_TRY(d_val.alloc((dbl ? 8 : 4) * std::max<size_t>((size_t)n_runs, 1)));
     HIP_TRY(d_off.alloc(8 * ((size_t)R + 1)));
-    if (n_runs) {  // (integer runs: 16-bit offsets within blocks where they fit, rcp_stage.h)
+    if (res) {  // device to device
+        if (n_runs) {
+            HIP_TRY(hipMemcpyAsync(d_len.p, res->lengths.p, 4 * (size_t)n_runs, hipMemcpyDeviceToDevice, s));
+            HIP_TRY(hipMemcpyAsync(d_val.p, res->values.p, 4 * (size_t)n_runs, hipMemcpyDeviceToDevice, s));
+        }
+        if (R > 0) HIP_TRY(hipMemcpyAsync(d_off.p, res->run_off.p, 8 * ((size_t)R + 1), hipMemcpyDeviceToDevice, s));
+    } else if (n_runs) {  // (integer runs: 16-bit offsets within blocks where they fit, rcp_stage.h)
         HIP_TRY(rcp::stage_h2d_i32(d_len.as<int32_t>(), cov->lengths, (size_t)n_runs, device, s));
         if (dbl) HIP_TRY(rcp::stage_h2d(d_val.p, cov->dvalues, 8 * (size_t)n_runs, device, s));
         else HIP_TRY(rcp::stage_h2d_i32(d_val.as<int32_t>(), cov->ivalues, (size_t)n_runs, device, s));
     }
     HIP_TRY(hipMemsetAsync(d_len.as<int32_t>() + n_runs, 0, 4, s));
-    if (R > 0) HIP_TRY(rcp::stage_h2d(d_off.p, cov->run_off, 8 * ((size_t)R + 1), device, s));
+    if (R > 0 && !res) HIP_TRY(rcp::stage_h2d(d_off.p, cov->run_off, 8 * ((size_t)R + 1), device, s));
     if (dev_rows && R > 0) {
         PoolBuf d_rl(s), d_bad(s);
         HIP_TRY(d_rl.alloc(4 * (size_t)R));
@@ -3286,6 +3314,45 @@ extern "C" int rcp_profile_rle_multi(const rcp_rle_desc* cov, const rcp_bins_des
         sub.is_null = cov->is_null ? cov->is_null + r0 : nullptr;
         return profile_rle_device(&sub, bins, device_ids[i], out ? out + r0 : nullptr, R,
                                   row_valid ? row_valid + r0 : nullptr);
+    });
+    RCP_CATCH
+}
+
+extern "C" int rcp_profile_cov(const rcp_cov* c, const rcp_bins_desc* bins, double* out, uint8_t* row_valid) {
+    RCP_TRY
+    if (!c || !bins) return fail(RCP_EINVAL, "NULL argument");
+    if (bins->n_parts < 1 || bins->n_parts > RCP_MAX_PARTS) return fail(RCP_EINVAL, "n_parts = %d", bins->n_parts);
+    const int32_t R = c->n_rows;
+    auto one = [&](const rcp_cov* part, double* o, int64_t ld, uint8_t* v) -> int {
+        RleJob job(nullptr);
+        const int rc = rle_prepare(nullptr, bins, part->device, nullptr, &job, true, 0, part);
+        if (rc) return rc;
+        return rle_finish(&job, part->device, o, ld, v, nullptr);
+    };
+    if (c->parts.empty()) return one(c, out, R, row_valid);
+    // several devices' row blocks (rcp_shards_coverage): each block profiled on its own device, its
+    // rows into the caller's matrix -- in place when the blocks are the caller's row ranges, else
+    // through a host matrix of the block scattered to the caller's rows (the shards' order)
+    int64_t C = 0;
+    for (int p = 0; p < bins->n_parts; ++p)
+        C += bins->n_bins[p] ? bins->n_bins[p] : (bins->per_base_width ? bins->per_base_width[p] : 0);
+    const int np = (int)c->parts.size();
+    return run_per_device(np, [&](int b) -> int {
+        const rcp_cov* p = c->parts[b].get();
+        const int32_t r0 = c->split[b], n = p->n_rows;
+        if (n == 0) return (int)RCP_OK;
+        if (c->order.empty()) return one(p, out ? out + r0 : nullptr, R, row_valid ? row_valid + r0 : nullptr);
+        std::vector<double> tmp(out ? (size_t)n * (size_t)C : 0);
+        std::vector<uint8_t> v((size_t)n);
+        const int rc = one(p, out ? tmp.data() : nullptr, n, v.data());
+        if (rc) return rc;
+        for (int32_t i = 0; i < n; ++i) {
+            const int32_t r = c->order[(size_t)r0 + i];
+            if (row_valid) row_valid[r] = v[i];
+            if (out)
+                for (int64_t k = 0; k < C; ++k) out[(size_t)k * R + r] = tmp[(size_t)k * n + i];
+        }
+        return (int)RCP_OK;
     });
     RCP_CATCH
 }

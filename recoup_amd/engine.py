@@ -450,6 +450,12 @@ class Shards:
         check(_lib.lib().rcp_shards_coverage(self.h, ctypes.byref(h)))
         return _cov_copy(h)
 
+    def coverage_rle_kept(self):
+        """rcp_shards_coverage, the result kept on the devices (CoverageHandle)."""
+        h = ctypes.c_void_p()
+        check(_lib.lib().rcp_shards_coverage(self.h, ctypes.byref(h)))
+        return CoverageHandle(h, self.rows.n_rows)
+
     def close(self):
         if getattr(self, "h", None):
             _lib.lib().rcp_shards_destroy(self.h)
@@ -596,18 +602,65 @@ def coverage_rle_host(readset, rows, timing=None):
     return res
 
 
+def _cov_arrays(h):
+    """rcp_cov_info + rcp_cov_copy of a coverage handle: (run_off, values, lengths, valid)."""
+    L = _lib.lib()
+    nr, nruns = ctypes.c_int32(), ctypes.c_int64()
+    check(L.rcp_cov_info(h, ctypes.byref(nr), ctypes.byref(nruns)))
+    run_off = np.empty(nr.value + 1, np.int64)
+    values = np.empty(max(nruns.value, 1), np.int32)
+    lengths = np.empty(max(nruns.value, 1), np.int32)
+    valid = np.empty(max(nr.value, 1), np.uint8)
+    check(L.rcp_cov_copy(h, cptr(run_off, _lib._i64p), cptr(values, _lib._i32p), cptr(lengths, _lib._i32p),
+                         cptr(valid, _lib._u8p)))
+    return run_off, values[:nruns.value], lengths[:nruns.value], valid[:nr.value]
+
+
 def _cov_copy(h):
     """rcp_cov_info + rcp_cov_copy + rcp_cov_free of a coverage handle."""
-    L = _lib.lib()
     try:
-        nr, nruns = ctypes.c_int32(), ctypes.c_int64()
-        check(L.rcp_cov_info(h, ctypes.byref(nr), ctypes.byref(nruns)))
-        run_off = np.empty(nr.value + 1, np.int64)
-        values = np.empty(max(nruns.value, 1), np.int32)
-        lengths = np.empty(max(nruns.value, 1), np.int32)
-        valid = np.empty(max(nr.value, 1), np.uint8)
-        check(L.rcp_cov_copy(h, cptr(run_off, _lib._i64p), cptr(values, _lib._i32p), cptr(lengths, _lib._i32p),
-                             cptr(valid, _lib._u8p)))
+        return _cov_arrays(h)
     finally:
-        L.rcp_cov_free(h)
-    return run_off, values[:nruns.value], lengths[:nruns.value], valid[:nr.value]
+        _lib.lib().rcp_cov_free(h)
+
+
+class CoverageHandle:
+    """A calcCoverage result kept on the device (rcp_coverage_rle / rcp_shards_coverage): its runs
+    copied to the host (copy(): the arrays the R shim builds the list of Rle from) and profiled
+    where they are (profile(): rcp_profile_cov -- what r/R/rcp.R does while the list it returned
+    is unchanged, instead of uploading the runs again)."""
+
+    def __init__(self, h, n_rows):
+        self.h, self.n_rows = h, n_rows
+
+    def copy(self):
+        return _cov_arrays(self.h)
+
+    def profile(self, bins, out=None):
+        """rcp_profile_cov -> (matrix (n_rows, n_cols) F-ordered float64, validity bool)."""
+        R = self.n_rows
+        if out is None:
+            out = np.zeros((R, bins.n_cols), order="F")
+        elif out.dtype != np.float64 or not out.flags.f_contiguous or out.shape != (R, bins.n_cols):
+            raise ValueError("out must be an F-ordered float64 array of n_rows x n_cols")
+        valid = np.zeros(max(R, 1), np.uint8)
+        bd = bins.desc()
+        check(_lib.lib().rcp_profile_cov(self.h, ctypes.byref(bd), cptr(out, _lib._dp), cptr(valid, _lib._u8p)))
+        return out, valid[:R].astype(bool)
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib().rcp_cov_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def coverage_rle_kept(readset, rows):
+    """rcp_coverage_rle, the result kept on the device (CoverageHandle)."""
+    rd = rows.desc()
+    h = ctypes.c_void_p()
+    with torch.cuda.device(readset.device):
+        check(_lib.lib().rcp_coverage_rle(readset.h, ctypes.byref(rd), ctypes.byref(h)))
+    return CoverageHandle(h, rows.n_rows)

@@ -18,11 +18,42 @@ MIRRORED = [".rcpDevices", ".rcpReadArgs", ".rcpReadSet", ".rcpFree", ".rcpSampl
 
 
 class NamedList(list):
-    """An R list with names (None = no names attribute), e.g. calcCoverage's list of Rle."""
+    """An R list with names (None = no names attribute), e.g. calcCoverage's list of Rle.
+    ``rcp_runs``: its attr(, "rcpRuns") (the device handle of the runs and their addresses), or
+    None -- R keeps the attribute when an element is replaced, not when the list is rebuilt."""
 
     def __init__(self, items, names=None):
         super().__init__(items)
         self.names = None if names is None else [str(x) for x in names]
+        self.rcp_runs = None
+
+
+class Rle(tuple):
+    """An S4Vectors::Rle: (runValue, runLength), with ``robj`` the R object (an rmini S4 object
+    with slots values / lengths) the shim sees -- one per Rle, as R's object identity."""
+
+    def __new__(cls, values, lengths, sh=None):
+        obj = super().__new__(cls, (values, lengths))
+        obj.robj = None if sh is None else sh.s4(values=np.asarray(values, np.int32) if np.asarray(values).dtype.kind
+                                                 in "iu" else np.asarray(values, np.float64),
+                                                 lengths=np.asarray(lengths, np.int32))
+        return obj
+
+
+# options(recoup.deviceRuns): calcCoverage's runs stay on the device beside the list (default TRUE)
+DEVICE_RUNS = True
+KEPT = []    # the handles the lists hold (R frees them when it collects the lists)
+PATHS = []   # .rcpProfileRle's choice per call: "device" (rcp_R_profile_cov) or "upload"
+
+
+def kept_alive(sh):
+    """Coverage handles still holding device runs (what R's garbage collector would release)."""
+    return sum(bool(sh.call("rcp_R_cov_alive", h)[0]) for h in KEPT)
+
+
+def rle_addresses(sh, cvrg):
+    """.Call("rcp_R_rle_addresses", cvrg)."""
+    return sh.call("rcp_R_rle_addresses", [getattr(x, "robj", None) for x in cvrg])
 
 
 def _rchar(names):
@@ -180,8 +211,14 @@ def rcp_coverage(sh, rs, rows, names=None):
             cov.append(None)
             continue
         a, b = int(res["runOff"][r]), int(res["runOff"][r + 1])
-        cov.append((res["values"][a:b], res["lengths"][a:b]))
-    return NamedList(cov, names)
+        cov.append(Rle(res["values"][a:b], res["lengths"][a:b], sh))
+    cov = NamedList(cov, names)
+    if DEVICE_RUNS:
+        cov.rcp_runs = dict(handle=res["handle"], addr=rle_addresses(sh, cov))
+        KEPT.append(res["handle"])
+    else:
+        sh.call("rcp_R_cov_free", res["handle"])
+    return cov
 
 
 class RStop(Exception):
@@ -298,13 +335,21 @@ INTERP = {"auto": 0, "spline": 1, "linear": 2, "neighborhood": 3}
 def rcp_profile_rle(sh, cvrg, where, flank, n_bins, per_base, stat="mean", interpolation="auto", rng_kind=0,
                     row_names=None):
     """.rcpProfileRle(cvrg, where, flank, nBins, perBase, stat, interpolation, rowNames): the
-    matrix (an rmini RArray carrying the dimnames the shim set)."""
+    matrix (an rmini RArray carrying the dimnames the shim set) -- from the runs still on the
+    device when the list is the one calcCoverage returned (its rcpRuns handle alive, its Rle
+    vectors at the recorded addresses), else from its Rle vectors uploaded."""
+    bin_args = [np.asarray(where, np.int32), np.asarray((0, 0) if flank is None else flank, np.int32),
+                np.asarray(n_bins, np.int32), np.asarray(per_base, np.int32), np.int32(STAT[stat]),
+                np.int32(INTERP[interpolation]), np.int32(rng_kind), 1.0]
+    h = getattr(cvrg, "rcp_runs", None)
+    if h is not None and sh.call("rcp_R_cov_alive", h["handle"])[0] and \
+            np.array_equal(rle_addresses(sh, cvrg), h["addr"]):
+        PATHS.append("device")
+        return sh.call("rcp_R_profile_cov", h["handle"], *bin_args, _rchar(row_names))["profile"]
+    PATHS.append("upload")
     a = rcp_rle_arrays(cvrg)
-    res = sh.call("rcp_R_profile_rle", a["runOff"], a["values"], a["lengths"], a["isNull"],
-                  np.asarray(where, np.int32), np.asarray((0, 0) if flank is None else flank, np.int32),
-                  np.asarray(n_bins, np.int32), np.asarray(per_base, np.int32), np.int32(STAT[stat]),
-                  np.int32(INTERP[interpolation]), np.int32(rng_kind), 1.0, np.asarray(rcp_devices(), np.int32),
-                  _rchar(row_names))
+    res = sh.call("rcp_R_profile_rle", a["runOff"], a["values"], a["lengths"], a["isNull"], *bin_args,
+                  np.asarray(rcp_devices(), np.int32), _rchar(row_names))
     return res["profile"]
 
 

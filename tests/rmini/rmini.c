@@ -28,7 +28,7 @@
 
 #include "Rinternals.h"
 
-enum { NILSXP = 0, CHARSXP = 9, EXTPTRSXP = 22 };
+enum { NILSXP = 0, CHARSXP = 9, S4SXP = 25 };
 
 struct SEXPREC {
     int type;
@@ -85,7 +85,8 @@ static size_t elt_size(int type) {
     case LGLSXP: return sizeof(int);
     case REALSXP: return sizeof(double);
     case STRSXP:
-    case VECSXP: return sizeof(SEXP);
+    case VECSXP:
+    case S4SXP: return sizeof(SEXP);
     case CHARSXP: return 1;
     default: return 0;
     }
@@ -411,6 +412,32 @@ int rmini_unguarded_handles(void) {
     int n = 0;
     for (int i = 0; i < n_ext; ++i) n += ext_tab[i]->addr != NULL && ext_tab[i]->fin == NULL;
     return n;
+}
+
+SEXP rmini_strings(int n, const char** c);
+
+/* S4 objects: named slots (a list of n SEXPs with a names vector); symbols are CHARSXPs */
+SEXP install(const char* name) { return mkChar(name); }
+int IS_S4_OBJECT(SEXP s) { return s->type == S4SXP; }
+static SEXP slot_of(SEXP obj, SEXP sym) {
+    if (obj->type != S4SXP || !obj->names) return NULL;
+    SEXP* slots = (SEXP*)obj->data;
+    SEXP* nm = (SEXP*)obj->names->data;
+    for (R_xlen_t i = 0; i < obj->len; ++i)
+        if (strcmp((const char*)nm[i]->data, (const char*)sym->data) == 0) return slots[i];
+    return NULL;
+}
+int R_has_slot(SEXP obj, SEXP sym) { return slot_of(obj, sym) != NULL; }
+SEXP R_do_slot(SEXP obj, SEXP sym) {
+    SEXP v = slot_of(obj, sym);
+    if (!v) Rf_error("no slot of name \"%s\" for this object", (const char*)sym->data);
+    return v;
+}
+SEXP rmini_s4(int n, const char** names, const SEXP* slots) {
+    SEXP s = new_obj(S4SXP, n);
+    for (int i = 0; i < n; ++i) ((SEXP*)s->data)[i] = slots[i];
+    s->names = rmini_strings(n, names);
+    return s;
 }
 
 SEXP rmini_vector(int type, R_xlen_t n, const void* src) {

@@ -101,6 +101,8 @@ class Shim:
         L.rmini_strings.restype = v
         L.rmini_strings.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
         L.rmini_nil.restype = v
+        L.rmini_s4.restype = v
+        L.rmini_s4.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(v)]
         L.rmini_fail_alloc_after.argtypes = [ctypes.c_long]
         assert L.rmini_init() == 0, "R_init_recoup registered no routines"
         self.L = L
@@ -131,6 +133,14 @@ class Shim:
             a, t = a.astype(np.float64), REALSXP
         a = np.ascontiguousarray(a.ravel(order="F"))
         return L.rmini_vector(t, a.size, a.ctypes.data if a.size else None)
+
+    def s4(self, **slots):
+        """An S4 object with these slots (e.g. an S4Vectors::Rle: values, lengths), made once: the
+        RObj passes the SAME R object to every later call (R's object identity)."""
+        names = [k.encode() for k in slots]
+        arr = (ctypes.c_char_p * max(len(names), 1))(*names)
+        vals = (ctypes.c_void_p * max(len(names), 1))(*[self.to_r(x) for x in slots.values()])
+        return RObj(self.L.rmini_s4(len(names), arr, vals))
 
     def from_r(self, p):
         L = self.L

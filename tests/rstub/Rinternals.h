@@ -2,7 +2,7 @@
 #ifndef RCP_RSTUB_RINTERNALS_H
 #define RCP_RSTUB_RINTERNALS_H
 #include "R.h"
-enum { INTSXP = 13, LGLSXP = 10, REALSXP = 14, STRSXP = 16, VECSXP = 19 };
+enum { INTSXP = 13, LGLSXP = 10, REALSXP = 14, STRSXP = 16, VECSXP = 19, EXTPTRSXP = 22 };
 extern SEXP R_NilValue, R_NamesSymbol, R_DimNamesSymbol;
 extern int R_NaInt;
 #define NA_INTEGER R_NaInt
@@ -32,6 +32,11 @@ void R_ClearExternalPtr(SEXP);
 void R_SetExternalPtrAddr(SEXP, void*);
 typedef void (*R_CFinalizer_t)(SEXP);
 void R_RegisterCFinalizerEx(SEXP, R_CFinalizer_t, int);
+/* S4 objects and their slots (S4Vectors::Rle: "values", "lengths") */
+SEXP install(const char*);
+int IS_S4_OBJECT(SEXP);
+int R_has_slot(SEXP, SEXP);
+SEXP R_do_slot(SEXP, SEXP);
 typedef void* (*DL_FUNC)(void);
 typedef struct { const char* name; DL_FUNC fun; int numArgs; } R_CallMethodDef;
 typedef struct _DllInfo DllInfo;

@@ -192,3 +192,37 @@ def test_coverage_rle_runs_across_sub_chunk_seams(gpu, seed, widths):
         v, ln = _runs(cov[r])
         np.testing.assert_array_equal(values[a:b], v)
         np.testing.assert_array_equal(lengths[a:b], ln)
+
+
+@pytest.mark.parametrize("devices", [None, (0, 0), (0, 0, 0)], ids=["one", "shards2", "shards3"])
+def test_profile_of_device_runs(gpu, devices):
+    """rcp_profile_cov: the profile of a calcCoverage result from the runs the handle keeps on the
+    device(s) -- one device, or shards whose blocks are in (chromosome, start) order, not the
+    caller's (rows placed back) -- bit-equal to rcp_profile_rle of the same runs copied to the
+    host and uploaded again: uniform and R-RNG bins, interpolated rows (flank / centre / flank
+    parts of unequal rows), per-base parts, median, NULL rows."""
+    from recoup_amd.engine import ReadSet, RowTable, Shards, coverage_rle_kept, profile_rle_arrays
+    from tests.test_gpu_rows import rna_rows
+    rng = np.random.default_rng(404)
+    reads = make_reads(rng, 200_000)
+    r0 = single_rows(rng, 900, 2000, edge=True)
+    r0.start[1], r0.end[1] = 1, 2000  # (a start at 0 shortens its row: not a per-base row of 2000)
+    perm = rng.permutation(900)
+    single = RowTable.from_ranges(r0.chrom[perm], r0.start[perm], r0.end[perm], r0.strand[perm])
+    cases = [(single, Bins([("whole", 200)])), (single, Bins([("whole", 300)])),
+             (single, Bins([("whole", 200)], stat="median")), (single, Bins([("whole", 0, 2000)])),
+             (rna_rows(rng, 200), Bins([("upstream", 50), ("center", 500), ("downstream", 50)], flank=(2000, 2000))),
+             (rna_rows(rng, 200), Bins([("upstream", 0, 2000), ("center", 300), ("downstream", 0, 2000)],
+                                       flank=(2000, 2000)))]
+    rs = ReadSet(*reads, CHROM_LEN, device=0)
+    for rows, bins in cases:
+        if devices is None:
+            kept = coverage_rle_kept(rs, rows)
+        else:
+            kept = Shards(*reads, CHROM_LEN, rows, list(devices)).coverage_rle_kept()
+        run_off, values, lengths, valid = kept.copy()
+        m, v = kept.profile(bins)
+        ref, rv = profile_rle_arrays(run_off, lengths, values, (valid == 0).astype(np.uint8), bins, 0)
+        np.testing.assert_array_equal(v, rv)
+        assert np.array_equal(np.asarray(m).view(np.uint64), np.asarray(ref).view(np.uint64)), (rows.n_rows, bins.n_cols)
+        kept.close()

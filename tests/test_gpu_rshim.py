@@ -74,7 +74,8 @@ def test_calc_coverage_of_a_split_list(sh, c1):
         for k in range(2):
             got = _decode(rm.calc_coverage(sh, rm.split_by_seqname(c1["reads"][k]), mask))
             _assert_cov_equal(got, _oracle_cov(c1["idx"][k], mask))
-    assert sh.live_handles() == 0  # every readset released (.rcpFree)
+    # every readset released (.rcpFree); the coverage lists' device runs live until R collects them
+    assert sh.live_handles() == rm.kept_alive(sh)
 
 
 def _assert_dimnames(m, want, what):
@@ -227,7 +228,7 @@ def test_profile_from_reads(sh, c1):
         np.testing.assert_allclose(one[k]["profile"], c1["gold"][f"tss_heat_s{k}"], rtol=MEAN_RTOL, atol=0)
         _assert_dimnames(one[k]["profile"], o.profile_dimnames(list(mask.names), (2000, 2000), bp, True), "reads")
         _assert_same_matrix(two[k]["profile"], one[k]["profile"], "two device slots vs one")
-    assert sh.live_handles() == 0
+    assert sh.live_handles() == rm.kept_alive(sh)
 
 
 def _same_coverage(a, b):
@@ -258,8 +259,10 @@ def test_recoup_path_on_several_devices(sh, c1, devs):
                 inp = rm.coverage_ref(sh, _inputs(c1), genes, region, (2000, 2000), sp)
             return rm.profile_matrix(sh, inp, (2000, 2000), bp)
         one = path()
+        rm.PATHS.clear()
         with _devices(devs):
             many = path()
+        assert "device" in rm.PATHS  # (the shards' coverage handle: parts on each device, in the caller's order)
         for a, b in zip(many, one):
             _same_coverage(a["coverage"], b["coverage"])
             _assert_same_matrix(a["profile"], b["profile"], f"{region}: {len(devs)} devices vs one")
@@ -281,7 +284,7 @@ def test_recoup_path_on_several_devices(sh, c1, devs):
                 rm.calc_coverage(sh, rs, other)
         finally:
             rm.rcp_free(sh, rs)
-    assert sh.live_handles() == 0
+    assert sh.live_handles() == rm.kept_alive(sh)
 
 
 def test_split_list_with_merged_seqinfo_and_strands(sh):
@@ -345,3 +348,57 @@ def test_library_errors_unwind_without_leaks(sh, c1):
     rm.rcp_free(sh, rs)
     sh.run_finalizers()
     assert sh.live_handles() == 0
+
+
+def test_profiles_from_device_runs(sh, c1):
+    """calcCoverage's runs stay on the GPU beside the list it returns (attr "rcpRuns": the handle
+    and the addresses of every Rle's vectors); profileMatrix and the forced heatmap pass profile
+    them there while the list is unchanged (R/recoup.R:551-597, :659-714), and upload the list's
+    own vectors otherwise: an element replaced (the attribute stays, an address differs), a
+    linear rescale (a new list, R/recoup.R:559-577), a handle released (save / load).  The same
+    bits every way."""
+    import copy
+    inp = rm.coverage_ref(sh, _inputs(c1), c1["genes"], "tss", (2000, 2000), {"strand": None, "ignoreStrand": True})
+    gold = c1["gold"]
+    bp = dict(flankBinSize=0, regionBinSize=0)
+    rm.PATHS.clear()
+    inp = rm.profile_matrix(sh, inp, (2000, 2000), bp)
+    heat = rm.ref_forced_heatmap(sh, inp, "tss", (2000, 2000), bp)
+    assert rm.PATHS and set(rm.PATHS) == {"device"}, rm.PATHS
+    for k, x in enumerate(inp):
+        np.testing.assert_array_equal(x["profile"], gold[f"tss_base_s{k}"].astype(np.float64))
+        np.testing.assert_allclose(heat[k], gold[f"tss_heat_s{k}"], rtol=MEAN_RTOL, atol=0)
+    cov = inp[0]["coverage"]
+    dev = rm.bin_coverage_matrix(sh, cov, 200)
+    # cov2[[i]] <- Rle(same runs): R keeps the list's attributes, the element is a new object
+    i = next(j for j, x in enumerate(cov) if x is not None)
+    cov2 = copy.copy(cov)
+    cov2[i] = rm.Rle(cov[i][0].copy(), cov[i][1].copy(), sh)
+    rm.PATHS.clear()
+    up = rm.bin_coverage_matrix(sh, cov2, 200)
+    assert rm.PATHS == ["upload"]
+    _assert_same_matrix(up, dev, "an element replaced: uploaded")
+    # a runValue changed in the copy: its profile differs where the value does
+    cov3 = copy.copy(cov)
+    cov3[i] = rm.Rle(cov[i][0] + 1, cov[i][1].copy(), sh)
+    assert not np.array_equal(rm.bin_coverage_matrix(sh, cov3, 200)[i], dev[i])
+    # lapply(cov, function(x) x * f): a new list without the attribute
+    scaled = rm.NamedList([None if x is None else rm.Rle(x[0] * 0.5, x[1], sh) for x in cov], cov.names)
+    rm.PATHS.clear()
+    half = rm.bin_coverage_matrix(sh, scaled, 200)
+    assert rm.PATHS == ["upload"]
+    np.testing.assert_allclose(half, 0.5 * dev, rtol=1e-15, atol=0)
+    # the handle released (what load() of a saved object leaves): uploaded
+    sh.call("rcp_R_cov_free", cov.rcp_runs["handle"])
+    rm.PATHS.clear()
+    _assert_same_matrix(rm.bin_coverage_matrix(sh, cov, 200), dev, "released handle: uploaded")
+    assert rm.PATHS == ["upload"]
+    # options(recoup.deviceRuns = FALSE): the runs are released at once
+    rm.DEVICE_RUNS = False
+    try:
+        n0 = rm.kept_alive(sh)
+        inp2 = rm.coverage_ref(sh, _inputs(c1), c1["genes"], "tss", (2000, 2000), {"strand": None, "ignoreStrand": True})
+        assert inp2[0]["coverage"].rcp_runs is None and rm.kept_alive(sh) == n0
+    finally:
+        rm.DEVICE_RUNS = True
+    assert sh.live_handles() == rm.kept_alive(sh)

@@ -615,10 +615,19 @@ def end_to_end(reads, seqlen, rows, bins, local, units, reps=3, rle=True):
     wv, wl = torch.unique_consecutive(sw, return_counts=True)
     ends = ((wv.cpu().numpy(), wl.to(torch.int64).cpu().numpy()) if wv.numel() <= sw.numel() // 4
             else end[order].cpu().numpy())
+    # the same reads in generation order, in the form r/R/rcp.R hands them over: one chromosome
+    # code per read (seqnames has about one run per read), the widths as runs when they are few
+    # (C4: one width), else one end per read
+    aw = (end - start + 1).to(torch.int32)
+    awv, awl = torch.unique_consecutive(aw, return_counts=True)
+    a_ends = ((awv.cpu().numpy(), awl.to(torch.int64).cpu().numpy()) if awv.numel() <= aw.numel() // 4
+              else end.cpu().numpy())
+    del aw, awv, awl
     forms = {
         "sorted_runs": [(rv.to(torch.int32).cpu().numpy(), rl.to(torch.int64).cpu().numpy()),
                         start[order].cpu().numpy(), ends, strand[order].cpu().numpy()],
-        "any_order": [x.cpu().numpy() for x in reads],
+        "any_order": [chrom.cpu().numpy(), start.cpu().numpy(), a_ends, strand.cpu().numpy()],
+        "any_order_ends": [x.cpu().numpy() for x in reads],
     }
     n_wruns = int(wv.numel()) if isinstance(ends, tuple) else None
     del order, sc, sw, wv, wl
@@ -643,6 +652,7 @@ def end_to_end(reads, seqlen, rows, bins, local, units, reps=3, rle=True):
     e2e = one_call(forms["sorted_runs"], seqlen, rows, bins, local, units, out, reps)
     e2e["two_calls"] = res["sorted_runs"]
     e2e["any_order"] = res["any_order"]
+    e2e["any_order_ends"] = res["any_order_ends"]
     e2e["samples_pipelined"] = samples_pipelined(forms["sorted_runs"], seqlen, rows, bins, local, units, out, reps)
     if rle:
         e2e["rle_path"] = rle_path(forms["sorted_runs"], seqlen, rows, bins, local, units, out, reps)
@@ -651,7 +661,8 @@ def end_to_end(reads, seqlen, rows, bins, local, units, reps=3, rle=True):
                    "(profileMatrixFromReads), reads coordinate-sorted with seqnames runs (a sorted BAM) and width "
                    "runs when few (width_runs: their count; null = per-read ends), streamed in row blocks; "
                    "two_calls: rcp_readset_create then rcp_profile (phases_ms); any_order: the two calls on "
-                   "unsorted reads, one code and one end per read")
+                   "unsorted reads as r/R/rcp.R hands them over (one chromosome code per read, width runs when "
+                   "few); any_order_ends: the same with one end per read")
     return e2e
 
 

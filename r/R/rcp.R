@@ -54,12 +54,16 @@
     })
     chrom <- list(unlist(lapply(sn, `[[`, 1), use.names = FALSE),
         unlist(lapply(sn, `[[`, 2), use.names = FALSE))
-    if (sum(chrom[[2]]) == 0)
-        chrom <- integer(0)
     # IRanges holds start and width: reads of a few lengths send width runs, not an end vector
     one <- length(input) == 1
     w <- Rle(if (one) width(input[[1]]) else unlist(lapply(input, width), use.names = FALSE))
     n <- length(w)
+    # reads in no particular order (recoup_test_data's are) have about one seqnames run per read:
+    # then one code per read (it travels as 16-bit offsets, 2 bytes a read, not 12 a run)
+    if (length(chrom[[1]]) > n %/% 4)
+        chrom <- rep.int(chrom[[1]], chrom[[2]])
+    else if (sum(chrom[[2]]) == 0)
+        chrom <- integer(0)
     ends <- if (n > 0 && nrun(w) <= n %/% 4)
         list(as.integer(runValue(w)), as.numeric(runLength(w))) else
         if (one) end(input[[1]]) else unlist(lapply(input, end), use.names = FALSE)

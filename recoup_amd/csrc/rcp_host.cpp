@@ -582,14 +582,33 @@ int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_reads
         HIP_TRY(in_strand.alloc(n));
         // caller-owned pageable arrays (R vectors): pinned double-buffered staging (rcp_stage.h),
         // coordinates as 16-bit offsets within blocks and strands four to a byte where they fit
-        if (d->chrom) HIP_TRY(rcp::stage_h2d_i32(in_chrom.as<int32_t>(), d->chrom, (size_t)n, d->device, s));
+        if (d->chrom)
+            HIP_TRY(rcp::stage_h2d_codes(in_chrom.as<int32_t>(), d->chrom, (size_t)n, d->n_chrom, d->device, s));
         HIP_TRY(rcp::stage_h2d_i32(in_start.as<int32_t>(), d->start, (size_t)n, d->device, s));
-        if (d->end) HIP_TRY(rcp::stage_h2d_i32(in_end.as<int32_t>(), d->end, (size_t)n, d->device, s));
+        // ends go up as widths (a block of them spans < 2^16 whatever the reads' order: 2 bytes a
+        // read where unsorted ends go raw) and are formed again on the device
+        bool widths = false;
+        if (d->end) {
+            bool unfit = false;
+            HIP_TRY(rcp::stage_h2d_width(in_end.as<int32_t>(), d->start, d->end, (size_t)n, d->device, s, &unfit));
+            if (unfit) HIP_TRY(rcp::stage_h2d_i32(in_end.as<int32_t>(), d->end, (size_t)n, d->device, s));
+            widths = !unfit;
+        }
         HIP_TRY(rcp::stage_h2d_strand(in_strand.as<int8_t>(), d->strand, (size_t)n, d->device, s));
         pc = in_chrom.as<int32_t>();
         ps = in_start.as<int32_t>();
         if (d->end) pe = in_end.as<int32_t>();
         pst = in_strand.as<int8_t>();
+        if (widths) {
+            PoolBuf over(s);
+            HIP_TRY(over.alloc(4));
+            HIP_TRY(hipMemsetAsync(over.p, 0, 4, s));
+            HIP_TRY(rcp_launch_width_end(n, ps, in_end.as<int32_t>(), over.as<uint32_t>(), s));
+            uint32_t h_over = 0;
+            HIP_TRY(hipMemcpyAsync(&h_over, over.p, 4, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (h_over) return fail(RCP_EINVAL, "internal: a read's end formed from its width overflows");
+        }
     }
     if (!d->end && n > 0) {
         // widths as runs: expanded on the device, end = start + width - 1 formed there

@@ -4328,6 +4328,40 @@ __global__ void __launch_bounds__(kBlock) rcp_unpack_strand_kernel(const uint8_t
     }
 }
 
+// chromosome codes one byte each (rcp_stage.cpp stage_h2d_codes): 255 -> -1 (the read is dropped)
+__global__ void __launch_bounds__(kBlock) rcp_unpack_code8_kernel(const uint8_t* __restrict__ src, int64_t n,
+                                                                  int32_t* __restrict__ dst) {
+    const int64_t i = 4 * ((int64_t)blockIdx.x * kBlock + threadIdx.x);
+    if (i >= n) return;
+    if (i + 4 <= n) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(src + i);
+        int4 v;
+        v.x = (int)(w & 255u);
+        v.y = (int)((w >> 8) & 255u);
+        v.z = (int)((w >> 16) & 255u);
+        v.w = (int)(w >> 24);
+        v.x = v.x == 255 ? -1 : v.x;
+        v.y = v.y == 255 ? -1 : v.y;
+        v.z = v.z == 255 ? -1 : v.z;
+        v.w = v.w == 255 ? -1 : v.w;
+        if ((reinterpret_cast<uintptr_t>(dst + i) & 15) == 0) {
+            *reinterpret_cast<int4*>(dst + i) = v;
+        } else {
+            dst[i] = v.x; dst[i + 1] = v.y; dst[i + 2] = v.z; dst[i + 3] = v.w;
+        }
+        return;
+    }
+    for (int64_t j = i; j < n; ++j) dst[j] = src[j] == 255 ? -1 : (int32_t)src[j];
+}
+
+extern "C" hipError_t rcp_launch_unpack_code8(const void* src, int64_t n, int32_t* dst, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const int64_t quads = (n + 3) / 4;
+    hipLaunchKernelGGL(rcp_unpack_code8_kernel, dim3((unsigned)((quads + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       stream, static_cast<const uint8_t*>(src), n, dst);
+    return hipGetLastError();
+}
+
 extern "C" int rcp_pack_block(void) { return kPackBlock; }
 
 extern "C" hipError_t rcp_launch_unpack_i32(const void* src, int64_t n, int32_t* dst, hipStream_t stream) {

@@ -16,22 +16,11 @@ static inline uint32_t rcp_pack_strand8(uint64_t w) {
     return (uint32_t)x;
 }
 
-// one block of int32 values as 16-bit offsets from a base: the first value when every value is
-// within 2^16 above it (coordinate-sorted starts), else the minimum when the span allows; 0: the
-// block does not fit (sent raw)
+// one block of int32 values as 16-bit offsets from their minimum when the block spans < 2^16
+// (coordinate-sorted starts, chromosome codes, read widths: nearly every block); 0: the block
+// does not fit (sent raw).  Two passes: the min / max reduction, then the offsets.
 static inline int rcp_pack_block16(const int32_t* v, int len, uint16_t* off, int32_t* base) {
-    int32_t lo = v[0];
-    uint32_t bad = 0;
-    for (int j = 0; j < len; ++j) {
-        const uint32_t o = (uint32_t)v[j] - (uint32_t)lo;
-        bad |= o;
-        off[j] = (uint16_t)o;
-    }
-    if ((bad >> 16) == 0) {
-        *base = lo;
-        return 1;
-    }
-    int32_t hi = v[0];
+    int32_t lo = v[0], hi = v[0];
     for (int j = 1; j < len; ++j) {
         lo = v[j] < lo ? v[j] : lo;
         hi = v[j] > hi ? v[j] : hi;
@@ -40,4 +29,11 @@ static inline int rcp_pack_block16(const int32_t* v, int len, uint16_t* off, int
     for (int j = 0; j < len; ++j) off[j] = (uint16_t)((uint32_t)v[j] - (uint32_t)lo);
     *base = lo;
     return 1;
+}
+
+// chromosome codes one byte each: a code in [0, n_codes) as itself, any other (R's NA from
+// match(), a level the readset does not hold) as 255 -- the device restores -1 for it, which
+// drops the read as the code did (n_codes <= 255)
+static inline uint8_t rcp_pack_code8(int32_t c, int32_t n_codes) {
+    return (uint32_t)c < (uint32_t)n_codes ? (uint8_t)c : (uint8_t)255;
 }

@@ -30,6 +30,7 @@ extern "C" {
 int rcp_pack_block(void);
 hipError_t rcp_launch_unpack_i32(const void* src, int64_t n, int32_t* dst, hipStream_t stream);
 hipError_t rcp_launch_unpack_strand(const void* src, int64_t n, int8_t* dst, hipStream_t stream);
+hipError_t rcp_launch_unpack_code8(const void* src, int64_t n, int32_t* dst, hipStream_t stream);
 hipError_t rcp_launch_pack_i32(const int32_t* src, int64_t n, void* dst, hipStream_t stream);
 }
 
@@ -343,16 +344,22 @@ hipError_t h2d_packed(Stager* st, size_t n, size_t per_chunk, hipStream_t stream
 }
 }  // namespace
 
-hipError_t stage_h2d_i32(int32_t* dst, const int32_t* src, size_t n, int device, hipStream_t stream) {
+namespace {
+
+// The packed upload of n int32 values a .. a + len - 1 of which `fill(tmp, a, len, &ok)` returns
+// (the caller's array itself, or values it forms into tmp on the way: read widths; ok false: a
+// value it cannot form).  A chunk whose
+// first blocks are mostly raw (unsorted coordinates: no block spans < 2^16) goes plain at once
+// rather than after half its blocks were copied into the raw area.  *unfit (may be NULL) is set
+// when fill reports a value it cannot form (returns false): nothing usable was sent then.
+hipError_t h2d_i32_from(int32_t* dst, size_t n, int device, hipStream_t stream, const char* what,
+                        const std::function<const int32_t*(int32_t* tmp, size_t a, size_t len, bool* ok)>& fill,
+                        bool* unfit) {
     Stager* st = stager(device, 0);
-    if (n < kPackMin || !st) return stage_h2d(dst, src, 4 * n, device, stream);
     std::unique_lock<std::mutex> g(st->mu);
-    if (!ready(st, 0) || !ready_dev(st, device)) {
-        g.unlock();
-        return stage_h2d(dst, src, 4 * n, device, stream);
-    }
     const size_t B = (size_t)rcp_pack_block();
     const size_t per_chunk = kChunk / 4;  // values: a plain chunk fills the buffer
+    std::atomic<bool> bad_value{false};
     auto encode = [&](char* pin, size_t a0, size_t m, bool* plain) -> size_t {
         const size_t nb = (m + B - 1) / B;
         int32_t* base = reinterpret_cast<int32_t*>(pin);
@@ -362,36 +369,60 @@ hipError_t stage_h2d_i32(int32_t* dst, const int32_t* src, size_t n, int device,
         const size_t cap = (kChunk - (size_t)(raw - pin)) / (4 * B);
         std::atomic<size_t> n_raw{0};
         std::atomic<bool> over{false};
-        const int32_t* s = src + a0;
-        st->pool->run(kParts, [&](int i) {
+        // probe: the chunk's first 16 blocks
+        {
+            alignas(16) int32_t v[1024];
             alignas(16) uint16_t tmp[1024 + 8];
-            const size_t b0 = nb * (size_t)i / kParts, b1 = nb * (size_t)(i + 1) / kParts;
-            for (size_t b = b0; b < b1 && !over.load(std::memory_order_relaxed); ++b) {
-                const size_t j0 = b * B, len = std::min(B, m - j0);
-                const int32_t* v = s + j0;
+            size_t probe_raw = 0;
+            const size_t np = std::min<size_t>(16, nb);
+            for (size_t b2 = 0; b2 < np; ++b2) {
+                const size_t j0 = b2 * B, len = std::min(B, m - j0);
                 int32_t lo = 0;
-                if (rcp_pack_block16(v, (int)len, tmp, &lo)) {
-                    base[b] = lo;
-                    slot[b] = -1;
-                    copy_nt(reinterpret_cast<char*>(off + j0), reinterpret_cast<const char*>(tmp), 2 * len);
-                } else {
-                    const size_t q = n_raw.fetch_add(1, std::memory_order_relaxed);
-                    if (q >= cap) {
-                        over.store(true, std::memory_order_relaxed);
-                        break;
-                    }
-                    base[b] = 0;
-                    slot[b] = (int32_t)q;
-                    copy_nt(raw + 4 * B * q, reinterpret_cast<const char*>(v), 4 * len);
-                }
+                bool ok = true;
+                const int32_t* pv = fill(v, a0 + j0, len, &ok);
+                if (!ok) bad_value.store(true);
+                if (!rcp_pack_block16(pv, (int)len, tmp, &lo)) ++probe_raw;
             }
-        });
+            if (np >= 8 && probe_raw * 4 >= np * 3) over.store(true);
+        }
+        if (!over.load())
+            st->pool->run(kParts, [&](int i) {
+                alignas(16) int32_t v[1024];
+                alignas(16) uint16_t tmp[1024 + 8];
+                const size_t b0 = nb * (size_t)i / kParts, b1 = nb * (size_t)(i + 1) / kParts;
+                for (size_t b = b0; b < b1 && !over.load(std::memory_order_relaxed); ++b) {
+                    const size_t j0 = b * B, len = std::min(B, m - j0);
+                    bool ok = true;
+                    const int32_t* pv = fill(v, a0 + j0, len, &ok);
+                    if (!ok) bad_value.store(true, std::memory_order_relaxed);
+                    int32_t lo = 0;
+                    if (rcp_pack_block16(pv, (int)len, tmp, &lo)) {
+                        base[b] = lo;
+                        slot[b] = -1;
+                        copy_nt(reinterpret_cast<char*>(off + j0), reinterpret_cast<const char*>(tmp), 2 * len);
+                    } else {
+                        const size_t q = n_raw.fetch_add(1, std::memory_order_relaxed);
+                        if (q >= cap) {
+                            over.store(true, std::memory_order_relaxed);
+                            break;
+                        }
+                        base[b] = 0;
+                        slot[b] = (int32_t)q;
+                        copy_nt(raw + 4 * B * q, reinterpret_cast<const char*>(pv), 4 * len);
+                    }
+                }
+            });
         if (over.load()) {  // too many raw blocks: the chunk as it is
             *plain = true;
             st->pool->run(kParts, [&](int i) {
                 size_t a, z;
-                part_range(4 * m, i, &a, &z);
-                if (z > a) copy_nt(pin + a, reinterpret_cast<const char*>(s) + a, z - a);
+                part_range(m, i, &a, &z);
+                if (z <= a) return;
+                int32_t* out = reinterpret_cast<int32_t*>(pin) + a;
+                bool ok = true;
+                const int32_t* pv = fill(out, a0 + a, z - a, &ok);
+                if (!ok) bad_value.store(true, std::memory_order_relaxed);
+                if (pv != out) copy_nt(reinterpret_cast<char*>(out), reinterpret_cast<const char*>(pv), 4 * (z - a));
             });
             return 4 * m;
         }
@@ -403,7 +434,93 @@ hipError_t stage_h2d_i32(int32_t* dst, const int32_t* src, size_t n, int device,
         if (e == hipSuccess) e = rcp_launch_unpack_i32(dev, (int64_t)m, dst + a0, s);
         return e;
     };
-    return h2d_packed(st, n, per_chunk, stream, "i32", encode, land);
+    const hipError_t e = h2d_packed(st, n, per_chunk, stream, what, encode, land);
+    if (unfit) *unfit = bad_value.load();
+    return e;
+}
+
+bool packed_ready(Stager* st, int device) {  // (under st->mu)
+    return ready(st, 0) && ready_dev(st, device);
+}
+
+}  // namespace
+
+hipError_t stage_h2d_i32(int32_t* dst, const int32_t* src, size_t n, int device, hipStream_t stream) {
+    Stager* st = stager(device, 0);
+    if (n < kPackMin || !st) return stage_h2d(dst, src, 4 * n, device, stream);
+    {
+        std::unique_lock<std::mutex> g(st->mu);
+        if (!packed_ready(st, device)) {
+            g.unlock();
+            return stage_h2d(dst, src, 4 * n, device, stream);
+        }
+    }
+    return h2d_i32_from(dst, n, device, stream, "i32",
+                        [&](int32_t*, size_t a, size_t, bool*) -> const int32_t* { return src + a; }, nullptr);
+}
+
+hipError_t stage_h2d_width(int32_t* dst, const int32_t* start, const int32_t* end, size_t n, int device,
+                           hipStream_t stream, bool* unfit) {
+    *unfit = false;
+    Stager* st = stager(device, 0);
+    bool packed = n >= kPackMin && st;
+    if (packed) {
+        std::unique_lock<std::mutex> g(st->mu);
+        packed = packed_ready(st, device);
+    }
+    if (!packed) {
+        // (few reads, or no landing buffers): the widths formed here, sent as they are
+        std::vector<int32_t> w(n);
+        for (size_t i = 0; i < n; ++i) {
+            const int64_t x = (int64_t)end[i] - (int64_t)start[i] + 1;
+            if (x < INT32_MIN || x > INT32_MAX) {
+                *unfit = true;
+                return hipSuccess;
+            }
+            w[i] = (int32_t)x;
+        }
+        return stage_h2d(dst, w.data(), 4 * n, device, stream);
+    }
+    return h2d_i32_from(dst, n, device, stream, "width",
+                        [&](int32_t* out, size_t a, size_t len, bool* ok) -> const int32_t* {
+                            bool good = true;
+                            for (size_t j = 0; j < len; ++j) {
+                                const int64_t x = (int64_t)end[a + j] - (int64_t)start[a + j] + 1;
+                                good = good && x >= INT32_MIN && x <= INT32_MAX;
+                                out[j] = (int32_t)x;
+                            }
+                            *ok = good;
+                            return out;
+                        },
+                        unfit);
+}
+
+hipError_t stage_h2d_codes(int32_t* dst, const int32_t* src, size_t n, int32_t n_codes, int device,
+                           hipStream_t stream) {
+    Stager* st = stager(device, 0);
+    if (n < kPackMin || !st || n_codes > 255) return stage_h2d_i32(dst, src, n, device, stream);
+    std::unique_lock<std::mutex> g(st->mu);
+    if (!packed_ready(st, device)) {
+        g.unlock();
+        return stage_h2d_i32(dst, src, n, device, stream);
+    }
+    const size_t per_chunk = kChunk;  // codes: one byte each
+    auto encode = [&](char* pin, size_t a0, size_t m, bool*) -> size_t {
+        const int32_t* s0 = src + a0;
+        uint8_t* o = reinterpret_cast<uint8_t*>(pin);
+        st->pool->run(kParts, [&](int i) {
+            size_t a, z;
+            part_range(m, i, &a, &z);
+            for (size_t j = a; j < z; ++j) o[j] = rcp_pack_code8(s0[j], n_codes);
+        });
+        return m;
+    };
+    auto land = [&](const char* dev, char* pin, size_t a0, size_t m, size_t bytes, bool, hipStream_t s) {
+        hipError_t e = hipMemcpyAsync(const_cast<char*>(dev), pin, bytes, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = rcp_launch_unpack_code8(dev, (int64_t)m, dst + a0, s);
+        return e;
+    };
+    return h2d_packed(st, n, per_chunk, stream, "codes", encode, land);
 }
 
 hipError_t stage_h2d_strand(int8_t* dst, const int8_t* src, size_t n, int device, hipStream_t stream) {

@@ -34,6 +34,15 @@ double trace_ms();  // a steady clock in ms
 // into dst.  Below 2^20 values, or without the device landing buffers: the plain staged copy.
 hipError_t stage_h2d_i32(int32_t* dst, const int32_t* src, size_t n, int device, hipStream_t stream);
 hipError_t stage_h2d_strand(int8_t* dst, const int8_t* src, size_t n, int device, hipStream_t stream);
+// Chromosome codes one byte each when n_codes <= 255 (a code outside [0, n_codes) arrives as -1
+// and still drops its read), else as stage_h2d_i32.
+hipError_t stage_h2d_codes(int32_t* dst, const int32_t* src, size_t n, int32_t n_codes, int device,
+                           hipStream_t stream);
+// Read widths end[i] - start[i] + 1 formed on the way and sent packed (a block's widths span far
+// less than 2^16 whatever the reads' order, where unsorted ends would go raw) into dst.  *unfit:
+// a width outside int32 (nothing usable sent: the caller uploads the ends instead).
+hipError_t stage_h2d_width(int32_t* dst, const int32_t* start, const int32_t* end, size_t n, int device,
+                           hipStream_t stream, bool* unfit);
 // ... and down (Rle runs): blocks packed on the device as their first value + 16-bit offsets,
 // expanded by the copy threads; blocks that do not fit are copied as they are
 hipError_t stage_d2h_i32(int32_t* dst, const int32_t* src, size_t n, int device, hipStream_t stream);

@@ -55,6 +55,15 @@ int main(void) {
         if (fits)
             for (int j = 0; j < len; ++j) bad += (int32_t)((uint32_t)base + off[j]) != v[j];
     }
+    /* chromosome codes one byte each: in-range codes as themselves, any other as 255 (the
+     * device's -1: the read is dropped, as the code would drop it) */
+    for (int32_t nc = 1; nc <= 255; nc += 17)
+        for (long t = 0; t < 20000; ++t) {
+            const int32_t c = t < 600 ? (int32_t)t - 300 : (int32_t)next();
+            const uint8_t b = rcp_pack_code8(c, nc);
+            const int32_t back = b == 255 ? -1 : (int32_t)b;
+            bad += (c >= 0 && c < nc) ? back != c : back != -1;
+        }
     printf("%ld\n", bad);
     return bad != 0;
 }

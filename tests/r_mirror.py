@@ -119,11 +119,13 @@ def rcp_read_args(inp, levels=None):
         rl.append(l)
     chrom = [np.concatenate(rv).astype(np.int32) if rv else np.zeros(0, np.int32),
              np.concatenate(rl).astype(np.float64) if rl else np.zeros(0)]
-    if chrom[1].sum() == 0:
-        chrom = np.zeros(0, np.int32)
     width = np.concatenate([g.width for g in inp]).astype(np.int32) if inp else np.zeros(0, np.int32)
     wv, wl = rle(width)
     n = width.size
+    if len(chrom[0]) > n // 4:  # about a run per read (unsorted): one code per read
+        chrom = np.repeat(chrom[0], chrom[1].astype(np.int64)).astype(np.int32)
+    elif chrom[1].sum() == 0:
+        chrom = np.zeros(0, np.int32)
     if n > 0 and wv.size <= n // 4:
         ends = [wv.astype(np.int32), wl.astype(np.float64)]
     else:

@@ -1539,6 +1539,11 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         while (P.rounds > 1 &&
                (int64_t)((R + tile * P.rounds - 1) / (tile * P.rounds)) * P.n_chunks_total < 2 * (int64_t)cus)
             P.rounds /= 2;
+        // (RCP_GEN_ROUNDS: diagnostics A/B of the rounds per workgroup, 1 / 2 / 4)
+        if (const char* e = std::getenv("RCP_GEN_ROUNDS")) {
+            const int v = std::atoi(e);
+            if (v == 1 || v == 2 || v == 4) P.rounds = std::min(v, rmax);
+        }
         plan->tile_rows = P.lean == 4 ? tile : (P.lean ? (P.lean_rounds == 2 ? 2 * tile : rcp_tile_rows()) : tile * P.rounds);
     }
     plan->grid = (int64_t)((R + plan->tile_rows - 1) / plan->tile_rows) * P.n_chunks_total;

@@ -1252,6 +1252,20 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         }
         P.fold = f ? 1 : 0;
     }
+    // ---- per-base lean plans of small tables in the merged layout (one GPU's shard of a per-base
+    // table: C5 1/8 spent locate 45 us ahead of a 143-us pileup): the store wave that claims an
+    // item searches its rows' read ranges while the pile waves work on the previous item -- no
+    // locate launch.  (Binned lean plans keep the locate: their skewed rows need the heavy slices.)
+    if (P.lean == 1 && P.lean_rounds == 2 && rows->ignore_strand && opts->heavy_threshold <= 0 &&
+        B.interp_row.empty() && R > 0 && R <= kFoldMaxRows && !std::getenv("RCP_NO_LEAN_FOLD")) {
+        bool f = true;
+        for (int r = 0; f && r < R; ++r) {
+            const int32_t j0 = B.row_seg[r], j1 = B.row_seg[r + 1];
+            if (B.row_static[r] || j1 == j0) continue;
+            if (j1 - j0 > 1 || B.segs[j0].multi || !B.segs[j0].query_ok) f = false;
+        }
+        P.fold = f ? 1 : 0;
+    }
     // (RCP_COOP_MIN: diagnostics A/B of the cooperative rows' threshold)
     P.coop_min = std::getenv("RCP_COOP_MIN") ? std::max(0, std::atoi(std::getenv("RCP_COOP_MIN"))) : kCoopMin;
     // ---- lean plans with few row tiles (one GPU's shard of a region table): the persistent
@@ -1406,7 +1420,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     if (hipDeviceGetAttribute(&lpt_cus, hipDeviceAttributeMultiprocessorCount, rs->device) != hipSuccess || lpt_cus <= 0)
         lpt_cus = 256;
     // (a full per-base table, e.g. C5's 6256 items, keeps the per-XCD order and its L2 locality)
-    P.lpt = P.lean == 1 && P.lean_rounds == 2 && keep_crange && R > 0 &&
+    P.lpt = P.lean == 1 && P.lean_rounds == 2 && keep_crange && R > 0 && !P.fold &&
             lpt_items <= (int64_t)kLeanItemsPerWgBase * 2 * lpt_cus;
     P.lpt_cap = P.lpt ? (int32_t)lpt_items : 0;
     const size_t w_order = al(w_crange + (keep_crange ? sizeof(uint2) * 3 * (size_t)P.n_chunks_total * Rw : 0));

@@ -1490,13 +1490,139 @@ __device__ __forceinline__ RowMeta decode_row(const RcpPlanDev& P, const RcpPart
     return m;
 }
 
+
+// Fold plans (P.fold; rcp_host.cpp sets it for small single-range tables in the merged layout):
+// the locate kernel's work for row r and one column chunk done by the pileup kernel itself --
+// four bound searches per row: (0, 1) the row's lower / upper bound, for the row hit and the NULL
+// rules (R/coverage.R:189-225), (2, 3) the chunk piece's, i.e. its candidate reads (the locate
+// kernel's crange).  No locate launch and no 64-B record round trip.  fold_geom is the part before
+// the searches (the chunk's slice of the row and its genomic piece), fold_finish the part after
+// (validity, written by the row's first lane in chunk 0, and the row's metadata).
+struct FoldRow {
+    RcpRowInfo ri;
+    RowMeta m;
+    bool in, ok, pile, piece;
+    int32_t L, n, gps, gpe;
+};
+
+__device__ __forceinline__ void fold_geom(const RcpPlanDev& P, const RcpPart& part, int32_t k0, int r, FoldRow& f) {
+    RowMeta& m = f.m;
+    m.flag = 2; m.bs = 0; m.lay = -1; m.P0 = 0; m.npos = 0; m.kend = k0; m.heavy = -1; m.fast = 0;
+    m.off = m.slo = m.shi = m.rev = m.gps = m.gpe = 0;
+    for (int s = 0; s < 3; ++s) m.lo[s] = m.hi[s] = 0;
+    f.in = r < P.n_rows;
+    {
+        uint4* d = reinterpret_cast<uint4*>(&f.ri);
+        const uint4* src = reinterpret_cast<const uint4*>(P.row_info + (f.in ? r : 0));
+#pragma unroll
+        for (int u = 0; u < (int)(sizeof(RcpRowInfo) / 16); ++u) d[u] = f.in ? src[u] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    const RcpRowInfo& ri = f.ri;
+    const RcpSeg& sg = ri.seg0;
+    f.ok = f.in && !ri.stat && ri.chrom >= 0 && ri.chrom < P.n_chrom && ri.j1 == ri.j0 + 1 && sg.query_ok &&
+           (sg.streams & 1);
+    // the chunk's slice of the row (decode_row)
+    int32_t head = 0;
+    rcp_part_slice(part, ri.row_len, &head, &f.L);
+    f.n = part.n_bins;
+    m.kend = min(k0 + part.chunk_bins, f.n);
+    f.pile = false;
+    if (f.in && k0 < f.n && !(!part.per_base && f.L < f.n)) {
+        if (part.per_base && f.L != f.n) {
+            m.flag = 1;  // (a width mismatch: raised by fold_finish when the row is valid)
+        } else {
+            f.pile = true;
+            if (part.per_base) {
+                m.bs = 1;
+            } else {
+                m.bs = f.L / f.n;
+                const int32_t dif = f.L - m.bs * f.n;
+                if (dif) {
+                    m.lay = P.lay_index[part.lay_base + dif];
+                    if (m.lay < 0) m.lay = -1;
+                }
+            }
+            const int32_t e0 = bin_edge(m.bs, m.lay, P.lay_cnt, k0);
+            const int32_t e1 = bin_edge(m.bs, m.lay, P.lay_cnt, m.kend);
+            m.P0 = head + e0;
+            m.npos = e1 - e0;
+        }
+    }
+    // the chunk's genomic piece of the range
+    const int32_t len = sg.hi - sg.lo + 1;
+    const int32_t a = max(m.P0, sg.off), b = min(m.P0 + m.npos, sg.off + len);
+    f.piece = f.pile && a < b;
+    f.gps = f.gpe = 0;
+    if (f.piece) {
+        if (!sg.rev) {
+            f.gps = sg.lo + (a - sg.off);
+            f.gpe = sg.lo + (b - 1 - sg.off);
+        } else {
+            f.gpe = sg.hi - (a - sg.off);
+            f.gps = sg.hi - (b - 1 - sg.off);
+        }
+    }
+}
+
+// first: the lane that writes the row's validity and raises its status bits; coop_min: chunks of
+// more candidate reads (fused-bins rows) are marked heavy = -2 -- the general kernel's workgroup
+// piles them together (coop_row) -- or 0: never
+template <bool MEDIAN>
+__device__ __forceinline__ RowMeta fold_finish(const RcpPlanDev& P, const RcpPart& part, int cidx, int r, FoldRow& f,
+                                               uint32_t rlo, uint32_t rhi, uint32_t plo, uint32_t phi, bool first,
+                                               uint32_t coop_min) {
+    RowMeta& m = f.m;
+    const RcpRowInfo& ri = f.ri;
+    const RcpSeg& sg = ri.seg0;
+    rhi = max(rlo, rhi);
+    bool valid = f.ok && rlo < rhi;
+    // Rle[i2k] past the Rle -> NULL: seqlength, or the hits' last end when NA (locate_rows)
+    if (valid) valid = ri.seqlen >= 0 ? (int64_t)sg.hi <= ri.seqlen : sg.hi <= P.pmax[rhi - 1];
+    if (f.in && first && cidx == 0) {
+        P.valid[r] = valid ? 1 : 0;
+        if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
+    }
+    if (!f.in) return m;
+    if (!valid) {
+        m.flag = 1;  // NULL row -> zeros (profile.R:191-197)
+        return m;
+    }
+    if (!f.pile) {
+        if (m.flag == 1 && first) atomicOr(P.status, RCP_STATUS_WIDTH);  // per-base width mismatch
+        return m;
+    }
+    if (m.lay < 0 && !part.per_base && f.L - m.bs * f.n != 0) {
+        if (first) atomicOr(P.status, RCP_STATUS_INTERP);
+    }
+    m.flag = 0;
+    if (MEDIAN && m.bs + (m.lay >= 0 ? 1 : 0) > P.chunk_cap) {
+        m.flag = 2;
+        return m;
+    }
+    if (m.npos <= P.chunk_cap) {
+        m.fast = 1;
+        m.off = sg.off; m.slo = sg.lo; m.shi = sg.hi; m.rev = sg.rev;
+        if (f.piece) {
+            m.gps = f.gps;
+            m.gpe = f.gpe;
+            const uint32_t clo = max(rlo, plo);
+            m.lo[0] = clo;
+            m.hi[0] = max(clo, min(rhi, phi));
+            const int need = (m.npos + 1 + 63) >> 6;
+            const int per = need <= 4 ? 4 : 1 << (32 - __clz(need - 1));
+            const bool fused = !MEDIAN && m.lay < 0 && (m.bs & (m.bs - 1)) == 0 && m.bs <= per && per <= 16;
+            if (coop_min && fused && m.hi[0] - m.lo[0] > coop_min) m.heavy = -2;
+        }
+    }
+    return m;
+}
+
 // A bound search (dir_bound_multi: lower_bound(pmax >= v) or, up, upper_bound(start > v),
 // inside v's bucket of the directory at entry d0, nb buckets) by a group of G consecutive lanes
 // of one wave (G divides 64, group-aligned): after the bucket's directory line, each step probes G
 // points at once and keeps the (G + 1)-th of the interval holding the answer -- log_{G+1} of the
-// bucket's reads in dependent loads instead of log_2 (a hot peak's bucket holds thousands of
-// reads: 10 bisection steps -> 4 or 5).  Returns the same index as the bisection, in every lane
-// of the group.
+// bucket's reads in dependent loads instead of log_2.  Returns the same index as the bisection, in
+// every lane of the group.
 template <int G>
 __device__ __forceinline__ uint32_t dir_bound_group(const RcpPlanDev& P, int64_t d0, int32_t nb, int32_t v, bool up,
                                                     bool active) {
@@ -1552,124 +1678,41 @@ __device__ __forceinline__ uint32_t dir_bound_group(const RcpPlanDev& P, int64_t
     return lo;
 }
 
-// Fold plans (P.fold, general kernel; rcp_host.cpp sets it for small single-range tables in the
-// merged layout): the locate kernel's work for row r and this workgroup's column chunk, done by
-// the 4 G lanes of the row (G = 512 / (4 x the workgroup's rows): the whole workgroup) -- search s
-// of the row by lanes 4 s' .. : (0, 1) the row's lower / upper bound, for the row hit and the NULL
-// rules (R/coverage.R:189-225), (2, 3) the chunk piece's, i.e. its candidate reads (the locate
-// kernel's crange), each a G-lane search (dir_bound_group).  No locate launch and no 64-B record
-// round trip.  Every lane returns the row's metadata; the row's first lane in chunk 0 writes its
-// validity.  A fused-bins row with more than coop_min candidate reads in the chunk is marked
-// heavy = -2: the whole workgroup piles it (coop_row).
+// The general kernel's fold: the 4 G lanes of the row (G = 512 / (4 x the workgroup's rows): the
+// whole workgroup), search s by lanes G s .. G s + G - 1 (dir_bound_group); skewed fused-bins
+// chunks marked for the workgroup (P.coop_min)
 template <bool MEDIAN, int G>
 __device__ __forceinline__ RowMeta fold_row(const RcpPlanDev& P, const RcpPart& part, int32_t k0, int cidx, int r) {
     const int lane = threadIdx.x & 63;
     const int rbase = lane & ~(4 * G - 1);  // the row's first lane
     const int q = (lane - rbase) / G;       // its search
-    RowMeta m;
-    m.flag = 2; m.bs = 0; m.lay = -1; m.P0 = 0; m.npos = 0; m.kend = k0; m.heavy = -1; m.fast = 0;
-    m.off = m.slo = m.shi = m.rev = m.gps = m.gpe = 0;
-    for (int s = 0; s < 3; ++s) m.lo[s] = m.hi[s] = 0;
-    const bool in = r < P.n_rows;
-    RcpRowInfo ri;
-    {
-        uint4* d = reinterpret_cast<uint4*>(&ri);
-        const uint4* src = reinterpret_cast<const uint4*>(P.row_info + (in ? r : 0));
-#pragma unroll
-        for (int u = 0; u < (int)(sizeof(RcpRowInfo) / 16); ++u) d[u] = in ? src[u] : make_uint4(0u, 0u, 0u, 0u);
-    }
-    const RcpSeg sg = ri.seg0;
-    const bool ok = in && !ri.stat && ri.chrom >= 0 && ri.chrom < P.n_chrom && ri.j1 == ri.j0 + 1 && sg.query_ok &&
-                    (sg.streams & 1);
-    // the chunk's slice of the row (decode_row)
-    int32_t head = 0, L = 0;
-    rcp_part_slice(part, ri.row_len, &head, &L);
-    const int32_t n = part.n_bins;
-    m.kend = min(k0 + part.chunk_bins, n);
-    bool pile = false;
-    if (in && k0 < n && !(!part.per_base && L < n)) {
-        if (part.per_base && L != n) {
-            m.flag = 1;  // (a width mismatch: raised below when the row is valid)
-        } else {
-            pile = true;
-            if (part.per_base) {
-                m.bs = 1;
-            } else {
-                m.bs = L / n;
-                const int32_t dif = L - m.bs * n;
-                if (dif) {
-                    m.lay = P.lay_index[part.lay_base + dif];
-                    if (m.lay < 0) m.lay = -1;
-                }
-            }
-            const int32_t e0 = bin_edge(m.bs, m.lay, P.lay_cnt, k0);
-            const int32_t e1 = bin_edge(m.bs, m.lay, P.lay_cnt, m.kend);
-            m.P0 = head + e0;
-            m.npos = e1 - e0;
-        }
-    }
-    // the chunk's genomic piece of the range
-    const int32_t len = sg.hi - sg.lo + 1;
-    const int32_t a = max(m.P0, sg.off), b = min(m.P0 + m.npos, sg.off + len);
-    const bool piece = pile && a < b;
-    int32_t gps = 0, gpe = 0;
-    if (piece) {
-        if (!sg.rev) {
-            gps = sg.lo + (a - sg.off);
-            gpe = sg.lo + (b - 1 - sg.off);
-        } else {
-            gpe = sg.hi - (a - sg.off);
-            gps = sg.hi - (b - 1 - sg.off);
-        }
-    }
-    // the row's four searches, G lanes each
-    const int32_t v = q == 0 ? sg.lo : (q == 1 ? sg.hi : (q == 2 ? gps : gpe));
-    const uint32_t res = dir_bound_group<G>(P, ri.d0, ri.nb, v, (q & 1) != 0, ok && (q < 2 || piece));
-    const uint32_t rlo = (uint32_t)__shfl((int)res, rbase);
-    const uint32_t rhi = max(rlo, (uint32_t)__shfl((int)res, rbase + G));
-    const uint32_t plo = (uint32_t)__shfl((int)res, rbase + 2 * G);
-    const uint32_t phi = (uint32_t)__shfl((int)res, rbase + 3 * G);
-    bool valid = ok && rlo < rhi;
-    // Rle[i2k] past the Rle -> NULL: seqlength, or the hits' last end when NA (locate_rows)
-    if (valid) valid = ri.seqlen >= 0 ? (int64_t)sg.hi <= ri.seqlen : sg.hi <= P.pmax[rhi - 1];
-    const bool first = lane == rbase;
-    if (in && first && cidx == 0) {
-        P.valid[r] = valid ? 1 : 0;
-        if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
-    }
-    if (!in) return m;
-    if (!valid) {
-        m.flag = 1;  // NULL row -> zeros (profile.R:191-197)
-        return m;
-    }
-    if (!pile) {
-        if (m.flag == 1 && first) atomicOr(P.status, RCP_STATUS_WIDTH);  // per-base width mismatch
-        return m;
-    }
-    if (m.lay < 0 && !part.per_base && L - m.bs * n != 0) {
-        if (first) atomicOr(P.status, RCP_STATUS_INTERP);
-    }
-    m.flag = 0;
-    if (MEDIAN && m.bs + (m.lay >= 0 ? 1 : 0) > P.chunk_cap) {
-        m.flag = 2;
-        return m;
-    }
-    if (m.npos <= P.chunk_cap) {
-        m.fast = 1;
-        m.off = sg.off; m.slo = sg.lo; m.shi = sg.hi; m.rev = sg.rev;
-        if (piece) {
-            m.gps = gps;
-            m.gpe = gpe;
-            const uint32_t clo = max(rlo, plo);
-            m.lo[0] = clo;
-            m.hi[0] = max(clo, min(rhi, phi));
-            const int need = (m.npos + 1 + 63) >> 6;
-            const int per = need <= 4 ? 4 : 1 << (32 - __clz(need - 1));
-            const bool fused = !MEDIAN && m.lay < 0 && (m.bs & (m.bs - 1)) == 0 && m.bs <= per && per <= 16;
-            if (fused && m.hi[0] - m.lo[0] > (uint32_t)P.coop_min) m.heavy = -2;
-        }
-    }
-    return m;
+    FoldRow f;
+    fold_geom(P, part, k0, r, f);
+    const RcpSeg& sg = f.ri.seg0;
+    const int32_t v = q == 0 ? sg.lo : (q == 1 ? sg.hi : (q == 2 ? f.gps : f.gpe));
+    const uint32_t res = dir_bound_group<G>(P, f.ri.d0, f.ri.nb, v, (q & 1) != 0, f.ok && (q < 2 || f.piece));
+    return fold_finish<MEDIAN>(P, part, cidx, r, f, (uint32_t)__shfl((int)res, rbase),
+                               (uint32_t)__shfl((int)res, rbase + G), (uint32_t)__shfl((int)res, rbase + 2 * G),
+                               (uint32_t)__shfl((int)res, rbase + 3 * G), lane == rbase, (uint32_t)P.coop_min);
+}
+
+// The lean kernel's fold (store wave 0 decoding the next item's 32 rows): two lanes per row, each
+// bisecting two bounds in lockstep (dir_bound_multi) -- lane 2 i the row's, lane 2 i + 1 the
+// chunk piece's; no cooperative rows (the lean kernel deals rows to single waves)
+__device__ __forceinline__ RowMeta fold_row_pair(const RcpPlanDev& P, const RcpPart& part, int32_t k0, int cidx, int r) {
+    const int lane = threadIdx.x & 63;
+    const int h = lane & 1, rb = lane & ~1;
+    FoldRow f;
+    fold_geom(P, part, k0, r, f);
+    const RcpSeg& sg = f.ri.seg0;
+    const int64_t d0[2] = {f.ri.d0, f.ri.d0};
+    const int32_t nb[2] = {f.ri.nb, f.ri.nb};
+    const int32_t v[2] = {h ? f.gps : sg.lo, h ? f.gpe : sg.hi};
+    const int dst[2] = {-2, -1};
+    uint32_t res[2] = {0u, 0u};
+    dir_bound_multi<2>(P, d0, nb, v, dst, (f.ok && (h == 0 || f.piece)) ? 2 : 0, res);
+    return fold_finish<false>(P, part, cidx, r, f, (uint32_t)__shfl((int)res[0], rb), (uint32_t)__shfl((int)res[1], rb),
+                              (uint32_t)__shfl((int)res[0], rb + 1), (uint32_t)__shfl((int)res[1], rb + 1), h == 0, 0u);
 }
 
 template <bool MEDIAN, bool CSR, bool UNI>
@@ -2856,9 +2899,16 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         }
         if (code >= 0) {
             const LeanItem it = lean_item(P, code);
-            if (lane < kIRows)
+            if (LR == 2 && P.fold) {
+                // fold plans (per-base shards): the item's 32 rows searched here, two lanes a row --
+                // while the pile waves work on the current item, as a decode would be
+                const int i = lane >> 1;
+                const RowMeta m = fold_row_pair(P, P.part[it.p], it.k0, it.cidx, it.tile * kIRows + i);
+                if ((lane & 1) == 0) lmeta[buf * kRows + i] = lean_pack(m);
+            } else if (lane < kIRows) {
                 lmeta[buf * kRows + lane] =
                     lean_pack(decode_row<false, false>(P, P.part[it.p], it.k0, it.cidx, it.tile * kIRows + lane));
+            }
         }
         if (lane == 0) item[buf] = code;
         // nothing of the claim stays in flight: later register writes of this wave never
@@ -2866,6 +2916,8 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     };
     if (wave == kLPWaves) claim(0);
+    // a fold plan launches no heavy kernel: zero the status set the next execution uses here
+    if (P.fold && blockIdx.x == 0 && tid < RCP_STATUS_WORDS) P.status_prev[tid] = 0u;
     if (tid == 0) {
         item[1] = -1;  // (always written by a claim before it is read; defined anyway)
         item[2] = 0;   // the pile waves' row counter (RCP_LEAN_DYN)

@@ -144,7 +144,11 @@ bool ready(Stager* s, int dir) {  // under s->mu, on the device
     }
     if (hipEventCreateWithFlags(&s->done, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) return false;
     try {
-        s->pool.reset(new Pool(kThreadsDir[dir] - 1));
+        int nt = kThreadsDir[dir];
+        // (RCP_H2D_THREADS / RCP_D2H_THREADS: diagnostics A/B of the copy threads per direction)
+        if (const char* e = std::getenv(dir == 0 ? "RCP_H2D_THREADS" : "RCP_D2H_THREADS"))
+            nt = std::min(32, std::max(1, std::atoi(e)));
+        s->pool.reset(new Pool(nt - 1));
     } catch (const std::exception&) {
         return false;
     }

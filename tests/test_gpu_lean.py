@@ -307,3 +307,32 @@ def test_lean_with_interpolated_single_rows(gpu, mode):
         assert (lean[0][short].sum(axis=1) > 0).all()
         check(lean, exp, rtol=1e-9, atol=1e-12)
         same(lean, gen)
+
+
+@pytest.mark.parametrize("seqlen", ["known", "NA"])
+def test_lean_per_base_fold(gpu, seqlen):
+    """Per-base lean plans of a small table (one GPU's shard of C5) search their rows' read
+    ranges in the kernel: the store wave that claims an item bisects each row's and the chunk's
+    bounds, two lanes a row (no locate launch, no heaviest-first item order).  Dense and sparse
+    rows, both strands, NULL rows, NA seqlengths, repeated executions: bit-equal to the locate
+    path (an explicit heavy threshold keeps it) and the oracle."""
+    from recoup_amd.engine import Bins, Plan, ReadSet
+    from tests import oracle_rows
+    rng = np.random.default_rng(808 + (seqlen == "NA"))
+    sl = CHROM_LEN if seqlen == "known" else np.full(3, -1, np.int64)
+    reads = make_reads(rng, 200_000, widths=(50, 50))
+    rows = single_rows(rng, 400, 4000, edge=True)
+    rows.start[1], rows.end[1] = 1, 4000  # (a start at 0 shortens its row: not a per-base row of 4000)
+    bins = Bins([("whole", 0, 4000)])
+    rs = ReadSet(*reads, sl, device=0)
+    fold = Plan(rs, rows, bins, kernel="lean")
+    located = Plan(rs, rows, bins, kernel="lean", heavy_threshold=4096)
+    assert fold.info["pileup_kernel"] == 1 and fold.info["fold"] == 1, fold.info
+    assert located.info["fold"] == 0
+    exp = oracle_rows.profile(oracle_rows.row_coverage(oracle_rows.index_for(reads, sl), rows), bins)
+    ref = located.run()
+    for _ in range(3):
+        got = fold.run()
+        check(got, exp)
+        same(got, ref)
+    np.testing.assert_array_equal(fold.validity(), exp[1])

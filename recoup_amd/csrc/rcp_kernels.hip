@@ -2685,7 +2685,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
 // k + 1 and decodes its 64 row records into the second metadata buffer, and the pile waves
 // prefetch its first reads during item k's last row: no workgroup start-up latency.
 // ---------------------------------------------------------------------------------
-// Not adopted (same-box A/B): 2 or 6 store waves, 10 pile waves, a third batch
+// Not adopted (same-box A/B, DESIGN_HISTORY.md, round 4): 2 or 6 store waves, 10 pile waves, a third batch
 // of reads in flight per row (neutral), 8-read batches for start-only streams.
 constexpr int kLPWaves = 8;       // pile waves per lean workgroup (<= 16 rows of a round)
 constexpr int kLStoreWaves = 4;

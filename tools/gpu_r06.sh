@@ -8,6 +8,7 @@
 #   c4       the default bench line (C4, cpu baseline and e2e)
 #   shards   C4 and C5 1/8 shards at D = 1 (--sim-shard 0/8)
 #   prof     rocprofv3 kernel summary of the C4 bench command
+#   configs  the C2, C3 and C5 bench lines (no host paths) and their rocprofv3 kernel summaries
 set -o pipefail
 STEPS=${1:-tests}
 OUT=${2:-gpurun_out/r06}
@@ -46,5 +47,13 @@ if has prof; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
       python3 bench.py --no-cpu --no-e2e --inflight 1 > "$OUT/c4_bench_under_rocprof.json" 2> "$OUT/prof.err" || { tail -30 "$OUT/prof.err"; exit 1; }
   find "$OUT/prof" -name "*kernel_stats.csv" | head -3
+fi
+if has configs; then
+  for c in c2 c3 c5; do
+    timeout -k 10 300 python3 bench.py --config $c --no-e2e > "$OUT/${c}_bench.json" 2> "$OUT/${c}_bench.err" || { tail -30 "$OUT/${c}_bench.err"; exit 1; }
+    python3 -c "import json; d=json.load(open('$OUT/${c}_bench.json')); print('$c', d['value'], d['ms_per_step'], d['config'].get('single_pass_ms'), d['roofline']['kernel'], d['roofline']['kernel_ms'], d['roofline']['frac'])"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$c" -o bench -- \
+        python3 bench.py --config $c --no-cpu --no-e2e --inflight 1 > "$OUT/${c}_under_rocprof.json" 2> "$OUT/prof_$c.err" || { tail -30 "$OUT/prof_$c.err"; exit 1; }
+  done
 fi
 exit 0

@@ -1156,6 +1156,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     // is one wave's pass (no sub-chunks) and holds <= rcp_lean_gen_max_bins() bins.  Measured
     // slower than the general kernel on C2 (0.082 vs 0.063 ms) and C3 (0.96 vs 0.88 ms), so
     // AUTO does not choose it.  RCP_KERNEL_GENERAL keeps every plan on the general kernel.
+    bool lean_base = false;  // a lean plan whose every part is per base
     {
         const int kind = opts->pileup_kernel;
         bool base = !cov_only && bins->stat == RCP_STAT_MEAN && P.chunk_cap <= 1023 && kind != RCP_KERNEL_GENERAL;
@@ -1181,7 +1182,11 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
         {
             bool per_base = true;
             for (int p = 0; p < P.n_parts; ++p) per_base = per_base && P.part[p].per_base;
-            P.lean_rounds = P.lean && per_base ? 2 : 0;
+            lean_base = P.lean && per_base;
+            P.lean_rounds = lean_base ? 2 : 0;
+            // (RCP_LEAN_ROUNDS=2: diagnostics A/B of two-round items for binned lean plans)
+            if (P.lean && !per_base && std::getenv("RCP_LEAN_ROUNDS") && std::atoi(std::getenv("RCP_LEAN_ROUNDS")) == 2)
+                P.lean_rounds = 2;
         }
         // row-wave kernel (lean == 3): mean bins of any layout, every bin inside one window;
         // AUTO takes it for plans with multi-range rows (coverageRnaRef, genebody + flanks)
@@ -1256,7 +1261,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     // table: C5 1/8 spent locate 45 us ahead of a 143-us pileup): the store wave that claims an
     // item searches its rows' read ranges while the pile waves work on the previous item -- no
     // locate launch.  (Binned lean plans keep the locate: their skewed rows need the heavy slices.)
-    if (P.lean == 1 && P.lean_rounds == 2 && rows->ignore_strand && opts->heavy_threshold <= 0 &&
+    if (P.lean == 1 && lean_base && rows->ignore_strand && opts->heavy_threshold <= 0 &&
         B.interp_row.empty() && R > 0 && R <= kFoldMaxRows && !std::getenv("RCP_NO_LEAN_FOLD")) {
         bool f = true;
         for (int r = 0; f && r < R; ++r) {
@@ -1296,7 +1301,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
                 P.n_chunks_total += pt.n_chunks;
             }
         };
-        const int64_t want = (P.lean_rounds == 2 ? kLeanItemsPerWgBase : kLeanItemsPerWg) * grid;
+        const int64_t want = (lean_base ? kLeanItemsPerWgBase : kLeanItemsPerWg) * grid;
         while (can_split() && (tiles * P.n_chunks_total < want || P.n_chunks_total < opts->min_col_chunks))
             split();
         P.stage_cap = 1;
@@ -1420,7 +1425,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     if (hipDeviceGetAttribute(&lpt_cus, hipDeviceAttributeMultiprocessorCount, rs->device) != hipSuccess || lpt_cus <= 0)
         lpt_cus = 256;
     // (a full per-base table, e.g. C5's 6256 items, keeps the per-XCD order and its L2 locality)
-    P.lpt = P.lean == 1 && P.lean_rounds == 2 && keep_crange && R > 0 && !P.fold &&
+    P.lpt = P.lean == 1 && lean_base && keep_crange && R > 0 && !P.fold &&
             lpt_items <= (int64_t)kLeanItemsPerWgBase * 2 * lpt_cus;
     P.lpt_cap = P.lpt ? (int32_t)lpt_items : 0;
     const size_t w_order = al(w_crange + (keep_crange ? sizeof(uint2) * 3 * (size_t)P.n_chunks_total * Rw : 0));
@@ -1478,7 +1483,7 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     // with starts (pileup 0.578 vs 0.555 ms, same box), C5's dense per-base rows 6 % faster
     // (0.58 vs 0.62), the 1/8 C4 shard's general kernel 4 % (profiles/r03/pipeline/general_starts_ab.log,
     // lean_starts_c4_ab.log)
-    const bool use_st = RL.st.p && (P.lean != 1 || P.lean_rounds == 2);
+    const bool use_st = RL.st.p && (P.lean != 1 || lean_base);
     P.st = use_st ? RL.st.as<int32_t>() : nullptr;
     P.st_w = RL.st_w;
     P.pmax = RL.pmax.as<int32_t>();

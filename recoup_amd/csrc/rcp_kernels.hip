@@ -23,6 +23,7 @@
 // a column (128 B) per 16 lanes of the R column-major matrix (64-B segments write at ~60 %
 // of the 128-B rate: tools/write_bench.hip).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <type_traits>
 #include <hipcub/hipcub.hpp>
 
@@ -3240,8 +3241,10 @@ rcp_pileup_lean_kernel(RcpPlanDev P, double* __restrict__ out) {
 // each wave piles its rows into its own D / F arrays and stages their numerators; the
 // workgroup then writes the tile column-major.
 // =================================================================================
-constexpr int kBDWaves = 16;  // waves per 16-row tile (16 / kBDWaves rows each; C2 pileup 4: 30.8,
-                              // 8: 28.7, 16: 28.1 us, profiles/r04/r4j/ab.log)
+constexpr int kBDWaves = 8;  // waves per 16-row tile, two rows each, located in one chain of searches:
+                             // four 8-wave workgroups fit a CU (one 16-wave one did: 106 SGPRs), so
+                             // C2's 625 tiles are one generation -- pass 0.033 -> 0.027 ms (16 / 8 / 4
+                             // waves: 0.033 / 0.027 / 0.032, profiles/r06/c2/ab_waves.log)
 static_assert(kTile % kBDWaves == 0, "a tile's rows are split evenly over the waves");
 constexpr int kBDMaxBins = 512;
 constexpr int kBDMinWidth = 4;
@@ -3251,13 +3254,13 @@ extern "C" int rcp_bins_min_width(void) { return kBDMinWidth; }
 __host__ __device__ __forceinline__ int bd_stage_stride(int n) { return ((n + 3) >> 2 << 2) + 4; }
 __host__ __device__ __forceinline__ int bd_wave_words(int n) { return 2 * (((n + 2) + 63) & ~63); }
 
-extern "C" size_t rcp_pileup_bins_lds_bytes(const RcpPlanDev* P) {
-    const int n = P->part[0].n_bins;
-    return 4 * ((size_t)kTile * bd_stage_stride(n) + (size_t)kBDWaves * bd_wave_words(n) + 2 * kTile);
+static size_t bins_lds_bytes(int n, int waves) {
+    return 4 * ((size_t)kTile * bd_stage_stride(n) + (size_t)waves * bd_wave_words(n) + 2 * kTile);
 }
+extern "C" size_t rcp_pileup_bins_lds_bytes(const RcpPlanDev* P) { return bins_lds_bytes(P->part[0].n_bins, 16); }
 
-template <bool UNI>
-__global__ void __launch_bounds__(64 * kBDWaves) __attribute__((amdgpu_waves_per_eu(4)))
+template <bool UNI, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4)))
 rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restrict__ binsum) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     using RdT = typename std::conditional<UNI, int32_t, int2>::type;
@@ -3269,7 +3272,7 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem);                 // [16][RS] numerators
     int32_t* D = reinterpret_cast<int32_t*>(stage + kTile * RS) + wave * WW;  // partial overlaps
     int32_t* F = D + WW / 2;                                              // full-bin differences
-    int32_t* rbs = reinterpret_cast<int32_t*>(stage + kTile * RS) + kBDWaves * WW;  // [16] bs, 0 NULL, -1 none
+    int32_t* rbs = reinterpret_cast<int32_t*>(stage + kTile * RS) + WAVES * WW;  // [16] bs, 0 NULL, -1 none
     // tiles of one XCD's workgroups are consecutive (round-robin dispatch over 8 XCDs):
     // neighbouring regions share reads in that L2
     const int nt = (P.n_rows + kTile - 1) / kTile;
@@ -3362,25 +3365,9 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
         R.rev = sg.rev;
         return R;
     };
-    auto row_of = [&](int r) -> Row {
+    // a row's description from its record (the locate kernel's, or the folded searches')
+    auto describe = [&](const RcpRowRec& R) -> Row {
         Row m{};
-        m.flag = -1;
-        if (r >= P.n_rows) return m;
-        RcpRowRec R;
-        if (P.fold) {
-            R = locate_row(r);
-        } else {
-            RcpRowRec rec;
-            const uint4* src = reinterpret_cast<const uint4*>(P.rec + r);
-            uint4* dst = reinterpret_cast<uint4*>(&rec);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) dst[q] = src[q];
-            int32_t v[16];
-            __builtin_memcpy(v, &rec, sizeof v);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = __builtin_amdgcn_readfirstlane(v[q]);
-            __builtin_memcpy(&R, v, sizeof R);
-        }
         if (!(R.flags & RCP_REC_VALID)) {
             m.flag = 0;  // NULL row -> zeros (profile.R:191-197)
             return m;
@@ -3417,6 +3404,122 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             m.hi[s] = a < b ? R.hi[s] : R.lo[s];
         }
         return m;
+    };
+    auto row_of = [&](int r) -> Row {
+        Row m{};
+        m.flag = -1;
+        if (r >= P.n_rows) return m;
+        RcpRowRec R;
+        if (P.fold) {
+            R = locate_row(r);
+        } else {
+            RcpRowRec rec;
+            const uint4* src = reinterpret_cast<const uint4*>(P.rec + r);
+            uint4* dst = reinterpret_cast<uint4*>(&rec);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[q] = src[q];
+            int32_t v[16];
+            __builtin_memcpy(v, &rec, sizeof v);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = __builtin_amdgcn_readfirstlane(v[q]);
+            __builtin_memcpy(&R, v, sizeof R);
+        }
+        return describe(R);
+    };
+    // P.fold with several rows a wave (kMine > 1): the locate work of all of them in ONE chain of
+    // round trips -- their row records loaded together, lane l bisecting bound l % 2ns of row
+    // l / 2ns (2ns lanes a row: lower / upper bound per strand stream), their NULL rules after --
+    // instead of one chain per row
+    constexpr int kMine = kTile / WAVES;
+    auto locate_rows = [&](const int (&rr)[kMine], Row (&rows)[kMine]) {
+        RcpRowInfo ri[kMine];
+        {
+            uint4 w[kMine][sizeof(RcpRowInfo) / 16];
+#pragma unroll
+            for (int j = 0; j < kMine; ++j) {
+                const uint4* src = reinterpret_cast<const uint4*>(P.row_info + min(rr[j], P.n_rows - 1));
+#pragma unroll
+                for (int q = 0; q < (int)(sizeof(RcpRowInfo) / 16); ++q) w[j][q] = src[q];
+            }
+#pragma unroll
+            for (int j = 0; j < kMine; ++j) {
+                int32_t v[sizeof(RcpRowInfo) / 4];
+                __builtin_memcpy(v, w[j], sizeof v);
+#pragma unroll
+                for (int q = 0; q < (int)(sizeof(RcpRowInfo) / 4); ++q) v[q] = __builtin_amdgcn_readfirstlane(v[q]);
+                __builtin_memcpy(&ri[j], v, sizeof(RcpRowInfo));
+            }
+        }
+        const int ns = P.merged ? 1 : 3, per = 2 * ns;
+        const int jl = lane / per, e = lane - jl * per, st = e >> 1;
+        bool ok[kMine];
+        int64_t d0[1] = {0};
+        int32_t nb[1] = {0};
+        int32_t v[1] = {0};
+        const int dst[1] = {(e & 1) ? -1 : -2};
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < kMine; ++j) {
+            const RcpSeg& sg = ri[j].seg0;
+            ok[j] = rr[j] < P.n_rows && !ri[j].stat && ri[j].chrom >= 0 && ri[j].chrom < P.n_chrom &&
+                    ri[j].j1 == ri[j].j0 + 1 && sg.query_ok;
+            if (jl == j && ok[j] && ((sg.streams >> st) & 1)) {
+                cnt = 1;
+                v[0] = (e & 1) ? sg.hi : sg.lo;
+                d0[0] = ri[j].d0;
+                nb[0] = ri[j].nb;
+                if (!P.merged) {
+                    d0[0] = P.dir_off[ri[j].chrom * 3 + st];
+                    nb[0] = (int32_t)(P.dir_off[ri[j].chrom * 3 + st + 1] - d0[0]) - 1;
+                }
+            }
+        }
+        uint32_t res[1];
+        dir_bound_multi<1>(P, d0, nb, v, dst, cnt, res);
+        RcpRowRec R[kMine];
+        int32_t maxend[kMine];
+        bool hit[kMine];
+#pragma unroll
+        for (int j = 0; j < kMine; ++j) {
+            const RcpSeg& sg = ri[j].seg0;
+            R[j] = RcpRowRec{};
+            R[j].row_len = ri[j].row_len;
+            R[j].heavy = -1;
+            hit[j] = false;
+            maxend[j] = INT32_MIN;
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)res[0], j * per + 2 * s);
+                const uint32_t hi = max(lo, (uint32_t)__builtin_amdgcn_readlane((int)res[0], j * per + 2 * s + 1));
+                R[j].lo[s] = R[j].hi[s] = 0;
+                if (ok[j] && s < ns && ((sg.streams >> s) & 1) && lo < hi) {
+                    R[j].lo[s] = lo;
+                    R[j].hi[s] = hi;
+                    hit[j] = true;
+                    if (ri[j].seqlen < 0) maxend[j] = max(maxend[j], P.pmax[hi - 1]);  // only NA seqlengths need it
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kMine; ++j) {
+            const RcpSeg& sg = ri[j].seg0;
+            const bool valid = ok[j] && hit[j] && (ri[j].seqlen >= 0 ? (int64_t)sg.hi <= ri[j].seqlen : sg.hi <= maxend[j]);
+            if (lane == 0 && rr[j] < P.n_rows) {
+                P.valid[rr[j]] = valid ? 1 : 0;
+                if (P.valid_out) P.valid_out[rr[j]] = valid ? 1 : 0;
+            }
+            R[j].flags = valid ? (RCP_REC_VALID | RCP_REC_FAST) : 0;
+            R[j].off = sg.off;
+            R[j].slo = sg.lo;
+            R[j].shi = sg.hi;
+            R[j].rev = sg.rev;
+            if (rr[j] < P.n_rows) {
+                rows[j] = describe(R[j]);
+            } else {
+                rows[j] = Row{};
+                rows[j].flag = -1;
+            }
+        }
     };
     auto n_cand = [&](const Row& m) -> uint32_t {
         return (m.hi[0] - m.lo[0]) + (m.hi[1] - m.lo[1]) + (m.hi[2] - m.lo[2]);
@@ -3462,77 +3565,90 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             }
         }
     };
-    // my rows of the tile: wave, wave + kBDWaves, ...
-    constexpr int kMine = kTile / kBDWaves;
-    RdT bufA[4], bufB[4];
-    Row cur = row_of(row0 + wave);
-    load_batch(cur, n_cand(cur), 0, bufA);
-#pragma unroll
-    for (int j = 0; j < kMine; ++j) {
-        const int i = wave + kBDWaves * j;  // tile row
-        RdT (&c)[4] = (j & 1) ? bufB : bufA;
-        RdT (&nx)[4] = (j & 1) ? bufA : bufB;
-        Row nxt{};
-        nxt.flag = -1;
-        if (j + 1 < kMine) {
-            nxt = row_of(row0 + i + kBDWaves);
-            load_batch(nxt, n_cand(nxt), 0, nx);
-        }
-        const Row m = cur;
+    // my rows of the tile: wave, wave + WAVES, ...
+    RdT buf[kMine][4];
+    auto pile = [&](const Row& m, int i, RdT (&c)[4]) {
         if (lane == 0) rbs[i] = m.flag == 1 ? m.bs : (m.flag == 0 ? 0 : -1);
-        if (m.flag == 1) {
-            const float rb = 1.0f / (float)m.bs;
-            if (m.heavy >= 0) {
-                // skewed row: its position difference array was piled up by
-                // rcp_heavy_pileup_kernel; depth by a wave scan, summed into D per position
-                const int32_t* g = P.heavy_gdiff + (size_t)m.heavy * P.heavy_stride;
-                int32_t carry = 0;
-                for (int q = lane; q < m.head; q += 64) carry += g[q];
-                carry = wave_sum(carry);
-                for (int32_t b0 = 0; b0 < m.L; b0 += 64) {
-                    const int32_t x = b0 + lane;
-                    const int32_t gv = x < m.L ? g[m.head + x] : 0;
-                    const int32_t incl = (int32_t)wave_inclusive_scan((uint32_t)gv);
-                    const int32_t depth = carry + incl;
-                    carry += __builtin_amdgcn_readlane(incl, 63);
-                    if (x < m.L && depth) atomicAdd(&D[bin_of(x, m.bs, rb)], depth);
-                }
-            } else {
-                const uint32_t nc = n_cand(m);
-                for (uint32_t q0 = 0; q0 < nc; q0 += 256) {
-                    RdT nb[4];
-                    load_batch(m, nc, q0 + 256, nb);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (q0 + ps_slot(lane, u) < nc) add_read(m, rd_pair(c[u]), rb);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) c[u] = nb[u];
-                }
-            }
-            lds_order();
-            // numerators: D[k] + bs * prefix(F)[k], 64 bins per step (lane t: bin 64 j + t; one
-            // wave scan per step): consecutive lanes, consecutive words -- no bank conflicts
-            uint32_t* srow = stage + i * RS;
+        if (m.flag != 1) return;
+        const float rb = 1.0f / (float)m.bs;
+        if (m.heavy >= 0) {
+            // skewed row: its position difference array was piled up by
+            // rcp_heavy_pileup_kernel; depth by a wave scan, summed into D per position
+            const int32_t* g = P.heavy_gdiff + (size_t)m.heavy * P.heavy_stride;
             int32_t carry = 0;
-            for (int32_t k0 = 0; k0 < n; k0 += 64) {
-                const int k = k0 + lane;
-                const int32_t f = k < n ? F[k] : 0;
-                const int32_t run = carry + (int32_t)wave_inclusive_scan((uint32_t)f);
-                carry = __builtin_amdgcn_readlane(run, 63);
-                if (k < n) {
-                    srow[k] = (uint32_t)(D[k] + m.bs * run);
-                    D[k] = 0;
-                    F[k] = 0;
-                }
+            for (int q = lane; q < m.head; q += 64) carry += g[q];
+            carry = wave_sum(carry);
+            for (int32_t b0 = 0; b0 < m.L; b0 += 64) {
+                const int32_t x = b0 + lane;
+                const int32_t gv = x < m.L ? g[m.head + x] : 0;
+                const int32_t incl = (int32_t)wave_inclusive_scan((uint32_t)gv);
+                const int32_t depth = carry + incl;
+                carry += __builtin_amdgcn_readlane(incl, 63);
+                if (x < m.L && depth) atomicAdd(&D[bin_of(x, m.bs, rb)], depth);
             }
-            lds_order();
+        } else {
+            const uint32_t nc = n_cand(m);
+            for (uint32_t q0 = 0; q0 < nc; q0 += 256) {
+                RdT nb[4];
+                load_batch(m, nc, q0 + 256, nb);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (q0 + ps_slot(lane, u) < nc) add_read(m, rd_pair(c[u]), rb);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) c[u] = nb[u];
+            }
         }
-        cur = nxt;
+        lds_order();
+        // numerators: D[k] + bs * prefix(F)[k], 64 bins per step (lane t: bin 64 j + t; one
+        // wave scan per step): consecutive lanes, consecutive words -- no bank conflicts
+        uint32_t* srow = stage + i * RS;
+        int32_t carry = 0;
+        for (int32_t k0 = 0; k0 < n; k0 += 64) {
+            const int k = k0 + lane;
+            const int32_t f = k < n ? F[k] : 0;
+            const int32_t run = carry + (int32_t)wave_inclusive_scan((uint32_t)f);
+            carry = __builtin_amdgcn_readlane(run, 63);
+            if (k < n) {
+                srow[k] = (uint32_t)(D[k] + m.bs * run);
+                D[k] = 0;
+                F[k] = 0;
+            }
+        }
+        lds_order();
+    };
+    if (P.fold && kMine > 1) {
+        // all my rows' searches in one chain, then all their first batches in flight together
+        int rr[kMine];
+#pragma unroll
+        for (int j = 0; j < kMine; ++j) rr[j] = row0 + wave + WAVES * j;
+        Row rows[kMine];
+        locate_rows(rr, rows);
+#pragma unroll
+        for (int j = 0; j < kMine; ++j) load_batch(rows[j], n_cand(rows[j]), 0, buf[j]);
+#pragma unroll
+        for (int j = 0; j < kMine; ++j) pile(rows[j], wave + WAVES * j, buf[j]);
+    } else {
+        Row cur = row_of(row0 + wave);
+        load_batch(cur, n_cand(cur), 0, buf[0]);
+#pragma unroll
+        for (int j = 0; j < kMine; ++j) {
+            const int i = wave + WAVES * j;  // tile row
+            RdT (&c)[4] = buf[j & 1 ? (kMine > 1 ? 1 : 0) : 0];
+            RdT (&nx)[4] = buf[j & 1 ? 0 : (kMine > 1 ? 1 : 0)];
+            Row nxt{};
+            nxt.flag = -1;
+            if (j + 1 < kMine) {
+                nxt = row_of(row0 + i + WAVES);
+                load_batch(nxt, n_cand(nxt), 0, nx);
+            }
+            pile(cur, i, c);
+            cur = nxt;
+        }
     }
     lds_barrier();
     // ---- the tile's 16 rows, column-major: thread (row ii, column group cg) stores columns cg,
     // cg + kCG, ...; the 16 lanes of a column write its 128-B line of the tile
-    constexpr int kCG = 64 * kBDWaves / kTile;
+    constexpr int kCG = 64 * WAVES / kTile;
     const int ii = tid & (kTile - 1), cg = tid >> 4;
     const int r = row0 + ii;
     if (r >= P.n_rows) return;
@@ -3552,16 +3668,24 @@ rcp_pileup_bins_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
     }
 }
 
-static hipError_t launch_pileup_bins(const RcpPlanDev* P, double* out, int64_t* binsum, hipStream_t stream) {
+template <int WAVES>
+static hipError_t launch_pileup_bins_w(const RcpPlanDev* P, double* out, int64_t* binsum, hipStream_t stream) {
     const int nt = (P->n_rows + kTile - 1) / kTile;
     const unsigned grid = (unsigned)(((nt + 7) / 8) * 8);
-    const size_t lds = rcp_pileup_bins_lds_bytes(P);
+    const size_t lds = bins_lds_bytes(P->part[0].n_bins, WAVES);
     if (P->st) {
-        hipLaunchKernelGGL(rcp_pileup_bins_kernel<true>, dim3(grid), dim3(64 * kBDWaves), lds, stream, *P, out, binsum);
+        hipLaunchKernelGGL((rcp_pileup_bins_kernel<true, WAVES>), dim3(grid), dim3(64 * WAVES), lds, stream, *P, out, binsum);
     } else {
-        hipLaunchKernelGGL(rcp_pileup_bins_kernel<false>, dim3(grid), dim3(64 * kBDWaves), lds, stream, *P, out, binsum);
+        hipLaunchKernelGGL((rcp_pileup_bins_kernel<false, WAVES>), dim3(grid), dim3(64 * WAVES), lds, stream, *P, out, binsum);
     }
     return hipGetLastError();
+}
+
+static hipError_t launch_pileup_bins(const RcpPlanDev* P, double* out, int64_t* binsum, hipStream_t stream) {
+    // (RCP_BD_WAVES=16: diagnostics A/B against round 5's one-row-a-wave tiles)
+    static const bool w16 = std::getenv("RCP_BD_WAVES") && std::atoi(std::getenv("RCP_BD_WAVES")) == 16;
+    if (w16) return launch_pileup_bins_w<16>(P, out, binsum, stream);
+    return launch_pileup_bins_w<kBDWaves>(P, out, binsum, stream);
 }
 
 // =================================================================================

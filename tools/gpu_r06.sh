@@ -49,7 +49,7 @@ if has prof; then
   find "$OUT/prof" -name "*kernel_stats.csv" | head -3
 fi
 if has configs; then
-  for c in c2 c3 c5; do
+  for c in ${CONFIGS:-c2 c3 c5}; do
     timeout -k 10 300 python3 bench.py --config $c --no-e2e > "$OUT/${c}_bench.json" 2> "$OUT/${c}_bench.err" || { tail -30 "$OUT/${c}_bench.err"; exit 1; }
     python3 -c "import json; d=json.load(open('$OUT/${c}_bench.json')); print('$c', d['value'], d['ms_per_step'], d['config'].get('single_pass_ms'), d['roofline']['kernel'], d['roofline']['kernel_ms'], d['roofline']['frac'])"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$c" -o bench -- \

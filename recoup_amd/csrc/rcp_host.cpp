@@ -492,6 +492,25 @@ int ensure_stranded(const rcp_readset* crs) {
 
 namespace rcpi {
 
+// the second H2D lane's stream of a device (rcp_readset_create), made on first use
+constexpr int64_t kTwoLaneMin = int64_t(1) << 22;  // reads; fewer go up on one lane
+static hipStream_t lane_stream(int device) {
+    static std::mutex mu;
+    static hipStream_t st[64] = {};
+    if (device < 0 || device >= 64) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    if (!st[device]) {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) cur = -1;
+        if ((cur == device || hipSetDevice(device) == hipSuccess) &&
+            hipStreamCreateWithFlags(&st[device], hipStreamNonBlocking) != hipSuccess)
+            st[device] = nullptr;
+        (void)hipGetLastError();
+        if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
+    }
+    return st[device];
+}
+
 // The read descriptor's shape (sizes, NULL arrays, runs that cover the reads), before any copy:
 // what readset_build and every entry point taking host read arrays check first
 int validate_reads(const rcp_reads_desc* d) {
@@ -581,20 +600,57 @@ int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_reads
         if (d->end) HIP_TRY(in_end.alloc(4 * n));
         HIP_TRY(in_strand.alloc(n));
         // caller-owned pageable arrays (R vectors): pinned double-buffered staging (rcp_stage.h),
-        // coordinates as 16-bit offsets within blocks and strands four to a byte where they fit
-        if (d->chrom)
-            HIP_TRY(rcp::stage_h2d_codes(in_chrom.as<int32_t>(), d->chrom, (size_t)n, d->n_chrom, d->device, s));
-        HIP_TRY(rcp::stage_h2d_i32(in_start.as<int32_t>(), d->start, (size_t)n, d->device, s));
-        // ends go up as widths (a block of them spans < 2^16 whatever the reads' order: 2 bytes a
-        // read where unsorted ends go raw) and are formed again on the device
-        bool widths = false;
-        if (d->end) {
-            bool unfit = false;
-            HIP_TRY(rcp::stage_h2d_width(in_end.as<int32_t>(), d->start, d->end, (size_t)n, d->device, s, &unfit));
-            if (unfit) HIP_TRY(rcp::stage_h2d_i32(in_end.as<int32_t>(), d->end, (size_t)n, d->device, s));
-            widths = !unfit;
+        // coordinates as 16-bit offsets within blocks and strands four to a byte where they fit.
+        // With one chromosome code per read (unsorted reads: R hands over per-read codes), the
+        // codes and strands -- host-encoded, their time is the copy threads' -- go up through the
+        // second H2D lane on a second thread and stream while this thread sends the starts and
+        // ends, whose time is the DMA's (RCP_ONE_H2D_LANE: diagnostics A/B, one lane)
+        hipStream_t s2 = d->chrom && n >= kTwoLaneMin && !std::getenv("RCP_ONE_H2D_LANE") ? lane_stream(d->device) : nullptr;
+        hipEvent_t ready_ev = nullptr;
+        if (s2) {
+            // s2 after the allocations' stream-ordered waits on s
+            if (hipEventCreateWithFlags(&ready_ev, hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(ready_ev, s) != hipSuccess || hipStreamWaitEvent(s2, ready_ev, 0) != hipSuccess) {
+                (void)hipGetLastError();
+                if (ready_ev) (void)hipEventDestroy(ready_ev);
+                ready_ev = nullptr;
+                s2 = nullptr;
+            }
         }
-        HIP_TRY(rcp::stage_h2d_strand(in_strand.as<int8_t>(), d->strand, (size_t)n, d->device, s));
+        hipError_t lane_err = hipSuccess;
+        std::thread lane1;
+        if (s2) {
+            lane1 = std::thread([&] {
+                lane_err = hipSetDevice(d->device);
+                rcp::H2dLane lane(1);
+                if (lane_err == hipSuccess)
+                    lane_err = rcp::stage_h2d_codes(in_chrom.as<int32_t>(), d->chrom, (size_t)n, d->n_chrom, d->device, s2);
+                if (lane_err == hipSuccess)
+                    lane_err = rcp::stage_h2d_strand(in_strand.as<int8_t>(), d->strand, (size_t)n, d->device, s2);
+            });
+        }
+        bool widths = false;
+        // (the lane-1 thread is joined before any return)
+        auto lane0 = [&]() -> hipError_t {
+            hipError_t e = hipSuccess;
+            if (d->chrom && !s2) e = rcp::stage_h2d_codes(in_chrom.as<int32_t>(), d->chrom, (size_t)n, d->n_chrom, d->device, s);
+            if (e == hipSuccess) e = rcp::stage_h2d_i32(in_start.as<int32_t>(), d->start, (size_t)n, d->device, s);
+            // ends go up as widths (a block of them spans < 2^16 whatever the reads' order: 2 bytes
+            // a read where unsorted ends go raw) and are formed again on the device
+            if (e == hipSuccess && d->end) {
+                bool unfit = false;
+                e = rcp::stage_h2d_width(in_end.as<int32_t>(), d->start, d->end, (size_t)n, d->device, s, &unfit);
+                if (e == hipSuccess && unfit) e = rcp::stage_h2d_i32(in_end.as<int32_t>(), d->end, (size_t)n, d->device, s);
+                widths = !unfit;
+            }
+            if (e == hipSuccess && !s2) e = rcp::stage_h2d_strand(in_strand.as<int8_t>(), d->strand, (size_t)n, d->device, s);
+            return e;
+        };
+        const hipError_t e0 = lane0();
+        if (lane1.joinable()) lane1.join();
+        if (ready_ev) (void)hipEventDestroy(ready_ev);
+        HIP_TRY(e0);
+        HIP_TRY(lane_err);
         pc = in_chrom.as<int32_t>();
         ps = in_start.as<int32_t>();
         if (d->end) pe = in_end.as<int32_t>();

@@ -127,11 +127,16 @@ struct Stager {
                                         // D2H packing (rcp_pack_i32_kernel)
 };
 
+// The host -> device lane of this thread (H2dLane): lane 1 has its own pinned buffers, landing
+// buffers and copy threads, so two uploads of one device run at once
+thread_local int t_h2d_lane = 0;
+
 // Process lifetime: the pinned buffers are returned to the OS at exit (freeing them from a
 // static destructor could run after the HIP runtime is gone).
-Stager* stager(int device, int dir) {  // dir 0: host -> device, 1: device -> host
-    static Stager* s = new Stager[2 * kMaxDevices];
-    return device >= 0 && device < kMaxDevices ? &s[2 * device + dir] : nullptr;
+Stager* stager(int device, int dir) {  // dir 0: host -> device (this thread's lane), 1: device -> host
+    static Stager* s = new Stager[3 * kMaxDevices];
+    const int k = dir == 0 && t_h2d_lane ? 2 : dir;
+    return device >= 0 && device < kMaxDevices ? &s[3 * device + k] : nullptr;
 }
 
 bool ready(Stager* s, int dir) {  // under s->mu, on the device
@@ -271,6 +276,9 @@ bool ready_dev(Stager* s, int device) {
 
 bool trace_on() { return trace(); }
 double trace_ms() { return now_ms(); }
+
+H2dLane::H2dLane(int lane) : prev_(t_h2d_lane) { t_h2d_lane = lane; }
+H2dLane::~H2dLane() { t_h2d_lane = prev_; }
 
 hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipStream_t stream) {
     if (bytes == 0) return hipSuccess;

@@ -25,6 +25,21 @@ hipError_t stage_h2d(void* dst, const void* src, size_t bytes, int device, hipSt
 hipError_t stage_d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
                         int device, hipStream_t stream);
 
+// The host -> device copies of the calling thread go through lane `lane` (0 or 1) while this
+// object lives: each lane has its own pinned and landing buffers and copy threads, so a second
+// thread can upload one array while the first uploads another (rcp_readset_create: chromosome
+// codes and strands beside the starts)
+class H2dLane {
+  public:
+    explicit H2dLane(int lane);
+    ~H2dLane();
+    H2dLane(const H2dLane&) = delete;
+    H2dLane& operator=(const H2dLane&) = delete;
+
+  private:
+    int prev_;
+};
+
 // RCP_TRACE set in the environment: stderr lines per staged copy / pipeline step (diagnostics)
 bool trace_on();
 double trace_ms();  // a steady clock in ms

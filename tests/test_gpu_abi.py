@@ -515,11 +515,12 @@ def test_packed_read_uploads(gpu, capfd, sorted_reads):
     more (gaps, chromosome changes) raw, chunks with too many such blocks plain (the unsorted
     sample) -- and strand codes four to a byte, codes outside 0..2 still dropping their reads.
     The readset equals one built from the same arrays already on the device: streams, kept reads
-    and a profile, bit for bit."""
+    and a profile, bit for bit.  (4.5 M reads with one code each: the codes and strands go up on
+    the second H2D lane, beside the starts and ends.)"""
     from recoup_amd.engine import ReadSet
     from tests.test_gpu_random import CHROM_LEN, single_rows
     rng = np.random.default_rng(3 + sorted_reads)
-    n = 3_000_000
+    n = 4_500_000
     codes = np.array([0, 1, 2, 0, 1, 2, -1, 7], np.int8)
     chrom = np.sort(rng.integers(0, 3, n)).astype(np.int32)
     start = np.empty(n, np.int32)

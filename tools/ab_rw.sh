@@ -1,9 +1,11 @@
-# C3 row-wave kernel: two claimed rows' searches in one chain (RCP_RW_PAIR=1) vs one row at a
-# time; parity on the row-wave tests in pair mode, then ms per pass alternating
+# C3 row-wave kernel: run-merged adds over consecutive candidates (RCP_RW_RUNS=1) vs interleaved
+# slots with one atomic per read; parity on the row-wave tests in runs mode, ms per pass alternating,
+# and the SQ counters of both
 set -o pipefail
-RCP_RW_PAIR=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_c3.py tests/test_gpu_rows.py tests/test_gpu_configs.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_rwp.log 2>&1 || { tail -30 gpurun_out/t_rwp.log; exit 1; }
-tail -1 gpurun_out/t_rwp.log
+RCP_RW_RUNS=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_c3.py tests/test_gpu_rows.py tests/test_gpu_configs.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_rwr.log 2>&1 || { tail -30 gpurun_out/t_rwr.log; exit 1; }
+tail -1 gpurun_out/t_rwr.log
 for k in 1 2 3; do
-  CFG=c3 timeout -k 10 200 python3 tools/diag_shard_kernels.py 0/1 auto 2>&1 | grep ms/pass | sed "s/^/single: /" || exit 1
-  RCP_RW_PAIR=1 CFG=c3 timeout -k 10 200 python3 tools/diag_shard_kernels.py 0/1 auto 2>&1 | grep ms/pass | sed "s/^/pair:   /" || exit 1
+  CFG=c3 timeout -k 10 200 python3 tools/diag_shard_kernels.py 0/1 auto 2>&1 | grep ms/pass | sed "s/^/atomics: /" || exit 1
+  RCP_RW_RUNS=1 CFG=c3 timeout -k 10 200 python3 tools/diag_shard_kernels.py 0/1 auto 2>&1 | grep ms/pass | sed "s/^/runs:    /" || exit 1
 done
+RCP_RW_RUNS=1 PASSES=sq bash tools/pmc.sh gpurun_out/c3pmc/runs c3

@@ -2609,20 +2609,34 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                 // bins [k0, k1): numerator = cum[b - 1] - cum[a - 1] (exact integers; the same
                 // divisions as the general kernel's epilogue, so the same bits)
                 const uint32_t* cum = reinterpret_cast<const uint32_t*>(diff);
-                for (int32_t k = k0 + lane; k < k1; k += 64) {
-                    const int32_t a = bin_edge(bs, lay, P.lay_cnt, k) - e0;
-                    const int32_t b = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
-                    const uint32_t num = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
-                    if (xs) {
-                        xs[k] = (double)num * sc;  // (rcp_interp_kernel's x[i])
-                        continue;
+                // four bins a lane per step, their layout edges loaded together before any store:
+                // gfx9 waits for a load and every earlier store with one counter, so a store
+                // between two bins' edge loads put a store round trip on each bin
+                for (int32_t kb = k0 + lane; kb < k1; kb += 256) {
+                    int32_t ea[4], eb[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int32_t k = min(kb + 64 * u, k1 - 1);
+                        ea[u] = bin_edge(bs, lay, P.lay_cnt, k) - e0;
+                        eb[u] = bin_edge(bs, lay, P.lay_cnt, k + 1) - e0;
                     }
-                    if (staged) {
-                        srow[part.col_off + k] = num;
-                        continue;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int32_t k = kb + 64 * u;
+                        if (k >= k1) break;
+                        const int32_t a = ea[u], b = eb[u];
+                        const uint32_t num = cum[lp(b - 1, sh)] - cum[lp(a - 1, sh)];
+                        if (xs) {
+                            xs[k] = (double)num * sc;  // (rcp_interp_kernel's x[i])
+                            continue;
+                        }
+                        if (staged) {
+                            srow[part.col_off + k] = num;
+                            continue;
+                        }
+                        rows_store(rows_mean(num, sc, pow2, b - a, bs, dd, rdd, dd1, rdd1), cell(r, part.col_off + k));
+                        if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = (int64_t)num;
                     }
-                    rows_store(rows_mean(num, sc, pow2, b - a, bs, dd, rdd, dd1, rdd1), cell(r, part.col_off + k));
-                    if (binsum) binsum[(size_t)(part.col_off + k) * R + r] = (int64_t)num;
                 }
                 lds_order();
             }

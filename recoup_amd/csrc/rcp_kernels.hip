@@ -2310,9 +2310,23 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                 const bool pow2 = lay < 0 && (bs & (bs - 1)) == 0;
                 const double dd = (double)bs, rdd = 1.0 / dd;
                 const double dd1 = (double)(bs + 1), rdd1 = 1.0 / dd1;
-                for (int32_t k0 = 0; k0 < n; k0 += 32) {
+                // the stage words (and the enlarged-bin mask word) of the next 32 columns are
+                // loaded before this step's stores: one vmcnt counts loads and stores in order on
+                // gfx9, so a load issued after the stores would wait for their acknowledgements
+                auto load_step = [&](int32_t k0, uint32_t (&q)[8], uint32_t& bits) {
                     // enlarged bins of the 32 columns (R-RNG layout) as one mask word
-                    const uint32_t bits = (f.x > 0 && lay >= 0) ? P.lay_bit[lay + (k0 >> 5)] : 0u;
+                    bits = (f.x > 0 && lay >= 0) ? P.lay_bit[lay + (k0 >> 5)] : 0u;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int32_t k = k0 + 4 * u + cq;
+                        q[u] = (f.x > 0 && k < n) ? srow[c0p + k] : 0u;
+                    }
+                };
+                uint32_t q[8], bits = 0;
+                load_step(0, q, bits);
+                for (int32_t k0 = 0; k0 < n; k0 += 32) {
+                    uint32_t qn[8], bitsn = 0;
+                    if (k0 + 32 < n) load_step(k0 + 32, qn, bitsn);
                     double v[8];
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
@@ -2320,7 +2334,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                         v[u] = 0.0;
                         if (f.x > 0 && k < n) {
                             const int32_t w = bs + (int32_t)((bits >> (4 * u + cq)) & 1u);
-                            v[u] = rows_mean(srow[c0p + k], sc, pow2, w, bs, dd, rdd, dd1, rdd1);
+                            v[u] = rows_mean(q[u], sc, pow2, w, bs, dd, rdd, dd1, rdd1);
                         }
                     }
 #pragma unroll
@@ -2329,6 +2343,9 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                         if (f.x >= 0 && k < n)
                             __builtin_nontemporal_store(v[u], out + (size_t)(c0p + k) * R + (size_t)(t16 + i));
                     }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) q[u] = qn[u];
+                    bits = bitsn;
                 }
             }
         }

@@ -2508,17 +2508,24 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     valid = valid && ok_g;
                 }
             }
-            if (lane == 0) {
-                P.valid[r] = valid ? 1 : 0;
-                if (P.valid_out) P.valid_out[r] = valid ? 1 : 0;
-            }
             flags = valid ? RCP_REC_VALID : 0;
         }
         uint32_t* const srow = stage_row(r, sl);
         int2* const sinfo = stage_info(r, sl);
-        if (staged && lane < P.n_parts) sinfo[lane] = make_int2(0, -1);  // zeros unless piled below
+        // the row's validity and its parts' stage info (lane p: part p; zeros unless piled
+        // below) are stored when the row is done: one vmcnt counts loads and stores in order on
+        // gfx9, so a store here would put its round trip on the row's first read loads
+        int2 info = make_int2(0, -1);
+        auto commit = [&]() {
+            if (P.fold && lane == 0) {
+                P.valid[r] = (flags & RCP_REC_VALID) ? 1 : 0;
+                if (P.valid_out) P.valid_out[r] = (flags & RCP_REC_VALID) ? 1 : 0;
+            }
+            if (staged && lane < P.n_parts) sinfo[lane] = info;
+        };
         if (!(flags & RCP_REC_VALID)) {  // NULL row -> zeros (profile.R:191-197)
             for (int p = 0; p < P.n_parts; ++p) zero_cols(r, P.part[p], P.part[p].n_bins);
+            commit();
             return itp_parts;
         }
 
@@ -2533,7 +2540,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             // after this one, takes the depth from there instead of piling the row again.
             const bool itp = !part.per_base && L < n_bins;
             if (itp) {
-                if (staged && lane == 0) sinfo[p] = make_int2(-1, -1);
+                if (lane == p) info = make_int2(-1, -1);
                 if (!staged || !P.interp_stage) continue;
             }
             const int32_t n = itp ? L : n_bins;  // the bins of this pass
@@ -2559,7 +2566,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
                     }
                 }
             }
-            if (staged && lane == 0 && !itp) sinfo[p] = make_int2(bs, lay);
+            if (lane == p && !itp) info = make_int2(bs, lay);
             const int32_t kw = max(1, kWinCap / (bs + (lay >= 0 ? 1 : 0)));  // bins per window
             const bool pow2 = lay < 0 && (bs & (bs - 1)) == 0;
             const double dd = (double)bs, rdd = 1.0 / dd;
@@ -2659,6 +2666,7 @@ rcp_pileup_rows_kernel(RcpPlanDev P, double* __restrict__ out, int64_t* __restri
             }
             if (xs) itp_parts |= 1u << p;
         }
+        commit();
         return itp_parts;
     };
     // splitVector of row r's piled slices (itp_parts: the parts with an interpolation entry) into

@@ -619,14 +619,24 @@ int readset_build(const rcp_reads_desc* d, hipStream_t s, int layouts, rcp_reads
         }
         hipError_t lane_err = hipSuccess;
         std::thread lane1;
+        struct Join {  // joined on every way out, exceptions included
+            std::thread& t;
+            ~Join() {
+                if (t.joinable()) t.join();
+            }
+        } join_lane1{lane1};
         if (s2) {
             lane1 = std::thread([&] {
-                lane_err = hipSetDevice(d->device);
-                rcp::H2dLane lane(1);
-                if (lane_err == hipSuccess)
-                    lane_err = rcp::stage_h2d_codes(in_chrom.as<int32_t>(), d->chrom, (size_t)n, d->n_chrom, d->device, s2);
-                if (lane_err == hipSuccess)
-                    lane_err = rcp::stage_h2d_strand(in_strand.as<int8_t>(), d->strand, (size_t)n, d->device, s2);
+                try {
+                    lane_err = hipSetDevice(d->device);
+                    rcp::H2dLane lane(1);
+                    if (lane_err == hipSuccess)
+                        lane_err = rcp::stage_h2d_codes(in_chrom.as<int32_t>(), d->chrom, (size_t)n, d->n_chrom, d->device, s2);
+                    if (lane_err == hipSuccess)
+                        lane_err = rcp::stage_h2d_strand(in_strand.as<int8_t>(), d->strand, (size_t)n, d->device, s2);
+                } catch (...) {
+                    lane_err = hipErrorOutOfMemory;  // (a host allocation of the staging failed)
+                }
             });
         }
         bool widths = false;

@@ -44,6 +44,7 @@ constexpr int kLeanItemsPerWg = 0;  // work items per persistent workgroup, at l
 // as long as the slowest workgroup's heavy items)
 constexpr int kLeanItemsPerWgBase = 4;
 constexpr int kLeanMinChunkBins = 64;                   // no column chunks narrower than this
+constexpr int32_t kFoldConcurrentMaxRows = 8192;        // per-base lean fold of plans in flight, rows at most
 // AUTO keeps binned plans of fewer rows on the general kernel: a lean item is 64 rows, the
 // general kernel's workgroup 32, and with about one item per workgroup the item's read round
 // trips set the pass.  C4 shards (1000 bins of 2 bp), ms per pass lean / general: 25 k rows
@@ -1327,8 +1328,12 @@ extern "C" int rcp_plan_create_ex(const rcp_readset* rs, const rcp_rows_desc* ro
     // table: C5 1/8 spent locate 45 us ahead of a 143-us pileup): the store wave that claims an
     // item searches its rows' read ranges while the pile waves work on the previous item -- no
     // locate launch.  (Binned lean plans keep the locate: their skewed rows need the heavy slices.)
+    // Plans built for several samples in flight (rcp_plan_opts.concurrent) of a larger table keep
+    // the locate launch: it runs beside another sample's pileup there, while the claim's searches
+    // lengthen this kernel (full C5 at D = 2: 0.459-0.463 vs 0.472-0.480 ms a step).
     if (P.lean == 1 && lean_base && rows->ignore_strand && opts->heavy_threshold <= 0 &&
-        B.interp_row.empty() && R > 0 && R <= kFoldMaxRows && !std::getenv("RCP_NO_LEAN_FOLD")) {
+        B.interp_row.empty() && R > 0 && R <= kFoldMaxRows && (opts->concurrent <= 1 || R <= kFoldConcurrentMaxRows) &&
+        !std::getenv("RCP_NO_LEAN_FOLD")) {
         bool f = true;
         for (int r = 0; f && r < R; ++r) {
             const int32_t j0 = B.row_seg[r], j1 = B.row_seg[r + 1];

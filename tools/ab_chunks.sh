@@ -1,3 +1,5 @@
+# (record of a round-6 A/B: the variant it selects was measured, not adopted, and removed from the
+# library -- results under profiles/r06/; the script runs only against that build)
 # C5 1/8 shard (per-base lean plan with the searches folded into the claim): column chunks
 # capped at 16 (the crange table's limit, RCP_FOLD_MAX_CHUNKS=16) vs 64; parity on the lean tests
 set -o pipefail

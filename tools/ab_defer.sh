@@ -1,3 +1,5 @@
+# (record of a round-6 A/B: the variant it selects was measured, not adopted, and removed from the
+# library -- results under profiles/r06/; the script runs only against that build)
 # Binned lean fold plans with the skewed chunks deferred (default) vs the locate + heavy path
 # (RCP_NO_LEAN_DEFER=1) vs the build before (abso/librecoup_amd_before.so): lean tests in both
 # modes (RCP_DEFER_MIN=64: small tables defer), then C4 passes (full and 1/4, 1/8 shards)

@@ -1,3 +1,5 @@
+# (record of a round-6 A/B: the variant it selects was measured, not adopted, and removed from the
+# library -- results under profiles/r06/; the script runs only against that build)
 # Concurrent plans' share of the workgroup slots (RCP_GRID_FILL eighths; 7 = default) on the C4
 # full table and its 1/2 and 1/4 shards, samples in flight auto (bench.py --sim-shard)
 set -o pipefail

@@ -1,3 +1,5 @@
+# (record of a round-6 A/B: the variant it selects was measured, not adopted, and removed from the
+# library -- results under profiles/r06/; the script runs only against that build)
 # C3 row-wave kernel: run-merged adds over consecutive candidates (RCP_RW_RUNS=1) vs interleaved
 # slots with one atomic per read; parity on the row-wave tests in runs mode, ms per pass alternating,
 # and the SQ counters of both

@@ -1,3 +1,4 @@
+# (record of a round-6 A/B: the 4-wave variant was removed after it; RCP_BD_WAVES=16 remains)
 # C2 bin-difference kernel: waves per 16-row tile (RCP_BD_WAVES 16 / 8 / 4; 8 and 4: the rows of a
 # wave located in one chain of searches); parity on the bin-difference tests, then ms per pass
 set -o pipefail

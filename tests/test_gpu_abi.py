@@ -558,6 +558,39 @@ def test_packed_read_uploads(gpu, capfd, sorted_reads):
     np.testing.assert_array_equal(a[1], b[1])
 
 
+def test_two_lane_upload_many_chromosomes(gpu, capfd):
+    """Unsorted reads of a 300-chromosome genome (codes past one byte: the second H2D lane sends
+    them as packed int32 blocks, not bytes) beside the starts on the first lane: the readset
+    equals one built from the same arrays on the device -- streams, kept reads, a profile."""
+    from recoup_amd.engine import ReadSet
+    rng = np.random.default_rng(77)
+    n_chrom = 300
+    lens = rng.integers(200_000, 400_000, n_chrom).astype(np.int64)
+    n = 4_500_000
+    chrom = rng.integers(0, n_chrom, n).astype(np.int32)
+    chrom[rng.integers(0, n, 20)] = n_chrom + 5  # no such chromosome: dropped
+    start = (1 + (rng.random(n) * (lens[np.minimum(chrom, n_chrom - 1)] - 1000))).astype(np.int32)
+    end = start + rng.integers(0, 300, n).astype(np.int32)
+    strand = rng.integers(0, 3, n).astype(np.int8)
+    os.environ["RCP_TRACE"] = "1"
+    try:
+        host = ReadSet(chrom, start, end, strand, lens, device=0)
+    finally:
+        del os.environ["RCP_TRACE"]
+    lines = [ln for ln in capfd.readouterr().err.splitlines() if "h2d-packed" in ln]
+    assert not any(" codes " in ln for ln in lines), lines  # > 255 codes: int32 blocks, not bytes
+    dev = ReadSet(*(torch.from_numpy(a).cuda() for a in (chrom, start, end, strand)), lens, device=0)
+    assert host.n == dev.n == int((chrom < n_chrom).sum())
+    np.testing.assert_array_equal(host.stream_off, dev.stream_off)
+    rc = rng.integers(0, n_chrom, 1_500).astype(np.int32)
+    rs_ = np.array([rng.integers(1, lens[c] - 3000) for c in rc], np.int64)
+    rows = RowTable.from_ranges(rc, rs_, rs_ + 2999, rng.integers(0, 2, len(rc)).astype(np.int8))
+    bins = Bins([("whole", 300)])
+    a, b = Plan(host, rows, bins).run(), Plan(dev, rows, bins).run()
+    assert np.array_equal(np.ascontiguousarray(a[0]).view(np.uint64), np.ascontiguousarray(b[0]).view(np.uint64))
+    np.testing.assert_array_equal(a[1], b[1])
+
+
 def test_packed_run_downloads(gpu, capfd):
     """calcCoverage's Rle list comes down packed (rcp_stage.h stage_d2h_i32: per-1024 blocks of
     depths and run lengths as a base + 16-bit offsets, blocks that do not fit -- a zero run of
